@@ -1,0 +1,204 @@
+#ifndef HEADER_fd_ed25519_gpu_h
+#define HEADER_fd_ed25519_gpu_h
+
+/* fd_ed25519_gpu.h -- C ABI of the MI355X batch ed25519 verify engine
+   (libfdgpu_ed25519.so).
+
+   Two layers:
+
+   1. Drop-in synchronous API.  Same names, signatures, argument meaning
+      and result codes as the reference's ballet/ed25519 verify API, so
+      a caller such as fd_verify_tile links this library in place of
+      the ballet ed25519 verify objects without source changes:
+
+        fd_ed25519_verify                  <- src/ballet/ed25519/fd_ed25519.h:96-101
+                                              (impl fd_ed25519_user.c:135-230)
+        fd_ed25519_verify_batch_single_msg <- src/ballet/ed25519/fd_ed25519.h:124-130
+                                              (impl fd_ed25519_user.c:232-310)
+        fd_ed25519_strerror                <- src/ballet/ed25519/fd_ed25519.h:137-138
+                                              (impl fd_ed25519_user.c:312-322)
+        FD_ED25519_SUCCESS/ERR_SIG/ERR_PUBKEY/ERR_MSG
+                                           <- src/ballet/ed25519/fd_ed25519.h:11-14
+
+      The fd_sha512_t * arguments are accepted and ignored (the GPU
+      computes SHA-512 itself); they are kept so the prototypes are
+      identical.  These calls each run one GPU round trip, so they are
+      correct but latency-bound; throughput comes from layer 2.
+
+   2. Batch / async API (new; prefix fdgpu_).  A batch is a set of
+      transactions described by fdgpu_txn_desc_t records (the fields
+      fd_txn_verify reads from fd_txn_t, src/disco/verify/
+      fd_verify_tile.h:59-108) over a byte arena of payloads.  Each
+      transaction's signature_cnt signatures are verified over its
+      message with fd_ed25519_verify_batch_single_msg semantics.
+
+   All pointers are plain C pointers; "d_" prefixed arguments are HIP
+   device pointers, "stream" is a hipStream_t passed as void *.
+   No torch / C++ types cross this boundary. */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef FD_ED25519_SUCCESS
+#define FD_ED25519_SUCCESS    ( 0) /* Operation was successful */
+#define FD_ED25519_ERR_SIG    (-1) /* signature was obviously invalid */
+#define FD_ED25519_ERR_PUBKEY (-2) /* public key was obviously invalid */
+#define FD_ED25519_ERR_MSG    (-3) /* message didn't match the signature */
+#endif
+
+#ifndef HEADER_fd_src_ballet_sha512_fd_sha512_h
+/* Opaque in this ABI; same tag as src/ballet/sha512/fd_sha512.h:129 so
+   the prototypes below are compatible with the reference header. */
+typedef struct fd_sha512_private fd_sha512_t;
+#endif
+
+/* ---- Layer 1: drop-in synchronous API ----------------------------- */
+
+int
+fd_ed25519_verify( unsigned char const   msg[], /* msg_sz */
+                   unsigned long         msg_sz,
+                   unsigned char const   sig[ 64 ],
+                   unsigned char const   public_key[ 32 ],
+                   fd_sha512_t *         sha );
+
+int
+fd_ed25519_verify_batch_single_msg( unsigned char const   msg[], /* msg_sz */
+                                    unsigned long const   msg_sz,
+                                    unsigned char const   signatures[ 64 ], /* 64 * batch_sz */
+                                    unsigned char const   pubkeys[ 32 ],    /* 32 * batch_sz */
+                                    fd_sha512_t *         shas[ 1 ],        /* batch_sz */
+                                    unsigned char const   batch_sz );
+
+char const *
+fd_ed25519_strerror( int err );
+
+/* ---- Layer 2: batch / async API ------------------------------------ */
+
+/* Result-code semantics.  The reference's AVX-512 (r43x6) and portable
+   (ref) backends agree on accept/reject but differ in two codes
+   (SURVEY.md §0.2): a public key that fails to decode gives ERR_SIG on
+   AVX-512 and ERR_PUBKEY on ref, and an encoding with x==0 and the
+   sign bit set is rejected at decode by AVX-512 only.  AVX-512 is the
+   default (it is the north-star CPU baseline). */
+#define FDGPU_SEMANTICS_AVX512 (0)
+#define FDGPU_SEMANTICS_REF    (1)
+
+#define FDGPU_TXN_MTU          (1232UL) /* FD_TPU_MTU, src/disco/fd_txn_m_t.h */
+#define FDGPU_SIG_MAX          (16UL)   /* fd_ed25519_user.c:238 MAX */
+
+/* One transaction of a batch.  16 bytes.  payload_off is the byte
+   offset of the payload in the batch arena; sig_base is the index of
+   this transaction's first signature in the per-signature output
+   (the exclusive prefix sum of sig_cnt, computed by the stager).
+   signature_off / acct_addr_off / message_off are the fd_txn_t fields
+   of the same name (src/ballet/txn/fd_txn.h); message bytes are
+   [message_off, payload_sz).  A transaction with sig_cnt==0 or
+   sig_cnt>16 gets FD_ED25519_ERR_SIG, exactly like
+   fd_ed25519_verify_batch_single_msg (fd_ed25519_user.c:238-241). */
+typedef struct fdgpu_txn_desc {
+  unsigned int   payload_off;
+  unsigned int   sig_base;
+  unsigned short payload_sz;
+  unsigned short message_off;
+  unsigned short acct_addr_off;
+  unsigned char  signature_off;
+  unsigned char  sig_cnt;
+} fdgpu_txn_desc_t;
+
+typedef struct fdgpu_ed25519_ctx fdgpu_ed25519_ctx_t;
+
+/* fdgpu_ed25519_ctx_new creates an engine bound to HIP device `device`
+   sized for batches of up to max_txn transactions / max_sig signatures
+   / max_payload_bytes of payload arena.  Allocates device scratch and
+   pinned staging buffers (call before entering a seccomp sandbox, i.e.
+   from privileged_init).  Returns NULL on failure (see
+   fdgpu_last_error). */
+fdgpu_ed25519_ctx_t *
+fdgpu_ed25519_ctx_new( int           device,
+                       unsigned long max_txn,
+                       unsigned long max_sig,
+                       unsigned long max_payload_bytes,
+                       int           semantics );
+
+void
+fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx );
+
+/* fdgpu_ed25519_verify_txns_device enqueues verification of a batch
+   whose arena and descriptors are already resident in device memory.
+   Writes one code per transaction to d_txn_out[txn_cnt] and one code
+   per signature to d_sig_out[sig_cnt] (the code fd_ed25519_verify
+   would return for that signature alone; may be NULL).  Asynchronous
+   on `stream` (NULL = the ctx's own stream).  Returns 0 on successful
+   enqueue, negative on bad arguments. */
+int
+fdgpu_ed25519_verify_txns_device( fdgpu_ed25519_ctx_t *    ctx,
+                                  unsigned char const *    d_payload,
+                                  fdgpu_txn_desc_t const * d_desc,
+                                  unsigned long            txn_cnt,
+                                  unsigned long            sig_cnt,
+                                  signed char *            d_txn_out,
+                                  signed char *            d_sig_out,
+                                  void *                   stream );
+
+/* fdgpu_ed25519_verify_txns_host: same from host memory; stages through
+   the ctx's pinned buffers, runs, and waits.  Synchronous. */
+int
+fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t *    ctx,
+                                unsigned char const *    payload,
+                                unsigned long            payload_bytes,
+                                fdgpu_txn_desc_t const * desc,
+                                unsigned long            txn_cnt,
+                                signed char *            txn_out,
+                                signed char *            sig_out );
+
+/* Async submit / poll pipeline (the offload shape fd_verify_tile needs,
+   SURVEY.md §8b).  submit copies one transaction payload into the
+   current pinned staging slot; when the slot fills (or on flush) it is
+   launched (H2D copy + kernels + D2H copy on the ctx stream) and the
+   next slot becomes current.  poll returns completed verdicts in
+   submission order: out_tags[i] is the tag given to submit and
+   out_codes[i] the fd_ed25519_verify_batch_single_msg code.  Returns
+   the number written (<= max).  submit returns 0 on success, -1 if
+   the transaction is malformed (it is then completed with ERR_SIG),
+   -2 if all slots are in flight (caller should poll). */
+int
+fdgpu_ed25519_submit( fdgpu_ed25519_ctx_t * ctx,
+                      unsigned char const * payload,
+                      unsigned short        payload_sz,
+                      unsigned char         signature_off,
+                      unsigned short        acct_addr_off,
+                      unsigned short        message_off,
+                      unsigned char         sig_cnt,
+                      unsigned long         tag );
+
+int
+fdgpu_ed25519_flush( fdgpu_ed25519_ctx_t * ctx );
+
+unsigned long
+fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx,
+                    unsigned long *       out_tags,
+                    signed char *         out_codes,
+                    unsigned long         max,
+                    int                   blocking );
+
+/* Per-kernel timing of the last device batch, in milliseconds, measured
+   with HIP events on the stream the kernels ran on.  idx: 0 = prep
+   (SHA-512 + decode + checks + A-table), 1 = dsm (double-scalar
+   multiplication + compare), 2 = reduce.  Only valid after the batch
+   completed and only when timing was enabled. */
+void
+fdgpu_ed25519_set_timing( fdgpu_ed25519_ctx_t * ctx, int enable );
+
+float
+fdgpu_ed25519_kernel_ms( fdgpu_ed25519_ctx_t * ctx, int idx );
+
+/* Last error string of the calling thread (never NULL). */
+char const *
+fdgpu_last_error( void );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEADER_fd_ed25519_gpu_h */

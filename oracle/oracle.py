@@ -1,0 +1,178 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes bindings of the CPU oracle.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+import this module.  It loads
+
+* ``oracle/liboracle.so``  -- the from-scratch C restatement of the
+  reference verify path (fd_ed25519_oracle.c), always available;
+* ``oracle/_ref/libfdref_{avx512,portable}.so`` -- the reference's own
+  verify sources compiled in place by ``oracle/Makefile ref`` (only
+  where /root/reference existed at build time; the built .so travels to
+  the GPU box, the sources do not).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SEM_AVX512 = 0
+SEM_REF = 1
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i8p = ctypes.POINTER(ctypes.c_int8)
+
+
+def build(ref: bool | None = None) -> None:
+    """Compile liboracle.so (and the reference build when its sources exist)."""
+    subprocess.run(["make", "-s", "-C", HERE, "liboracle.so"], check=True)
+    if ref is None:
+        ref = os.path.isdir("/root/reference/src/ballet/ed25519")
+    if ref:
+        subprocess.run(["make", "-s", "-C", HERE, "ref"], check=True)
+
+
+def _ptr(a: np.ndarray, t=_u8p):
+    return a.ctypes.data_as(t)
+
+
+class Oracle:
+    """The C restatement (oracle/fd_ed25519_oracle.c)."""
+
+    def __init__(self, path: str | None = None):
+        path = path or os.path.join(HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build(ref=False)
+        self.lib = L = ctypes.CDLL(path)
+        L.oracle_ed25519_verify.restype = ctypes.c_int
+        L.oracle_ed25519_verify.argtypes = [_u8p, ctypes.c_size_t, _u8p, _u8p, ctypes.c_int]
+        L.oracle_ed25519_verify_batch_single_msg.restype = ctypes.c_int
+        L.oracle_ed25519_verify_batch_single_msg.argtypes = [_u8p, ctypes.c_size_t, _u8p, _u8p, ctypes.c_uint8, ctypes.c_int]
+        L.oracle_verify_txns.restype = None
+        L.oracle_verify_txns.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_size_t, _i8p, _i8p, ctypes.c_int, ctypes.c_int]
+        L.oracle_sha512.argtypes = [_u8p, ctypes.c_size_t, _u8p]
+        L.oracle_scalar_reduce.argtypes = [_u8p, _u8p]
+        L.oracle_scalar_validate.argtypes = [_u8p]
+        L.oracle_point_decode.argtypes = [_u8p, _u8p, _u8p, ctypes.c_int]
+        L.oracle_ed25519_public_from_private.argtypes = [_u8p, _u8p]
+        L.oracle_ed25519_sign.argtypes = [_u8p, _u8p, ctypes.c_size_t, _u8p, _u8p]
+        L.oracle_dsm_encode.argtypes = [_u8p, _u8p, _u8p, _u8p]
+
+    @staticmethod
+    def _b(x: bytes) -> np.ndarray:
+        return np.frombuffer(bytes(x) + b"\0", dtype=np.uint8)
+
+    def verify(self, msg: bytes, sig: bytes, pub: bytes, sem: int = SEM_AVX512) -> int:
+        m = self._b(msg)
+        return self.lib.oracle_ed25519_verify(_ptr(m), len(msg), _ptr(self._b(sig)), _ptr(self._b(pub)), sem)
+
+    def verify_batch_single_msg(self, msg: bytes, sigs: bytes, pubs: bytes, n: int, sem: int = SEM_AVX512) -> int:
+        return self.lib.oracle_ed25519_verify_batch_single_msg(
+            _ptr(self._b(msg)), len(msg), _ptr(self._b(sigs)), _ptr(self._b(pubs)), n, sem)
+
+    def verify_txns(self, payload: np.ndarray, desc: np.ndarray, sig_cnt_total: int,
+                    sem: int = SEM_AVX512, threads: int = 1):
+        txn_out = np.zeros(len(desc), dtype=np.int8)
+        sig_out = np.zeros(max(sig_cnt_total, 1), dtype=np.int8)
+        self.lib.oracle_verify_txns(_ptr(payload), desc.ctypes.data, len(desc), _ptr(txn_out, _i8p),
+                                    _ptr(sig_out, _i8p), sem, threads)
+        return txn_out, sig_out[:sig_cnt_total]
+
+    def sha512(self, data: bytes) -> bytes:
+        out = np.zeros(64, np.uint8)
+        self.lib.oracle_sha512(_ptr(self._b(data)), len(data), _ptr(out))
+        return out.tobytes()
+
+    def scalar_reduce(self, x: bytes) -> bytes:
+        out = np.zeros(32, np.uint8)
+        self.lib.oracle_scalar_reduce(_ptr(out), _ptr(self._b(x)))
+        return out.tobytes()
+
+    def scalar_validate(self, s: bytes) -> bool:
+        return bool(self.lib.oracle_scalar_validate(_ptr(self._b(s))))
+
+    def point_decode(self, enc: bytes, sem: int = SEM_AVX512):
+        x = np.zeros(32, np.uint8); y = np.zeros(32, np.uint8)
+        rc = self.lib.oracle_point_decode(_ptr(x), _ptr(y), _ptr(self._b(enc)), sem)
+        return rc, x.tobytes(), y.tobytes()
+
+    def public_from_private(self, prv: bytes) -> bytes:
+        out = np.zeros(32, np.uint8)
+        self.lib.oracle_ed25519_public_from_private(_ptr(out), _ptr(self._b(prv)))
+        return out.tobytes()
+
+    def sign(self, msg: bytes, pub: bytes, prv: bytes) -> bytes:
+        out = np.zeros(64, np.uint8)
+        self.lib.oracle_ed25519_sign(_ptr(out), _ptr(self._b(msg)), len(msg), _ptr(self._b(pub)), _ptr(self._b(prv)))
+        return out.tobytes()
+
+    def dsm_encode(self, k: bytes, A: bytes, S: bytes):
+        out = np.zeros(32, np.uint8)
+        rc = self.lib.oracle_dsm_encode(_ptr(out), _ptr(self._b(k)), _ptr(self._b(A)), _ptr(self._b(S)))
+        return rc, out.tobytes()
+
+
+def cpu_has_avx512_ifma() -> bool:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    fl = set(line.split(":", 1)[1].split())
+                    return {"avx512f", "avx512ifma", "avx512vl", "avx512bw", "avx512dq"} <= fl
+    except OSError:
+        pass
+    return False
+
+
+class Reference:
+    """The reference's verify path, compiled from its own sources (oracle/_ref)."""
+
+    def __init__(self, variant: str = "avx512"):
+        path = os.path.join(HERE, "_ref", f"libfdref_{variant}.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        if variant == "avx512" and not cpu_has_avx512_ifma():
+            raise RuntimeError("host CPU lacks AVX-512 IFMA; cannot run the AVX-512 reference build")
+        self.variant = variant
+        self.lib = L = ctypes.CDLL(path)
+        L.ref_verify.restype = ctypes.c_int
+        L.ref_verify.argtypes = [_u8p, ctypes.c_ulong, _u8p, _u8p]
+        L.ref_verify_batch.restype = ctypes.c_int
+        L.ref_verify_batch.argtypes = [_u8p, ctypes.c_ulong, _u8p, _u8p, ctypes.c_uint8]
+        L.ref_sign.argtypes = [_u8p, _u8p, ctypes.c_ulong, _u8p, _u8p]
+        L.ref_public_from_private.argtypes = [_u8p, _u8p]
+        L.ref_sha512.argtypes = [_u8p, ctypes.c_ulong, _u8p]
+        L.ref_verify_txns.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_ulong, _i8p, _i8p, ctypes.c_int]
+
+    _b = staticmethod(Oracle._b)
+
+    def verify(self, msg: bytes, sig: bytes, pub: bytes) -> int:
+        return self.lib.ref_verify(_ptr(self._b(msg)), len(msg), _ptr(self._b(sig)), _ptr(self._b(pub)))
+
+    def verify_batch_single_msg(self, msg: bytes, sigs: bytes, pubs: bytes, n: int) -> int:
+        return self.lib.ref_verify_batch(_ptr(self._b(msg)), len(msg), _ptr(self._b(sigs)), _ptr(self._b(pubs)), n)
+
+    def sign(self, msg: bytes, pub: bytes, prv: bytes) -> bytes:
+        out = np.zeros(64, np.uint8)
+        self.lib.ref_sign(_ptr(out), _ptr(self._b(msg)), len(msg), _ptr(self._b(pub)), _ptr(self._b(prv)))
+        return out.tobytes()
+
+    def public_from_private(self, prv: bytes) -> bytes:
+        out = np.zeros(32, np.uint8)
+        self.lib.ref_public_from_private(_ptr(out), _ptr(self._b(prv)))
+        return out.tobytes()
+
+    def sha512(self, data: bytes) -> bytes:
+        out = np.zeros(64, np.uint8)
+        self.lib.ref_sha512(_ptr(self._b(data)), len(data), _ptr(out))
+        return out.tobytes()
+
+    def verify_txns(self, payload: np.ndarray, desc: np.ndarray, sig_cnt_total: int, threads: int = 1):
+        txn_out = np.zeros(len(desc), dtype=np.int8)
+        sig_out = np.zeros(max(sig_cnt_total, 1), dtype=np.int8)
+        self.lib.ref_verify_txns(_ptr(payload), desc.ctypes.data, len(desc), _ptr(txn_out, _i8p),
+                                 _ptr(sig_out, _i8p), threads)
+        return txn_out, sig_out[:sig_cnt_total]
