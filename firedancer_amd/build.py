@@ -1,0 +1,50 @@
+"""In-tree build of the native parts (run on the CPU build container; the
+.so files travel to the GPU box with the snapshot).
+
+* libfdgpu_ed25519.so -- HIP kernels + C-ABI runtime, hipcc for gfx950
+* libfdsynth.so       -- host C synthetic-transaction generator
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+ARCH = os.environ.get("FDGPU_ARCH", "gfx950")
+
+HIP_SRCS = ["fd_ed25519_gpu.hip"]
+HIP_DEPS = ["fd_gpu_f25519.h", "fd_gpu_sha512.h", "fd_gpu_curve.h", "../../include/fd_ed25519_gpu.h"]
+
+
+def _stale(out: str, deps: list[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(os.path.join(CSRC, d)) > t for d in deps)
+
+
+def build_engine(force: bool = False, extra: list[str] | None = None) -> str:
+    out = os.path.join(PKG, "libfdgpu_ed25519.so")
+    if force or extra or _stale(out, HIP_SRCS + HIP_DEPS):
+        cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wall", "-Wno-unused-function", "-o", out] + (extra or []) + [os.path.join(CSRC, s) for s in HIP_SRCS]
+        subprocess.run(cmd, check=True, cwd=CSRC)
+    return out
+
+
+def build_synth(force: bool = False) -> str:
+    out = os.path.join(PKG, "libfdsynth.so")
+    if force or _stale(out, ["fd_synth.c", "../../include/fd_ed25519_gpu.h"]):
+        subprocess.run(["gcc", "-std=gnu11", "-O2", "-fPIC", "-shared", "-pthread", "-o", out,
+                        os.path.join(CSRC, "fd_synth.c")], check=True)
+    return out
+
+
+def build_all(force: bool = False) -> None:
+    build_synth(force)
+    build_engine(force)
+
+
+if __name__ == "__main__":
+    build_all(force=True)

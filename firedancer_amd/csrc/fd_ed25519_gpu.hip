@@ -1,0 +1,704 @@
+/* fd_ed25519_gpu.hip -- MI355X (gfx950) batch ed25519 verify engine.
+
+   Kernels (one signature per lane, wave64, 256-thread workgroups):
+
+     fd_expand_kernel  txn -> signature map (sig_base prefix from the stager)
+     fd_prep_kernel    per signature: S < l, decode A and R (two
+                       interleaved pow22523 chains), small-order tests,
+                       SHA-512(R||A||M) straight from the payload, k mod l,
+                       signed radix-16 digits of k / radix-256 digits of S,
+                       the 9-entry table [0..8](-A) (cached form) -> HBM
+     fd_dsm_kernel     [k](-A) + [S]B by signed fixed windows: 252
+                       doublings, 64 table adds (entries gathered from HBM,
+                       prefetched one window ahead), 32 base-point adds from
+                       a 129-entry affine table held in LDS; projective
+                       compare with R -> FD_ED25519_SUCCESS / ERR_MSG
+     fd_reduce_kernel  per transaction: fd_ed25519_verify_batch_single_msg
+                       code from its signatures' codes
+
+   Replaces (behaviour, not code) fd_ed25519_verify /
+   fd_ed25519_verify_batch_single_msg (src/ballet/ed25519/
+   fd_ed25519_user.c:135-310) as called from fd_txn_verify
+   (src/disco/verify/fd_verify_tile.h:59-108).
+
+   Fixed windows instead of the reference's sliding wNAF
+   (fd_curve25519.c:109-153): every lane of a wave performs the same
+   doubling/add sequence, so SIMT lanes never diverge in the hot loop;
+   only the table index is data dependent. */
+
+#include "fd_gpu_sha512.h"
+#include "fd_gpu_curve.h"
+#include "../../include/fd_ed25519_gpu.h"
+
+#include <hip/hip_runtime.h>
+#include <mutex>
+#include <string.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string>
+#include <vector>
+#include <deque>
+
+#define FD_WG 256
+#define FD_ATAB_ENTRIES 9          /* [0..8](-A), cached form, 128 B each */
+#define FD_BTAB_ENTRIES 129        /* [0..128]B, affine precomp, 96 B each */
+#define FD_ARENA_SLACK  512UL      /* readable bytes past the last payload */
+
+typedef signed char i8;
+
+/* ------------------------------------------------------------------ */
+/* scratch layout (structure of arrays over signatures, stride = nsig) */
+/*   tab : uint4 [FD_ATAB_ENTRIES][8 quads][nsig]                      */
+/*   Rxy : uint4 [4 quads (x lo,x hi,y lo,y hi)][nsig]                 */
+/*   digA: i8    [64][nsig]   radix-16 signed digits of k              */
+/*   digB: i8    [32][nsig]   radix-256 signed digits of S             */
+/* ------------------------------------------------------------------ */
+
+FD_DEV void fe_store2( uint4 * base, size_t stride, fe const & a ) {
+  base[0]      = make_uint4( a.v[0], a.v[1], a.v[2], a.v[3] );
+  base[stride] = make_uint4( a.v[4], a.v[5], a.v[6], a.v[7] );
+}
+FD_DEV void fe_load2( fe & a, uint4 const * base, size_t stride ) {
+  uint4 x = base[0], y = base[stride];
+  a.v[0]=x.x; a.v[1]=x.y; a.v[2]=x.z; a.v[3]=x.w; a.v[4]=y.x; a.v[5]=y.y; a.v[6]=y.z; a.v[7]=y.w;
+}
+
+FD_DEV void atab_store( uint4 * tab, size_t n, u32 s, int e, ge_cached const & c ) {
+  uint4 * b = tab + ((size_t)e * 8) * n + s;
+  fe_store2( b + 0*n, n, c.YpX );
+  fe_store2( b + 2*n, n, c.YmX );
+  fe_store2( b + 4*n, n, c.Z   );
+  fe_store2( b + 6*n, n, c.T2d );
+}
+FD_DEV void atab_load( ge_cached & c, uint4 const * tab, size_t n, u32 s, int e ) {
+  uint4 const * b = tab + ((size_t)e * 8) * n + s;
+  fe_load2( c.YpX, b + 0*n, n );
+  fe_load2( c.YmX, b + 2*n, n );
+  fe_load2( c.Z,   b + 4*n, n );
+  fe_load2( c.T2d, b + 6*n, n );
+}
+
+/* ------------------------------------------------------------------ */
+
+__global__ void __launch_bounds__( FD_WG )
+fd_expand_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 * __restrict__ map, u32 nsig ) {
+  u32 t = blockIdx.x * FD_WG + threadIdx.x;
+  if( t >= txn_cnt ) return;
+  fdgpu_txn_desc_t d = desc[t];
+  for( u32 j=0; j<d.sig_cnt; j++ ) {
+    u32 s = d.sig_base + j;
+    if( s < nsig ) map[s] = t | (j << 24);
+  }
+}
+
+__global__ void __launch_bounds__( FD_WG )
+fd_prep_kernel( unsigned char const *    __restrict__ payload,
+                fdgpu_txn_desc_t const * __restrict__ desc,
+                u32 const *              __restrict__ map,
+                u32                                   nsig,
+                int                                   semantics,
+                i8 *                     __restrict__ code_out,
+                uint4 *                  __restrict__ tab,
+                uint4 *                  __restrict__ Rxy,
+                i8 *                     __restrict__ digA,
+                i8 *                     __restrict__ digB ) {
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  size_t n = nsig;
+  u32 m = map[s];
+  u32 t = m & 0xffffffu, j = m >> 24;
+  fdgpu_txn_desc_t d = desc[t];
+
+  /* transaction sanity (batch size and bounds): ERR_SIG, like
+     fd_ed25519_verify_batch_single_msg's batch_sz check (fd_ed25519_user.c:238-241) */
+  u32 cnt = d.sig_cnt;
+  if( cnt==0u || cnt>16u
+      || (u32)d.signature_off + 64u*cnt > (u32)d.payload_sz
+      || (u32)d.acct_addr_off + 32u*cnt > (u32)d.payload_sz
+      || (u32)d.message_off > (u32)d.payload_sz ) {
+    code_out[s] = FD_ED25519_ERR_SIG;
+    return;
+  }
+
+  unsigned char const * base = payload + d.payload_off;
+  u32 Rw[8], Sw[8], Aw[8];
+  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
+  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
+  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
+
+  int code = FD_ED25519_SUCCESS;
+  /* 1. S canonical (fd_ed25519_user.c:174-176) */
+  if( !sc_is_canonical( Sw ) ) code = FD_ED25519_ERR_SIG;
+
+  /* 2. decode A and R (fd_ed25519_user.c:179-193) */
+  ge_p3 A, R; int ra, rb;
+  ge_decode2( A, ra, Aw, R, rb, Rw );
+  if( code==FD_ED25519_SUCCESS ) {
+    if( semantics==FDGPU_SEMANTICS_AVX512 ) {
+      if( ra | rb ) code = FD_ED25519_ERR_SIG;
+    } else {
+      if( ra==1 ) code = FD_ED25519_ERR_PUBKEY;
+      else if( rb==1 ) code = FD_ED25519_ERR_SIG;
+    }
+  }
+  /* 3. small order (fd_ed25519_user.c:194-199) */
+  if( code==FD_ED25519_SUCCESS ) {
+    if( ge_affine_is_small_order( A ) ) code = FD_ED25519_ERR_PUBKEY;
+    else if( ge_affine_is_small_order( R ) ) code = FD_ED25519_ERR_SIG;
+  }
+  code_out[s] = (i8)code;
+  if( code!=FD_ED25519_SUCCESS ) return;
+
+  /* 4. k = SHA-512(R||A||M) mod l (fd_ed25519_user.c:204-206) */
+  u32 h[16], k[8];
+  fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
+  sc_reduce( k, h );
+
+  /* 5. signed digits */
+  {
+    int carry = 0;
+#pragma unroll
+    for( int i=0; i<64; i++ ) {
+      int v = (int)((k[i>>3] >> (4*(i&7))) & 15u) + carry;
+      carry = (v + 8) >> 4;
+      digA[(size_t)i*n + s] = (i8)(v - (carry << 4));
+    }
+    carry = 0;
+#pragma unroll
+    for( int i=0; i<32; i++ ) {
+      int v = (int)((Sw[i>>2] >> (8*(i&3))) & 255u) + carry;
+      carry = (v + 128) >> 8;
+      digB[(size_t)i*n + s] = (i8)(v - (carry << 8));
+    }
+  }
+
+  /* 6. R affine for the final compare */
+  fe_canon( R.X, R.X );
+  fe_store2( Rxy + 0*n + s, n, R.X );
+  fe_store2( Rxy + 2*n + s, n, R.Y );
+
+  /* 7. table [0..8](-A) in cached form (fd_ed25519_point_neg +
+        the odd-multiple table of fd_curve25519.c:118-131, here all
+        multiples for a signed fixed window) */
+  fe_neg( A.X, A.X ); fe_neg( A.T, A.T );
+  ge_cached c1, c;
+  c.YpX = fe_one(); c.YmX = fe_one(); c.Z = fe_one(); c.T2d = fe_zero();
+  atab_store( tab, n, s, 0, c );
+  ge_p3_to_cached( c1, A );
+  atab_store( tab, n, s, 1, c1 );
+  ge_p3 cur = A;
+#pragma unroll 1
+  for( int e=2; e<FD_ATAB_ENTRIES; e++ ) {
+    ge_p1p1 tt;
+    ge_add_cached( tt, cur, c1, 0 );
+    ge_p1p1_to_p3( cur, tt );
+    ge_p3_to_cached( c, cur );
+    atab_store( tab, n, s, e, c );
+  }
+}
+
+__global__ void __launch_bounds__( FD_WG )
+fd_dsm_kernel( u32                      nsig,
+               uint4 const * __restrict__ tab,
+               uint4 const * __restrict__ Rxy,
+               i8 const *    __restrict__ digA,
+               i8 const *    __restrict__ digB,
+               uint4 const * __restrict__ btab_g,
+               i8 *          __restrict__ code ) {
+  __shared__ uint4 btab[ FD_BTAB_ENTRIES * 6 ];
+  for( int i=threadIdx.x; i<FD_BTAB_ENTRIES*6; i+=FD_WG ) btab[i] = btab_g[i];
+  __syncthreads();
+
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  if( code[s] != FD_ED25519_SUCCESS ) return;
+  size_t n = nsig;
+
+  ge_p3 P; ge_p3_identity( P );
+  ge_p2 P2;
+  int da = digA[ (size_t)63*n + s ];
+  ge_cached q;
+  atab_load( q, tab, n, s, da < 0 ? -da : da );
+
+#pragma unroll 1
+  for( int w=63; w>=0; w-- ) {
+    ge_p1p1 t;
+    if( w != 63 ) {
+#pragma unroll 1
+      for( int r=0; r<3; r++ ) { ge_dbl( t, P2 ); ge_p1p1_to_p2( P2, t ); }
+      ge_dbl( t, P2 ); ge_p1p1_to_p3( P, t );
+    }
+    ge_add_cached( t, P, q, da < 0 );
+    int dn = 0;
+    if( w > 0 ) {
+      dn = digA[ (size_t)(w-1)*n + s ];
+      atab_load( q, tab, n, s, dn < 0 ? -dn : dn );   /* prefetch next window's entry */
+    }
+    if( !(w & 1) ) {
+      ge_p1p1_to_p3( P, t );
+      int db = digB[ (size_t)(w>>1)*n + s ];
+      int e = db < 0 ? -db : db;
+      ge_precomp bq;
+      uint4 const * bp = btab + e*6;
+      uint4 x0=bp[0], x1=bp[1], x2=bp[2], x3=bp[3], x4=bp[4], x5=bp[5];
+      bq.ypx.v[0]=x0.x; bq.ypx.v[1]=x0.y; bq.ypx.v[2]=x0.z; bq.ypx.v[3]=x0.w;
+      bq.ypx.v[4]=x1.x; bq.ypx.v[5]=x1.y; bq.ypx.v[6]=x1.z; bq.ypx.v[7]=x1.w;
+      bq.ymx.v[0]=x2.x; bq.ymx.v[1]=x2.y; bq.ymx.v[2]=x2.z; bq.ymx.v[3]=x2.w;
+      bq.ymx.v[4]=x3.x; bq.ymx.v[5]=x3.y; bq.ymx.v[6]=x3.z; bq.ymx.v[7]=x3.w;
+      bq.xy2d.v[0]=x4.x; bq.xy2d.v[1]=x4.y; bq.xy2d.v[2]=x4.z; bq.xy2d.v[3]=x4.w;
+      bq.xy2d.v[4]=x5.x; bq.xy2d.v[5]=x5.y; bq.xy2d.v[6]=x5.z; bq.xy2d.v[7]=x5.w;
+      ge_add_precomp( t, P, bq, db < 0 );
+    }
+    ge_p1p1_to_p2( P2, t );
+    da = dn;
+  }
+
+  /* fd_ed25519_point_eq_z1: X == x_R Z and Y == y_R Z */
+  fe x, y, u;
+  fe_load2( x, Rxy + 0*n + s, n );
+  fe_load2( y, Rxy + 2*n + s, n );
+  fe_mul( u, x, P2.Z ); int okx = fe_eq( u, P2.X );
+  fe_mul( u, y, P2.Z ); int oky = fe_eq( u, P2.Y );
+  code[s] = (okx & oky) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+__global__ void __launch_bounds__( FD_WG )
+fd_reduce_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 nsig,
+                  i8 const * __restrict__ code, i8 * __restrict__ txn_out ) {
+  u32 t = blockIdx.x * FD_WG + threadIdx.x;
+  if( t >= txn_cnt ) return;
+  fdgpu_txn_desc_t d = desc[t];
+  u32 cnt = d.sig_cnt;
+  int r;
+  if( cnt==0u || cnt>16u ) r = FD_ED25519_ERR_SIG;           /* fd_ed25519_user.c:238-241 */
+  else {
+    int first = 0, any_msg = 0;
+    for( u32 j=0; j<cnt; j++ ) {
+      u32 s = d.sig_base + j;
+      int c = s < nsig ? (int)code[s] : FD_ED25519_ERR_SIG;
+      if( c==FD_ED25519_ERR_MSG ) any_msg = 1;
+      else if( c && !first ) first = c;                       /* pass-1 order, :264-294 */
+    }
+    r = first ? first : ( any_msg ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS );  /* pass 2, :297-306 */
+  }
+  txn_out[t] = (i8)r;
+}
+
+/* [e]B for e in [0,128], affine precomputed (y+x, y-x, 2dxy), canonical.
+   Generated on the device at context creation (the GPU analogue of
+   table/fd_curve25519_table_*.c fd_ed25519_base_point_wnaf_table). */
+__global__ void fd_btab_kernel( uint4 * out ) {
+  int e = threadIdx.x;
+  if( e >= FD_BTAB_ENTRIES ) return;
+  ge_p3 B; B.X = fe_Bx(); B.Y = fe_By(); B.Z = fe_one(); fe_mul( B.T, B.X, B.Y );
+  ge_p3 acc; ge_p3_identity( acc );
+  for( int b=7; b>=0; b-- ) {
+    ge_p3_dbl( acc, acc );
+    if( (e >> b) & 1 ) ge_p3_add( acc, acc, B );
+  }
+  fe zi, x, y, ypx, ymx, xy;
+  fe_invert( zi, acc.Z );
+  fe_mul( x, acc.X, zi ); fe_mul( y, acc.Y, zi );
+  fe_add( ypx, y, x ); fe_sub( ymx, y, x ); fe_mul( xy, x, y ); fe d2 = fe_d2(); fe_mul( xy, xy, d2 );
+  fe_canon( ypx, ypx ); fe_canon( ymx, ymx ); fe_canon( xy, xy );
+  uint4 * o = out + e*6;
+  o[0] = make_uint4( ypx.v[0], ypx.v[1], ypx.v[2], ypx.v[3] ); o[1] = make_uint4( ypx.v[4], ypx.v[5], ypx.v[6], ypx.v[7] );
+  o[2] = make_uint4( ymx.v[0], ymx.v[1], ymx.v[2], ymx.v[3] ); o[3] = make_uint4( ymx.v[4], ymx.v[5], ymx.v[6], ymx.v[7] );
+  o[4] = make_uint4( xy.v[0],  xy.v[1],  xy.v[2],  xy.v[3]  ); o[5] = make_uint4( xy.v[4],  xy.v[5],  xy.v[6],  xy.v[7]  );
+}
+
+/* ==================================================================
+   Host runtime: C ABI (include/fd_ed25519_gpu.h)
+   ================================================================== */
+
+static thread_local std::string fd_err;
+static void set_err( char const * what, hipError_t e ) {
+  fd_err = std::string( what ) + ": " + hipGetErrorString( e );
+}
+#define HIPCHK( call, ret ) do { hipError_t _e = (call); if( _e != hipSuccess ) { set_err( #call, _e ); return ret; } } while(0)
+
+struct fd_slot {               /* one in-flight host batch of the async pipeline */
+  unsigned char *    h_payload;
+  fdgpu_txn_desc_t * h_desc;
+  i8 *               h_txn_out;
+  unsigned long *    h_tags;
+  unsigned char *    d_payload;
+  fdgpu_txn_desc_t * d_desc;
+  i8 *               d_txn_out;
+  size_t             payload_used;
+  unsigned long      txn_cnt, sig_cnt;
+  hipEvent_t         done;
+  int                state;   /* 0 filling, 1 in flight */
+};
+
+struct fdgpu_ed25519_ctx {
+  int device, semantics, timing;
+  unsigned long max_txn, max_sig, max_payload;
+  hipStream_t stream;
+  /* scratch */
+  u32 *   d_map;
+  i8 *    d_code;
+  uint4 * d_tab;
+  uint4 * d_Rxy;
+  i8 *    d_digA;
+  i8 *    d_digB;
+  uint4 * d_btab;
+  hipEvent_t ev[4];
+  enum { NRING = 64 };
+  hipEvent_t ring[ NRING ][ 4 ];  /* per-batch kernel boundaries while timing is on */
+  unsigned long ring_cnt;
+  /* async pipeline */
+  enum { NSLOT = 2 };
+  fd_slot slot[ NSLOT ];
+  int cur;                       /* slot being filled */
+  std::deque<int> inflight;      /* slot order */
+  std::deque<std::pair<unsigned long,i8>> ready;
+};
+
+extern "C" char const * fdgpu_last_error( void ) { return fd_err.c_str(); }
+
+static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_desc_t const * d_desc,
+                         unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, i8 * d_sig_out, hipStream_t st ) {
+  if( !txn_cnt ) return 0;
+  i8 * code = d_sig_out ? d_sig_out : ctx->d_code;
+  hipEvent_t * ev = ctx->ev;
+  if( ctx->timing ) { ev = ctx->ring[ ctx->ring_cnt % fdgpu_ed25519_ctx_t::NRING ]; ctx->ring_cnt++; }
+  u32 nsig = (u32)sig_cnt;
+  unsigned tg = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
+  unsigned sg = (unsigned)( (sig_cnt + FD_WG - 1) / FD_WG );
+  if( nsig ) {
+    hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig );
+    if( ctx->timing ) hipEventRecord( ev[0], st );
+    hipLaunchKernelGGL( fd_prep_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+                        ctx->semantics, code, ctx->d_tab, ctx->d_Rxy, ctx->d_digA, ctx->d_digB );
+    if( ctx->timing ) hipEventRecord( ev[1], st );
+    hipLaunchKernelGGL( fd_dsm_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
+                        ctx->d_digA, ctx->d_digB, ctx->d_btab, code );
+    if( ctx->timing ) hipEventRecord( ev[2], st );
+  }
+  hipLaunchKernelGGL( fd_reduce_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, nsig, code, d_txn_out );
+  if( ctx->timing ) hipEventRecord( ev[3], st );
+  HIPCHK( hipGetLastError(), -3 );
+  return 0;
+}
+
+extern "C" fdgpu_ed25519_ctx_t *
+fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
+                       unsigned long max_payload_bytes, int semantics ) {
+  if( max_txn==0 || max_txn >= (1UL<<24) || max_sig==0 || max_sig >= (1UL<<31) ) { fd_err = "bad sizes"; return NULL; }
+  if( semantics!=FDGPU_SEMANTICS_AVX512 && semantics!=FDGPU_SEMANTICS_REF ) { fd_err = "bad semantics"; return NULL; }
+  HIPCHK( hipSetDevice( device ), NULL );
+  fdgpu_ed25519_ctx_t * ctx = new fdgpu_ed25519_ctx_t();
+  ctx->device = device; ctx->semantics = semantics; ctx->timing = 0;
+  ctx->max_txn = max_txn; ctx->max_sig = max_sig; ctx->max_payload = max_payload_bytes;
+  size_t ns = max_sig;
+  HIPCHK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_map,  ns * sizeof(u32) ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_code, ns ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_tab,  ns * FD_ATAB_ENTRIES * 8 * sizeof(uint4) ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_Rxy,  ns * 4 * sizeof(uint4) ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_digA, ns * 64 ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_digB, ns * 32 ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_btab, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), NULL );
+  for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), NULL );
+  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), NULL );
+  ctx->ring_cnt = 0;
+  hipLaunchKernelGGL( fd_btab_kernel, dim3(1), dim3(FD_BTAB_ENTRIES), 0, ctx->stream, ctx->d_btab );
+  HIPCHK( hipGetLastError(), NULL );
+  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
+    fd_slot & sl = ctx->slot[i];
+    memset( &sl, 0, sizeof(sl) );
+    if( max_payload_bytes ) {
+      HIPCHK( hipHostMalloc( (void**)&sl.h_payload, max_payload_bytes + FD_ARENA_SLACK, hipHostMallocDefault ), NULL );
+      HIPCHK( hipHostMalloc( (void**)&sl.h_desc, max_txn * sizeof(fdgpu_txn_desc_t), hipHostMallocDefault ), NULL );
+      HIPCHK( hipHostMalloc( (void**)&sl.h_txn_out, max_txn, hipHostMallocDefault ), NULL );
+      HIPCHK( hipHostMalloc( (void**)&sl.h_tags, max_txn * sizeof(unsigned long), hipHostMallocDefault ), NULL );
+      HIPCHK( hipMalloc( &sl.d_payload, max_payload_bytes + FD_ARENA_SLACK ), NULL );
+      HIPCHK( hipMalloc( &sl.d_desc, max_txn * sizeof(fdgpu_txn_desc_t) ), NULL );
+      HIPCHK( hipMalloc( &sl.d_txn_out, max_txn ), NULL );
+      memset( sl.h_payload, 0, max_payload_bytes + FD_ARENA_SLACK );
+    }
+    HIPCHK( hipEventCreateWithFlags( &sl.done, hipEventDisableTiming ), NULL );
+  }
+  ctx->cur = 0;
+  HIPCHK( hipStreamSynchronize( ctx->stream ), NULL );
+  return ctx;
+}
+
+extern "C" void
+fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
+  if( !ctx ) return;
+  hipSetDevice( ctx->device );
+  hipStreamSynchronize( ctx->stream );
+  hipFree( ctx->d_map ); hipFree( ctx->d_code ); hipFree( ctx->d_tab ); hipFree( ctx->d_Rxy );
+  hipFree( ctx->d_digA ); hipFree( ctx->d_digB ); hipFree( ctx->d_btab );
+  for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ev[i] );
+  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ring[r][i] );
+  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
+    fd_slot & sl = ctx->slot[i];
+    if( sl.h_payload ) { hipHostFree( sl.h_payload ); hipHostFree( sl.h_desc ); hipHostFree( sl.h_txn_out ); hipHostFree( sl.h_tags );
+                         hipFree( sl.d_payload ); hipFree( sl.d_desc ); hipFree( sl.d_txn_out ); }
+    hipEventDestroy( sl.done );
+  }
+  hipStreamDestroy( ctx->stream );
+  delete ctx;
+}
+
+extern "C" void fdgpu_ed25519_set_timing( fdgpu_ed25519_ctx_t * ctx, int enable ) { ctx->timing = enable; ctx->ring_cnt = 0; }
+
+/* mean duration of kernel idx over the batches launched since timing was
+   enabled (at most the last NRING), from HIP events recorded on the
+   stream the kernels ran on */
+extern "C" float
+fdgpu_ed25519_kernel_ms( fdgpu_ed25519_ctx_t * ctx, int idx ) {
+  if( idx<0 || idx>2 || !ctx->ring_cnt ) return -1.f;
+  unsigned long n = ctx->ring_cnt < (unsigned long)fdgpu_ed25519_ctx_t::NRING ? ctx->ring_cnt : (unsigned long)fdgpu_ed25519_ctx_t::NRING;
+  double sum = 0.;
+  for( unsigned long r=0; r<n; r++ ) {
+    float ms = 0.f;
+    if( hipEventElapsedTime( &ms, ctx->ring[r][idx], ctx->ring[r][idx+1] ) != hipSuccess ) return -1.f;
+    sum += ms;
+  }
+  return (float)( sum / (double)n );
+}
+
+/* ---- VALU integer peak probe --------------------------------------------
+   Sustained v_mad_u64_u32 rate of this device: 16 independent 64-bit
+   accumulator chains per lane (no memory traffic), full grid.  This is the
+   "peak" the prep/dsm kernels' multiply-accumulate count is priced against
+   (MI355X_MICROARCH.md has no integer-multiply row). */
+__global__ void __launch_bounds__( 256 )
+fd_mad_probe_kernel( u32 iters, u32 seed, u64 * out ) {
+  u64 acc[16]; u32 a = seed + threadIdx.x, b = seed ^ (blockIdx.x * 2654435761u);
+#pragma unroll
+  for( int i=0; i<16; i++ ) acc[i] = (u64)(a + i) << 7;
+  for( u32 it=0; it<iters; it++ ) {
+#pragma unroll
+    for( int i=0; i<16; i++ ) {
+      asm volatile( "v_mad_u64_u32 %0, vcc, %1, %2, %0" : "+v"(acc[i]) : "v"(a), "v"(b) : "vcc" );
+    }
+  }
+  u64 x = 0;
+#pragma unroll
+  for( int i=0; i<16; i++ ) x ^= acc[i];
+  if( x == 0x1234567ull ) out[0] = x;
+}
+
+extern "C" double
+fdgpu_mad_peak_per_s( int device ) {
+  if( hipSetDevice( device ) != hipSuccess ) return -1.;
+  hipDeviceProp_t prop; hipGetDeviceProperties( &prop, device );
+  int grid = prop.multiProcessorCount * 8;   /* 8 x 256 threads per CU = 8 waves/SIMD */
+  u64 * d_out; hipMalloc( &d_out, 8 );
+  hipEvent_t e0, e1; hipEventCreate( &e0 ); hipEventCreate( &e1 );
+  u32 iters = 4096;
+  hipLaunchKernelGGL( fd_mad_probe_kernel, dim3(grid), dim3(256), 0, 0, 16u, 1u, d_out );
+  hipEventRecord( e0, 0 );
+  hipLaunchKernelGGL( fd_mad_probe_kernel, dim3(grid), dim3(256), 0, 0, iters, 1u, d_out );
+  hipEventRecord( e1, 0 );
+  hipEventSynchronize( e1 );
+  float ms = 0.f; hipEventElapsedTime( &ms, e0, e1 );
+  hipEventDestroy( e0 ); hipEventDestroy( e1 ); hipFree( d_out );
+  double macs = (double)grid * 256. * 16. * (double)iters;
+  return ms > 0.f ? macs / ( (double)ms * 1e-3 ) : -1.;
+}
+
+extern "C" int
+fdgpu_ed25519_verify_txns_device( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload,
+                                  fdgpu_txn_desc_t const * d_desc, unsigned long txn_cnt, unsigned long sig_cnt,
+                                  signed char * d_txn_out, signed char * d_sig_out, void * stream ) {
+  if( !ctx ) { fd_err = "NULL ctx"; return -1; }
+  if( txn_cnt > ctx->max_txn || sig_cnt > ctx->max_sig ) { fd_err = "batch larger than ctx"; return -1; }
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  return launch_batch( ctx, d_payload, d_desc, txn_cnt, sig_cnt, (i8*)d_txn_out, (i8*)d_sig_out,
+                       stream ? (hipStream_t)stream : ctx->stream );
+}
+
+/* Host-side validation of a batch before staging: payload bounds and
+   the sig_base prefix (the device kernels additionally bound-check every
+   transaction against its own payload). */
+static int check_batch( fdgpu_txn_desc_t const * desc, unsigned long txn_cnt, unsigned long payload_bytes,
+                        unsigned long * sig_total ) {
+  unsigned long s = 0;
+  for( unsigned long i=0; i<txn_cnt; i++ ) {
+    if( desc[i].sig_base != s ) { fd_err = "sig_base is not the prefix sum of sig_cnt"; return -1; }
+    if( (unsigned long)desc[i].payload_off + desc[i].payload_sz > payload_bytes ) { fd_err = "payload out of arena"; return -1; }
+    s += desc[i].sig_cnt;
+  }
+  *sig_total = s;
+  return 0;
+}
+
+extern "C" int
+fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload, unsigned long payload_bytes,
+                                fdgpu_txn_desc_t const * desc, unsigned long txn_cnt,
+                                signed char * txn_out, signed char * sig_out ) {
+  if( !ctx ) { fd_err = "NULL ctx"; return -1; }
+  unsigned long nsig;
+  if( check_batch( desc, txn_cnt, payload_bytes, &nsig ) ) return -1;
+  if( txn_cnt > ctx->max_txn || nsig > ctx->max_sig || payload_bytes > ctx->max_payload ) { fd_err = "batch larger than ctx"; return -1; }
+  if( !txn_cnt ) return 0;
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  fd_slot & sl = ctx->slot[0];
+  if( !ctx->inflight.empty() ) { fd_err = "async batches in flight"; return -1; }
+  memcpy( sl.h_payload, payload, payload_bytes );
+  memset( sl.h_payload + payload_bytes, 0, FD_ARENA_SLACK );
+  memcpy( sl.h_desc, desc, txn_cnt * sizeof(fdgpu_txn_desc_t) );
+  hipStream_t st = ctx->stream;
+  HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, payload_bytes + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+  HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
+  int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, txn_cnt, nsig, sl.d_txn_out, NULL, st );
+  if( rc ) return rc;
+  HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
+  if( sig_out && nsig ) HIPCHK( hipMemcpyAsync( sig_out, ctx->d_code, nsig, hipMemcpyDeviceToHost, st ), -2 );
+  HIPCHK( hipStreamSynchronize( st ), -2 );
+  memcpy( txn_out, sl.h_txn_out, txn_cnt );
+  return 0;
+}
+
+/* ---- async submit / poll ------------------------------------------ */
+
+static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
+  fd_slot & sl = ctx->slot[i];
+  hipStream_t st = ctx->stream;
+  memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
+  HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+  HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
+  int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
+  if( rc ) return rc;
+  HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
+  HIPCHK( hipEventRecord( sl.done, st ), -2 );
+  sl.state = 1;
+  ctx->inflight.push_back( i );
+  return 0;
+}
+
+static void slot_reap( fdgpu_ed25519_ctx_t * ctx, int i ) {
+  fd_slot & sl = ctx->slot[i];
+  for( unsigned long t=0; t<sl.txn_cnt; t++ ) ctx->ready.emplace_back( sl.h_tags[t], sl.h_txn_out[t] );
+  sl.txn_cnt = 0; sl.sig_cnt = 0; sl.payload_used = 0; sl.state = 0;
+}
+
+/* make ctx->cur a free slot; -2 if every slot is in flight */
+static int next_free( fdgpu_ed25519_ctx_t * ctx ) {
+  for( int k=0; k<fdgpu_ed25519_ctx_t::NSLOT; k++ ) {
+    int i = (ctx->cur + k) % fdgpu_ed25519_ctx_t::NSLOT;
+    if( ctx->slot[i].state==0 ) { ctx->cur = i; return 0; }
+  }
+  return -2;
+}
+
+extern "C" int
+fdgpu_ed25519_flush( fdgpu_ed25519_ctx_t * ctx ) {
+  fd_slot & sl = ctx->slot[ ctx->cur ];
+  if( sl.state!=0 || sl.txn_cnt==0 ) return 0;
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  int rc = slot_launch( ctx, ctx->cur );
+  if( rc ) return rc;
+  next_free( ctx );
+  return 0;
+}
+
+extern "C" int
+fdgpu_ed25519_submit( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload, unsigned short payload_sz,
+                      unsigned char signature_off, unsigned short acct_addr_off, unsigned short message_off,
+                      unsigned char sig_cnt, unsigned long tag ) {
+  if( !ctx->slot[0].h_payload ) { fd_err = "ctx has no staging buffers (max_payload_bytes==0)"; return -3; }
+  if( next_free( ctx ) ) return -2;
+  fd_slot * sl = &ctx->slot[ ctx->cur ];
+  if( sl->txn_cnt + 1 > ctx->max_txn || sl->sig_cnt + sig_cnt > ctx->max_sig || sl->payload_used + payload_sz + 8 > ctx->max_payload ) {
+    int rc = fdgpu_ed25519_flush( ctx );
+    if( rc ) return rc;
+    if( next_free( ctx ) ) return -2;
+    sl = &ctx->slot[ ctx->cur ];
+  }
+  size_t off = sl->payload_used;
+  memcpy( sl->h_payload + off, payload, payload_sz );
+  fdgpu_txn_desc_t & d = sl->h_desc[ sl->txn_cnt ];
+  d.payload_off = (unsigned)off; d.sig_base = (unsigned)sl->sig_cnt; d.payload_sz = payload_sz;
+  d.message_off = message_off; d.acct_addr_off = acct_addr_off; d.signature_off = signature_off; d.sig_cnt = sig_cnt;
+  sl->h_tags[ sl->txn_cnt ] = tag;
+  sl->txn_cnt++; sl->sig_cnt += sig_cnt; sl->payload_used = (off + payload_sz + 7) & ~(size_t)7;
+  int malformed = sig_cnt==0 || sig_cnt>16 || (unsigned)signature_off + 64u*sig_cnt > payload_sz
+               || (unsigned)acct_addr_off + 32u*sig_cnt > payload_sz || message_off > payload_sz;
+  return malformed ? -1 : 0;
+}
+
+extern "C" unsigned long
+fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes,
+                    unsigned long max, int blocking ) {
+  hipSetDevice( ctx->device );
+  while( !ctx->inflight.empty() ) {
+    int i = ctx->inflight.front();
+    hipError_t e = blocking ? hipEventSynchronize( ctx->slot[i].done ) : hipEventQuery( ctx->slot[i].done );
+    if( e != hipSuccess ) break;
+    ctx->inflight.pop_front();
+    slot_reap( ctx, i );
+    if( ctx->ready.size() >= max ) break;
+  }
+  unsigned long n = 0;
+  while( n < max && !ctx->ready.empty() ) {
+    out_tags[n] = ctx->ready.front().first; out_codes[n] = ctx->ready.front().second;
+    ctx->ready.pop_front(); n++;
+  }
+  return n;
+}
+
+/* ---- drop-in synchronous API (fd_ed25519.h) ------------------------- */
+
+static std::mutex g_mu;
+static fdgpu_ed25519_ctx_t * g_ctx = NULL;
+
+static fdgpu_ed25519_ctx_t * global_ctx( void ) {
+  if( g_ctx ) return g_ctx;
+  char const * dev = getenv( "FDGPU_DEVICE" );
+  char const * sem = getenv( "FDGPU_SEMANTICS" );
+  g_ctx = fdgpu_ed25519_ctx_new( dev ? atoi( dev ) : 0, 64, 64, 1UL<<17,
+                                 ( sem && !strcmp( sem, "ref" ) ) ? FDGPU_SEMANTICS_REF : FDGPU_SEMANTICS_AVX512 );
+  return g_ctx;
+}
+
+extern "C" int
+fd_ed25519_verify_batch_single_msg( unsigned char const msg[], unsigned long const msg_sz,
+                                    unsigned char const signatures[ 64 ], unsigned char const pubkeys[ 32 ],
+                                    fd_sha512_t * shas[ 1 ], unsigned char const batch_sz ) {
+  (void)shas;
+  if( batch_sz==0 || batch_sz>16 ) return FD_ED25519_ERR_SIG;   /* fd_ed25519_user.c:238-241 */
+  unsigned long n = batch_sz;
+  unsigned long sz = 96UL*n + msg_sz;
+  if( sz > 0xffffUL ) return -4; /* message beyond the 64 KiB descriptor limit: see fd_ed25519_gpu.h */
+  std::lock_guard<std::mutex> lk( g_mu );
+  fdgpu_ed25519_ctx_t * ctx = global_ctx();
+  if( !ctx ) { fprintf( stderr, "fdgpu: no GPU context: %s\n", fdgpu_last_error() ); abort(); }
+  std::vector<unsigned char> buf( sz );
+  memcpy( buf.data(), signatures, 64*n );
+  memcpy( buf.data() + 64*n, pubkeys, 32*n );
+  if( msg_sz ) memcpy( buf.data() + 96*n, msg, msg_sz );
+  fdgpu_txn_desc_t d;
+  d.payload_off = 0; d.sig_base = 0; d.payload_sz = (unsigned short)sz; d.message_off = (unsigned short)(96*n);
+  d.acct_addr_off = (unsigned short)(64*n); d.signature_off = 0; d.sig_cnt = (unsigned char)n;
+  signed char out = 0;
+  if( fdgpu_ed25519_verify_txns_host( ctx, buf.data(), sz, &d, 1, &out, NULL ) ) {
+    fprintf( stderr, "fdgpu: verify failed: %s\n", fdgpu_last_error() ); abort();
+  }
+  return out;
+}
+
+extern "C" int
+fd_ed25519_verify( unsigned char const msg[], unsigned long msg_sz, unsigned char const sig[ 64 ],
+                   unsigned char const public_key[ 32 ], fd_sha512_t * sha ) {
+  fd_sha512_t * shas[1] = { sha };
+  return fd_ed25519_verify_batch_single_msg( msg, msg_sz, sig, public_key, shas, 1 );
+}
+
+extern "C" char const *
+fd_ed25519_strerror( int err ) {   /* fd_ed25519_user.c:312-322 */
+  switch( err ) {
+  case FD_ED25519_SUCCESS:    return "success";
+  case FD_ED25519_ERR_SIG:    return "bad signature";
+  case FD_ED25519_ERR_PUBKEY: return "bad public key";
+  case FD_ED25519_ERR_MSG:    return "bad message";
+  default: break;
+  }
+  return "unknown";
+}

@@ -1,0 +1,197 @@
+"""Host-side mirror of the reference's verify API over the C ABI.
+
+Loads ``firedancer_amd/libfdgpu_ed25519.so`` (HIP kernels + C runtime, see
+include/fd_ed25519_gpu.h) with ctypes.  The module-level functions mirror
+the reference's ``fd_ed25519_verify`` / ``fd_ed25519_verify_batch_single_msg``
+(src/ballet/ed25519/fd_ed25519.h:96-130): same argument meaning, same
+FD_ED25519_* result codes.  :class:`Engine` is the batch API used by the
+verify-stage offload and the bench.
+
+There is no CPU fallback: if the shared library or the GPU is missing,
+every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libfdgpu_ed25519.so")
+
+FD_ED25519_SUCCESS = 0
+FD_ED25519_ERR_SIG = -1
+FD_ED25519_ERR_PUBKEY = -2
+FD_ED25519_ERR_MSG = -3
+SEMANTICS_AVX512 = 0
+SEMANTICS_REF = 1
+
+DESC_DTYPE = np.dtype([("payload_off", "<u4"), ("sig_base", "<u4"), ("payload_sz", "<u2"),
+                       ("message_off", "<u2"), ("acct_addr_off", "<u2"), ("signature_off", "u1"),
+                       ("sig_cnt", "u1")])
+assert DESC_DTYPE.itemsize == 16
+
+# every symbol include/fd_ed25519_gpu.h declares
+EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed25519_strerror",
+           "fdgpu_ed25519_ctx_new", "fdgpu_ed25519_ctx_delete", "fdgpu_ed25519_verify_txns_device",
+           "fdgpu_ed25519_verify_txns_host", "fdgpu_ed25519_submit", "fdgpu_ed25519_flush",
+           "fdgpu_ed25519_poll", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
+           "fdgpu_last_error")
+
+_lib = None
+_lock = threading.Lock()
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+def load_library():
+    """dlopen the engine.  Raises if it has not been built."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        # torch-ROCm ships its own libamdhip64 with the same SONAME
+        # (libamdhip64.so.7).  Load it first so this library binds to that
+        # one HIP runtime: torch tensors/streams and the engine then share
+        # one runtime (two runtimes in one process do not see each other's
+        # streams, and the second fails to enumerate GPUs).
+        try:
+            import torch  # noqa: F401
+            if getattr(torch.version, "hip", None):
+                torch.cuda.device_count()
+        except ImportError:
+            pass
+        L = ctypes.CDLL(LIB_PATH)
+        L.fd_ed25519_verify.restype = ctypes.c_int
+        L.fd_ed25519_verify.argtypes = [_u8p, ctypes.c_ulong, _u8p, _u8p, ctypes.c_void_p]
+        L.fd_ed25519_verify_batch_single_msg.restype = ctypes.c_int
+        L.fd_ed25519_verify_batch_single_msg.argtypes = [_u8p, ctypes.c_ulong, _u8p, _u8p, ctypes.c_void_p, ctypes.c_uint8]
+        L.fd_ed25519_strerror.restype = ctypes.c_char_p
+        L.fd_ed25519_strerror.argtypes = [ctypes.c_int]
+        L.fdgpu_ed25519_ctx_new.restype = ctypes.c_void_p
+        L.fdgpu_ed25519_ctx_new.argtypes = [ctypes.c_int, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong, ctypes.c_int]
+        L.fdgpu_ed25519_ctx_delete.argtypes = [ctypes.c_void_p]
+        L.fdgpu_ed25519_verify_txns_device.restype = ctypes.c_int
+        L.fdgpu_ed25519_verify_txns_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
+                                                      ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.fdgpu_ed25519_verify_txns_host.restype = ctypes.c_int
+        L.fdgpu_ed25519_verify_txns_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                                                    ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p]
+        L.fdgpu_ed25519_submit.restype = ctypes.c_int
+        L.fdgpu_ed25519_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ushort, ctypes.c_ubyte,
+                                           ctypes.c_ushort, ctypes.c_ushort, ctypes.c_ubyte, ctypes.c_ulong]
+        L.fdgpu_ed25519_flush.restype = ctypes.c_int
+        L.fdgpu_ed25519_flush.argtypes = [ctypes.c_void_p]
+        L.fdgpu_ed25519_poll.restype = ctypes.c_ulong
+        L.fdgpu_ed25519_poll.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int]
+        L.fdgpu_ed25519_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.fdgpu_ed25519_kernel_ms.restype = ctypes.c_float
+        L.fdgpu_ed25519_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.fdgpu_last_error.restype = ctypes.c_char_p
+        _lib = L
+        return L
+
+
+def last_error() -> str:
+    return load_library().fdgpu_last_error().decode()
+
+
+def _buf(b: bytes):
+    a = np.frombuffer(bytes(b) + b"\0", np.uint8)
+    return a, a.ctypes.data_as(_u8p)
+
+
+def fd_ed25519_verify(msg: bytes, sig: bytes, public_key: bytes) -> int:
+    """Drop-in for fd_ed25519_verify (fd_ed25519.h:96-101) on the GPU."""
+    L = load_library()
+    m, mp = _buf(msg); s, sp = _buf(sig); p, pp = _buf(public_key)
+    return L.fd_ed25519_verify(mp, len(msg), sp, pp, None)
+
+
+def fd_ed25519_verify_batch_single_msg(msg: bytes, signatures: bytes, pubkeys: bytes, batch_sz: int) -> int:
+    """Drop-in for fd_ed25519_verify_batch_single_msg (fd_ed25519.h:124-130) on the GPU."""
+    L = load_library()
+    m, mp = _buf(msg); s, sp = _buf(signatures); p, pp = _buf(pubkeys)
+    return L.fd_ed25519_verify_batch_single_msg(mp, len(msg), sp, pp, None, batch_sz & 0xff)
+
+
+def fd_ed25519_strerror(err: int) -> str:
+    return load_library().fd_ed25519_strerror(err).decode()
+
+
+class Engine:
+    """A verify engine bound to one GPU (fdgpu_ed25519_ctx_t)."""
+
+    def __init__(self, device: int = 0, max_txn: int = 1 << 20, max_sig: int | None = None,
+                 max_payload: int = 0, semantics: int = SEMANTICS_AVX512):
+        L = load_library()
+        self.L = L
+        self.max_txn = max_txn
+        self.max_sig = max_sig or max_txn
+        self.max_payload = max_payload
+        self.ctx = L.fdgpu_ed25519_ctx_new(device, max_txn, self.max_sig, max_payload, semantics)
+        if not self.ctx:
+            raise RuntimeError(f"fdgpu_ed25519_ctx_new failed: {last_error()}")
+
+    def close(self):
+        if self.ctx:
+            self.L.fdgpu_ed25519_ctx_delete(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_timing(self, on: bool = True):
+        self.L.fdgpu_ed25519_set_timing(self.ctx, 1 if on else 0)
+
+    def kernel_ms(self, idx: int) -> float:
+        return float(self.L.fdgpu_ed25519_kernel_ms(self.ctx, idx))
+
+    def verify_txns_host(self, payload: np.ndarray, desc: np.ndarray, want_sig_codes: bool = True):
+        """Synchronous batch from host memory.  Returns (txn_codes, sig_codes)."""
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        nsig = int(desc["sig_cnt"].astype(np.int64).sum())
+        txn_out = np.zeros(len(desc), np.int8)
+        sig_out = np.zeros(max(nsig, 1), np.int8) if want_sig_codes else None
+        rc = self.L.fdgpu_ed25519_verify_txns_host(self.ctx, payload.ctypes.data, payload.nbytes, desc.ctypes.data,
+                                                   len(desc), txn_out.ctypes.data,
+                                                   sig_out.ctypes.data if sig_out is not None else None)
+        if rc:
+            raise RuntimeError(f"fdgpu_ed25519_verify_txns_host: {rc} {last_error()}")
+        return txn_out, (sig_out[:nsig] if sig_out is not None else None)
+
+    def verify_txns_device(self, d_payload: int, d_desc: int, txn_cnt: int, sig_cnt: int,
+                           d_txn_out: int, d_sig_out: int | None = None, stream: int | None = None):
+        """Enqueue a batch already resident in HBM (raw device pointers)."""
+        rc = self.L.fdgpu_ed25519_verify_txns_device(self.ctx, d_payload, d_desc, txn_cnt, sig_cnt, d_txn_out,
+                                                     d_sig_out, stream)
+        if rc:
+            raise RuntimeError(f"fdgpu_ed25519_verify_txns_device: {rc} {last_error()}")
+
+    # -- async pipeline ------------------------------------------------------
+    def submit(self, payload: bytes, signature_off: int, acct_addr_off: int, message_off: int,
+               sig_cnt: int, tag: int) -> int:
+        b = np.frombuffer(payload, np.uint8)
+        rc = self.L.fdgpu_ed25519_submit(self.ctx, b.ctypes.data, len(payload), signature_off, acct_addr_off,
+                                         message_off, sig_cnt, tag)
+        if rc <= -3:
+            raise RuntimeError(f"fdgpu_ed25519_submit: {rc} {last_error()}")
+        return rc
+
+    def flush(self):
+        rc = self.L.fdgpu_ed25519_flush(self.ctx)
+        if rc:
+            raise RuntimeError(f"fdgpu_ed25519_flush: {rc} {last_error()}")
+
+    def poll(self, max_n: int = 4096, blocking: bool = False):
+        tags = np.zeros(max_n, np.uint64)
+        codes = np.zeros(max_n, np.int8)
+        n = self.L.fdgpu_ed25519_poll(self.ctx, tags.ctypes.data, codes.ctypes.data, max_n, 1 if blocking else 0)
+        return tags[:n], codes[:n]

@@ -182,16 +182,24 @@ fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx,
                     unsigned long         max,
                     int                   blocking );
 
-/* Per-kernel timing of the last device batch, in milliseconds, measured
-   with HIP events on the stream the kernels ran on.  idx: 0 = prep
+/* Per-kernel timing, in milliseconds: the mean over the batches launched
+   since fdgpu_ed25519_set_timing(ctx,1) (at most the last 64) of HIP
+   events recorded on the stream the kernels ran on.  idx: 0 = prep
    (SHA-512 + decode + checks + A-table), 1 = dsm (double-scalar
-   multiplication + compare), 2 = reduce.  Only valid after the batch
-   completed and only when timing was enabled. */
+   multiplication + compare), 2 = reduce.  Valid once those batches
+   completed; -1 when nothing was timed. */
 void
 fdgpu_ed25519_set_timing( fdgpu_ed25519_ctx_t * ctx, int enable );
 
 float
 fdgpu_ed25519_kernel_ms( fdgpu_ed25519_ctx_t * ctx, int idx );
+
+/* Diagnostics: sustained v_mad_u64_u32 rate of `device` in 32x32+64
+   multiply-accumulates per second (a register-only probe kernel over the
+   whole chip).  The VALU-integer roofline the kernels are priced
+   against; MI355X_MICROARCH.md has no integer-multiply row. */
+double
+fdgpu_mad_peak_per_s( int device );
 
 /* Last error string of the calling thread (never NULL). */
 char const *

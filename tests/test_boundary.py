@@ -1,0 +1,50 @@
+"""CPU: the C-ABI library builds for gfx950, loads, and exports exactly what
+include/*.h declares (no compute calls -- no GPU here)."""
+import os
+import re
+import subprocess
+
+from firedancer_amd import engine
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    txt = open(os.path.join(ROOT, "include", "fd_ed25519_gpu.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", txt)) - {"sizeof"})
+
+
+def test_header_matches_exports_list():
+    assert sorted(engine.EXPORTS) == _header_functions()
+
+
+def test_library_loads_and_exports():
+    lib = engine.load_library()
+    for name in engine.EXPORTS:
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", engine.LIB_PATH], capture_output=True, text=True).stdout
+    syms = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    for name in engine.EXPORTS:
+        assert name in syms, name
+
+
+def test_library_has_gfx950_code_object():
+    data = open(engine.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+
+
+def test_strerror_no_gpu_needed():
+    lib = engine.load_library()
+    assert lib.fd_ed25519_strerror(0) == b"success"
+    assert lib.fd_ed25519_strerror(-1) == b"bad signature"
+    assert lib.fd_ed25519_strerror(-2) == b"bad public key"
+    assert lib.fd_ed25519_strerror(-3) == b"bad message"
+    assert lib.fd_ed25519_strerror(7) == b"unknown"
+
+
+def test_desc_layout():
+    import numpy as np
+    assert engine.DESC_DTYPE.itemsize == 16
+    assert [engine.DESC_DTYPE.fields[k][1] for k in engine.DESC_DTYPE.names] == [0, 4, 8, 10, 12, 14, 15]
+    assert np.dtype(engine.DESC_DTYPE).names[-1] == "sig_cnt"

@@ -1,0 +1,175 @@
+"""GPU parity: the HIP engine, called through the C ABI, against the
+reference's own outputs (tests/golden, from oracle/_ref) and the oracle."""
+import numpy as np
+import pytest
+
+from tests.golden_io import txns_fixture, vectors_as_txns
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fa():
+    import firedancer_amd
+    firedancer_amd.load_library()
+    return firedancer_amd
+
+
+def _engine(fa, n_txn, n_sig, payload_bytes, sem):
+    return fa.Engine(device=0, max_txn=max(n_txn, 1), max_sig=max(n_sig, 1), max_payload=payload_bytes, semantics=sem)
+
+
+@pytest.mark.parametrize("sem,key", [(0, "code_avx"), (1, "code_ref")])
+def test_golden_vectors(fa, golden, sem, key):
+    """CCTV + Wycheproof + malleability + fuzz corpus + edge encodings + random: identical codes."""
+    v = golden["vectors"]
+    payload, desc = vectors_as_txns(v)
+    eng = _engine(fa, len(desc), len(desc), payload.nbytes, sem)
+    txn, sig = eng.verify_txns_host(payload, desc)
+    eng.close()
+    bad = np.nonzero(txn != v[key])[0]
+    assert len(bad) == 0, [(int(v["set_id"][i]), int(v["tc_id"][i]), int(txn[i]), int(v[key][i])) for i in bad[:20]]
+    np.testing.assert_array_equal(sig, v[key])
+
+
+@pytest.mark.parametrize("sem,sfx", [(0, "avx"), (1, "ref")])
+def test_golden_txns(fa, golden, sem, sfx):
+    """Multi-signer txns (0..17 signers, injected faults, malformed descriptors)."""
+    t = golden["txns"]
+    payload, desc, nsig = txns_fixture(t)
+    eng = _engine(fa, len(desc), nsig, payload.nbytes, sem)
+    txn, sig = eng.verify_txns_host(payload, desc)
+    eng.close()
+    np.testing.assert_array_equal(txn, t[f"txn_code_{sfx}"])
+    np.testing.assert_array_equal(sig, t[f"sig_code_{sfx}"])
+
+
+@pytest.mark.parametrize("kind,ms,inv,n", [(0, 1, 0.1, 6000), (2, 12, 0.2, 3000), (1, 1, 0.1, 6000)])
+def test_synth_vs_oracle(fa, oracle, kind, ms, inv, n):
+    """Adversarial mix (BASELINE configs[2]) and multi-signer (configs[3]) vs the oracle."""
+    from firedancer_amd import synth
+    payload, desc, expect, nsig = synth.make_batch(n, kind, ms, inv, seed=99 + kind)
+    eng = _engine(fa, n, nsig, payload.nbytes, 0)
+    txn, sig = eng.verify_txns_host(payload, desc)
+    eng.close()
+    np.testing.assert_array_equal(txn, expect)
+    o_txn, o_sig = oracle.verify_txns(payload, desc, nsig, threads=16)
+    np.testing.assert_array_equal(txn, o_txn)
+    np.testing.assert_array_equal(sig, o_sig)
+
+
+def test_device_api(fa):
+    """Inputs resident in HBM (torch tensors), engine on torch's current stream."""
+    import torch
+    from firedancer_amd import synth
+    n = 4096
+    payload, desc, expect, nsig = synth.make_batch(n, synth.LARGE_NOOP, seed=5)
+    pay_d = torch.from_numpy(payload).cuda()
+    desc_d = torch.from_numpy(desc.view(np.uint8)).cuda()
+    out_d = torch.full((n,), 7, dtype=torch.int8, device="cuda")
+    sig_d = torch.full((nsig,), 7, dtype=torch.int8, device="cuda")
+    eng = fa.Engine(device=0, max_txn=n, max_sig=nsig)
+    st = torch.cuda.current_stream().cuda_stream
+    eng.verify_txns_device(pay_d.data_ptr(), desc_d.data_ptr(), n, nsig, out_d.data_ptr(), sig_d.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert (out_d.cpu().numpy() == 0).all() and (sig_d.cpu().numpy() == 0).all()
+    # flip one message byte in 37 txns -> exactly those become ERR_MSG
+    rng = np.random.default_rng(3)
+    idx = rng.choice(n, 37, replace=False)
+    for t in idx:
+        off = int(desc["payload_off"][t]) + int(rng.integers(101, 1232))   # past the signer pubkey (69..100)
+        payload[off] ^= 0x40
+    pay_d.copy_(torch.from_numpy(payload))
+    eng.verify_txns_device(pay_d.data_ptr(), desc_d.data_ptr(), n, nsig, out_d.data_ptr(), None, st)
+    torch.cuda.synchronize()
+    got = out_d.cpu().numpy()
+    want = np.zeros(n, np.int8); want[idx] = -3
+    np.testing.assert_array_equal(got, want)
+    eng.close()
+
+
+def test_dropin_sync_api(fa, golden):
+    """fd_ed25519_verify / fd_ed25519_verify_batch_single_msg drop-ins (one GPU round trip each)."""
+    v = golden["vectors"]
+    rng = np.random.default_rng(1)
+    for i in rng.choice(len(v["msg_sz"]), 60, replace=False):
+        m = v["msg_arena"][v["msg_off"][i]: v["msg_off"][i] + v["msg_sz"][i]].tobytes()
+        assert fa.fd_ed25519_verify(m, v["sig"][i].tobytes(), v["pub"][i].tobytes()) == v["code_avx"][i]
+    t = golden["txns"]
+    payload, desc, _ = txns_fixture(t)
+    for i in range(0, 120):
+        d = {k: int(desc[i][k]) for k in desc.dtype.names}
+        if not (1 <= d["sig_cnt"] <= 16):
+            continue
+        b = d["payload_off"]
+        msg = payload[b + d["message_off"]: b + d["payload_sz"]].tobytes()
+        sigs = payload[b + d["signature_off"]: b + d["signature_off"] + 64 * d["sig_cnt"]].tobytes()
+        pubs = payload[b + d["acct_addr_off"]: b + d["acct_addr_off"] + 32 * d["sig_cnt"]].tobytes()
+        assert fa.fd_ed25519_verify_batch_single_msg(msg, sigs, pubs, d["sig_cnt"]) == t["txn_code_avx"][i]
+    assert fa.fd_ed25519_verify_batch_single_msg(b"x", b"", b"", 0) == -1
+    assert fa.fd_ed25519_verify_batch_single_msg(b"x", bytes(64 * 17), bytes(32 * 17), 17) == -1
+
+
+def test_async_submit_poll(fa):
+    """submit/poll pipeline: verdicts come back in submission order with the right codes."""
+    from firedancer_amd import synth
+    n = 5000
+    payload, desc, expect, nsig = synth.make_batch(n, synth.MULTI, max_signers=4, invalid_frac=0.15, seed=21)
+    eng = fa.Engine(device=0, max_txn=1024, max_sig=1024 * 4, max_payload=1024 * 1240)
+    tags_out, codes_out = [], []
+    for t in range(n):
+        d = desc[t]
+        b = int(d["payload_off"])
+        body = payload[b: b + int(d["payload_sz"])].tobytes()
+        while True:
+            rc = eng.submit(body, int(d["signature_off"]), int(d["acct_addr_off"]), int(d["message_off"]),
+                            int(d["sig_cnt"]), t)
+            if rc != -2:
+                break
+            tg, cd = eng.poll(4096, blocking=True)
+            tags_out.extend(tg.tolist()); codes_out.extend(cd.tolist())
+        tg, cd = eng.poll(4096, blocking=False)
+        tags_out.extend(tg.tolist()); codes_out.extend(cd.tolist())
+    eng.flush()
+    while len(tags_out) < n:
+        tg, cd = eng.poll(4096, blocking=True)
+        tags_out.extend(tg.tolist()); codes_out.extend(cd.tolist())
+    eng.close()
+    assert tags_out == list(range(n))
+    np.testing.assert_array_equal(np.array(codes_out, np.int8), expect)
+
+
+def test_full_size_property(fa):
+    """BASELINE configs[1] at full size (1M x 1232-byte txns): every valid
+    signature accepted; a checksum of the verdicts after corrupting a known
+    set of transactions equals the known set (size-independent property)."""
+    import torch
+    from firedancer_amd import synth
+    n = 1 << 20
+    payload, desc, expect, nsig = synth.make_batch(n, synth.LARGE_NOOP, seed=1234)
+    rng = np.random.default_rng(77)
+    bad = rng.choice(n, 1000, replace=False)
+    for t in bad[:500]:                 # message bit flips -> ERR_MSG
+        payload[int(desc["payload_off"][t]) + 1000] ^= 1
+    for t in bad[500:]:                 # S += 2^255 (non-canonical) -> ERR_SIG
+        payload[int(desc["payload_off"][t]) + 64] ^= 0x80
+    pay_d = torch.from_numpy(payload).cuda()
+    desc_d = torch.from_numpy(desc.view(np.uint8)).cuda()
+    out_d = torch.empty(n, dtype=torch.int8, device="cuda")
+    eng = fa.Engine(device=0, max_txn=n, max_sig=nsig)
+    eng.verify_txns_device(pay_d.data_ptr(), desc_d.data_ptr(), n, nsig, out_d.data_ptr(), None,
+                           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = out_d.cpu().numpy()
+    eng.close()
+    want = np.zeros(n, np.int8); want[bad[:500]] = -3; want[bad[500:]] = -1
+    np.testing.assert_array_equal(got, want)
+
+
+def test_mad_probe(fa):
+    r = fa.load_library()
+    import ctypes
+    r.fdgpu_mad_peak_per_s.restype = ctypes.c_double
+    r.fdgpu_mad_peak_per_s.argtypes = [ctypes.c_int]
+    v = r.fdgpu_mad_peak_per_s(0)
+    assert v > 1e12, v
