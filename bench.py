@@ -92,14 +92,12 @@ def main():
     ap.add_argument("--latency-batch", type=int, default=8192)
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-
     import torch
     import torch.distributed as dist
-    from firedancer_amd import Engine, load_library, synth
+    from firedancer_amd import Engine, load_library, shard, synth
 
+    env = shard.dist_env()
+    world, rank, local_rank = env.world, env.rank, env.local_rank
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
@@ -111,15 +109,15 @@ def main():
     n = args.txns
     gen_threads = min(16, os.cpu_count() or 1)
     t_gen = time.time()
-    payload, desc, expect, nsig = synth.make_batch(n, synth.LARGE_NOOP, seed=1234 + 7919 * rank, threads=gen_threads)
+    payload, desc, expect, nsig = synth.make_batch(n, synth.LARGE_NOOP, seed=shard.shard_seed(1234, rank),
+                                                   threads=gen_threads)
     t_gen = time.time() - t_gen
 
     pay_d = torch.from_numpy(payload).cuda()
     desc_d = torch.from_numpy(desc.view(np.uint8)).cuda()
     out_d = torch.empty(n, dtype=torch.int8, device="cuda")
     eng = Engine(device=local_rank, max_txn=n, max_sig=nsig)
-    stream = torch.cuda.current_stream()
-    st = stream.cuda_stream
+    st = torch.cuda.current_stream().cuda_stream
 
     def step():
         eng.verify_txns_device(pay_d.data_ptr(), desc_d.data_ptr(), n, nsig, out_d.data_ptr(), None, st)
@@ -128,25 +126,13 @@ def main():
         step()
     torch.cuda.synchronize()
     eng.set_timing(True)
-    barrier(); torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(); barrier()
-    dt = time.perf_counter() - t0
+    dt = shard.timed_steps(step, args.steps, 0, torch.cuda.synchronize, barrier)
     ms_prep, ms_dsm, ms_red = eng.kernel_ms(0), eng.kernel_ms(1), eng.kernel_ms(2)
     eng.set_timing(False)
 
     got = out_d.cpu().numpy()
     ok = bool(np.array_equal(got, expect))
-
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-    okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-    dt_max = float(t.item())
-    all_ok = bool(okt.item())
+    dt_max, all_ok = shard.reduce_max_min(dist if world > 1 else None, dt, ok, "cuda")
 
     lat = None
     if rank == 0 and args.latency_batch > 0:
@@ -183,7 +169,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(payload, desc, nsig, threads=gen_threads)
-        value = world * nsig * args.steps / dt_max
+        value = shard.aggregate_rate(world, nsig, args.steps, dt_max)
         rec = {
             "metric": "ed25519 verified sigs/sec at 1/8 MI355X vs host AVX-512; p99 batch latency",
             "value": value,

@@ -43,39 +43,53 @@
 #define FD_ATAB_ENTRIES 9          /* [0..8](-A), cached form, 128 B each */
 #define FD_BTAB_ENTRIES 129        /* [0..128]B, affine precomp, 96 B each */
 #define FD_ARENA_SLACK  512UL      /* readable bytes past the last payload */
+#ifndef FD_DSM_PREFETCH
+#define FD_DSM_PREFETCH 1          /* issue the -A table gather before the window's doublings */
+#endif
 
 typedef signed char i8;
 
 /* ------------------------------------------------------------------ */
-/* scratch layout (structure of arrays over signatures, stride = nsig) */
-/*   tab : uint4 [FD_ATAB_ENTRIES][8 quads][nsig]                      */
-/*   Rxy : uint4 [4 quads (x lo,x hi,y lo,y hi)][nsig]                 */
-/*   digA: i8    [64][nsig]   radix-16 signed digits of k              */
-/*   digB: i8    [32][nsig]   radix-256 signed digits of S             */
+/* scratch layout                                                      */
+/*   tab : uint4 [nsig][FD_ATAB_ENTRIES][8]  entry e of signature s =   */
+/*         e*(-A) in cached form, 4 canonical field elements packed    */
+/*         8x32 (YpX, YmX, Z, T2d) = 128 B = one cache line, so the    */
+/*         per-lane gather of a random entry moves exactly one line    */
+/*   Rxy : uint4 [nsig][4]   canonical x, y of R                       */
+/*   digA: i8    [64][nsig]  radix-16 signed digits of k (coalesced)   */
+/*   digB: i8    [32][nsig]  radix-256 signed digits of S              */
 /* ------------------------------------------------------------------ */
 
-FD_DEV void fe_store2( uint4 * base, size_t stride, fe const & a ) {
-  base[0]      = make_uint4( a.v[0], a.v[1], a.v[2], a.v[3] );
-  base[stride] = make_uint4( a.v[4], a.v[5], a.v[6], a.v[7] );
+FD_DEV void fe_store_packed( uint4 * dst, fe const & a ) {
+  u32 w[8]; fe_pack( w, a );
+  dst[0] = make_uint4( w[0], w[1], w[2], w[3] );
+  dst[1] = make_uint4( w[4], w[5], w[6], w[7] );
 }
-FD_DEV void fe_load2( fe & a, uint4 const * base, size_t stride ) {
-  uint4 x = base[0], y = base[stride];
-  a.v[0]=x.x; a.v[1]=x.y; a.v[2]=x.z; a.v[3]=x.w; a.v[4]=y.x; a.v[5]=y.y; a.v[6]=y.z; a.v[7]=y.w;
+FD_DEV void fe_from_quads( fe & a, uint4 x, uint4 y ) {
+  u32 w[8] = { x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w };
+  fe_unpack( a, w );
 }
 
-FD_DEV void atab_store( uint4 * tab, size_t n, u32 s, int e, ge_cached const & c ) {
-  uint4 * b = tab + ((size_t)e * 8) * n + s;
-  fe_store2( b + 0*n, n, c.YpX );
-  fe_store2( b + 2*n, n, c.YmX );
-  fe_store2( b + 4*n, n, c.Z   );
-  fe_store2( b + 6*n, n, c.T2d );
+FD_DEV void atab_store( uint4 * tab, u32 s, int e, ge_cached const & c ) {
+  uint4 * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8;
+  fe_store_packed( b + 0, c.YpX );
+  fe_store_packed( b + 2, c.YmX );
+  fe_store_packed( b + 4, c.Z   );
+  fe_store_packed( b + 6, c.T2d );
 }
-FD_DEV void atab_load( ge_cached & c, uint4 const * tab, size_t n, u32 s, int e ) {
-  uint4 const * b = tab + ((size_t)e * 8) * n + s;
-  fe_load2( c.YpX, b + 0*n, n );
-  fe_load2( c.YmX, b + 2*n, n );
-  fe_load2( c.Z,   b + 4*n, n );
-  fe_load2( c.T2d, b + 6*n, n );
+
+struct atab_raw { uint4 q[8]; };
+
+FD_DEV void atab_fetch( atab_raw & r, uint4 const * tab, u32 s, int e ) {
+  uint4 const * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8;
+#pragma unroll
+  for( int i=0; i<8; i++ ) r.q[i] = b[i];
+}
+FD_DEV void atab_unpack( ge_cached & c, atab_raw const & r ) {
+  fe_from_quads( c.YpX, r.q[0], r.q[1] );
+  fe_from_quads( c.YmX, r.q[2], r.q[3] );
+  fe_from_quads( c.Z,   r.q[4], r.q[5] );
+  fe_from_quads( c.T2d, r.q[6], r.q[7] );
 }
 
 /* ------------------------------------------------------------------ */
@@ -91,20 +105,20 @@ fd_expand_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 *
   }
 }
 
+/* Stage 1 -- checks and decompression (fd_ed25519_user.c:174-199).
+   Writes the per-signature code (0 = still pending) and, for pending
+   signatures, the canonical affine R and A to scratch. */
 __global__ void __launch_bounds__( FD_WG )
-fd_prep_kernel( unsigned char const *    __restrict__ payload,
-                fdgpu_txn_desc_t const * __restrict__ desc,
-                u32 const *              __restrict__ map,
-                u32                                   nsig,
-                int                                   semantics,
-                i8 *                     __restrict__ code_out,
-                uint4 *                  __restrict__ tab,
-                uint4 *                  __restrict__ Rxy,
-                i8 *                     __restrict__ digA,
-                i8 *                     __restrict__ digB ) {
+fd_decode_kernel( unsigned char const *    __restrict__ payload,
+                  fdgpu_txn_desc_t const * __restrict__ desc,
+                  u32 const *              __restrict__ map,
+                  u32                                   nsig,
+                  int                                   semantics,
+                  i8 *                     __restrict__ code_out,
+                  uint4 *                  __restrict__ Rxy,
+                  uint4 *                  __restrict__ Axy ) {
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
-  size_t n = nsig;
   u32 m = map[s];
   u32 t = m & 0xffffffu, j = m >> 24;
   fdgpu_txn_desc_t d = desc[t];
@@ -132,7 +146,8 @@ fd_prep_kernel( unsigned char const *    __restrict__ payload,
 
   /* 2. decode A and R (fd_ed25519_user.c:179-193) */
   ge_p3 A, R; int ra, rb;
-  ge_decode2( A, ra, Aw, R, rb, Rw );
+  ge_decode1( A, ra, Aw );
+  ge_decode1( R, rb, Rw );
   if( code==FD_ED25519_SUCCESS ) {
     if( semantics==FDGPU_SEMANTICS_AVX512 ) {
       if( ra | rb ) code = FD_ED25519_ERR_SIG;
@@ -148,52 +163,83 @@ fd_prep_kernel( unsigned char const *    __restrict__ payload,
   }
   code_out[s] = (i8)code;
   if( code!=FD_ED25519_SUCCESS ) return;
+  fe_store_packed( Rxy + (size_t)s*4 + 0, R.X );
+  fe_store_packed( Rxy + (size_t)s*4 + 2, R.Y );
+  fe_store_packed( Axy + (size_t)s*4 + 0, A.X );
+  fe_store_packed( Axy + (size_t)s*4 + 2, A.Y );
+}
 
-  /* 4. k = SHA-512(R||A||M) mod l (fd_ed25519_user.c:204-206) */
+/* Stage 2 -- k = SHA-512(R||A||M) mod l (fd_ed25519_user.c:204-206) and
+   the signed digits of k (radix 16) and S (radix 256). */
+__global__ void __launch_bounds__( FD_WG )
+fd_hash_kernel( unsigned char const *    __restrict__ payload,
+                fdgpu_txn_desc_t const * __restrict__ desc,
+                u32 const *              __restrict__ map,
+                u32                                   nsig,
+                i8 const *               __restrict__ code,
+                i8 *                     __restrict__ digA,
+                i8 *                     __restrict__ digB ) {
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  if( code[s] != FD_ED25519_SUCCESS ) return;
+  size_t n = nsig;
+  u32 m = map[s];
+  u32 t = m & 0xffffffu, j = m >> 24;
+  fdgpu_txn_desc_t d = desc[t];
+  unsigned char const * base = payload + d.payload_off;
+  u32 Rw[8], Aw[8];
+  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
+  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
   u32 h[16], k[8];
   fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
   sc_reduce( k, h );
-
-  /* 5. signed digits */
-  {
-    int carry = 0;
+  int carry = 0;
 #pragma unroll
-    for( int i=0; i<64; i++ ) {
-      int v = (int)((k[i>>3] >> (4*(i&7))) & 15u) + carry;
-      carry = (v + 8) >> 4;
-      digA[(size_t)i*n + s] = (i8)(v - (carry << 4));
-    }
-    carry = 0;
-#pragma unroll
-    for( int i=0; i<32; i++ ) {
-      int v = (int)((Sw[i>>2] >> (8*(i&3))) & 255u) + carry;
-      carry = (v + 128) >> 8;
-      digB[(size_t)i*n + s] = (i8)(v - (carry << 8));
-    }
+  for( int i=0; i<64; i++ ) {
+    int v = (int)((k[i>>3] >> (4*(i&7))) & 15u) + carry;
+    carry = (v + 8) >> 4;
+    digA[(size_t)i*n + s] = (i8)(v - (carry << 4));
   }
+  u32 Sw[8];
+  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
+  carry = 0;
+#pragma unroll
+  for( int i=0; i<32; i++ ) {
+    int v = (int)((Sw[i>>2] >> (8*(i&3))) & 255u) + carry;
+    carry = (v + 128) >> 8;
+    digB[(size_t)i*n + s] = (i8)(v - (carry << 8));
+  }
+}
 
-  /* 6. R affine for the final compare */
-  fe_canon( R.X, R.X );
-  fe_store2( Rxy + 0*n + s, n, R.X );
-  fe_store2( Rxy + 2*n + s, n, R.Y );
-
-  /* 7. table [0..8](-A) in cached form (fd_ed25519_point_neg +
-        the odd-multiple table of fd_curve25519.c:118-131, here all
-        multiples for a signed fixed window) */
-  fe_neg( A.X, A.X ); fe_neg( A.T, A.T );
+/* Stage 3 -- table [0..8](-A) in cached form (fd_ed25519_point_neg + the
+   odd-multiple table of fd_curve25519.c:118-131; here all multiples, for a
+   signed fixed window). */
+__global__ void __launch_bounds__( FD_WG )
+fd_table_kernel( u32 nsig, i8 const * __restrict__ code, uint4 const * __restrict__ Axy,
+                 uint4 * __restrict__ tab ) {
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  if( code[s] != FD_ED25519_SUCCESS ) return;
+  uint4 const * ap = Axy + (size_t)s*4;
+  ge_p3 A;
+  fe_from_quads( A.X, ap[0], ap[1] );
+  fe_from_quads( A.Y, ap[2], ap[3] );
+  A.Z = fe_one();
+  fe_neg( A.X, A.X ); fe_wcarry( A.X, A.X );              /* -A */
+  fe_mul( A.T, A.X, A.Y );
   ge_cached c1, c;
   c.YpX = fe_one(); c.YmX = fe_one(); c.Z = fe_one(); c.T2d = fe_zero();
-  atab_store( tab, n, s, 0, c );
+  atab_store( tab, s, 0, c );
   ge_p3_to_cached( c1, A );
-  atab_store( tab, n, s, 1, c1 );
+  atab_store( tab, s, 1, c1 );
   ge_p3 cur = A;
 #pragma unroll 1
   for( int e=2; e<FD_ATAB_ENTRIES; e++ ) {
     ge_p1p1 tt;
-    ge_add_cached( tt, cur, c1, 0 );
+    ge_add_cached( tt, cur, c1 );
     ge_p1p1_to_p3( cur, tt );
     ge_p3_to_cached( c, cur );
-    atab_store( tab, n, s, e, c );
+    atab_store( tab, s, e, c );
   }
 }
 
@@ -216,47 +262,48 @@ fd_dsm_kernel( u32                      nsig,
 
   ge_p3 P; ge_p3_identity( P );
   ge_p2 P2;
+  atab_raw raw;
   int da = digA[ (size_t)63*n + s ];
-  ge_cached q;
-  atab_load( q, tab, n, s, da < 0 ? -da : da );
 
 #pragma unroll 1
   for( int w=63; w>=0; w-- ) {
+#if FD_DSM_PREFETCH
+    atab_fetch( raw, tab, s, da < 0 ? -da : da );   /* in flight during the doublings */
+#endif
     ge_p1p1 t;
     if( w != 63 ) {
 #pragma unroll 1
       for( int r=0; r<3; r++ ) { ge_dbl( t, P2 ); ge_p1p1_to_p2( P2, t ); }
       ge_dbl( t, P2 ); ge_p1p1_to_p3( P, t );
     }
-    ge_add_cached( t, P, q, da < 0 );
-    int dn = 0;
-    if( w > 0 ) {
-      dn = digA[ (size_t)(w-1)*n + s ];
-      atab_load( q, tab, n, s, dn < 0 ? -dn : dn );   /* prefetch next window's entry */
+    {
+#if !FD_DSM_PREFETCH
+      atab_fetch( raw, tab, s, da < 0 ? -da : da );
+#endif
+      ge_cached q; atab_unpack( q, raw ); ge_cached_cneg( q, da < 0 );
+      ge_add_cached( t, P, q );
     }
     if( !(w & 1) ) {
       ge_p1p1_to_p3( P, t );
       int db = digB[ (size_t)(w>>1)*n + s ];
       int e = db < 0 ? -db : db;
-      ge_precomp bq;
       uint4 const * bp = btab + e*6;
-      uint4 x0=bp[0], x1=bp[1], x2=bp[2], x3=bp[3], x4=bp[4], x5=bp[5];
-      bq.ypx.v[0]=x0.x; bq.ypx.v[1]=x0.y; bq.ypx.v[2]=x0.z; bq.ypx.v[3]=x0.w;
-      bq.ypx.v[4]=x1.x; bq.ypx.v[5]=x1.y; bq.ypx.v[6]=x1.z; bq.ypx.v[7]=x1.w;
-      bq.ymx.v[0]=x2.x; bq.ymx.v[1]=x2.y; bq.ymx.v[2]=x2.z; bq.ymx.v[3]=x2.w;
-      bq.ymx.v[4]=x3.x; bq.ymx.v[5]=x3.y; bq.ymx.v[6]=x3.z; bq.ymx.v[7]=x3.w;
-      bq.xy2d.v[0]=x4.x; bq.xy2d.v[1]=x4.y; bq.xy2d.v[2]=x4.z; bq.xy2d.v[3]=x4.w;
-      bq.xy2d.v[4]=x5.x; bq.xy2d.v[5]=x5.y; bq.xy2d.v[6]=x5.z; bq.xy2d.v[7]=x5.w;
-      ge_add_precomp( t, P, bq, db < 0 );
+      ge_precomp bq;
+      fe_from_quads( bq.ypx,  bp[0], bp[1] );
+      fe_from_quads( bq.ymx,  bp[2], bp[3] );
+      fe_from_quads( bq.xy2d, bp[4], bp[5] );
+      ge_precomp_cneg( bq, db < 0 );
+      ge_add_precomp( t, P, bq );
     }
     ge_p1p1_to_p2( P2, t );
-    da = dn;
+    if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
   }
 
   /* fd_ed25519_point_eq_z1: X == x_R Z and Y == y_R Z */
+  uint4 const * rp = Rxy + (size_t)s*4;
   fe x, y, u;
-  fe_load2( x, Rxy + 0*n + s, n );
-  fe_load2( y, Rxy + 2*n + s, n );
+  fe_from_quads( x, rp[0], rp[1] );
+  fe_from_quads( y, rp[2], rp[3] );
   fe_mul( u, x, P2.Z ); int okx = fe_eq( u, P2.X );
   fe_mul( u, y, P2.Z ); int oky = fe_eq( u, P2.Y );
   code[s] = (okx & oky) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
@@ -284,9 +331,9 @@ fd_reduce_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 n
   txn_out[t] = (i8)r;
 }
 
-/* [e]B for e in [0,128], affine precomputed (y+x, y-x, 2dxy), canonical.
-   Generated on the device at context creation (the GPU analogue of
-   table/fd_curve25519_table_*.c fd_ed25519_base_point_wnaf_table). */
+/* [e]B for e in [0,128], affine precomputed (y+x, y-x, 2dxy), canonical,
+   packed 8x32.  Generated on the device at context creation (the GPU
+   analogue of table/fd_curve25519_table_*.c fd_ed25519_base_point_wnaf_table). */
 __global__ void fd_btab_kernel( uint4 * out ) {
   int e = threadIdx.x;
   if( e >= FD_BTAB_ENTRIES ) return;
@@ -300,11 +347,10 @@ __global__ void fd_btab_kernel( uint4 * out ) {
   fe_invert( zi, acc.Z );
   fe_mul( x, acc.X, zi ); fe_mul( y, acc.Y, zi );
   fe_add( ypx, y, x ); fe_sub( ymx, y, x ); fe_mul( xy, x, y ); fe d2 = fe_d2(); fe_mul( xy, xy, d2 );
-  fe_canon( ypx, ypx ); fe_canon( ymx, ymx ); fe_canon( xy, xy );
   uint4 * o = out + e*6;
-  o[0] = make_uint4( ypx.v[0], ypx.v[1], ypx.v[2], ypx.v[3] ); o[1] = make_uint4( ypx.v[4], ypx.v[5], ypx.v[6], ypx.v[7] );
-  o[2] = make_uint4( ymx.v[0], ymx.v[1], ymx.v[2], ymx.v[3] ); o[3] = make_uint4( ymx.v[4], ymx.v[5], ymx.v[6], ymx.v[7] );
-  o[4] = make_uint4( xy.v[0],  xy.v[1],  xy.v[2],  xy.v[3]  ); o[5] = make_uint4( xy.v[4],  xy.v[5],  xy.v[6],  xy.v[7]  );
+  fe_store_packed( o + 0, ypx );
+  fe_store_packed( o + 2, ymx );
+  fe_store_packed( o + 4, xy );
 }
 
 /* ==================================================================
@@ -340,6 +386,7 @@ struct fdgpu_ed25519_ctx {
   i8 *    d_code;
   uint4 * d_tab;
   uint4 * d_Rxy;
+  uint4 * d_Axy;
   i8 *    d_digA;
   i8 *    d_digB;
   uint4 * d_btab;
@@ -369,8 +416,11 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
   if( nsig ) {
     hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig );
     if( ctx->timing ) hipEventRecord( ev[0], st );
-    hipLaunchKernelGGL( fd_prep_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
-                        ctx->semantics, code, ctx->d_tab, ctx->d_Rxy, ctx->d_digA, ctx->d_digB );
+    hipLaunchKernelGGL( fd_decode_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+                        ctx->semantics, code, ctx->d_Rxy, ctx->d_Axy );
+    hipLaunchKernelGGL( fd_hash_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+                        code, ctx->d_digA, ctx->d_digB );
+    hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_Axy, ctx->d_tab );
     if( ctx->timing ) hipEventRecord( ev[1], st );
     hipLaunchKernelGGL( fd_dsm_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                         ctx->d_digA, ctx->d_digB, ctx->d_btab, code );
@@ -397,6 +447,7 @@ fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
   HIPCHK( hipMalloc( &ctx->d_code, ns ), NULL );
   HIPCHK( hipMalloc( &ctx->d_tab,  ns * FD_ATAB_ENTRIES * 8 * sizeof(uint4) ), NULL );
   HIPCHK( hipMalloc( &ctx->d_Rxy,  ns * 4 * sizeof(uint4) ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_Axy,  ns * 4 * sizeof(uint4) ), NULL );
   HIPCHK( hipMalloc( &ctx->d_digA, ns * 64 ), NULL );
   HIPCHK( hipMalloc( &ctx->d_digB, ns * 32 ), NULL );
   HIPCHK( hipMalloc( &ctx->d_btab, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), NULL );
@@ -430,7 +481,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   if( !ctx ) return;
   hipSetDevice( ctx->device );
   hipStreamSynchronize( ctx->stream );
-  hipFree( ctx->d_map ); hipFree( ctx->d_code ); hipFree( ctx->d_tab ); hipFree( ctx->d_Rxy );
+  hipFree( ctx->d_map ); hipFree( ctx->d_code ); hipFree( ctx->d_tab ); hipFree( ctx->d_Rxy ); hipFree( ctx->d_Axy );
   hipFree( ctx->d_digA ); hipFree( ctx->d_digB ); hipFree( ctx->d_btab );
   for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ev[i] );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ring[r][i] );

@@ -13,9 +13,13 @@
 
 struct ge_p2    { fe X, Y, Z; };        /* projective                    */
 struct ge_p3    { fe X, Y, Z, T; };     /* extended, T = XY/Z            */
-struct ge_p1p1  { fe X, Y, Z, T; };     /* completed: (X:Z),(Y:T)        */
+struct ge_p1p1  { fe X, Y, Z, T; };     /* completed: (X:T),(Y:Z)        */
 struct ge_cached{ fe YpX, YmX, Z, T2d; };
 struct ge_precomp{ fe ypx, ymx, xy2d; };/* affine, Z = 1                 */
+
+/* Bound annotations (fd_gpu_f25519.h): every coordinate handed to a
+   multiply is T or L; the two "D-C"/"E" style differences of loose
+   values are brought back to T with fe_wcarry. */
 
 FD_DEV void ge_p3_identity( ge_p3 & p ) { p.X = fe_zero(); p.Y = fe_one(); p.Z = fe_one(); p.T = fe_zero(); }
 
@@ -26,62 +30,77 @@ FD_DEV void ge_p1p1_to_p3( ge_p3 & r, ge_p1p1 const & p ) {
   fe_mul( r.X, p.X, p.T ); fe_mul( r.Y, p.Y, p.Z ); fe_mul( r.Z, p.Z, p.T ); fe_mul( r.T, p.X, p.Y );
 }
 
-/* 2P for a=-1 twisted Edwards from (X:Y:Z) -- eprint 2008/522 §4.4:
-   4 squarings. */
+/* 2P for a=-1 twisted Edwards from (X:Y:Z) T -- eprint 2008/522 §4.4:
+   4 squarings.  Out: X=E (T), Y=H (L), Z=G (L), T=F (T). */
 FD_DEV void ge_dbl( ge_p1p1 & r, ge_p2 const & p ) {
-  fe t0;
-  fe_sqr( r.X, p.X );                 /* XX        */
-  fe_sqr( r.Z, p.Y );                 /* YY        */
-  fe_sqr( r.T, p.Z );                 /* ZZ        */
-  fe_add( r.T, r.T, r.T );            /* 2ZZ       */
-  fe_add( r.Y, p.X, p.Y );
-  fe_sqr( t0, r.Y );                  /* (X+Y)^2   */
-  fe_add( r.Y, r.Z, r.X );            /* YY+XX     */
-  fe_sub( r.Z, r.Z, r.X );            /* YY-XX     */
-  fe_sub( r.X, t0, r.Y );             /* 2XY       */
-  fe_sub( r.T, r.T, r.Z );            /* 2ZZ-YY+XX */
+  fe xx, yy, zz, s;
+  fe_sqr( xx, p.X );                  /* XX (T)               */
+  fe_sqr( yy, p.Y );                  /* YY (T)               */
+  fe_sqr( zz, p.Z );                  /* ZZ (T)               */
+  fe_add( s, p.X, p.Y );              /* X+Y (L)              */
+  fe_sqr( s, s );                     /* (X+Y)^2 (T)          */
+  fe_add( r.Y, yy, xx );              /* H = YY+XX (L)        */
+  fe_sub( r.Z, yy, xx );              /* G = YY-XX (L)        */
+  fe_sub4( r.X, s, r.Y );             /* E = (X+Y)^2-H = 2XY  */
+  fe_wcarry( r.X, r.X );
+  fe_add( zz, zz, zz );               /* 2ZZ (L)              */
+  fe_sub4( r.T, zz, r.Z );            /* F = 2ZZ-G            */
+  fe_wcarry( r.T, r.T );
 }
 
-/* P + (neg ? -Q : Q), Q cached (eprint 2008/522 §4.2, 4 mul).  -Q swaps
-   YpX/YmX and negates T2d, i.e. swaps the roles of D+C and D-C. */
-FD_DEV void ge_add_cached( ge_p1p1 & r, ge_p3 const & p, ge_cached const & q, int neg ) {
-  fe a, b, c, d, qp, qm;
-  fe_sel( qp, neg, q.YmX, q.YpX );
-  fe_sel( qm, neg, q.YpX, q.YmX );
+/* P + Q, P T, Q cached (already negated by the caller if needed)
+   (eprint 2008/522 §4.2, 4 mul).  Out: X=E, Y=H, Z=G (L), T=F (T). */
+FD_DEV void ge_add_cached( ge_p1p1 & r, ge_p3 const & p, ge_cached const & q ) {
+  fe a, b, c, d;
   fe_add( a, p.Y, p.X );
   fe_sub( b, p.Y, p.X );
-  fe_mul( a, a, qp );
-  fe_mul( b, b, qm );
-  fe_mul( c, q.T2d, p.T );
+  fe_mul( a, a, q.YpX );              /* A (T) */
+  fe_mul( b, b, q.YmX );              /* B (T) */
+  fe_mul( c, q.T2d, p.T );            /* C (T) */
   fe_mul( d, p.Z, q.Z );
-  fe_add( d, d, d );
-  fe_sub( r.X, a, b );
-  fe_add( r.Y, a, b );
-  fe_add( a, d, c );
-  fe_sub( b, d, c );
-  fe_sel( r.Z, neg, b, a );
-  fe_sel( r.T, neg, a, b );
+  fe_add( d, d, d );                  /* D = 2 Z1 Z2 (L) */
+  fe_sub( r.X, a, b );                /* E (L) */
+  fe_add( r.Y, a, b );                /* H (L) */
+  fe_add( r.Z, d, c );                /* G (L) */
+  fe_sub( r.T, d, c );                /* F */
+  fe_wcarry( r.T, r.T );
 }
 
-/* P + (neg ? -Q : Q), Q affine precomputed (3 mul). */
-FD_DEV void ge_add_precomp( ge_p1p1 & r, ge_p3 const & p, ge_precomp const & q, int neg ) {
-  fe a, b, c, d, qp, qm;
-  fe_sel( qp, neg, q.ymx, q.ypx );
-  fe_sel( qm, neg, q.ypx, q.ymx );
+/* P + Q, Q affine precomputed (Z=1), already negated if needed (3 mul). */
+FD_DEV void ge_add_precomp( ge_p1p1 & r, ge_p3 const & p, ge_precomp const & q ) {
+  fe a, b, c, d;
   fe_add( a, p.Y, p.X );
   fe_sub( b, p.Y, p.X );
-  fe_mul( a, a, qp );
-  fe_mul( b, b, qm );
+  fe_mul( a, a, q.ypx );
+  fe_mul( b, b, q.ymx );
   fe_mul( c, q.xy2d, p.T );
   fe_add( d, p.Z, p.Z );
   fe_sub( r.X, a, b );
   fe_add( r.Y, a, b );
-  fe_add( a, d, c );
-  fe_sub( b, d, c );
-  fe_sel( r.Z, neg, b, a );
-  fe_sel( r.T, neg, a, b );
+  fe_add( r.Z, d, c );
+  fe_sub( r.T, d, c );
+  fe_wcarry( r.T, r.T );
 }
 
+/* -Q for a cached point: swap Y+X / Y-X, negate 2dT (T in -> L out) */
+FD_DEV void ge_cached_cneg( ge_cached & q, int neg ) {
+  fe t, n;
+  fe_sel( t, neg, q.YmX, q.YpX );
+  fe_sel( q.YmX, neg, q.YpX, q.YmX );
+  q.YpX = t;
+  fe_neg( n, q.T2d );
+  fe_sel( q.T2d, neg, n, q.T2d );
+}
+FD_DEV void ge_precomp_cneg( ge_precomp & q, int neg ) {
+  fe t, n;
+  fe_sel( t, neg, q.ymx, q.ypx );
+  fe_sel( q.ymx, neg, q.ypx, q.ymx );
+  q.ypx = t;
+  fe_neg( n, q.xy2d );
+  fe_sel( q.xy2d, neg, n, q.xy2d );
+}
+
+/* p T */
 FD_DEV void ge_p3_to_cached( ge_cached & r, ge_p3 const & p ) {
   fe_add( r.YpX, p.Y, p.X );
   fe_sub( r.YmX, p.Y, p.X );
@@ -97,8 +116,11 @@ FD_DEV void ge_p3_dbl( ge_p3 & r, ge_p3 const & p ) {
 
 FD_DEV void ge_p3_add( ge_p3 & r, ge_p3 const & p, ge_p3 const & q ) {
   ge_cached c; ge_p3_to_cached( c, q );
-  ge_p1p1 t; ge_add_cached( t, p, c, 0 ); ge_p1p1_to_p3( r, t );
+  ge_p1p1 t; ge_add_cached( t, p, c ); ge_p1p1_to_p3( r, t );
 }
+
+/* canonicalise in place (pack + unpack): any value with limbs < 2^31 -> T canonical */
+FD_DEV void fe_canon( fe & a ) { u32 w[8]; fe_pack( w, a ); fe_unpack( a, w ); }
 
 /* ---- decompression -------------------------------------------------- */
 
@@ -109,57 +131,57 @@ FD_DEV void ge_p3_add( ge_p3 & r, ge_p3 const & p, ge_p3 const & q ) {
    Returns per point: 0 ok, 1 not a square, 2 x==0 with sign bit set
    (the AVX-512 decode rejects this, avx512/fd_r43x6_ge.c:230-232; the
    portable decode negates 0 and accepts, fd_curve25519.c:41-43 -- the
-   caller decides).  On 0 or 2, x has the requested sign. */
-FD_DEV void ge_decode2( ge_p3 & Pa, int & ra, u32 const wa[ 8 ],
-                        ge_p3 & Pb, int & rb, u32 const wb[ 8 ] ) {
+   caller decides).  Outputs are canonical T with Z=1, T=xy. */
+FD_DEV void ge_decode1( ge_p3 & P, int & rc, u32 const w[ 8 ] ) {
   fe one = fe_one(), d = fe_d();
-  fe ya, yb; fe_from_words( ya, wa ); fe_from_words( yb, wb );
-  int sa = (int)(wa[7] >> 31), sb = (int)(wb[7] >> 31);
-  fe ua, ub, va, vb, t, s;
-  fe_sqr( ua, ya );              fe_sqr( ub, yb );
-  fe_mul( va, ua, d );           fe_mul( vb, ub, d );
-  fe_sub( ua, ua, one );         fe_sub( ub, ub, one );
-  fe_add( va, va, one );         fe_add( vb, vb, one );
-  fe v3a, v3b, uv3a, uv3b, uv7a, uv7b;
-  fe_sqr( t, va );               fe_sqr( s, vb );
-  fe_mul( v3a, t, va );          fe_mul( v3b, s, vb );
-  fe_mul( uv3a, ua, v3a );       fe_mul( uv3b, ub, v3b );
-  fe_sqr( t, v3a );              fe_sqr( s, v3b );
-  fe_mul( t, t, va );            fe_mul( s, s, vb );          /* v^7 */
-  fe_mul( uv7a, ua, t );         fe_mul( uv7b, ub, s );
-  fe xa, xb;
-  fe_pow22523_2( xa, uv7a, xb, uv7b );
-  fe_mul( xa, xa, uv3a );        fe_mul( xb, xb, uv3b );
-  /* check */
-  fe_sqr( t, xa );               fe_sqr( s, xb );
-  fe_mul( t, t, va );            fe_mul( s, s, vb );          /* v x^2 */
-  fe na, nb;
-  fe_sub( na, t, ua );           fe_sub( nb, s, ub );
-  int oka = fe_is_zero( na ),    okb = fe_is_zero( nb );
-  fe_add( na, t, ua );           fe_add( nb, s, ub );
-  int fla = fe_is_zero( na ),    flb = fe_is_zero( nb );
-  fe i = fe_sqrtm1();
-  fe_mul( t, xa, i );            fe_mul( s, xb, i );
-  fe_sel( xa, !oka, t, xa );     fe_sel( xb, !okb, s, xb );
-  /* sign */
-  fe_canon( xa, xa );            fe_canon( xb, xb );
-  u32 za = 0, zb = 0;
+  fe y; fe_unpack( y, w );
+  int sgn = (int)(w[7] >> 31);
+  fe u, v, t, uv3, x;
+  fe_sqr( u, y );
+  fe_mul( v, u, d );
+  fe_sub( u, u, one );           /* u = y^2-1 (L) */
+  fe_add( v, v, one );           /* v = dy^2+1 (L) */
+  fe_sqr( t, v );
+  fe_mul( t, t, v );             /* v^3 */
+  fe_mul( uv3, u, t );           /* u v^3 */
+  fe_sqr( t, t );
+  fe_mul( t, t, v );             /* v^7 */
+  fe_mul( t, u, t );             /* u v^7 */
+  fe_pow22523( x, t );
+  fe_mul( x, x, uv3 );
+  fe_sqr( t, x );
+  fe_mul( t, t, v );             /* v x^2 (T) */
+  u32 wt[8], wu[8], wn[8];
+  fe n; fe_add( n, t, u );       /* v x^2 + u */
+  fe_pack( wt, t ); fe_pack( wu, u ); fe_pack( wn, n );
+  u32 ne = 0, nz = 0;
 #pragma unroll
-  for( int k=0; k<8; k++ ) { za |= xa.v[k]; zb |= xb.v[k]; }
-  fe_neg( t, xa );               fe_neg( s, xb );
-  fe_sel( xa, (int)(xa.v[0] & 1u) != sa, t, xa );
-  fe_sel( xb, (int)(xb.v[0] & 1u) != sb, s, xb );
-  ra = ( oka | fla ) ? ( ( za==0u && sa ) ? 2 : 0 ) : 1;
-  rb = ( okb | flb ) ? ( ( zb==0u && sb ) ? 2 : 0 ) : 1;
-  Pa.X = xa; Pa.Y = ya; Pa.Z = one; fe_mul( Pa.T, xa, ya );
-  Pb.X = xb; Pb.Y = yb; Pb.Z = one; fe_mul( Pb.T, xb, yb );
+  for( int k=0; k<8; k++ ) { ne |= wt[k] ^ wu[k]; nz |= wn[k]; }
+  int ok = ne==0u, flip = nz==0u;
+  fe i = fe_sqrtm1();
+  fe_mul( t, x, i );
+  fe_sel( x, !ok, t, x );
+  u32 wx[8]; fe_pack( wx, x );
+  u32 z = 0;
+#pragma unroll
+  for( int k=0; k<8; k++ ) z |= wx[k];
+  fe_unpack( x, wx );            /* canonical */
+  fe_neg( t, x ); fe_canon( t );
+  fe_sel( x, (int)(wx[0] & 1u) != sgn, t, x );
+  rc = ( ok | flip ) ? ( ( z==0u && sgn ) ? 2 : 0 ) : 1;
+  P.X = x; P.Y = y; P.Z = one; fe_mul( P.T, x, y );
 }
 
 /* fd_ed25519_affine_is_small_order (fd_curve25519.h:88-118): on a decoded
    (Z=1) point, X==0 | Y==0 | Y==y0 | Y==y1. */
 FD_DEV int ge_affine_is_small_order( ge_p3 const & p ) {
-  fe y0 = fe_y0(), y1 = fe_y1();
-  return fe_is_zero( p.X ) | fe_is_zero( p.Y ) | fe_eq( p.Y, y0 ) | fe_eq( p.Y, y1 );
+  u32 const y0[8] = FD_Y0_W, y1[8] = FD_Y1_W;
+  u32 wy[8]; fe_pack( wy, p.Y );
+  u32 zx = 0, zy = 0, e0 = 0, e1 = 0;
+  u32 wx[8]; fe_pack( wx, p.X );
+#pragma unroll
+  for( int k=0; k<8; k++ ) { zx |= wx[k]; zy |= wy[k]; e0 |= wy[k] ^ y0[k]; e1 |= wy[k] ^ y1[k]; }
+  return (zx==0u) | (zy==0u) | (e0==0u) | (e1==0u);
 }
 
 /* ---- scalars mod l ---------------------------------------------------- */

@@ -1,20 +1,32 @@
 #pragma once
 /* fd_gpu_f25519.h -- GF(2^255-19) for CDNA4 (gfx950), one field element
-   per lane in 8 x 32-bit limbs (little endian), device code only.
+   per lane, device code only.
 
    MI355X-native replacement for the reference's field layer
    (src/ballet/ed25519/fd_f25519.h API; AVX-512 r43x6 backend
    avx512/fd_r43x6.h, portable fiat 5x51 backend ref/fd_f25519.h).  Not a
    port of either: the reference packs ONE element into 6 lanes of a zmm
    (latency-optimised, one signature at a time); here each of the 64
-   lanes of a wave owns a whole element of its own signature, and the
-   limb products are v_mad_u64_u32 (32x32+64 -> 64, carry-out in an SGPR
-   pair) carry chains.
+   lanes of a wave owns a whole element of its own signature.
 
-   Representation invariant: a "fe" holds any value in [0, 2^256) that is
-   congruent to the field element (weakly reduced); fe_canon() maps to
-   [0,p).  Every operation below accepts and returns weakly reduced
-   values, so there is no overflow bookkeeping between operations. */
+   Representation: 10 unsigned 32-bit limbs, radix 2^25.5 (limb i sits
+   at bit ceil(25.5 i), 26 bits wide for even i, 25 for odd i).  Products
+   are v_mad_u64_u32 (32x32+64 -> 64) accumulated carry-free in 64-bit
+   column sums; one carry chain per multiply.  Measured on MI355X
+   (tools/fieldbench) this beats a saturated 8x32-bit Comba multiply:
+   the 10 column sums are independent chains (ILP instead of one serial
+   carry chain), additions need no carry propagation at all, and a
+   squaring costs 55 products instead of 100.
+
+   Bounds (unsigned; every function states what it accepts):
+     T "tight": limbs < 2^26+2^17 (even) / 2^25+2^17 (odd).  Output of
+                fe_mul, fe_sqr, fe_wcarry, fe_unpack.
+     L "loose": limbs < 1.5*2^27+2^17 (even) / 1.5*2^26+2^17 (odd).
+                T+T, T+T+T, T-T (2p bias) and 2p-T are L.
+   fe_mul/fe_sqr accept L inputs (every 32-bit operand, incl. 19*g and
+   4*f, stays < 2^32 and every 64-bit column sum < 2^63).  fe_sub needs a
+   T subtrahend.  Anything looser (e.g. L-L via fe_sub4) must go through
+   fe_wcarry (one parallel carry step) before it reaches a multiply. */
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -25,159 +37,145 @@ typedef uint32_t u32;
 typedef uint64_t u64;
 typedef int64_t  i64;
 
-struct fe { u32 v[8]; };
+struct fe { u32 v[10]; };
 
 FD_DEV u64 fd_mad( u32 a, u32 b, u64 c ) { return (u64)a * (u64)b + c; }
 
+#define FE_W(i)    ( ((i) & 1) ? 25 : 26 )
+#define FE_M(i)    ( ((i) & 1) ? 0x1ffffffu : 0x3ffffffu )
+#define FE_S(i)    ( (51*(i)+1) / 2 )            /* ceil(25.5 i) */
+
 /* ---- constants ----------------------------------------------------- */
 
-#define FE_C(a0,a1,a2,a3,a4,a5,a6,a7) {{a0,a1,a2,a3,a4,a5,a6,a7}}
+#define FE10(a0,a1,a2,a3,a4,a5,a6,a7,a8,a9) {{a0,a1,a2,a3,a4,a5,a6,a7,a8,a9}}
 
-FD_DEV fe fe_zero( void ) { fe r = FE_C(0,0,0,0,0,0,0,0); return r; }
-FD_DEV fe fe_one ( void ) { fe r = FE_C(1,0,0,0,0,0,0,0); return r; }
+FD_DEV fe fe_zero( void ) { fe r = FE10(0,0,0,0,0,0,0,0,0,0); return r; }
+FD_DEV fe fe_one ( void ) { fe r = FE10(1,0,0,0,0,0,0,0,0,0); return r; }
 /* d = -121665/121666 */
-FD_DEV fe fe_d   ( void ) { fe r = FE_C(0x135978a3u,0x75eb4dcau,0x4141d8abu,0x00700a4du,0x7779e898u,0x8cc74079u,0x2b6ffe73u,0x52036ceeu); return r; }
-FD_DEV fe fe_d2  ( void ) { fe r = FE_C(0x26b2f159u,0xebd69b94u,0x8283b156u,0x00e0149au,0xeef3d130u,0x198e80f2u,0x56dffce7u,0x2406d9dcu); return r; }
+FD_DEV fe fe_d( void )  { fe r = FE10(0x35978a3u,0x0d37284u,0x3156ebdu,0x06a0a0eu,0x001c029u,0x179e898u,0x3a03cbbu,0x1ce7198u,0x2e2b6ffu,0x1480db3u); return r; }
+FD_DEV fe fe_d2( void ) { fe r = FE10(0x2b2f159u,0x1a6e509u,0x22add7au,0x0d4141du,0x0038052u,0x0f3d130u,0x3407977u,0x19ce331u,0x1c56dffu,0x0901b67u); return r; }
 /* sqrt(-1) = 2^((p-1)/4) */
-FD_DEV fe fe_sqrtm1( void ) { fe r = FE_C(0x4a0ea0b0u,0xc4ee1b27u,0xad2fe478u,0x2f431806u,0x3dfbd7a7u,0x2b4d0099u,0x4fc1df0bu,0x2b832480u); return r; }
-/* y coordinates of the order-8 points (fd_curve25519.h:88-118) */
-FD_DEV fe fe_y0  ( void ) { fe r = FE_C(0x8f95e826u,0xb027b2c2u,0x89f4c345u,0xf098eff2u,0x05acdfd5u,0x3933c6d3u,0x880238b1u,0x05fc536du); return r; }
-FD_DEV fe fe_y1  ( void ) { fe r = FE_C(0x706a17c7u,0x4fd84d3du,0x760b3cbau,0x0f67100du,0xfa53202au,0xc6cc392cu,0x77fdc74eu,0x7a03ac92u); return r; }
+FD_DEV fe fe_sqrtm1( void ) { fe r = FE10(0x20ea0b0u,0x186c9d2u,0x08f189du,0x035697fu,0x0bd0c60u,0x1fbd7a7u,0x2804c9eu,0x1e16569u,0x004fc1du,0x0ae0c92u); return r; }
 /* base point B (affine) */
-FD_DEV fe fe_Bx  ( void ) { fe r = FE_C(0x8f25d51au,0xc9562d60u,0x9525a7b2u,0x692cc760u,0xfdd6dc5cu,0xc0a4e231u,0xcd6e53feu,0x216936d3u); return r; }
-FD_DEV fe fe_By  ( void ) { fe r = FE_C(0x66666658u,0x66666666u,0x66666666u,0x66666666u,0x66666666u,0x66666666u,0x66666666u,0x66666666u); return r; }
+FD_DEV fe fe_Bx( void ) { fe r = FE10(0x325d51au,0x18b5823u,0x0f6592au,0x104a92du,0x1a4b31du,0x1d6dc5cu,0x27118feu,0x07fd814u,0x13cd6e5u,0x085a4dbu); return r; }
+FD_DEV fe fe_By( void ) { fe r = FE10(0x2666658u,0x1999999u,0x0ccccccu,0x1333333u,0x1999999u,0x0666666u,0x3333333u,0x0ccccccu,0x2666666u,0x1999999u); return r; }
 
-/* ---- add / sub ----------------------------------------------------- */
+/* y coordinates of the order-8 points (fd_curve25519.h:88-118), canonical 8x32 */
+#define FD_Y0_W { 0x8f95e826u,0xb027b2c2u,0x89f4c345u,0xf098eff2u,0x05acdfd5u,0x3933c6d3u,0x880238b1u,0x05fc536du }
+#define FD_Y1_W { 0x706a17c7u,0x4fd84d3du,0x760b3cbau,0x0f67100du,0xfa53202au,0xc6cc392cu,0x77fdc74eu,0x7a03ac92u }
 
-/* r = a + b mod p (weak).  a+b < 2^257: fold the carry as 38 (2^256 = 38
-   mod p); a second carry is only possible when the low 256 bits are
-   < 38, so the final 38*c cannot overflow. */
+/* ---- add / sub / carry ----------------------------------------------- */
+
+/* r = a + b (no carry).  T+T -> L; (T+T)+T -> L. */
 FD_DEV void fe_add( fe & r, fe const & a, fe const & b ) {
-  u64 c = 0;
 #pragma unroll
-  for( int i=0; i<8; i++ ) { c += (u64)a.v[i] + (u64)b.v[i]; r.v[i] = (u32)c; c >>= 32; }
-  c *= 38u;
-#pragma unroll
-  for( int i=0; i<8; i++ ) { c += (u64)r.v[i]; r.v[i] = (u32)c; c >>= 32; }
-  r.v[0] += (u32)c * 38u;
+  for( int i=0; i<10; i++ ) r.v[i] = a.v[i] + b.v[i];
 }
 
-/* r = a - b mod p (weak).  A borrow means the result wrapped by 2^256
-   = 38 mod p, so subtract 38; a second borrow (low part < 38) wraps
-   again and is fixed by one more -38 that cannot borrow. */
+/* r = a - b + 2p.  b must be T (limbs <= 2p limbs).  a T -> r L. */
 FD_DEV void fe_sub( fe & r, fe const & a, fe const & b ) {
-  u64 c = 0;
 #pragma unroll
-  for( int i=0; i<8; i++ ) { c = (u64)a.v[i] - (u64)b.v[i] - c; r.v[i] = (u32)c; c = (c >> 32) & 1u; }
-  c *= 38u;
-#pragma unroll
-  for( int i=0; i<8; i++ ) { c = (u64)r.v[i] - c; r.v[i] = (u32)c; c = (c >> 32) & 1u; }
-  r.v[0] -= (u32)c * 38u;
+  for( int i=0; i<10; i++ ) {
+    u32 twop = (i==0) ? 0x7ffffdau : ( (i & 1) ? 0x3fffffeu : 0x7fffffeu );
+    r.v[i] = a.v[i] + twop - b.v[i];
+  }
 }
 
+/* r = a - b + 4p.  b may be L.  Result must be fe_wcarry'd before a mul. */
+FD_DEV void fe_sub4( fe & r, fe const & a, fe const & b ) {
+#pragma unroll
+  for( int i=0; i<10; i++ ) {
+    u32 fourp = (i==0) ? 0xfffffb4u : ( (i & 1) ? 0x7fffffcu : 0xffffffcu );
+    r.v[i] = a.v[i] + fourp - b.v[i];
+  }
+}
+
+/* r = -a = 2p - a (a T -> r L) */
 FD_DEV void fe_neg( fe & r, fe const & a ) { fe z = fe_zero(); fe_sub( r, z, a ); }
 
-/* ---- 256x256 -> 512 products and the 512 -> 256 fold -------------- */
-
-/* r = t mod p (weak), t = 16 words.  2^256 = 38 mod p. */
-FD_DEV void fe_fold512( fe & r, u32 const t[ 16 ] ) {
-  u64 c = 0;
+/* one parallel carry step: limbs < 2^31 in -> T out */
+FD_DEV void fe_wcarry( fe & r, fe const & a ) {
+  u32 c[10];
 #pragma unroll
-  for( int i=0; i<8; i++ ) { c = fd_mad( t[8+i], 38u, c + (u64)t[i] ); r.v[i] = (u32)c; c >>= 32; }
-  c *= 38u;                         /* c <= 38 -> <= 1444 */
+  for( int i=0; i<10; i++ ) c[i] = a.v[i] >> FE_W(i);
+  r.v[0] = (a.v[0] & FE_M(0)) + 19u * c[9];
 #pragma unroll
-  for( int i=0; i<8; i++ ) { c += (u64)r.v[i]; r.v[i] = (u32)c; c >>= 32; }
-  r.v[0] += (u32)c * 38u;
+  for( int i=1; i<10; i++ ) r.v[i] = (a.v[i] & FE_M(i)) + c[i-1];
 }
 
-#ifndef FD_GPU_MUL_ASM
-#define FD_GPU_MUL_ASM 1
-#endif
-
-#if FD_GPU_MUL_ASM
-/* Product scanning (Comba) with a 96-bit column accumulator {acc64,hi}:
-   v_mad_u64_u32 acc = a*b + acc (carry-out -> SGPR pair), then
-   v_addc_co_u32 hi += carry.  Two VALU ops per 32x32 product. */
-FD_DEV void fd_mac( u64 & acc, u32 & hi, u32 a, u32 b ) {
-  u64 cc;
-  asm( "v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
-                "v_addc_co_u32_e64 %1, %2, %1, 0, %2"
-                : "+v"(acc), "+v"(hi), "=&s"(cc)
-                : "v"(a), "v"(b) );
-}
-/* first product of a column whose running accumulator is {acc64} only */
-FD_DEV void fd_mac0( u64 & acc, u32 & hi, u32 a, u32 b ) {
-  u64 cc;
-  asm( "v_mad_u64_u32 %0, %2, %3, %4, %0\n\t"
-                "v_addc_co_u32_e64 %1, %2, 0, 0, %2"
-                : "+v"(acc), "=v"(hi), "=&s"(cc)
-                : "v"(a), "v"(b) );
+/* 64-bit column sums -> T (carry order of ref10 fe_mul) */
+FD_DEV void fe_carry64( fe & r, u64 h[ 10 ] ) {
+  u64 c;
+  c = h[0] >> 26; h[1] += c; h[0] &= 0x3ffffffUL;
+  c = h[4] >> 26; h[5] += c; h[4] &= 0x3ffffffUL;
+  c = h[1] >> 25; h[2] += c; h[1] &= 0x1ffffffUL;
+  c = h[5] >> 25; h[6] += c; h[5] &= 0x1ffffffUL;
+  c = h[2] >> 26; h[3] += c; h[2] &= 0x3ffffffUL;
+  c = h[6] >> 26; h[7] += c; h[6] &= 0x3ffffffUL;
+  c = h[3] >> 25; h[4] += c; h[3] &= 0x1ffffffUL;
+  c = h[7] >> 25; h[8] += c; h[7] &= 0x1ffffffUL;
+  c = h[4] >> 26; h[5] += c; h[4] &= 0x3ffffffUL;
+  c = h[8] >> 26; h[9] += c; h[8] &= 0x3ffffffUL;
+  c = h[9] >> 25; h[0] += c * 19u; h[9] &= 0x1ffffffUL;
+  c = h[0] >> 26; h[1] += c; h[0] &= 0x3ffffffUL;
+#pragma unroll
+  for( int i=0; i<10; i++ ) r.v[i] = (u32)h[i];
 }
 
-FD_DEV void fe_mul_wide( u32 t[ 16 ], fe const & a, fe const & b ) {
-  u64 acc = 0; u32 hi = 0;
+/* ---- multiply / square ------------------------------------------------- */
+
+/* r = f * g; f, g L -> r T.  Column k sums f_i g_j over i+j == k (mod 10);
+   weight 2 when i and j are both odd (ceil(25.5i)+ceil(25.5j) =
+   ceil(25.5(i+j)) + 1), weight 19 when i+j >= 10 (2^255 = 19). */
+FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
+  u32 g19[10], f2[10];
 #pragma unroll
-  for( int k=0; k<15; k++ ) {
-    int first = 1;
+  for( int i=0; i<10; i++ ) { g19[i] = 19u * g.v[i]; f2[i] = 2u * f.v[i]; }
+  u64 h[10];
 #pragma unroll
-    for( int i=0; i<8; i++ ) {
-      int j = k - i;
-      if( j<0 || j>7 ) continue;
-      if( first ) { fd_mac0( acc, hi, a.v[i], b.v[j] ); first = 0; }
-      else          fd_mac ( acc, hi, a.v[i], b.v[j] );
+  for( int k=0; k<10; k++ ) {
+    u64 acc = 0;
+#pragma unroll
+    for( int i=0; i<10; i++ ) {
+      int j = k - i, wrap = j < 0;
+      if( wrap ) j += 10;
+      u32 a = ( (i & 1) && (j & 1) ) ? f2[i] : f.v[i];
+      u32 b = wrap ? g19[j] : g.v[j];
+      acc = fd_mad( a, b, acc );
     }
-    t[k] = (u32)acc;
-    acc  = (acc >> 32) | ((u64)hi << 32);
+    h[k] = acc;
   }
-  t[15] = (u32)acc;
+  fe_carry64( r, h );
 }
 
-/* squaring: cross products once, doubled, plus the diagonal */
-FD_DEV void fe_sqr_wide( u32 t[ 16 ], fe const & a ) {
-  u64 acc = 0; u32 hi = 0;
+/* r = f^2; f L -> r T.  55 products: pair (i<j) weight 2, both odd x2,
+   wrap x19; operands 2f/4f (<2^28.6) and 19f (<2^31.9). */
+FD_DEV void fe_sqr( fe & r, fe const & f ) {
+  u32 f2[10], f4[10], f19[10];
 #pragma unroll
-  for( int k=0; k<15; k++ ) {
-    /* column k: sum_{i<j, i+j=k} a_i a_j, doubled, + a_{k/2}^2 */
-    u64 x = 0; u32 xh = 0; int first = 1;
+  for( int i=0; i<10; i++ ) { f2[i] = 2u * f.v[i]; f4[i] = 4u * f.v[i]; f19[i] = 19u * f.v[i]; }
+  u64 h[10];
 #pragma unroll
-    for( int i=0; i<8; i++ ) {
-      int j = k - i;
-      if( j<=i || j>7 ) continue;
-      if( first ) { fd_mac0( x, xh, a.v[i], a.v[j] ); first = 0; }
-      else          fd_mac ( x, xh, a.v[i], a.v[j] );
+  for( int k=0; k<10; k++ ) {
+    u64 acc = 0;
+#pragma unroll
+    for( int i=0; i<10; i++ ) {
+#pragma unroll
+      for( int j=i; j<10; j++ ) {
+        if( ( (i + j) % 10 ) != k ) continue;
+        int odd2 = (i & 1) && (j & 1);
+        int pair = i < j;
+        int wrap = i + j >= 10;
+        int m = (pair ? 2 : 1) * (odd2 ? 2 : 1);   /* 1, 2 or 4 */
+        u32 a = m==1 ? f.v[i] : ( m==2 ? f2[i] : f4[i] );
+        u32 b = wrap ? f19[j] : f.v[j];
+        acc = fd_mad( a, b, acc );
+      }
     }
-    /* acc += 2*x */
-    u64 x2 = x << 1; u32 x2h = (xh << 1) | (u32)(x >> 63);
-    if( first ) { x2 = 0; x2h = 0; }
-    if( !(k & 1) ) { u32 d = a.v[k>>1]; u64 sq = (u64)d * d; u64 s = x2 + sq; x2h += (s < x2); x2 = s; }
-    u64 s = acc + x2; u32 carry = (s < acc);
-    acc = s; hi += x2h + carry;
-    t[k] = (u32)acc;
-    acc  = (acc >> 32) | ((u64)hi << 32);
-    hi = 0;
+    h[k] = acc;
   }
-  t[15] = (u32)acc;
+  fe_carry64( r, h );
 }
-#else
-/* Operand scanning in plain C (compiler picks v_mad_u64_u32). */
-FD_DEV void fe_mul_wide( u32 t[ 16 ], fe const & a, fe const & b ) {
-  { u64 c = 0;
-#pragma unroll
-    for( int j=0; j<8; j++ ) { c = fd_mad( a.v[0], b.v[j], c ); t[j] = (u32)c; c >>= 32; }
-    t[8] = (u32)c; }
-#pragma unroll
-  for( int i=1; i<8; i++ ) {
-    u64 c = 0;
-#pragma unroll
-    for( int j=0; j<8; j++ ) { c = fd_mad( a.v[i], b.v[j], (u64)t[i+j] + c ); t[i+j] = (u32)c; c >>= 32; }
-    t[i+8] = (u32)c;
-  }
-}
-FD_DEV void fe_sqr_wide( u32 t[ 16 ], fe const & a ) { fe_mul_wide( t, a, a ); }
-#endif
-
-FD_DEV void fe_mul( fe & r, fe const & a, fe const & b ) { u32 t[16]; fe_mul_wide( t, a, b ); fe_fold512( r, t ); }
-FD_DEV void fe_sqr( fe & r, fe const & a ) { u32 t[16]; fe_sqr_wide( t, a ); fe_fold512( r, t ); }
 
 /* r = a^(2^n) */
 FD_DEV void fe_sqrn( fe & r, fe const & a, int n ) {
@@ -186,42 +184,76 @@ FD_DEV void fe_sqrn( fe & r, fe const & a, int n ) {
   for( int i=1; i<n; i++ ) fe_sqr( r, r );
 }
 
-/* ---- canonical form and comparisons -------------------------------- */
+/* ---- packed 8 x 32-bit form (canonical) ---------------------------------- */
 
-/* r = a mod p in [0,p) */
-FD_DEV void fe_canon( fe & r, fe const & a ) {
-  /* fold bit 255: a = h*2^255 + l, 2^255 = 19 mod p */
-  u32 h = a.v[7] >> 31;
-  u64 c = (u64)h * 19u;
+/* w (8 LE words, bit 255 ignored) -> limbs (T); accepts non-canonical
+   values >= p (fd_f25519_frombytes / fiat curve25519_64.c:802) */
+FD_DEV void fe_unpack( fe & r, u32 const w[ 8 ] ) {
 #pragma unroll
-  for( int i=0; i<8; i++ ) { c += (u64)( i==7 ? (a.v[7] & 0x7fffffffu) : a.v[i] ); r.v[i] = (u32)c; c >>= 32; }
-  /* now r < 2^255 + 19; r >= p  <=>  r + 19 >= 2^255 */
-  u32 t[8]; c = 19;
+  for( int i=0; i<10; i++ ) {
+    int s = FE_S(i), wi = s >> 5, sh = s & 31;
+    u32 lo = w[wi], hi = wi+1 < 8 ? w[wi+1] : 0u;
+    r.v[i] = __builtin_amdgcn_alignbit( hi, lo, (u32)sh ) & FE_M(i);
+  }
+}
+
+/* canonical value in [0,p) as 8 LE words; input limbs < 2^31 */
+FD_DEV void fe_pack( u32 w[ 8 ], fe const & a ) {
+  u32 h[10];
 #pragma unroll
-  for( int i=0; i<8; i++ ) { c += (u64)r.v[i]; t[i] = (u32)c; c >>= 32; }
-  u32 ge = t[7] >> 31;
+  for( int i=0; i<10; i++ ) h[i] = a.v[i];
 #pragma unroll
-  for( int i=0; i<8; i++ ) r.v[i] = ge ? t[i] : r.v[i];
-  r.v[7] &= ge ? 0x7fffffffu : 0xffffffffu;
+  for( int pass=0; pass<2; pass++ ) {
+#pragma unroll
+    for( int i=0; i<9; i++ ) { h[i+1] += h[i] >> FE_W(i); h[i] &= FE_M(i); }
+    h[0] += 19u * (h[9] >> 25); h[9] &= 0x1ffffffu;
+  }
+  /* now h < 2^255 + 2^26: subtract p iff h + 19 >= 2^255 */
+  u32 q = (h[0] + 19u) >> 26;
+#pragma unroll
+  for( int i=1; i<10; i++ ) q = (h[i] + q) >> FE_W(i);
+  h[0] += 19u * q;
+#pragma unroll
+  for( int i=0; i<9; i++ ) { h[i+1] += h[i] >> FE_W(i); h[i] &= FE_M(i); }
+  h[9] &= 0x1ffffffu;
+#pragma unroll
+  for( int k=0; k<8; k++ ) w[k] = 0u;
+#pragma unroll
+  for( int i=0; i<10; i++ ) {
+    int s = FE_S(i), wi = s >> 5, sh = s & 31;
+    w[wi] |= h[i] << sh;
+    if( sh + FE_W(i) > 32 && wi+1 < 8 ) w[wi+1] |= h[i] >> (32 - sh);
+  }
 }
 
 FD_DEV int fe_is_zero( fe const & a ) {
-  fe c; fe_canon( c, a );
+  u32 w[8]; fe_pack( w, a );
   u32 o = 0;
 #pragma unroll
-  for( int i=0; i<8; i++ ) o |= c.v[i];
+  for( int i=0; i<8; i++ ) o |= w[i];
   return o==0u;
 }
 
-FD_DEV int fe_eq( fe const & a, fe const & b ) { fe d; fe_sub( d, a, b ); return fe_is_zero( d ); }
+/* a == b (a, b L at most) */
+FD_DEV int fe_eq( fe const & a, fe const & b ) { fe d; fe_sub4( d, a, b ); return fe_is_zero( d ); }
+
+FD_DEV int fe_eq_words( fe const & a, u32 const w[ 8 ] ) {
+  u32 x[8]; fe_pack( x, a );
+  u32 o = 0;
+#pragma unroll
+  for( int i=0; i<8; i++ ) o |= x[i] ^ w[i];
+  return o==0u;
+}
 
 /* parity of the canonical value ("sign" of x, RFC 8032) */
-FD_DEV int fe_is_odd( fe const & a ) { fe c; fe_canon( c, a ); return (int)(c.v[0] & 1u); }
+FD_DEV int fe_is_odd( fe const & a ) { u32 w[8]; fe_pack( w, a ); return (int)(w[0] & 1u); }
 
 FD_DEV void fe_sel( fe & r, int c, fe const & a, fe const & b ) { /* r = c ? a : b */
 #pragma unroll
-  for( int i=0; i<8; i++ ) r.v[i] = c ? a.v[i] : b.v[i];
+  for( int i=0; i<10; i++ ) r.v[i] = c ? a.v[i] : b.v[i];
 }
+
+/* ---- exponentiations ------------------------------------------------------ */
 
 /* r = a^(2^252-3): the addition chain of fd_f25519_pow22523
    (src/ballet/ed25519/fd_f25519.c:10-59). */
@@ -252,8 +284,7 @@ FD_DEV void fe_pow22523( fe & r, fe const & a ) {
 }
 
 /* r = a^(p-2) = a^-1: the addition chain of fd_f25519_inv
-   (src/ballet/ed25519/fd_f25519.c:62-103).  Only used off the hot path
-   (base-table setup). */
+   (src/ballet/ed25519/fd_f25519.c:62-103).  Off the hot path. */
 FD_DEV void fe_invert( fe & r, fe const & z ) {
   fe t0, t1, t2, t3;
   fe_sqr ( t0, z );
@@ -271,49 +302,4 @@ FD_DEV void fe_invert( fe & r, fe const & z ) {
   fe_sqrn( t2, t2, 50 );  fe_mul( t1, t2, t1 );
   fe_sqrn( t1, t1, 5 );
   fe_mul ( r, t1, t0 );
-}
-
-/* Two independent pow22523 chains interleaved (decode of A and R at
-   once, the GPU analogue of FD_R43X6_POW22523_2_INL): the two chains give
-   the scheduler independent v_mad_u64_u32 streams to overlap. */
-FD_DEV void fe_sqrn2( fe & r, fe const & a, fe & s, fe const & b, int n ) {
-  fe_sqr( r, a ); fe_sqr( s, b );
-#pragma unroll 1
-  for( int i=1; i<n; i++ ) { fe_sqr( r, r ); fe_sqr( s, s ); }
-}
-
-FD_DEV void fe_pow22523_2( fe & r, fe const & a, fe & s, fe const & b ) {
-  fe t0, t1, t2, u0, u1, u2;
-  fe_sqr ( t0, a );              fe_sqr ( u0, b );
-  fe_sqrn2( t1, t0, u1, u0, 2 );
-  fe_mul ( t1, a, t1 );          fe_mul ( u1, b, u1 );
-  fe_mul ( t0, t0, t1 );         fe_mul ( u0, u0, u1 );
-  fe_sqr ( t0, t0 );             fe_sqr ( u0, u0 );
-  fe_mul ( t0, t1, t0 );         fe_mul ( u0, u1, u0 );
-  fe_sqrn2( t1, t0, u1, u0, 5 );
-  fe_mul ( t0, t1, t0 );         fe_mul ( u0, u1, u0 );
-  fe_sqrn2( t1, t0, u1, u0, 10 );
-  fe_mul ( t1, t1, t0 );         fe_mul ( u1, u1, u0 );
-  fe_sqrn2( t2, t1, u2, u1, 20 );
-  fe_mul ( t1, t2, t1 );         fe_mul ( u1, u2, u1 );
-  fe_sqrn2( t1, t1, u1, u1, 10 );
-  fe_mul ( t0, t1, t0 );         fe_mul ( u0, u1, u0 );
-  fe_sqrn2( t1, t0, u1, u0, 50 );
-  fe_mul ( t1, t1, t0 );         fe_mul ( u1, u1, u0 );
-  fe_sqrn2( t2, t1, u2, u1, 100 );
-  fe_mul ( t1, t2, t1 );         fe_mul ( u1, u2, u1 );
-  fe_sqrn2( t1, t1, u1, u1, 50 );
-  fe_mul ( t0, t1, t0 );         fe_mul ( u0, u1, u0 );
-  fe_sqrn2( t0, t0, u0, u0, 2 );
-  fe_mul ( r, t0, a );           fe_mul ( s, u0, b );
-}
-
-/* ---- byte <-> limb -------------------------------------------------- */
-
-/* limbs from 8 little-endian words, bit 255 dropped (non-canonical y >= p
-   accepted as in fd_f25519_frombytes / fiat curve25519_64.c:802) */
-FD_DEV void fe_from_words( fe & r, u32 const w[ 8 ] ) {
-#pragma unroll
-  for( int i=0; i<8; i++ ) r.v[i] = w[i];
-  r.v[7] &= 0x7fffffffu;
 }
