@@ -28,7 +28,7 @@ def build_engine(force: bool = False, extra: list[str] | None = None) -> str:
     out = os.path.join(PKG, "libfdgpu_ed25519.so")
     if force or extra or _stale(out, HIP_SRCS + HIP_DEPS):
         cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", "-Wno-unused-function", "-o", out] + (extra or []) + [os.path.join(CSRC, s) for s in HIP_SRCS]
+               "-Wall", "-Wno-unused-function", "-Wno-unused-value", "-Wno-unused-result", "-o", out] + (extra or []) + [os.path.join(CSRC, s) for s in HIP_SRCS]
         subprocess.run(cmd, check=True, cwd=CSRC)
     return out
 

@@ -105,88 +105,91 @@ fd_expand_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 *
   }
 }
 
-/* Stage 1 -- checks and decompression (fd_ed25519_user.c:174-199).
-   Writes the per-signature code (0 = still pending) and, for pending
-   signatures, the canonical affine R and A to scratch. */
+/* Stage 1 -- point decompression, two lanes per signature (lane 2s
+   decodes the public key A, lane 2s+1 the signature's R): one pow22523
+   chain per lane keeps the kernel at 3 waves/SIMD and doubles the
+   parallelism.  Per point: status byte rc | small_order<<2 (rc: 0 ok,
+   1 not a square, 2 x==0 with sign set), 0xff if the transaction is
+   malformed; the canonical affine point goes to Axy / Rxy. */
 __global__ void __launch_bounds__( FD_WG )
 fd_decode_kernel( unsigned char const *    __restrict__ payload,
                   fdgpu_txn_desc_t const * __restrict__ desc,
                   u32 const *              __restrict__ map,
                   u32                                   nsig,
-                  int                                   semantics,
-                  i8 *                     __restrict__ code_out,
+                  unsigned char *          __restrict__ pstat,
                   uint4 *                  __restrict__ Rxy,
                   uint4 *                  __restrict__ Axy ) {
-  u32 s = blockIdx.x * FD_WG + threadIdx.x;
-  if( s >= nsig ) return;
+  u32 p = blockIdx.x * FD_WG + threadIdx.x;
+  if( p >= 2u*nsig ) return;
+  u32 s = p >> 1, is_r = p & 1u;
   u32 m = map[s];
   u32 t = m & 0xffffffu, j = m >> 24;
   fdgpu_txn_desc_t d = desc[t];
-
-  /* transaction sanity (batch size and bounds): ERR_SIG, like
-     fd_ed25519_verify_batch_single_msg's batch_sz check (fd_ed25519_user.c:238-241) */
+  /* transaction sanity (batch size and bounds) -> ERR_SIG for all its
+     signatures, like the batch_sz check of fd_ed25519_user.c:238-241 */
   u32 cnt = d.sig_cnt;
   if( cnt==0u || cnt>16u
       || (u32)d.signature_off + 64u*cnt > (u32)d.payload_sz
       || (u32)d.acct_addr_off + 32u*cnt > (u32)d.payload_sz
       || (u32)d.message_off > (u32)d.payload_sz ) {
-    code_out[s] = FD_ED25519_ERR_SIG;
+    pstat[p] = 0xffu;
     return;
   }
-
   unsigned char const * base = payload + d.payload_off;
-  u32 Rw[8], Sw[8], Aw[8];
-  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
-  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
-  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
-
-  int code = FD_ED25519_SUCCESS;
-  /* 1. S canonical (fd_ed25519_user.c:174-176) */
-  if( !sc_is_canonical( Sw ) ) code = FD_ED25519_ERR_SIG;
-
-  /* 2. decode A and R (fd_ed25519_user.c:179-193) */
-  ge_p3 A, R; int ra, rb;
-  ge_decode1( A, ra, Aw );
-  ge_decode1( R, rb, Rw );
-  if( code==FD_ED25519_SUCCESS ) {
-    if( semantics==FDGPU_SEMANTICS_AVX512 ) {
-      if( ra | rb ) code = FD_ED25519_ERR_SIG;
-    } else {
-      if( ra==1 ) code = FD_ED25519_ERR_PUBKEY;
-      else if( rb==1 ) code = FD_ED25519_ERR_SIG;
-    }
-  }
-  /* 3. small order (fd_ed25519_user.c:194-199) */
-  if( code==FD_ED25519_SUCCESS ) {
-    if( ge_affine_is_small_order( A ) ) code = FD_ED25519_ERR_PUBKEY;
-    else if( ge_affine_is_small_order( R ) ) code = FD_ED25519_ERR_SIG;
-  }
-  code_out[s] = (i8)code;
-  if( code!=FD_ED25519_SUCCESS ) return;
-  fe_store_packed( Rxy + (size_t)s*4 + 0, R.X );
-  fe_store_packed( Rxy + (size_t)s*4 + 2, R.Y );
-  fe_store_packed( Axy + (size_t)s*4 + 0, A.X );
-  fe_store_packed( Axy + (size_t)s*4 + 2, A.Y );
+  u32 w[8];
+  fd_load_words<8>( w, base + ( is_r ? (u32)d.signature_off + 64u*j : (u32)d.acct_addr_off + 32u*j ) );
+  ge_p3 P; int rc;
+  ge_decode1( P, rc, w );
+  int so = ge_affine_is_small_order( P );
+  pstat[p] = (unsigned char)( rc | (so << 2) );
+  u32 x[8], y[8];
+  fe_pack( x, P.X ); fe_pack( y, P.Y );
+  uint4 * o = ( is_r ? Rxy : Axy ) + (size_t)s*4;
+  o[0] = make_uint4( x[0], x[1], x[2], x[3] ); o[1] = make_uint4( x[4], x[5], x[6], x[7] );
+  o[2] = make_uint4( y[0], y[1], y[2], y[3] ); o[3] = make_uint4( y[4], y[5], y[6], y[7] );
 }
 
-/* Stage 2 -- k = SHA-512(R||A||M) mod l (fd_ed25519_user.c:204-206) and
-   the signed digits of k (radix 16) and S (radix 256). */
+/* Stage 2 -- the result-code procedure of fd_ed25519_verify
+   (fd_ed25519_user.c:174-199) from S and the two point
+   statuses, then for pending signatures k = SHA-512(R||A||M) mod l
+   (:204-206) and the signed digits of k (radix 16) and S (radix 256). */
 __global__ void __launch_bounds__( FD_WG )
 fd_hash_kernel( unsigned char const *    __restrict__ payload,
                 fdgpu_txn_desc_t const * __restrict__ desc,
                 u32 const *              __restrict__ map,
                 u32                                   nsig,
-                i8 const *               __restrict__ code,
+                int                                   semantics,
+                unsigned char const *    __restrict__ pstat,
+                i8 *                     __restrict__ code_out,
                 i8 *                     __restrict__ digA,
                 i8 *                     __restrict__ digB ) {
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
-  if( code[s] != FD_ED25519_SUCCESS ) return;
   size_t n = nsig;
+  u32 pa = pstat[2*s], pr = pstat[2*s+1];
+  if( pa==0xffu ) { code_out[s] = FD_ED25519_ERR_SIG; return; }
   u32 m = map[s];
   u32 t = m & 0xffffffu, j = m >> 24;
   fdgpu_txn_desc_t d = desc[t];
   unsigned char const * base = payload + d.payload_off;
+  u32 Sw[8];
+  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
+  int ra = (int)(pa & 3u), rb = (int)(pr & 3u);
+  int code = FD_ED25519_SUCCESS;
+  if( !sc_is_canonical( Sw ) ) code = FD_ED25519_ERR_SIG;                /* S < l */
+  else if( semantics==FDGPU_SEMANTICS_AVX512 ) {
+    if( ra | rb ) code = FD_ED25519_ERR_SIG;                              /* decode (AVX-512) */
+  } else {
+    if( ra==1 ) code = FD_ED25519_ERR_PUBKEY;                             /* decode (portable) */
+    else if( rb==1 ) code = FD_ED25519_ERR_SIG;
+  }
+  if( code==FD_ED25519_SUCCESS ) {
+    if( pa & 4u ) code = FD_ED25519_ERR_PUBKEY;                           /* small-order A */
+    else if( pr & 4u ) code = FD_ED25519_ERR_SIG;                         /* small-order R */
+  }
+  code_out[s] = (i8)code;
+  if( code != FD_ED25519_SUCCESS ) return;
+
   u32 Rw[8], Aw[8];
   fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
   fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
@@ -200,8 +203,6 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
     carry = (v + 8) >> 4;
     digA[(size_t)i*n + s] = (i8)(v - (carry << 4));
   }
-  u32 Sw[8];
-  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
   carry = 0;
 #pragma unroll
   for( int i=0; i<32; i++ ) {
@@ -214,7 +215,7 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
 /* Stage 3 -- table [0..8](-A) in cached form (fd_ed25519_point_neg + the
    odd-multiple table of fd_curve25519.c:118-131; here all multiples, for a
    signed fixed window). */
-__global__ void __launch_bounds__( FD_WG )
+__global__ void __launch_bounds__( FD_WG, 3 )
 fd_table_kernel( u32 nsig, i8 const * __restrict__ code, uint4 const * __restrict__ Axy,
                  uint4 * __restrict__ tab ) {
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
@@ -384,6 +385,7 @@ struct fdgpu_ed25519_ctx {
   /* scratch */
   u32 *   d_map;
   i8 *    d_code;
+  unsigned char * d_pstat;
   uint4 * d_tab;
   uint4 * d_Rxy;
   uint4 * d_Axy;
@@ -416,10 +418,11 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
   if( nsig ) {
     hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig );
     if( ctx->timing ) hipEventRecord( ev[0], st );
-    hipLaunchKernelGGL( fd_decode_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
-                        ctx->semantics, code, ctx->d_Rxy, ctx->d_Axy );
+    unsigned pg = (unsigned)( (2UL*sig_cnt + FD_WG - 1) / FD_WG );
+    hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+                        ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy );
     hipLaunchKernelGGL( fd_hash_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
-                        code, ctx->d_digA, ctx->d_digB );
+                        ctx->semantics, ctx->d_pstat, code, ctx->d_digA, ctx->d_digB );
     hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_Axy, ctx->d_tab );
     if( ctx->timing ) hipEventRecord( ev[1], st );
     hipLaunchKernelGGL( fd_dsm_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
@@ -445,6 +448,7 @@ fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
   HIPCHK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ), NULL );
   HIPCHK( hipMalloc( &ctx->d_map,  ns * sizeof(u32) ), NULL );
   HIPCHK( hipMalloc( &ctx->d_code, ns ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_pstat, 2*ns ), NULL );
   HIPCHK( hipMalloc( &ctx->d_tab,  ns * FD_ATAB_ENTRIES * 8 * sizeof(uint4) ), NULL );
   HIPCHK( hipMalloc( &ctx->d_Rxy,  ns * 4 * sizeof(uint4) ), NULL );
   HIPCHK( hipMalloc( &ctx->d_Axy,  ns * 4 * sizeof(uint4) ), NULL );
@@ -481,7 +485,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   if( !ctx ) return;
   hipSetDevice( ctx->device );
   hipStreamSynchronize( ctx->stream );
-  hipFree( ctx->d_map ); hipFree( ctx->d_code ); hipFree( ctx->d_tab ); hipFree( ctx->d_Rxy ); hipFree( ctx->d_Axy );
+  hipFree( ctx->d_map ); hipFree( ctx->d_code ); hipFree( ctx->d_pstat ); hipFree( ctx->d_tab ); hipFree( ctx->d_Rxy ); hipFree( ctx->d_Axy );
   hipFree( ctx->d_digA ); hipFree( ctx->d_digB ); hipFree( ctx->d_btab );
   for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ev[i] );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ring[r][i] );

@@ -41,6 +41,14 @@ struct fe { u32 v[10]; };
 
 FD_DEV u64 fd_mad( u32 a, u32 b, u64 c ) { return (u64)a * (u64)b + c; }
 
+/* Scheduling fence after each multiply/square: keeps the machine
+   scheduler from hoisting the next operation's operand preparation into
+   this one's carry chain, which otherwise inflates register pressure
+   several-fold on long dependent chains (pow22523: 256 -> ~110 VGPRs). */
+#ifndef FD_SCHED_FENCE
+#define FD_SCHED_FENCE() __builtin_amdgcn_sched_barrier( 0 )
+#endif
+
 #define FE_W(i)    ( ((i) & 1) ? 25 : 26 )
 #define FE_M(i)    ( ((i) & 1) ? 0x1ffffffu : 0x3ffffffu )
 #define FE_S(i)    ( (51*(i)+1) / 2 )            /* ceil(25.5 i) */
@@ -130,7 +138,7 @@ FD_DEV void fe_carry64( fe & r, u64 h[ 10 ] ) {
 FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
   u32 g19[10], f2[10];
 #pragma unroll
-  for( int i=0; i<10; i++ ) { g19[i] = 19u * g.v[i]; f2[i] = 2u * f.v[i]; }
+  for( int i=0; i<10; i++ ) { g19[i] = 19u * g.v[i]; f2[i] = 2u * f.v[i]; asm( "" : "+v"(g19[i]), "+v"(f2[i]) ); }
   u64 h[10];
 #pragma unroll
   for( int k=0; k<10; k++ ) {
@@ -146,6 +154,7 @@ FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
     h[k] = acc;
   }
   fe_carry64( r, h );
+  FD_SCHED_FENCE();
 }
 
 /* r = f^2; f L -> r T.  55 products: pair (i<j) weight 2, both odd x2,
@@ -153,7 +162,7 @@ FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
 FD_DEV void fe_sqr( fe & r, fe const & f ) {
   u32 f2[10], f4[10], f19[10];
 #pragma unroll
-  for( int i=0; i<10; i++ ) { f2[i] = 2u * f.v[i]; f4[i] = 4u * f.v[i]; f19[i] = 19u * f.v[i]; }
+  for( int i=0; i<10; i++ ) { f2[i] = 2u * f.v[i]; f4[i] = 4u * f.v[i]; f19[i] = 19u * f.v[i]; asm( "" : "+v"(f2[i]), "+v"(f4[i]), "+v"(f19[i]) ); }
   u64 h[10];
 #pragma unroll
   for( int k=0; k<10; k++ ) {
@@ -175,6 +184,7 @@ FD_DEV void fe_sqr( fe & r, fe const & f ) {
     h[k] = acc;
   }
   fe_carry64( r, h );
+  FD_SCHED_FENCE();
 }
 
 /* r = a^(2^n) */

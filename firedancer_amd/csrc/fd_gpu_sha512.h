@@ -36,7 +36,17 @@ __constant__ u64 fd_gpu_sha512_k[ 80 ] = {
   0x4cc5d4becb3e42b6UL, 0x597f299cfc657e2aUL, 0x5fcb6fab3ad6faecUL, 0x6c44198c4a475817UL
 };
 
-FD_DEV u64 fd_rotr64( u64 x, int n ) { return (x >> n) | (x << (64 - n)); }
+/* 64-bit rotate / shift as two v_alignbit_b32 on the VGPR halves */
+FD_DEV u64 fd_mk64( u32 lo, u32 hi ) { return ((u64)hi << 32) | (u64)lo; }
+FD_DEV u64 fd_rotr64( u64 x, int n ) {
+  u32 lo = (u32)x, hi = (u32)(x >> 32);
+  if( n >= 32 ) { u32 t = lo; lo = hi; hi = t; n -= 32; }
+  return fd_mk64( __builtin_amdgcn_alignbit( hi, lo, (u32)n ), __builtin_amdgcn_alignbit( lo, hi, (u32)n ) );
+}
+FD_DEV u64 fd_shr64( u64 x, int n ) {   /* n < 32 */
+  u32 lo = (u32)x, hi = (u32)(x >> 32);
+  return fd_mk64( __builtin_amdgcn_alignbit( hi, lo, (u32)n ), hi >> n );
+}
 FD_DEV u32 fd_bswap32( u32 x ) { return __builtin_bswap32( x ); }
 
 /* Load n32 consecutive little-endian 32-bit words starting at an
@@ -54,22 +64,39 @@ FD_DEV void fd_load_words( u32 w[ N32 ], unsigned char const * p ) {
   for( int i=0; i<N32; i++ ) w[i] = __builtin_amdgcn_alignbyte( d[i+1], d[i], sh );
 }
 
+/* One 128-byte block.  A rolled loop over 5 groups of 16 unrolled rounds:
+   the message schedule index is static inside a group (w[] stays in 32
+   VGPRs) and the group's 16 round constants come from scalar loads, so
+   neither the 80 constants nor the whole expanded schedule are ever live
+   at once (a fully unrolled block needed ~200 VGPRs). */
+#define FD_SHA512_ROUND( kt, wt ) do {                                              \
+    u64 S1 = fd_rotr64( e,14 ) ^ fd_rotr64( e,18 ) ^ fd_rotr64( e,41 );           \
+    u64 ch = g ^ ( e & ( f ^ g ) );                                                 \
+    u64 t1 = hh + S1 + ch + (kt) + (wt);                                            \
+    u64 S0 = fd_rotr64( a,28 ) ^ fd_rotr64( a,34 ) ^ fd_rotr64( a,39 );           \
+    u64 mj = ( a & b ) | ( c & ( a | b ) );                                         \
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;      \
+  } while(0)
+
 FD_DEV void fd_sha512_block( u64 h[ 8 ], u64 w[ 16 ] ) {
   u64 a=h[0], b=h[1], c=h[2], d=h[3], e=h[4], f=h[5], g=h[6], hh=h[7];
 #pragma unroll
-  for( int t=0; t<80; t++ ) {
-    if( t>=16 ) {
-      u64 w15 = w[(t-15)&15], w2 = w[(t-2)&15];
-      u64 s0 = fd_rotr64( w15, 1 ) ^ fd_rotr64( w15, 8 ) ^ (w15 >> 7);
-      u64 s1 = fd_rotr64( w2, 19 ) ^ fd_rotr64( w2, 61 ) ^ (w2 >> 6);
-      w[t&15] += s0 + w[(t-7)&15] + s1;
+  for( int r=0; r<16; r++ ) {
+    FD_SHA512_ROUND( fd_gpu_sha512_k[r], w[r] );
+    if( (r & 3)==3 ) __builtin_amdgcn_sched_barrier( 0 );
+  }
+#pragma unroll 1
+  for( int grp=1; grp<5; grp++ ) {
+    u64 const * kg = fd_gpu_sha512_k + 16*grp;
+#pragma unroll
+    for( int r=0; r<16; r++ ) {
+      u64 w15 = w[(r+1)&15], w2 = w[(r+14)&15];
+      u64 s0 = fd_rotr64( w15, 1 ) ^ fd_rotr64( w15, 8 ) ^ fd_shr64( w15, 7 );
+      u64 s1 = fd_rotr64( w2, 19 ) ^ fd_rotr64( w2, 61 ) ^ fd_shr64( w2, 6 );
+      w[r] += s0 + w[(r+9)&15] + s1;
+      FD_SHA512_ROUND( kg[r], w[r] );
+      if( (r & 3)==3 ) __builtin_amdgcn_sched_barrier( 0 );
     }
-    u64 S1 = fd_rotr64( e,14 ) ^ fd_rotr64( e,18 ) ^ fd_rotr64( e,41 );
-    u64 ch = (e & f) ^ (~e & g);
-    u64 t1 = hh + S1 + ch + fd_gpu_sha512_k[t] + w[t&15];
-    u64 S0 = fd_rotr64( a,28 ) ^ fd_rotr64( a,34 ) ^ fd_rotr64( a,39 );
-    u64 mj = (a & b) ^ (a & c) ^ (b & c);
-    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }
   h[0]+=a; h[1]+=b; h[2]+=c; h[3]+=d; h[4]+=e; h[5]+=f; h[6]+=g; h[7]+=hh;
 }

@@ -19,7 +19,7 @@ import threading
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libfdgpu_ed25519.so")
+LIB_PATH = os.environ.get("FDGPU_LIB") or os.path.join(PKG_DIR, "libfdgpu_ed25519.so")
 
 FD_ED25519_SUCCESS = 0
 FD_ED25519_ERR_SIG = -1
