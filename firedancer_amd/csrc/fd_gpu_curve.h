@@ -23,29 +23,31 @@ struct ge_precomp{ fe ypx, ymx, xy2d; };/* affine, Z = 1                 */
 
 FD_DEV void ge_p3_identity( ge_p3 & p ) { p.X = fe_zero(); p.Y = fe_one(); p.Z = fe_one(); p.T = fe_zero(); }
 
+/* The completed -> projective/extended conversions share the 19x
+   multiples of the operand used twice (T, and Y for p3). */
 FD_DEV void ge_p1p1_to_p2( ge_p2 & r, ge_p1p1 const & p ) {
-  fe_mul( r.X, p.X, p.T ); fe_mul( r.Y, p.Y, p.Z ); fe_mul( r.Z, p.Z, p.T );
+  fe19 t19; fe_x19( t19, p.T );
+  fe_mul19( r.X, p.X, p.T, t19 ); fe_mul( r.Y, p.Y, p.Z ); fe_mul19( r.Z, p.Z, p.T, t19 );
 }
 FD_DEV void ge_p1p1_to_p3( ge_p3 & r, ge_p1p1 const & p ) {
-  fe_mul( r.X, p.X, p.T ); fe_mul( r.Y, p.Y, p.Z ); fe_mul( r.Z, p.Z, p.T ); fe_mul( r.T, p.X, p.Y );
+  fe19 t19; fe_x19( t19, p.T );
+  fe_mul19( r.X, p.X, p.T, t19 ); fe_mul19( r.Z, p.Z, p.T, t19 );
+  fe19 y19; fe_x19( y19, p.Y );
+  fe_mul19( r.Y, p.Z, p.Y, y19 ); fe_mul19( r.T, p.X, p.Y, y19 );
 }
 
 /* 2P for a=-1 twisted Edwards from (X:Y:Z) T -- eprint 2008/522 §4.4:
-   4 squarings.  Out: X=E (T), Y=H (L), Z=G (L), T=F (T). */
+   4 squarings.  Out: X=E (T), Y=H (L), Z=G (L), T=F (T).  E = (X+Y)^2-H
+   and F = 2Z^2-G are folded into their squarings' carry chains. */
 FD_DEV void ge_dbl( ge_p1p1 & r, ge_p2 const & p ) {
-  fe xx, yy, zz, s;
+  fe xx, yy, s;
   fe_sqr( xx, p.X );                  /* XX (T)               */
   fe_sqr( yy, p.Y );                  /* YY (T)               */
-  fe_sqr( zz, p.Z );                  /* ZZ (T)               */
-  fe_add( s, p.X, p.Y );              /* X+Y (L)              */
-  fe_sqr( s, s );                     /* (X+Y)^2 (T)          */
   fe_add( r.Y, yy, xx );              /* H = YY+XX (L)        */
   fe_sub( r.Z, yy, xx );              /* G = YY-XX (L)        */
-  fe_sub4( r.X, s, r.Y );             /* E = (X+Y)^2-H = 2XY  */
-  fe_wcarry( r.X, r.X );
-  fe_add( zz, zz, zz );               /* 2ZZ (L)              */
-  fe_sub4( r.T, zz, r.Z );            /* F = 2ZZ-G            */
-  fe_wcarry( r.T, r.T );
+  fe_add( s, p.X, p.Y );              /* X+Y (L)              */
+  fe_sqr_sub( r.X, s, r.Y );          /* E = (X+Y)^2-H = 2XY  */
+  fe_sqr2_sub( r.T, p.Z, r.Z );       /* F = 2ZZ-G            */
 }
 
 /* P + Q, P T, Q cached (already negated by the caller if needed)

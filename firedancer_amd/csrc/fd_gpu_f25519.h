@@ -132,13 +132,29 @@ FD_DEV void fe_carry64( fe & r, u64 h[ 10 ] ) {
 
 /* ---- multiply / square ------------------------------------------------- */
 
-/* r = f * g; f, g L -> r T.  Column k sums f_i g_j over i+j == k (mod 10);
-   weight 2 when i and j are both odd (ceil(25.5i)+ceil(25.5j) =
-   ceil(25.5(i+j)) + 1), weight 19 when i+j >= 10 (2^255 = 19). */
-FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
-  u32 g19[10], f2[10];
+/* Operand multiples are formed only for the limbs that use them, each
+   behind an empty asm so the compiler keeps one register per multiple
+   instead of re-deriving it at every use (VALU-issue bound: every
+   instruction counts). */
+#define FD_KEEP( x ) asm( "" : "+v"( x ) )
+
+/* 19 g_j for j = 1..9 (the wrapped columns of a product with g) */
+struct fe19 { u32 v[10]; };
+FD_DEV void fe_x19( fe19 & r, fe const & g ) {
+  r.v[0] = 0u;
 #pragma unroll
-  for( int i=0; i<10; i++ ) { g19[i] = 19u * g.v[i]; f2[i] = 2u * f.v[i]; asm( "" : "+v"(g19[i]), "+v"(f2[i]) ); }
+  for( int j=1; j<10; j++ ) { r.v[j] = 19u * g.v[j]; FD_KEEP( r.v[j] ); }
+}
+
+/* r = f * g with g19 = fe_x19( g ) precomputed (shared by several
+   products with the same g); f, g L -> r T.  Column k sums f_i g_j over
+   i+j == k (mod 10); weight 2 when i and j are both odd
+   (ceil(25.5i)+ceil(25.5j) = ceil(25.5(i+j)) + 1), weight 19 when
+   i+j >= 10 (2^255 = 19).  100 v_mad_u64_u32 + 5 doublings. */
+FD_DEV void fe_mul19( fe & r, fe const & f, fe const & g, fe19 const & g19 ) {
+  u32 f2[10];
+#pragma unroll
+  for( int i=0; i<10; i++ ) { f2[i] = f.v[i]; if( i & 1 ) { f2[i] = 2u * f.v[i]; FD_KEEP( f2[i] ); } }
   u64 h[10];
 #pragma unroll
   for( int k=0; k<10; k++ ) {
@@ -148,7 +164,7 @@ FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
       int j = k - i, wrap = j < 0;
       if( wrap ) j += 10;
       u32 a = ( (i & 1) && (j & 1) ) ? f2[i] : f.v[i];
-      u32 b = wrap ? g19[j] : g.v[j];
+      u32 b = wrap ? g19.v[j] : g.v[j];
       acc = fd_mad( a, b, acc );
     }
     h[k] = acc;
@@ -157,13 +173,25 @@ FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
   FD_SCHED_FENCE();
 }
 
-/* r = f^2; f L -> r T.  55 products: pair (i<j) weight 2, both odd x2,
-   wrap x19; operands 2f/4f (<2^28.6) and 19f (<2^31.9). */
-FD_DEV void fe_sqr( fe & r, fe const & f ) {
-  u32 f2[10], f4[10], f19[10];
+FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
+  fe19 g19; fe_x19( g19, g );
+  fe_mul19( r, f, g, g19 );
+}
+
+/* r = f^2; f L -> r T.  55 products; coefficient c = (i<j ? 2 : 1) x
+   (i, j both odd ? 2 : 1) x (i+j >= 10 ? 19 : 1) is carried by the
+   operands f, 2f (i<=8), 38f (odd j>=5) and 19f (even j>=6) -- 14
+   multiples.  Largest operand 38f_odd < 2^31.9 (L input). */
+FD_DEV void fe_sqr_cols( u64 h[ 10 ], fe const & f ) {
+  u32 f2[10], fw[10];
 #pragma unroll
-  for( int i=0; i<10; i++ ) { f2[i] = 2u * f.v[i]; f4[i] = 4u * f.v[i]; f19[i] = 19u * f.v[i]; asm( "" : "+v"(f2[i]), "+v"(f4[i]), "+v"(f19[i]) ); }
-  u64 h[10];
+  for( int i=0; i<9; i++ ) { f2[i] = 2u * f.v[i]; FD_KEEP( f2[i] ); }
+  f2[9] = 0u;
+#pragma unroll
+  for( int j=0; j<10; j++ ) {
+    fw[j] = 0u;
+    if( j >= 5 ) { fw[j] = ( (j & 1) ? 38u : 19u ) * f.v[j]; FD_KEEP( fw[j] ); }
+  }
 #pragma unroll
   for( int k=0; k<10; k++ ) {
     u64 acc = 0;
@@ -175,14 +203,54 @@ FD_DEV void fe_sqr( fe & r, fe const & f ) {
         int odd2 = (i & 1) && (j & 1);
         int pair = i < j;
         int wrap = i + j >= 10;
-        int m = (pair ? 2 : 1) * (odd2 ? 2 : 1);   /* 1, 2 or 4 */
-        u32 a = m==1 ? f.v[i] : ( m==2 ? f2[i] : f4[i] );
-        u32 b = wrap ? f19[j] : f.v[j];
+        u32 a, b;
+        if( !wrap ) {
+          int c = (pair ? 2 : 1) * (odd2 ? 2 : 1);
+          a = c==1 ? f.v[i] : f2[i];
+          b = c==4 ? f2[j]  : f.v[j];
+        } else if( j & 1 ) {                 /* b = 38 f_j: c/38 = 1/2 (i==j), 1, 2 */
+          int c2 = (pair ? 2 : 1) * (odd2 ? 2 : 1);   /* c / 19 */
+          a = c2==4 ? f2[i] : f.v[i];
+          b = fw[j];
+        } else {                             /* even j: b = 19 f_j, c/19 = 1 (i==j) or 2 */
+          a = pair ? f2[i] : f.v[i];
+          b = fw[j];
+        }
         acc = fd_mad( a, b, acc );
       }
     }
     h[k] = acc;
   }
+}
+
+FD_DEV void fe_sqr( fe & r, fe const & f ) {
+  u64 h[10];
+  fe_sqr_cols( h, f );
+  fe_carry64( r, h );
+  FD_SCHED_FENCE();
+}
+
+/* 4p limbs: a bias larger than any L limb, for subtractions folded into
+   the column sums of a square before its carry chain */
+#define FE_4P(i) ( (i)==0 ? 0xfffffb4u : ( ((i) & 1) ? 0x7fffffcu : 0xffffffcu ) )
+
+/* r = f^2 + 4p - b (b L) -> T: the subtraction rides on the squaring's
+   carry chain instead of a separate biased sub + fe_wcarry */
+FD_DEV void fe_sqr_sub( fe & r, fe const & f, fe const & b ) {
+  u64 h[10];
+  fe_sqr_cols( h, f );
+#pragma unroll
+  for( int i=0; i<10; i++ ) h[i] += (u64)( FE_4P(i) - b.v[i] );
+  fe_carry64( r, h );
+  FD_SCHED_FENCE();
+}
+
+/* r = 2 f^2 + 4p - b (b L) -> T */
+FD_DEV void fe_sqr2_sub( fe & r, fe const & f, fe const & b ) {
+  u64 h[10];
+  fe_sqr_cols( h, f );
+#pragma unroll
+  for( int i=0; i<10; i++ ) h[i] = ( h[i] << 1 ) + (u64)( FE_4P(i) - b.v[i] );
   fe_carry64( r, h );
   FD_SCHED_FENCE();
 }

@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench (full), rocprof kernel stats,
+# then separate PMC passes on the bench (one counter group per pass).
+# usage (from the container): gpurun --timeout 1100 -- 'bash tools/gpu_round.sh [tag]'
+tag="${1:-run}"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-batch 0"
+P="timeout -s KILL 90 rocprofv3 --kernel-include-regex fd_ -f csv"
+exec_specs=(
+  "tests:420:python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread"
+  "smoke:120:python -u -c 'import __graft_entry__ as g; g.smoke()'"
+  "bench:300:python -u bench.py > gpurun_out/bench_${tag}.json"
+  "stats:180:rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_${tag}/stats -o run -- $B"
+  "pmc_fetch:120:$P --pmc FETCH_SIZE -d gpurun_out/prof_${tag}/fetch -o run -- $B"
+  "pmc_write:120:$P --pmc WRITE_SIZE -d gpurun_out/prof_${tag}/write -o run -- $B"
+  "pmc_sq:120:$P --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/prof_${tag}/sq -o run -- $B"
+)
+bash "$(dirname "$0")/gpu_job.sh" "${exec_specs[@]}"

@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Summarise a tools/gpu_round.sh profile directory (rocprofv3 csv) into
+per-kernel, per-launch numbers and write profiles/<round>/pmc_summary.json
+(+ profiles/dsm_pmc.json, which bench.py reads for roofline.traffic).
+
+Corrections (MI355X_MICROARCH.md, HBM section):
+  * FETCH_SIZE / WRITE_SIZE are reported in KiB.
+  * gfx950 FETCH_SIZE counts 128-B requests as 64 B for wide streaming
+    reads: hbm_read_bytes = 2 x FETCH_SIZE x 1024 (an upper estimate for
+    the DSM's 16-B-per-lane gathers, which are not calibrated).
+  * GRBM_GUI_ACTIVE is summed over the 8 XCDs; VALU busy =
+    SQ_ACTIVE_INST_VALU x 4 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8).
+usage: tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<round>/<tag>
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+os.makedirs(dst, exist_ok=True)
+per = collections.defaultdict(lambda: collections.defaultdict(list))
+for p in ("fetch", "write", "sq"):
+    f = os.path.join(src, p, "run_counter_collection.csv")
+    if not os.path.exists(f):
+        continue
+    for r in csv.DictReader(open(f)):
+        per[r["Kernel_Name"].split("(")[0]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+out = {}
+for k, c in per.items():
+    m = {n: sum(v) / len(v) for n, v in c.items()}
+    e = {"launches_sampled": max(len(v) for v in c.values()), "counters_mean_per_launch": m}
+    if "FETCH_SIZE" in m:
+        e["hbm_read_bytes"] = 2 * m["FETCH_SIZE"] * 1024
+    if "WRITE_SIZE" in m:
+        e["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
+    if "SQ_ACTIVE_INST_VALU" in m and m.get("GRBM_GUI_ACTIVE"):
+        e["valu_busy"] = m["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * m["GRBM_GUI_ACTIVE"] / 8)
+    if "SQ_INSTS_VALU" in m and m.get("SQ_WAVES"):
+        e["valu_insts_per_wave"] = m["SQ_INSTS_VALU"] / m["SQ_WAVES"]
+    out[k] = e
+json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1, sort_keys=True)
+stats = os.path.join(src, "stats", "run_kernel_stats.csv")
+if os.path.exists(stats):
+    shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+d = out.get("fd_dsm_kernel")
+if d and "hbm_read_bytes" in d:
+    json.dump({"kernel": "fd_dsm_kernel", "source": dst,
+               "hbm_bytes_per_launch": d["hbm_read_bytes"] + d.get("hbm_write_bytes", 0),
+               "valu_busy": d.get("valu_busy"), "valu_insts_per_wave": d.get("valu_insts_per_wave")},
+              open(os.path.join(os.path.dirname(dst.rstrip("/")), "..", "dsm_pmc.json"), "w"), indent=1)
+for k, e in sorted(out.items()):
+    print(k, {x: (round(y, 3) if isinstance(y, float) else y) for x, y in e.items() if x != "counters_mean_per_launch"})
