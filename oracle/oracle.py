@@ -60,6 +60,10 @@ class Oracle:
         L.oracle_ed25519_public_from_private.argtypes = [_u8p, _u8p]
         L.oracle_ed25519_sign.argtypes = [_u8p, _u8p, ctypes.c_size_t, _u8p, _u8p]
         L.oracle_dsm_encode.argtypes = [_u8p, _u8p, _u8p, _u8p]
+        L.oracle_txn_parse.restype = ctypes.c_uint32
+        L.oracle_txn_parse.argtypes = [_u8p, ctypes.c_uint32, _u8p]
+        L.oracle_txn_parse_batch.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, _u8p,
+                                             ctypes.c_uint64, ctypes.c_void_p]
 
     @staticmethod
     def _b(x: bytes) -> np.ndarray:
@@ -109,10 +113,52 @@ class Oracle:
         self.lib.oracle_ed25519_sign(_ptr(out), _ptr(self._b(msg)), len(msg), _ptr(self._b(pub)), _ptr(self._b(prv)))
         return out.tobytes()
 
+    def txn_parse(self, payload: bytes):
+        """fd_txn_parse restated: (footprint, fd_txn_t image bytes) -- footprint 0 = rejected."""
+        out = np.zeros(1024, np.uint8)
+        fp = self.lib.oracle_txn_parse(_ptr(self._b(payload)), len(payload), _ptr(out))
+        return fp, out[:fp].tobytes()
+
+    def txn_parse_batch(self, arena: np.ndarray, off: np.ndarray, sz: np.ndarray, stride: int = 864):
+        return _parse_batch(self.lib.oracle_txn_parse_batch, arena, off, sz, stride)
+
     def dsm_encode(self, k: bytes, A: bytes, S: bytes):
         out = np.zeros(32, np.uint8)
         rc = self.lib.oracle_dsm_encode(_ptr(out), _ptr(self._b(k)), _ptr(self._b(A)), _ptr(self._b(S)))
         return rc, out.tobytes()
+
+
+def _parse_batch(fn, arena, off, sz, stride):
+    arena = np.ascontiguousarray(arena, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    sz = np.ascontiguousarray(sz, np.uint16)
+    n = len(off)
+    out = np.zeros((n, stride), np.uint8)
+    fp = np.zeros(n, np.uint16)
+    fn(_ptr(arena), off.ctypes.data, sz.ctypes.data, n, _ptr(out), stride, fp.ctypes.data)
+    return fp, out
+
+
+class RefTxn:
+    """The reference's fd_txn_parse compiled from its own source (oracle/_ref/libfdref_txn.so)."""
+
+    def __init__(self):
+        path = os.path.join(HERE, "_ref", "libfdref_txn.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.lib = L = ctypes.CDLL(path)
+        L.ref_txn_parse.restype = ctypes.c_ulong
+        L.ref_txn_parse.argtypes = [_u8p, ctypes.c_ulong, _u8p]
+        L.ref_txn_parse_batch.argtypes = [_u8p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, _u8p,
+                                          ctypes.c_ulong, ctypes.c_void_p]
+
+    def txn_parse(self, payload: bytes):
+        out = np.zeros(1024, np.uint8)
+        fp = self.lib.ref_txn_parse(_ptr(Oracle._b(payload)), len(payload), _ptr(out))
+        return fp, out[:fp].tobytes()
+
+    def txn_parse_batch(self, arena, off, sz, stride: int = 864):
+        return _parse_batch(self.lib.ref_txn_parse_batch, arena, off, sz, stride)
 
 
 def cpu_has_avx512_ifma() -> bool:
