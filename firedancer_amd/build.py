@@ -14,7 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 ARCH = os.environ.get("FDGPU_ARCH", "gfx950")
 
 HIP_SRCS = ["fd_ed25519_gpu.hip"]
-HIP_DEPS = ["fd_gpu_f25519.h", "fd_gpu_sha512.h", "fd_gpu_curve.h", "../../include/fd_ed25519_gpu.h"]
+HIP_DEPS = ["fd_gpu_f25519.h", "fd_gpu_sha512.h", "fd_gpu_curve.h", "fd_gpu_txn.h", "../../include/fd_ed25519_gpu.h"]
 
 
 def _stale(out: str, deps: list[str]) -> bool:

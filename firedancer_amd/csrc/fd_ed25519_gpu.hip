@@ -15,6 +15,9 @@
                        compare with R -> FD_ED25519_SUCCESS / ERR_MSG
      fd_reduce_kernel  per transaction: fd_ed25519_verify_batch_single_msg
                        code from its signatures' codes
+     fd_parse_kernel   (raw-payload batches) per transaction: fd_txn_parse,
+                       fd_txn_t image, and the descriptor the kernels
+                       above consume
 
    Replaces (behaviour, not code) fd_ed25519_verify /
    fd_ed25519_verify_batch_single_msg (src/ballet/ed25519/
@@ -28,6 +31,7 @@
 
 #include "fd_gpu_sha512.h"
 #include "fd_gpu_curve.h"
+#include "fd_gpu_txn.h"
 #include "../../include/fd_ed25519_gpu.h"
 
 #include <hip/hip_runtime.h>
@@ -312,13 +316,15 @@ fd_dsm_kernel( u32                      nsig,
 
 __global__ void __launch_bounds__( FD_WG )
 fd_reduce_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 nsig,
-                  i8 const * __restrict__ code, i8 * __restrict__ txn_out ) {
+                  i8 const * __restrict__ code, unsigned char const * __restrict__ pflag,
+                  i8 * __restrict__ txn_out ) {
   u32 t = blockIdx.x * FD_WG + threadIdx.x;
   if( t >= txn_cnt ) return;
   fdgpu_txn_desc_t d = desc[t];
   u32 cnt = d.sig_cnt;
   int r;
-  if( cnt==0u || cnt>16u ) r = FD_ED25519_ERR_SIG;           /* fd_ed25519_user.c:238-241 */
+  if( pflag && pflag[t] ) r = FDGPU_ERR_PARSE;               /* fd_verify_tile.c:127-131 */
+  else if( cnt==0u || cnt>16u ) r = FD_ED25519_ERR_SIG;      /* fd_ed25519_user.c:238-241 */
   else {
     int first = 0, any_msg = 0;
     for( u32 j=0; j<cnt; j++ ) {
@@ -330,6 +336,44 @@ fd_reduce_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 n
     r = first ? first : ( any_msg ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS );  /* pass 2, :297-306 */
   }
   txn_out[t] = (i8)r;
+}
+
+/* Raw-payload batches: fd_txn_parse per transaction (fd_gpu_txn.h), then
+   the descriptor the verify kernels consume.  A rejected payload keeps
+   its reserved signature lanes (sig_lanes) but gets payload_sz = 0, so
+   the decode kernel's bounds check retires those lanes at once, and its
+   pflag makes the reduce kernel report FDGPU_ERR_PARSE.  A parsed
+   transaction with more than 16 signatures gets sig_cnt = 0 (no lanes;
+   the reduce kernel's batch-size rule gives ERR_SIG). */
+__global__ void __launch_bounds__( FD_WG )
+fd_parse_kernel( unsigned char const *    __restrict__ payload,
+                 fdgpu_txn_raw_t const *  __restrict__ raw,
+                 u32                                    txn_cnt,
+                 fdgpu_txn_desc_t *       __restrict__ desc_out,
+                 unsigned char *          __restrict__ pflag,
+                 unsigned char *          __restrict__ img,
+                 u32                                    img_stride,
+                 unsigned short *         __restrict__ fp_out ) {
+  u32 t = blockIdx.x * FD_WG + threadIdx.x;
+  if( t >= txn_cnt ) return;
+  fdgpu_txn_raw_t r = raw[t];
+  fd_txn_hdr h;
+  u32 fp = fd_txn_parse_dev( payload + r.payload_off, (u32)r.payload_sz,
+                             img ? img + (size_t)t*img_stride : (unsigned char *)0, h );
+  if( fp_out ) fp_out[t] = (unsigned short)fp;
+  if( !desc_out ) return;
+  fdgpu_txn_desc_t d;
+  d.payload_off = r.payload_off; d.sig_base = r.sig_base;
+  u32 lanes = h.sig_cnt <= 16u ? h.sig_cnt : 0u;
+  int ok = fp != 0u && lanes == (u32)r.sig_lanes;   /* lanes != sig_lanes only if the stager lied */
+  if( ok ) {
+    d.payload_sz = r.payload_sz; d.message_off = (unsigned short)h.msg_off; d.acct_addr_off = (unsigned short)h.acct_off;
+    d.signature_off = (unsigned char)h.sig_off; d.sig_cnt = (unsigned char)lanes;
+  } else {
+    d.payload_sz = 0; d.message_off = 0; d.acct_addr_off = 0; d.signature_off = 0; d.sig_cnt = r.sig_lanes;
+  }
+  desc_out[t] = d;
+  pflag[t] = ok ? 0u : 1u;
 }
 
 /* [e]B for e in [0,128], affine precomputed (y+x, y-x, 2dxy), canonical,
@@ -392,6 +436,8 @@ struct fdgpu_ed25519_ctx {
   i8 *    d_digA;
   i8 *    d_digB;
   uint4 * d_btab;
+  fdgpu_txn_desc_t * d_rdesc;    /* raw path: descriptors derived by fd_parse_kernel */
+  unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
   hipEvent_t ev[4];
   enum { NRING = 64 };
   hipEvent_t ring[ NRING ][ 4 ];  /* per-batch kernel boundaries while timing is on */
@@ -407,7 +453,8 @@ struct fdgpu_ed25519_ctx {
 extern "C" char const * fdgpu_last_error( void ) { return fd_err.c_str(); }
 
 static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_desc_t const * d_desc,
-                         unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, i8 * d_sig_out, hipStream_t st ) {
+                         unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, i8 * d_sig_out, hipStream_t st,
+                         unsigned char const * d_pflag = NULL ) {
   if( !txn_cnt ) return 0;
   i8 * code = d_sig_out ? d_sig_out : ctx->d_code;
   hipEvent_t * ev = ctx->ev;
@@ -429,7 +476,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
                         ctx->d_digA, ctx->d_digB, ctx->d_btab, code );
     if( ctx->timing ) hipEventRecord( ev[2], st );
   }
-  hipLaunchKernelGGL( fd_reduce_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, nsig, code, d_txn_out );
+  hipLaunchKernelGGL( fd_reduce_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, nsig, code, d_pflag, d_txn_out );
   if( ctx->timing ) hipEventRecord( ev[3], st );
   HIPCHK( hipGetLastError(), -3 );
   return 0;
@@ -455,6 +502,8 @@ fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
   HIPCHK( hipMalloc( &ctx->d_digA, ns * 64 ), NULL );
   HIPCHK( hipMalloc( &ctx->d_digB, ns * 32 ), NULL );
   HIPCHK( hipMalloc( &ctx->d_btab, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_rdesc, max_txn * sizeof(fdgpu_txn_desc_t) ), NULL );
+  HIPCHK( hipMalloc( &ctx->d_pflag, max_txn ), NULL );
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), NULL );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), NULL );
   ctx->ring_cnt = 0;
@@ -486,7 +535,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   hipSetDevice( ctx->device );
   hipStreamSynchronize( ctx->stream );
   hipFree( ctx->d_map ); hipFree( ctx->d_code ); hipFree( ctx->d_pstat ); hipFree( ctx->d_tab ); hipFree( ctx->d_Rxy ); hipFree( ctx->d_Axy );
-  hipFree( ctx->d_digA ); hipFree( ctx->d_digB ); hipFree( ctx->d_btab );
+  hipFree( ctx->d_digA ); hipFree( ctx->d_digB ); hipFree( ctx->d_btab ); hipFree( ctx->d_rdesc ); hipFree( ctx->d_pflag );
   for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ev[i] );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ring[r][i] );
   for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
@@ -606,6 +655,92 @@ fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
   if( rc ) return rc;
   HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
   if( sig_out && nsig ) HIPCHK( hipMemcpyAsync( sig_out, ctx->d_code, nsig, hipMemcpyDeviceToHost, st ), -2 );
+  HIPCHK( hipStreamSynchronize( st ), -2 );
+  memcpy( txn_out, sl.h_txn_out, txn_cnt );
+  return 0;
+}
+
+/* ---- raw-payload batches (device fd_txn_parse + verify) ------------- */
+
+extern "C" int
+fdgpu_txn_parse_device( unsigned char const * d_payload, fdgpu_txn_raw_t const * d_raw, unsigned long txn_cnt,
+                        unsigned char * d_img, unsigned long img_stride, unsigned short * d_fp, void * stream ) {
+  if( !txn_cnt ) return 0;
+  if( txn_cnt >= (1UL<<31) || ( d_img && ( img_stride < 852UL || img_stride > 0xffffffffUL ) ) ) { fd_err = "bad arguments"; return -1; }
+  unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
+  hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, (hipStream_t)stream, d_payload, d_raw, (u32)txn_cnt,
+                      (fdgpu_txn_desc_t *)NULL, (unsigned char *)NULL, d_img, (u32)img_stride, d_fp );
+  HIPCHK( hipGetLastError(), -3 );
+  return 0;
+}
+
+static int launch_raw( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_raw_t const * d_raw,
+                       unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, unsigned char * d_img,
+                       unsigned long img_stride, unsigned short * d_fp, hipStream_t st ) {
+  if( !txn_cnt ) return 0;
+  unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
+  hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, st, d_payload, d_raw, (u32)txn_cnt,
+                      ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp );
+  HIPCHK( hipGetLastError(), -3 );
+  return launch_batch( ctx, d_payload, ctx->d_rdesc, txn_cnt, sig_cnt, d_txn_out, NULL, st, ctx->d_pflag );
+}
+
+extern "C" int
+fdgpu_ed25519_verify_raw_device( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_raw_t const * d_raw,
+                                 unsigned long txn_cnt, unsigned long sig_cnt, signed char * d_txn_out,
+                                 unsigned char * d_img, unsigned long img_stride, unsigned short * d_fp, void * stream ) {
+  if( !ctx ) { fd_err = "NULL ctx"; return -1; }
+  if( txn_cnt > ctx->max_txn || sig_cnt > ctx->max_sig ) { fd_err = "batch larger than ctx"; return -1; }
+  if( d_img && ( img_stride < 852UL || img_stride > 0xffffffffUL ) ) { fd_err = "img_stride < FD_TXN_MAX_SZ"; return -1; }
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  return launch_raw( ctx, d_payload, d_raw, txn_cnt, sig_cnt, (i8 *)d_txn_out, d_img, img_stride, d_fp,
+                     stream ? (hipStream_t)stream : ctx->stream );
+}
+
+/* host side of the raw path: signature lanes from each payload's first
+   byte (the parsed signature_cnt, fd_txn_parse.c:86) and their prefix */
+static int stage_raw( unsigned char const * payload, unsigned long payload_bytes, fdgpu_txn_raw_t * raw,
+                      unsigned long txn_cnt, unsigned long * sig_total ) {
+  unsigned long s = 0;
+  for( unsigned long i=0; i<txn_cnt; i++ ) {
+    if( (unsigned long)raw[i].payload_off + raw[i].payload_sz > payload_bytes ) { fd_err = "payload out of arena"; return -1; }
+    unsigned b0 = raw[i].payload_sz ? payload[ raw[i].payload_off ] : 0u;
+    raw[i].sig_lanes = (unsigned char)( ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u );
+    raw[i].sig_base  = (unsigned)s;
+    s += raw[i].sig_lanes;
+  }
+  *sig_total = s;
+  return 0;
+}
+
+extern "C" int
+fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload, unsigned long payload_bytes,
+                               fdgpu_txn_raw_t * raw, unsigned long txn_cnt, signed char * txn_out,
+                               unsigned char * img, unsigned long img_stride, unsigned short * fp ) {
+  if( !ctx ) { fd_err = "NULL ctx"; return -1; }
+  unsigned long nsig;
+  if( stage_raw( payload, payload_bytes, raw, txn_cnt, &nsig ) ) return -1;
+  if( txn_cnt > ctx->max_txn || nsig > ctx->max_sig || payload_bytes > ctx->max_payload ) { fd_err = "batch larger than ctx"; return -1; }
+  if( img && img_stride < 852UL ) { fd_err = "img_stride < FD_TXN_MAX_SZ"; return -1; }
+  if( !txn_cnt ) return 0;
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  fd_slot & sl = ctx->slot[0];
+  if( !ctx->inflight.empty() ) { fd_err = "async batches in flight"; return -1; }
+  memcpy( sl.h_payload, payload, payload_bytes );
+  memset( sl.h_payload + payload_bytes, 0, FD_ARENA_SLACK );
+  memcpy( sl.h_desc, raw, txn_cnt * sizeof(fdgpu_txn_raw_t) );
+  hipStream_t st = ctx->stream;
+  unsigned char * d_img = NULL; unsigned short * d_fp = NULL;
+  if( img ) HIPCHK( hipMallocAsync( (void **)&d_img, txn_cnt * img_stride, st ), -2 );
+  if( fp  ) HIPCHK( hipMallocAsync( (void **)&d_fp,  txn_cnt * sizeof(unsigned short), st ), -2 );
+  HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, payload_bytes + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+  HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, txn_cnt * sizeof(fdgpu_txn_raw_t), hipMemcpyHostToDevice, st ), -2 );
+  int rc = launch_raw( ctx, sl.d_payload, (fdgpu_txn_raw_t const *)sl.d_desc, txn_cnt, nsig, sl.d_txn_out, d_img,
+                       img_stride, d_fp, st );
+  if( rc ) return rc;
+  HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
+  if( img ) { HIPCHK( hipMemcpyAsync( img, d_img, txn_cnt * img_stride, hipMemcpyDeviceToHost, st ), -2 ); HIPCHK( hipFreeAsync( d_img, st ), -2 ); }
+  if( fp  ) { HIPCHK( hipMemcpyAsync( fp, d_fp, txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 ); HIPCHK( hipFreeAsync( d_fp, st ), -2 ); }
   HIPCHK( hipStreamSynchronize( st ), -2 );
   memcpy( txn_out, sl.h_txn_out, txn_cnt );
   return 0;

@@ -281,12 +281,30 @@ static void * job( void * _j ) {
     size_t msg_off; size_t sz = txn_layout( j->kind, nsig, &msg_off );
     uint8_t * p = j->payload + t * j->stride;
     fdgpu_txn_desc_t * d = j->desc + t;
-    /* body: header, accounts (signers first), blockhash, filler */
+    /* body: a well-formed legacy message (fd_txn_parse accepts it):
+       header, accounts (signers first, then the program ids),
+       blockhash, instructions.  LARGE_NOOP / SMALL_MSG follow fd_benchg's
+       large_noop_t (fd_benchg.c:102-171): 3 accounts, a 9-byte compute
+       budget instruction and a filler instruction to the program at
+       account 2; MULTI has nsig+1 accounts and one filler instruction
+       (which is what lets 12 signers fit in 1232 bytes). */
     uint8_t * m = p + msg_off;
     size_t msz = sz - msg_off;
     for( size_t i=0; i<msz; i+=8 ) { uint64_t x = xs( &st ); size_t n = msz-i < 8 ? msz-i : 8; memcpy( m+i, &x, n ); }
+    int nprog = j->kind==FDSYNTH_MULTI ? 1 : 2;
+    size_t acct = (size_t)nsig + (size_t)nprog;
     p[0] = (uint8_t)nsig;
-    m[0] = (uint8_t)nsig; m[1] = 0; m[2] = (uint8_t)(j->kind==FDSYNTH_MULTI ? 1 : 2); m[3] = (uint8_t)(nsig + 2);
+    m[0] = (uint8_t)nsig; m[1] = 0; m[2] = (uint8_t)nprog; m[3] = (uint8_t)acct;
+    {
+      uint8_t * q = m + 4 + 32*acct + 32;             /* after accounts and blockhash */
+      *q++ = (uint8_t)nprog;                           /* instr_cnt */
+      if( nprog==2 ) { q[0] = (uint8_t)nsig; q[1] = 0; q[2] = 9; q[3] = 3; q += 12; }   /* set CU price */
+      size_t rem = (size_t)( (m + msz) - q ) - 2;      /* prog_id + acct_cnt */
+      size_t dsz = rem - 1 <= 127 ? rem - 1 : rem - 2; /* compact-u16 data_sz (sizes here never hit 129) */
+      q[0] = (uint8_t)( nsig + nprog - 1 ); q[1] = 0; q += 2;
+      if( dsz <= 127 ) *q++ = (uint8_t)dsz;
+      else { *q++ = (uint8_t)( 0x80 | (dsz & 0x7f) ); *q++ = (uint8_t)( dsz >> 7 ); }
+    }
     fdsynth_key_t const * ks[16];
     for( int s=0; s<nsig; s++ ) { ks[s] = &j->keys[ (t*7 + (size_t)s*13 + (xs( &st ) & 3)) % j->nkeys ]; memcpy( m + 4 + 32*s, ks[s]->pub, 32 ); }
     int8_t code = 0;
@@ -331,7 +349,7 @@ size_t fdsynth_txns( uint8_t * payload, size_t stride, fdgpu_txn_desc_t * desc, 
   if( threads < 1 ) threads = 1;
   if( threads > 64 ) threads = 64;
   if( max_signers < 1 ) max_signers = 1;
-  if( max_signers > 16 ) max_signers = 16;
+  if( max_signers > 12 ) max_signers = 12;   /* 13 signer accounts no longer fit 1232 bytes */
   pthread_t th[64]; job_t jb[64];
   for( int i=0; i<threads; i++ ) {
     jb[i] = (job_t){ payload, desc, expect, keys, nkeys, n*(size_t)i/(size_t)threads, n*(size_t)(i+1)/(size_t)threads,

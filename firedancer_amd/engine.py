@@ -32,11 +32,17 @@ DESC_DTYPE = np.dtype([("payload_off", "<u4"), ("sig_base", "<u4"), ("payload_sz
                        ("message_off", "<u2"), ("acct_addr_off", "<u2"), ("signature_off", "u1"),
                        ("sig_cnt", "u1")])
 assert DESC_DTYPE.itemsize == 16
+RAW_DTYPE = np.dtype([("payload_off", "<u4"), ("sig_base", "<u4"), ("payload_sz", "<u2"), ("sig_lanes", "u1"),
+                      ("_pad", "u1", (5,))])
+assert RAW_DTYPE.itemsize == 16
+FDGPU_ERR_PARSE = -16
+TXN_IMG_STRIDE = 864
 
 # every symbol include/fd_ed25519_gpu.h declares
 EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed25519_strerror",
            "fdgpu_ed25519_ctx_new", "fdgpu_ed25519_ctx_delete", "fdgpu_ed25519_verify_txns_device",
-           "fdgpu_ed25519_verify_txns_host", "fdgpu_ed25519_submit", "fdgpu_ed25519_flush",
+           "fdgpu_ed25519_verify_txns_host", "fdgpu_txn_parse_device", "fdgpu_ed25519_verify_raw_device",
+           "fdgpu_ed25519_verify_raw_host", "fdgpu_ed25519_submit", "fdgpu_ed25519_flush",
            "fdgpu_ed25519_poll", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_last_error")
 
@@ -80,6 +86,17 @@ def load_library():
         L.fdgpu_ed25519_verify_txns_host.restype = ctypes.c_int
         L.fdgpu_ed25519_verify_txns_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
                                                     ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p]
+        L.fdgpu_txn_parse_device.restype = ctypes.c_int
+        L.fdgpu_txn_parse_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                                             ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p]
+        L.fdgpu_ed25519_verify_raw_device.restype = ctypes.c_int
+        L.fdgpu_ed25519_verify_raw_device.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
+                                                      ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
+                                                      ctypes.c_void_p, ctypes.c_void_p]
+        L.fdgpu_ed25519_verify_raw_host.restype = ctypes.c_int
+        L.fdgpu_ed25519_verify_raw_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                                                    ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
+                                                    ctypes.c_void_p]
         L.fdgpu_ed25519_submit.restype = ctypes.c_int
         L.fdgpu_ed25519_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ushort, ctypes.c_ubyte,
                                            ctypes.c_ushort, ctypes.c_ushort, ctypes.c_ubyte, ctypes.c_ulong]
@@ -116,6 +133,26 @@ def fd_ed25519_verify_batch_single_msg(msg: bytes, signatures: bytes, pubkeys: b
     L = load_library()
     m, mp = _buf(msg); s, sp = _buf(signatures); p, pp = _buf(pubkeys)
     return L.fd_ed25519_verify_batch_single_msg(mp, len(msg), sp, pp, None, batch_sz & 0xff)
+
+
+def txn_parse_device(d_payload: int, d_raw: int, txn_cnt: int, d_img: int | None, d_fp: int,
+                     stream: int | None = None, img_stride: int = TXN_IMG_STRIDE) -> None:
+    """Batch fd_txn_parse on the GPU (fdgpu_txn_parse_device), device pointers."""
+    rc = load_library().fdgpu_txn_parse_device(d_payload, d_raw, txn_cnt, d_img, img_stride, d_fp, stream)
+    if rc:
+        raise RuntimeError(f"fdgpu_txn_parse_device: {rc} {last_error()}")
+
+
+def raw_records(payload: np.ndarray, off: np.ndarray, sz: np.ndarray):
+    """Host staging of a raw-payload batch: (RAW_DTYPE records, total signature lanes)."""
+    raw = np.zeros(len(off), RAW_DTYPE)
+    raw["payload_off"] = off
+    raw["payload_sz"] = sz
+    b0 = np.where(np.asarray(sz) > 0, payload[np.minimum(off, len(payload) - 1)], 0)
+    lanes = np.where((b0 >= 1) & (b0 <= 16), b0, 0).astype(np.uint32)
+    raw["sig_lanes"] = lanes
+    raw["sig_base"] = np.concatenate([[0], np.cumsum(lanes)[:-1]]).astype(np.uint32) if len(off) else []
+    return raw, int(lanes.sum())
 
 
 def fd_ed25519_strerror(err: int) -> str:
@@ -174,6 +211,33 @@ class Engine:
                                                      d_sig_out, stream)
         if rc:
             raise RuntimeError(f"fdgpu_ed25519_verify_txns_device: {rc} {last_error()}")
+
+    # -- raw payloads: device fd_txn_parse + verify ---------------------------
+    def verify_raw_host(self, payload: np.ndarray, off: np.ndarray, sz: np.ndarray, want_img: bool = False):
+        """Parse + verify raw transaction payloads (payload[off[t]:off[t]+sz[t]]).
+        Returns (codes int8 -- FDGPU_ERR_PARSE or the batch verify code, footprints uint16,
+        fd_txn_t images uint8[n, TXN_IMG_STRIDE] or None)."""
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        n = len(off)
+        raw = np.zeros(n, RAW_DTYPE)
+        raw["payload_off"] = off
+        raw["payload_sz"] = sz
+        codes = np.zeros(n, np.int8)
+        fp = np.zeros(n, np.uint16)
+        img = np.zeros((n, TXN_IMG_STRIDE), np.uint8) if want_img else None
+        rc = self.L.fdgpu_ed25519_verify_raw_host(self.ctx, payload.ctypes.data, payload.nbytes, raw.ctypes.data, n,
+                                                  codes.ctypes.data, img.ctypes.data if img is not None else None,
+                                                  TXN_IMG_STRIDE, fp.ctypes.data)
+        if rc:
+            raise RuntimeError(f"fdgpu_ed25519_verify_raw_host: {rc} {last_error()}")
+        return codes, fp, img
+
+    def verify_raw_device(self, d_payload: int, d_raw: int, txn_cnt: int, sig_cnt: int, d_txn_out: int,
+                          d_img: int | None = None, d_fp: int | None = None, stream: int | None = None):
+        rc = self.L.fdgpu_ed25519_verify_raw_device(self.ctx, d_payload, d_raw, txn_cnt, sig_cnt, d_txn_out, d_img,
+                                                    TXN_IMG_STRIDE, d_fp, stream)
+        if rc:
+            raise RuntimeError(f"fdgpu_ed25519_verify_raw_device: {rc} {last_error()}")
 
     # -- async pipeline ------------------------------------------------------
     def submit(self, payload: bytes, signature_off: int, acct_addr_off: int, message_off: int,

@@ -106,6 +106,29 @@ typedef struct fdgpu_txn_desc {
   unsigned char  sig_cnt;
 } fdgpu_txn_desc_t;
 
+/* Raw-payload batches (the verify tile's after_frag work, fd_txn_parse +
+   fd_txn_verify, src/disco/verify/fd_verify_tile.c:110-140, moved onto
+   the GPU).  One 16-byte record per transaction: the stager only copies
+   the payload and reads its first byte.  sig_lanes = payload[0] if
+   1 <= payload[0] <= 16, else 0 (a parsed transaction's signature_cnt
+   is its first byte, fd_txn_parse.c:86); sig_base = exclusive prefix
+   sum of sig_lanes.  The device parses every payload
+   (fd_txn_parse_core semantics), derives the fdgpu_txn_desc_t itself and
+   verifies the parsed transactions.  Per-transaction result:
+   FDGPU_ERR_PARSE if fd_txn_parse rejects the payload, else the
+   fd_ed25519_verify_batch_single_msg code (ERR_SIG for signature_cnt
+   > 16). */
+typedef struct fdgpu_txn_raw {
+  unsigned int   payload_off;
+  unsigned int   sig_base;
+  unsigned short payload_sz;
+  unsigned char  sig_lanes;
+  unsigned char  _pad[ 5 ];
+} fdgpu_txn_raw_t;
+
+#define FDGPU_ERR_PARSE        (-16)    /* fd_txn_parse returned 0 */
+#define FDGPU_TXN_IMG_STRIDE   (864UL)  /* >= FD_TXN_MAX_SZ (852), fd_txn.h:99 */
+
 typedef struct fdgpu_ed25519_ctx fdgpu_ed25519_ctx_t;
 
 /* fdgpu_ed25519_ctx_new creates an engine bound to HIP device `device`
@@ -151,6 +174,54 @@ fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t *    ctx,
                                 unsigned long            txn_cnt,
                                 signed char *            txn_out,
                                 signed char *            sig_out );
+
+/* fdgpu_txn_parse_device: batch fd_txn_parse (src/ballet/txn/fd_txn.h:
+   713-715 / fd_txn_parse.c:6-252) on the device.  Transaction t is
+   d_payload[ d_raw[t].payload_off, +payload_sz ); its fd_txn_t image
+   goes to d_img + t*img_stride (img_stride >= 852; d_img may be NULL)
+   and its footprint (0 = rejected) to d_fp[t].  Only payload_off and
+   payload_sz of d_raw are read.  Asynchronous on `stream`. */
+int
+fdgpu_txn_parse_device( unsigned char const *   d_payload,
+                        fdgpu_txn_raw_t const * d_raw,
+                        unsigned long           txn_cnt,
+                        unsigned char *         d_img,
+                        unsigned long           img_stride,
+                        unsigned short *        d_fp,
+                        void *                  stream );
+
+/* fdgpu_ed25519_verify_raw_device: parse + verify a raw-payload batch
+   resident in device memory (see fdgpu_txn_raw_t).  sig_cnt = sum of
+   sig_lanes.  d_txn_out[t] gets FDGPU_ERR_PARSE or the batch verify
+   code; d_img / d_fp (optional) get the parser's fd_txn_t images and
+   footprints, which the tile publishes after the payload
+   (fd_verify_tile.c:111).  Asynchronous. */
+int
+fdgpu_ed25519_verify_raw_device( fdgpu_ed25519_ctx_t *   ctx,
+                                 unsigned char const *   d_payload,
+                                 fdgpu_txn_raw_t const * d_raw,
+                                 unsigned long           txn_cnt,
+                                 unsigned long           sig_cnt,
+                                 signed char *           d_txn_out,
+                                 unsigned char *         d_img,
+                                 unsigned long           img_stride,
+                                 unsigned short *        d_fp,
+                                 void *                  stream );
+
+/* fdgpu_ed25519_verify_raw_host: the same from host memory (payload
+   arena + raw records; sig_lanes / sig_base are recomputed here from
+   the payloads, so only payload_off / payload_sz need be set).
+   Synchronous.  img (txn_cnt*img_stride bytes) and fp may be NULL. */
+int
+fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t *   ctx,
+                               unsigned char const *   payload,
+                               unsigned long           payload_bytes,
+                               fdgpu_txn_raw_t *       raw,
+                               unsigned long           txn_cnt,
+                               signed char *           txn_out,
+                               unsigned char *         img,
+                               unsigned long           img_stride,
+                               unsigned short *        fp );
 
 /* Async submit / poll pipeline (the offload shape fd_verify_tile needs,
    SURVEY.md §8b).  submit copies one transaction payload into the
