@@ -410,16 +410,22 @@ static void set_err( char const * what, hipError_t e ) {
 
 struct fd_slot {               /* one in-flight host batch of the async pipeline */
   unsigned char *    h_payload;
-  fdgpu_txn_desc_t * h_desc;
+  fdgpu_txn_desc_t * h_desc;   /* desc mode: fdgpu_txn_desc_t; raw mode: fdgpu_txn_raw_t (same size) */
   i8 *               h_txn_out;
   unsigned long *    h_tags;
   unsigned char *    d_payload;
   fdgpu_txn_desc_t * d_desc;
   i8 *               d_txn_out;
+  unsigned short *   h_fp;     /* raw mode: footprints + fd_txn_t images (allocated on first raw use) */
+  unsigned char *    h_img;
+  unsigned short *   d_fp;
+  unsigned char *    d_img;
   size_t             payload_used;
   unsigned long      txn_cnt, sig_cnt;
-  hipEvent_t         done;
-  int                state;   /* 0 filling, 1 in flight */
+  unsigned long      cursor;   /* results already handed out by poll */
+  hipEvent_t         h2d, kdone, done;
+  int                state;    /* 0 filling, 1 in flight / draining */
+  int                mode;     /* 0 desc (fdgpu_ed25519_submit), 1 raw (fdgpu_ed25519_submit_raw) */
 };
 
 struct fdgpu_ed25519_ctx {
@@ -442,15 +448,26 @@ struct fdgpu_ed25519_ctx {
   enum { NRING = 64 };
   hipEvent_t ring[ NRING ][ 4 ];  /* per-batch kernel boundaries while timing is on */
   unsigned long ring_cnt;
-  /* async pipeline */
-  enum { NSLOT = 2 };
+  /* async pipeline: NSLOT pinned staging slots; H2D / D2H on the copy
+     stream, kernels on the compute stream, so slot k+1's upload overlaps
+     slot k's kernels (the ctx scratch is only touched in compute-stream
+     order) */
+  enum { NSLOT = 4 };
   fd_slot slot[ NSLOT ];
   int cur;                       /* slot being filled */
   std::deque<int> inflight;      /* slot order */
-  std::deque<std::pair<unsigned long,i8>> ready;
+  hipStream_t cstream;
 };
 
 extern "C" char const * fdgpu_last_error( void ) { return fd_err.c_str(); }
+
+/* the synchronous host calls stage through slot 0: only when the async
+   pipeline holds nothing */
+static int async_busy( fdgpu_ed25519_ctx_t const * ctx ) {
+  if( !ctx->inflight.empty() ) return 1;
+  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) if( ctx->slot[i].txn_cnt ) return 1;
+  return 0;
+}
 
 static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_desc_t const * d_desc,
                          unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, i8 * d_sig_out, hipStream_t st,
@@ -493,6 +510,7 @@ fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
   ctx->max_txn = max_txn; ctx->max_sig = max_sig; ctx->max_payload = max_payload_bytes;
   size_t ns = max_sig;
   HIPCHK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ), NULL );
+  HIPCHK( hipStreamCreateWithFlags( &ctx->cstream, hipStreamNonBlocking ), NULL );
   HIPCHK( hipMalloc( &ctx->d_map,  ns * sizeof(u32) ), NULL );
   HIPCHK( hipMalloc( &ctx->d_code, ns ), NULL );
   HIPCHK( hipMalloc( &ctx->d_pstat, 2*ns ), NULL );
@@ -523,6 +541,8 @@ fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
       memset( sl.h_payload, 0, max_payload_bytes + FD_ARENA_SLACK );
     }
     HIPCHK( hipEventCreateWithFlags( &sl.done, hipEventDisableTiming ), NULL );
+    HIPCHK( hipEventCreateWithFlags( &sl.h2d, hipEventDisableTiming ), NULL );
+    HIPCHK( hipEventCreateWithFlags( &sl.kdone, hipEventDisableTiming ), NULL );
   }
   ctx->cur = 0;
   HIPCHK( hipStreamSynchronize( ctx->stream ), NULL );
@@ -542,8 +562,11 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
     fd_slot & sl = ctx->slot[i];
     if( sl.h_payload ) { hipHostFree( sl.h_payload ); hipHostFree( sl.h_desc ); hipHostFree( sl.h_txn_out ); hipHostFree( sl.h_tags );
                          hipFree( sl.d_payload ); hipFree( sl.d_desc ); hipFree( sl.d_txn_out ); }
-    hipEventDestroy( sl.done );
+    if( sl.h_img ) { hipHostFree( sl.h_img ); hipHostFree( sl.h_fp ); hipFree( sl.d_img ); hipFree( sl.d_fp ); }
+    hipEventDestroy( sl.done ); hipEventDestroy( sl.h2d ); hipEventDestroy( sl.kdone );
   }
+  hipStreamSynchronize( ctx->cstream );
+  hipStreamDestroy( ctx->cstream );
   hipStreamDestroy( ctx->stream );
   delete ctx;
 }
@@ -644,7 +667,7 @@ fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
   if( !txn_cnt ) return 0;
   HIPCHK( hipSetDevice( ctx->device ), -2 );
   fd_slot & sl = ctx->slot[0];
-  if( !ctx->inflight.empty() ) { fd_err = "async batches in flight"; return -1; }
+  if( async_busy( ctx ) ) { fd_err = "async batches pending or in flight"; return -1; }
   memcpy( sl.h_payload, payload, payload_bytes );
   memset( sl.h_payload + payload_bytes, 0, FD_ARENA_SLACK );
   memcpy( sl.h_desc, desc, txn_cnt * sizeof(fdgpu_txn_desc_t) );
@@ -725,7 +748,7 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
   if( !txn_cnt ) return 0;
   HIPCHK( hipSetDevice( ctx->device ), -2 );
   fd_slot & sl = ctx->slot[0];
-  if( !ctx->inflight.empty() ) { fd_err = "async batches in flight"; return -1; }
+  if( async_busy( ctx ) ) { fd_err = "async batches pending or in flight"; return -1; }
   memcpy( sl.h_payload, payload, payload_bytes );
   memset( sl.h_payload + payload_bytes, 0, FD_ARENA_SLACK );
   memcpy( sl.h_desc, raw, txn_cnt * sizeof(fdgpu_txn_raw_t) );
@@ -750,23 +773,28 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
 
 static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
   fd_slot & sl = ctx->slot[i];
-  hipStream_t st = ctx->stream;
+  hipStream_t cs = ctx->cstream, st = ctx->stream;
   memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
-  HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
-  HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
-  int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
+  HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, cs ), -2 );
+  HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, cs ), -2 );
+  HIPCHK( hipEventRecord( sl.h2d, cs ), -2 );
+  HIPCHK( hipStreamWaitEvent( st, sl.h2d, 0 ), -2 );
+  int rc = sl.mode
+         ? launch_raw( ctx, sl.d_payload, (fdgpu_txn_raw_t const *)sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out,
+                       sl.d_img, FDGPU_TXN_IMG_STRIDE, sl.d_fp, st )
+         : launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
   if( rc ) return rc;
-  HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
-  HIPCHK( hipEventRecord( sl.done, st ), -2 );
-  sl.state = 1;
+  HIPCHK( hipEventRecord( sl.kdone, st ), -2 );
+  HIPCHK( hipStreamWaitEvent( cs, sl.kdone, 0 ), -2 );
+  HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, cs ), -2 );
+  if( sl.mode ) {
+    HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, cs ), -2 );
+    HIPCHK( hipMemcpyAsync( sl.h_img, sl.d_img, sl.txn_cnt * FDGPU_TXN_IMG_STRIDE, hipMemcpyDeviceToHost, cs ), -2 );
+  }
+  HIPCHK( hipEventRecord( sl.done, cs ), -2 );
+  sl.state = 1; sl.cursor = 0;
   ctx->inflight.push_back( i );
   return 0;
-}
-
-static void slot_reap( fdgpu_ed25519_ctx_t * ctx, int i ) {
-  fd_slot & sl = ctx->slot[i];
-  for( unsigned long t=0; t<sl.txn_cnt; t++ ) ctx->ready.emplace_back( sl.h_tags[t], sl.h_txn_out[t] );
-  sl.txn_cnt = 0; sl.sig_cnt = 0; sl.payload_used = 0; sl.state = 0;
 }
 
 /* make ctx->cur a free slot; -2 if every slot is in flight */
@@ -789,19 +817,29 @@ fdgpu_ed25519_flush( fdgpu_ed25519_ctx_t * ctx ) {
   return 0;
 }
 
+/* the filling slot, flushed first if it cannot take one more transaction
+   of payload_sz bytes / sig_cnt signatures in `mode` */
+static fd_slot * slot_for( fdgpu_ed25519_ctx_t * ctx, unsigned long payload_sz, unsigned long sig_cnt, int mode, int * rc ) {
+  *rc = 0;
+  if( !ctx->slot[0].h_payload ) { fd_err = "ctx has no staging buffers (max_payload_bytes==0)"; *rc = -3; return NULL; }
+  if( next_free( ctx ) ) { *rc = -2; return NULL; }
+  fd_slot * sl = &ctx->slot[ ctx->cur ];
+  if( sl->txn_cnt && ( sl->mode != mode || sl->txn_cnt + 1 > ctx->max_txn || sl->sig_cnt + sig_cnt > ctx->max_sig
+                       || sl->payload_used + payload_sz + 8 > ctx->max_payload ) ) {
+    if( ( *rc = fdgpu_ed25519_flush( ctx ) ) ) return NULL;
+    if( next_free( ctx ) ) { *rc = -2; return NULL; }
+    sl = &ctx->slot[ ctx->cur ];
+  }
+  if( sl->txn_cnt==0 ) sl->mode = mode;
+  return sl;
+}
+
 extern "C" int
 fdgpu_ed25519_submit( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload, unsigned short payload_sz,
                       unsigned char signature_off, unsigned short acct_addr_off, unsigned short message_off,
                       unsigned char sig_cnt, unsigned long tag ) {
-  if( !ctx->slot[0].h_payload ) { fd_err = "ctx has no staging buffers (max_payload_bytes==0)"; return -3; }
-  if( next_free( ctx ) ) return -2;
-  fd_slot * sl = &ctx->slot[ ctx->cur ];
-  if( sl->txn_cnt + 1 > ctx->max_txn || sl->sig_cnt + sig_cnt > ctx->max_sig || sl->payload_used + payload_sz + 8 > ctx->max_payload ) {
-    int rc = fdgpu_ed25519_flush( ctx );
-    if( rc ) return rc;
-    if( next_free( ctx ) ) return -2;
-    sl = &ctx->slot[ ctx->cur ];
-  }
+  int rc; fd_slot * sl = slot_for( ctx, payload_sz, sig_cnt, 0, &rc );
+  if( !sl ) return rc;
   size_t off = sl->payload_used;
   memcpy( sl->h_payload + off, payload, payload_sz );
   fdgpu_txn_desc_t & d = sl->h_desc[ sl->txn_cnt ];
@@ -814,24 +852,77 @@ fdgpu_ed25519_submit( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload, 
   return malformed ? -1 : 0;
 }
 
+static int slot_raw_bufs( fdgpu_ed25519_ctx_t * ctx, fd_slot * sl ) {
+  if( sl->h_img ) return 0;
+  HIPCHK( hipSetDevice( ctx->device ), -3 );
+  HIPCHK( hipHostMalloc( (void **)&sl->h_img, ctx->max_txn * FDGPU_TXN_IMG_STRIDE, hipHostMallocDefault ), -3 );
+  HIPCHK( hipHostMalloc( (void **)&sl->h_fp, ctx->max_txn * sizeof(unsigned short), hipHostMallocDefault ), -3 );
+  HIPCHK( hipMalloc( (void **)&sl->d_img, ctx->max_txn * FDGPU_TXN_IMG_STRIDE ), -3 );
+  HIPCHK( hipMalloc( (void **)&sl->d_fp, ctx->max_txn * sizeof(unsigned short) ), -3 );
+  return 0;
+}
+
+extern "C" int
+fdgpu_ed25519_submit_raw( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload, unsigned short payload_sz,
+                          unsigned long tag ) {
+  unsigned b0 = payload_sz ? payload[0] : 0u;
+  unsigned lanes = ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u;
+  int rc; fd_slot * sl = slot_for( ctx, payload_sz, lanes, 1, &rc );
+  if( !sl ) return rc;
+  if( slot_raw_bufs( ctx, sl ) ) return -3;
+  size_t off = sl->payload_used;
+  memcpy( sl->h_payload + off, payload, payload_sz );
+  fdgpu_txn_raw_t & r = ((fdgpu_txn_raw_t *)sl->h_desc)[ sl->txn_cnt ];
+  r.payload_off = (unsigned)off; r.sig_base = (unsigned)sl->sig_cnt; r.payload_sz = payload_sz; r.sig_lanes = (unsigned char)lanes;
+  sl->h_tags[ sl->txn_cnt ] = tag;
+  sl->txn_cnt++; sl->sig_cnt += lanes; sl->payload_used = (off + payload_sz + 7) & ~(size_t)7;
+  return 0;
+}
+
+/* Drain completed slots in submission order, at most max results. */
+static unsigned long
+poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes, unsigned char * out_img,
+          unsigned short * out_fp, unsigned long max, int blocking ) {
+  hipSetDevice( ctx->device );
+  unsigned long n = 0;
+  while( n < max && !ctx->inflight.empty() ) {
+    int i = ctx->inflight.front();
+    fd_slot & sl = ctx->slot[i];
+    if( sl.cursor==0 ) {
+      hipError_t e = blocking ? hipEventSynchronize( sl.done ) : hipEventQuery( sl.done );
+      if( e != hipSuccess ) break;
+    }
+    unsigned long k = sl.txn_cnt - sl.cursor;
+    if( k > max - n ) k = max - n;
+    for( unsigned long t=0; t<k; t++ ) {
+      unsigned long u = sl.cursor + t;
+      out_tags[n+t]  = sl.h_tags[u];
+      out_codes[n+t] = sl.h_txn_out[u];
+      if( out_fp )  out_fp[n+t] = sl.mode ? sl.h_fp[u] : 0;
+      if( out_img && sl.mode ) {
+        unsigned fp = sl.h_fp[u];
+        memcpy( out_img + (n+t)*FDGPU_TXN_IMG_STRIDE, sl.h_img + u*FDGPU_TXN_IMG_STRIDE, fp );
+      }
+    }
+    n += k; sl.cursor += k;
+    if( sl.cursor==sl.txn_cnt ) {
+      ctx->inflight.pop_front();
+      sl.txn_cnt = 0; sl.sig_cnt = 0; sl.payload_used = 0; sl.cursor = 0; sl.state = 0;
+    }
+  }
+  return n;
+}
+
 extern "C" unsigned long
 fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes,
                     unsigned long max, int blocking ) {
-  hipSetDevice( ctx->device );
-  while( !ctx->inflight.empty() ) {
-    int i = ctx->inflight.front();
-    hipError_t e = blocking ? hipEventSynchronize( ctx->slot[i].done ) : hipEventQuery( ctx->slot[i].done );
-    if( e != hipSuccess ) break;
-    ctx->inflight.pop_front();
-    slot_reap( ctx, i );
-    if( ctx->ready.size() >= max ) break;
-  }
-  unsigned long n = 0;
-  while( n < max && !ctx->ready.empty() ) {
-    out_tags[n] = ctx->ready.front().first; out_codes[n] = ctx->ready.front().second;
-    ctx->ready.pop_front(); n++;
-  }
-  return n;
+  return poll_any( ctx, out_tags, out_codes, NULL, NULL, max, blocking );
+}
+
+extern "C" unsigned long
+fdgpu_ed25519_poll_raw( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes,
+                        unsigned char * out_img, unsigned short * out_fp, unsigned long max, int blocking ) {
+  return poll_any( ctx, out_tags, out_codes, out_img, out_fp, max, blocking );
 }
 
 /* ---- drop-in synchronous API (fd_ed25519.h) ------------------------- */

@@ -43,7 +43,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_ctx_new", "fdgpu_ed25519_ctx_delete", "fdgpu_ed25519_verify_txns_device",
            "fdgpu_ed25519_verify_txns_host", "fdgpu_txn_parse_device", "fdgpu_ed25519_verify_raw_device",
            "fdgpu_ed25519_verify_raw_host", "fdgpu_ed25519_submit", "fdgpu_ed25519_flush",
-           "fdgpu_ed25519_poll", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
+           "fdgpu_ed25519_poll", "fdgpu_ed25519_submit_raw", "fdgpu_ed25519_poll_raw", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_last_error")
 
 _lib = None
@@ -104,6 +104,11 @@ def load_library():
         L.fdgpu_ed25519_flush.argtypes = [ctypes.c_void_p]
         L.fdgpu_ed25519_poll.restype = ctypes.c_ulong
         L.fdgpu_ed25519_poll.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int]
+        L.fdgpu_ed25519_submit_raw.restype = ctypes.c_int
+        L.fdgpu_ed25519_submit_raw.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ushort, ctypes.c_ulong]
+        L.fdgpu_ed25519_poll_raw.restype = ctypes.c_ulong
+        L.fdgpu_ed25519_poll_raw.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int]
         L.fdgpu_ed25519_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.fdgpu_ed25519_kernel_ms.restype = ctypes.c_float
         L.fdgpu_ed25519_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_int]
@@ -253,6 +258,23 @@ class Engine:
         rc = self.L.fdgpu_ed25519_flush(self.ctx)
         if rc:
             raise RuntimeError(f"fdgpu_ed25519_flush: {rc} {last_error()}")
+
+    def submit_raw(self, payload: bytes, tag: int) -> int:
+        b = np.frombuffer(payload, np.uint8) if len(payload) else np.zeros(1, np.uint8)
+        rc = self.L.fdgpu_ed25519_submit_raw(self.ctx, b.ctypes.data, len(payload), tag)
+        if rc <= -3:
+            raise RuntimeError(f"fdgpu_ed25519_submit_raw: {rc} {last_error()}")
+        return rc
+
+    def poll_raw(self, max_n: int = 4096, blocking: bool = False):
+        """Completed raw submissions in order: (tags, codes, footprints, images)."""
+        tags = np.zeros(max_n, np.uint64)
+        codes = np.zeros(max_n, np.int8)
+        fp = np.zeros(max_n, np.uint16)
+        img = np.zeros((max_n, TXN_IMG_STRIDE), np.uint8)
+        n = self.L.fdgpu_ed25519_poll_raw(self.ctx, tags.ctypes.data, codes.ctypes.data, img.ctypes.data,
+                                          fp.ctypes.data, max_n, 1 if blocking else 0)
+        return tags[:n], codes[:n], fp[:n], img[:n]
 
     def poll(self, max_n: int = 4096, blocking: bool = False):
         tags = np.zeros(max_n, np.uint64)

@@ -253,6 +253,29 @@ fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx,
                     unsigned long         max,
                     int                   blocking );
 
+/* Raw-payload form of the pipeline (what fd_verify_tile's during_frag /
+   after_frag pair needs, with fd_txn_parse moved onto the GPU):
+   submit_raw copies one raw payload (no host parse); poll_raw returns,
+   in submission order, the tag, the code (FDGPU_ERR_PARSE or the batch
+   verify code), and, when out_img / out_fp are non-NULL, the parser's
+   fd_txn_t image (out_img + i*FDGPU_TXN_IMG_STRIDE, footprint bytes) and
+   footprint.  A slot holds one kind of submission; switching kinds
+   flushes.  Returns as fdgpu_ed25519_submit / fdgpu_ed25519_poll. */
+int
+fdgpu_ed25519_submit_raw( fdgpu_ed25519_ctx_t * ctx,
+                          unsigned char const * payload,
+                          unsigned short        payload_sz,
+                          unsigned long         tag );
+
+unsigned long
+fdgpu_ed25519_poll_raw( fdgpu_ed25519_ctx_t * ctx,
+                        unsigned long *       out_tags,
+                        signed char *         out_codes,
+                        unsigned char *       out_img,
+                        unsigned short *      out_fp,
+                        unsigned long         max,
+                        int                   blocking );
+
 /* Per-kernel timing, in milliseconds: the mean over the batches launched
    since fdgpu_ed25519_set_timing(ctx,1) (at most the last 64) of HIP
    events recorded on the stream the kernels ran on.  idx: 0 = prep

@@ -141,3 +141,37 @@ def test_verify_raw_device_full_size(oracle):
     want[bad[0::2]] = engine.FDGPU_ERR_PARSE
     want[bad[1::2]] = -3
     np.testing.assert_array_equal(out, want)
+
+
+def test_async_raw_submit_poll(oracle):
+    """submit_raw / poll_raw: in-order completions, codes and fd_txn_t images match the oracle,
+    with several slots in flight and mixed desc / raw submissions."""
+    from firedancer_amd import Engine
+    cases = _raw_cases()
+    arena, off, sz = tb.pack(cases)
+    want, wfp, wimg = raw_expect.expected_codes(oracle, arena, off, sz)
+    eng = Engine(device=0, max_txn=300, max_sig=300 * 16, max_payload=300 * 1240)
+    got_t, got_c, got_fp, got_img = [], [], [], []
+    pending = 0
+    for i, c in enumerate(cases):
+        while True:
+            rc = eng.submit_raw(c, 1000 + i)
+            if rc != -2:
+                break
+            t, cd, fp, im = eng.poll_raw(256, blocking=True)
+            got_t.append(t); got_c.append(cd); got_fp.append(fp); got_img.append(im)
+        assert rc == 0
+        if i % 97 == 0:
+            t, cd, fp, im = eng.poll_raw(64)
+            got_t.append(t); got_c.append(cd); got_fp.append(fp); got_img.append(im)
+    eng.flush()
+    while sum(len(t) for t in got_t) < len(cases):
+        t, cd, fp, im = eng.poll_raw(512, blocking=True)
+        got_t.append(t); got_c.append(cd); got_fp.append(fp); got_img.append(im)
+    eng.close()
+    tags = np.concatenate(got_t); codes = np.concatenate(got_c); fps = np.concatenate(got_fp)
+    imgs = np.concatenate(got_img)
+    np.testing.assert_array_equal(tags, 1000 + np.arange(len(cases)))
+    np.testing.assert_array_equal(codes, want)
+    np.testing.assert_array_equal(fps, wfp)
+    np.testing.assert_array_equal(crcs(fps, imgs), crcs(wfp, wimg))
