@@ -41,9 +41,21 @@ def build_synth(force: bool = False) -> str:
     return out
 
 
+def build_vtile(force: bool = False) -> str:
+    """libfdgpu_vtile.so: the verify tile over the engine (host C, links libfdgpu_ed25519.so)."""
+    out = os.path.join(PKG, "libfdgpu_vtile.so")
+    eng = os.path.join(PKG, "libfdgpu_ed25519.so")
+    if force or _stale(out, ["fd_verify_gpu.c", "../../include/fd_verify_gpu.h", "../../include/fd_ed25519_gpu.h"]) \
+            or os.path.getmtime(eng) > os.path.getmtime(out):
+        subprocess.run(["gcc", "-std=gnu11", "-O2", "-fPIC", "-shared", "-pthread", "-Wall", "-Wextra",
+                        "-o", out, os.path.join(CSRC, "fd_verify_gpu.c"), eng, "-Wl,-rpath,$ORIGIN"], check=True)
+    return out
+
+
 def build_all(force: bool = False) -> None:
     build_synth(force)
     build_engine(force)
+    build_vtile(force)
 
 
 if __name__ == "__main__":

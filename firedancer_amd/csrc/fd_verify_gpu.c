@@ -1,0 +1,510 @@
+/* fd_verify_gpu.c -- the verify tile's frag callbacks over the GPU engine,
+   a minimal tango (mcache / dcache / tcache) and the streaming benchmark.
+   Host C; see include/fd_verify_gpu.h for the contract and the reference
+   lines each part replaces. */
+
+#define _GNU_SOURCE
+#include "../../include/fd_verify_gpu.h"
+#include "../../include/fd_ed25519_gpu.h"
+
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+typedef unsigned long ulong;
+typedef unsigned char uchar;
+
+static ulong now_ns( void ) {
+  struct timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (ulong)ts.tv_sec * 1000000000UL + (ulong)ts.tv_nsec;
+}
+
+static ulong pow2_up( ulong x ) { ulong p = 1UL; while( p < x ) p <<= 1; return p; }
+
+/* ---- dedup tag: XXH64 of the first signature -----------------------
+   fd_txn_verify tags a transaction with fd_hash( seed, sig0, 64 )
+   (src/disco/verify/fd_verify_tile.h:79); fd_hash is XXH64 (r39), so
+   this is the published XXH64 algorithm specialised to 64-byte input. */
+
+#define P1 0x9E3779B185EBCA87UL
+#define P2 0xC2B2AE3D27D4EB4FUL
+#define P3 0x165667B19E3779F9UL
+#define P4 0x85EBCA77C2B2AE63UL
+#define P5 0x27D4EB2F165667C5UL
+
+static ulong rotl64( ulong x, int r ) { return (x << r) | (x >> (64 - r)); }
+static ulong ld64( uchar const * p ) { ulong x; memcpy( &x, p, 8 ); return x; }
+static ulong xxh_round( ulong acc, ulong in ) { acc += in * P2; acc = rotl64( acc, 31 ); return acc * P1; }
+
+static ulong
+xxh64_64( ulong seed, uchar const * p ) {
+  ulong v[4] = { seed + P1 + P2, seed + P2, seed, seed - P1 };
+  for( int blk=0; blk<2; blk++ )
+    for( int i=0; i<4; i++ ) v[i] = xxh_round( v[i], ld64( p + 32*blk + 8*i ) );
+  ulong h = rotl64( v[0], 1 ) + rotl64( v[1], 7 ) + rotl64( v[2], 12 ) + rotl64( v[3], 18 );
+  for( int i=0; i<4; i++ ) { h ^= xxh_round( 0UL, v[i] ); h = h * P1 + P4; }
+  h += 64UL;
+  h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+  return h;
+}
+
+ulong fdgpu_dedup_tag( ulong seed, uchar const sig[ 64 ] ) { return xxh64_64( seed, sig ); }
+
+/* ---- tcache ----------------------------------------------------------
+   Semantics of FD_TCACHE_QUERY / FD_TCACHE_INSERT (src/tango/tcache/
+   fd_tcache.h:281-404): a ring of the last depth unique tags plus an
+   open-addressed (linear probe) map; inserting a new tag evicts the
+   oldest.  Tag 0 is the null tag (a query for it always "finds" it). */
+
+struct fdgpu_tcache {
+  ulong depth, map_cnt, oldest;
+  ulong * ring;
+  ulong * map;
+};
+
+static ulong tc_slot( ulong tag, ulong map_cnt ) { return (tag * P1 >> 17) & (map_cnt - 1UL); }
+
+fdgpu_tcache_t *
+fdgpu_tcache_new( ulong depth ) {
+  if( !depth ) return NULL;
+  fdgpu_tcache_t * tc = (fdgpu_tcache_t *)calloc( 1, sizeof(fdgpu_tcache_t) );
+  if( !tc ) return NULL;
+  tc->depth = depth; tc->map_cnt = pow2_up( 2UL*depth + 2UL ); tc->oldest = 0UL;
+  tc->ring = (ulong *)calloc( depth, sizeof(ulong) );
+  tc->map  = (ulong *)calloc( tc->map_cnt, sizeof(ulong) );
+  if( !tc->ring || !tc->map ) { free( tc->ring ); free( tc->map ); free( tc ); return NULL; }
+  return tc;
+}
+
+void fdgpu_tcache_delete( fdgpu_tcache_t * tc ) { if( tc ) { free( tc->ring ); free( tc->map ); free( tc ); } }
+
+static int tc_find( fdgpu_tcache_t const * tc, ulong tag, ulong * idx ) {
+  ulong i = tc_slot( tag, tc->map_cnt );
+  for( ;; ) {
+    ulong m = tc->map[i];
+    if( m==tag ) { *idx = i; return 1; }
+    if( !m )     { *idx = i; return 0; }
+    i = (i + 1UL) & (tc->map_cnt - 1UL);
+  }
+}
+
+int fdgpu_tcache_query( fdgpu_tcache_t const * tc, ulong tag ) {
+  if( !tag ) return 1;
+  ulong i; return tc_find( tc, tag, &i );
+}
+
+/* delete map slot i keeping every probe chain intact (backward shift) */
+static void tc_map_remove( fdgpu_tcache_t * tc, ulong i ) {
+  ulong mask = tc->map_cnt - 1UL;
+  ulong j = i;
+  for( ;; ) {
+    j = (j + 1UL) & mask;
+    ulong t = tc->map[j];
+    if( !t ) break;
+    ulong home = tc_slot( t, tc->map_cnt );
+    /* move t into the hole at i unless its home lies cyclically in (i, j] */
+    int stay = ( i <= j ) ? ( home > i && home <= j ) : ( home > i || home <= j );
+    if( !stay ) { tc->map[i] = t; i = j; }
+  }
+  tc->map[i] = 0UL;
+}
+
+int fdgpu_tcache_insert( fdgpu_tcache_t * tc, ulong tag ) {
+  if( !tag ) return 1;
+  ulong i;
+  if( tc_find( tc, tag, &i ) ) return 1;
+  tc->map[i] = tag;
+  ulong old = tc->ring[ tc->oldest ];
+  tc->ring[ tc->oldest ] = tag;
+  tc->oldest = ( tc->oldest + 1UL == tc->depth ) ? 0UL : tc->oldest + 1UL;
+  if( old && tc_find( tc, old, &i ) ) tc_map_remove( tc, i );
+  return 0;
+}
+
+/* ---- mcache / dcache -------------------------------------------------
+   An mcache is a ring of frag metadata indexed by seq & (depth-1); the
+   producer writes the entry and then its seq (release); a consumer
+   waiting for seq reads the entry between two acquire loads of its seq
+   field and classifies: equal = ready, behind = not yet published,
+   ahead = overrun (src/tango/mcache/fd_mcache.h:288-325 semantics). */
+
+typedef struct {
+  _Atomic ulong     seq;
+  fdgpu_frag_meta_t m;
+} mc_line_t;
+
+struct fdgpu_mcache {
+  ulong       depth;
+  mc_line_t * line;
+};
+
+fdgpu_mcache_t *
+fdgpu_mcache_new( ulong depth, ulong seq0 ) {
+  if( !depth || (depth & (depth - 1UL)) ) return NULL;
+  fdgpu_mcache_t * mc = (fdgpu_mcache_t *)calloc( 1, sizeof(fdgpu_mcache_t) );
+  if( !mc ) return NULL;
+  mc->depth = depth;
+  mc->line = (mc_line_t *)aligned_alloc( 64, depth * sizeof(mc_line_t) + 64 );
+  if( !mc->line ) { free( mc ); return NULL; }
+  memset( mc->line, 0, depth * sizeof(mc_line_t) );
+  /* every line starts "one lap behind" so seq0.. read as not yet published */
+  for( ulong i=0; i<depth; i++ ) atomic_store_explicit( &mc->line[i].seq, seq0 + i - depth, memory_order_relaxed );
+  return mc;
+}
+
+void fdgpu_mcache_delete( fdgpu_mcache_t * mc ) { if( mc ) { free( mc->line ); free( mc ); } }
+
+void
+fdgpu_mcache_publish( fdgpu_mcache_t * mc, ulong seq, ulong sig, unsigned chunk, unsigned sz, ulong tsorig, ulong tspub ) {
+  mc_line_t * l = &mc->line[ seq & (mc->depth - 1UL) ];
+  atomic_store_explicit( &l->seq, seq - 1UL, memory_order_relaxed );   /* mark in-progress */
+  atomic_thread_fence( memory_order_release );
+  l->m.seq = seq; l->m.sig = sig; l->m.chunk = chunk; l->m.sz = sz; l->m.tsorig = tsorig; l->m.tspub = tspub;
+  atomic_store_explicit( &l->seq, seq, memory_order_release );
+}
+
+int
+fdgpu_mcache_poll( fdgpu_mcache_t const * mc, ulong seq, fdgpu_frag_meta_t * out ) {
+  mc_line_t const * l = &mc->line[ seq & (mc->depth - 1UL) ];
+  ulong s0 = atomic_load_explicit( (_Atomic ulong *)&l->seq, memory_order_acquire );
+  if( (long)(s0 - seq) < 0 ) return 1;
+  if( s0 != seq ) return -1;
+  fdgpu_frag_meta_t m = l->m;
+  atomic_thread_fence( memory_order_acquire );
+  ulong s1 = atomic_load_explicit( (_Atomic ulong *)&l->seq, memory_order_relaxed );
+  if( s1 != seq ) return -1;
+  *out = m;
+  return 0;
+}
+
+/* fd_dcache_compact_next (src/tango/dcache/fd_dcache.h:263-269): advance
+   by whole 128-byte chunk pairs, wrap to chunk0 past wmark */
+ulong
+fdgpu_dcache_compact_next( ulong chunk, ulong sz, ulong chunk0, ulong wmark ) {
+  chunk += ( ( sz + 2UL*FDGPU_CHUNK_SZ - 1UL ) >> 7 ) << 1;
+  return chunk > wmark ? chunk0 : chunk;
+}
+
+/* ---- the verify tile ------------------------------------------------ */
+
+#define VT_RESERVE_MAX ( FDGPU_TXNM_HDR_SZ + 1232UL + 2UL + 852UL )   /* header + MTU payload + fd_txn_t */
+
+typedef struct {
+  ulong seq, tsorig, chunk;
+} vt_pend_t;
+
+struct fdgpu_vtile {
+  fdgpu_ed25519_ctx_t * ctx;
+  fdgpu_tcache_t *      tcache;
+  ulong                 seed;
+  uchar *               dcache;
+  ulong                 chunk0, wmark, out_chunk;
+  vt_pend_t *           pend;            /* FIFO of frags between during_frag and after_frags */
+  ulong                 pend_cap, pend_head, pend_tail;   /* monotonic counters */
+  int                   bundle_failed;
+  ulong                 bundle_id;
+  ulong                 metrics[5];
+  /* poll scratch */
+  ulong                 batch;
+  ulong *               p_tags;
+  signed char *         p_codes;
+  uchar *               p_img;
+  unsigned short *      p_fp;
+};
+
+fdgpu_vtile_t *
+fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ulong out_dcache_bytes, int semantics ) {
+  if( !batch_txn || !tcache_depth || out_dcache_bytes < 8UL*VT_RESERVE_MAX ) return NULL;
+  fdgpu_vtile_t * vt = (fdgpu_vtile_t *)calloc( 1, sizeof(fdgpu_vtile_t) );
+  if( !vt ) return NULL;
+  vt->ctx = fdgpu_ed25519_ctx_new( device, batch_txn, 16UL*batch_txn, batch_txn*(1232UL+8UL), semantics );
+  vt->tcache = fdgpu_tcache_new( tcache_depth );
+  ulong nchunk = ( out_dcache_bytes / FDGPU_CHUNK_SZ ) & ~1UL;
+  vt->dcache = (uchar *)aligned_alloc( 128, nchunk * FDGPU_CHUNK_SZ );
+  ulong rchunk = ( ( VT_RESERVE_MAX + 127UL ) >> 7 ) << 1;
+  vt->chunk0 = 0UL; vt->wmark = nchunk - rchunk; vt->out_chunk = 0UL;
+  /* frags in flight: the ring must hold them all plus one wrap's waste */
+  vt->pend_cap = nchunk / rchunk - 2UL;
+  vt->pend = (vt_pend_t *)calloc( vt->pend_cap, sizeof(vt_pend_t) );
+  vt->seed = seed;
+  vt->batch = batch_txn;
+  vt->p_tags = (ulong *)malloc( batch_txn * sizeof(ulong) );
+  vt->p_codes = (signed char *)malloc( batch_txn );
+  vt->p_img = (uchar *)malloc( batch_txn * FDGPU_TXN_IMG_STRIDE );
+  vt->p_fp = (unsigned short *)malloc( batch_txn * sizeof(unsigned short) );
+  if( !vt->ctx || !vt->tcache || !vt->dcache || !vt->pend || !vt->p_tags || !vt->p_codes || !vt->p_img || !vt->p_fp ) {
+    fdgpu_vtile_delete( vt );
+    return NULL;
+  }
+  return vt;
+}
+
+void
+fdgpu_vtile_delete( fdgpu_vtile_t * vt ) {
+  if( !vt ) return;
+  if( vt->ctx ) fdgpu_ed25519_ctx_delete( vt->ctx );
+  fdgpu_tcache_delete( vt->tcache );
+  free( vt->dcache ); free( vt->pend ); free( vt->p_tags ); free( vt->p_codes ); free( vt->p_img ); free( vt->p_fp );
+  free( vt );
+}
+
+uchar * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt ) { return vt->dcache; }
+ulong   fdgpu_vtile_pending( fdgpu_vtile_t const * vt ) { return vt->pend_tail - vt->pend_head; }
+void    fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, ulong out[ 5 ] ) { memcpy( out, vt->metrics, sizeof(vt->metrics) ); }
+int     fdgpu_vtile_flush( fdgpu_vtile_t * vt ) { return fdgpu_ed25519_flush( vt->ctx ); }
+
+int
+fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
+  fdgpu_txnm_t const * in = (fdgpu_txnm_t const *)frag;
+  /* fd_verify_tile.c:78-85: the frag must hold its header + payload and
+     the payload must fit the MTU (the reference FD_LOG_ERRs) */
+  if( sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U || FDGPU_TXNM_HDR_SZ + in->payload_sz > sz ) return -4;
+  if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_ed25519_flush( vt->ctx ); return -2; }
+  uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
+  memcpy( dst, frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
+  int rc = fdgpu_ed25519_submit_raw( vt->ctx, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
+  if( rc ) return rc;
+  vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
+  p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk;
+  vt->pend_tail++;
+  ulong reserve = ( ( FDGPU_TXNM_HDR_SZ + in->payload_sz + 1UL ) & ~1UL ) + 852UL;
+  vt->out_chunk = fdgpu_dcache_compact_next( vt->out_chunk, reserve, vt->chunk0, vt->wmark );
+  return 0;
+}
+
+/* after_frag (fd_verify_tile.c:103-157) for one completed frag */
+static int
+vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, unsigned fp, fdgpu_vtile_done_t * d ) {
+  fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( vt->dcache + p->chunk * FDGPU_CHUNK_SZ );
+  uchar * payload = (uchar *)txnm + FDGPU_TXNM_HDR_SZ;
+  txnm->txn_t_sz = (unsigned short)fp;
+  d->seq = p->seq; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
+  int is_bundle = txnm->bundle_id != 0UL;
+  if( is_bundle && txnm->bundle_id != vt->bundle_id ) { vt->bundle_failed = 0; vt->bundle_id = txnm->bundle_id; }
+  if( is_bundle && vt->bundle_failed ) { vt->metrics[3]++; return FDGPU_VTILE_BUNDLE_PEER_FAIL; }
+  if( code == FDGPU_ERR_PARSE ) {
+    if( is_bundle ) vt->bundle_failed = 1;
+    vt->metrics[0]++;
+    return FDGPU_VTILE_PARSE_FAIL;
+  }
+  /* fd_txn_verify (fd_verify_tile.h:59-108): dedup query, verify, insert */
+  unsigned sig_off = (unsigned)img[2] | ((unsigned)img[3] << 8);
+  ulong tag = xxh64_64( vt->seed, payload + sig_off );
+  int res = 0;   /* 0 success, 1 verify failed, 2 dedup */
+  if( !is_bundle && fdgpu_tcache_query( vt->tcache, tag ) ) res = 2;
+  else if( code != 0 ) res = 1;
+  else if( !is_bundle && fdgpu_tcache_insert( vt->tcache, tag ) ) res = 2;
+  if( res ) {
+    if( is_bundle ) vt->bundle_failed = 1;
+    if( res==2 ) { vt->metrics[2]++; return FDGPU_VTILE_DEDUP_FAIL; }
+    vt->metrics[1]++;
+    return FDGPU_VTILE_VERIFY_FAIL;
+  }
+  /* publish: fd_txn_t behind the payload at a 2-byte boundary */
+  ulong t_off = ( FDGPU_TXNM_HDR_SZ + txnm->payload_sz + 1UL ) & ~1UL;
+  memcpy( (uchar *)txnm + t_off, img, fp );
+  d->sz = t_off + fp;                                  /* fd_txn_m_realized_footprint( txnm, 1, 0 ) */
+  d->tag = is_bundle ? 0UL : tag;
+  vt->metrics[4]++;
+  return FDGPU_VTILE_PUBLISH;
+}
+
+ulong
+fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max, int blocking ) {
+  ulong n = 0UL;
+  if( blocking ) fdgpu_ed25519_flush( vt->ctx );   /* a blocking drain must not wait on an unlaunched batch */
+  while( n < max && vt->pend_head < vt->pend_tail ) {
+    ulong want = max - n;
+    if( want > vt->batch ) want = vt->batch;
+    ulong k = fdgpu_ed25519_poll_raw( vt->ctx, vt->p_tags, vt->p_codes, vt->p_img, vt->p_fp, want, blocking );
+    if( !k ) break;
+    for( ulong i=0; i<k; i++ ) {
+      vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
+      /* tags are the pending counter: completions come back in order */
+      out[n].result = vt_after( vt, p, (int)vt->p_codes[i], vt->p_img + i*FDGPU_TXN_IMG_STRIDE, vt->p_fp[i], &out[n] );
+      vt->pend_head++; n++;
+    }
+    blocking = 0;
+  }
+  return n;
+}
+
+/* ---- streaming benchmark -------------------------------------------- */
+
+typedef struct {
+  /* shared */
+  fdgpu_mcache_t *       mc;
+  uchar *                in_dcache;
+  ulong                  in_chunk0, in_wmark;
+  ulong                  n_frags;
+  int                    tiles;
+  _Atomic ulong *        fseq;        /* per tile: next seq it has yet to consume (credit return) */
+  _Atomic int            go, fail, ready;
+  float *                lat_us;      /* per frag */
+  unsigned char const *  payload; unsigned int const * off; unsigned short const * sz; ulong n_payload;
+  double                 rate_fps;
+  ulong                  depth;
+  ulong                  t_start, t_end;
+  _Atomic ulong          t_last;
+  _Atomic ulong          sigs, published, overruns;
+  ulong                  metrics[5];
+  pthread_mutex_t        mu;
+  int                    device; ulong batch_txn;
+} sb_t;
+
+static void * sb_producer( void * _s ) {
+  sb_t * s = (sb_t *)_s;
+  while( !atomic_load( &s->go ) ) ;
+  ulong chunk = s->in_chunk0;
+  ulong t0 = now_ns();
+  s->t_start = t0;
+  for( ulong seq=0; seq<s->n_frags; seq++ ) {
+    if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) break;
+    /* reliable link: wait for credits (every tile within depth/2 of seq) */
+    for( ;; ) {
+      ulong lo = ~0UL;
+      for( int t=0; t<s->tiles; t++ ) { ulong f = atomic_load_explicit( &s->fseq[t], memory_order_acquire ); if( f < lo ) lo = f; }
+      if( seq - lo < s->depth/2 ) break;
+      if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) return NULL;
+    }
+    if( s->rate_fps > 0. ) {
+      ulong due = t0 + (ulong)( (double)seq * 1e9 / s->rate_fps );
+      while( now_ns() < due ) ;
+    }
+    ulong p = seq % s->n_payload;
+    fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( s->in_dcache + chunk * FDGPU_CHUNK_SZ );
+    memset( txnm, 0, FDGPU_TXNM_HDR_SZ );
+    txnm->payload_sz = s->sz[p];
+    memcpy( (uchar *)txnm + FDGPU_TXNM_HDR_SZ, s->payload + s->off[p], s->sz[p] );
+    ulong fsz = FDGPU_TXNM_HDR_SZ + s->sz[p];
+    ulong ts = now_ns();
+    fdgpu_mcache_publish( s->mc, seq, 0UL, (unsigned)chunk, (unsigned)fsz, ts, ts );
+    chunk = fdgpu_dcache_compact_next( chunk, fsz, s->in_chunk0, s->in_wmark );
+  }
+  return NULL;
+}
+
+typedef struct { sb_t * s; int idx; } sb_tile_arg_t;
+
+static void sb_account( sb_t * s, fdgpu_vtile_t * vt, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs ) {
+  ulong t = now_ns();
+  for( ulong i=0; i<n; i++ ) {
+    ulong lat = t - d[i].tsorig;
+    s->lat_us[ d[i].seq ] = (float)( (double)lat * 1e-3 );
+    if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL ) {
+      uchar const * pl = fdgpu_vtile_out_dcache( vt ) + d[i].chunk * FDGPU_CHUNK_SZ + FDGPU_TXNM_HDR_SZ;
+      *sigs += pl[0];
+    }
+  }
+  if( n ) {
+    ulong prev = atomic_load( &s->t_last );
+    while( t > prev && !atomic_compare_exchange_weak( &s->t_last, &prev, t ) ) ;
+  }
+}
+
+static void * sb_tile( void * _a ) {
+  sb_tile_arg_t * a = (sb_tile_arg_t *)_a;
+  sb_t * s = a->s;
+  int idx = a->idx;
+  fdgpu_vtile_t * vt = fdgpu_vtile_new( s->device, s->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
+                                        ( 6UL*s->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
+  if( !vt ) { atomic_store( &s->fail, 1 ); return NULL; }
+  atomic_fetch_add( &s->ready, 1 );              /* the producer starts once every tile has its GPU context */
+  ulong dcap = 4096UL;
+  fdgpu_vtile_done_t * done = (fdgpu_vtile_done_t *)malloc( dcap * sizeof(fdgpu_vtile_done_t) );
+  ulong sigs = 0UL, mine = 0UL, got = 0UL;
+  for( ulong seq=0; seq<s->n_frags; ) mine += ( seq++ % (ulong)s->tiles ) == (ulong)idx;
+  ulong seq = 0UL;
+  int idle = 0;
+  while( got < mine ) {
+    if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) break;
+    int progressed = 0;
+    if( seq < s->n_frags ) {
+      fdgpu_frag_meta_t m;
+      int r = fdgpu_mcache_poll( s->mc, seq, &m );
+      if( r == 0 ) {
+        if( (seq % (ulong)s->tiles) == (ulong)idx ) {            /* before_frag round robin */
+          int rc = fdgpu_vtile_during_frag( vt, s->in_dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, seq, m.tsorig );
+          if( rc == -2 ) {                                          /* staging full: drain, retry this seq */
+            ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
+            sb_account( s, vt, done, n, &sigs ); got += n;
+            continue;
+          }
+          if( rc ) { atomic_store( &s->fail, 2 ); break; }
+        }
+        seq++;
+        atomic_store_explicit( &s->fseq[idx], seq, memory_order_release );
+        progressed = 1; idle = 0;
+      } else if( r < 0 ) {
+        atomic_fetch_add( &s->overruns, 1 ); atomic_store( &s->fail, 3 ); break;
+      }
+    }
+    if( !progressed ) {
+      if( ++idle == 64 ) fdgpu_vtile_flush( vt );                    /* input idle: launch the partial batch */
+    }
+    if( !progressed || (seq & 255UL) == 0 ) {
+      ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
+      sb_account( s, vt, done, n, &sigs ); got += n;
+    }
+  }
+  ulong m5[5]; fdgpu_vtile_metrics( vt, m5 );
+  pthread_mutex_lock( &s->mu );
+  for( int i=0; i<5; i++ ) s->metrics[i] += m5[i];
+  pthread_mutex_unlock( &s->mu );
+  atomic_fetch_add( &s->sigs, sigs );
+  free( done );
+  fdgpu_vtile_delete( vt );
+  return NULL;
+}
+
+static int cmp_f( void const * a, void const * b ) {
+  float x = *(float const *)a, y = *(float const *)b;
+  return x < y ? -1 : x > y ? 1 : 0;
+}
+
+int
+fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, unsigned short const * sz, ulong n_payload,
+                    ulong n_frags, int tiles, ulong batch_txn, ulong mcache_depth, double rate_fps,
+                    fdgpu_stream_stats_t * st ) {
+  if( tiles < 1 || tiles > 64 || !n_frags || !n_payload || !batch_txn || mcache_depth < 64 ) return -1;
+  sb_t * s = (sb_t *)calloc( 1, sizeof(sb_t) );
+  s->depth = pow2_up( mcache_depth );
+  s->mc = fdgpu_mcache_new( s->depth, 0UL );
+  ulong in_bytes = s->depth * 2UL * 1408UL;
+  s->in_dcache = (uchar *)aligned_alloc( 128, in_bytes );
+  s->in_chunk0 = 0UL; s->in_wmark = in_bytes / FDGPU_CHUNK_SZ - 24UL;
+  s->n_frags = n_frags; s->tiles = tiles;
+  s->fseq = (_Atomic ulong *)calloc( (size_t)tiles, sizeof(_Atomic ulong) );
+  s->lat_us = (float *)calloc( n_frags, sizeof(float) );
+  s->payload = payload; s->off = off; s->sz = sz; s->n_payload = n_payload; s->rate_fps = rate_fps;
+  s->device = device; s->batch_txn = batch_txn;
+  pthread_mutex_init( &s->mu, NULL );
+  pthread_t prod, th[64]; sb_tile_arg_t args[64];
+  for( int t=0; t<tiles; t++ ) { args[t].s = s; args[t].idx = t; pthread_create( &th[t], NULL, sb_tile, &args[t] ); }
+  pthread_create( &prod, NULL, sb_producer, s );
+  while( atomic_load( &s->ready ) < tiles && !atomic_load( &s->fail ) ) ;
+  atomic_store( &s->go, 1 );
+  pthread_join( prod, NULL );
+  for( int t=0; t<tiles; t++ ) pthread_join( th[t], NULL );
+  int rc = atomic_load( &s->fail );
+  memset( st, 0, sizeof(*st) );
+  if( !rc ) {
+    st->seconds = (double)( atomic_load( &s->t_last ) - s->t_start ) * 1e-9;
+    st->frags = n_frags; st->sigs = atomic_load( &s->sigs ); st->published = s->metrics[4];
+    st->frags_per_s = (double)n_frags / st->seconds;
+    st->sigs_per_s = (double)st->sigs / st->seconds;
+    qsort( s->lat_us, n_frags, sizeof(float), cmp_f );
+    st->lat_p50_us = s->lat_us[ n_frags/2 ];
+    st->lat_p99_us = s->lat_us[ (n_frags*99UL)/100UL ];
+    st->lat_max_us = s->lat_us[ n_frags-1UL ];
+    memcpy( st->metrics, s->metrics, sizeof(st->metrics) );
+    st->overruns = atomic_load( &s->overruns );
+  }
+  fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( (void *)s->fseq ); free( s->lat_us );
+  pthread_mutex_destroy( &s->mu );
+  free( s );
+  return rc ? -rc - 10 : 0;
+}

@@ -1,0 +1,182 @@
+"""ctypes mirror of include/fd_verify_gpu.h (libfdgpu_vtile.so): the GPU
+verify tile's frag callbacks, its tcache / mcache / dcache pieces, and
+the streaming benchmark.  No CPU fallback: the tile needs the engine and
+a GPU; the tango pieces (tcache, mcache, dedup tag) are host-only."""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from .engine import PKG_DIR, load_library as load_engine
+
+LIB_PATH = os.path.join(PKG_DIR, "libfdgpu_vtile.so")
+TXNM_HDR_SZ = 80
+CHUNK_SZ = 64
+PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL = range(5)
+
+EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
+           "fdgpu_mcache_new", "fdgpu_mcache_delete", "fdgpu_mcache_publish", "fdgpu_mcache_poll",
+           "fdgpu_dcache_compact_next", "fdgpu_vtile_new", "fdgpu_vtile_delete", "fdgpu_vtile_out_dcache",
+           "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
+           "fdgpu_vtile_metrics", "fdgpu_stream_bench")
+
+TXNM_DTYPE = np.dtype([("reference_slot", "<u8"), ("payload_sz", "<u2"), ("txn_t_sz", "<u2"), ("source_ipv4", "<u4"),
+                       ("source_tpu", "u1"), ("_pad0", "u1", (7,)), ("bundle_id", "<u8"), ("bundle_txn_cnt", "<u8"),
+                       ("commission", "u1"), ("commission_pubkey", "u1", (32,)), ("_pad1", "u1", (7,))])
+assert TXNM_DTYPE.itemsize == TXNM_HDR_SZ
+
+
+class FragMeta(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_ulong), ("sig", ctypes.c_ulong), ("chunk", ctypes.c_uint), ("sz", ctypes.c_uint),
+                ("tsorig", ctypes.c_ulong), ("tspub", ctypes.c_ulong)]
+
+
+class Done(ctypes.Structure):
+    _fields_ = [("seq", ctypes.c_ulong), ("tsorig", ctypes.c_ulong), ("chunk", ctypes.c_ulong), ("sz", ctypes.c_ulong),
+                ("tag", ctypes.c_ulong), ("result", ctypes.c_int)]
+
+
+class StreamStats(ctypes.Structure):
+    _fields_ = [("seconds", ctypes.c_double), ("frags", ctypes.c_ulong), ("sigs", ctypes.c_ulong),
+                ("published", ctypes.c_ulong), ("frags_per_s", ctypes.c_double), ("sigs_per_s", ctypes.c_double),
+                ("lat_p50_us", ctypes.c_double), ("lat_p99_us", ctypes.c_double), ("lat_max_us", ctypes.c_double),
+                ("metrics", ctypes.c_ulong * 5), ("overruns", ctypes.c_ulong)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run __graft_entry__.build()")
+        load_engine()
+        L = ctypes.CDLL(LIB_PATH)
+        vp, ul = ctypes.c_void_p, ctypes.c_ulong
+        L.fdgpu_dedup_tag.restype = ul
+        L.fdgpu_dedup_tag.argtypes = [ul, vp]
+        L.fdgpu_tcache_new.restype = vp
+        L.fdgpu_tcache_new.argtypes = [ul]
+        L.fdgpu_tcache_delete.argtypes = [vp]
+        L.fdgpu_tcache_query.argtypes = [vp, ul]
+        L.fdgpu_tcache_insert.argtypes = [vp, ul]
+        L.fdgpu_mcache_new.restype = vp
+        L.fdgpu_mcache_new.argtypes = [ul, ul]
+        L.fdgpu_mcache_delete.argtypes = [vp]
+        L.fdgpu_mcache_publish.argtypes = [vp, ul, ul, ctypes.c_uint, ctypes.c_uint, ul, ul]
+        L.fdgpu_mcache_poll.argtypes = [vp, ul, ctypes.POINTER(FragMeta)]
+        L.fdgpu_dcache_compact_next.restype = ul
+        L.fdgpu_dcache_compact_next.argtypes = [ul, ul, ul, ul]
+        L.fdgpu_vtile_new.restype = vp
+        L.fdgpu_vtile_new.argtypes = [ctypes.c_int, ul, ul, ul, ul, ctypes.c_int]
+        L.fdgpu_vtile_delete.argtypes = [vp]
+        L.fdgpu_vtile_out_dcache.restype = vp
+        L.fdgpu_vtile_out_dcache.argtypes = [vp]
+        L.fdgpu_vtile_during_frag.argtypes = [vp, vp, ul, ul, ul]
+        L.fdgpu_vtile_flush.argtypes = [vp]
+        L.fdgpu_vtile_after_frags.restype = ul
+        L.fdgpu_vtile_after_frags.argtypes = [vp, ctypes.POINTER(Done), ul, ctypes.c_int]
+        L.fdgpu_vtile_pending.restype = ul
+        L.fdgpu_vtile_pending.argtypes = [vp]
+        L.fdgpu_vtile_metrics.argtypes = [vp, ctypes.POINTER(ctypes.c_ulong)]
+        L.fdgpu_stream_bench.argtypes = [ctypes.c_int, vp, vp, vp, ul, ul, ctypes.c_int, ul, ul, ctypes.c_double,
+                                         ctypes.POINTER(StreamStats)]
+        _lib = L
+    return _lib
+
+
+def dedup_tag(seed: int, sig: bytes) -> int:
+    b = np.frombuffer(bytes(sig[:64]).ljust(64, b"\0"), np.uint8)
+    return int(load().fdgpu_dedup_tag(seed, b.ctypes.data))
+
+
+class TCache:
+    def __init__(self, depth: int):
+        self.L = load()
+        self.p = self.L.fdgpu_tcache_new(depth)
+
+    def query(self, tag: int) -> bool:
+        return bool(self.L.fdgpu_tcache_query(self.p, tag))
+
+    def insert(self, tag: int) -> bool:
+        return bool(self.L.fdgpu_tcache_insert(self.p, tag))
+
+    def __del__(self):
+        if getattr(self, "p", None):
+            self.L.fdgpu_tcache_delete(self.p)
+            self.p = None
+
+
+def frag_bytes(payload: bytes, bundle_id: int = 0) -> bytes:
+    h = np.zeros(1, TXNM_DTYPE)
+    h["payload_sz"] = len(payload)
+    h["bundle_id"] = bundle_id
+    return h.tobytes() + bytes(payload)
+
+
+class VTile:
+    """One GPU verify tile (fdgpu_vtile_t)."""
+
+    def __init__(self, device: int = 0, batch_txn: int = 1024, tcache_depth: int = 1 << 16, seed: int = 0x5eed,
+                 out_dcache_bytes: int | None = None, semantics: int = 0):
+        self.L = load()
+        out_dcache_bytes = out_dcache_bytes or (6 * batch_txn + 64) * 2304
+        self.p = self.L.fdgpu_vtile_new(device, batch_txn, tcache_depth, seed, out_dcache_bytes, semantics)
+        if not self.p:
+            raise RuntimeError("fdgpu_vtile_new failed: " + load_engine().fdgpu_last_error().decode())
+        self.seed = seed
+        self.dcache = self.L.fdgpu_vtile_out_dcache(self.p)
+
+    def during_frag(self, frag: bytes, seq: int, tsorig: int = 0) -> int:
+        b = np.frombuffer(frag, np.uint8)
+        return self.L.fdgpu_vtile_during_frag(self.p, b.ctypes.data, len(frag), seq, tsorig)
+
+    def flush(self):
+        return self.L.fdgpu_vtile_flush(self.p)
+
+    def after_frags(self, max_n: int = 4096, blocking: bool = False):
+        out = (Done * max_n)()
+        n = self.L.fdgpu_vtile_after_frags(self.p, out, max_n, 1 if blocking else 0)
+        return [(d.seq, d.result, d.chunk, d.sz, d.tag) for d in out[:n]]
+
+    def pending(self) -> int:
+        return int(self.L.fdgpu_vtile_pending(self.p))
+
+    def metrics(self):
+        m = (ctypes.c_ulong * 5)()
+        self.L.fdgpu_vtile_metrics(self.p, m)
+        return list(m)
+
+    def record(self, chunk: int, sz: int) -> bytes:
+        return ctypes.string_at(self.dcache + chunk * CHUNK_SZ, sz)
+
+    def close(self):
+        if self.p:
+            self.L.fdgpu_vtile_delete(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def stream_bench(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,
+                 batch_txn: int = 4096, mcache_depth: int = 1 << 16, rate_fps: float = 0.0, device: int = 0) -> dict:
+    L = load()
+    payload = np.ascontiguousarray(payload, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    sz = np.ascontiguousarray(sz, np.uint16)
+    st = StreamStats()
+    rc = L.fdgpu_stream_bench(device, payload.ctypes.data, off.ctypes.data, sz.ctypes.data, len(off), n_frags, tiles,
+                              batch_txn, mcache_depth, rate_fps, ctypes.byref(st))
+    if rc:
+        raise RuntimeError(f"fdgpu_stream_bench: {rc} " + load_engine().fdgpu_last_error().decode())
+    return {"seconds": st.seconds, "frags": st.frags, "sigs": st.sigs, "published": st.published,
+            "frags_per_s": st.frags_per_s, "sigs_per_s": st.sigs_per_s, "lat_p50_us": st.lat_p50_us,
+            "lat_p99_us": st.lat_p99_us, "lat_max_us": st.lat_max_us, "metrics": list(st.metrics),
+            "overruns": st.overruns}

@@ -1,0 +1,175 @@
+#ifndef HEADER_fd_verify_gpu_h
+#define HEADER_fd_verify_gpu_h
+
+/* fd_verify_gpu.h -- the verify tile's frag callbacks with the GPU engine
+   behind them (libfdgpu_vtile.so, host C over libfdgpu_ed25519.so).
+
+   Replaces, for one verify tile, the work of
+
+     before_frag   src/disco/verify/fd_verify_tile.c:36-59  (round robin)
+     during_frag   src/disco/verify/fd_verify_tile.c:65-101 (copy to out dcache)
+     after_frag    src/disco/verify/fd_verify_tile.c:103-157
+                   (fd_txn_parse, bundle state, fd_txn_verify = HA dedup
+                   + fd_ed25519_verify_batch_single_msg, publish)
+
+   The reference does all of after_frag synchronously per frag.  Here
+   during_frag copies the frag into the out dcache exactly as before and
+   hands its payload to the GPU (fdgpu_ed25519_submit_raw: parse and
+   verify happen on the device); after_frags drains verdicts in frag
+   order and applies the parts of after_frag that depend on order --
+   bundle state, the tcache HA dedup query / insert, metrics, the
+   fd_txn_t write-back behind the payload and the publish decision --
+   with the reference's decision order, so the published stream and the
+   four metrics equal the reference tile's for the same input stream
+   (tests/test_gpu_vtile.py checks this against a sequential model).
+
+   Also here: a minimal tango (mcache / dcache rings with the frag
+   metadata and chunk addressing of src/tango/mcache/fd_mcache.h and
+   src/tango/dcache/fd_dcache.h) and a tcache with fd_tcache's
+   insert/evict semantics (src/tango/tcache/fd_tcache.h:281-404), used
+   by the tile and by the streaming benchmark (BASELINE configs[4]). */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- frag record: fd_txn_m_t (src/disco/fd_txn_m_t.h:14-64) -------- */
+
+typedef struct fdgpu_txnm {
+  unsigned long  reference_slot;
+  unsigned short payload_sz;
+  unsigned short txn_t_sz;
+  unsigned int   source_ipv4;
+  unsigned char  source_tpu;
+  unsigned char  _pad0[ 7 ];
+  unsigned long  bundle_id;
+  unsigned long  bundle_txn_cnt;
+  unsigned char  commission;
+  unsigned char  commission_pubkey[ 32 ];
+  unsigned char  _pad1[ 7 ];
+  /* followed by payload[ payload_sz ], then (after verify) the fd_txn_t
+     at the next 2-byte boundary */
+} fdgpu_txnm_t;
+
+#define FDGPU_TXNM_HDR_SZ (80UL)
+#define FDGPU_CHUNK_SZ    (64UL)   /* FD_CHUNK_SZ, src/tango/fd_tango_base.h */
+
+/* ---- HA dedup tag -------------------------------------------------- */
+
+/* fd_hash( seed, sig0, 64 ) of fd_txn_verify (fd_verify_tile.h:79):
+   XXH64 of the transaction's first signature */
+unsigned long fdgpu_dedup_tag( unsigned long seed, unsigned char const sig[ 64 ] );
+
+/* ---- tcache: HA dedup of the last `depth` unique tags -------------- */
+
+typedef struct fdgpu_tcache fdgpu_tcache_t;
+
+fdgpu_tcache_t * fdgpu_tcache_new   ( unsigned long depth );
+void             fdgpu_tcache_delete( fdgpu_tcache_t * tc );
+/* 1 if tag is among the last depth unique tags inserted (tag 0 is null) */
+int              fdgpu_tcache_query ( fdgpu_tcache_t const * tc, unsigned long tag );
+/* FD_TCACHE_INSERT: returns 1 (dup, nothing changes) or inserts tag,
+   evicting the oldest when depth tags are held, and returns 0 */
+int              fdgpu_tcache_insert( fdgpu_tcache_t * tc, unsigned long tag );
+
+/* ---- mcache / dcache ----------------------------------------------- */
+
+typedef struct fdgpu_frag_meta {   /* fd_frag_meta_t fields the verify path uses */
+  unsigned long seq;
+  unsigned long sig;
+  unsigned int  chunk;
+  unsigned int  sz;
+  unsigned long tsorig;
+  unsigned long tspub;
+} fdgpu_frag_meta_t;
+
+typedef struct fdgpu_mcache fdgpu_mcache_t;
+
+fdgpu_mcache_t * fdgpu_mcache_new    ( unsigned long depth, unsigned long seq0 );   /* depth: power of 2 */
+void             fdgpu_mcache_delete ( fdgpu_mcache_t * mc );
+/* producer: publish frag seq (seq must be the producer's next) */
+void             fdgpu_mcache_publish( fdgpu_mcache_t * mc, unsigned long seq, unsigned long sig, unsigned int chunk,
+                                       unsigned int sz, unsigned long tsorig, unsigned long tspub );
+/* consumer: 0 = frag seq copied to *out; 1 = not yet published; -1 = overrun
+   (the producer has lapped seq) */
+int              fdgpu_mcache_poll   ( fdgpu_mcache_t const * mc, unsigned long seq, fdgpu_frag_meta_t * out );
+
+/* next chunk after a frag of sz bytes at chunk, wrapping to chunk0 past
+   wmark (fd_dcache_compact_next, src/tango/dcache/fd_dcache.h) */
+unsigned long    fdgpu_dcache_compact_next( unsigned long chunk, unsigned long sz, unsigned long chunk0,
+                                            unsigned long wmark );
+
+/* ---- the GPU verify tile ------------------------------------------ */
+
+#define FDGPU_VTILE_PUBLISH          (0)
+#define FDGPU_VTILE_PARSE_FAIL       (1)
+#define FDGPU_VTILE_VERIFY_FAIL      (2)
+#define FDGPU_VTILE_DEDUP_FAIL       (3)
+#define FDGPU_VTILE_BUNDLE_PEER_FAIL (4)
+
+typedef struct fdgpu_vtile_done {
+  unsigned long seq;      /* as given to during_frag */
+  unsigned long tsorig;
+  unsigned long chunk;    /* out dcache chunk of the fd_txn_m_t record */
+  unsigned long sz;       /* realized footprint (fd_txn_m_realized_footprint) when published */
+  unsigned long tag;      /* HA dedup tag (0 for bundles) */
+  int           result;   /* FDGPU_VTILE_* */
+} fdgpu_vtile_done_t;
+
+typedef struct fdgpu_vtile fdgpu_vtile_t;
+
+/* device: HIP device; batch_txn: transactions per GPU batch (staging
+   slot); tcache_depth: HA dedup depth (verify.tcache_depth); seed: the
+   dedup hash seed (ctx->hashmap_seed); out_dcache_bytes: size of the
+   tile's out dcache (fd_txn_m_t records, 64-B chunks);  semantics:
+   FDGPU_SEMANTICS_*.  NULL on failure (fdgpu_last_error). */
+fdgpu_vtile_t * fdgpu_vtile_new( int device, unsigned long batch_txn, unsigned long tcache_depth, unsigned long seed,
+                                 unsigned long out_dcache_bytes, int semantics );
+void            fdgpu_vtile_delete( fdgpu_vtile_t * vt );
+unsigned char * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt );   /* chunk c is at base + 64 c */
+
+/* during_frag: copy the frag (fd_txn_m_t header + payload, sz bytes)
+   into the out dcache and submit its payload.  Returns 0, or -2 when the
+   out dcache or the GPU staging is full (call fdgpu_vtile_after_frags
+   and retry), <= -3 on error. */
+int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, unsigned long sz, unsigned long seq,
+                                         unsigned long tsorig );
+/* launch the partially filled batch (call when the input is idle) */
+int             fdgpu_vtile_flush( fdgpu_vtile_t * vt );
+/* after_frag for completed frags, in during_frag order: at most max
+   records to out[]; blocking waits for the oldest batch. */
+unsigned long   fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, unsigned long max, int blocking );
+/* frags submitted but not yet returned by after_frags */
+unsigned long   fdgpu_vtile_pending( fdgpu_vtile_t const * vt );
+/* metrics: [0] parse_fail [1] verify_fail [2] dedup_fail
+   [3] bundle_peer_fail [4] published (fd_verify_tile.c:29-34) */
+void            fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, unsigned long out[ 5 ] );
+
+/* ---- streaming benchmark (BASELINE configs[4]) --------------------- */
+
+typedef struct fdgpu_stream_stats {
+  double        seconds;         /* first frag published by the producer -> last verdict */
+  unsigned long frags, sigs, published;
+  double        frags_per_s, sigs_per_s;
+  double        lat_p50_us, lat_p99_us, lat_max_us;   /* tsorig (producer publish) -> after_frag verdict */
+  unsigned long metrics[ 5 ];
+  unsigned long overruns;        /* producer lapped a tile (frags lost, as in tango) */
+} fdgpu_stream_stats_t;
+
+/* A producer thread publishes n_frags frags built from the payload
+   arena (payload t at payload + off[t], sz[t] bytes, cycling over
+   n_payload) into an in mcache / dcache (depth mcache_depth), paced to
+   at most rate_fps frags/s (0 = as fast as possible); tiles verify
+   tiles (one host thread each, before_frag's seq % tiles round robin,
+   each with its own GPU context on `device`) consume it.  Returns 0 and
+   fills *st. */
+int             fdgpu_stream_bench( int device, unsigned char const * payload, unsigned int const * off,
+                                    unsigned short const * sz, unsigned long n_payload, unsigned long n_frags,
+                                    int tiles, unsigned long batch_txn, unsigned long mcache_depth, double rate_fps,
+                                    fdgpu_stream_stats_t * st );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEADER_fd_verify_gpu_h */

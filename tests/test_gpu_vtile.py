@@ -1,0 +1,181 @@
+"""GPU: the verify tile over the engine (libfdgpu_vtile.so) against a
+sequential model of the reference tile's after_frag
+(src/disco/verify/fd_verify_tile.c:103-157 + fd_txn_verify,
+fd_verify_tile.h:59-108): same per-frag outcome, same metrics, same
+published fd_txn_m_t records (payload + fd_txn_t image), over a stream
+with valid / invalid signatures, parse failures, HA duplicates (incl.
+tcache eviction) and bundles with failing members."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import raw_expect  # noqa: E402
+import txn_builder as tb  # noqa: E402
+from test_tango import TCacheModel  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def make_stream(seed=11):
+    from firedancer_amd import synth
+    rng = np.random.default_rng(seed)
+    base = []
+    for kind, ms, inv, n, s in ((synth.LARGE_NOOP, 1, 0.0, 300, 1), (synth.MULTI, 12, 0.25, 200, 2),
+                                (synth.SMALL_MSG, 1, 0.1, 100, 3)):
+        payload, desc, _, _ = synth.make_batch(n, kind, ms, inv, seed=s)
+        base += [payload[d["payload_off"]: d["payload_off"] + d["payload_sz"]].tobytes() for d in desc]
+    base += [tb.build_txn(rng) for _ in range(60)]
+    base += [tb.mutate(rng, base[int(rng.integers(600))]) for _ in range(60)]
+    base = [b for b in base if len(b) <= 1232]          # the tile FD_LOG_ERRs on > FD_TPU_MTU (fd_verify_tile.c:83-85)
+    order = list(rng.permutation(len(base)))
+    frags, bid = [], 0
+    i = 0
+    while i < len(order):
+        r = rng.random()
+        if r < 0.15:                                   # HA duplicate of something seen earlier
+            j = int(rng.integers(max(1, len(frags))))
+            frags.append((frags[j][0] if frags else base[order[i]], 0))
+        elif r < 0.25:                                 # a bundle of 2..5 frags
+            bid += 1
+            for _ in range(int(rng.integers(2, 6))):
+                if i < len(order):
+                    frags.append((base[order[i]], 1000 + bid)); i += 1
+            continue
+        else:
+            frags.append((base[order[i]], 0))
+        i += 1
+    return frags
+
+
+def model(oracle, frags, seed, depth):
+    from firedancer_amd import vtile
+    import xxhash
+    arena, off, sz = tb.pack([p for p, _ in frags])
+    codes, fp, img = raw_expect.expected_codes(oracle, arena, off, sz)
+    tc, bundle_failed, bundle_id = TCacheModel(depth), 0, 0
+    res, metrics, recs = [], [0] * 5, {}
+    for i, (p, b) in enumerate(frags):
+        is_bundle = b != 0
+        if is_bundle and b != bundle_id:
+            bundle_failed, bundle_id = 0, b
+        if is_bundle and bundle_failed:
+            metrics[3] += 1; res.append(vtile.BUNDLE_PEER_FAIL); continue
+        if fp[i] == 0:
+            bundle_failed |= is_bundle; metrics[0] += 1; res.append(vtile.PARSE_FAIL); continue
+        so = int(img[i, 2]) | int(img[i, 3]) << 8
+        tag = xxhash.xxh64(p[so: so + 64], seed=seed).intdigest()
+        if not is_bundle and tc.query(tag):
+            r = vtile.DEDUP_FAIL
+        elif codes[i] != 0:
+            r = vtile.VERIFY_FAIL
+        elif not is_bundle and tc.insert(tag):
+            r = vtile.DEDUP_FAIL
+        else:
+            r = vtile.PUBLISH
+        if r != vtile.PUBLISH:
+            bundle_failed |= is_bundle
+            metrics[2 if r == vtile.DEDUP_FAIL else 1] += 1
+        else:
+            metrics[4] += 1
+            h = np.frombuffer(vtile.frag_bytes(p, b), np.uint8).copy()
+            h[10:12] = np.frombuffer(np.uint16(fp[i]).tobytes(), np.uint8)   # txn_t_sz
+            recs[i] = (h.tobytes(), img[i, : fp[i]].tobytes())   # the alignment pad byte between them is unspecified
+        res.append(r)
+    return res, metrics, recs
+
+
+@pytest.mark.parametrize("batch,depth", [(64, 32), (512, 1 << 12)])
+def test_vtile_vs_model(oracle, batch, depth):
+    pytest.importorskip("xxhash")
+    from firedancer_amd import vtile
+    frags = make_stream()
+    seed = 0x1234abcd
+    want_res, want_m, want_recs = model(oracle, frags, seed, depth)
+    vt = vtile.VTile(device=0, batch_txn=batch, tcache_depth=depth, seed=seed)
+    got, bad = [], []
+
+    def drain(blocking):
+        # downstream reads each published record as it is published (the out dcache is a ring)
+        out = vt.after_frags(blocking=blocking)
+        for seq, r, chunk, sz, tag in out:
+            if r == vtile.PUBLISH:
+                head, timg = want_recs.get(seq, (b"", b""))
+                rec = vt.record(chunk, sz)
+                if rec[: len(head)] != head or rec[(len(head) + 1) & ~1:] != timg or sz != ((len(head) + 1) & ~1) + len(timg):
+                    bad.append(seq)
+        return out
+
+    for seq, (p, b) in enumerate(frags):
+        fb = vtile.frag_bytes(p, b)
+        while True:
+            rc = vt.during_frag(fb, seq)
+            if rc != -2:
+                break
+            got += drain(True)
+        assert rc == 0, rc
+        if seq % 37 == 0:
+            got += drain(False)
+    vt.flush()
+    while vt.pending():
+        got += drain(True)
+    assert [g[0] for g in got] == list(range(len(frags)))
+    assert [g[1] for g in got] == want_res
+    assert vt.metrics() == want_m
+    assert bad == []
+    assert sum(want_m[:4]) > 100 and want_m[2] > 10 and want_m[3] > 0
+    vt.close()
+
+
+def _run_frags(vt, frags, seq0=0):
+    from firedancer_amd import vtile
+    out = []
+    for i, (p, b) in enumerate(frags):
+        while vt.during_frag(vtile.frag_bytes(p, b), seq0 + i) == -2:
+            out += vt.after_frags(blocking=True)
+    vt.flush()
+    while vt.pending():
+        out += vt.after_frags(blocking=True)
+    return [r for _, r, _, _, _ in out]
+
+
+def test_reference_tile_scenarios():
+    """The four fd_txn_verify scenarios of src/disco/verify/test_verify.c:161-347 on its own real
+    transactions, through the GPU tile.  dedup=0 calls are bundle frags (each its own bundle id);
+    fd_tcache_reset is a fresh tile."""
+    import json
+    from firedancer_amd import vtile
+    d = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "verify_tile_txns.json")))
+    V1, V2 = bytes.fromhex(d["valid_txn_1sig"]), bytes.fromhex(d["valid_txn_2sigs"])
+    I1, I2 = bytes.fromhex(d["invalid_txn_same_1sig"]), bytes.fromhex(d["invalid_txn_2sigs"])
+    I64 = bytes.fromhex(d["invalid_txn_1sig_same_64bit"])
+    P, F, D = vtile.PUBLISH, vtile.VERIFY_FAIL, vtile.DEDUP_FAIL
+
+    def tile():
+        return vtile.VTile(device=0, batch_txn=64, tcache_depth=128)
+
+    # test_verify_success (:161-208)
+    assert _run_frags(tile(), [(V2, 0), (V2, 0), (V2, 0), (V2, 1), (V1, 0), (V1, 0), (V1, 0)]) == [P, D, D, P, P, D, D]
+    # test_verify_invalid_sigs_success (:210-237): no dedup for failed txns
+    assert _run_frags(tile(), [(I2, 0), (I2, 0)]) == [F, F]
+    # test_verify_invalid_dedup_success (:239-311)
+    assert _run_frags(tile(), [(I1, 0), (V1, 0)]) == [F, P]
+    assert _run_frags(tile(), [(V1, 0), (I1, 0)]) == [P, D]
+    assert _run_frags(tile(), [(V1, 2), (I1, 3), (I1, 0), (I1, 0)]) == [P, F, F, F]
+    # test_verify_invalid_dedup_with_collision_success (:313-347)
+    assert _run_frags(tile(), [(V1, 0), (I64, 0)]) == [P, F]
+
+
+def test_stream_bench_small():
+    """The configs[4] harness end to end at a small size: every frag gets a verdict."""
+    from firedancer_amd import synth, vtile
+    payload, desc, _, _ = synth.make_batch(4096, synth.LARGE_NOOP, seed=9)
+    st = vtile.stream_bench(payload, desc["payload_off"], desc["payload_sz"], n_frags=50000, tiles=2, batch_txn=1024,
+                            mcache_depth=8192)
+    assert st["frags"] == 50000 and st["overruns"] == 0
+    m = st["metrics"]
+    # 4096 distinct payloads cycled: the first copy of each publishes per tile, repeats are HA duplicates
+    assert m[0] == 0 and m[1] == 0 and m[4] + m[2] == 50000 and m[4] >= 4096
+    assert st["lat_p99_us"] > 0
