@@ -90,6 +90,11 @@ def main():
     ap.add_argument("--txns", type=int, default=1 << 20, help="txns per GPU per step (BASELINE configs[1]: 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-batch", type=int, default=8192)
+    ap.add_argument("--stream-frags", type=int, default=2_000_000,
+                    help="BASELINE configs[4]: frags streamed through the GPU verify tiles (0 = skip)")
+    ap.add_argument("--stream-tiles", type=int, default=6)
+    ap.add_argument("--stream-batch", type=int, default=8192)
+    ap.add_argument("--stream-rate", type=float, default=2e6, help="paced rate (frags/s) of the latency run")
     args = ap.parse_args()
 
     import torch
@@ -152,18 +157,45 @@ def main():
         lat = {"batch_txns": lb, "p50_ms": float(np.percentile(times, 50)), "p99_ms": float(np.percentile(times, 99)),
                "path": "fdgpu_ed25519_verify_txns_host: pinned staging, H2D, 4 kernels, D2H"}
 
+    # BASELINE configs[4]: the same payloads streamed through GPU verify tiles
+    # (tango mcache/dcache in, fd_txn_parse + verify on the GPU, in-order
+    # after_frag, out dcache).  Every rank streams its own shard at once.
+    stream = None
+    if args.stream_frags > 0:
+        from firedancer_amd import vtile
+        off, psz = desc["payload_off"], desc["payload_sz"]
+        barrier()
+        smax = vtile.stream_bench(payload, off, psz, n_frags=args.stream_frags, tiles=args.stream_tiles,
+                                  batch_txn=args.stream_batch, max_inflight=2)
+        barrier()
+        slat = vtile.stream_bench(payload, off, psz, n_frags=args.stream_frags, tiles=args.stream_tiles,
+                                  batch_txn=args.stream_batch, max_inflight=2, rate_fps=args.stream_rate)
+        ok_s = smax["metrics"][:4] == [0, 0, 0, 0] and smax["published"] == args.stream_frags
+        sig_tot, t_max, _ = shard.reduce_sum_max(dist if world > 1 else None, smax["sigs"], smax["seconds"], "cuda")
+        stream = {"workload": "BASELINE configs[4]: 1232-byte txns through mcache/dcache -> GPU verify tiles "
+                              "(device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> out dcache",
+                  "sigs_per_s": sig_tot / t_max, "per_gpu_sigs_per_s": smax["sigs_per_s"], "n_gpus": world,
+                  "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch, "frags_per_gpu": args.stream_frags,
+                  "max_rate": {"p50_us": smax["lat_p50_us"], "p99_us": smax["lat_p99_us"]},
+                  "paced": {"rate_frags_per_s": args.stream_rate, "achieved": slat["frags_per_s"],
+                            "p50_us": slat["lat_p50_us"], "p99_us": slat["lat_p99_us"], "max_us": slat["lat_max_us"]},
+                  "all_published": bool(ok_s),
+                  "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
+
     if rank == 0:
         L = load_library()
         L.fdgpu_mad_peak_per_s.restype = ctypes.c_double
         L.fdgpu_mad_peak_per_s.argtypes = [ctypes.c_int]
-        peak = float(L.fdgpu_mad_peak_per_s(local_rank))
+        peak = max(float(L.fdgpu_mad_peak_per_s(local_rank)) for _ in range(3))
         dom_ms = ms_dsm
         achieved = DSM_MAC * nsig / (dom_ms * 1e-3)
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "dsm_pmc.json")
+        valu_busy = None
         if os.path.exists(pmc):
             try:
-                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                pm = json.load(open(pmc))
+                traffic, valu_busy = pm.get("hbm_bytes_per_launch"), pm.get("valu_busy")
             except Exception:
                 traffic = None
         cpu = None
@@ -193,9 +225,12 @@ def main():
                          "kernel": "fd_dsm_kernel",
                          "work_per_sig": f"{DSM_MAC} v_mad_u64_u32 (1008 S + 1341 M of the reference wNAF DSM, "
                                          f"S=44 M=72 MAC)",
-                         "peak_source": "fdgpu_mad_peak_per_s: measured v_mad_u64_u32 throughput, this device"},
+                         "peak_source": "fdgpu_mad_peak_per_s: measured v_mad_u64_u32 throughput, this device (max of 3)",
+                         "valu_busy": valu_busy,
+                         "valu_busy_source": "profiles/dsm_pmc.json: SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE/8)"},
             "cpu_baseline": cpu,
             "latency": lat,
+            "stream": stream,
             "gen_s": t_gen,
         }
         print(json.dumps(rec), flush=True)

@@ -423,7 +423,7 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   size_t             payload_used;
   unsigned long      txn_cnt, sig_cnt;
   unsigned long      cursor;   /* results already handed out by poll */
-  hipEvent_t         h2d, kdone, done;
+  hipEvent_t         done;
   int                state;    /* 0 filling, 1 in flight / draining */
   int                mode;     /* 0 desc (fdgpu_ed25519_submit), 1 raw (fdgpu_ed25519_submit_raw) */
 };
@@ -448,15 +448,11 @@ struct fdgpu_ed25519_ctx {
   enum { NRING = 64 };
   hipEvent_t ring[ NRING ][ 4 ];  /* per-batch kernel boundaries while timing is on */
   unsigned long ring_cnt;
-  /* async pipeline: NSLOT pinned staging slots; H2D / D2H on the copy
-     stream, kernels on the compute stream, so slot k+1's upload overlaps
-     slot k's kernels (the ctx scratch is only touched in compute-stream
-     order) */
+  /* async pipeline: NSLOT pinned staging slots, all on ctx->stream */
   enum { NSLOT = 4 };
   fd_slot slot[ NSLOT ];
   int cur;                       /* slot being filled */
   std::deque<int> inflight;      /* slot order */
-  hipStream_t cstream;
 };
 
 extern "C" char const * fdgpu_last_error( void ) { return fd_err.c_str(); }
@@ -510,7 +506,6 @@ fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
   ctx->max_txn = max_txn; ctx->max_sig = max_sig; ctx->max_payload = max_payload_bytes;
   size_t ns = max_sig;
   HIPCHK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ), NULL );
-  HIPCHK( hipStreamCreateWithFlags( &ctx->cstream, hipStreamNonBlocking ), NULL );
   HIPCHK( hipMalloc( &ctx->d_map,  ns * sizeof(u32) ), NULL );
   HIPCHK( hipMalloc( &ctx->d_code, ns ), NULL );
   HIPCHK( hipMalloc( &ctx->d_pstat, 2*ns ), NULL );
@@ -541,8 +536,6 @@ fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
       memset( sl.h_payload, 0, max_payload_bytes + FD_ARENA_SLACK );
     }
     HIPCHK( hipEventCreateWithFlags( &sl.done, hipEventDisableTiming ), NULL );
-    HIPCHK( hipEventCreateWithFlags( &sl.h2d, hipEventDisableTiming ), NULL );
-    HIPCHK( hipEventCreateWithFlags( &sl.kdone, hipEventDisableTiming ), NULL );
   }
   ctx->cur = 0;
   HIPCHK( hipStreamSynchronize( ctx->stream ), NULL );
@@ -563,10 +556,8 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
     if( sl.h_payload ) { hipHostFree( sl.h_payload ); hipHostFree( sl.h_desc ); hipHostFree( sl.h_txn_out ); hipHostFree( sl.h_tags );
                          hipFree( sl.d_payload ); hipFree( sl.d_desc ); hipFree( sl.d_txn_out ); }
     if( sl.h_img ) { hipHostFree( sl.h_img ); hipHostFree( sl.h_fp ); hipFree( sl.d_img ); hipFree( sl.d_fp ); }
-    hipEventDestroy( sl.done ); hipEventDestroy( sl.h2d ); hipEventDestroy( sl.kdone );
+    hipEventDestroy( sl.done );
   }
-  hipStreamSynchronize( ctx->cstream );
-  hipStreamDestroy( ctx->cstream );
   hipStreamDestroy( ctx->stream );
   delete ctx;
 }
@@ -771,27 +762,30 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
 
 /* ---- async submit / poll ------------------------------------------ */
 
+/* One stream per context: upload, kernels and download of a slot are
+   in stream order.  (A separate copy stream with cross-stream event
+   waits deadlocked once several contexts' streams were multiplexed onto
+   the device's few hardware queues -- a waiter's barrier packet can sit
+   ahead of the work it waits for in a shared queue.  Overlap of one
+   context's upload with another's kernels comes from running several
+   contexts, one per verify tile.) */
 static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
   fd_slot & sl = ctx->slot[i];
-  hipStream_t cs = ctx->cstream, st = ctx->stream;
+  hipStream_t st = ctx->stream;
   memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
-  HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, cs ), -2 );
-  HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, cs ), -2 );
-  HIPCHK( hipEventRecord( sl.h2d, cs ), -2 );
-  HIPCHK( hipStreamWaitEvent( st, sl.h2d, 0 ), -2 );
+  HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+  HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
   int rc = sl.mode
          ? launch_raw( ctx, sl.d_payload, (fdgpu_txn_raw_t const *)sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out,
                        sl.d_img, FDGPU_TXN_IMG_STRIDE, sl.d_fp, st )
          : launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
   if( rc ) return rc;
-  HIPCHK( hipEventRecord( sl.kdone, st ), -2 );
-  HIPCHK( hipStreamWaitEvent( cs, sl.kdone, 0 ), -2 );
-  HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, cs ), -2 );
+  HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
   if( sl.mode ) {
-    HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, cs ), -2 );
-    HIPCHK( hipMemcpyAsync( sl.h_img, sl.d_img, sl.txn_cnt * FDGPU_TXN_IMG_STRIDE, hipMemcpyDeviceToHost, cs ), -2 );
+    HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
+    HIPCHK( hipMemcpyAsync( sl.h_img, sl.d_img, sl.txn_cnt * FDGPU_TXN_IMG_STRIDE, hipMemcpyDeviceToHost, st ), -2 );
   }
-  HIPCHK( hipEventRecord( sl.done, cs ), -2 );
+  HIPCHK( hipEventRecord( sl.done, st ), -2 );
   sl.state = 1; sl.cursor = 0;
   ctx->inflight.push_back( i );
   return 0;
@@ -911,6 +905,12 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
     }
   }
   return n;
+}
+
+extern "C" void
+fdgpu_ed25519_pipeline_state( fdgpu_ed25519_ctx_t const * ctx, unsigned long * filling, unsigned long * inflight ) {
+  *filling  = ctx->slot[ ctx->cur ].state==0 ? ctx->slot[ ctx->cur ].txn_cnt : 0UL;
+  *inflight = (unsigned long)ctx->inflight.size();
 }
 
 extern "C" unsigned long

@@ -8,6 +8,7 @@
 #include "../../include/fd_ed25519_gpu.h"
 
 #include <pthread.h>
+#include <stdio.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -197,6 +198,7 @@ typedef struct {
 } vt_pend_t;
 
 struct fdgpu_vtile {
+  /* (fields below; ctx first so the watchdog can report pipeline state) */
   fdgpu_ed25519_ctx_t * ctx;
   fdgpu_tcache_t *      tcache;
   ulong                 seed;
@@ -255,6 +257,18 @@ uchar * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt ) { return vt->dcache; }
 ulong   fdgpu_vtile_pending( fdgpu_vtile_t const * vt ) { return vt->pend_tail - vt->pend_head; }
 void    fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, ulong out[ 5 ] ) { memcpy( out, vt->metrics, sizeof(vt->metrics) ); }
 int     fdgpu_vtile_flush( fdgpu_vtile_t * vt ) { return fdgpu_ed25519_flush( vt->ctx ); }
+
+int
+fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
+  ulong filling, inflight;
+  fdgpu_ed25519_pipeline_state( vt->ctx, &filling, &inflight );
+  /* keep at least one staging slot free to accumulate in: with every slot
+     in flight, each freed slot would be relaunched after a handful of
+     frags and the pipeline would degenerate into tiny batches */
+  if( max_inflight > 3UL ) max_inflight = 3UL;
+  if( !filling || inflight >= max_inflight ) return 0;
+  return fdgpu_ed25519_flush( vt->ctx ) ? 0 : 1;
+}
 
 int
 fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
@@ -341,10 +355,11 @@ typedef struct {
   ulong                  in_chunk0, in_wmark;
   ulong                  n_frags;
   int                    tiles;
-  _Atomic ulong *        fseq;        /* per tile: next seq it has yet to consume (credit return) */
+  struct { _Atomic ulong v; uchar pad[56]; } * fseq;   /* per tile, own cache line: next seq it has yet to consume */
   _Atomic int            go, fail, ready;
   float *                lat_us;      /* per frag */
   unsigned char const *  payload; unsigned int const * off; unsigned short const * sz; ulong n_payload;
+  ulong *                frag_chunk;  /* in dcache chunk of payload p's prefilled frag record */
   double                 rate_fps;
   ulong                  depth;
   ulong                  t_start, t_end;
@@ -352,37 +367,42 @@ typedef struct {
   _Atomic ulong          sigs, published, overruns;
   ulong                  metrics[5];
   pthread_mutex_t        mu;
-  int                    device; ulong batch_txn;
+  int                    device; ulong batch_txn, max_inflight;
 } sb_t;
 
+/* The producer stands in for the QUIC tiles: every distinct payload is
+   written once, before the run, into the in dcache as an fd_txn_m_t frag
+   record (as the NIC / QUIC reassembly would have left it), and the
+   timed loop only publishes metadata -- frag seq points at payload
+   seq % n_payload.  The link is reliable (credit based): the producer
+   runs at most depth/2 frags ahead of the slowest tile, re-reading the
+   tiles' fseqs only when its cached credits run out. */
 static void * sb_producer( void * _s ) {
   sb_t * s = (sb_t *)_s;
   while( !atomic_load( &s->go ) ) ;
-  ulong chunk = s->in_chunk0;
   ulong t0 = now_ns();
   s->t_start = t0;
+  ulong cr_until = 0UL;                     /* may publish seq < cr_until */
   for( ulong seq=0; seq<s->n_frags; seq++ ) {
-    if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) break;
-    /* reliable link: wait for credits (every tile within depth/2 of seq) */
-    for( ;; ) {
-      ulong lo = ~0UL;
-      for( int t=0; t<s->tiles; t++ ) { ulong f = atomic_load_explicit( &s->fseq[t], memory_order_acquire ); if( f < lo ) lo = f; }
-      if( seq - lo < s->depth/2 ) break;
+    ulong t_wait = 0UL;
+    while( seq >= cr_until ) {
       if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) return NULL;
+      if( !t_wait ) t_wait = now_ns();
+      else if( now_ns() - t_wait > 30000000000UL ) {            /* watchdog: 30 s without credits */
+        fprintf( stderr, "fdgpu_stream_bench: producer starved of credits at seq %lu\n", seq );
+        atomic_store( &s->fail, 4 ); return NULL;
+      }
+      ulong lo = ~0UL;
+      for( int t=0; t<s->tiles; t++ ) { ulong f = atomic_load_explicit( &s->fseq[t].v, memory_order_acquire ); if( f < lo ) lo = f; }
+      cr_until = lo + s->depth/2;
     }
     if( s->rate_fps > 0. ) {
       ulong due = t0 + (ulong)( (double)seq * 1e9 / s->rate_fps );
       while( now_ns() < due ) ;
     }
     ulong p = seq % s->n_payload;
-    fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( s->in_dcache + chunk * FDGPU_CHUNK_SZ );
-    memset( txnm, 0, FDGPU_TXNM_HDR_SZ );
-    txnm->payload_sz = s->sz[p];
-    memcpy( (uchar *)txnm + FDGPU_TXNM_HDR_SZ, s->payload + s->off[p], s->sz[p] );
-    ulong fsz = FDGPU_TXNM_HDR_SZ + s->sz[p];
     ulong ts = now_ns();
-    fdgpu_mcache_publish( s->mc, seq, 0UL, (unsigned)chunk, (unsigned)fsz, ts, ts );
-    chunk = fdgpu_dcache_compact_next( chunk, fsz, s->in_chunk0, s->in_wmark );
+    fdgpu_mcache_publish( s->mc, seq, 0UL, (unsigned)s->frag_chunk[p], (unsigned)( FDGPU_TXNM_HDR_SZ + s->sz[p] ), ts, ts );
   }
   return NULL;
 }
@@ -418,9 +438,17 @@ static void * sb_tile( void * _a ) {
   ulong sigs = 0UL, mine = 0UL, got = 0UL;
   for( ulong seq=0; seq<s->n_frags; ) mine += ( seq++ % (ulong)s->tiles ) == (ulong)idx;
   ulong seq = 0UL;
-  int idle = 0;
+  ulong last_seq = ~0UL, last_got = ~0UL, t_prog = now_ns();
   while( got < mine ) {
     if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) break;
+    if( seq != last_seq || got != last_got ) { last_seq = seq; last_got = got; t_prog = now_ns(); }
+    else if( now_ns() - t_prog > 30000000000UL ) {                /* watchdog: 30 s without progress */
+      ulong filling = 0, inflight = 0;
+      fdgpu_ed25519_pipeline_state( vt->ctx, &filling, &inflight );
+      fprintf( stderr, "fdgpu_stream_bench: tile %d stalled: seq %lu got %lu/%lu pending %lu filling %lu inflight %lu\n",
+               idx, seq, got, mine, fdgpu_vtile_pending( vt ), filling, inflight );
+      atomic_store( &s->fail, 5 ); break;
+    }
     int progressed = 0;
     if( seq < s->n_frags ) {
       fdgpu_frag_meta_t m;
@@ -436,15 +464,13 @@ static void * sb_tile( void * _a ) {
           if( rc ) { atomic_store( &s->fail, 2 ); break; }
         }
         seq++;
-        atomic_store_explicit( &s->fseq[idx], seq, memory_order_release );
-        progressed = 1; idle = 0;
+        if( !(seq & 63UL) || seq==s->n_frags ) atomic_store_explicit( &s->fseq[idx].v, seq, memory_order_release );   /* batched credit return */
+        progressed = 1;
       } else if( r < 0 ) {
         atomic_fetch_add( &s->overruns, 1 ); atomic_store( &s->fail, 3 ); break;
       }
     }
-    if( !progressed ) {
-      if( ++idle == 64 ) fdgpu_vtile_flush( vt );                    /* input idle: launch the partial batch */
-    }
+    if( !progressed || !(seq & 15UL) ) fdgpu_vtile_housekeep( vt, s->max_inflight );   /* adaptive batching */
     if( !progressed || (seq & 255UL) == 0 ) {
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
       sb_account( s, vt, done, n, &sigs ); got += n;
@@ -467,20 +493,31 @@ static int cmp_f( void const * a, void const * b ) {
 
 int
 fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, unsigned short const * sz, ulong n_payload,
-                    ulong n_frags, int tiles, ulong batch_txn, ulong mcache_depth, double rate_fps,
+                    ulong n_frags, int tiles, ulong batch_txn, ulong max_inflight, ulong mcache_depth, double rate_fps,
                     fdgpu_stream_stats_t * st ) {
   if( tiles < 1 || tiles > 64 || !n_frags || !n_payload || !batch_txn || mcache_depth < 64 ) return -1;
   sb_t * s = (sb_t *)calloc( 1, sizeof(sb_t) );
   s->depth = pow2_up( mcache_depth );
   s->mc = fdgpu_mcache_new( s->depth, 0UL );
-  ulong in_bytes = s->depth * 2UL * 1408UL;
-  s->in_dcache = (uchar *)aligned_alloc( 128, in_bytes );
-  s->in_chunk0 = 0UL; s->in_wmark = in_bytes / FDGPU_CHUNK_SZ - 24UL;
+  /* in dcache: one prefilled fd_txn_m_t frag record per distinct payload */
+  ulong in_bytes = 0UL;
+  for( ulong p=0; p<n_payload; p++ ) in_bytes += ( ( FDGPU_TXNM_HDR_SZ + sz[p] + 127UL ) >> 7 ) << 7;
+  s->in_dcache = (uchar *)aligned_alloc( 128, in_bytes + 128UL );
+  s->frag_chunk = (ulong *)malloc( n_payload * sizeof(ulong) );
+  if( !s->in_dcache || !s->frag_chunk ) { free( s->in_dcache ); free( s->frag_chunk ); fdgpu_mcache_delete( s->mc ); free( s ); return -2; }
+  for( ulong p=0, c=0; p<n_payload; p++ ) {
+    fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( s->in_dcache + c * FDGPU_CHUNK_SZ );
+    memset( txnm, 0, FDGPU_TXNM_HDR_SZ );
+    txnm->payload_sz = sz[p];
+    memcpy( (uchar *)txnm + FDGPU_TXNM_HDR_SZ, payload + off[p], sz[p] );
+    s->frag_chunk[p] = c;
+    c = fdgpu_dcache_compact_next( c, FDGPU_TXNM_HDR_SZ + sz[p], 0UL, ~0UL );
+  }
   s->n_frags = n_frags; s->tiles = tiles;
-  s->fseq = (_Atomic ulong *)calloc( (size_t)tiles, sizeof(_Atomic ulong) );
+  s->fseq = calloc( (size_t)tiles, sizeof(*s->fseq) );
   s->lat_us = (float *)calloc( n_frags, sizeof(float) );
   s->payload = payload; s->off = off; s->sz = sz; s->n_payload = n_payload; s->rate_fps = rate_fps;
-  s->device = device; s->batch_txn = batch_txn;
+  s->device = device; s->batch_txn = batch_txn; s->max_inflight = max_inflight ? max_inflight : 2UL;
   pthread_mutex_init( &s->mu, NULL );
   pthread_t prod, th[64]; sb_tile_arg_t args[64];
   for( int t=0; t<tiles; t++ ) { args[t].s = s; args[t].idx = t; pthread_create( &th[t], NULL, sb_tile, &args[t] ); }
@@ -503,7 +540,7 @@ fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, uns
     memcpy( st->metrics, s->metrics, sizeof(st->metrics) );
     st->overruns = atomic_load( &s->overruns );
   }
-  fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( (void *)s->fseq ); free( s->lat_us );
+  fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( s->frag_chunk ); free( (void *)s->fseq ); free( s->lat_us );
   pthread_mutex_destroy( &s->mu );
   free( s );
   return rc ? -rc - 10 : 0;

@@ -62,3 +62,16 @@ def reduce_max_min(dist, dt: float, ok: bool, device) -> tuple[float, bool]:
 def aggregate_rate(world: int, units_per_rank: int, steps: int, dt_max: float) -> float:
     """Whole-job throughput: all ranks' units over the slowest rank's time (weak scaling)."""
     return world * units_per_rank * steps / dt_max
+
+
+def reduce_sum_max(dist, units: float, seconds: float, device) -> tuple[float, float, int]:
+    """SUM over ranks of units, MAX of seconds (a concurrent per-rank stream), and the rank count."""
+    import torch
+    u = torch.tensor([float(units)], dtype=torch.float64, device=device)
+    s = torch.tensor([float(seconds)], dtype=torch.float64, device=device)
+    w = 1
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(u, op=dist.ReduceOp.SUM)
+        dist.all_reduce(s, op=dist.ReduceOp.MAX)
+        w = dist.get_world_size()
+    return float(u.item()), float(s.item()), w

@@ -19,7 +19,7 @@ PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL = range(5)
 EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
            "fdgpu_mcache_new", "fdgpu_mcache_delete", "fdgpu_mcache_publish", "fdgpu_mcache_poll",
            "fdgpu_dcache_compact_next", "fdgpu_vtile_new", "fdgpu_vtile_delete", "fdgpu_vtile_out_dcache",
-           "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
+           "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_housekeep", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
            "fdgpu_vtile_metrics", "fdgpu_stream_bench")
 
 TXNM_DTYPE = np.dtype([("reference_slot", "<u8"), ("payload_sz", "<u2"), ("txn_t_sz", "<u2"), ("source_ipv4", "<u4"),
@@ -77,12 +77,13 @@ def load():
         L.fdgpu_vtile_out_dcache.argtypes = [vp]
         L.fdgpu_vtile_during_frag.argtypes = [vp, vp, ul, ul, ul]
         L.fdgpu_vtile_flush.argtypes = [vp]
+        L.fdgpu_vtile_housekeep.argtypes = [vp, ul]
         L.fdgpu_vtile_after_frags.restype = ul
         L.fdgpu_vtile_after_frags.argtypes = [vp, ctypes.POINTER(Done), ul, ctypes.c_int]
         L.fdgpu_vtile_pending.restype = ul
         L.fdgpu_vtile_pending.argtypes = [vp]
         L.fdgpu_vtile_metrics.argtypes = [vp, ctypes.POINTER(ctypes.c_ulong)]
-        L.fdgpu_stream_bench.argtypes = [ctypes.c_int, vp, vp, vp, ul, ul, ctypes.c_int, ul, ul, ctypes.c_double,
+        L.fdgpu_stream_bench.argtypes = [ctypes.c_int, vp, vp, vp, ul, ul, ctypes.c_int, ul, ul, ul, ctypes.c_double,
                                          ctypes.POINTER(StreamStats)]
         _lib = L
     return _lib
@@ -166,14 +167,15 @@ class VTile:
 
 
 def stream_bench(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,
-                 batch_txn: int = 4096, mcache_depth: int = 1 << 16, rate_fps: float = 0.0, device: int = 0) -> dict:
+                 batch_txn: int = 4096, max_inflight: int = 2, mcache_depth: int = 1 << 16, rate_fps: float = 0.0,
+                 device: int = 0) -> dict:
     L = load()
     payload = np.ascontiguousarray(payload, np.uint8)
     off = np.ascontiguousarray(off, np.uint32)
     sz = np.ascontiguousarray(sz, np.uint16)
     st = StreamStats()
     rc = L.fdgpu_stream_bench(device, payload.ctypes.data, off.ctypes.data, sz.ctypes.data, len(off), n_frags, tiles,
-                              batch_txn, mcache_depth, rate_fps, ctypes.byref(st))
+                              batch_txn, max_inflight, mcache_depth, rate_fps, ctypes.byref(st))
     if rc:
         raise RuntimeError(f"fdgpu_stream_bench: {rc} " + load_engine().fdgpu_last_error().decode())
     return {"seconds": st.seconds, "frags": st.frags, "sigs": st.sigs, "published": st.published,

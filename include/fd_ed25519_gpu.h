@@ -253,6 +253,14 @@ fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx,
                     unsigned long         max,
                     int                   blocking );
 
+/* Pipeline occupancy: transactions in the slot being filled, and
+   launched slots not yet fully drained by poll.  Lets a caller launch
+   early when the GPU is idle and let batches grow while it is busy. */
+void
+fdgpu_ed25519_pipeline_state( fdgpu_ed25519_ctx_t const * ctx,
+                              unsigned long *             filling,
+                              unsigned long *             inflight );
+
 /* Raw-payload form of the pipeline (what fd_verify_tile's during_frag /
    after_frag pair needs, with fd_txn_parse moved onto the GPU):
    submit_raw copies one raw payload (no host parse); poll_raw returns,

@@ -136,6 +136,12 @@ int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, 
                                          unsigned long tsorig );
 /* launch the partially filled batch (call when the input is idle) */
 int             fdgpu_vtile_flush( fdgpu_vtile_t * vt );
+/* adaptive batching, for the tile's housekeeping / before_credit hook:
+   launch the filling batch when fewer than max_inflight batches are on
+   the GPU -- batches stay small (low latency) while the GPU keeps up and
+   grow with the backlog when it does not (max_inflight is capped at one
+   less than the engine's 4 staging slots).  Returns 1 if it launched. */
+int             fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, unsigned long max_inflight );
 /* after_frag for completed frags, in during_frag order: at most max
    records to out[]; blocking waits for the oldest batch. */
 unsigned long   fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, unsigned long max, int blocking );
@@ -161,12 +167,13 @@ typedef struct fdgpu_stream_stats {
    n_payload) into an in mcache / dcache (depth mcache_depth), paced to
    at most rate_fps frags/s (0 = as fast as possible); tiles verify
    tiles (one host thread each, before_frag's seq % tiles round robin,
-   each with its own GPU context on `device`) consume it.  Returns 0 and
-   fills *st. */
+   each with its own GPU context on `device`, batches of at most
+   batch_txn launched by fdgpu_vtile_housekeep( max_inflight )) consume
+   it.  Returns 0 and fills *st. */
 int             fdgpu_stream_bench( int device, unsigned char const * payload, unsigned int const * off,
                                     unsigned short const * sz, unsigned long n_payload, unsigned long n_frags,
-                                    int tiles, unsigned long batch_txn, unsigned long mcache_depth, double rate_fps,
-                                    fdgpu_stream_stats_t * st );
+                                    int tiles, unsigned long batch_txn, unsigned long max_inflight,
+                                    unsigned long mcache_depth, double rate_fps, fdgpu_stream_stats_t * st );
 
 #ifdef __cplusplus
 }

@@ -36,6 +36,9 @@ def _worker(rank, world, port, q):
     dt_max, ok = shard.reduce_max_min(dist, dt, ok=(rank == 0 or True), device="cpu")
     _, not_ok = shard.reduce_max_min(dist, dt, ok=(rank == 0), device="cpu")
     value = shard.aggregate_rate(world, nsig, 3, dt_max)
+    # the configs[4] stream aggregate: SUM of per-rank sigs over the MAX per-rank stream time
+    ssum, smax, sw = shard.reduce_sum_max(dist, units=1000 * (rank + 1), seconds=0.5 * (rank + 1), device="cpu")
+    assert (ssum, smax, sw) == (3000.0, 1.0, 2)
     q.put((rank, dt, dt_max, ok, not_ok, value, [g.numpy().tobytes() for g in gathered], nsig))
     dist.barrier()
     dist.destroy_process_group()
