@@ -376,6 +376,21 @@ fd_parse_kernel( unsigned char const *    __restrict__ payload,
   pflag[t] = ok ? 0u : 1u;
 }
 
+/* Batch SHA-512 (the fd_sha512_batch_* API, src/ballet/sha512/
+   fd_sha512.h:234-419, one message per lane instead of 4 / 8 AVX lanes):
+   hash + 64 t = SHA-512( data[ off[t], off[t]+sz[t] ) ). */
+__global__ void __launch_bounds__( FD_WG )
+fd_sha512_batch_kernel( unsigned char const * __restrict__ data, unsigned long const * __restrict__ off,
+                        unsigned int const * __restrict__ sz, u32 cnt, uint4 * __restrict__ hash ) {
+  u32 t = blockIdx.x * FD_WG + threadIdx.x;
+  if( t >= cnt ) return;
+  u32 h[16];
+  fd_sha512_bytes( h, data + off[t], sz[t] );
+  uint4 * o = hash + (size_t)t*4;
+#pragma unroll
+  for( int i=0; i<4; i++ ) o[i] = make_uint4( h[4*i], h[4*i+1], h[4*i+2], h[4*i+3] );
+}
+
 /* [e]B for e in [0,128], affine precomputed (y+x, y-x, 2dxy), canonical,
    packed 8x32.  Generated on the device at context creation (the GPU
    analogue of table/fd_curve25519_table_*.c fd_ed25519_base_point_wnaf_table). */
@@ -672,6 +687,45 @@ fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
   HIPCHK( hipStreamSynchronize( st ), -2 );
   memcpy( txn_out, sl.h_txn_out, txn_cnt );
   return 0;
+}
+
+/* ---- batch SHA-512 ---------------------------------------------------- */
+
+extern "C" int
+fdgpu_sha512_batch_device( unsigned char const * d_data, unsigned long const * d_off, unsigned int const * d_sz,
+                           unsigned long cnt, unsigned char * d_hash, void * stream ) {
+  if( !cnt ) return 0;
+  if( cnt >= (1UL<<31) ) { fd_err = "batch too large"; return -1; }
+  unsigned g = (unsigned)( (cnt + FD_WG - 1) / FD_WG );
+  hipLaunchKernelGGL( fd_sha512_batch_kernel, dim3(g), dim3(FD_WG), 0, (hipStream_t)stream, d_data, d_off, d_sz,
+                      (u32)cnt, (uint4 *)d_hash );
+  HIPCHK( hipGetLastError(), -3 );
+  return 0;
+}
+
+extern "C" int
+fdgpu_sha512_batch_host( int device, unsigned char const * data, unsigned long data_sz, unsigned long const * off,
+                         unsigned int const * sz, unsigned long cnt, unsigned char * hash ) {
+  if( !cnt ) return 0;
+  for( unsigned long t=0; t<cnt; t++ )
+    if( off[t] > data_sz || sz[t] > data_sz - off[t] ) { fd_err = "message out of buffer"; return -1; }
+  HIPCHK( hipSetDevice( device ), -2 );
+  unsigned char * d_data = NULL, * d_hash = NULL; unsigned long * d_off = NULL; unsigned int * d_sz = NULL;
+  size_t slack = 256;                                   /* fd_sha512_bytes reads past the last block */
+  int rc = -2;
+  if( hipMalloc( (void **)&d_data, data_sz + slack ) != hipSuccess ||
+      hipMalloc( (void **)&d_off, cnt * sizeof(unsigned long) ) != hipSuccess ||
+      hipMalloc( (void **)&d_sz, cnt * sizeof(unsigned int) ) != hipSuccess ||
+      hipMalloc( (void **)&d_hash, cnt * 64UL ) != hipSuccess ) { fd_err = "hipMalloc failed"; goto done; }
+  if( hipMemset( d_data + data_sz, 0, slack ) != hipSuccess ||
+      hipMemcpy( d_data, data, data_sz, hipMemcpyHostToDevice ) != hipSuccess ||
+      hipMemcpy( d_off, off, cnt * sizeof(unsigned long), hipMemcpyHostToDevice ) != hipSuccess ||
+      hipMemcpy( d_sz, sz, cnt * sizeof(unsigned int), hipMemcpyHostToDevice ) != hipSuccess ) { fd_err = "upload failed"; goto done; }
+  rc = fdgpu_sha512_batch_device( d_data, d_off, d_sz, cnt, d_hash, NULL );
+  if( !rc && hipMemcpy( hash, d_hash, cnt * 64UL, hipMemcpyDeviceToHost ) != hipSuccess ) { fd_err = "download failed"; rc = -2; }
+done:
+  hipFree( d_data ); hipFree( d_off ); hipFree( d_sz ); hipFree( d_hash );
+  return rc;
 }
 
 /* ---- raw-payload batches (device fd_txn_parse + verify) ------------- */

@@ -140,3 +140,41 @@ FD_DEV void fd_sha512_RAM( u32 out[ 16 ], u32 const R[ 8 ], u32 const A[ 8 ],
 #pragma unroll
   for( int i=0; i<8; i++ ) { out[2*i] = fd_bswap32( (u32)(h[i] >> 32) ); out[2*i+1] = fd_bswap32( (u32)h[i] ); }
 }
+
+/* SHA-512( M ) of msg_sz bytes at msg (any alignment) -> digest bytes as
+   16 words in digest byte order.  Reads up to 132 bytes past the last
+   whole block of the message; the caller's buffer carries that slack. */
+FD_DEV void fd_sha512_bytes( u32 out[ 16 ], unsigned char const * msg, u32 msg_sz ) {
+  u64 h[8] = { 0x6a09e667f3bcc908UL, 0xbb67ae8584caa73bUL, 0x3c6ef372fe94f82bUL, 0xa54ff53a5f1d36f1UL,
+               0x510e527fade682d1UL, 0x9b05688c2b3e6c1fUL, 0x1f83d9abfb41bd6bUL, 0x5be0cd19137e2179UL };
+  u32 L  = msg_sz;
+  u32 nb = ( L + 17u + 127u ) >> 7;
+#pragma unroll 1
+  for( u32 b=0; b<nb; b++ ) {
+    u64 w[16];
+    u32 lw[32];
+    /* blocks wholly past the message (the last one or two: padding and
+       length only) read nothing */
+    if( 128u*b < L ) fd_load_words<32>( lw, msg + 128u*b );
+    else {
+#pragma unroll
+      for( int i=0; i<32; i++ ) lw[i] = 0u;
+    }
+#pragma unroll
+    for( int i=0; i<16; i++ ) {
+      u64 x = ((u64)fd_bswap32( lw[2*i] ) << 32) | (u64)fd_bswap32( lw[2*i+1] );
+      int pos = (int)(128u*b) + 8*i;
+      int nv  = (int)L - pos;
+      u64 m = nv>=8 ? ~0UL : ( nv<=0 ? 0UL : ( ~0UL << (8*(8-nv)) ) );
+      x &= m;
+      if( nv>=0 && nv<8 ) x |= 0x80UL << (8*(7-nv));
+      if( b==nb-1u && i==15 ) x = (u64)L << 3;
+      if( b==nb-1u && i==14 ) x = 0UL;
+      w[i] = x;
+    }
+    fd_sha512_block( h, w );
+  }
+#pragma unroll
+  for( int i=0; i<8; i++ ) { out[2*i] = fd_bswap32( (u32)(h[i] >> 32) ); out[2*i+1] = fd_bswap32( (u32)h[i] ); }
+}
+

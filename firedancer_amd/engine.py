@@ -44,7 +44,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_verify_txns_host", "fdgpu_txn_parse_device", "fdgpu_ed25519_verify_raw_device",
            "fdgpu_ed25519_verify_raw_host", "fdgpu_ed25519_submit", "fdgpu_ed25519_flush",
            "fdgpu_ed25519_poll", "fdgpu_ed25519_submit_raw", "fdgpu_ed25519_poll_raw",
-           "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
+           "fdgpu_ed25519_pipeline_state", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_last_error")
 
 _lib = None
@@ -98,6 +98,11 @@ def load_library():
         L.fdgpu_ed25519_verify_raw_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
                                                     ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
                                                     ctypes.c_void_p]
+        L.fdgpu_sha512_batch_device.restype = ctypes.c_int
+        L.fdgpu_sha512_batch_device.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p]
+        L.fdgpu_sha512_batch_host.restype = ctypes.c_int
+        L.fdgpu_sha512_batch_host.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p]
         L.fdgpu_ed25519_submit.restype = ctypes.c_int
         L.fdgpu_ed25519_submit.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ushort, ctypes.c_ubyte,
                                            ctypes.c_ushort, ctypes.c_ushort, ctypes.c_ubyte, ctypes.c_ulong]
@@ -147,6 +152,24 @@ def txn_parse_device(d_payload: int, d_raw: int, txn_cnt: int, d_img: int | None
     rc = load_library().fdgpu_txn_parse_device(d_payload, d_raw, txn_cnt, d_img, img_stride, d_fp, stream)
     if rc:
         raise RuntimeError(f"fdgpu_txn_parse_device: {rc} {last_error()}")
+
+
+def sha512_batch(msgs, device: int = 0) -> list[bytes]:
+    """SHA-512 of each message on the GPU (fdgpu_sha512_batch_host)."""
+    L = load_library()
+    off = np.zeros(len(msgs), np.uint64)
+    sz = np.zeros(len(msgs), np.uint32)
+    pos = 0
+    for i, m in enumerate(msgs):
+        off[i], sz[i] = pos, len(m)
+        pos += len(m)
+    data = np.frombuffer(b"".join(bytes(m) for m in msgs) + b"\0", np.uint8)
+    out = np.zeros((len(msgs), 64), np.uint8)
+    rc = L.fdgpu_sha512_batch_host(device, data.ctypes.data, pos, off.ctypes.data, sz.ctypes.data, len(msgs),
+                                   out.ctypes.data)
+    if rc:
+        raise RuntimeError(f"fdgpu_sha512_batch_host: {rc} {last_error()}")
+    return [out[i].tobytes() for i in range(len(msgs))]
 
 
 def raw_records(payload: np.ndarray, off: np.ndarray, sz: np.ndarray):

@@ -223,6 +223,29 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t *   ctx,
                                unsigned long           img_stride,
                                unsigned short *        fp );
 
+/* Batch SHA-512 (replaces fd_sha512_batch_init / add / fini,
+   src/ballet/sha512/fd_sha512.h:234-419, for any number of messages):
+   hash[64 t, 64 t + 64) = SHA-512 of the sz[t] bytes at data + off[t].
+   The device form reads up to 132 bytes past each message's last whole
+   128-byte block, so d_data must carry 256 readable bytes of slack after
+   its last message.  The host form copies, runs on `device` and waits. */
+int
+fdgpu_sha512_batch_device( unsigned char const * d_data,
+                           unsigned long const * d_off,
+                           unsigned int const *  d_sz,
+                           unsigned long         cnt,
+                           unsigned char *       d_hash,
+                           void *                stream );
+
+int
+fdgpu_sha512_batch_host( int                   device,
+                         unsigned char const * data,
+                         unsigned long         data_sz,
+                         unsigned long const * off,
+                         unsigned int const *  sz,
+                         unsigned long         cnt,
+                         unsigned char *       hash );
+
 /* Async submit / poll pipeline (the offload shape fd_verify_tile needs,
    SURVEY.md §8b).  submit copies one transaction payload into the
    current pinned staging slot; when the slot fills (or on flush) it is
