@@ -689,6 +689,51 @@ fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
   return 0;
 }
 
+/* Independent (msg, sig, pub) triples -- the batched form of
+   fd_ed25519_verify for callers that verify unrelated messages (gossip
+   CRDS values and ping/pong, fd_gossvf_tile.c:367-446; precompiles).
+   Each triple is packed sig | pub | msg into the staging arena as a
+   one-signer transaction; chunks of up to max_txn triples. */
+extern "C" int
+fdgpu_ed25519_verify_many_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * const * msgs,
+                                unsigned long const * msg_szs, unsigned char const * const * sigs,
+                                unsigned char const * const * pubs, unsigned long cnt, signed char * out ) {
+  if( !ctx ) { fd_err = "NULL ctx"; return -1; }
+  if( !ctx->slot[0].h_payload ) { fd_err = "ctx has no staging buffers (max_payload_bytes==0)"; return -3; }
+  if( async_busy( ctx ) ) { fd_err = "async batches pending or in flight"; return -1; }
+  for( unsigned long i=0; i<cnt; i++ )
+    if( msg_szs[i] > 0xffffUL - 96UL || 96UL + msg_szs[i] + 8UL > ctx->max_payload ) { fd_err = "message too long"; return -1; }
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  fd_slot & sl = ctx->slot[0];
+  hipStream_t st = ctx->stream;
+  unsigned long done = 0;
+  while( done < cnt ) {
+    unsigned long n = 0; size_t used = 0;
+    while( done + n < cnt && n < ctx->max_txn && n < ctx->max_sig ) {
+      unsigned long i = done + n;
+      size_t need = 96UL + msg_szs[i];
+      if( used + need + 8UL > ctx->max_payload ) break;
+      unsigned char * b = sl.h_payload + used;
+      memcpy( b, sigs[i], 64 ); memcpy( b + 64, pubs[i], 32 );
+      if( msg_szs[i] ) memcpy( b + 96, msgs[i], msg_szs[i] );
+      fdgpu_txn_desc_t & d = sl.h_desc[n];
+      d.payload_off = (unsigned)used; d.sig_base = (unsigned)n; d.payload_sz = (unsigned short)need;
+      d.message_off = 96; d.acct_addr_off = 64; d.signature_off = 0; d.sig_cnt = 1;
+      used = ( used + need + 7UL ) & ~(size_t)7; n++;
+    }
+    memset( sl.h_payload + used, 0, FD_ARENA_SLACK );
+    HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+    HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, n * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
+    int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, n, n, sl.d_txn_out, NULL, st );
+    if( rc ) return rc;
+    HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, n, hipMemcpyDeviceToHost, st ), -2 );
+    HIPCHK( hipStreamSynchronize( st ), -2 );
+    memcpy( out + done, sl.h_txn_out, n );
+    done += n;
+  }
+  return 0;
+}
+
 /* ---- batch SHA-512 ---------------------------------------------------- */
 
 extern "C" int

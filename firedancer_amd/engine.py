@@ -44,7 +44,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_verify_txns_host", "fdgpu_txn_parse_device", "fdgpu_ed25519_verify_raw_device",
            "fdgpu_ed25519_verify_raw_host", "fdgpu_ed25519_submit", "fdgpu_ed25519_flush",
            "fdgpu_ed25519_poll", "fdgpu_ed25519_submit_raw", "fdgpu_ed25519_poll_raw",
-           "fdgpu_ed25519_pipeline_state", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
+           "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_last_error")
 
 _lib = None
@@ -98,6 +98,8 @@ def load_library():
         L.fdgpu_ed25519_verify_raw_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_void_p,
                                                     ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong,
                                                     ctypes.c_void_p]
+        L.fdgpu_ed25519_verify_many_host.restype = ctypes.c_int
+        L.fdgpu_ed25519_verify_many_host.argtypes = [ctypes.c_void_p] * 5 + [ctypes.c_ulong, ctypes.c_void_p]
         L.fdgpu_sha512_batch_device.restype = ctypes.c_int
         L.fdgpu_sha512_batch_device.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p]
         L.fdgpu_sha512_batch_host.restype = ctypes.c_int
@@ -240,6 +242,20 @@ class Engine:
                                                      d_sig_out, stream)
         if rc:
             raise RuntimeError(f"fdgpu_ed25519_verify_txns_device: {rc} {last_error()}")
+
+    def verify_many(self, msgs, sigs, pubs) -> np.ndarray:
+        """fd_ed25519_verify codes of independent (msg, sig, pub) triples (fdgpu_ed25519_verify_many_host)."""
+        n = len(msgs)
+        keep = [np.frombuffer(bytes(x) + b"\0", np.uint8) for x in list(msgs) + list(sigs) + list(pubs)]
+        ptrs = np.array([k.ctypes.data for k in keep], np.uint64)
+        szs = np.array([len(m) for m in msgs], np.uint64)
+        out = np.zeros(n, np.int8)
+        rc = self.L.fdgpu_ed25519_verify_many_host(self.ctx, ptrs[:n].ctypes.data, szs.ctypes.data,
+                                                   ptrs[n:2 * n].ctypes.data, ptrs[2 * n:].ctypes.data, n,
+                                                   out.ctypes.data)
+        if rc:
+            raise RuntimeError(f"fdgpu_ed25519_verify_many_host: {rc} {last_error()}")
+        return out
 
     # -- raw payloads: device fd_txn_parse + verify ---------------------------
     def verify_raw_host(self, payload: np.ndarray, off: np.ndarray, sz: np.ndarray, want_img: bool = False):

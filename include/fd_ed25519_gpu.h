@@ -223,6 +223,20 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t *   ctx,
                                unsigned long           img_stride,
                                unsigned short *        fp );
 
+/* fdgpu_ed25519_verify_many_host: out[i] = fd_ed25519_verify( msgs[i],
+   msg_szs[i], sigs[i], pubs[i] ) for cnt independent triples, in GPU
+   batches of up to max_txn (the batched form of fd_ed25519_verify for the
+   gossip / precompile callers).  Synchronous; needs a ctx
+   with staging (max_payload_bytes > 0); messages up to 65439 bytes. */
+int
+fdgpu_ed25519_verify_many_host( fdgpu_ed25519_ctx_t *         ctx,
+                                unsigned char const * const * msgs,
+                                unsigned long const *         msg_szs,
+                                unsigned char const * const * sigs,
+                                unsigned char const * const * pubs,
+                                unsigned long                 cnt,
+                                signed char *                 out );
+
 /* Batch SHA-512 (replaces fd_sha512_batch_init / add / fini,
    src/ballet/sha512/fd_sha512.h:234-419, for any number of messages):
    hash[64 t, 64 t + 64) = SHA-512 of the sz[t] bytes at data + off[t].

@@ -173,3 +173,16 @@ def test_mad_probe(fa):
     r.fdgpu_mad_peak_per_s.argtypes = [ctypes.c_int]
     v = r.fdgpu_mad_peak_per_s(0)
     assert v > 1e12, v
+
+
+@pytest.mark.parametrize("sem,key", [(0, "code_avx"), (1, "code_ref")])
+def test_verify_many_golden(fa, golden, sem, key):
+    """fdgpu_ed25519_verify_many_host (independent triples, the gossip-style caller) on every
+    single-signature golden vector, in several GPU batches (max_txn 300)."""
+    v = golden["vectors"]
+    n = len(v["msg_sz"])
+    msgs = [v["msg_arena"][v["msg_off"][i]: v["msg_off"][i] + v["msg_sz"][i]].tobytes() for i in range(n)]
+    eng = fa.Engine(device=0, max_txn=300, max_sig=300, max_payload=300 * 1400, semantics=sem)
+    got = eng.verify_many(msgs, [v["sig"][i].tobytes() for i in range(n)], [v["pub"][i].tobytes() for i in range(n)])
+    eng.close()
+    np.testing.assert_array_equal(got, v[key])
