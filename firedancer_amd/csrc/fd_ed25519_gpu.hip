@@ -440,7 +440,10 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   unsigned long      cursor;   /* results already handed out by poll */
   hipEvent_t         done;
   int                state;    /* 0 filling, 1 in flight / draining */
-  int                mode;     /* 0 desc (fdgpu_ed25519_submit), 1 raw (fdgpu_ed25519_submit_raw) */
+  int                mode;     /* 0 desc (fdgpu_ed25519_submit), 1 raw (fdgpu_ed25519_submit_raw),
+                                  2 raw in place (fdgpu_ed25519_submit_raw_ref) */
+  unsigned char const * ref_base; /* mode 2: the caller's pinned region; payloads at [ref_lo, ref_hi) */
+  size_t             ref_lo, ref_hi;
 };
 
 struct fdgpu_ed25519_ctx {
@@ -871,8 +874,12 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
 static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
   fd_slot & sl = ctx->slot[i];
   hipStream_t st = ctx->stream;
-  memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
-  HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+  if( sl.mode==2 ) {   /* in place: one upload of the caller's region range, no host copy */
+    HIPCHK( hipMemcpyAsync( sl.d_payload, sl.ref_base + sl.ref_lo, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+  } else {
+    memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
+    HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+  }
   HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
   int rc = sl.mode
          ? launch_raw( ctx, sl.d_payload, (fdgpu_txn_raw_t const *)sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out,
@@ -880,7 +887,7 @@ static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
          : launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
   if( rc ) return rc;
   HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
-  if( sl.mode ) {
+  if( sl.mode ) {   /* raw and in-place raw */
     HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
     HIPCHK( hipMemcpyAsync( sl.h_img, sl.d_img, sl.txn_cnt * FDGPU_TXN_IMG_STRIDE, hipMemcpyDeviceToHost, st ), -2 );
   }
@@ -971,6 +978,44 @@ fdgpu_ed25519_submit_raw( fdgpu_ed25519_ctx_t * ctx, unsigned char const * paylo
   sl->txn_cnt++; sl->sig_cnt += lanes; sl->payload_used = (off + payload_sz + 7) & ~(size_t)7;
   return 0;
 }
+
+/* In-place raw submission: the payload already sits in a pinned host
+   region the caller owns (the tile's out dcache, allocated with
+   fdgpu_host_alloc); a batch uploads the contiguous range of its
+   payloads straight from there.  Payloads of one batch must be at
+   increasing addresses in one region (a ring wrap simply starts a new
+   batch), with 512 readable bytes after each. */
+extern "C" int
+fdgpu_ed25519_submit_raw_ref( fdgpu_ed25519_ctx_t * ctx, unsigned char const * base, unsigned char const * payload,
+                              unsigned short payload_sz, unsigned long tag ) {
+  unsigned b0 = payload_sz ? payload[0] : 0u;
+  unsigned lanes = ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u;
+  size_t off = (size_t)( payload - base );
+  int rc; fd_slot * sl = slot_for( ctx, 0UL, lanes, 2, &rc );
+  if( !sl ) return rc;
+  if( sl->txn_cnt && ( sl->ref_base != base || off < sl->ref_hi || off + payload_sz - sl->ref_lo + 8UL > ctx->max_payload ) ) {
+    if( ( rc = fdgpu_ed25519_flush( ctx ) ) ) return rc;
+    if( !( sl = slot_for( ctx, 0UL, lanes, 2, &rc ) ) ) return rc;
+  }
+  if( slot_raw_bufs( ctx, sl ) ) return -3;
+  if( !sl->txn_cnt ) { sl->ref_base = base; sl->ref_lo = off; }
+  fdgpu_txn_raw_t & r = ((fdgpu_txn_raw_t *)sl->h_desc)[ sl->txn_cnt ];
+  r.payload_off = (unsigned)( off - sl->ref_lo ); r.sig_base = (unsigned)sl->sig_cnt; r.payload_sz = payload_sz;
+  r.sig_lanes = (unsigned char)lanes;
+  sl->h_tags[ sl->txn_cnt ] = tag;
+  sl->txn_cnt++; sl->sig_cnt += lanes;
+  sl->ref_hi = off + payload_sz; sl->payload_used = sl->ref_hi - sl->ref_lo;
+  return 0;
+}
+
+extern "C" void *
+fdgpu_host_alloc( unsigned long sz ) {
+  void * p = NULL;
+  if( hipHostMalloc( &p, sz, hipHostMallocDefault ) != hipSuccess ) { fd_err = "hipHostMalloc failed"; return NULL; }
+  return p;
+}
+
+extern "C" void fdgpu_host_free( void * p ) { if( p ) hipHostFree( p ); }
 
 /* Drain completed slots in submission order, at most max results. */
 static unsigned long

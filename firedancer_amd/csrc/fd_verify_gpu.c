@@ -222,10 +222,12 @@ fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ul
   if( !batch_txn || !tcache_depth || out_dcache_bytes < 8UL*VT_RESERVE_MAX ) return NULL;
   fdgpu_vtile_t * vt = (fdgpu_vtile_t *)calloc( 1, sizeof(fdgpu_vtile_t) );
   if( !vt ) return NULL;
-  vt->ctx = fdgpu_ed25519_ctx_new( device, batch_txn, 16UL*batch_txn, batch_txn*(1232UL+8UL), semantics );
+  /* staging arena of a batch = its range of the out dcache (in-place submits): up to
+     batch_txn records of at most VT_RESERVE_MAX bytes (rounded to chunk pairs) */
+  vt->ctx = fdgpu_ed25519_ctx_new( device, batch_txn, 16UL*batch_txn, batch_txn*2304UL + 1024UL, semantics );
   vt->tcache = fdgpu_tcache_new( tcache_depth );
   ulong nchunk = ( out_dcache_bytes / FDGPU_CHUNK_SZ ) & ~1UL;
-  vt->dcache = (uchar *)aligned_alloc( 128, nchunk * FDGPU_CHUNK_SZ );
+  vt->dcache = (uchar *)fdgpu_host_alloc( nchunk * FDGPU_CHUNK_SZ );   /* pinned: batches upload from it in place */
   ulong rchunk = ( ( VT_RESERVE_MAX + 127UL ) >> 7 ) << 1;
   vt->chunk0 = 0UL; vt->wmark = nchunk - rchunk; vt->out_chunk = 0UL;
   /* frags in flight: the ring must hold them all plus one wrap's waste */
@@ -249,7 +251,7 @@ fdgpu_vtile_delete( fdgpu_vtile_t * vt ) {
   if( !vt ) return;
   if( vt->ctx ) fdgpu_ed25519_ctx_delete( vt->ctx );
   fdgpu_tcache_delete( vt->tcache );
-  free( vt->dcache ); free( vt->pend ); free( vt->p_tags ); free( vt->p_codes ); free( vt->p_img ); free( vt->p_fp );
+  fdgpu_host_free( vt->dcache ); free( vt->pend ); free( vt->p_tags ); free( vt->p_codes ); free( vt->p_img ); free( vt->p_fp );
   free( vt );
 }
 
@@ -279,7 +281,7 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_ed25519_flush( vt->ctx ); return -2; }
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
   memcpy( dst, frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
-  int rc = fdgpu_ed25519_submit_raw( vt->ctx, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
+  int rc = fdgpu_ed25519_submit_raw_ref( vt->ctx, vt->dcache, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
   if( rc ) return rc;
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
   p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk;
@@ -365,6 +367,7 @@ typedef struct {
   ulong                  t_start, t_end;
   _Atomic ulong          t_last;
   _Atomic ulong          sigs, published, overruns;
+  _Atomic ulong          ns[4];        /* summed over tiles: during_frag, after_frags, housekeep, loop total */
   ulong                  metrics[5];
   pthread_mutex_t        mu;
   int                    device; ulong batch_txn, max_inflight;
@@ -439,6 +442,7 @@ static void * sb_tile( void * _a ) {
   for( ulong seq=0; seq<s->n_frags; ) mine += ( seq++ % (ulong)s->tiles ) == (ulong)idx;
   ulong seq = 0UL;
   ulong last_seq = ~0UL, last_got = ~0UL, t_prog = now_ns();
+  ulong t_hk = 0UL, ns_during = 0UL, ns_after = 0UL, ns_hk = 0UL, t_begin = now_ns();
   while( got < mine ) {
     if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) break;
     if( seq != last_seq || got != last_got ) { last_seq = seq; last_got = got; t_prog = now_ns(); }
@@ -449,15 +453,18 @@ static void * sb_tile( void * _a ) {
                idx, seq, got, mine, fdgpu_vtile_pending( vt ), filling, inflight );
       atomic_store( &s->fail, 5 ); break;
     }
-    int progressed = 0;
     if( seq < s->n_frags ) {
       fdgpu_frag_meta_t m;
       int r = fdgpu_mcache_poll( s->mc, seq, &m );
       if( r == 0 ) {
         if( (seq % (ulong)s->tiles) == (ulong)idx ) {            /* before_frag round robin */
+          ulong t0 = now_ns();
           int rc = fdgpu_vtile_during_frag( vt, s->in_dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, seq, m.tsorig );
+          ns_during += now_ns() - t0;
           if( rc == -2 ) {                                          /* staging full: drain, retry this seq */
+            ulong t1 = now_ns();
             ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
+            ns_after += now_ns() - t1;
             sb_account( s, vt, done, n, &sigs ); got += n;
             continue;
           }
@@ -465,17 +472,27 @@ static void * sb_tile( void * _a ) {
         }
         seq++;
         if( !(seq & 63UL) || seq==s->n_frags ) atomic_store_explicit( &s->fseq[idx].v, seq, memory_order_release );   /* batched credit return */
-        progressed = 1;
       } else if( r < 0 ) {
         atomic_fetch_add( &s->overruns, 1 ); atomic_store( &s->fail, 3 ); break;
       }
     }
-    if( !progressed || !(seq & 15UL) ) fdgpu_vtile_housekeep( vt, s->max_inflight );   /* adaptive batching */
-    if( !progressed || (seq & 255UL) == 0 ) {
+    /* housekeeping: launch / drain at most every 10 us while frags flow
+       (the HIP runtime calls behind them take locks shared by all tiles) */
+    ulong tnow = now_ns();
+    if( tnow - t_hk >= 10000UL ) {
+      t_hk = tnow;
+      ulong t0 = now_ns();
+      fdgpu_vtile_housekeep( vt, s->max_inflight );                 /* adaptive batching */
+      ulong t1 = now_ns();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
+      ulong t2 = now_ns();
       sb_account( s, vt, done, n, &sigs ); got += n;
+      ns_hk += t1 - t0; ns_after += t2 - t1;
     }
   }
+  ulong t_end = now_ns();
+  atomic_fetch_add( &s->ns[0], ns_during ); atomic_fetch_add( &s->ns[1], ns_after );
+  atomic_fetch_add( &s->ns[2], ns_hk );     atomic_fetch_add( &s->ns[3], t_end - t_begin );
   ulong m5[5]; fdgpu_vtile_metrics( vt, m5 );
   pthread_mutex_lock( &s->mu );
   for( int i=0; i<5; i++ ) s->metrics[i] += m5[i];
@@ -539,6 +556,7 @@ fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, uns
     st->lat_max_us = s->lat_us[ n_frags-1UL ];
     memcpy( st->metrics, s->metrics, sizeof(st->metrics) );
     st->overruns = atomic_load( &s->overruns );
+    for( int i=0; i<4; i++ ) st->tile_ns[i] = atomic_load( &s->ns[i] );
   }
   fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( s->frag_chunk ); free( (void *)s->fseq ); free( s->lat_us );
   pthread_mutex_destroy( &s->mu );

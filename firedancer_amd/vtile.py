@@ -42,7 +42,7 @@ class StreamStats(ctypes.Structure):
     _fields_ = [("seconds", ctypes.c_double), ("frags", ctypes.c_ulong), ("sigs", ctypes.c_ulong),
                 ("published", ctypes.c_ulong), ("frags_per_s", ctypes.c_double), ("sigs_per_s", ctypes.c_double),
                 ("lat_p50_us", ctypes.c_double), ("lat_p99_us", ctypes.c_double), ("lat_max_us", ctypes.c_double),
-                ("metrics", ctypes.c_ulong * 5), ("overruns", ctypes.c_ulong)]
+                ("metrics", ctypes.c_ulong * 5), ("overruns", ctypes.c_ulong), ("tile_ns", ctypes.c_ulong * 4)]
 
 
 _lib = None
@@ -181,4 +181,4 @@ def stream_bench(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: 
     return {"seconds": st.seconds, "frags": st.frags, "sigs": st.sigs, "published": st.published,
             "frags_per_s": st.frags_per_s, "sigs_per_s": st.sigs_per_s, "lat_p50_us": st.lat_p50_us,
             "lat_p99_us": st.lat_p99_us, "lat_max_us": st.lat_max_us, "metrics": list(st.metrics),
-            "overruns": st.overruns}
+            "overruns": st.overruns, "tile_ns": list(st.tile_ns)}

@@ -312,6 +312,26 @@ fdgpu_ed25519_submit_raw( fdgpu_ed25519_ctx_t * ctx,
                           unsigned short        payload_sz,
                           unsigned long         tag );
 
+/* In-place form (zero-copy staging): the payload already sits at
+   `payload` inside a pinned region starting at `base` (the tile's out
+   dcache, allocated with fdgpu_host_alloc); a batch uploads the
+   contiguous range of its payloads straight from the region instead of
+   a staging copy.  Payloads of one batch must lie at increasing addresses
+   of one region (a lower address, e.g. a ring wrap, starts a new batch)
+   with 512 readable bytes after each; the caller keeps them unchanged
+   until poll_raw returns their verdicts.  Completions come back through
+   fdgpu_ed25519_poll_raw. */
+int
+fdgpu_ed25519_submit_raw_ref( fdgpu_ed25519_ctx_t * ctx,
+                              unsigned char const * base,
+                              unsigned char const * payload,
+                              unsigned short        payload_sz,
+                              unsigned long         tag );
+
+/* pinned (page-locked) host memory for fdgpu_ed25519_submit_raw_ref regions */
+void * fdgpu_host_alloc( unsigned long sz );
+void   fdgpu_host_free ( void * p );
+
 unsigned long
 fdgpu_ed25519_poll_raw( fdgpu_ed25519_ctx_t * ctx,
                         unsigned long *       out_tags,
