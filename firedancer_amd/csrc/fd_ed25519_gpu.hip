@@ -513,6 +513,52 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
   return 0;
 }
 
+extern "C" void fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx );
+
+/* allocations of a new context; on failure the caller deletes the
+   partially built context (every handle starts NULL) */
+static int
+ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned long max_sig,
+          unsigned long max_payload_bytes, int semantics ) {
+  ctx->device = device; ctx->semantics = semantics; ctx->timing = 0;
+  ctx->max_txn = max_txn; ctx->max_sig = max_sig; ctx->max_payload = max_payload_bytes;
+  size_t ns = max_sig;
+  HIPCHK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_map,  ns * sizeof(u32) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_code, ns ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_pstat, 2*ns ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_tab,  ns * FD_ATAB_ENTRIES * 8 * sizeof(uint4) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_Rxy,  ns * 4 * sizeof(uint4) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_Axy,  ns * 4 * sizeof(uint4) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_digA, ns * 64 ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_digB, ns * 32 ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_btab, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_rdesc, max_txn * sizeof(fdgpu_txn_desc_t) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_pflag, max_txn ), -1 );
+  for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
+  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
+  ctx->ring_cnt = 0;
+  hipLaunchKernelGGL( fd_btab_kernel, dim3(1), dim3(FD_BTAB_ENTRIES), 0, ctx->stream, ctx->d_btab );
+  HIPCHK( hipGetLastError(), -1 );
+  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
+    fd_slot & sl = ctx->slot[i];
+    if( max_payload_bytes ) {
+      HIPCHK( hipHostMalloc( (void**)&sl.h_payload, max_payload_bytes + FD_ARENA_SLACK, hipHostMallocDefault ), -1 );
+      HIPCHK( hipHostMalloc( (void**)&sl.h_desc, max_txn * sizeof(fdgpu_txn_desc_t), hipHostMallocDefault ), -1 );
+      HIPCHK( hipHostMalloc( (void**)&sl.h_txn_out, max_txn, hipHostMallocDefault ), -1 );
+      HIPCHK( hipHostMalloc( (void**)&sl.h_tags, max_txn * sizeof(unsigned long), hipHostMallocDefault ), -1 );
+      HIPCHK( hipMalloc( &sl.d_payload, max_payload_bytes + FD_ARENA_SLACK ), -1 );
+      HIPCHK( hipMalloc( &sl.d_desc, max_txn * sizeof(fdgpu_txn_desc_t) ), -1 );
+      HIPCHK( hipMalloc( &sl.d_txn_out, max_txn ), -1 );
+      memset( sl.h_payload, 0, max_payload_bytes + FD_ARENA_SLACK );
+    }
+    HIPCHK( hipEventCreateWithFlags( &sl.done, hipEventDisableTiming ), -1 );
+  }
+  ctx->cur = 0;
+  HIPCHK( hipStreamSynchronize( ctx->stream ), -1 );
+  return 0;
+}
+
 extern "C" fdgpu_ed25519_ctx_t *
 fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
                        unsigned long max_payload_bytes, int semantics ) {
@@ -520,63 +566,38 @@ fdgpu_ed25519_ctx_new( int device, unsigned long max_txn, unsigned long max_sig,
   if( semantics!=FDGPU_SEMANTICS_AVX512 && semantics!=FDGPU_SEMANTICS_REF ) { fd_err = "bad semantics"; return NULL; }
   HIPCHK( hipSetDevice( device ), NULL );
   fdgpu_ed25519_ctx_t * ctx = new fdgpu_ed25519_ctx_t();
-  ctx->device = device; ctx->semantics = semantics; ctx->timing = 0;
-  ctx->max_txn = max_txn; ctx->max_sig = max_sig; ctx->max_payload = max_payload_bytes;
-  size_t ns = max_sig;
-  HIPCHK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_map,  ns * sizeof(u32) ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_code, ns ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_pstat, 2*ns ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_tab,  ns * FD_ATAB_ENTRIES * 8 * sizeof(uint4) ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_Rxy,  ns * 4 * sizeof(uint4) ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_Axy,  ns * 4 * sizeof(uint4) ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_digA, ns * 64 ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_digB, ns * 32 ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_btab, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_rdesc, max_txn * sizeof(fdgpu_txn_desc_t) ), NULL );
-  HIPCHK( hipMalloc( &ctx->d_pflag, max_txn ), NULL );
-  for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), NULL );
-  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), NULL );
-  ctx->ring_cnt = 0;
-  hipLaunchKernelGGL( fd_btab_kernel, dim3(1), dim3(FD_BTAB_ENTRIES), 0, ctx->stream, ctx->d_btab );
-  HIPCHK( hipGetLastError(), NULL );
-  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
-    fd_slot & sl = ctx->slot[i];
-    memset( &sl, 0, sizeof(sl) );
-    if( max_payload_bytes ) {
-      HIPCHK( hipHostMalloc( (void**)&sl.h_payload, max_payload_bytes + FD_ARENA_SLACK, hipHostMallocDefault ), NULL );
-      HIPCHK( hipHostMalloc( (void**)&sl.h_desc, max_txn * sizeof(fdgpu_txn_desc_t), hipHostMallocDefault ), NULL );
-      HIPCHK( hipHostMalloc( (void**)&sl.h_txn_out, max_txn, hipHostMallocDefault ), NULL );
-      HIPCHK( hipHostMalloc( (void**)&sl.h_tags, max_txn * sizeof(unsigned long), hipHostMallocDefault ), NULL );
-      HIPCHK( hipMalloc( &sl.d_payload, max_payload_bytes + FD_ARENA_SLACK ), NULL );
-      HIPCHK( hipMalloc( &sl.d_desc, max_txn * sizeof(fdgpu_txn_desc_t) ), NULL );
-      HIPCHK( hipMalloc( &sl.d_txn_out, max_txn ), NULL );
-      memset( sl.h_payload, 0, max_payload_bytes + FD_ARENA_SLACK );
-    }
-    HIPCHK( hipEventCreateWithFlags( &sl.done, hipEventDisableTiming ), NULL );
+  if( ctx_init( ctx, device, max_txn, max_sig, max_payload_bytes, semantics ) ) {
+    std::string err = fd_err;
+    fdgpu_ed25519_ctx_delete( ctx );
+    fd_err = err;
+    return NULL;
   }
-  ctx->cur = 0;
-  HIPCHK( hipStreamSynchronize( ctx->stream ), NULL );
   return ctx;
 }
 
 extern "C" void
 fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   if( !ctx ) return;
-  hipSetDevice( ctx->device );
-  hipStreamSynchronize( ctx->stream );
-  hipFree( ctx->d_map ); hipFree( ctx->d_code ); hipFree( ctx->d_pstat ); hipFree( ctx->d_tab ); hipFree( ctx->d_Rxy ); hipFree( ctx->d_Axy );
-  hipFree( ctx->d_digA ); hipFree( ctx->d_digB ); hipFree( ctx->d_btab ); hipFree( ctx->d_rdesc ); hipFree( ctx->d_pflag );
-  for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ev[i] );
-  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) hipEventDestroy( ctx->ring[r][i] );
+  (void)hipSetDevice( ctx->device );
+  if( ctx->stream ) (void)hipStreamSynchronize( ctx->stream );
+  (void)hipFree( ctx->d_map ); (void)hipFree( ctx->d_code ); (void)hipFree( ctx->d_pstat ); (void)hipFree( ctx->d_tab );
+  (void)hipFree( ctx->d_Rxy ); (void)hipFree( ctx->d_Axy ); (void)hipFree( ctx->d_digA ); (void)hipFree( ctx->d_digB );
+  (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_rdesc ); (void)hipFree( ctx->d_pflag );
+  for( int i=0; i<4; i++ ) if( ctx->ev[i] ) (void)hipEventDestroy( ctx->ev[i] );
+  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) if( ctx->ring[r][i] ) (void)hipEventDestroy( ctx->ring[r][i] );
   for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
     fd_slot & sl = ctx->slot[i];
-    if( sl.h_payload ) { hipHostFree( sl.h_payload ); hipHostFree( sl.h_desc ); hipHostFree( sl.h_txn_out ); hipHostFree( sl.h_tags );
-                         hipFree( sl.d_payload ); hipFree( sl.d_desc ); hipFree( sl.d_txn_out ); }
-    if( sl.h_img ) { hipHostFree( sl.h_img ); hipHostFree( sl.h_fp ); hipFree( sl.d_img ); hipFree( sl.d_fp ); }
-    hipEventDestroy( sl.done );
+    if( sl.h_payload ) (void)hipHostFree( sl.h_payload );
+    if( sl.h_desc    ) (void)hipHostFree( sl.h_desc );
+    if( sl.h_txn_out ) (void)hipHostFree( sl.h_txn_out );
+    if( sl.h_tags    ) (void)hipHostFree( sl.h_tags );
+    if( sl.h_img     ) (void)hipHostFree( sl.h_img );
+    if( sl.h_fp      ) (void)hipHostFree( sl.h_fp );
+    (void)hipFree( sl.d_payload ); (void)hipFree( sl.d_desc ); (void)hipFree( sl.d_txn_out );
+    (void)hipFree( sl.d_img ); (void)hipFree( sl.d_fp );
+    if( sl.done ) (void)hipEventDestroy( sl.done );
   }
-  hipStreamDestroy( ctx->stream );
+  if( ctx->stream ) (void)hipStreamDestroy( ctx->stream );
   delete ctx;
 }
 

@@ -48,3 +48,23 @@ def test_desc_layout():
     assert engine.DESC_DTYPE.itemsize == 16
     assert [engine.DESC_DTYPE.fields[k][1] for k in engine.DESC_DTYPE.names] == [0, 4, 8, 10, 12, 14, 15]
     assert np.dtype(engine.DESC_DTYPE).names[-1] == "sig_cnt"
+
+
+def test_ctx_new_rejects_bad_sizes_without_gpu():
+    lib = engine.load_library()
+    assert not lib.fdgpu_ed25519_ctx_new(0, 0, 16, 0, 0)
+    assert engine.last_error() == "bad sizes"
+    assert not lib.fdgpu_ed25519_ctx_new(0, 16, 16, 0, 7)
+    assert engine.last_error() == "bad semantics"
+
+
+def test_raw_record_layout_and_staging():
+    import numpy as np
+    assert engine.RAW_DTYPE.itemsize == 16
+    assert [engine.RAW_DTYPE.fields[k][1] for k in engine.RAW_DTYPE.names] == [0, 4, 8, 10, 11]
+    # sig lanes = first payload byte when in 1..16 (fd_txn_parse.c:86), else 0; sig_base = prefix
+    payload = np.array([1, 0, 0, 3, 0, 0, 17, 0, 0, 0, 0, 0, 2, 0], np.uint8)
+    off = np.array([0, 3, 6, 9, 12], np.uint32)
+    sz = np.array([3, 3, 3, 0, 2], np.uint16)
+    raw, lanes = engine.raw_records(payload, off, sz)
+    assert raw["sig_lanes"].tolist() == [1, 3, 0, 0, 2] and raw["sig_base"].tolist() == [0, 1, 4, 4, 4] and lanes == 6
