@@ -10,9 +10,10 @@
                        the 9-entry table [0..8](-A) (cached form) -> HBM
      fd_dsm_kernel     [k](-A) + [S]B by signed fixed windows: 252
                        doublings, 64 table adds (entries gathered from HBM,
-                       prefetched one window ahead), 32 base-point adds from
-                       a 129-entry affine table held in LDS; projective
-                       compare with R -> FD_ED25519_SUCCESS / ERR_MSG
+                       prefetched one window ahead), 16 base-point adds from
+                       the [0..32768]B affine table (L2 / Infinity Cache
+                       resident); projective compare with R ->
+                       FD_ED25519_SUCCESS / ERR_MSG
      fd_reduce_kernel  per transaction: fd_ed25519_verify_batch_single_msg
                        code from its signatures' codes
      fd_parse_kernel   (raw-payload batches) per transaction: fd_txn_parse,
@@ -45,7 +46,21 @@
 
 #define FD_WG 256
 #define FD_ATAB_ENTRIES 9          /* [0..8](-A), cached form, 128 B each */
+/* Base-point window: FD_BWIN = 8 keeps [0..128]B (12.4 KB) in LDS and adds
+   it every 2nd A window (32 adds); FD_BWIN = 16 keeps [0..32768]B (3.1 MB,
+   L2 / Infinity-Cache resident) in HBM, gathered per lane one window
+   ahead, and adds it every 4th A window (16 adds). */
+#ifndef FD_BWIN
+#define FD_BWIN 16
+#endif
+#if FD_BWIN==8
 #define FD_BTAB_ENTRIES 129        /* [0..128]B, affine precomp, 96 B each */
+#elif FD_BWIN==16
+#define FD_BTAB_ENTRIES 32769      /* [0..32768]B */
+#else
+#error "FD_BWIN must be 8 or 16"
+#endif
+#define FD_BDIG ( 256 / FD_BWIN )  /* signed radix-2^FD_BWIN digits of S */
 #define FD_ARENA_SLACK  512UL      /* readable bytes past the last payload */
 #ifndef FD_DSM_PREFETCH
 #define FD_DSM_PREFETCH 1          /* issue the -A table gather before the window's doublings */
@@ -61,7 +76,7 @@ typedef signed char i8;
 /*         per-lane gather of a random entry moves exactly one line    */
 /*   Rxy : uint4 [nsig][4]   canonical x, y of R                       */
 /*   digA: i8    [64][nsig]  radix-16 signed digits of k (coalesced)   */
-/*   digB: i8    [32][nsig]  radix-256 signed digits of S              */
+/*   digB: short [FD_BDIG][nsig] radix-2^FD_BWIN signed digits of S   */
 /* ------------------------------------------------------------------ */
 
 FD_DEV void fe_store_packed( uint4 * dst, fe const & a ) {
@@ -166,7 +181,7 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
                 unsigned char const *    __restrict__ pstat,
                 i8 *                     __restrict__ code_out,
                 i8 *                     __restrict__ digA,
-                i8 *                     __restrict__ digB ) {
+                short *                  __restrict__ digB ) {
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
   size_t n = nsig;
@@ -209,10 +224,11 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
   }
   carry = 0;
 #pragma unroll
-  for( int i=0; i<32; i++ ) {
-    int v = (int)((Sw[i>>2] >> (8*(i&3))) & 255u) + carry;
-    carry = (v + 128) >> 8;
-    digB[(size_t)i*n + s] = (i8)(v - (carry << 8));
+  for( int i=0; i<FD_BDIG; i++ ) {
+    int bit = FD_BWIN*i;
+    int v = (int)((Sw[bit>>5] >> (bit&31)) & ((1u<<FD_BWIN)-1u)) + carry;
+    carry = (v + (1<<(FD_BWIN-1))) >> FD_BWIN;
+    digB[(size_t)i*n + s] = (short)(v - (carry << FD_BWIN));
   }
 }
 
@@ -253,12 +269,14 @@ fd_dsm_kernel( u32                      nsig,
                uint4 const * __restrict__ tab,
                uint4 const * __restrict__ Rxy,
                i8 const *    __restrict__ digA,
-               i8 const *    __restrict__ digB,
+               short const * __restrict__ digB,
                uint4 const * __restrict__ btab_g,
                i8 *          __restrict__ code ) {
+#if FD_BWIN==8
   __shared__ uint4 btab[ FD_BTAB_ENTRIES * 6 ];
   for( int i=threadIdx.x; i<FD_BTAB_ENTRIES*6; i+=FD_WG ) btab[i] = btab_g[i];
   __syncthreads();
+#endif
 
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
@@ -270,10 +288,21 @@ fd_dsm_kernel( u32                      nsig,
   atab_raw raw;
   int da = digA[ (size_t)63*n + s ];
 
+#if FD_BWIN==16
+  uint4 braw[6]; int db = 0;
+#endif
 #pragma unroll 1
   for( int w=63; w>=0; w-- ) {
 #if FD_DSM_PREFETCH
     atab_fetch( raw, tab, s, da < 0 ? -da : da );   /* in flight during the doublings */
+#endif
+#if FD_BWIN==16
+    if( !(w & 3) ) {                                 /* base-point entry, also in flight */
+      db = digB[ (size_t)(w>>2)*n + s ];
+      uint4 const * bp = btab_g + (size_t)( db < 0 ? -db : db )*6;
+#pragma unroll
+      for( int i=0; i<6; i++ ) braw[i] = bp[i];
+    }
 #endif
     ge_p1p1 t;
     if( w != 63 ) {
@@ -288,6 +317,7 @@ fd_dsm_kernel( u32                      nsig,
       ge_cached q; atab_unpack( q, raw ); ge_cached_cneg( q, da < 0 );
       ge_add_cached( t, P, q );
     }
+#if FD_BWIN==8
     if( !(w & 1) ) {
       ge_p1p1_to_p3( P, t );
       int db = digB[ (size_t)(w>>1)*n + s ];
@@ -300,6 +330,17 @@ fd_dsm_kernel( u32                      nsig,
       ge_precomp_cneg( bq, db < 0 );
       ge_add_precomp( t, P, bq );
     }
+#else
+    if( !(w & 3) ) {
+      ge_p1p1_to_p3( P, t );
+      ge_precomp bq;
+      fe_from_quads( bq.ypx,  braw[0], braw[1] );
+      fe_from_quads( bq.ymx,  braw[2], braw[3] );
+      fe_from_quads( bq.xy2d, braw[4], braw[5] );
+      ge_precomp_cneg( bq, db < 0 );
+      ge_add_precomp( t, P, bq );
+    }
+#endif
     ge_p1p1_to_p2( P2, t );
     if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
   }
@@ -391,15 +432,17 @@ fd_sha512_batch_kernel( unsigned char const * __restrict__ data, unsigned long c
   for( int i=0; i<4; i++ ) o[i] = make_uint4( h[4*i], h[4*i+1], h[4*i+2], h[4*i+3] );
 }
 
-/* [e]B for e in [0,128], affine precomputed (y+x, y-x, 2dxy), canonical,
-   packed 8x32.  Generated on the device at context creation (the GPU
-   analogue of table/fd_curve25519_table_*.c fd_ed25519_base_point_wnaf_table). */
-__global__ void fd_btab_kernel( uint4 * out ) {
-  int e = threadIdx.x;
+/* [e]B for e in [0,FD_BTAB_ENTRIES), affine precomputed (y+x, y-x, 2dxy),
+   canonical, packed 8x32.  Generated on the device at context creation
+   (the GPU analogue of table/fd_curve25519_table_*.c
+   fd_ed25519_base_point_wnaf_table). */
+__global__ void __launch_bounds__( 256 ) fd_btab_kernel( uint4 * out ) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
   if( e >= FD_BTAB_ENTRIES ) return;
   ge_p3 B; B.X = fe_Bx(); B.Y = fe_By(); B.Z = fe_one(); fe_mul( B.T, B.X, B.Y );
   ge_p3 acc; ge_p3_identity( acc );
-  for( int b=7; b>=0; b-- ) {
+#pragma unroll 1
+  for( int b=FD_BWIN; b>=0; b-- ) {
     ge_p3_dbl( acc, acc );
     if( (e >> b) & 1 ) ge_p3_add( acc, acc, B );
   }
@@ -458,7 +501,7 @@ struct fdgpu_ed25519_ctx {
   uint4 * d_Rxy;
   uint4 * d_Axy;
   i8 *    d_digA;
-  i8 *    d_digB;
+  short * d_digB;
   uint4 * d_btab;
   fdgpu_txn_desc_t * d_rdesc;    /* raw path: descriptors derived by fd_parse_kernel */
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
@@ -531,14 +574,14 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   HIPCHK( hipMalloc( &ctx->d_Rxy,  ns * 4 * sizeof(uint4) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_Axy,  ns * 4 * sizeof(uint4) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_digA, ns * 64 ), -1 );
-  HIPCHK( hipMalloc( &ctx->d_digB, ns * 32 ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_digB, ns * FD_BDIG * sizeof(short) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_btab, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_rdesc, max_txn * sizeof(fdgpu_txn_desc_t) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_pflag, max_txn ), -1 );
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
-  hipLaunchKernelGGL( fd_btab_kernel, dim3(1), dim3(FD_BTAB_ENTRIES), 0, ctx->stream, ctx->d_btab );
+  hipLaunchKernelGGL( fd_btab_kernel, dim3((FD_BTAB_ENTRIES + 255)/256), dim3(256), 0, ctx->stream, ctx->d_btab );
   HIPCHK( hipGetLastError(), -1 );
   for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
     fd_slot & sl = ctx->slot[i];
@@ -648,7 +691,7 @@ fdgpu_mad_peak_per_s( int device ) {
   int grid = prop.multiProcessorCount * 8;   /* 8 x 256 threads per CU = 8 waves/SIMD */
   u64 * d_out; hipMalloc( &d_out, 8 );
   hipEvent_t e0, e1; hipEventCreate( &e0 ); hipEventCreate( &e1 );
-  u32 iters = 4096;
+  u32 iters = 16384;
   hipLaunchKernelGGL( fd_mad_probe_kernel, dim3(grid), dim3(256), 0, 0, 16u, 1u, d_out );
   hipEventRecord( e0, 0 );
   hipLaunchKernelGGL( fd_mad_probe_kernel, dim3(grid), dim3(256), 0, 0, iters, 1u, d_out );
