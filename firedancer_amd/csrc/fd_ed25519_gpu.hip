@@ -1155,7 +1155,7 @@ fd_ed25519_verify_batch_single_msg( unsigned char const msg[], unsigned long con
   if( batch_sz==0 || batch_sz>16 ) return FD_ED25519_ERR_SIG;   /* fd_ed25519_user.c:238-241 */
   unsigned long n = batch_sz;
   unsigned long sz = 96UL*n + msg_sz;
-  if( sz > 0xffffUL ) return -4; /* message beyond the 64 KiB descriptor limit: see fd_ed25519_gpu.h */
+  if( sz > 0xffffUL ) return FDGPU_ERR_TOO_LONG; /* beyond the 64 KiB descriptor limit: see fd_ed25519_gpu.h */
   std::lock_guard<std::mutex> lk( g_mu );
   fdgpu_ed25519_ctx_t * ctx = global_ctx();
   if( !ctx ) { fprintf( stderr, "fdgpu: no GPU context: %s\n", fdgpu_last_error() ); abort(); }

@@ -23,7 +23,10 @@
       The fd_sha512_t * arguments are accepted and ignored (the GPU
       computes SHA-512 itself); they are kept so the prototypes are
       identical.  These calls each run one GPU round trip, so they are
-      correct but latency-bound; throughput comes from layer 2.
+      correct but latency-bound; throughput comes from layer 2.  One
+      limit the reference does not have: 96*batch_sz + msg_sz must fit
+      the 16-bit descriptor (<= 65535 bytes; every verify-path message is
+      <= 1232), else the call returns FDGPU_ERR_TOO_LONG.
 
    2. Batch / async API (new; prefix fdgpu_).  A batch is a set of
       transactions described by fdgpu_txn_desc_t records (the fields
@@ -81,6 +84,8 @@ fd_ed25519_strerror( int err );
    AVX-512 and ERR_PUBKEY on ref, and an encoding with x==0 and the
    sign bit set is rejected at decode by AVX-512 only.  AVX-512 is the
    default (it is the north-star CPU baseline). */
+#define FDGPU_ERR_TOO_LONG     (-4)   /* drop-in call beyond the 64 KiB descriptor limit */
+
 #define FDGPU_SEMANTICS_AVX512 (0)
 #define FDGPU_SEMANTICS_REF    (1)
 

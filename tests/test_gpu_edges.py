@@ -1,0 +1,79 @@
+"""GPU edge cases of the boundary: empty batches, odd batch sizes around the
+wave / workgroup widths, all-rejected batches (no lane reaches the DSM),
+the largest message the drop-in takes, and its documented limit."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def fa():
+    import firedancer_amd
+    firedancer_amd.load_library()
+    return firedancer_amd
+
+
+def _keys(oracle, n, seed=3):
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        prv = rng.bytes(32)
+        out.append((prv, oracle.public_from_private(prv)))
+    return out
+
+
+def test_empty_batches(fa):
+    from firedancer_amd import engine
+    eng = fa.Engine(device=0, max_txn=16, max_sig=16, max_payload=4096)
+    t, s = eng.verify_txns_host(np.zeros(64, np.uint8), np.zeros(0, engine.DESC_DTYPE))
+    assert len(t) == 0 and len(s) == 0
+    c, fp, _ = eng.verify_raw_host(np.zeros(64, np.uint8), np.zeros(0, np.uint32), np.zeros(0, np.uint16))
+    assert len(c) == 0
+    assert len(eng.verify_many([], [], [])) == 0
+    eng.flush()
+    assert len(eng.poll(16, blocking=True)[0]) == 0
+    eng.close()
+    assert engine.sha512_batch([]) == []
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 257, 1031])
+def test_odd_batch_sizes(fa, oracle, n):
+    """Lanes past the end of a wave / workgroup never leak into results."""
+    from firedancer_amd import synth
+    payload, desc, expect, nsig = synth.make_batch(n, synth.MULTI, max_signers=3, invalid_frac=0.3, seed=n)
+    eng = fa.Engine(device=0, max_txn=n, max_sig=nsig, max_payload=payload.nbytes)
+    t, s = eng.verify_txns_host(payload, desc)
+    eng.close()
+    np.testing.assert_array_equal(t, expect)
+    ot, os_ = oracle.verify_txns(payload, desc, nsig)
+    np.testing.assert_array_equal(s, os_)
+
+
+def test_all_rejected_before_dsm(fa, oracle):
+    """Every signature fails the S < l check: no lane reaches the hash / table / DSM stages."""
+    l_le = (2**252 + 27742317777372353535851937790883648493).to_bytes(32, "little")
+    msgs, sigs, pubs = [], [], []
+    for i, (prv, pub) in enumerate(_keys(oracle, 300)):
+        m = bytes([i & 255]) * (i % 200)
+        sig = oracle.sign(m, pub, prv)
+        msgs.append(m); sigs.append(sig[:32] + l_le); pubs.append(pub)
+    eng = fa.Engine(device=0, max_txn=128, max_sig=128, max_payload=128 * 400)
+    got = eng.verify_many(msgs, sigs, pubs)
+    eng.close()
+    assert (got == -1).all()
+
+
+def test_largest_dropin_message(fa, oracle):
+    """fd_ed25519_verify on a 65439-byte message (the 16-bit descriptor limit less 96 bytes of
+    signature and key); one byte more returns -4 (documented in fd_ed25519_gpu.h)."""
+    (prv, pub), = _keys(oracle, 1, seed=11)
+    rng = np.random.default_rng(2)
+    m = rng.bytes(65439)
+    sig = oracle.sign(m, pub, prv)
+    assert oracle.verify(m, sig, pub) == 0
+    assert fa.fd_ed25519_verify(m, sig, pub) == 0
+    bad = bytearray(m); bad[40000] ^= 1
+    assert fa.fd_ed25519_verify(bytes(bad), sig, pub) == -3
+    m2 = m + b"\0"
+    assert fa.fd_ed25519_verify(m2, oracle.sign(m2, pub, prv), pub) == -4
