@@ -95,6 +95,8 @@ def main():
     ap.add_argument("--stream-tiles", type=int, default=6)
     ap.add_argument("--stream-batch", type=int, default=8192)
     ap.add_argument("--stream-rate", type=float, default=2e6, help="paced rate (frags/s) of the latency run")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="skip the BASELINE configs[0,2,3] side measurements (small / adversarial / multi-sig)")
     args = ap.parse_args()
 
     import torch
@@ -138,6 +140,32 @@ def main():
     got = out_d.cpu().numpy()
     ok = bool(np.array_equal(got, expect))
     dt_max, all_ok = shard.reduce_max_min(dist if world > 1 else None, dt, ok, "cuda")
+
+    # BASELINE configs[0] / [2] / [3] on the same device path, rank 0 only:
+    # throughput with HBM-resident input plus a check of every result code
+    # against the generator's intended code (the GPU parity tests pin those
+    # workloads against the oracle and the reference)
+    extra = None
+    if rank == 0 and not args.no_extra_configs:
+        extra = {}
+        for name, kind, nt, ms, inv in (("configs0_small_msg_200B", synth.SMALL_MSG, 1 << 16, 1, 0.0),
+                                        ("configs2_adversarial_10pct", synth.LARGE_NOOP, 1 << 20, 1, 0.1),
+                                        ("configs3_multisig_1to12", synth.MULTI, 1 << 18, 12, 0.1)):
+            xp, xd, xe, xn = synth.make_batch(nt, kind, ms, inv, seed=shard.shard_seed(4321, rank), threads=gen_threads)
+            xe_d = Engine(device=local_rank, max_txn=nt, max_sig=xn)
+            xpd = torch.from_numpy(xp).cuda()
+            xdd = torch.from_numpy(xd.view(np.uint8)).cuda()
+            xo = torch.empty(nt, dtype=torch.int8, device="cuda")
+
+            def xstep():
+                xe_d.verify_txns_device(xpd.data_ptr(), xdd.data_ptr(), nt, xn, xo.data_ptr(), None, st)
+            xstep(); torch.cuda.synchronize()
+            xdt = shard.timed_steps(xstep, 3, 0, torch.cuda.synchronize, lambda: None)
+            xok = bool(np.array_equal(xo.cpu().numpy(), xe))
+            xe_d.close()
+            codes = {int(c): int(k) for c, k in zip(*np.unique(xe, return_counts=True))}
+            extra[name] = {"sigs_per_s": xn * 3 / xdt, "txns": nt, "sigs": xn, "results_ok": xok, "txn_codes": codes}
+            del xpd, xdd, xo
 
     lat = None
     if rank == 0 and args.latency_batch > 0:
@@ -231,6 +259,7 @@ def main():
             "cpu_baseline": cpu,
             "latency": lat,
             "stream": stream,
+            "extra_configs": extra,
             "gen_s": t_gen,
         }
         print(json.dumps(rec), flush=True)
