@@ -513,6 +513,7 @@ struct fdgpu_ed25519_ctx {
   enum { NSLOT = 4 };
   fd_slot slot[ NSLOT ];
   int cur;                       /* slot being filled */
+  int fault;                     /* a batch failed on the device: the pipeline refuses new work */
   std::deque<int> inflight;      /* slot order */
 };
 
@@ -985,6 +986,7 @@ fdgpu_ed25519_flush( fdgpu_ed25519_ctx_t * ctx ) {
    of payload_sz bytes / sig_cnt signatures in `mode` */
 static fd_slot * slot_for( fdgpu_ed25519_ctx_t * ctx, unsigned long payload_sz, unsigned long sig_cnt, int mode, int * rc ) {
   *rc = 0;
+  if( ctx->fault ) { fd_err = "ctx faulted (see the poll error); delete and recreate it"; *rc = -3; return NULL; }
   if( !ctx->slot[0].h_payload ) { fd_err = "ctx has no staging buffers (max_payload_bytes==0)"; *rc = -3; return NULL; }
   if( next_free( ctx ) ) { *rc = -2; return NULL; }
   fd_slot * sl = &ctx->slot[ ctx->cur ];
@@ -1092,7 +1094,8 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
     fd_slot & sl = ctx->slot[i];
     if( sl.cursor==0 ) {
       hipError_t e = blocking ? hipEventSynchronize( sl.done ) : hipEventQuery( sl.done );
-      if( e != hipSuccess ) break;
+      if( e == hipErrorNotReady ) break;
+      if( e != hipSuccess ) { set_err( "fdgpu_ed25519_poll: batch failed", e ); ctx->fault = 1; break; }
     }
     unsigned long k = sl.txn_cnt - sl.cursor;
     if( k > max - n ) k = max - n;

@@ -134,6 +134,10 @@ typedef struct fdgpu_txn_raw {
 #define FDGPU_ERR_PARSE        (-16)    /* fd_txn_parse returned 0 */
 #define FDGPU_TXN_IMG_STRIDE   (864UL)  /* >= FD_TXN_MAX_SZ (852), fd_txn.h:99 */
 
+/* A context is single-threaded (one per verify tile / thread); several
+   contexts may share a device.  If a batch fails on the device, poll
+   stops at it, fdgpu_last_error says why and every later submit returns
+   -3: delete and recreate the context. */
 typedef struct fdgpu_ed25519_ctx fdgpu_ed25519_ctx_t;
 
 /* fdgpu_ed25519_ctx_new creates an engine bound to HIP device `device`
