@@ -41,6 +41,22 @@ struct fe { u32 v[10]; };
 
 FD_DEV u64 fd_mad( u32 a, u32 b, u64 c ) { return (u64)a * (u64)b + c; }
 
+/* The same, with the result pinned behind an empty asm: the compiler may
+   not re-associate a column chain (it would pull a non-zero initial
+   accumulator -- a folded carry -- out into a separate 64-bit add). */
+FD_DEV u64 fd_mad_a( u32 a, u32 b, u64 c ) {
+  u64 r = (u64)a * (u64)b + c;
+  asm( "" : "+v"( r ) );
+  return r;
+}
+/* One opaque v_mad_u64_u32 (early-clobber dst: the 64-bit result must
+   not partially overlap a source). */
+FD_DEV u64 fd_mad_x( u32 a, u32 b, u64 c ) {
+  u64 r;
+  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=&v"( r ) : "v"( a ), "v"( b ), "v"( c ) : "vcc" );
+  return r;
+}
+
 /* Scheduling fence after each multiply/square: keeps the machine
    scheduler from hoisting the next operation's operand preparation into
    this one's carry chain, which otherwise inflates register pressure
@@ -132,6 +148,37 @@ FD_DEV void fe_carry64( fe & r, u64 h[ 10 ] ) {
 
 /* ---- multiply / square ------------------------------------------------- */
 
+/* Carry folding (FD_CARRY_FOLD=1): the columns are produced in two
+   chains, 0..4 and 5..9, and each column's v_mad_u64_u32 chain starts
+   from the carry out of the previous column, so the carry costs a shift
+   and a mask but no 64-bit add (≈10 fewer VALU instructions per
+   multiply).  The chains meet at limb 5 (carry out of 4) and limb 0
+   (19 x carry out of 9), each a short second step.  Output T:
+   r5 and r0 are re-masked, r6 and r1 take carries < 2^12 and < 2^15. */
+#ifndef FD_CARRY_FOLD
+#define FD_CARRY_FOLD 1
+#endif
+#if FD_CARRY_FOLD==1
+#define FD_COL_MAD( a, b, c, first ) fd_mad_a( a, b, c )
+#elif FD_CARRY_FOLD==2
+#define FD_COL_MAD( a, b, c, first ) ( (first) ? fd_mad_a( a, b, c ) : fd_mad( a, b, c ) )
+#elif FD_CARRY_FOLD==3
+#define FD_COL_MAD( a, b, c, first ) fd_mad_x( a, b, c )
+#else
+#define FD_COL_MAD( a, b, c, first ) fd_mad( a, b, c )
+#endif
+#define FE_FOLD_CHAINS( r, COL, ca, cb ) do {                               \
+    _Pragma("unroll") for( int s_=0; s_<5; s_++ ) {                          \
+      COL( s_, ca );     r.v[s_]   = (u32)ca & FE_M(s_);   ca >>= FE_W(s_);  \
+      COL( s_+5, cb );   r.v[s_+5] = (u32)cb & FE_M(s_+5); cb >>= FE_W(s_+5);\
+    }                                                                        \
+    u64 t5_ = (u64)r.v[5] + ca;                                              \
+    r.v[5] = (u32)t5_ & FE_M(5); r.v[6] += (u32)( t5_ >> 25 );                \
+    u64 t0_ = (u64)r.v[0] + cb * 19u;                                        \
+    r.v[0] = (u32)t0_ & FE_M(0); r.v[1] += (u32)( t0_ >> 26 );                \
+  } while(0)
+
+
 /* Operand multiples are formed only for the limbs that use them, each
    behind an empty asm so the compiler keeps one register per multiple
    instead of re-deriving it at every use (VALU-issue bound: every
@@ -155,21 +202,25 @@ FD_DEV void fe_mul19( fe & r, fe const & f, fe const & g, fe19 const & g19 ) {
   u32 f2[10];
 #pragma unroll
   for( int i=0; i<10; i++ ) { f2[i] = f.v[i]; if( i & 1 ) { f2[i] = 2u * f.v[i]; FD_KEEP( f2[i] ); } }
+#define FE_MUL_COL( k, acc ) do {                                      \
+    _Pragma("unroll") for( int i=0; i<10; i++ ) {                       \
+      int j = (k) - i, wrap = j < 0;                                    \
+      if( wrap ) j += 10;                                               \
+      u32 a_ = ( (i & 1) && (j & 1) ) ? f2[i] : f.v[i];                 \
+      u32 b_ = wrap ? g19.v[j] : g.v[j];                                \
+      acc = FD_COL_MAD( a_, b_, acc, i==0 );                            \
+    } } while(0)
+#if FD_CARRY_FOLD
+  u64 ca = 0, cb = 0; fe o;   /* o: r may alias f or g */
+  FE_FOLD_CHAINS( o, FE_MUL_COL, ca, cb );
+  r = o;
+#else
   u64 h[10];
 #pragma unroll
-  for( int k=0; k<10; k++ ) {
-    u64 acc = 0;
-#pragma unroll
-    for( int i=0; i<10; i++ ) {
-      int j = k - i, wrap = j < 0;
-      if( wrap ) j += 10;
-      u32 a = ( (i & 1) && (j & 1) ) ? f2[i] : f.v[i];
-      u32 b = wrap ? g19.v[j] : g.v[j];
-      acc = fd_mad( a, b, acc );
-    }
-    h[k] = acc;
-  }
+  for( int k=0; k<10; k++ ) { u64 acc = 0; FE_MUL_COL( k, acc ); h[k] = acc; }
   fe_carry64( r, h );
+#endif
+#undef FE_MUL_COL
   FD_SCHED_FENCE();
 }
 
@@ -182,51 +233,55 @@ FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
    (i, j both odd ? 2 : 1) x (i+j >= 10 ? 19 : 1) is carried by the
    operands f, 2f (i<=8), 38f (odd j>=5) and 19f (even j>=6) -- 14
    multiples.  Largest operand 38f_odd < 2^31.9 (L input). */
-FD_DEV void fe_sqr_cols( u64 h[ 10 ], fe const & f ) {
-  u32 f2[10], fw[10];
-#pragma unroll
-  for( int i=0; i<9; i++ ) { f2[i] = 2u * f.v[i]; FD_KEEP( f2[i] ); }
-  f2[9] = 0u;
-#pragma unroll
-  for( int j=0; j<10; j++ ) {
-    fw[j] = 0u;
-    if( j >= 5 ) { fw[j] = ( (j & 1) ? 38u : 19u ) * f.v[j]; FD_KEEP( fw[j] ); }
+#define FE_SQR_OPERANDS( f )                                                  \
+  u32 f2[10], fw[10];                                                         \
+  _Pragma("unroll") for( int i=0; i<9; i++ ) { f2[i] = 2u * f.v[i]; FD_KEEP( f2[i] ); } \
+  f2[9] = 0u;                                                                 \
+  _Pragma("unroll") for( int j=0; j<10; j++ ) {                               \
+    fw[j] = 0u;                                                               \
+    if( j >= 5 ) { fw[j] = ( (j & 1) ? 38u : 19u ) * f.v[j]; FD_KEEP( fw[j] ); } \
   }
-#pragma unroll
-  for( int k=0; k<10; k++ ) {
-    u64 acc = 0;
-#pragma unroll
-    for( int i=0; i<10; i++ ) {
-#pragma unroll
-      for( int j=i; j<10; j++ ) {
-        if( ( (i + j) % 10 ) != k ) continue;
-        int odd2 = (i & 1) && (j & 1);
-        int pair = i < j;
-        int wrap = i + j >= 10;
-        u32 a, b;
-        if( !wrap ) {
-          int c = (pair ? 2 : 1) * (odd2 ? 2 : 1);
-          a = c==1 ? f.v[i] : f2[i];
-          b = c==4 ? f2[j]  : f.v[j];
-        } else if( j & 1 ) {                 /* b = 38 f_j: c/38 = 1/2 (i==j), 1, 2 */
-          int c2 = (pair ? 2 : 1) * (odd2 ? 2 : 1);   /* c / 19 */
-          a = c2==4 ? f2[i] : f.v[i];
-          b = fw[j];
-        } else {                             /* even j: b = 19 f_j, c/19 = 1 (i==j) or 2 */
-          a = pair ? f2[i] : f.v[i];
-          b = fw[j];
-        }
-        acc = fd_mad( a, b, acc );
-      }
-    }
-    h[k] = acc;
-  }
-}
+#define FE_SQR_COL( k, acc ) do {                                             \
+    int first_ = 1;                                                            \
+    _Pragma("unroll") for( int i=0; i<10; i++ ) {                              \
+      _Pragma("unroll") for( int j=i; j<10; j++ ) {                            \
+        if( ( (i + j) % 10 ) != (k) ) continue;                                \
+        int odd2 = (i & 1) && (j & 1);                                         \
+        int pair = i < j;                                                      \
+        int wrap = i + j >= 10;                                                \
+        u32 a_, b_;                                                            \
+        if( !wrap ) {                                                          \
+          int c = (pair ? 2 : 1) * (odd2 ? 2 : 1);                             \
+          a_ = c==1 ? f.v[i] : f2[i];                                          \
+          b_ = c==4 ? f2[j]  : f.v[j];                                         \
+        } else if( j & 1 ) {  /* b = 38 f_j: c/38 = 1/2 (i==j), 1, 2 */        \
+          int c2 = (pair ? 2 : 1) * (odd2 ? 2 : 1);                            \
+          a_ = c2==4 ? f2[i] : f.v[i];                                         \
+          b_ = fw[j];                                                          \
+        } else {              /* even j: b = 19 f_j, c/19 = 1 (i==j) or 2 */   \
+          a_ = pair ? f2[i] : f.v[i];                                          \
+          b_ = fw[j];                                                          \
+        }                                                                      \
+        acc = FD_COL_MAD( a_, b_, acc, first_ ); first_ = 0;                   \
+      }                                                                        \
+    } } while(0)
 
+/* r = f^2; f L -> r T.  55 products; coefficient c = (i<j ? 2 : 1) x
+   (i, j both odd ? 2 : 1) x (i+j >= 10 ? 19 : 1) is carried by the
+   operands f, 2f (i<=8), 38f (odd j>=5) and 19f (even j>=6) -- 14
+   multiples.  Largest operand 38f_odd < 2^31.9 (L input). */
 FD_DEV void fe_sqr( fe & r, fe const & f ) {
+  FE_SQR_OPERANDS( f );
+#if FD_CARRY_FOLD
+  u64 ca = 0, cb = 0; fe o;
+  FE_FOLD_CHAINS( o, FE_SQR_COL, ca, cb );
+  r = o;
+#else
   u64 h[10];
-  fe_sqr_cols( h, f );
+#pragma unroll
+  for( int k=0; k<10; k++ ) { u64 acc = 0; FE_SQR_COL( k, acc ); h[k] = acc; }
   fe_carry64( r, h );
+#endif
   FD_SCHED_FENCE();
 }
 
@@ -237,21 +292,37 @@ FD_DEV void fe_sqr( fe & r, fe const & f ) {
 /* r = f^2 + 4p - b (b L) -> T: the subtraction rides on the squaring's
    carry chain instead of a separate biased sub + fe_wcarry */
 FD_DEV void fe_sqr_sub( fe & r, fe const & f, fe const & b ) {
+  FE_SQR_OPERANDS( f );
+#if FD_CARRY_FOLD
+#define FE_SQR_SUB_COL( k, acc ) do { acc += (u64)( FE_4P(k) - b.v[k] ); FE_SQR_COL( k, acc ); } while(0)
+  u64 ca = 0, cb = 0; fe o;
+  FE_FOLD_CHAINS( o, FE_SQR_SUB_COL, ca, cb );
+  r = o;
+#undef FE_SQR_SUB_COL
+#else
   u64 h[10];
-  fe_sqr_cols( h, f );
 #pragma unroll
-  for( int i=0; i<10; i++ ) h[i] += (u64)( FE_4P(i) - b.v[i] );
+  for( int k=0; k<10; k++ ) { u64 acc = 0; FE_SQR_COL( k, acc ); h[k] = acc + (u64)( FE_4P(k) - b.v[k] ); }
   fe_carry64( r, h );
+#endif
   FD_SCHED_FENCE();
 }
 
 /* r = 2 f^2 + 4p - b (b L) -> T */
 FD_DEV void fe_sqr2_sub( fe & r, fe const & f, fe const & b ) {
+  FE_SQR_OPERANDS( f );
+#if FD_CARRY_FOLD
+#define FE_SQR2_SUB_COL( k, acc ) do { u64 h_ = 0; FE_SQR_COL( k, h_ ); acc = ( h_ << 1 ) + acc + (u64)( FE_4P(k) - b.v[k] ); } while(0)
+  u64 ca = 0, cb = 0; fe o;
+  FE_FOLD_CHAINS( o, FE_SQR2_SUB_COL, ca, cb );
+  r = o;
+#undef FE_SQR2_SUB_COL
+#else
   u64 h[10];
-  fe_sqr_cols( h, f );
 #pragma unroll
-  for( int i=0; i<10; i++ ) h[i] = ( h[i] << 1 ) + (u64)( FE_4P(i) - b.v[i] );
+  for( int k=0; k<10; k++ ) { u64 acc = 0; FE_SQR_COL( k, acc ); h[k] = ( acc << 1 ) + (u64)( FE_4P(k) - b.v[k] ); }
   fe_carry64( r, h );
+#endif
   FD_SCHED_FENCE();
 }
 
