@@ -90,8 +90,11 @@ def main():
     ap.add_argument("--txns", type=int, default=1 << 20, help="txns per GPU per step (BASELINE configs[1]: 1M)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-batch", type=int, default=8192)
-    ap.add_argument("--stream-frags", type=int, default=2_000_000,
-                    help="BASELINE configs[4]: frags streamed through the GPU verify tiles (0 = skip)")
+    ap.add_argument("--stream-frags", type=int, default=-1,
+                    help="BASELINE configs[4]: frags per stream run through the GPU verify tiles "
+                         "(0 = skip; default: sized to --stream-seconds from a short calibration run)")
+    ap.add_argument("--stream-seconds", type=float, default=10.0,
+                    help="sustained length of each stream run (max rate, then paced)")
     ap.add_argument("--stream-tiles", type=int, default=6)
     ap.add_argument("--stream-batch", type=int, default=8192)
     ap.add_argument("--stream-rate", type=float, default=2e6, help="paced rate (frags/s) of the latency run")
@@ -189,24 +192,36 @@ def main():
     # (tango mcache/dcache in, fd_txn_parse + verify on the GPU, in-order
     # after_frag, out dcache).  Every rank streams its own shard at once.
     stream = None
-    if args.stream_frags > 0:
+    if args.stream_frags != 0:
         from firedancer_amd import vtile
         off, psz = desc["payload_off"], desc["payload_sz"]
+        if args.stream_frags > 0:
+            n_max = n_pace = args.stream_frags
+        else:                                   # sustained runs of --stream-seconds each
+            barrier()
+            cal = vtile.stream_bench(payload, off, psz, n_frags=2_000_000, tiles=args.stream_tiles,
+                                     batch_txn=args.stream_batch, max_inflight=2)
+            n_max = int(1.2 * cal["frags_per_s"] * args.stream_seconds)   # short runs under-read the rate
+            n_pace = int(args.stream_rate * args.stream_seconds)
         barrier()
-        smax = vtile.stream_bench(payload, off, psz, n_frags=args.stream_frags, tiles=args.stream_tiles,
+        smax = vtile.stream_bench(payload, off, psz, n_frags=n_max, tiles=args.stream_tiles,
                                   batch_txn=args.stream_batch, max_inflight=2)
         barrier()
-        slat = vtile.stream_bench(payload, off, psz, n_frags=args.stream_frags, tiles=args.stream_tiles,
+        slat = vtile.stream_bench(payload, off, psz, n_frags=n_pace, tiles=args.stream_tiles,
                                   batch_txn=args.stream_batch, max_inflight=2, rate_fps=args.stream_rate)
-        ok_s = smax["metrics"][:4] == [0, 0, 0, 0] and smax["published"] == args.stream_frags
+        ok_s = (smax["metrics"][:4] == [0, 0, 0, 0] and smax["published"] == n_max
+                and slat["metrics"][:4] == [0, 0, 0, 0] and slat["published"] == n_pace)
         sig_tot, t_max, _ = shard.reduce_sum_max(dist if world > 1 else None, smax["sigs"], smax["seconds"], "cuda")
         stream = {"workload": "BASELINE configs[4]: 1232-byte txns through mcache/dcache -> GPU verify tiles "
                               "(device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> out dcache",
                   "sigs_per_s": sig_tot / t_max, "per_gpu_sigs_per_s": smax["sigs_per_s"], "n_gpus": world,
-                  "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch, "frags_per_gpu": args.stream_frags,
-                  "max_rate": {"p50_us": smax["lat_p50_us"], "p99_us": smax["lat_p99_us"]},
-                  "paced": {"rate_frags_per_s": args.stream_rate, "achieved": slat["frags_per_s"],
-                            "p50_us": slat["lat_p50_us"], "p99_us": slat["lat_p99_us"], "max_us": slat["lat_max_us"]},
+                  "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch,
+                  "max_rate": {"frags": n_max, "seconds": smax["seconds"], "p50_us": smax["lat_p50_us"],
+                               "p99_us": smax["lat_p99_us"], "tile_host_ns_per_frag":
+                                   [round(x / max(n_max, 1), 1) for x in smax["tile_ns"]]},
+                  "paced": {"frags": n_pace, "seconds": slat["seconds"], "rate_frags_per_s": args.stream_rate,
+                            "achieved": slat["frags_per_s"], "p50_us": slat["lat_p50_us"],
+                            "p99_us": slat["lat_p99_us"], "max_us": slat["lat_max_us"]},
                   "all_published": bool(ok_s),
                   "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
 

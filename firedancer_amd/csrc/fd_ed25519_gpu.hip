@@ -65,6 +65,14 @@
 #ifndef FD_DSM_PREFETCH
 #define FD_DSM_PREFETCH 1          /* issue the -A table gather before the window's doublings */
 #endif
+/* R is not decompressed up front (see the R-check kernels after
+   fd_dsm_kernel); 0 = decode A and R before the DSM and compare
+   projectively at its end. */
+#ifndef FD_DEFER_R
+#define FD_DEFER_R 1
+#endif
+#define FD_PEND_ASMALL 2           /* per-signature code in flight: A small order, R's decode picks ERR_SIG / ERR_PUBKEY */
+#define FD_PEND_REQ    3           /* per-signature code in flight: P's encoding != R's bytes -> decode R, compare */
 
 typedef signed char i8;
 
@@ -104,6 +112,23 @@ FD_DEV void atab_fetch( atab_raw & r, uint4 const * tab, u32 s, int e ) {
 #pragma unroll
   for( int i=0; i<8; i++ ) r.q[i] = b[i];
 }
+FD_DEV void fe_load_planar( fe & r, u32 const * p, size_t n ) {
+#pragma unroll
+  for( int i=0; i<10; i++ ) r.v[i] = p[(size_t)i*n];
+}
+FD_DEV void fe_store_planar( u32 * p, size_t n, fe const & a ) {
+#pragma unroll
+  for( int i=0; i<10; i++ ) p[(size_t)i*n] = a.v[i];
+}
+FD_DEV void fe_shfl_up( fe & r, fe const & a, int d ) {
+#pragma unroll
+  for( int i=0; i<10; i++ ) r.v[i] = (u32)__shfl_up( (int)a.v[i], (unsigned)d, 64 );
+}
+FD_DEV void fe_shfl_down( fe & r, fe const & a, int d ) {
+#pragma unroll
+  for( int i=0; i<10; i++ ) r.v[i] = (u32)__shfl_down( (int)a.v[i], (unsigned)d, 64 );
+}
+
 FD_DEV void atab_unpack( ge_cached & c, atab_raw const & r ) {
   fe_from_quads( c.YpX, r.q[0], r.q[1] );
   fe_from_quads( c.YmX, r.q[2], r.q[3] );
@@ -139,8 +164,13 @@ fd_decode_kernel( unsigned char const *    __restrict__ payload,
                   uint4 *                  __restrict__ Rxy,
                   uint4 *                  __restrict__ Axy ) {
   u32 p = blockIdx.x * FD_WG + threadIdx.x;
+#if FD_DEFER_R
+  if( p >= nsig ) return;                       /* one lane per signature: A only */
+  u32 s = p, is_r = 0u;
+#else
   if( p >= 2u*nsig ) return;
   u32 s = p >> 1, is_r = p & 1u;
+#endif
   u32 m = map[s];
   u32 t = m & 0xffffffu, j = m >> 24;
   fdgpu_txn_desc_t d = desc[t];
@@ -151,7 +181,7 @@ fd_decode_kernel( unsigned char const *    __restrict__ payload,
       || (u32)d.signature_off + 64u*cnt > (u32)d.payload_sz
       || (u32)d.acct_addr_off + 32u*cnt > (u32)d.payload_sz
       || (u32)d.message_off > (u32)d.payload_sz ) {
-    pstat[p] = 0xffu;
+    pstat[2u*s + is_r] = 0xffu;
     return;
   }
   unsigned char const * base = payload + d.payload_off;
@@ -160,7 +190,7 @@ fd_decode_kernel( unsigned char const *    __restrict__ payload,
   ge_p3 P; int rc;
   ge_decode1( P, rc, w );
   int so = ge_affine_is_small_order( P );
-  pstat[p] = (unsigned char)( rc | (so << 2) );
+  pstat[2u*s + is_r] = (unsigned char)( rc | (so << 2) );
   u32 x[8], y[8];
   fe_pack( x, P.X ); fe_pack( y, P.Y );
   uint4 * o = ( is_r ? Rxy : Axy ) + (size_t)s*4;
@@ -181,11 +211,16 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
                 unsigned char const *    __restrict__ pstat,
                 i8 *                     __restrict__ code_out,
                 i8 *                     __restrict__ digA,
-                short *                  __restrict__ digB ) {
+                short *                  __restrict__ digB,
+                uint4 *                  __restrict__ Rraw ) {
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
   size_t n = nsig;
+#if FD_DEFER_R
+  u32 pa = pstat[2*s], pr = 0u;                 /* R is checked after the DSM */
+#else
   u32 pa = pstat[2*s], pr = pstat[2*s+1];
+#endif
   if( pa==0xffu ) { code_out[s] = FD_ED25519_ERR_SIG; return; }
   u32 m = map[s];
   u32 t = m & 0xffffffu, j = m >> 24;
@@ -203,14 +238,19 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
     else if( rb==1 ) code = FD_ED25519_ERR_SIG;
   }
   if( code==FD_ED25519_SUCCESS ) {
-    if( pa & 4u ) code = FD_ED25519_ERR_PUBKEY;                           /* small-order A */
+    if( pa & 4u ) code = FD_DEFER_R ? FD_PEND_ASMALL : FD_ED25519_ERR_PUBKEY;   /* small-order A (after R's decode) */
     else if( pr & 4u ) code = FD_ED25519_ERR_SIG;                         /* small-order R */
   }
   code_out[s] = (i8)code;
-  if( code != FD_ED25519_SUCCESS ) return;
+  if( code != FD_ED25519_SUCCESS && code != FD_PEND_ASMALL ) return;
 
   u32 Rw[8], Aw[8];
   fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
+#if FD_DEFER_R
+  Rraw[2*(size_t)s]   = make_uint4( Rw[0], Rw[1], Rw[2], Rw[3] );        /* R's bytes for the R-check kernels */
+  Rraw[2*(size_t)s+1] = make_uint4( Rw[4], Rw[5], Rw[6], Rw[7] );
+  if( code != FD_ED25519_SUCCESS ) return;
+#endif
   fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
   u32 h[16], k[8];
   fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
@@ -271,7 +311,8 @@ fd_dsm_kernel( u32                      nsig,
                i8 const *    __restrict__ digA,
                short const * __restrict__ digB,
                uint4 const * __restrict__ btab_g,
-               i8 *          __restrict__ code ) {
+               i8 *          __restrict__ code,
+               u32 *         __restrict__ Pbuf ) {
 #if FD_BWIN==8
   __shared__ uint4 btab[ FD_BTAB_ENTRIES * 6 ];
   for( int i=threadIdx.x; i<FD_BTAB_ENTRIES*6; i+=FD_WG ) btab[i] = btab_g[i];
@@ -345,7 +386,15 @@ fd_dsm_kernel( u32                      nsig,
     if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
   }
 
+#if FD_DEFER_R
+  /* P for the R-check kernels, planar limbs (coalesced) */
+  (void)Rxy;
+  fe_store_planar( Pbuf + s, n, P2.X );
+  fe_store_planar( Pbuf + 10*n + s, n, P2.Y );
+  fe_store_planar( Pbuf + 20*n + s, n, P2.Z );
+#else
   /* fd_ed25519_point_eq_z1: X == x_R Z and Y == y_R Z */
+  (void)Pbuf;
   uint4 const * rp = Rxy + (size_t)s*4;
   fe x, y, u;
   fe_from_quads( x, rp[0], rp[1] );
@@ -353,6 +402,152 @@ fd_dsm_kernel( u32                      nsig,
   fe_mul( u, x, P2.Z ); int okx = fe_eq( u, P2.X );
   fe_mul( u, y, P2.Z ); int oky = fe_eq( u, P2.Y );
   code[s] = (okx & oky) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+#endif
+}
+
+/* ---- deferred R check (FD_DEFER_R) ---------------------------------------
+   The signature's R is never decompressed on the common path.
+   fd_dsm_kernel leaves P = [k](-A) + [S]B projective, and P's affine
+   encoding is compared with the 32 bytes of R:
+     fd_rprod_kernel   Montgomery's trick per 256-signature block: each lane
+                       gets the product of every other Z of its block (wave
+                       prefix / suffix products by lane shuffles, the 4 wave
+                       totals through LDS); the block writes the product of
+                       all its Z;
+     fd_rinv_kernel    one inversion per block;
+     fd_rcheck_kernel  1/Z = (others' product) x (block inverse), x = X/Z,
+                       y = Y/Z, canonical pack, compare with R.
+   Equal bytes mean R decodes to exactly P (P's encoding is canonical and
+   decoding is deterministic), so checks (3) and (6) of the result-code
+   procedure hold and (5), R small order, is P's.  Every
+   other case -- different bytes (ERR_MSG, or a non-canonical /
+   undecodable / small-order R) and the A-small-order signatures, whose
+   code depends on whether R decodes -- goes through fd_rslow_kernel: the
+   full decode of R and the reference's checks in order.  The inversion
+   costs 1/256 of a decode per signature instead of one decode each.
+   Lanes without a pending verdict carry Z = 1. */
+__global__ void __launch_bounds__( FD_WG )
+fd_rprod_kernel( u32 nsig, i8 const * __restrict__ code, u32 const * __restrict__ Pbuf,
+                 u32 * __restrict__ Obuf, u32 * __restrict__ blk, u32 * __restrict__ slow_cnt ) {
+  __shared__ fe wtot[ FD_WG/64 ];
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;
+  if( s == 0u ) *slow_cnt = 0u;                      /* fd_rcheck_kernel's append counter for this batch */
+  int lane = (int)( threadIdx.x & 63u ), w = (int)( threadIdx.x >> 6 );
+  size_t n = nsig;
+  fe one = fe_one(), z = one;
+  if( s < nsig && code[s]==FD_ED25519_SUCCESS ) fe_load_planar( z, Pbuf + 20*n + s, n );
+  fe pre = z, suf = z, t;
+#pragma unroll 1
+  for( int d=1; d<64; d<<=1 ) {
+    fe_shfl_up( t, pre, d );   fe_sel( t, lane >= d, t, one );     fe_mul( pre, pre, t );
+    fe_shfl_down( t, suf, d ); fe_sel( t, lane + d < 64, t, one ); fe_mul( suf, suf, t );
+  }
+  fe o, e;
+  fe_shfl_up( o, pre, 1 );   fe_sel( o, lane > 0, o, one );        /* Z of the lanes below */
+  fe_shfl_down( e, suf, 1 ); fe_sel( e, lane < 63, e, one );       /* Z of the lanes above */
+  fe_mul( o, o, e );
+  if( lane == 63 ) wtot[w] = pre;
+  __syncthreads();
+#pragma unroll
+  for( int v=0; v<FD_WG/64; v++ ) if( v != w ) { fe tv = wtot[v]; fe_mul( o, o, tv ); }
+  if( s < nsig ) fe_store_planar( Obuf + s, n, o );
+  if( threadIdx.x == 0 ) {
+    fe b = wtot[0];
+#pragma unroll
+    for( int v=1; v<FD_WG/64; v++ ) { fe tv = wtot[v]; fe_mul( b, b, tv ); }
+#pragma unroll
+    for( int i=0; i<10; i++ ) blk[(size_t)blockIdx.x*10 + i] = b.v[i];
+  }
+}
+
+__global__ void __launch_bounds__( FD_WG )
+fd_rinv_kernel( u32 nblk, u32 * __restrict__ blk ) {
+  u32 b = blockIdx.x * FD_WG + threadIdx.x;
+  if( b >= nblk ) return;
+  fe z, r;
+#pragma unroll
+  for( int i=0; i<10; i++ ) z.v[i] = blk[(size_t)b*10 + i];
+  fe_invert( r, z );
+#pragma unroll
+  for( int i=0; i<10; i++ ) blk[(size_t)b*10 + i] = r.v[i];
+}
+
+__global__ void __launch_bounds__( FD_WG )
+fd_rcheck_kernel( u32 nsig, i8 * __restrict__ code, uint4 const * __restrict__ Rraw, u32 const * __restrict__ Pbuf,
+                  u32 const * __restrict__ Obuf, u32 const * __restrict__ blk, u32 * __restrict__ slow,
+                  u32 * __restrict__ slow_cnt ) {
+  __shared__ u32 nslow, base;
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;          /* same grid as fd_rprod_kernel: block = 256 signatures */
+  if( threadIdx.x == 0u ) nslow = 0u;
+  __syncthreads();
+  int c = s < nsig ? (int)code[s] : FD_ED25519_ERR_SIG;
+  int is_slow = c == FD_PEND_ASMALL;
+  if( c == FD_ED25519_SUCCESS ) {
+    size_t n = nsig;
+    fe o, bi, zi, X, Y, x, y;
+    fe_load_planar( o, Obuf + s, n );
+#pragma unroll
+    for( int i=0; i<10; i++ ) bi.v[i] = blk[(size_t)blockIdx.x*10 + i];
+    fe_mul( zi, o, bi );
+    fe_load_planar( X, Pbuf + s, n );
+    fe_load_planar( Y, Pbuf + 10*n + s, n );
+    fe_mul( x, X, zi ); fe_mul( y, Y, zi );
+    u32 wx[8], wy[8]; fe_pack( wx, x ); fe_pack( wy, y );
+    uint4 r0 = Rraw[2*(size_t)s], r1 = Rraw[2*(size_t)s+1];
+    u32 rw[8] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w };
+    u32 diff = ( wx[0] & 1u ) ^ ( rw[7] >> 31 );      /* sign bit = parity of x */
+    rw[7] &= 0x7fffffffu;
+#pragma unroll
+    for( int k=0; k<8; k++ ) diff |= wy[k] ^ rw[k];
+    if( diff ) is_slow = 1;
+    else {
+      /* R == P: fd_ed25519_affine_is_small_order on P's canonical coordinates */
+      u32 const y0[8] = FD_Y0_W, y1[8] = FD_Y1_W;
+      u32 zx = 0u, zy = 0u, e0 = 0u, e1 = 0u;
+#pragma unroll
+      for( int k=0; k<8; k++ ) { zx |= wx[k]; zy |= wy[k]; e0 |= wy[k] ^ y0[k]; e1 |= wy[k] ^ y1[k]; }
+      int small = (zx==0u) | (zy==0u) | (e0==0u) | (e1==0u);
+      code[s] = small ? FD_ED25519_ERR_SIG : FD_ED25519_SUCCESS;
+    }
+  }
+  /* compact the slow signatures into one list (an LDS count per block, one
+     global atomic per block that has any), so fd_rslow_kernel's decodes
+     fill whole waves instead of stalling every wave that holds one */
+  u32 li = 0u;
+  if( is_slow ) { if( c == FD_ED25519_SUCCESS ) code[s] = FD_PEND_REQ; li = atomicAdd( &nslow, 1u ); }
+  __syncthreads();
+  if( threadIdx.x == 0u && nslow ) base = atomicAdd( slow_cnt, nslow );
+  __syncthreads();
+  if( is_slow ) slow[ base + li ] = s;
+}
+
+__global__ void __launch_bounds__( FD_WG )
+fd_rslow_kernel( u32 nsig, int semantics, i8 * __restrict__ code, uint4 const * __restrict__ Rraw,
+                 u32 const * __restrict__ Pbuf, u32 const * __restrict__ slow, u32 const * __restrict__ slow_cnt ) {
+  u32 i = blockIdx.x * FD_WG + threadIdx.x;
+  if( i >= *slow_cnt ) return;
+  u32 s = slow[i];
+  int c = code[s];
+  size_t n = nsig;
+  uint4 r0 = Rraw[2*(size_t)s], r1 = Rraw[2*(size_t)s+1];
+  u32 rw[8] = { r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w };
+  ge_p3 R; int rb;
+  ge_decode1( R, rb, rw );
+  /* (3) R fails to decode: AVX-512 also rejects x==0 with the sign bit set */
+  int rfail = semantics==FDGPU_SEMANTICS_AVX512 ? rb != 0 : rb == 1;
+  int r;
+  if( c == FD_PEND_ASMALL ) r = rfail ? FD_ED25519_ERR_SIG : FD_ED25519_ERR_PUBKEY;       /* (3) before (4) */
+  else if( rfail || ge_affine_is_small_order( R ) ) r = FD_ED25519_ERR_SIG;               /* (3), (5) */
+  else {                                                /* (6) fd_ed25519_point_eq_z1 */
+    fe X, Y, Z, u;
+    fe_load_planar( X, Pbuf + s, n );
+    fe_load_planar( Y, Pbuf + 10*n + s, n );
+    fe_load_planar( Z, Pbuf + 20*n + s, n );
+    fe_mul( u, R.X, Z ); int okx = fe_eq( u, X );
+    fe_mul( u, R.Y, Z ); int oky = fe_eq( u, Y );
+    r = (okx & oky) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  }
+  code[s] = (i8)r;
 }
 
 __global__ void __launch_bounds__( FD_WG )
@@ -505,6 +700,10 @@ struct fdgpu_ed25519_ctx {
   uint4 * d_btab;
   fdgpu_txn_desc_t * d_rdesc;    /* raw path: descriptors derived by fd_parse_kernel */
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
+  u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
+  u32 *   d_O;                   /*             product of the block's other Z, planar [10][max_sig] */
+  u32 *   d_blk;                 /*             per 256-signature block: product of Z, then its inverse */
+  u32 *   d_slow;                /*             signatures needing R's full decode, [max_sig] + count */
   hipEvent_t ev[4];
   enum { NRING = 64 };
   hipEvent_t ring[ NRING ][ 4 ];  /* per-batch kernel boundaries while timing is on */
@@ -540,16 +739,25 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
   if( nsig ) {
     hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig );
     if( ctx->timing ) hipEventRecord( ev[0], st );
-    unsigned pg = (unsigned)( (2UL*sig_cnt + FD_WG - 1) / FD_WG );
+    unsigned pg = (unsigned)( ( (FD_DEFER_R ? 1UL : 2UL)*sig_cnt + FD_WG - 1) / FD_WG );
     hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
                         ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy );
     hipLaunchKernelGGL( fd_hash_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
-                        ctx->semantics, ctx->d_pstat, code, ctx->d_digA, ctx->d_digB );
+                        ctx->semantics, ctx->d_pstat, code, ctx->d_digA, ctx->d_digB, ctx->d_Rxy );
     hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_Axy, ctx->d_tab );
     if( ctx->timing ) hipEventRecord( ev[1], st );
     hipLaunchKernelGGL( fd_dsm_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
-                        ctx->d_digA, ctx->d_digB, ctx->d_btab, code );
+                        ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P );
     if( ctx->timing ) hipEventRecord( ev[2], st );
+#if FD_DEFER_R
+    u32 * slow_cnt = ctx->d_slow + ctx->max_sig;
+    hipLaunchKernelGGL( fd_rprod_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_P, ctx->d_O, ctx->d_blk, slow_cnt );
+    hipLaunchKernelGGL( fd_rinv_kernel, dim3((sg + FD_WG - 1)/FD_WG), dim3(FD_WG), 0, st, sg, ctx->d_blk );
+    hipLaunchKernelGGL( fd_rcheck_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_Rxy, ctx->d_P, ctx->d_O, ctx->d_blk,
+                        ctx->d_slow, slow_cnt );
+    hipLaunchKernelGGL( fd_rslow_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, code, ctx->d_Rxy, ctx->d_P,
+                        ctx->d_slow, slow_cnt );
+#endif
   }
   hipLaunchKernelGGL( fd_reduce_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, nsig, code, d_pflag, d_txn_out );
   if( ctx->timing ) hipEventRecord( ev[3], st );
@@ -579,6 +787,12 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   HIPCHK( hipMalloc( &ctx->d_btab, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_rdesc, max_txn * sizeof(fdgpu_txn_desc_t) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_pflag, max_txn ), -1 );
+#if FD_DEFER_R
+  HIPCHK( hipMalloc( &ctx->d_P, ns * 30 * sizeof(u32) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_O, ns * 10 * sizeof(u32) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_blk, ( ( ns + FD_WG - 1 ) / FD_WG ) * 10 * sizeof(u32) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_slow, ( ns + 1 ) * sizeof(u32) ), -1 );
+#endif
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
@@ -627,6 +841,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   (void)hipFree( ctx->d_map ); (void)hipFree( ctx->d_code ); (void)hipFree( ctx->d_pstat ); (void)hipFree( ctx->d_tab );
   (void)hipFree( ctx->d_Rxy ); (void)hipFree( ctx->d_Axy ); (void)hipFree( ctx->d_digA ); (void)hipFree( ctx->d_digB );
   (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_rdesc ); (void)hipFree( ctx->d_pflag );
+  (void)hipFree( ctx->d_P ); (void)hipFree( ctx->d_O ); (void)hipFree( ctx->d_blk ); (void)hipFree( ctx->d_slow );
   for( int i=0; i<4; i++ ) if( ctx->ev[i] ) (void)hipEventDestroy( ctx->ev[i] );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) if( ctx->ring[r][i] ) (void)hipEventDestroy( ctx->ring[r][i] );
   for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {

@@ -49,13 +49,7 @@ FD_DEV u64 fd_mad_a( u32 a, u32 b, u64 c ) {
   asm( "" : "+v"( r ) );
   return r;
 }
-/* One opaque v_mad_u64_u32 (early-clobber dst: the 64-bit result must
-   not partially overlap a source). */
-FD_DEV u64 fd_mad_x( u32 a, u32 b, u64 c ) {
-  u64 r;
-  asm( "v_mad_u64_u32 %0, vcc, %1, %2, %3" : "=&v"( r ) : "v"( a ), "v"( b ), "v"( c ) : "vcc" );
-  return r;
-}
+
 
 /* Scheduling fence after each multiply/square: keeps the machine
    scheduler from hoisting the next operation's operand preparation into
@@ -158,14 +152,10 @@ FD_DEV void fe_carry64( fe & r, u64 h[ 10 ] ) {
 #ifndef FD_CARRY_FOLD
 #define FD_CARRY_FOLD 1
 #endif
-#if FD_CARRY_FOLD==1
-#define FD_COL_MAD( a, b, c, first ) fd_mad_a( a, b, c )
-#elif FD_CARRY_FOLD==2
-#define FD_COL_MAD( a, b, c, first ) ( (first) ? fd_mad_a( a, b, c ) : fd_mad( a, b, c ) )
-#elif FD_CARRY_FOLD==3
-#define FD_COL_MAD( a, b, c, first ) fd_mad_x( a, b, c )
+#if FD_CARRY_FOLD
+#define FD_COL_MAD fd_mad_a
 #else
-#define FD_COL_MAD( a, b, c, first ) fd_mad( a, b, c )
+#define FD_COL_MAD fd_mad
 #endif
 #define FE_FOLD_CHAINS( r, COL, ca, cb ) do {                               \
     _Pragma("unroll") for( int s_=0; s_<5; s_++ ) {                          \
@@ -208,7 +198,7 @@ FD_DEV void fe_mul19( fe & r, fe const & f, fe const & g, fe19 const & g19 ) {
       if( wrap ) j += 10;                                               \
       u32 a_ = ( (i & 1) && (j & 1) ) ? f2[i] : f.v[i];                 \
       u32 b_ = wrap ? g19.v[j] : g.v[j];                                \
-      acc = FD_COL_MAD( a_, b_, acc, i==0 );                            \
+      acc = FD_COL_MAD( a_, b_, acc );                                  \
     } } while(0)
 #if FD_CARRY_FOLD
   u64 ca = 0, cb = 0; fe o;   /* o: r may alias f or g */
@@ -242,7 +232,6 @@ FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
     if( j >= 5 ) { fw[j] = ( (j & 1) ? 38u : 19u ) * f.v[j]; FD_KEEP( fw[j] ); } \
   }
 #define FE_SQR_COL( k, acc ) do {                                             \
-    int first_ = 1;                                                            \
     _Pragma("unroll") for( int i=0; i<10; i++ ) {                              \
       _Pragma("unroll") for( int j=i; j<10; j++ ) {                            \
         if( ( (i + j) % 10 ) != (k) ) continue;                                \
@@ -262,7 +251,7 @@ FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
           a_ = pair ? f2[i] : f.v[i];                                          \
           b_ = fw[j];                                                          \
         }                                                                      \
-        acc = FD_COL_MAD( a_, b_, acc, first_ ); first_ = 0;                   \
+        acc = FD_COL_MAD( a_, b_, acc );                                       \
       }                                                                        \
     } } while(0)
 

@@ -14,6 +14,9 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 typedef unsigned long ulong;
 typedef unsigned char uchar;
@@ -191,6 +194,34 @@ fdgpu_dcache_compact_next( ulong chunk, ulong sz, ulong chunk0, ulong wmark ) {
 
 /* ---- the verify tile ------------------------------------------------ */
 
+/* during_frag's copy into the out dcache.  The GPU reads the payload by
+   DMA and after_frag comes back to the record only milliseconds later, so
+   the bulk goes out with non-temporal stores (no read-for-ownership of
+   destination lines that would be evicted before their next use).
+   vt_fence() makes them visible before anything that can launch a batch:
+   at the top of during_frag (a launch inside submit_raw_ref only uploads
+   earlier frags), housekeep, flush and blocking drains. */
+static void
+vt_copy( uchar * dst, uchar const * src, ulong sz ) {
+#if defined(__x86_64__)
+  ulong n16 = sz & ~15UL;                         /* dst is chunk (64-B) aligned */
+  for( ulong i=0UL; i<n16; i+=16UL )
+    _mm_stream_si128( (__m128i *)( dst + i ), _mm_loadu_si128( (__m128i const *)( src + i ) ) );
+  if( sz > n16 ) memcpy( dst + n16, src + n16, sz - n16 );
+#else
+  memcpy( dst, src, sz );
+#endif
+}
+
+static inline void
+vt_fence( void ) {
+#if defined(__x86_64__)
+  _mm_sfence();
+#else
+  atomic_thread_fence( memory_order_seq_cst );
+#endif
+}
+
 #define VT_RESERVE_MAX ( FDGPU_TXNM_HDR_SZ + 1232UL + 2UL + 852UL )   /* header + MTU payload + fd_txn_t */
 
 typedef struct {
@@ -258,7 +289,7 @@ fdgpu_vtile_delete( fdgpu_vtile_t * vt ) {
 uchar * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt ) { return vt->dcache; }
 ulong   fdgpu_vtile_pending( fdgpu_vtile_t const * vt ) { return vt->pend_tail - vt->pend_head; }
 void    fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, ulong out[ 5 ] ) { memcpy( out, vt->metrics, sizeof(vt->metrics) ); }
-int     fdgpu_vtile_flush( fdgpu_vtile_t * vt ) { return fdgpu_ed25519_flush( vt->ctx ); }
+int     fdgpu_vtile_flush( fdgpu_vtile_t * vt ) { vt_fence(); return fdgpu_ed25519_flush( vt->ctx ); }
 
 int
 fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
@@ -269,6 +300,7 @@ fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
      frags and the pipeline would degenerate into tiny batches */
   if( max_inflight > 3UL ) max_inflight = 3UL;
   if( !filling || inflight >= max_inflight ) return 0;
+  vt_fence();
   return fdgpu_ed25519_flush( vt->ctx ) ? 0 : 1;
 }
 
@@ -278,9 +310,10 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   /* fd_verify_tile.c:78-85: the frag must hold its header + payload and
      the payload must fit the MTU (the reference FD_LOG_ERRs) */
   if( sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U || FDGPU_TXNM_HDR_SZ + in->payload_sz > sz ) return -4;
+  vt_fence();
   if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_ed25519_flush( vt->ctx ); return -2; }
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
-  memcpy( dst, frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
+  vt_copy( dst, (uchar const *)frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
   int rc = fdgpu_ed25519_submit_raw_ref( vt->ctx, vt->dcache, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
   if( rc ) return rc;
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
@@ -331,7 +364,7 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
 ulong
 fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max, int blocking ) {
   ulong n = 0UL;
-  if( blocking ) fdgpu_ed25519_flush( vt->ctx );   /* a blocking drain must not wait on an unlaunched batch */
+  if( blocking ) { vt_fence(); fdgpu_ed25519_flush( vt->ctx ); }   /* a blocking drain must not wait on an unlaunched batch */
   while( n < max && vt->pend_head < vt->pend_tail ) {
     ulong want = max - n;
     if( want > vt->batch ) want = vt->batch;
@@ -359,7 +392,8 @@ typedef struct {
   int                    tiles;
   struct { _Atomic ulong v; uchar pad[56]; } * fseq;   /* per tile, own cache line: next seq it has yet to consume */
   _Atomic int            go, fail, ready;
-  float *                lat_us;      /* per frag */
+  ulong *                lh;          /* merged latency histogram (lh_idx buckets) */
+  ulong                  lmax;        /* max latency, ns */
   unsigned char const *  payload; unsigned int const * off; unsigned short const * sz; ulong n_payload;
   ulong *                frag_chunk;  /* in dcache chunk of payload p's prefilled frag record */
   double                 rate_fps;
@@ -412,11 +446,35 @@ static void * sb_producer( void * _s ) {
 
 typedef struct { sb_t * s; int idx; } sb_tile_arg_t;
 
-static void sb_account( sb_t * s, fdgpu_vtile_t * vt, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs ) {
+/* Latency histogram (per tile, merged at the end): log-linear buckets,
+   64 per octave (< 1.6 % wide), exact below 64 ns. */
+#define LH_SUB 64UL
+#define LH_N   ( LH_SUB + 40UL*LH_SUB )
+static ulong lh_idx( ulong ns ) {
+  if( ns < LH_SUB ) return ns;
+  ulong b = 63UL - (ulong)__builtin_clzl( ns );                  /* >= 6 */
+  ulong i = LH_SUB + ( b - 6UL ) * LH_SUB + ( ( ns >> ( b - 6UL ) ) & ( LH_SUB - 1UL ) );
+  return i < LH_N ? i : LH_N - 1UL;
+}
+static double lh_val( ulong i ) {                                   /* bucket midpoint, ns */
+  if( i < LH_SUB ) return (double)i;
+  ulong b = ( i - LH_SUB ) / LH_SUB + 6UL, sub = ( i - LH_SUB ) % LH_SUB;
+  return ( (double)( LH_SUB + sub ) + 0.5 ) * (double)( 1UL << ( b - 6UL ) );
+}
+static double lh_quantile( ulong const * h, ulong tot, double q ) {
+  ulong want = (ulong)( q * (double)tot ), cum = 0UL;
+  if( want >= tot ) want = tot - 1UL;
+  for( ulong i=0UL; i<LH_N; i++ ) { cum += h[i]; if( cum > want ) return lh_val( i ); }
+  return lh_val( LH_N - 1UL );
+}
+
+static void sb_account( sb_t * s, fdgpu_vtile_t * vt, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs,
+                        ulong * lh, ulong * lmax ) {
   ulong t = now_ns();
   for( ulong i=0; i<n; i++ ) {
     ulong lat = t - d[i].tsorig;
-    s->lat_us[ d[i].seq ] = (float)( (double)lat * 1e-3 );
+    lh[ lh_idx( lat ) ]++;
+    if( lat > *lmax ) *lmax = lat;
     if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL ) {
       uchar const * pl = fdgpu_vtile_out_dcache( vt ) + d[i].chunk * FDGPU_CHUNK_SZ + FDGPU_TXNM_HDR_SZ;
       *sigs += pl[0];
@@ -438,74 +496,79 @@ static void * sb_tile( void * _a ) {
   atomic_fetch_add( &s->ready, 1 );              /* the producer starts once every tile has its GPU context */
   ulong dcap = 4096UL;
   fdgpu_vtile_done_t * done = (fdgpu_vtile_done_t *)malloc( dcap * sizeof(fdgpu_vtile_done_t) );
+  ulong * lh = (ulong *)calloc( LH_N, sizeof(ulong) ), lmax = 0UL;
+  ulong const T = (ulong)s->tiles;
   ulong sigs = 0UL, mine = 0UL, got = 0UL;
-  for( ulong seq=0; seq<s->n_frags; ) mine += ( seq++ % (ulong)s->tiles ) == (ulong)idx;
+  for( ulong q=0; q<s->n_frags; q++ ) mine += ( q % T ) == (ulong)idx;
   ulong seq = 0UL;
   ulong last_seq = ~0UL, last_got = ~0UL, t_prog = now_ns();
-  ulong t_hk = 0UL, ns_during = 0UL, ns_after = 0UL, ns_hk = 0UL, t_begin = now_ns();
+  ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, t_begin = now_ns();
   while( got < mine ) {
     if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) break;
-    if( seq != last_seq || got != last_got ) { last_seq = seq; last_got = got; t_prog = now_ns(); }
-    else if( now_ns() - t_prog > 30000000000UL ) {                /* watchdog: 30 s without progress */
+    ulong t0 = now_ns();
+    if( seq != last_seq || got != last_got ) { last_seq = seq; last_got = got; t_prog = t0; }
+    else if( t0 - t_prog > 30000000000UL ) {                      /* watchdog: 30 s without progress */
       ulong filling = 0, inflight = 0;
       fdgpu_ed25519_pipeline_state( vt->ctx, &filling, &inflight );
       fprintf( stderr, "fdgpu_stream_bench: tile %d stalled: seq %lu got %lu/%lu pending %lu filling %lu inflight %lu\n",
                idx, seq, got, mine, fdgpu_vtile_pending( vt ), filling, inflight );
       atomic_store( &s->fail, 5 ); break;
     }
-    if( seq < s->n_frags ) {
+    /* intake: up to 64 frags per pass.  Every seq's mcache line is read, as
+       the stem loop does; before_frag keeps seq % tiles == idx. */
+    int drain = 0;
+    for( int k=0; k<64 && seq < s->n_frags; k++ ) {
       fdgpu_frag_meta_t m;
       int r = fdgpu_mcache_poll( s->mc, seq, &m );
-      if( r == 0 ) {
-        if( (seq % (ulong)s->tiles) == (ulong)idx ) {            /* before_frag round robin */
-          ulong t0 = now_ns();
-          int rc = fdgpu_vtile_during_frag( vt, s->in_dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, seq, m.tsorig );
-          ns_during += now_ns() - t0;
-          if( rc == -2 ) {                                          /* staging full: drain, retry this seq */
-            ulong t1 = now_ns();
-            ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
-            ns_after += now_ns() - t1;
-            sb_account( s, vt, done, n, &sigs ); got += n;
-            continue;
-          }
-          if( rc ) { atomic_store( &s->fail, 2 ); break; }
+      if( r > 0 ) break;
+      if( r < 0 ) { atomic_fetch_add( &s->overruns, 1 ); atomic_store( &s->fail, 3 ); break; }
+      if( ( seq % T ) == (ulong)idx ) {                             /* before_frag round robin */
+        int rc = fdgpu_vtile_during_frag( vt, s->in_dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, seq, m.tsorig );
+        if( rc == -2 ) { drain = 1; break; }                        /* staging full: drain, retry this seq */
+        if( rc ) { atomic_store( &s->fail, 2 ); break; }
+        /* this tile's next frag is usually published already: start its cold lines */
+        fdgpu_frag_meta_t nx;
+        if( seq + T < s->n_frags && !fdgpu_mcache_poll( s->mc, seq + T, &nx ) ) {
+          uchar const * pf = s->in_dcache + (ulong)nx.chunk * FDGPU_CHUNK_SZ;
+          for( ulong o=0UL; o<nx.sz; o+=64UL ) __builtin_prefetch( pf + o );
         }
-        seq++;
-        if( !(seq & 63UL) || seq==s->n_frags ) atomic_store_explicit( &s->fseq[idx].v, seq, memory_order_release );   /* batched credit return */
-      } else if( r < 0 ) {
-        atomic_fetch_add( &s->overruns, 1 ); atomic_store( &s->fail, 3 ); break;
       }
+      seq++;
+      if( !(seq & 63UL) || seq==s->n_frags ) atomic_store_explicit( &s->fseq[idx].v, seq, memory_order_release );   /* batched credit return */
+    }
+    ulong t1 = now_ns();
+    ns_in += t1 - t0;
+    if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) break;
+    if( drain ) {
+      ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
+      sb_account( s, vt, done, n, &sigs, lh, &lmax ); got += n;
+      ns_after += now_ns() - t1;
+      continue;
     }
     /* housekeeping: launch / drain at most every 10 us while frags flow
        (the HIP runtime calls behind them take locks shared by all tiles) */
-    ulong tnow = now_ns();
-    if( tnow - t_hk >= 10000UL ) {
-      t_hk = tnow;
-      ulong t0 = now_ns();
+    if( t1 - t_hk >= 10000UL ) {
+      t_hk = t1;
       fdgpu_vtile_housekeep( vt, s->max_inflight );                 /* adaptive batching */
-      ulong t1 = now_ns();
-      ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
       ulong t2 = now_ns();
-      sb_account( s, vt, done, n, &sigs ); got += n;
-      ns_hk += t1 - t0; ns_after += t2 - t1;
+      ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
+      sb_account( s, vt, done, n, &sigs, lh, &lmax ); got += n;
+      ns_hk += t2 - t1; ns_after += now_ns() - t2;
     }
   }
   ulong t_end = now_ns();
-  atomic_fetch_add( &s->ns[0], ns_during ); atomic_fetch_add( &s->ns[1], ns_after );
+  atomic_fetch_add( &s->ns[0], ns_in );     atomic_fetch_add( &s->ns[1], ns_after );
   atomic_fetch_add( &s->ns[2], ns_hk );     atomic_fetch_add( &s->ns[3], t_end - t_begin );
   ulong m5[5]; fdgpu_vtile_metrics( vt, m5 );
   pthread_mutex_lock( &s->mu );
   for( int i=0; i<5; i++ ) s->metrics[i] += m5[i];
+  for( ulong i=0UL; i<LH_N; i++ ) s->lh[i] += lh[i];
+  if( lmax > s->lmax ) s->lmax = lmax;
   pthread_mutex_unlock( &s->mu );
   atomic_fetch_add( &s->sigs, sigs );
-  free( done );
+  free( done ); free( lh );
   fdgpu_vtile_delete( vt );
   return NULL;
-}
-
-static int cmp_f( void const * a, void const * b ) {
-  float x = *(float const *)a, y = *(float const *)b;
-  return x < y ? -1 : x > y ? 1 : 0;
 }
 
 int
@@ -532,7 +595,7 @@ fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, uns
   }
   s->n_frags = n_frags; s->tiles = tiles;
   s->fseq = calloc( (size_t)tiles, sizeof(*s->fseq) );
-  s->lat_us = (float *)calloc( n_frags, sizeof(float) );
+  s->lh = (ulong *)calloc( LH_N, sizeof(ulong) );
   s->payload = payload; s->off = off; s->sz = sz; s->n_payload = n_payload; s->rate_fps = rate_fps;
   s->device = device; s->batch_txn = batch_txn; s->max_inflight = max_inflight ? max_inflight : 2UL;
   pthread_mutex_init( &s->mu, NULL );
@@ -550,15 +613,16 @@ fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, uns
     st->frags = n_frags; st->sigs = atomic_load( &s->sigs ); st->published = s->metrics[4];
     st->frags_per_s = (double)n_frags / st->seconds;
     st->sigs_per_s = (double)st->sigs / st->seconds;
-    qsort( s->lat_us, n_frags, sizeof(float), cmp_f );
-    st->lat_p50_us = s->lat_us[ n_frags/2 ];
-    st->lat_p99_us = s->lat_us[ (n_frags*99UL)/100UL ];
-    st->lat_max_us = s->lat_us[ n_frags-1UL ];
+    ulong tot = 0UL;
+    for( ulong i=0UL; i<LH_N; i++ ) tot += s->lh[i];
+    st->lat_p50_us = tot ? lh_quantile( s->lh, tot, 0.50 ) * 1e-3 : 0.;
+    st->lat_p99_us = tot ? lh_quantile( s->lh, tot, 0.99 ) * 1e-3 : 0.;
+    st->lat_max_us = (double)s->lmax * 1e-3;
     memcpy( st->metrics, s->metrics, sizeof(st->metrics) );
     st->overruns = atomic_load( &s->overruns );
     for( int i=0; i<4; i++ ) st->tile_ns[i] = atomic_load( &s->ns[i] );
   }
-  fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( s->frag_chunk ); free( (void *)s->fseq ); free( s->lat_us );
+  fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( s->frag_chunk ); free( (void *)s->fseq ); free( s->lh );
   pthread_mutex_destroy( &s->mu );
   free( s );
   return rc ? -rc - 10 : 0;

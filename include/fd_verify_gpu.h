@@ -160,8 +160,8 @@ typedef struct fdgpu_stream_stats {
   double        lat_p50_us, lat_p99_us, lat_max_us;   /* tsorig (producer publish) -> after_frag verdict */
   unsigned long metrics[ 5 ];
   unsigned long overruns;        /* producer lapped a tile (frags lost, as in tango) */
-  unsigned long tile_ns[ 4 ];    /* host time summed over tiles: during_frag, after_frags,
-                                    housekeep, whole tile loop */
+  unsigned long tile_ns[ 4 ];    /* host time summed over tiles: frag intake (mcache polls +
+                                    during_frag), after_frags, housekeep, whole tile loop */
 } fdgpu_stream_stats_t;
 
 /* A producer thread publishes n_frags frags built from the payload

@@ -77,3 +77,24 @@ def test_largest_dropin_message(fa, oracle):
     assert fa.fd_ed25519_verify(bytes(bad), sig, pub) == -3
     m2 = m + b"\0"
     assert fa.fd_ed25519_verify(m2, oracle.sign(m2, pub, prv), pub) == -4
+
+
+@pytest.mark.parametrize("frac", [1.0, 0.5])
+def test_r_check_slow_path(fa, oracle, frac):
+    """Signatures whose R does not match [k](-A)+[S]B take the deferred full
+    decode of R (fd_rslow_kernel, compacted across blocks): every one of
+    them, or every other one, in a 5000-signature batch."""
+    from firedancer_amd import synth
+    n = 5000
+    payload, desc, expect, nsig = synth.make_batch(n, synth.LARGE_NOOP, seed=31)
+    rng = np.random.default_rng(5)
+    bad = rng.choice(n, int(n * frac), replace=False)
+    for t in bad:
+        payload[int(desc["payload_off"][t]) + 700] ^= 0x10      # message byte -> ERR_MSG
+    eng = fa.Engine(device=0, max_txn=n, max_sig=nsig, max_payload=payload.nbytes)
+    t, s = eng.verify_txns_host(payload, desc)
+    eng.close()
+    want = np.zeros(n, np.int8); want[bad] = -3
+    np.testing.assert_array_equal(t, want)
+    ot, os_ = oracle.verify_txns(payload, desc, nsig, threads=16)
+    np.testing.assert_array_equal(t, ot)

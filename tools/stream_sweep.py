@@ -18,7 +18,8 @@ for tiles in [int(x) for x in os.environ.get("TILES", "1,2,4,8").split(",")]:
     for batch in [int(x) for x in os.environ.get("BATCH", "1024,4096").split(",")]:
         for rate in [float(x) for x in os.environ.get("RATE", "0").split(",")]:
           for infl in [int(x) for x in os.environ.get("INFL", "2").split(",")]:
-            st = vtile.stream_bench(payload, desc["payload_off"], desc["payload_sz"], n_frags=int(os.environ.get("NF", 1000000)),
+           for nf in [int(x) for x in os.environ.get("NF", "1000000").split(",")]:
+            st = vtile.stream_bench(payload, desc["payload_off"], desc["payload_sz"], n_frags=nf,
                                     tiles=tiles, batch_txn=batch, max_inflight=infl, mcache_depth=1 << 16, rate_fps=rate)
             st.update(tiles=tiles, batch=batch, rate=rate, inflight=infl)
             print(json.dumps(st), flush=True)
