@@ -6,8 +6,8 @@
    fd_sha512.c:265-398) over the AVX2 block core fd_sha512_core_avx2.S and
    the 4/8-lane AVX batch API (fd_sha512_batch_avx512.c).  Here every
    lane of a wave hashes its own signature's R||A||M: the 64-bit state
-   words are VGPR pairs, rotations are v_alignbit_b32 pairs, Ch/Maj are
-   v_bfi_b32.  The message is read straight from the transaction payload
+   words are VGPR pairs, rotations are v_alignbit_b32 pairs, Ch is v_bfi_b32,
+   the 3-way xors and Maj are v_bitop3_b32.  The message is read straight from the transaction payload
    (arbitrary byte alignment) with dword loads + v_alignbyte_b32; padding
    and the length block are synthesised in registers. */
 
@@ -37,7 +37,10 @@ __constant__ u64 fd_gpu_sha512_k[ 80 ] = {
 };
 
 /* 64-bit rotate / shift as two v_alignbit_b32 on the VGPR halves */
-FD_DEV u64 fd_mk64( u32 lo, u32 hi ) { return ((u64)hi << 32) | (u64)lo; }
+/* (hi:lo) as a bit cast of a 2-vector: written as (hi<<32)|lo the
+   compiler splits later 64-bit adds into a low add and a high add */
+typedef u32 fd_u32x2 __attribute__(( ext_vector_type( 2 ) ));
+FD_DEV u64 fd_mk64( u32 lo, u32 hi ) { fd_u32x2 v = { lo, hi }; return __builtin_bit_cast( u64, v ); }
 FD_DEV u64 fd_rotr64( u64 x, int n ) {
   u32 lo = (u32)x, hi = (u32)(x >> 32);
   if( n >= 32 ) { u32 t = lo; lo = hi; hi = t; n -= 32; }
@@ -48,6 +51,18 @@ FD_DEV u64 fd_shr64( u64 x, int n ) {   /* n < 32 */
   return fd_mk64( __builtin_amdgcn_alignbit( hi, lo, (u32)n ), hi >> n );
 }
 FD_DEV u32 fd_bswap32( u32 x ) { return __builtin_bswap32( x ); }
+
+/* Three-input boolean functions as one gfx950 v_bitop3_b32 per 32-bit
+   half (truth table immediate: 0x96 = x^y^z, 0xe8 = majority).  The
+   compiler leaves a 3-way xor as two v_xor_b32 per half. */
+FD_DEV u64 fd_xor3_64( u64 x, u64 y, u64 z ) {
+  return fd_mk64( __builtin_amdgcn_bitop3_b32( (u32)x, (u32)y, (u32)z, 0x96 ),
+                  __builtin_amdgcn_bitop3_b32( (u32)(x>>32), (u32)(y>>32), (u32)(z>>32), 0x96 ) );
+}
+FD_DEV u64 fd_maj64( u64 x, u64 y, u64 z ) {
+  return fd_mk64( __builtin_amdgcn_bitop3_b32( (u32)x, (u32)y, (u32)z, 0xe8 ),
+                  __builtin_amdgcn_bitop3_b32( (u32)(x>>32), (u32)(y>>32), (u32)(z>>32), 0xe8 ) );
+}
 
 /* Load n32 consecutive little-endian 32-bit words starting at an
    arbitrary byte address p: aligned dword loads + v_alignbyte_b32.  Reads
@@ -70,11 +85,11 @@ FD_DEV void fd_load_words( u32 w[ N32 ], unsigned char const * p ) {
    neither the 80 constants nor the whole expanded schedule are ever live
    at once (a fully unrolled block needed ~200 VGPRs). */
 #define FD_SHA512_ROUND( kt, wt ) do {                                              \
-    u64 S1 = fd_rotr64( e,14 ) ^ fd_rotr64( e,18 ) ^ fd_rotr64( e,41 );           \
+    u64 S1 = fd_xor3_64( fd_rotr64( e,14 ), fd_rotr64( e,18 ), fd_rotr64( e,41 ) ); \
     u64 ch = g ^ ( e & ( f ^ g ) );                                                 \
     u64 t1 = hh + S1 + ch + (kt) + (wt);                                            \
-    u64 S0 = fd_rotr64( a,28 ) ^ fd_rotr64( a,34 ) ^ fd_rotr64( a,39 );           \
-    u64 mj = ( a & b ) | ( c & ( a | b ) );                                         \
+    u64 S0 = fd_xor3_64( fd_rotr64( a,28 ), fd_rotr64( a,34 ), fd_rotr64( a,39 ) ); \
+    u64 mj = fd_maj64( a, b, c );                                                   \
     hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;      \
   } while(0)
 
@@ -91,8 +106,8 @@ FD_DEV void fd_sha512_block( u64 h[ 8 ], u64 w[ 16 ] ) {
 #pragma unroll
     for( int r=0; r<16; r++ ) {
       u64 w15 = w[(r+1)&15], w2 = w[(r+14)&15];
-      u64 s0 = fd_rotr64( w15, 1 ) ^ fd_rotr64( w15, 8 ) ^ fd_shr64( w15, 7 );
-      u64 s1 = fd_rotr64( w2, 19 ) ^ fd_rotr64( w2, 61 ) ^ fd_shr64( w2, 6 );
+      u64 s0 = fd_xor3_64( fd_rotr64( w15, 1 ), fd_rotr64( w15, 8 ), fd_shr64( w15, 7 ) );
+      u64 s1 = fd_xor3_64( fd_rotr64( w2, 19 ), fd_rotr64( w2, 61 ), fd_shr64( w2, 6 ) );
       w[r] += s0 + w[(r+9)&15] + s1;
       FD_SHA512_ROUND( kg[r], w[r] );
       if( (r & 3)==3 ) __builtin_amdgcn_sched_barrier( 0 );
