@@ -186,7 +186,9 @@ def main():
             assert (lo == 0).all()
         leng.close()
         lat = {"batch_txns": lb, "p50_ms": float(np.percentile(times, 50)), "p99_ms": float(np.percentile(times, 99)),
-               "path": "fdgpu_ed25519_verify_txns_host: pinned staging, H2D, 4 kernels, D2H"}
+               "path": "fdgpu_ed25519_verify_txns_host: pinned staging in 1-MB chunks overlapped with H2D, "
+                       "latency path (one fused decode-A / decode-R / hash launch, table, DSM with R compare, "
+                       "reduce), D2H"}
 
     # BASELINE configs[4]: the same payloads streamed through GPU verify tiles
     # (tango mcache/dcache in, fd_txn_parse + verify on the GPU, in-order

@@ -71,6 +71,13 @@
 #ifndef FD_DEFER_R
 #define FD_DEFER_R 1
 #endif
+/* Batches of at most this many signatures take the latency path
+   (fd_prep_kernel, R decoded up front): they cannot fill the GPU, so
+   per-wave instruction streams, not total work, set their time. */
+#ifndef FD_SMALL_BATCH_MAX
+#define FD_SMALL_BATCH_MAX 65536UL
+#endif
+#define FD_STAGE_CHUNK ( 1UL << 20 )   /* host-staged batches: bytes per memcpy / H2D step */
 #define FD_PEND_ASMALL 2           /* per-signature code in flight: A small order, R's decode picks ERR_SIG / ERR_PUBKEY */
 #define FD_PEND_REQ    3           /* per-signature code in flight: P's encoding != R's bytes -> decode R, compare */
 
@@ -149,41 +156,27 @@ fd_expand_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 *
   }
 }
 
-/* Stage 1 -- point decompression, two lanes per signature (lane 2s
-   decodes the public key A, lane 2s+1 the signature's R): one pow22523
-   chain per lane keeps the kernel at 3 waves/SIMD and doubles the
-   parallelism.  Per point: status byte rc | small_order<<2 (rc: 0 ok,
-   1 not a square, 2 x==0 with sign set), 0xff if the transaction is
+/* transaction sanity (batch size and bounds) -> ERR_SIG for all its
+   signatures, like the batch_sz check of fd_ed25519_user.c:238-241 */
+FD_DEV int txn_desc_ok( fdgpu_txn_desc_t const & d ) {
+  u32 cnt = d.sig_cnt;
+  return !( cnt==0u || cnt>16u
+            || (u32)d.signature_off + 64u*cnt > (u32)d.payload_sz
+            || (u32)d.acct_addr_off + 32u*cnt > (u32)d.payload_sz
+            || (u32)d.message_off > (u32)d.payload_sz );
+}
+
+/* Stage 1 -- point decompression of signature s's public key A (is_r 0)
+   or its R (is_r 1).  Status byte rc | small_order<<2 (rc: 0 ok, 1 not
+   a square, 2 x==0 with sign set), 0xff if the transaction is
    malformed; the canonical affine point goes to Axy / Rxy. */
-__global__ void __launch_bounds__( FD_WG )
-fd_decode_kernel( unsigned char const *    __restrict__ payload,
-                  fdgpu_txn_desc_t const * __restrict__ desc,
-                  u32 const *              __restrict__ map,
-                  u32                                   nsig,
-                  unsigned char *          __restrict__ pstat,
-                  uint4 *                  __restrict__ Rxy,
-                  uint4 *                  __restrict__ Axy ) {
-  u32 p = blockIdx.x * FD_WG + threadIdx.x;
-#if FD_DEFER_R
-  if( p >= nsig ) return;                       /* one lane per signature: A only */
-  u32 s = p, is_r = 0u;
-#else
-  if( p >= 2u*nsig ) return;
-  u32 s = p >> 1, is_r = p & 1u;
-#endif
+FD_DEV void decode_one( unsigned char const * __restrict__ payload, fdgpu_txn_desc_t const * __restrict__ desc,
+                        u32 const * __restrict__ map, u32 s, u32 is_r, unsigned char * __restrict__ pstat,
+                        uint4 * __restrict__ Rxy, uint4 * __restrict__ Axy ) {
   u32 m = map[s];
   u32 t = m & 0xffffffu, j = m >> 24;
   fdgpu_txn_desc_t d = desc[t];
-  /* transaction sanity (batch size and bounds) -> ERR_SIG for all its
-     signatures, like the batch_sz check of fd_ed25519_user.c:238-241 */
-  u32 cnt = d.sig_cnt;
-  if( cnt==0u || cnt>16u
-      || (u32)d.signature_off + 64u*cnt > (u32)d.payload_sz
-      || (u32)d.acct_addr_off + 32u*cnt > (u32)d.payload_sz
-      || (u32)d.message_off > (u32)d.payload_sz ) {
-    pstat[2u*s + is_r] = 0xffu;
-    return;
-  }
+  if( !txn_desc_ok( d ) ) { pstat[2u*s + is_r] = 0xffu; return; }
   unsigned char const * base = payload + d.payload_off;
   u32 w[8];
   fd_load_words<8>( w, base + ( is_r ? (u32)d.signature_off + 64u*j : (u32)d.acct_addr_off + 32u*j ) );
@@ -198,63 +191,27 @@ fd_decode_kernel( unsigned char const *    __restrict__ payload,
   o[2] = make_uint4( y[0], y[1], y[2], y[3] ); o[3] = make_uint4( y[4], y[5], y[6], y[7] );
 }
 
-/* Stage 2 -- the result-code procedure of fd_ed25519_verify
-   (fd_ed25519_user.c:174-199) from S and the two point
-   statuses, then for pending signatures k = SHA-512(R||A||M) mod l
-   (:204-206) and the signed digits of k (radix 16) and S (radix 256). */
+/* Large batches (deferred R): one lane per signature, A only.  With
+   both = 1 (FD_DEFER_R=0 builds): lane 2s decodes A, lane 2s+1 R. */
 __global__ void __launch_bounds__( FD_WG )
-fd_hash_kernel( unsigned char const *    __restrict__ payload,
-                fdgpu_txn_desc_t const * __restrict__ desc,
-                u32 const *              __restrict__ map,
-                u32                                   nsig,
-                int                                   semantics,
-                unsigned char const *    __restrict__ pstat,
-                i8 *                     __restrict__ code_out,
-                i8 *                     __restrict__ digA,
-                short *                  __restrict__ digB,
-                uint4 *                  __restrict__ Rraw ) {
-  u32 s = blockIdx.x * FD_WG + threadIdx.x;
-  if( s >= nsig ) return;
-  size_t n = nsig;
-#if FD_DEFER_R
-  u32 pa = pstat[2*s], pr = 0u;                 /* R is checked after the DSM */
-#else
-  u32 pa = pstat[2*s], pr = pstat[2*s+1];
-#endif
-  if( pa==0xffu ) { code_out[s] = FD_ED25519_ERR_SIG; return; }
-  u32 m = map[s];
-  u32 t = m & 0xffffffu, j = m >> 24;
-  fdgpu_txn_desc_t d = desc[t];
-  unsigned char const * base = payload + d.payload_off;
-  u32 Sw[8];
-  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
-  int ra = (int)(pa & 3u), rb = (int)(pr & 3u);
-  int code = FD_ED25519_SUCCESS;
-  if( !sc_is_canonical( Sw ) ) code = FD_ED25519_ERR_SIG;                /* S < l */
-  else if( semantics==FDGPU_SEMANTICS_AVX512 ) {
-    if( ra | rb ) code = FD_ED25519_ERR_SIG;                              /* decode (AVX-512) */
-  } else {
-    if( ra==1 ) code = FD_ED25519_ERR_PUBKEY;                             /* decode (portable) */
-    else if( rb==1 ) code = FD_ED25519_ERR_SIG;
-  }
-  if( code==FD_ED25519_SUCCESS ) {
-    if( pa & 4u ) code = FD_DEFER_R ? FD_PEND_ASMALL : FD_ED25519_ERR_PUBKEY;   /* small-order A (after R's decode) */
-    else if( pr & 4u ) code = FD_ED25519_ERR_SIG;                         /* small-order R */
-  }
-  code_out[s] = (i8)code;
-  if( code != FD_ED25519_SUCCESS && code != FD_PEND_ASMALL ) return;
+fd_decode_kernel( unsigned char const *    __restrict__ payload,
+                  fdgpu_txn_desc_t const * __restrict__ desc,
+                  u32 const *              __restrict__ map,
+                  u32                                   nsig,
+                  int                                   both,
+                  unsigned char *          __restrict__ pstat,
+                  uint4 *                  __restrict__ Rxy,
+                  uint4 *                  __restrict__ Axy ) {
+  u32 p = blockIdx.x * FD_WG + threadIdx.x;
+  if( p >= ( both ? 2u*nsig : nsig ) ) return;
+  u32 s = both ? p >> 1 : p, is_r = both ? p & 1u : 0u;
+  decode_one( payload, desc, map, s, is_r, pstat, Rxy, Axy );
+}
 
-  u32 Rw[8], Aw[8];
-  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
-#if FD_DEFER_R
-  Rraw[2*(size_t)s]   = make_uint4( Rw[0], Rw[1], Rw[2], Rw[3] );        /* R's bytes for the R-check kernels */
-  Rraw[2*(size_t)s+1] = make_uint4( Rw[4], Rw[5], Rw[6], Rw[7] );
-  if( code != FD_ED25519_SUCCESS ) return;
-#endif
-  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
-  u32 h[16], k[8];
-  fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
-  sc_reduce( k, h );
+/* Signed digits of k (radix 16, digA[64][n]) and S (radix 2^FD_BWIN,
+   digB[FD_BDIG][n]), stored coalesced. */
+FD_DEV void store_digits( u32 const k[ 8 ], u32 const Sw[ 8 ], u32 s, size_t n,
+                          i8 * __restrict__ digA, short * __restrict__ digB ) {
   int carry = 0;
 #pragma unroll
   for( int i=0; i<64; i++ ) {
@@ -272,15 +229,128 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
   }
 }
 
+/* The result-code procedure of fd_ed25519_verify (fd_ed25519_user.c:
+   174-199) from S's check (code so far: SUCCESS or
+   ERR_SIG) and the point statuses pa (A) and pr (R).  defer: R has not
+   been decoded (pr = 0); a small-order A is parked as FD_PEND_ASMALL,
+   because its code depends on whether R decodes (check 3 comes before
+   check 4). */
+FD_DEV int result_code( int code, u32 pa, u32 pr, int semantics, int defer ) {
+  if( pa==0xffu || pr==0xffu ) return FD_ED25519_ERR_SIG;                    /* malformed transaction */
+  if( code != FD_ED25519_SUCCESS ) return code;                             /* (1) S < l */
+  int ra = (int)(pa & 3u), rb = (int)(pr & 3u);
+  if( semantics==FDGPU_SEMANTICS_AVX512 ) {
+    if( ra | rb ) return FD_ED25519_ERR_SIG;                                /* (2)(3) decode (AVX-512) */
+  } else {
+    if( ra==1 ) return FD_ED25519_ERR_PUBKEY;                               /* (2) decode (portable) */
+    if( rb==1 ) return FD_ED25519_ERR_SIG;                                  /* (3) */
+  }
+  if( pa & 4u ) return defer ? FD_PEND_ASMALL : FD_ED25519_ERR_PUBKEY;      /* (4) small-order A */
+  if( pr & 4u ) return FD_ED25519_ERR_SIG;                                  /* (5) small-order R */
+  return FD_ED25519_SUCCESS;
+}
+
+/* Stage 2 -- S's check and k = SHA-512(R||A||M) mod l (:204-206) with
+   the signed digits of k and S.
+   defer = 1 (large batches): after the decode of A; sets the code from
+   pstat and hashes only pending signatures; keeps R's bytes for the
+   R-check kernels.
+   defer = 0, statuses = 0 (small batches, fd_prep_kernel): runs beside
+   the decodes; writes ERR_SIG (malformed or S >= l) or SUCCESS and
+   hashes every well-formed signature; fd_table_kernel applies the
+   point statuses. */
+FD_DEV void hash_one( unsigned char const * __restrict__ payload, fdgpu_txn_desc_t const * __restrict__ desc,
+                      u32 const * __restrict__ map, u32 s, size_t n, int semantics, int defer,
+                      unsigned char const * __restrict__ pstat, i8 * __restrict__ code_out,
+                      i8 * __restrict__ digA, short * __restrict__ digB, uint4 * __restrict__ Rraw ) {
+  u32 m = map[s];
+  u32 t = m & 0xffffffu, j = m >> 24;
+  fdgpu_txn_desc_t d = desc[t];
+  if( !txn_desc_ok( d ) ) { code_out[s] = FD_ED25519_ERR_SIG; return; }
+  unsigned char const * base = payload + d.payload_off;
+  u32 Sw[8];
+  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
+  int code = sc_is_canonical( Sw ) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_SIG;
+  if( defer ) code = result_code( code, pstat[2*s], 0u, semantics, 1 );
+  code_out[s] = (i8)code;
+  if( code != FD_ED25519_SUCCESS && code != FD_PEND_ASMALL ) return;
+
+  u32 Rw[8], Aw[8];
+  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
+  if( defer ) {
+    Rraw[2*(size_t)s]   = make_uint4( Rw[0], Rw[1], Rw[2], Rw[3] );        /* R's bytes for the R-check kernels */
+    Rraw[2*(size_t)s+1] = make_uint4( Rw[4], Rw[5], Rw[6], Rw[7] );
+    if( code != FD_ED25519_SUCCESS ) return;
+  }
+  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
+  u32 h[16], k[8];
+  fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
+  sc_reduce( k, h );
+  store_digits( k, Sw, s, n, digA, digB );
+}
+
+__global__ void __launch_bounds__( FD_WG )
+fd_hash_kernel( unsigned char const *    __restrict__ payload,
+                fdgpu_txn_desc_t const * __restrict__ desc,
+                u32 const *              __restrict__ map,
+                u32                                   nsig,
+                int                                   semantics,
+                int                                   defer,
+                unsigned char const *    __restrict__ pstat,
+                i8 *                     __restrict__ code_out,
+                i8 *                     __restrict__ digA,
+                short *                  __restrict__ digB,
+                uint4 *                  __restrict__ Rraw ) {
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  if( !defer ) {                                 /* FD_DEFER_R=0 builds: both points decoded already */
+    hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rraw );
+    int c = code_out[s];
+    if( c==FD_ED25519_SUCCESS || c==FD_ED25519_ERR_SIG )
+      code_out[s] = (i8)result_code( c, pstat[2*s], pstat[2*s+1], semantics, 0 );
+    return;
+  }
+  hash_one( payload, desc, map, s, nsig, semantics, 1, pstat, code_out, digA, digB, Rraw );
+}
+
+/* Small batches (latency): the three independent parts of the prep in
+   ONE launch -- blocks [0,sg) decode A, [sg,2sg) decode R, [2sg,3sg)
+   check S and hash -- so a batch that cannot fill the GPU pays the
+   longest of them instead of their sum.  Every block has one role, so
+   no wave diverges. */
+__global__ void __launch_bounds__( FD_WG )
+fd_prep_kernel( unsigned char const *    __restrict__ payload,
+                fdgpu_txn_desc_t const * __restrict__ desc,
+                u32 const *              __restrict__ map,
+                u32                                   nsig,
+                u32                                   sg,
+                int                                   semantics,
+                unsigned char *          __restrict__ pstat,
+                uint4 *                  __restrict__ Rxy,
+                uint4 *                  __restrict__ Axy,
+                i8 *                     __restrict__ code_out,
+                i8 *                     __restrict__ digA,
+                short *                  __restrict__ digB ) {
+  u32 role = blockIdx.x / sg, b = blockIdx.x - role*sg;
+  u32 s = b * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  if( role < 2u ) decode_one( payload, desc, map, s, role, pstat, Rxy, Axy );
+  else            hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rxy );
+}
+
 /* Stage 3 -- table [0..8](-A) in cached form (fd_ed25519_point_neg + the
    odd-multiple table of fd_curve25519.c:118-131; here all multiples, for a
    signed fixed window). */
 __global__ void __launch_bounds__( FD_WG, 3 )
-fd_table_kernel( u32 nsig, i8 const * __restrict__ code, uint4 const * __restrict__ Axy,
-                 uint4 * __restrict__ tab ) {
+fd_table_kernel( u32 nsig, int semantics, unsigned char const * __restrict__ pstat, i8 * __restrict__ code,
+                 uint4 const * __restrict__ Axy, uint4 * __restrict__ tab ) {
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
-  if( code[s] != FD_ED25519_SUCCESS ) return;
+  if( pstat ) {                                  /* small batches: fd_prep_kernel left S's check only */
+    int c = result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 );
+    code[s] = (i8)c;
+    if( c != FD_ED25519_SUCCESS ) return;
+  } else if( code[s] != FD_ED25519_SUCCESS ) return;
   uint4 const * ap = Axy + (size_t)s*4;
   ge_p3 A;
   fe_from_quads( A.X, ap[0], ap[1] );
@@ -312,7 +382,8 @@ fd_dsm_kernel( u32                      nsig,
                short const * __restrict__ digB,
                uint4 const * __restrict__ btab_g,
                i8 *          __restrict__ code,
-               u32 *         __restrict__ Pbuf ) {
+               u32 *         __restrict__ Pbuf,
+               int                        defer ) {
 #if FD_BWIN==8
   __shared__ uint4 btab[ FD_BTAB_ENTRIES * 6 ];
   for( int i=threadIdx.x; i<FD_BTAB_ENTRIES*6; i+=FD_WG ) btab[i] = btab_g[i];
@@ -386,15 +457,15 @@ fd_dsm_kernel( u32                      nsig,
     if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
   }
 
-#if FD_DEFER_R
-  /* P for the R-check kernels, planar limbs (coalesced) */
-  (void)Rxy;
-  fe_store_planar( Pbuf + s, n, P2.X );
-  fe_store_planar( Pbuf + 10*n + s, n, P2.Y );
-  fe_store_planar( Pbuf + 20*n + s, n, P2.Z );
-#else
-  /* fd_ed25519_point_eq_z1: X == x_R Z and Y == y_R Z */
-  (void)Pbuf;
+  if( defer ) {
+    /* P for the R-check kernels, planar limbs (coalesced) */
+    fe_store_planar( Pbuf + s, n, P2.X );
+    fe_store_planar( Pbuf + 10*n + s, n, P2.Y );
+    fe_store_planar( Pbuf + 20*n + s, n, P2.Z );
+    return;
+  }
+  /* R decoded up front (small batches): fd_ed25519_point_eq_z1,
+     X == x_R Z and Y == y_R Z */
   uint4 const * rp = Rxy + (size_t)s*4;
   fe x, y, u;
   fe_from_quads( x, rp[0], rp[1] );
@@ -402,7 +473,6 @@ fd_dsm_kernel( u32                      nsig,
   fe_mul( u, x, P2.Z ); int okx = fe_eq( u, P2.X );
   fe_mul( u, y, P2.Z ); int oky = fe_eq( u, P2.Y );
   code[s] = (okx & oky) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
-#endif
 }
 
 /* ---- deferred R check (FD_DEFER_R) ---------------------------------------
@@ -700,6 +770,7 @@ struct fdgpu_ed25519_ctx {
   uint4 * d_btab;
   fdgpu_txn_desc_t * d_rdesc;    /* raw path: descriptors derived by fd_parse_kernel */
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
+  unsigned long small_max;       /* batches of at most this many signatures take the latency path */
   u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
   u32 *   d_O;                   /*             product of the block's other Z, planar [10][max_sig] */
   u32 *   d_blk;                 /*             per 256-signature block: product of Z, then its inverse */
@@ -715,6 +786,14 @@ struct fdgpu_ed25519_ctx {
   int fault;                     /* a batch failed on the device: the pipeline refuses new work */
   std::deque<int> inflight;      /* slot order */
 };
+
+extern "C" unsigned long
+fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long small_max ) {
+  if( !ctx ) return 0UL;
+  unsigned long old = ctx->small_max;
+  ctx->small_max = small_max;
+  return old;
+}
 
 extern "C" char const * fdgpu_last_error( void ) { return fd_err.c_str(); }
 
@@ -739,25 +818,38 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
   if( nsig ) {
     hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig );
     if( ctx->timing ) hipEventRecord( ev[0], st );
-    unsigned pg = (unsigned)( ( (FD_DEFER_R ? 1UL : 2UL)*sig_cnt + FD_WG - 1) / FD_WG );
-    hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
-                        ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy );
-    hipLaunchKernelGGL( fd_hash_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
-                        ctx->semantics, ctx->d_pstat, code, ctx->d_digA, ctx->d_digB, ctx->d_Rxy );
-    hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_Axy, ctx->d_tab );
+    /* small batch: cannot fill the GPU, so latency is the sum of the kernels' per-wave
+       instruction streams -- decode A, decode R and hash side by side in one launch,
+       R compared at the end of the DSM (no R-check chain and its inversion) */
+    int small = nsig <= ctx->small_max;
+    int defer = FD_DEFER_R && !small;
+    if( small ) {
+      hipLaunchKernelGGL( fd_prep_kernel, dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, (u32)sg,
+                          ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB );
+      hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, ctx->d_pstat, code,
+                          ctx->d_Axy, ctx->d_tab );
+    } else {
+      unsigned pg = (unsigned)( ( (defer ? 1UL : 2UL)*sig_cnt + FD_WG - 1) / FD_WG );
+      hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, !defer,
+                          ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy );
+      hipLaunchKernelGGL( fd_hash_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+                          ctx->semantics, defer, ctx->d_pstat, code, ctx->d_digA, ctx->d_digB, ctx->d_Rxy );
+      hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics,
+                          (unsigned char const *)NULL, code, ctx->d_Axy, ctx->d_tab );
+    }
     if( ctx->timing ) hipEventRecord( ev[1], st );
     hipLaunchKernelGGL( fd_dsm_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
-                        ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P );
+                        ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P, defer );
     if( ctx->timing ) hipEventRecord( ev[2], st );
-#if FD_DEFER_R
-    u32 * slow_cnt = ctx->d_slow + ctx->max_sig;
-    hipLaunchKernelGGL( fd_rprod_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_P, ctx->d_O, ctx->d_blk, slow_cnt );
-    hipLaunchKernelGGL( fd_rinv_kernel, dim3((sg + FD_WG - 1)/FD_WG), dim3(FD_WG), 0, st, sg, ctx->d_blk );
-    hipLaunchKernelGGL( fd_rcheck_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_Rxy, ctx->d_P, ctx->d_O, ctx->d_blk,
-                        ctx->d_slow, slow_cnt );
-    hipLaunchKernelGGL( fd_rslow_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, code, ctx->d_Rxy, ctx->d_P,
-                        ctx->d_slow, slow_cnt );
-#endif
+    if( defer ) {
+      u32 * slow_cnt = ctx->d_slow + ctx->max_sig;
+      hipLaunchKernelGGL( fd_rprod_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_P, ctx->d_O, ctx->d_blk, slow_cnt );
+      hipLaunchKernelGGL( fd_rinv_kernel, dim3((sg + FD_WG - 1)/FD_WG), dim3(FD_WG), 0, st, sg, ctx->d_blk );
+      hipLaunchKernelGGL( fd_rcheck_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_Rxy, ctx->d_P, ctx->d_O, ctx->d_blk,
+                          ctx->d_slow, slow_cnt );
+      hipLaunchKernelGGL( fd_rslow_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, code, ctx->d_Rxy, ctx->d_P,
+                          ctx->d_slow, slow_cnt );
+    }
   }
   hipLaunchKernelGGL( fd_reduce_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, nsig, code, d_pflag, d_txn_out );
   if( ctx->timing ) hipEventRecord( ev[3], st );
@@ -787,12 +879,12 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   HIPCHK( hipMalloc( &ctx->d_btab, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_rdesc, max_txn * sizeof(fdgpu_txn_desc_t) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_pflag, max_txn ), -1 );
-#if FD_DEFER_R
   HIPCHK( hipMalloc( &ctx->d_P, ns * 30 * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_O, ns * 10 * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_blk, ( ( ns + FD_WG - 1 ) / FD_WG ) * 10 * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_slow, ( ns + 1 ) * sizeof(u32) ), -1 );
-#endif
+  { char const * e = getenv( "FDGPU_SMALL_BATCH_MAX" );   /* A/B knob: signatures at or below take the latency path */
+    ctx->small_max = e ? strtoul( e, NULL, 0 ) : FD_SMALL_BATCH_MAX; }
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
@@ -957,12 +1049,16 @@ fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
   HIPCHK( hipSetDevice( ctx->device ), -2 );
   fd_slot & sl = ctx->slot[0];
   if( async_busy( ctx ) ) { fd_err = "async batches pending or in flight"; return -1; }
-  memcpy( sl.h_payload, payload, payload_bytes );
-  memset( sl.h_payload + payload_bytes, 0, FD_ARENA_SLACK );
-  memcpy( sl.h_desc, desc, txn_cnt * sizeof(fdgpu_txn_desc_t) );
   hipStream_t st = ctx->stream;
-  HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, payload_bytes + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+  memcpy( sl.h_desc, desc, txn_cnt * sizeof(fdgpu_txn_desc_t) );
   HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
+  /* stage in chunks: the DMA of chunk i overlaps the host copy of chunk i+1 */
+  memset( sl.h_payload + payload_bytes, 0, FD_ARENA_SLACK );
+  for( unsigned long off=0UL; off<payload_bytes+FD_ARENA_SLACK; off+=FD_STAGE_CHUNK ) {
+    unsigned long end = off + FD_STAGE_CHUNK < payload_bytes + FD_ARENA_SLACK ? off + FD_STAGE_CHUNK : payload_bytes + FD_ARENA_SLACK;
+    if( off < payload_bytes ) memcpy( sl.h_payload + off, payload + off, ( end < payload_bytes ? end : payload_bytes ) - off );
+    HIPCHK( hipMemcpyAsync( sl.d_payload + off, sl.h_payload + off, end - off, hipMemcpyHostToDevice, st ), -2 );
+  }
   int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, txn_cnt, nsig, sl.d_txn_out, NULL, st );
   if( rc ) return rc;
   HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, txn_cnt, hipMemcpyDeviceToHost, st ), -2 );

@@ -45,7 +45,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_verify_raw_host", "fdgpu_ed25519_submit", "fdgpu_ed25519_flush",
            "fdgpu_ed25519_poll", "fdgpu_ed25519_submit_raw", "fdgpu_ed25519_poll_raw", "fdgpu_ed25519_submit_raw_ref",
            "fdgpu_host_alloc", "fdgpu_host_free",
-           "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
+           "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_last_error")
 
 _lib = None
@@ -119,6 +119,8 @@ def load_library():
         L.fdgpu_ed25519_poll_raw.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int]
         L.fdgpu_ed25519_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.fdgpu_ed25519_set_small_batch_max.restype = ctypes.c_ulong
+        L.fdgpu_ed25519_set_small_batch_max.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
         L.fdgpu_ed25519_kernel_ms.restype = ctypes.c_float
         L.fdgpu_ed25519_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.fdgpu_last_error.restype = ctypes.c_char_p
@@ -215,6 +217,10 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+    def set_small_batch_max(self, n: int) -> int:
+        """Signatures per batch at or below which the latency path runs (0: never, 2**64-1: always)."""
+        return int(self.L.fdgpu_ed25519_set_small_batch_max(self.ctx, ctypes.c_ulong(n)))
 
     def set_timing(self, on: bool = True):
         self.L.fdgpu_ed25519_set_timing(self.ctx, 1 if on else 0)

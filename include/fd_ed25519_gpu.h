@@ -350,6 +350,17 @@ fdgpu_ed25519_poll_raw( fdgpu_ed25519_ctx_t * ctx,
                         unsigned long         max,
                         int                   blocking );
 
+/* Batches of at most small_max signatures take the latency path: one
+   launch decodes A, decodes R and hashes side by side, and R is compared
+   at the end of the DSM.  Larger batches take the throughput path: R is
+   not decompressed up front but checked against P's encoding after one
+   batched inversion per 256 signatures.  Both give identical codes.
+   Default FD_SMALL_BATCH_MAX (env FDGPU_SMALL_BATCH_MAX at context
+   creation); 0 forces the throughput path, ~0UL the latency path.
+   Returns the previous value. */
+unsigned long
+fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long small_max );
+
 /* Per-kernel timing, in milliseconds: the mean over the batches launched
    since fdgpu_ed25519_set_timing(ctx,1) (at most the last 64) of HIP
    events recorded on the stream the kernels ran on.  idx: 0 = prep

@@ -23,3 +23,22 @@ def golden():
     import numpy as np
     d = os.path.join(ROOT, "tests", "golden")
     return {k: dict(np.load(os.path.join(d, f"{k}.npz"))) for k in ("vectors", "txns", "sha")}
+
+
+# Every GPU test runs on both engine paths (include/fd_ed25519_gpu.h,
+# fdgpu_ed25519_set_small_batch_max): "throughput" (R checked after one
+# batched inversion per 256 signatures) and "latency" (one fused prep
+# launch, R decoded up front).  The engine reads FDGPU_SMALL_BATCH_MAX
+# when a context is created, so the choice reaches contexts the verify
+# tile library creates too.
+def pytest_generate_tests(metafunc):
+    if metafunc.definition.get_closest_marker("gpu") is not None and "engine_path" in metafunc.fixturenames:
+        metafunc.parametrize("engine_path", ["throughput", "latency"], indirect=True)
+
+
+@pytest.fixture(autouse=True)
+def engine_path(request, monkeypatch):
+    path = getattr(request, "param", None)
+    if path is not None:
+        monkeypatch.setenv("FDGPU_SMALL_BATCH_MAX", "0" if path == "throughput" else str(2**63))
+    return path
