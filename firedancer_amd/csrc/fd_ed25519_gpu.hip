@@ -75,7 +75,7 @@
    (fd_prep_kernel, R decoded up front): they cannot fill the GPU, so
    per-wave instruction streams, not total work, set their time. */
 #ifndef FD_SMALL_BATCH_MAX
-#define FD_SMALL_BATCH_MAX 65536UL
+#define FD_SMALL_BATCH_MAX 32768UL
 #endif
 #define FD_STAGE_CHUNK ( 1UL << 20 )   /* host-staged batches: bytes per memcpy / H2D step */
 #define FD_PEND_ASMALL 2           /* per-signature code in flight: A small order, R's decode picks ERR_SIG / ERR_PUBKEY */
@@ -153,6 +153,31 @@ fd_expand_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 *
   for( u32 j=0; j<d.sig_cnt; j++ ) {
     u32 s = d.sig_base + j;
     if( s < nsig ) map[s] = t | (j << 24);
+  }
+}
+
+/* [0..8](-A) in cached form from A's canonical affine coordinates */
+FD_DEV void atab_build( uint4 * __restrict__ tab, u32 s, uint4 const * __restrict__ Axy ) {
+  uint4 const * ap = Axy + (size_t)s*4;
+  ge_p3 A;
+  fe_from_quads( A.X, ap[0], ap[1] );
+  fe_from_quads( A.Y, ap[2], ap[3] );
+  A.Z = fe_one();
+  fe_neg( A.X, A.X ); fe_wcarry( A.X, A.X );              /* -A */
+  fe_mul( A.T, A.X, A.Y );
+  ge_cached c1, c;
+  c.YpX = fe_one(); c.YmX = fe_one(); c.Z = fe_one(); c.T2d = fe_zero();
+  atab_store( tab, s, 0, c );
+  ge_p3_to_cached( c1, A );
+  atab_store( tab, s, 1, c1 );
+  ge_p3 cur = A;
+#pragma unroll 1
+  for( int e=2; e<FD_ATAB_ENTRIES; e++ ) {
+    ge_p1p1 tt;
+    ge_add_cached( tt, cur, c1 );
+    ge_p1p1_to_p3( cur, tt );
+    ge_p3_to_cached( c, cur );
+    atab_store( tab, s, e, c );
   }
 }
 
@@ -330,12 +355,18 @@ fd_prep_kernel( unsigned char const *    __restrict__ payload,
                 uint4 *                  __restrict__ Axy,
                 i8 *                     __restrict__ code_out,
                 i8 *                     __restrict__ digA,
-                short *                  __restrict__ digB ) {
+                short *                  __restrict__ digB,
+                uint4 *                  __restrict__ tab ) {
   u32 role = blockIdx.x / sg, b = blockIdx.x - role*sg;
   u32 s = b * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
-  if( role < 2u ) decode_one( payload, desc, map, s, role, pstat, Rxy, Axy );
-  else            hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rxy );
+  if( role < 2u ) {
+    decode_one( payload, desc, map, s, role, pstat, Rxy, Axy );
+    /* tab != NULL: the A lane goes on to the -A table (for every A that
+       decoded; fd_dsm2_kernel applies the result-code procedure) */
+    if( tab && role==0u && ( pstat[2u*s] & 3u )==0u ) atab_build( tab, s, Axy );
+  }
+  else hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rxy );
 }
 
 /* Stage 3 -- table [0..8](-A) in cached form (fd_ed25519_point_neg + the
@@ -351,27 +382,7 @@ fd_table_kernel( u32 nsig, int semantics, unsigned char const * __restrict__ pst
     code[s] = (i8)c;
     if( c != FD_ED25519_SUCCESS ) return;
   } else if( code[s] != FD_ED25519_SUCCESS ) return;
-  uint4 const * ap = Axy + (size_t)s*4;
-  ge_p3 A;
-  fe_from_quads( A.X, ap[0], ap[1] );
-  fe_from_quads( A.Y, ap[2], ap[3] );
-  A.Z = fe_one();
-  fe_neg( A.X, A.X ); fe_wcarry( A.X, A.X );              /* -A */
-  fe_mul( A.T, A.X, A.Y );
-  ge_cached c1, c;
-  c.YpX = fe_one(); c.YmX = fe_one(); c.Z = fe_one(); c.T2d = fe_zero();
-  atab_store( tab, s, 0, c );
-  ge_p3_to_cached( c1, A );
-  atab_store( tab, s, 1, c1 );
-  ge_p3 cur = A;
-#pragma unroll 1
-  for( int e=2; e<FD_ATAB_ENTRIES; e++ ) {
-    ge_p1p1 tt;
-    ge_add_cached( tt, cur, c1 );
-    ge_p1p1_to_p3( cur, tt );
-    ge_p3_to_cached( c, cur );
-    atab_store( tab, s, e, c );
-  }
+  atab_build( tab, s, Axy );
 }
 
 __global__ void __launch_bounds__( FD_WG )
@@ -473,6 +484,182 @@ fd_dsm_kernel( u32                      nsig,
   fe_mul( u, x, P2.Z ); int okx = fe_eq( u, P2.X );
   fe_mul( u, y, P2.Z ); int oky = fe_eq( u, P2.Y );
   code[s] = (okx & oky) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+/* ---- latency path: two lanes per signature ------------------------------
+   A batch too small to fill the GPU finishes when one wave has issued its
+   whole DSM, so the latency path halves each lane's share of the field
+   work: lanes 2s and 2s+1 (h = 0, 1) of a wave share signature s and
+   exchange field elements with one DPP quad_perm[1,0,3,2] move per limb.
+   Every group-law step is split into two multiplications per lane:
+     doubling    lane 0 squares X and X+Y, lane 1 Y and Z; both lanes form
+                 E, F, G, H (eprint 2008/522 §4.4);
+     addition    lane 0 A = (Y+X)(Y2+X2) and C = T 2dT2, lane 1
+                 B = (Y-X)(Y2-X2) and D = Z Z2 (§4.2); a base-point
+                 entry (Z2 = 1) is the same step with Z2 = 1;
+     M-step      completed -> extended: lane 0 X3 = EF and T3 = EH, lane 1
+                 Y3 = GH and Z3 = GF.
+   The M-step output (lane 0 X3, T3; lane 1 Y3, Z3) is exactly what both
+   the next doubling and an addition take in, so between steps each lane
+   receives one element of its partner.  Each lane gathers only the two
+   coordinates of a table entry it multiplies by.  Per lane: 2 S + 2 M
+   and ~100 moves / selects per doubling instead of 4 S + 3 M -- about
+   0.73x the instruction stream of fd_dsm_kernel, at 1.35x its total
+   work, so it is only used when the batch leaves SIMDs idle. */
+/* Partner-lane exchange as DPP quad_perm[1,0,3,2] moves in inline asm,
+   one s_nop 1 ahead of them for the VALU-write -> DPP-read hazard.  (The
+   compiler's own lowering of __builtin_amdgcn_update_dpp gave wrong
+   results here on gfx950 -- measured: every valid signature rejected --
+   while these moves and a ds_swizzle __shfl_xor agree with the oracle.) */
+FD_DEV u32 fd_pair_xchg( u32 x ) {            /* value of the partner lane (lane ^ 1) */
+  u32 r;
+  asm volatile( "s_nop 1\n\tv_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=&v"( r ) : "v"( x ) );
+  return r;
+}
+FD_DEV void fe_xchg( fe & r, fe const & a ) {
+  asm volatile( "s_nop 1\n\t"
+                "v_mov_b32_dpp %0, %10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_mov_b32_dpp %1, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_mov_b32_dpp %2, %12 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_mov_b32_dpp %3, %13 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_mov_b32_dpp %4, %14 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_mov_b32_dpp %5, %15 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_mov_b32_dpp %6, %16 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_mov_b32_dpp %7, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_mov_b32_dpp %8, %18 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                "v_mov_b32_dpp %9, %19 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
+                : "=&v"( r.v[0] ), "=&v"( r.v[1] ), "=&v"( r.v[2] ), "=&v"( r.v[3] ), "=&v"( r.v[4] ),
+                  "=&v"( r.v[5] ), "=&v"( r.v[6] ), "=&v"( r.v[7] ), "=&v"( r.v[8] ), "=&v"( r.v[9] )
+                : "v"( a.v[0] ), "v"( a.v[1] ), "v"( a.v[2] ), "v"( a.v[3] ), "v"( a.v[4] ),
+                  "v"( a.v[5] ), "v"( a.v[6] ), "v"( a.v[7] ), "v"( a.v[8] ), "v"( a.v[9] ) );
+}
+
+/* M-step: from completed (E, F, G, H) on both lanes to lane 0 (m0, m1) =
+   (X3, T3), lane 1 (m0, m1) = (Y3, Z3); E, F, G, H T or L */
+FD_DEV void pair_mstep( fe & m0, fe & m1, int h, fe const & E, fe const & F, fe const & G, fe const & H ) {
+  fe u, v0, v1;
+  fe_sel( u,  h, G, E );
+  fe_sel( v0, h, H, F );
+  fe_sel( v1, h, F, H );
+  fe_mul( m0, u, v0 );
+  fe_mul( m1, u, v1 );
+}
+
+/* doubling of the point held as M-step output -> completed (E,F,G,H) on
+   both lanes */
+FD_DEV void pair_dbl( fe & E, fe & F, fe & G, fe & H, int h, fe const & m0, fe const & m1 ) {
+  fe s, a1, q0, q1, p0, p1, XX, YY, SS, ZZ, t;
+  fe_xchg( s, m0 );                                  /* lane 0: Y, lane 1: X */
+  fe_add( t, m0, s );                                /* X + Y */
+  fe_sel( a1, h, m1, t );                            /* lane 0: X+Y, lane 1: Z */
+  fe_sqr( q0, m0 );                                  /* lane 0: XX, lane 1: YY */
+  fe_sqr( q1, a1 );                                  /* lane 0: SS, lane 1: ZZ */
+  fe_xchg( p0, q0 ); fe_xchg( p1, q1 );
+  fe_sel( XX, h, p0, q0 ); fe_sel( YY, h, q0, p0 );
+  fe_sel( SS, h, p1, q1 ); fe_sel( ZZ, h, q1, p1 );
+  fe_add( H, YY, XX );                               /* H = YY+XX (L) */
+  fe_sub( G, YY, XX );                               /* G = YY-XX (L) */
+  fe_sub4( E, SS, H ); fe_wcarry( E, E );            /* E = SS-H = 2XY */
+  fe_add( t, ZZ, ZZ ); fe_sub4( F, t, G ); fe_wcarry( F, F );   /* F = 2ZZ-G */
+}
+
+/* P + Q from the M-step output; each lane passes the two coordinates of Q
+   it multiplies by (lane 0: Y2+X2 and 2dT2, lane 1: Y2-X2 and Z2), already
+   conditionally negated -> completed (E,F,G,H) on both lanes */
+FD_DEV void pair_add( fe & E, fe & F, fe & G, fe & H, int h, fe const & m0, fe const & m1,
+                      fe const & q0, fe const & q1 ) {
+  fe s, a, b, u, n0, n1, x0, x1, A, B, C, D;
+  fe_xchg( s, m0 );                                  /* lane 0: Y, lane 1: X */
+  fe_add( a, m0, s );                                /* lane 0: X+Y          */
+  fe_sub( b, m0, s );                                /* lane 1: Y-X          */
+  fe_sel( u, h, b, a );
+  fe_mul( n0, u, q0 );                               /* lane 0: A, lane 1: B */
+  fe_mul( n1, m1, q1 );                              /* lane 0: C, lane 1: Z Z2 */
+  fe_xchg( x0, n0 ); fe_xchg( x1, n1 );
+  fe_sel( A, h, x0, n0 ); fe_sel( B, h, n0, x0 );
+  fe_sel( C, h, x1, n1 ); fe_sel( D, h, n1, x1 );
+  fe_add( D, D, D );                                 /* D = 2 Z Z2 (L) */
+  fe_sub( E, A, B );                                 /* E = A-B (L) */
+  fe_add( H, A, B );                                 /* H = A+B (L) */
+  fe_add( G, D, C );                                 /* G = D+C (L) */
+  fe_sub4( F, D, C ); fe_wcarry( F, F );             /* F = D-C (T) */
+}
+
+__global__ void __launch_bounds__( FD_WG )
+fd_dsm2_kernel( u32                      nsig,
+                uint4 const * __restrict__ tab,
+                uint4 const * __restrict__ Rxy,
+                i8 const *    __restrict__ digA,
+                short const * __restrict__ digB,
+                uint4 const * __restrict__ btab_g,
+                i8 *          __restrict__ code,
+                int                        semantics,
+                unsigned char const * __restrict__ pstat ) {
+  u32 gl = blockIdx.x * FD_WG + threadIdx.x;
+  u32 s = gl >> 1;
+  int h = (int)( gl & 1u );
+  if( s >= nsig ) return;                            /* both lanes of a pair leave together */
+  {                                                  /* fd_prep_kernel left S's check only */
+    int c = result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 );
+    if( c != FD_ED25519_SUCCESS ) { if( !h ) code[s] = (i8)c; return; }
+  }
+  size_t n = nsig;
+
+  fe m0, m1, E, F, G, H, q0, q1;
+  fe one = fe_one(), zero = fe_zero();
+  fe_sel( m0, h, one, zero );                        /* identity: lane 0 X=0, T=0; lane 1 Y=1, Z=1 */
+  m1 = m0;
+  int da = digA[ (size_t)63*n + s ];
+  uint4 araw[4], braw[4];
+  int db = 0;
+#pragma unroll 1
+  for( int w=63; w>=0; w-- ) {
+    {                                                /* this lane's two coordinates of the -A entry */
+      int neg = da < 0, e = neg ? -da : da;
+      uint4 const * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8;
+      int c0 = h ^ neg;                              /* 0 YpX, 1 YmX (swapped when negated) */
+      int c1 = h ? 2 : 3;                            /* lane 0 T2d, lane 1 Z */
+      araw[0] = b[2*c0]; araw[1] = b[2*c0+1]; araw[2] = b[2*c1]; araw[3] = b[2*c1+1];
+    }
+    if( !(w & 3) ) {
+      db = digB[ (size_t)(w>>2)*n + s ];
+      int neg = db < 0, e = neg ? -db : db;
+      uint4 const * b = btab_g + (size_t)e*6;
+      int c0 = h ^ neg;                              /* 0 ypx, 1 ymx */
+      braw[0] = b[2*c0]; braw[1] = b[2*c0+1];
+      if( !h ) { braw[2] = b[4]; braw[3] = b[5]; }   /* lane 0 xy2d; lane 1 Z2 = 1 */
+    }
+    if( w != 63 ) {
+#pragma unroll 1
+      for( int r=0; r<4; r++ ) { pair_dbl( E, F, G, H, h, m0, m1 ); pair_mstep( m0, m1, h, E, F, G, H ); }
+    }
+    fe_from_quads( q0, araw[0], araw[1] );
+    fe_from_quads( q1, araw[2], araw[3] );
+    { fe nq; fe_neg( nq, q1 ); fe_sel( q1, !h && da < 0, nq, q1 ); }
+    pair_add( E, F, G, H, h, m0, m1, q0, q1 );
+    pair_mstep( m0, m1, h, E, F, G, H );
+    if( !(w & 3) ) {
+      fe_from_quads( q0, braw[0], braw[1] );
+      if( h ) q1 = one;
+      else {
+        fe_from_quads( q1, braw[2], braw[3] );
+        fe nq; fe_neg( nq, q1 ); fe_sel( q1, db < 0, nq, q1 );
+      }
+      pair_add( E, F, G, H, h, m0, m1, q0, q1 );
+      pair_mstep( m0, m1, h, E, F, G, H );
+    }
+    if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
+  }
+  /* fd_ed25519_point_eq_z1: lane 0 X == x_R Z, lane 1 Y == y_R Z */
+  fe z, r, u;
+  fe_xchg( z, m1 );
+  fe_sel( z, h, m1, z );
+  uint4 const * rp = Rxy + (size_t)s*4 + 2*h;
+  fe_from_quads( r, rp[0], rp[1] );
+  fe_mul( u, r, z );
+  u32 ok = (u32)fe_eq( u, m0 );
+  ok &= fd_pair_xchg( ok );
+  if( !h ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
 /* ---- deferred R check (FD_DEFER_R) ---------------------------------------
@@ -770,6 +957,7 @@ struct fdgpu_ed25519_ctx {
   uint4 * d_btab;
   fdgpu_txn_desc_t * d_rdesc;    /* raw path: descriptors derived by fd_parse_kernel */
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
+  int dsm2;                      /* latency path: two lanes per signature in the DSM (env FDGPU_DSM2=0 turns it off) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
   u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
   u32 *   d_O;                   /*             product of the block's other Z, planar [10][max_sig] */
@@ -824,10 +1012,13 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     int small = nsig <= ctx->small_max;
     int defer = FD_DEFER_R && !small;
     if( small ) {
+      int d2 = ctx->dsm2;
       hipLaunchKernelGGL( fd_prep_kernel, dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, (u32)sg,
-                          ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB );
-      hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, ctx->d_pstat, code,
-                          ctx->d_Axy, ctx->d_tab );
+                          ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
+                          d2 ? ctx->d_tab : (uint4 *)NULL );
+      if( !d2 )
+        hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, ctx->d_pstat, code,
+                            ctx->d_Axy, ctx->d_tab );
     } else {
       unsigned pg = (unsigned)( ( (defer ? 1UL : 2UL)*sig_cnt + FD_WG - 1) / FD_WG );
       hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, !defer,
@@ -838,8 +1029,12 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
                           (unsigned char const *)NULL, code, ctx->d_Axy, ctx->d_tab );
     }
     if( ctx->timing ) hipEventRecord( ev[1], st );
-    hipLaunchKernelGGL( fd_dsm_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
-                        ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P, defer );
+    if( small && ctx->dsm2 )
+      hipLaunchKernelGGL( fd_dsm2_kernel, dim3(2*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
+                          ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat );
+    else
+      hipLaunchKernelGGL( fd_dsm_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
+                          ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P, defer );
     if( ctx->timing ) hipEventRecord( ev[2], st );
     if( defer ) {
       u32 * slow_cnt = ctx->d_slow + ctx->max_sig;
@@ -884,7 +1079,9 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   HIPCHK( hipMalloc( &ctx->d_blk, ( ( ns + FD_WG - 1 ) / FD_WG ) * 10 * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_slow, ( ns + 1 ) * sizeof(u32) ), -1 );
   { char const * e = getenv( "FDGPU_SMALL_BATCH_MAX" );   /* A/B knob: signatures at or below take the latency path */
-    ctx->small_max = e ? strtoul( e, NULL, 0 ) : FD_SMALL_BATCH_MAX; }
+    ctx->small_max = e ? strtoul( e, NULL, 0 ) : FD_SMALL_BATCH_MAX;
+    char const * d2 = getenv( "FDGPU_DSM2" );
+    ctx->dsm2 = d2 ? atoi( d2 ) : 1; }
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
