@@ -77,6 +77,9 @@
 #ifndef FD_SMALL_BATCH_MAX
 #define FD_SMALL_BATCH_MAX 32768UL
 #endif
+#ifndef FD_DSM4_MAX
+#define FD_DSM4_MAX 16384UL          /* latency path: four lanes per signature up to here, then two */
+#endif
 #define FD_STAGE_CHUNK ( 1UL << 20 )   /* host-staged batches: bytes per memcpy / H2D step */
 #define FD_PEND_ASMALL 2           /* per-signature code in flight: A small order, R's decode picks ERR_SIG / ERR_PUBKEY */
 #define FD_PEND_REQ    3           /* per-signature code in flight: P's encoding != R's bytes -> decode R, compare */
@@ -506,33 +509,40 @@ fd_dsm_kernel( u32                      nsig,
    and ~100 moves / selects per doubling instead of 4 S + 3 M -- about
    0.73x the instruction stream of fd_dsm_kernel, at 1.35x its total
    work, so it is only used when the batch leaves SIMDs idle. */
-/* Partner-lane exchange as DPP quad_perm[1,0,3,2] moves in inline asm,
+/* Lane exchanges as DPP quad_perm moves in inline asm,
    one s_nop 1 ahead of them for the VALU-write -> DPP-read hazard.  (The
    compiler's own lowering of __builtin_amdgcn_update_dpp gave wrong
    results here on gfx950 -- measured: every valid signature rejected --
    while these moves and a ds_swizzle __shfl_xor agree with the oracle.) */
-FD_DEV u32 fd_pair_xchg( u32 x ) {            /* value of the partner lane (lane ^ 1) */
-  u32 r;
-  asm volatile( "s_nop 1\n\tv_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "=&v"( r ) : "v"( x ) );
-  return r;
+#define FD_DPP_MOV( d, a, PERM ) "v_mov_b32_dpp %" #d ", %" #a " " PERM " row_mask:0xf bank_mask:0xf\n\t"
+/* r = a as seen through one quad_perm (10 moves, one asm block) */
+#define FD_DEF_FE_DPP( name, PERM )                                                        \
+FD_DEV void name( fe & r, fe const & a ) {                                                 \
+  asm volatile( "s_nop 1\n\t"                                                              \
+                FD_DPP_MOV( 0, 10, PERM ) FD_DPP_MOV( 1, 11, PERM ) FD_DPP_MOV( 2, 12, PERM ) \
+                FD_DPP_MOV( 3, 13, PERM ) FD_DPP_MOV( 4, 14, PERM ) FD_DPP_MOV( 5, 15, PERM ) \
+                FD_DPP_MOV( 6, 16, PERM ) FD_DPP_MOV( 7, 17, PERM ) FD_DPP_MOV( 8, 18, PERM ) \
+                FD_DPP_MOV( 9, 19, PERM )                                                  \
+                : "=&v"( r.v[0] ), "=&v"( r.v[1] ), "=&v"( r.v[2] ), "=&v"( r.v[3] ), "=&v"( r.v[4] ), \
+                  "=&v"( r.v[5] ), "=&v"( r.v[6] ), "=&v"( r.v[7] ), "=&v"( r.v[8] ), "=&v"( r.v[9] ) \
+                : "v"( a.v[0] ), "v"( a.v[1] ), "v"( a.v[2] ), "v"( a.v[3] ), "v"( a.v[4] ),  \
+                  "v"( a.v[5] ), "v"( a.v[6] ), "v"( a.v[7] ), "v"( a.v[8] ), "v"( a.v[9] ) ); \
 }
-FD_DEV void fe_xchg( fe & r, fe const & a ) {
-  asm volatile( "s_nop 1\n\t"
-                "v_mov_b32_dpp %0, %10 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                "v_mov_b32_dpp %1, %11 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                "v_mov_b32_dpp %2, %12 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                "v_mov_b32_dpp %3, %13 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                "v_mov_b32_dpp %4, %14 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                "v_mov_b32_dpp %5, %15 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                "v_mov_b32_dpp %6, %16 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                "v_mov_b32_dpp %7, %17 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                "v_mov_b32_dpp %8, %18 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                "v_mov_b32_dpp %9, %19 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
-                : "=&v"( r.v[0] ), "=&v"( r.v[1] ), "=&v"( r.v[2] ), "=&v"( r.v[3] ), "=&v"( r.v[4] ),
-                  "=&v"( r.v[5] ), "=&v"( r.v[6] ), "=&v"( r.v[7] ), "=&v"( r.v[8] ), "=&v"( r.v[9] )
-                : "v"( a.v[0] ), "v"( a.v[1] ), "v"( a.v[2] ), "v"( a.v[3] ), "v"( a.v[4] ),
-                  "v"( a.v[5] ), "v"( a.v[6] ), "v"( a.v[7] ), "v"( a.v[8] ), "v"( a.v[9] ) );
+#define FD_DEF_U32_DPP( name, PERM )                                                       \
+FD_DEV u32 name( u32 x ) {                                                                 \
+  u32 r;                                                                                   \
+  asm volatile( "s_nop 1\n\t" FD_DPP_MOV( 0, 1, PERM ) : "=&v"( r ) : "v"( x ) );          \
+  return r;                                                                                \
 }
+FD_DEF_U32_DPP( fd_pair_xchg, "quad_perm:[1,0,3,2]" )   /* value of the partner lane (lane ^ 1) */
+FD_DEF_FE_DPP( fe_xchg,   "quad_perm:[1,0,3,2]" )
+FD_DEF_FE_DPP( fe_bcast0, "quad_perm:[0,0,0,0]" )       /* quad lane k's value in all four lanes */
+FD_DEF_FE_DPP( fe_bcast1, "quad_perm:[1,1,1,1]" )
+FD_DEF_FE_DPP( fe_bcast2, "quad_perm:[2,2,2,2]" )
+FD_DEF_FE_DPP( fe_bcast3, "quad_perm:[3,3,3,3]" )
+FD_DEF_FE_DPP( fe_swap23, "quad_perm:[0,1,3,2]" )       /* lanes 2 and 3 trade */
+FD_DEF_U32_DPP( fd_bcast0, "quad_perm:[0,0,0,0]" )
+FD_DEF_U32_DPP( fd_bcast1, "quad_perm:[1,1,1,1]" )
 
 /* M-step: from completed (E, F, G, H) on both lanes to lane 0 (m0, m1) =
    (X3, T3), lane 1 (m0, m1) = (Y3, Z3); E, F, G, H T or L */
@@ -660,6 +670,129 @@ fd_dsm2_kernel( u32                      nsig,
   u32 ok = (u32)fe_eq( u, m0 );
   ok &= fd_pair_xchg( ok );
   if( !h ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+/* ---- latency path: four lanes per signature -----------------------------
+   The same split taken one step further for the smallest batches: the
+   four lanes q = 0..3 of a DPP quad share signature s, and every
+   group-law step is ONE field multiplication per lane:
+     doubling    lane q squares X, Y, Z, X+Y;
+     addition    lane 0 A = (Y+X)(Y2+X2), lane 1 B = (Y-X)(Y2-X2),
+                 lane 2 C = T 2dT2, lane 3 D = Z Z2;
+     M-step      lane q forms X3 = EF, Y3 = GH, Z3 = GF, T3 = EH,
+   so after an M-step lane q holds coordinate q of the point.  Between
+   steps the lanes read each other's results with quad_perm broadcasts
+   (10 DPP moves per element).  Per lane and doubling: 1 S + 1 M and
+   ~200 moves / adds / selects -- about 0.7x the chain of fd_dsm2_kernel
+   for 2.1x the total work of fd_dsm_kernel. */
+
+/* M-step: E, F, G, H (T or L) on all lanes -> coordinate q of the point */
+FD_DEV void quad_mstep( fe & m, int q, fe const & E, fe const & F, fe const & G, fe const & H ) {
+  fe u, v;
+  fe_sel( u, q==0 || q==3, E, G );
+  fe_sel( v, q & 1, H, F );
+  fe_mul( m, u, v );
+}
+
+FD_DEV void quad_dbl( fe & E, fe & F, fe & G, fe & H, int q, fe const & m ) {
+  fe x, y, a, sq, XX, YY, ZZ, SS, t;
+  fe_bcast0( x, m ); fe_bcast1( y, m );
+  fe_add( t, x, y );
+  fe_sel( a, q==3, t, m );                           /* X, Y, Z, X+Y */
+  fe_sqr( sq, a );
+  fe_bcast0( XX, sq ); fe_bcast1( YY, sq ); fe_bcast2( ZZ, sq ); fe_bcast3( SS, sq );
+  fe_add( H, YY, XX );                               /* H = YY+XX (L) */
+  fe_sub( G, YY, XX );                               /* G = YY-XX (L) */
+  fe_sub4( E, SS, H ); fe_wcarry( E, E );            /* E = SS-H = 2XY */
+  fe_add( t, ZZ, ZZ ); fe_sub4( F, t, G ); fe_wcarry( F, F );   /* F = 2ZZ-G */
+}
+
+/* P + Q; lane q passes the coordinate of Q it multiplies by (Y2+X2,
+   Y2-X2, 2dT2, Z2), already conditionally negated */
+FD_DEV void quad_add( fe & E, fe & F, fe & G, fe & H, int q, fe const & m, fe const & c ) {
+  fe x, y, w, a, b, u, n, A, B, C, D;
+  fe_bcast0( x, m ); fe_bcast1( y, m ); fe_swap23( w, m );   /* lane 2: T, lane 3: Z */
+  fe_add( a, y, x );
+  fe_sub( b, y, x );
+  fe_sel( u, q==1, b, a );
+  fe_sel( u, q>=2, w, u );
+  fe_mul( n, u, c );
+  fe_bcast0( A, n ); fe_bcast1( B, n ); fe_bcast2( C, n ); fe_bcast3( D, n );
+  fe_add( D, D, D );                                 /* D = 2 Z Z2 (L) */
+  fe_sub( E, A, B );
+  fe_add( H, A, B );
+  fe_add( G, D, C );
+  fe_sub4( F, D, C ); fe_wcarry( F, F );
+}
+
+__global__ void __launch_bounds__( FD_WG )
+fd_dsm4_kernel( u32                      nsig,
+                uint4 const * __restrict__ tab,
+                uint4 const * __restrict__ Rxy,
+                i8 const *    __restrict__ digA,
+                short const * __restrict__ digB,
+                uint4 const * __restrict__ btab_g,
+                i8 *          __restrict__ code,
+                int                        semantics,
+                unsigned char const * __restrict__ pstat ) {
+  u32 gl = blockIdx.x * FD_WG + threadIdx.x;
+  u32 s = gl >> 2;
+  int q = (int)( gl & 3u );
+  if( s >= nsig ) return;                            /* the four lanes of a quad leave together */
+  {                                                  /* fd_prep_kernel left S's check only */
+    int c = result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 );
+    if( c != FD_ED25519_SUCCESS ) { if( !q ) code[s] = (i8)c; return; }
+  }
+  size_t n = nsig;
+  fe m, E, F, G, H, c;
+  fe one = fe_one(), zero = fe_zero();
+  fe_sel( m, q==1 || q==2, one, zero );              /* identity (0 : 1 : 1 : 0) */
+  int da = digA[ (size_t)63*n + s ];
+  uint4 araw[2], braw[2];
+  int db = 0;
+#pragma unroll 1
+  for( int w=63; w>=0; w-- ) {
+    {                                                /* this lane's coordinate of the -A entry */
+      int neg = da < 0, e = neg ? -da : da;
+      int ci = q < 2 ? ( q ^ neg ) : ( q==2 ? 3 : 2 );   /* YpX / YmX (swapped when negated), T2d, Z */
+      uint4 const * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8 + 2*ci;
+      araw[0] = b[0]; araw[1] = b[1];
+    }
+    if( !(w & 3) ) {
+      db = digB[ (size_t)(w>>2)*n + s ];
+      int neg = db < 0, e = neg ? -db : db;
+      int ci = q < 2 ? ( q ^ neg ) : 2;              /* ypx / ymx, xy2d; lane 3: Z2 = 1 */
+      uint4 const * b = btab_g + (size_t)e*6 + 2*ci;
+      if( q < 3 ) { braw[0] = b[0]; braw[1] = b[1]; }
+    }
+    if( w != 63 ) {
+#pragma unroll 1
+      for( int r=0; r<4; r++ ) { quad_dbl( E, F, G, H, q, m ); quad_mstep( m, q, E, F, G, H ); }
+    }
+    fe_from_quads( c, araw[0], araw[1] );
+    { fe nc; fe_neg( nc, c ); fe_sel( c, q==2 && da < 0, nc, c ); }
+    quad_add( E, F, G, H, q, m, c );
+    quad_mstep( m, q, E, F, G, H );
+    if( !(w & 3) ) {
+      if( q == 3 ) c = one;
+      else {
+        fe_from_quads( c, braw[0], braw[1] );
+        fe nc; fe_neg( nc, c ); fe_sel( c, q==2 && db < 0, nc, c );
+      }
+      quad_add( E, F, G, H, q, m, c );
+      quad_mstep( m, q, E, F, G, H );
+    }
+    if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
+  }
+  /* fd_ed25519_point_eq_z1: lane 0 X == x_R Z, lane 1 Y == y_R Z */
+  fe z, r, u;
+  fe_bcast2( z, m );
+  uint4 const * rp = Rxy + (size_t)s*4 + 2*( q & 1 );
+  fe_from_quads( r, rp[0], rp[1] );
+  fe_mul( u, r, z );
+  u32 ok = (u32)fe_eq( u, m );
+  ok = fd_bcast0( ok ) & fd_bcast1( ok );
+  if( !q ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
 /* ---- deferred R check (FD_DEFER_R) ---------------------------------------
@@ -957,7 +1090,7 @@ struct fdgpu_ed25519_ctx {
   uint4 * d_btab;
   fdgpu_txn_desc_t * d_rdesc;    /* raw path: descriptors derived by fd_parse_kernel */
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
-  int dsm2;                      /* latency path: two lanes per signature in the DSM (env FDGPU_DSM2=0 turns it off) */
+  int dsm_lanes;                 /* latency path: lanes per signature in the DSM, 0 = by batch size (env FDGPU_DSM_LANES) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
   u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
   u32 *   d_O;                   /*             product of the block's other Z, planar [10][max_sig] */
@@ -1009,10 +1142,13 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     /* small batch: cannot fill the GPU, so latency is the sum of the kernels' per-wave
        instruction streams -- decode A, decode R and hash side by side in one launch,
        R compared at the end of the DSM (no R-check chain and its inversion) */
-    int small = nsig <= ctx->small_max;
+    int small = nsig <= ctx->small_max, lanes = 1;
     int defer = FD_DEFER_R && !small;
     if( small ) {
-      int d2 = ctx->dsm2;
+      /* lanes per signature in the DSM: 4 while a quad per signature still fits one wave per
+         SIMD (n <= 16K), else 2 */
+      lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM4_MAX ? 4 : 2 );
+      int d2 = lanes > 1;
       hipLaunchKernelGGL( fd_prep_kernel, dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, (u32)sg,
                           ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
                           d2 ? ctx->d_tab : (uint4 *)NULL );
@@ -1029,7 +1165,10 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
                           (unsigned char const *)NULL, code, ctx->d_Axy, ctx->d_tab );
     }
     if( ctx->timing ) hipEventRecord( ev[1], st );
-    if( small && ctx->dsm2 )
+    if( small && lanes==4 )
+      hipLaunchKernelGGL( fd_dsm4_kernel, dim3(4*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
+                          ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat );
+    else if( small && lanes==2 )
       hipLaunchKernelGGL( fd_dsm2_kernel, dim3(2*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                           ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat );
     else
@@ -1080,8 +1219,8 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   HIPCHK( hipMalloc( &ctx->d_slow, ( ns + 1 ) * sizeof(u32) ), -1 );
   { char const * e = getenv( "FDGPU_SMALL_BATCH_MAX" );   /* A/B knob: signatures at or below take the latency path */
     ctx->small_max = e ? strtoul( e, NULL, 0 ) : FD_SMALL_BATCH_MAX;
-    char const * d2 = getenv( "FDGPU_DSM2" );
-    ctx->dsm2 = d2 ? atoi( d2 ) : 1; }
+    char const * dl = getenv( "FDGPU_DSM_LANES" );
+    ctx->dsm_lanes = dl ? atoi( dl ) : 0; }
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;

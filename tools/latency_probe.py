@@ -22,9 +22,10 @@ def main():
     nmax = max(sizes)
     payload, desc, expect, nsig = synth.make_batch(nmax, synth.LARGE_NOOP, seed=7, threads=16)
     out = {}
-    for n, path in [(n, p) for n in sizes for p in ("throughput", "latency")]:
+    for n, path in [(n, p) for n in sizes for p in ("throughput", "latency4", "latency2")]:
         lpay = payload[: int(desc["payload_off"][n - 1]) + 1232 + 64]
         d = desc[:n].copy()
+        os.environ["FDGPU_DSM_LANES"] = path[-1] if path.startswith("latency") else "0"   # read at ctx creation
         eng = Engine(device=0, max_txn=n, max_sig=n, max_payload=lpay.nbytes)
         eng.set_small_batch_max(0 if path == "throughput" else 2**63)
         pay_d = torch.from_numpy(lpay).cuda()
