@@ -197,8 +197,8 @@ def main():
         leng.close()
         lat = {"batch_txns": lb, "p50_ms": float(np.percentile(times, 50)), "p99_ms": float(np.percentile(times, 99)),
                "path": "fdgpu_ed25519_verify_txns_host: pinned staging in 1-MB chunks overlapped with H2D, "
-                       "latency path (one fused launch: decode A + -A table / decode R / hash; two-lanes-per-"
-                       "signature DSM with R compare; reduce), D2H",
+                       "latency path (one fused launch: decode A + -A table / decode R / hash; DSM on four lanes "
+                       "per signature with R compare; reduce), D2H",
                "device_p50_ms": float(np.percentile(dtimes, 50)), "device_p99_ms": float(np.percentile(dtimes, 99)),
                "device_path": "same batch resident in HBM: kernels only, launch -> stream idle",
                "samples": len(times)}
