@@ -1,0 +1,78 @@
+// Issue-rate probe for single VALU instructions on gfx950: every lane runs
+// 16 independent chains of one instruction (inline asm, so the compiler
+// cannot rewrite it), 8 waves per SIMD over the whole chip.  Prints
+// G instructions (lane-ops) / s per instruction kind.
+// build: hipcc --offload-arch=gfx950 -O3 -o tools/instprobe/instprobe tools/instprobe/instprobe.hip
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+
+#define CH 16
+#define DEF_K( NAME, BODY )                                                         \
+__global__ void __launch_bounds__( 256 ) NAME( unsigned iters, unsigned seed, unsigned * out ) {  \
+  unsigned v[CH];                                                                   \
+  _Pragma("unroll") for( int c=0; c<CH; c++ ) v[c] = seed + threadIdx.x * 7u + c;    \
+  for( unsigned i=0; i<iters; i++ ) {                                               \
+    _Pragma("unroll") for( int c=0; c<CH; c++ ) { BODY; }                           \
+  }                                                                                 \
+  unsigned r = 0; _Pragma("unroll") for( int c=0; c<CH; c++ ) r ^= v[c];             \
+  if( r == 0x12345678u ) out[0] = r;                                                \
+}
+DEF_K( k_add,    asm volatile( "v_add_u32 %0, %0, %1" : "+v"( v[c] ) : "v"( seed ) ) )
+DEF_K( k_addself,asm volatile( "v_add_u32 %0, %0, %0" : "+v"( v[c] ) ) )
+DEF_K( k_lshl,   asm volatile( "v_lshlrev_b32 %0, 1, %0" : "+v"( v[c] ) ) )
+DEF_K( k_and,    asm volatile( "v_and_b32 %0, %0, %1" : "+v"( v[c] ) : "v"( seed ) ) )
+DEF_K( k_mullo,  asm volatile( "v_mul_lo_u32 %0, %0, 19" : "+v"( v[c] ) ) )
+DEF_K( k_mad24,  asm volatile( "v_mad_u32_u24 %0, %0, 19, %1" : "+v"( v[c] ) : "v"( seed ) ) )
+DEF_K( k_align,  asm volatile( "v_alignbit_b32 %0, %0, %1, 7" : "+v"( v[c] ) : "v"( seed ) ) )
+DEF_K( k_bitop3, asm volatile( "v_bitop3_b32 %0, %0, %1, %1 bitop3:0x96" : "+v"( v[c] ) : "v"( seed ) ) )
+DEF_K( k_cndmask,asm volatile( "v_cmp_gt_u32 vcc, 3, %1\n\tv_cndmask_b32 %0, %0, %1, vcc" : "+v"( v[c] ) : "v"( threadIdx.x ) : "vcc" ) )
+DEF_K( k_cndsel, unsigned m = threadIdx.x & 1u; v[c] = m ? v[c] + seed : v[c] ^ seed )
+DEF_K( k_dpp,    asm volatile( "v_mov_b32_dpp %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf" : "+v"( v[c] ) ) )
+DEF_K( k_lshladd,asm volatile( "v_lshl_add_u32 %0, %0, 4, %1" : "+v"( v[c] ) : "v"( seed ) ) )
+
+__global__ void __launch_bounds__( 256 ) k_mad64( unsigned iters, unsigned seed, unsigned * out ) {
+  uint64_t v[CH / 2];
+  for( int c=0; c<CH/2; c++ ) v[c] = seed + threadIdx.x * 7u + c;
+  for( unsigned i=0; i<iters; i++ ) {
+#pragma unroll
+    for( int c=0; c<CH/2; c++ ) asm volatile( "v_mad_u64_u32 %0, vcc, %1, %1, %0" : "+v"( v[c] ) : "v"( seed ) : "vcc" );
+  }
+  uint64_t r = 0; for( int c=0; c<CH/2; c++ ) r ^= v[c];
+  if( r == 0x12345678u ) out[0] = (unsigned)r;
+}
+__global__ void __launch_bounds__( 256 ) k_lshr64( unsigned iters, unsigned seed, unsigned * out ) {
+  uint64_t v[CH / 2];
+  for( int c=0; c<CH/2; c++ ) v[c] = seed + threadIdx.x * 7u + c;
+  for( unsigned i=0; i<iters; i++ ) {
+#pragma unroll
+    for( int c=0; c<CH/2; c++ ) asm volatile( "v_lshrrev_b64 %0, 1, %0" : "+v"( v[c] ) );
+  }
+  uint64_t r = 0; for( int c=0; c<CH/2; c++ ) r ^= v[c];
+  if( r == 0x12345678u ) out[0] = (unsigned)r;
+}
+
+typedef void (*kfn)( unsigned, unsigned, unsigned * );
+int main() {
+  struct { char const * name; kfn f; int per; } ks[] = {
+    { "v_add_u32",         k_add,     CH }, { "v_add_u32 (x+x)", k_addself, CH }, { "v_lshlrev_b32", k_lshl, CH },
+    { "v_and_b32",         k_and,     CH }, { "v_mul_lo_u32",    k_mullo,   CH }, { "v_mad_u32_u24", k_mad24, CH },
+    { "v_alignbit_b32",    k_align,   CH }, { "v_bitop3_b32",    k_bitop3,  CH }, { "v_cmp+v_cndmask", k_cndmask, CH },
+    { "sel (compiler)", k_cndsel, CH }, { "v_mov_b32_dpp", k_dpp, CH }, { "v_lshl_add_u32", k_lshladd, CH },
+    { "v_mad_u64_u32",     k_mad64, CH/2 }, { "v_lshrrev_b64",   k_lshr64, CH/2 } };
+  int ncu = 0; hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, 0 );
+  unsigned * out; hipMalloc( &out, 4 );
+  unsigned iters = 4096; int blocks = ncu * 8;        /* 8 x 256 threads per CU = 8 waves per SIMD */
+  hipEvent_t a, b; hipEventCreate( &a ); hipEventCreate( &b );
+  for( auto & k : ks ) {
+    hipLaunchKernelGGL( k.f, dim3(blocks), dim3(256), 0, 0, 16u, 1u, out );
+    float best = 1e30f;
+    for( int r=0; r<3; r++ ) {
+      hipEventRecord( a ); hipLaunchKernelGGL( k.f, dim3(blocks), dim3(256), 0, 0, iters, 1u, out ); hipEventRecord( b );
+      hipEventSynchronize( b ); float ms; hipEventElapsedTime( &ms, a, b ); if( ms < best ) best = ms;
+    }
+    double ops = (double)blocks * 256.0 * iters * k.per;
+    printf( "%-18s %8.1f G lane-ops/s\n", k.name, ops / ( best * 1e-3 ) * 1e-9 );
+  }
+  return 0;
+}
