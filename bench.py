@@ -244,11 +244,20 @@ def main():
                   "all_published": bool(ok_s),
                   "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
 
+    # per-GPU VALU utilisation (north star): every rank prices its own DSM launches against its own
+    # measured v_mad_u64_u32 peak; rank 0 reports the list
+    L = load_library()
+    L.fdgpu_mad_peak_per_s.restype = ctypes.c_double
+    L.fdgpu_mad_peak_per_s.argtypes = [ctypes.c_int]
+    my_peak = max(float(L.fdgpu_mad_peak_per_s(local_rank)) for _ in range(3))
+    my_ach = DSM_MAC * nsig / (ms_dsm * 1e-3)
+    rows = shard.gather_rows(dist if world > 1 else None, [rank, ms_dsm, ms_prep, my_ach, my_peak, dt], "cuda")
+    per_gpu = [{"rank": int(r[0]), "dsm_ms": r[1], "prep_ms": r[2], "achieved_gmac_s": r[3] / 1e9,
+                "peak_gmac_s": r[4] / 1e9, "frac": r[3] / r[4] if r[4] > 0 else None,
+                "sigs_per_s": nsig * args.steps / r[5]} for r in rows]
+
     if rank == 0:
-        L = load_library()
-        L.fdgpu_mad_peak_per_s.restype = ctypes.c_double
-        L.fdgpu_mad_peak_per_s.argtypes = [ctypes.c_int]
-        peak = max(float(L.fdgpu_mad_peak_per_s(local_rank)) for _ in range(3))
+        peak = my_peak
         dom_ms = ms_dsm
         achieved = DSM_MAC * nsig / (dom_ms * 1e-3)
         traffic = None
@@ -291,6 +300,7 @@ def main():
                          "valu_busy": valu_busy,
                          "valu_busy_source": "profiles/dsm_pmc.json: SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE/8)"},
             "cpu_baseline": cpu,
+            "per_gpu": per_gpu,
             "latency": lat,
             "stream": stream,
             "extra_configs": extra,

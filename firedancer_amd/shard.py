@@ -75,3 +75,14 @@ def reduce_sum_max(dist, units: float, seconds: float, device) -> tuple[float, f
         dist.all_reduce(s, op=dist.ReduceOp.MAX)
         w = dist.get_world_size()
     return float(u.item()), float(s.item()), w
+
+
+def gather_rows(dist, row: list[float], device) -> list[list[float]]:
+    """Every rank's small vector of measurements, in rank order (rank 0 uses them for the per-GPU report)."""
+    import torch
+    t = torch.tensor([float(x) for x in row], dtype=torch.float64, device=device)
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [t.tolist()]
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [o.tolist() for o in out]

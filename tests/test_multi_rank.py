@@ -39,6 +39,9 @@ def _worker(rank, world, port, q):
     # the configs[4] stream aggregate: SUM of per-rank sigs over the MAX per-rank stream time
     ssum, smax, sw = shard.reduce_sum_max(dist, units=1000 * (rank + 1), seconds=0.5 * (rank + 1), device="cpu")
     assert (ssum, smax, sw) == (3000.0, 1.0, 2)
+    # the per-GPU report: every rank's row, in rank order
+    rows = shard.gather_rows(dist, [rank, 10.0 * rank + 0.5], device="cpu")
+    assert rows == [[float(r), 10.0 * r + 0.5] for r in range(world)]
     q.put((rank, dt, dt_max, ok, not_ok, value, [g.numpy().tobytes() for g in gathered], nsig))
     dist.barrier()
     dist.destroy_process_group()
