@@ -1041,6 +1041,26 @@ __global__ void __launch_bounds__( 256 ) fd_btab_kernel( uint4 * out ) {
   fe_store_packed( o + 4, xy );
 }
 
+struct fd_gather {             /* mode 3: copy sz bytes from src (host, device view) to arena / region offset dst */
+  unsigned long src;
+  unsigned int  dst;
+  unsigned int  sz;            /* multiple of 16 */
+};
+
+/* Gathered raw batches (fdgpu_ed25519_submit_raw_gather): one 64-lane
+   group per record copies it, 16 B per lane, from the caller's in region
+   (host memory registered with the GPU, read over PCIe) into the batch
+   arena and into the record's place in the caller's out region -- the
+   host never touches the payload bytes. */
+__global__ void __launch_bounds__( 64 )
+fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__ arena, unsigned char * __restrict__ out ) {
+  fd_gather r = g[ blockIdx.x ];
+  uint4 const * src = (uint4 const *)r.src;
+  uint4 * a = (uint4 *)( arena + r.dst );
+  uint4 * o = (uint4 *)( out + r.dst );
+  for( u32 i=threadIdx.x; i<(r.sz >> 4); i+=64u ) { uint4 v = src[i]; a[i] = v; o[i] = v; }
+}
+
 /* ==================================================================
    Host runtime: C ABI (include/fd_ed25519_gpu.h)
    ================================================================== */
@@ -1069,9 +1089,13 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   hipEvent_t         done;
   int                state;    /* 0 filling, 1 in flight / draining */
   int                mode;     /* 0 desc (fdgpu_ed25519_submit), 1 raw (fdgpu_ed25519_submit_raw),
-                                  2 raw in place (fdgpu_ed25519_submit_raw_ref) */
-  unsigned char const * ref_base; /* mode 2: the caller's pinned region; payloads at [ref_lo, ref_hi) */
+                                  2 raw in place (fdgpu_ed25519_submit_raw_ref),
+                                  3 raw gathered by the GPU (fdgpu_ed25519_submit_raw_gather) */
+  unsigned char const * ref_base; /* mode 2, 3: the caller's pinned region; payloads at [ref_lo, ref_hi) */
   size_t             ref_lo, ref_hi;
+  unsigned char *    ref_dev;  /* mode 3: the device address of ref_base (the gather kernel writes the records back) */
+  struct fd_gather * h_gat;    /* mode 3: one gather record per transaction */
+  struct fd_gather * d_gat;
 };
 
 struct fdgpu_ed25519_ctx {
@@ -1280,8 +1304,9 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
     if( sl.h_tags    ) (void)hipHostFree( sl.h_tags );
     if( sl.h_img     ) (void)hipHostFree( sl.h_img );
     if( sl.h_fp      ) (void)hipHostFree( sl.h_fp );
+    if( sl.h_gat     ) (void)hipHostFree( sl.h_gat );
     (void)hipFree( sl.d_payload ); (void)hipFree( sl.d_desc ); (void)hipFree( sl.d_txn_out );
-    (void)hipFree( sl.d_img ); (void)hipFree( sl.d_fp );
+    (void)hipFree( sl.d_img ); (void)hipFree( sl.d_fp ); (void)hipFree( sl.d_gat );
     if( sl.done ) (void)hipEventDestroy( sl.done );
   }
   if( ctx->stream ) (void)hipStreamDestroy( ctx->stream );
@@ -1588,6 +1613,11 @@ static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
   hipStream_t st = ctx->stream;
   if( sl.mode==2 ) {   /* in place: one upload of the caller's region range, no host copy */
     HIPCHK( hipMemcpyAsync( sl.d_payload, sl.ref_base + sl.ref_lo, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+  } else if( sl.mode==3 ) {   /* gathered: the GPU reads each record from the caller's in region */
+    HIPCHK( hipMemcpyAsync( sl.d_gat, sl.h_gat, sl.txn_cnt * sizeof(fd_gather), hipMemcpyHostToDevice, st ), -2 );
+    hipLaunchKernelGGL( fd_gather_kernel, dim3( (unsigned)sl.txn_cnt ), dim3( 64 ), 0, st, sl.d_gat, sl.d_payload,
+                        sl.ref_dev + sl.ref_lo );
+    HIPCHK( hipGetLastError(), -2 );
   } else {
     memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
     HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
@@ -1672,6 +1702,8 @@ static int slot_raw_bufs( fdgpu_ed25519_ctx_t * ctx, fd_slot * sl ) {
   HIPCHK( hipHostMalloc( (void **)&sl->h_fp, ctx->max_txn * sizeof(unsigned short), hipHostMallocDefault ), -3 );
   HIPCHK( hipMalloc( (void **)&sl->d_img, ctx->max_txn * FDGPU_TXN_IMG_STRIDE ), -3 );
   HIPCHK( hipMalloc( (void **)&sl->d_fp, ctx->max_txn * sizeof(unsigned short) ), -3 );
+  HIPCHK( hipHostMalloc( (void **)&sl->h_gat, ctx->max_txn * sizeof(fd_gather), hipHostMallocDefault ), -3 );
+  HIPCHK( hipMalloc( (void **)&sl->d_gat, ctx->max_txn * sizeof(fd_gather) ), -3 );
   return 0;
 }
 
@@ -1721,14 +1753,96 @@ fdgpu_ed25519_submit_raw_ref( fdgpu_ed25519_ctx_t * ctx, unsigned char const * b
   return 0;
 }
 
+/* Host regions the GPU may read or write directly (fdgpu_host_alloc
+   allocations and fdgpu_host_register-ed ranges): host base -> device
+   address, for the gather path. */
+struct fd_region { unsigned char const * h; unsigned char * d; unsigned long sz; };
+static std::mutex g_reg_mu;
+static std::vector<fd_region> g_regions;
+
+static void region_add( void * h, void * d, unsigned long sz ) {
+  std::lock_guard<std::mutex> lk( g_reg_mu );
+  g_regions.push_back( fd_region{ (unsigned char const *)h, (unsigned char *)d, sz } );
+}
+static void region_del( void * h ) {
+  std::lock_guard<std::mutex> lk( g_reg_mu );
+  for( size_t i=0; i<g_regions.size(); i++ ) if( g_regions[i].h == (unsigned char const *)h ) { g_regions.erase( g_regions.begin() + (long)i ); return; }
+}
+/* device address of [p, p+sz) if it lies inside one registered region, else NULL */
+static unsigned char * region_dev( void const * p, unsigned long sz ) {
+  std::lock_guard<std::mutex> lk( g_reg_mu );
+  unsigned char const * q = (unsigned char const *)p;
+  for( fd_region const & r : g_regions )
+    if( q >= r.h && q + sz <= r.h + r.sz ) return r.d + ( q - r.h );
+  return NULL;
+}
+
 extern "C" void *
 fdgpu_host_alloc( unsigned long sz ) {
   void * p = NULL;
   if( hipHostMalloc( &p, sz, hipHostMallocDefault ) != hipSuccess ) { fd_err = "hipHostMalloc failed"; return NULL; }
+  void * d = NULL;
+  if( hipHostGetDevicePointer( &d, p, 0 ) == hipSuccess ) region_add( p, d, sz );
   return p;
 }
 
-extern "C" void fdgpu_host_free( void * p ) { if( p ) hipHostFree( p ); }
+extern "C" void fdgpu_host_free( void * p ) { if( p ) { region_del( p ); hipHostFree( p ); } }
+
+extern "C" int
+fdgpu_host_register( void * p, unsigned long sz ) {
+  if( !p || !sz ) { fd_err = "fdgpu_host_register: empty range"; return -1; }
+  HIPCHK( hipHostRegister( p, sz, hipHostRegisterMapped ), -2 );
+  void * d = NULL;
+  hipError_t e = hipHostGetDevicePointer( &d, p, 0 );
+  if( e != hipSuccess ) { set_err( "hipHostGetDevicePointer", e ); (void)hipHostUnregister( p ); return -2; }
+  region_add( p, d, sz );
+  return 0;
+}
+
+extern "C" void
+fdgpu_host_unregister( void * p ) { if( p ) { region_del( p ); (void)hipHostUnregister( p ); } }
+
+/* Gathered raw submission: the record (copy_sz bytes at src, the payload
+   at src + payload_off) stays where the caller's producer wrote it, in a
+   registered host region; the batch's gather kernel copies it into the
+   device arena and into dst, the record's place in the caller's pinned
+   out region dst_base.  Records of one batch lie at increasing dst
+   addresses (a lower one starts a new batch), chunk aligned. */
+extern "C" int
+fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char * dst_base,
+                                 unsigned char * dst, unsigned short copy_sz, unsigned short payload_off,
+                                 unsigned short payload_sz, unsigned long tag ) {
+  if( (unsigned)payload_off + payload_sz > copy_sz || ( (uintptr_t)src & 15 ) || ( (uintptr_t)( dst - dst_base ) & 15 ) ) {
+    fd_err = "fdgpu_ed25519_submit_raw_gather: bad record"; return -1;
+  }
+  unsigned long csz = ( (unsigned long)copy_sz + 15UL ) & ~15UL;
+  unsigned char * dsrc = region_dev( src, csz );
+  if( !dsrc ) { fd_err = "fdgpu_ed25519_submit_raw_gather: src not in a registered region"; return -3; }
+  unsigned b0 = payload_sz ? src[ payload_off ] : 0u;
+  unsigned lanes = ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u;
+  size_t off = (size_t)( dst - dst_base );
+  int rc; fd_slot * sl = slot_for( ctx, 0UL, lanes, 3, &rc );
+  if( !sl ) return rc;
+  if( sl->txn_cnt && ( sl->ref_base != dst_base || off < sl->ref_hi || off + csz - sl->ref_lo + 8UL > ctx->max_payload ) ) {
+    if( ( rc = fdgpu_ed25519_flush( ctx ) ) ) return rc;
+    if( !( sl = slot_for( ctx, 0UL, lanes, 3, &rc ) ) ) return rc;
+  }
+  if( slot_raw_bufs( ctx, sl ) ) return -3;
+  if( !sl->txn_cnt ) {
+    unsigned char * d = region_dev( dst_base, 1UL );
+    if( !d ) { fd_err = "fdgpu_ed25519_submit_raw_gather: dst_base not from fdgpu_host_alloc"; return -3; }
+    sl->ref_base = dst_base; sl->ref_dev = d; sl->ref_lo = off;
+  }
+  fdgpu_txn_raw_t & r = ((fdgpu_txn_raw_t *)sl->h_desc)[ sl->txn_cnt ];
+  r.payload_off = (unsigned)( off - sl->ref_lo + payload_off ); r.sig_base = (unsigned)sl->sig_cnt;
+  r.payload_sz = payload_sz; r.sig_lanes = (unsigned char)lanes;
+  fd_gather & g = sl->h_gat[ sl->txn_cnt ];
+  g.src = (unsigned long)dsrc; g.dst = (unsigned)( off - sl->ref_lo ); g.sz = (unsigned)csz;
+  sl->h_tags[ sl->txn_cnt ] = tag;
+  sl->txn_cnt++; sl->sig_cnt += lanes;
+  sl->ref_hi = off + csz; sl->payload_used = sl->ref_hi - sl->ref_lo;
+  return 0;
+}
 
 /* Drain completed slots in submission order, at most max results. */
 static unsigned long

@@ -240,6 +240,11 @@ struct fdgpu_vtile {
   int                   bundle_failed;
   ulong                 bundle_id;
   ulong                 metrics[5];
+  /* zero-copy intake (fdgpu_vtile_set_in_link): frags stay in the in
+     dcache, the GPU gathers them; in_mc (optional) for the overrun check */
+  int                   zc;
+  fdgpu_mcache_t const * in_mc;
+  ulong                 overruns;
   /* poll scratch */
   ulong                 batch;
   ulong *               p_tags;
@@ -290,6 +295,19 @@ uchar * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt ) { return vt->dcache; }
 ulong   fdgpu_vtile_pending( fdgpu_vtile_t const * vt ) { return vt->pend_tail - vt->pend_head; }
 void    fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, ulong out[ 5 ] ) { memcpy( out, vt->metrics, sizeof(vt->metrics) ); }
 int     fdgpu_vtile_flush( fdgpu_vtile_t * vt ) { vt_fence(); return fdgpu_ed25519_flush( vt->ctx ); }
+ulong   fdgpu_vtile_overruns( fdgpu_vtile_t const * vt ) { return vt->overruns; }
+
+int
+fdgpu_vtile_set_in_link( fdgpu_vtile_t * vt, fdgpu_mcache_t const * in_mc ) {
+  if( vt->pend_tail != vt->pend_head ) return -1;       /* switch only while idle */
+  vt->zc = 1; vt->in_mc = in_mc;
+  return 0;
+}
+
+ulong
+fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt ) {
+  return vt->pend_head < vt->pend_tail ? vt->pend[ vt->pend_head % vt->pend_cap ].seq : ~0UL;
+}
 
 int
 fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
@@ -313,8 +331,15 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   vt_fence();
   if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_ed25519_flush( vt->ctx ); return -2; }
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
-  vt_copy( dst, (uchar const *)frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
-  int rc = fdgpu_ed25519_submit_raw_ref( vt->ctx, vt->dcache, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
+  int rc;
+  if( vt->zc ) {   /* the GPU copies the frag into dst itself (no host copy) */
+    rc = fdgpu_ed25519_submit_raw_gather( vt->ctx, (uchar const *)frag, vt->dcache, dst,
+                                          (unsigned short)( FDGPU_TXNM_HDR_SZ + in->payload_sz ),
+                                          (unsigned short)FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
+  } else {
+    vt_copy( dst, (uchar const *)frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
+    rc = fdgpu_ed25519_submit_raw_ref( vt->ctx, vt->dcache, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
+  }
   if( rc ) return rc;
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
   p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk;
@@ -329,8 +354,16 @@ static int
 vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, unsigned fp, fdgpu_vtile_done_t * d ) {
   fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( vt->dcache + p->chunk * FDGPU_CHUNK_SZ );
   uchar * payload = (uchar *)txnm + FDGPU_TXNM_HDR_SZ;
-  txnm->txn_t_sz = (unsigned short)fp;
   d->seq = p->seq; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
+  if( vt->zc && vt->in_mc ) {
+    /* zero-copy: the GPU read the frag at batch launch, after during_frag.
+       If the producer has since reused the frag's mcache line, its dcache
+       bytes may have been overwritten before that read: drop it, as the
+       stem loop drops a frag overrun during its copy. */
+    fdgpu_frag_meta_t m;
+    if( fdgpu_mcache_poll( vt->in_mc, p->seq, &m ) != 0 ) { vt->overruns++; return FDGPU_VTILE_OVERRUN; }
+  }
+  txnm->txn_t_sz = (unsigned short)fp;
   int is_bundle = txnm->bundle_id != 0UL;
   if( is_bundle && txnm->bundle_id != vt->bundle_id ) { vt->bundle_failed = 0; vt->bundle_id = txnm->bundle_id; }
   if( is_bundle && vt->bundle_failed ) { vt->metrics[3]++; return FDGPU_VTILE_BUNDLE_PEER_FAIL; }
@@ -405,6 +438,7 @@ typedef struct {
   ulong                  metrics[5];
   pthread_mutex_t        mu;
   int                    device; ulong batch_txn, max_inflight;
+  int                    zc;          /* zero-copy intake: tiles leave frags in the in dcache */
 } sb_t;
 
 /* The producer stands in for the QUIC tiles: every distinct payload is
@@ -445,6 +479,16 @@ static void * sb_producer( void * _s ) {
 }
 
 typedef struct { sb_t * s; int idx; } sb_tile_arg_t;
+
+/* credit a tile returns to the producer: every seq below it may be
+   overwritten.  With zero-copy intake a frag's bytes must survive until
+   the GPU has read them, so the credit stops at the oldest frag still
+   pending in the tile. */
+static void sb_credit( sb_t * s, int idx, fdgpu_vtile_t const * vt, ulong seq ) {
+  ulong c = seq;
+  if( s->zc ) { ulong o = fdgpu_vtile_oldest_pending_seq( vt ); if( o < c ) c = o; }
+  atomic_store_explicit( &s->fseq[idx].v, c, memory_order_release );
+}
 
 /* Latency histogram (per tile, merged at the end): log-linear buckets,
    64 per octave (< 1.6 % wide), exact below 64 ns. */
@@ -493,6 +537,7 @@ static void * sb_tile( void * _a ) {
   fdgpu_vtile_t * vt = fdgpu_vtile_new( s->device, s->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                         ( 6UL*s->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
   if( !vt ) { atomic_store( &s->fail, 1 ); return NULL; }
+  if( s->zc && fdgpu_vtile_set_in_link( vt, s->mc ) ) { atomic_store( &s->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL; }
   atomic_fetch_add( &s->ready, 1 );              /* the producer starts once every tile has its GPU context */
   ulong dcap = 4096UL;
   fdgpu_vtile_done_t * done = (fdgpu_vtile_done_t *)malloc( dcap * sizeof(fdgpu_vtile_done_t) );
@@ -534,7 +579,7 @@ static void * sb_tile( void * _a ) {
         }
       }
       seq++;
-      if( !(seq & 63UL) || seq==s->n_frags ) atomic_store_explicit( &s->fseq[idx].v, seq, memory_order_release );   /* batched credit return */
+      if( !(seq & 63UL) || seq==s->n_frags ) sb_credit( s, idx, vt, seq );   /* batched credit return */
     }
     ulong t1 = now_ns();
     ns_in += t1 - t0;
@@ -542,6 +587,7 @@ static void * sb_tile( void * _a ) {
     if( drain ) {
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
       sb_account( s, vt, done, n, &sigs, lh, &lmax ); got += n;
+      if( s->zc ) sb_credit( s, idx, vt, seq );
       ns_after += now_ns() - t1;
       continue;
     }
@@ -553,6 +599,7 @@ static void * sb_tile( void * _a ) {
       ulong t2 = now_ns();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
       sb_account( s, vt, done, n, &sigs, lh, &lmax ); got += n;
+      if( s->zc && n ) sb_credit( s, idx, vt, seq );
       ns_hk += t2 - t1; ns_after += now_ns() - t2;
     }
   }
@@ -560,6 +607,7 @@ static void * sb_tile( void * _a ) {
   atomic_fetch_add( &s->ns[0], ns_in );     atomic_fetch_add( &s->ns[1], ns_after );
   atomic_fetch_add( &s->ns[2], ns_hk );     atomic_fetch_add( &s->ns[3], t_end - t_begin );
   ulong m5[5]; fdgpu_vtile_metrics( vt, m5 );
+  atomic_fetch_add( &s->overruns, fdgpu_vtile_overruns( vt ) );
   pthread_mutex_lock( &s->mu );
   for( int i=0; i<5; i++ ) s->metrics[i] += m5[i];
   for( ulong i=0UL; i<LH_N; i++ ) s->lh[i] += lh[i];
@@ -574,7 +622,7 @@ static void * sb_tile( void * _a ) {
 int
 fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, unsigned short const * sz, ulong n_payload,
                     ulong n_frags, int tiles, ulong batch_txn, ulong max_inflight, ulong mcache_depth, double rate_fps,
-                    fdgpu_stream_stats_t * st ) {
+                    int zero_copy, fdgpu_stream_stats_t * st ) {
   if( tiles < 1 || tiles > 64 || !n_frags || !n_payload || !batch_txn || mcache_depth < 64 ) return -1;
   sb_t * s = (sb_t *)calloc( 1, sizeof(sb_t) );
   s->depth = pow2_up( mcache_depth );
@@ -598,6 +646,11 @@ fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, uns
   s->lh = (ulong *)calloc( LH_N, sizeof(ulong) );
   s->payload = payload; s->off = off; s->sz = sz; s->n_payload = n_payload; s->rate_fps = rate_fps;
   s->device = device; s->batch_txn = batch_txn; s->max_inflight = max_inflight ? max_inflight : 2UL;
+  s->zc = zero_copy;
+  if( zero_copy && fdgpu_host_register( s->in_dcache, in_bytes + 128UL ) ) {
+    fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( s->frag_chunk ); free( (void *)s->fseq ); free( s->lh );
+    free( s ); return -3;
+  }
   pthread_mutex_init( &s->mu, NULL );
   pthread_t prod, th[64]; sb_tile_arg_t args[64];
   for( int t=0; t<tiles; t++ ) { args[t].s = s; args[t].idx = t; pthread_create( &th[t], NULL, sb_tile, &args[t] ); }
@@ -622,6 +675,7 @@ fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, uns
     st->overruns = atomic_load( &s->overruns );
     for( int i=0; i<4; i++ ) st->tile_ns[i] = atomic_load( &s->ns[i] );
   }
+  if( zero_copy ) fdgpu_host_unregister( s->in_dcache );
   fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( s->frag_chunk ); free( (void *)s->fseq ); free( s->lh );
   pthread_mutex_destroy( &s->mu );
   free( s );

@@ -44,7 +44,8 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_verify_txns_host", "fdgpu_txn_parse_device", "fdgpu_ed25519_verify_raw_device",
            "fdgpu_ed25519_verify_raw_host", "fdgpu_ed25519_submit", "fdgpu_ed25519_flush",
            "fdgpu_ed25519_poll", "fdgpu_ed25519_submit_raw", "fdgpu_ed25519_poll_raw", "fdgpu_ed25519_submit_raw_ref",
-           "fdgpu_host_alloc", "fdgpu_host_free",
+           "fdgpu_host_alloc", "fdgpu_host_free", "fdgpu_host_register", "fdgpu_host_unregister",
+           "fdgpu_ed25519_submit_raw_gather",
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_last_error")
 
@@ -187,6 +188,17 @@ def raw_records(payload: np.ndarray, off: np.ndarray, sz: np.ndarray):
     raw["sig_lanes"] = lanes
     raw["sig_base"] = np.concatenate([[0], np.cumsum(lanes)[:-1]]).astype(np.uint32) if len(off) else []
     return raw, int(lanes.sum())
+
+
+def host_register(buf: np.ndarray) -> None:
+    """fdgpu_host_register: page-lock and map a host array for the GPU (zero-copy intake); keep it alive."""
+    L = load_library()
+    if L.fdgpu_host_register(ctypes.c_void_p(buf.ctypes.data), ctypes.c_ulong(buf.nbytes)):
+        raise RuntimeError("fdgpu_host_register failed: " + last_error())
+
+
+def host_unregister(buf: np.ndarray) -> None:
+    load_library().fdgpu_host_unregister(ctypes.c_void_p(buf.ctypes.data))
 
 
 def fd_ed25519_strerror(err: int) -> str:

@@ -14,13 +14,14 @@ from .engine import PKG_DIR, load_library as load_engine
 LIB_PATH = os.path.join(PKG_DIR, "libfdgpu_vtile.so")
 TXNM_HDR_SZ = 80
 CHUNK_SZ = 64
-PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL = range(5)
+PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL, OVERRUN = range(6)
 
 EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
            "fdgpu_mcache_new", "fdgpu_mcache_delete", "fdgpu_mcache_publish", "fdgpu_mcache_poll",
            "fdgpu_dcache_compact_next", "fdgpu_vtile_new", "fdgpu_vtile_delete", "fdgpu_vtile_out_dcache",
            "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_housekeep", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
-           "fdgpu_vtile_metrics", "fdgpu_stream_bench")
+           "fdgpu_vtile_metrics", "fdgpu_vtile_set_in_link", "fdgpu_vtile_oldest_pending_seq", "fdgpu_vtile_overruns",
+           "fdgpu_stream_bench")
 
 TXNM_DTYPE = np.dtype([("reference_slot", "<u8"), ("payload_sz", "<u2"), ("txn_t_sz", "<u2"), ("source_ipv4", "<u4"),
                        ("source_tpu", "u1"), ("_pad0", "u1", (7,)), ("bundle_id", "<u8"), ("bundle_txn_cnt", "<u8"),
@@ -83,8 +84,13 @@ def load():
         L.fdgpu_vtile_pending.restype = ul
         L.fdgpu_vtile_pending.argtypes = [vp]
         L.fdgpu_vtile_metrics.argtypes = [vp, ctypes.POINTER(ctypes.c_ulong)]
+        L.fdgpu_vtile_set_in_link.argtypes = [vp, vp]
+        L.fdgpu_vtile_oldest_pending_seq.restype = ul
+        L.fdgpu_vtile_oldest_pending_seq.argtypes = [vp]
+        L.fdgpu_vtile_overruns.restype = ul
+        L.fdgpu_vtile_overruns.argtypes = [vp]
         L.fdgpu_stream_bench.argtypes = [ctypes.c_int, vp, vp, vp, ul, ul, ctypes.c_int, ul, ul, ul, ctypes.c_double,
-                                         ctypes.POINTER(StreamStats)]
+                                         ctypes.c_int, ctypes.POINTER(StreamStats)]
         _lib = L
     return _lib
 
@@ -135,6 +141,17 @@ class VTile:
         b = np.frombuffer(frag, np.uint8)
         return self.L.fdgpu_vtile_during_frag(self.p, b.ctypes.data, len(frag), seq, tsorig)
 
+    def during_frag_at(self, addr: int, sz: int, seq: int, tsorig: int = 0) -> int:
+        """during_frag on a frag already in memory at addr (zero-copy intake: inside a registered in dcache)."""
+        return self.L.fdgpu_vtile_during_frag(self.p, addr, sz, seq, tsorig)
+
+    def set_in_link(self, mcache=None) -> int:
+        """Switch to zero-copy intake (fdgpu_vtile_set_in_link); mcache: an in-link mcache handle or None."""
+        return int(self.L.fdgpu_vtile_set_in_link(self.p, mcache))
+
+    def overruns(self) -> int:
+        return int(self.L.fdgpu_vtile_overruns(self.p))
+
     def flush(self):
         return self.L.fdgpu_vtile_flush(self.p)
 
@@ -168,14 +185,14 @@ class VTile:
 
 def stream_bench(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,
                  batch_txn: int = 4096, max_inflight: int = 2, mcache_depth: int = 1 << 16, rate_fps: float = 0.0,
-                 device: int = 0) -> dict:
+                 device: int = 0, zero_copy: bool = False) -> dict:
     L = load()
     payload = np.ascontiguousarray(payload, np.uint8)
     off = np.ascontiguousarray(off, np.uint32)
     sz = np.ascontiguousarray(sz, np.uint16)
     st = StreamStats()
     rc = L.fdgpu_stream_bench(device, payload.ctypes.data, off.ctypes.data, sz.ctypes.data, len(off), n_frags, tiles,
-                              batch_txn, max_inflight, mcache_depth, rate_fps, ctypes.byref(st))
+                              batch_txn, max_inflight, mcache_depth, rate_fps, 1 if zero_copy else 0, ctypes.byref(st))
     if rc:
         raise RuntimeError(f"fdgpu_stream_bench: {rc} " + load_engine().fdgpu_last_error().decode())
     return {"seconds": st.seconds, "frags": st.frags, "sigs": st.sigs, "published": st.published,

@@ -341,6 +341,36 @@ fdgpu_ed25519_submit_raw_ref( fdgpu_ed25519_ctx_t * ctx,
 void * fdgpu_host_alloc( unsigned long sz );
 void   fdgpu_host_free ( void * p );
 
+/* Page-lock an existing host range and map it for the GPU (a tile's in
+   dcache: the workspace the producer writes frags into), so that
+   fdgpu_ed25519_submit_raw_gather can read records there.  0 on
+   success. */
+int    fdgpu_host_register  ( void * p, unsigned long sz );
+void   fdgpu_host_unregister( void * p );
+
+/* Gathered form (no host copy at all; the zero-copy staging of SURVEY.md
+   §8f rank 2): the record -- copy_sz bytes at src, 16-B aligned, inside
+   a range given to fdgpu_host_register or fdgpu_host_alloc, with the
+   transaction payload at src + payload_off -- stays where the producer
+   wrote it.  The batch's first kernel reads it over PCIe, into the
+   device arena and into dst: the record's place in the caller's pinned
+   out region dst_base (from fdgpu_host_alloc).  So after poll_raw
+   returns its verdict the out region holds the record, as if the host
+   had copied it (the reference's during_frag copy, fd_verify_tile.c:
+   77-79).  Records of one batch lie at increasing dst addresses of one
+   region (a lower one starts a new batch), 16-B aligned, with room for
+   copy_sz rounded up to 16 at dst; src must stay valid until the batch
+   is launched (the caller checks for overruns after the verdict). */
+int
+fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx,
+                                 unsigned char const * src,
+                                 unsigned char *       dst_base,
+                                 unsigned char *       dst,
+                                 unsigned short        copy_sz,
+                                 unsigned short        payload_off,
+                                 unsigned short        payload_sz,
+                                 unsigned long         tag );
+
 unsigned long
 fdgpu_ed25519_poll_raw( fdgpu_ed25519_ctx_t * ctx,
                         unsigned long *       out_tags,

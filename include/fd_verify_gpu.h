@@ -106,6 +106,7 @@ unsigned long    fdgpu_dcache_compact_next( unsigned long chunk, unsigned long s
 #define FDGPU_VTILE_VERIFY_FAIL      (2)
 #define FDGPU_VTILE_DEDUP_FAIL       (3)
 #define FDGPU_VTILE_BUNDLE_PEER_FAIL (4)
+#define FDGPU_VTILE_OVERRUN          (5)   /* zero-copy intake: the frag was overwritten before the GPU read it */
 
 typedef struct fdgpu_vtile_done {
   unsigned long seq;      /* as given to during_frag */
@@ -134,6 +135,21 @@ unsigned char * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt );   /* chunk c is at
    and retry), <= -3 on error. */
 int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, unsigned long sz, unsigned long seq,
                                          unsigned long tsorig );
+/* Zero-copy intake: from now on during_frag leaves the frag where it
+   is -- frag must then lie in a range registered with
+   fdgpu_host_register (the in dcache), 16-B aligned -- and the GPU
+   copies it into the out dcache record itself
+   (fdgpu_ed25519_submit_raw_gather).  in_mc (may be NULL): the in link's
+   mcache; after the verdict, a frag whose mcache line the producer has
+   reused is reported FDGPU_VTILE_OVERRUN instead of published.  A
+   reliable producer must not reuse a frag's dcache bytes before
+   fdgpu_vtile_oldest_pending_seq has passed it (credits).  Call while no
+   frag is pending; 0 on success. */
+int             fdgpu_vtile_set_in_link( fdgpu_vtile_t * vt, fdgpu_mcache_t const * in_mc );
+/* seq of the oldest frag not yet returned by after_frags (~0UL if none) */
+unsigned long   fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt );
+/* frags dropped as FDGPU_VTILE_OVERRUN */
+unsigned long   fdgpu_vtile_overruns( fdgpu_vtile_t const * vt );
 /* launch the partially filled batch (call when the input is idle) */
 int             fdgpu_vtile_flush( fdgpu_vtile_t * vt );
 /* adaptive batching, for the tile's housekeeping / before_credit hook:
@@ -171,11 +187,15 @@ typedef struct fdgpu_stream_stats {
    tiles (one host thread each, before_frag's seq % tiles round robin,
    each with its own GPU context on `device`, batches of at most
    batch_txn launched by fdgpu_vtile_housekeep( max_inflight )) consume
-   it.  Returns 0 and fills *st. */
+   it.  zero_copy: the in dcache is registered with the GPU and the tiles
+   take frags by fdgpu_vtile_set_in_link (no host copy); each tile's
+   credit then stops at its oldest pending frag.  Returns 0 and fills
+   *st. */
 int             fdgpu_stream_bench( int device, unsigned char const * payload, unsigned int const * off,
                                     unsigned short const * sz, unsigned long n_payload, unsigned long n_frags,
                                     int tiles, unsigned long batch_txn, unsigned long max_inflight,
-                                    unsigned long mcache_depth, double rate_fps, fdgpu_stream_stats_t * st );
+                                    unsigned long mcache_depth, double rate_fps, int zero_copy,
+                                    fdgpu_stream_stats_t * st );
 
 #ifdef __cplusplus
 }

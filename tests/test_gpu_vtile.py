@@ -87,14 +87,35 @@ def model(oracle, frags, seed, depth):
     return res, metrics, recs
 
 
+def in_dcache(frag_list):
+    """The frags as fd_txn_m_t records in one 64-B-chunked in dcache (numpy, page-locked by the caller)."""
+    offs, pos = [], 0
+    for fb in frag_list:
+        offs.append(pos)
+        pos += (len(fb) + 63) & ~63
+    buf = np.zeros(pos + 4096 + 128, np.uint8)
+    base = (-buf.ctypes.data) % 64                       # chunk-align the first record
+    for fb, o in zip(frag_list, offs):
+        buf[base + o: base + o + len(fb)] = np.frombuffer(fb, np.uint8)
+    return buf, [base + o for o in offs]
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
 @pytest.mark.parametrize("batch,depth", [(64, 32), (512, 1 << 12)])
-def test_vtile_vs_model(oracle, batch, depth):
+def test_vtile_vs_model(oracle, batch, depth, zero_copy):
+    """zero_copy: the frags stay in a registered in dcache and the GPU gathers them into the out
+    dcache records (fdgpu_vtile_set_in_link); outcomes and published records must not change."""
     pytest.importorskip("xxhash")
-    from firedancer_amd import vtile
+    from firedancer_amd import engine, vtile
     frags = make_stream()
     seed = 0x1234abcd
     want_res, want_m, want_recs = model(oracle, frags, seed, depth)
     vt = vtile.VTile(device=0, batch_txn=batch, tcache_depth=depth, seed=seed)
+    if zero_copy:
+        fbs = [vtile.frag_bytes(p, b) for p, b in frags]
+        buf, offs = in_dcache(fbs)
+        engine.host_register(buf)
+        assert vt.set_in_link(None) == 0
     got, bad = [], []
 
     def drain(blocking):
@@ -111,7 +132,7 @@ def test_vtile_vs_model(oracle, batch, depth):
     for seq, (p, b) in enumerate(frags):
         fb = vtile.frag_bytes(p, b)
         while True:
-            rc = vt.during_frag(fb, seq)
+            rc = vt.during_frag_at(buf.ctypes.data + offs[seq], len(fb), seq) if zero_copy else vt.during_frag(fb, seq)
             if rc != -2:
                 break
             got += drain(True)
@@ -127,6 +148,39 @@ def test_vtile_vs_model(oracle, batch, depth):
     assert bad == []
     assert sum(want_m[:4]) > 100 and want_m[2] > 10 and want_m[3] > 0
     vt.close()
+    if zero_copy:
+        engine.host_unregister(buf)
+
+
+def test_vtile_zero_copy_overrun():
+    """Zero-copy intake: a frag whose in-link mcache line the producer reuses before the verdict is
+    reported OVERRUN (its bytes may have changed before the GPU read them); the others verify."""
+    from firedancer_amd import engine, synth, vtile
+    L = vtile.load()
+    depth, n = 64, 64
+    payload, desc, _, _ = synth.make_batch(n, synth.LARGE_NOOP, seed=21)
+    fbs = [vtile.frag_bytes(payload[d["payload_off"]: d["payload_off"] + d["payload_sz"]].tobytes()) for d in desc]
+    buf, offs = in_dcache(fbs)
+    engine.host_register(buf)
+    mc = L.fdgpu_mcache_new(depth, 0)
+    for seq in range(n):
+        L.fdgpu_mcache_publish(mc, seq, 0, seq, len(fbs[seq]), 0, 0)
+    vt = vtile.VTile(device=0, batch_txn=256, tcache_depth=1024)
+    assert vt.set_in_link(mc) == 0
+    for seq in range(n):
+        assert vt.during_frag_at(buf.ctypes.data + offs[seq], len(fbs[seq]), seq) == 0
+    for seq in range(n, n + 24):                       # the producer laps lines 0..23 before the verdicts
+        L.fdgpu_mcache_publish(mc, seq, 0, 0, 0, 0, 0)
+    vt.flush()
+    got = []
+    while vt.pending():
+        got += vt.after_frags(blocking=True)
+    assert [g[0] for g in got] == list(range(n))
+    assert [g[1] for g in got] == [vtile.OVERRUN] * 24 + [vtile.PUBLISH] * (n - 24)
+    assert vt.overruns() == 24 and vt.metrics()[4] == n - 24
+    vt.close()
+    L.fdgpu_mcache_delete(mc)
+    engine.host_unregister(buf)
 
 
 def _run_frags(vt, frags, seq0=0):
@@ -168,12 +222,14 @@ def test_reference_tile_scenarios():
     assert _run_frags(tile(), [(V1, 0), (I64, 0)]) == [P, F]
 
 
-def test_stream_bench_small():
-    """The configs[4] harness end to end at a small size: every frag gets a verdict."""
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_stream_bench_small(zero_copy):
+    """The configs[4] harness end to end at a small size: every frag gets a verdict (with and
+    without zero-copy intake)."""
     from firedancer_amd import synth, vtile
     payload, desc, _, _ = synth.make_batch(4096, synth.LARGE_NOOP, seed=9)
     st = vtile.stream_bench(payload, desc["payload_off"], desc["payload_sz"], n_frags=50000, tiles=2, batch_txn=1024,
-                            mcache_depth=8192)
+                            mcache_depth=8192, zero_copy=zero_copy)
     assert st["frags"] == 50000 and st["overruns"] == 0
     m = st["metrics"]
     # 4096 distinct payloads cycled: the first copy of each publishes per tile, repeats are HA duplicates

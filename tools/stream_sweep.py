@@ -19,7 +19,9 @@ for tiles in [int(x) for x in os.environ.get("TILES", "1,2,4,8").split(",")]:
         for rate in [float(x) for x in os.environ.get("RATE", "0").split(",")]:
           for infl in [int(x) for x in os.environ.get("INFL", "2").split(",")]:
            for nf in [int(x) for x in os.environ.get("NF", "1000000").split(",")]:
-            st = vtile.stream_bench(payload, desc["payload_off"], desc["payload_sz"], n_frags=nf,
-                                    tiles=tiles, batch_txn=batch, max_inflight=infl, mcache_depth=1 << 16, rate_fps=rate)
-            st.update(tiles=tiles, batch=batch, rate=rate, inflight=infl)
-            print(json.dumps(st), flush=True)
+            for zc in [int(x) for x in os.environ.get("ZC", "0").split(",")]:
+             st = vtile.stream_bench(payload, desc["payload_off"], desc["payload_sz"], n_frags=nf,
+                                     tiles=tiles, batch_txn=batch, max_inflight=infl,
+                                     mcache_depth=int(os.environ.get("DEPTH", 1 << 16)), rate_fps=rate, zero_copy=bool(zc))
+             st.update(tiles=tiles, batch=batch, rate=rate, inflight=infl, zero_copy=zc)
+             print(json.dumps(st), flush=True)
