@@ -96,6 +96,9 @@ def main():
     ap.add_argument("--stream-seconds", type=float, default=10.0,
                     help="sustained length of each stream run (max rate, then paced)")
     ap.add_argument("--stream-tiles", type=int, default=6)
+    ap.add_argument("--stream-copy", action="store_true",
+                    help="stream tiles copy each frag into the out dcache on the host (the reference tile's "
+                         "during_frag) instead of the zero-copy intake (GPU gathers from the registered in dcache)")
     ap.add_argument("--stream-batch", type=int, default=8192)
     ap.add_argument("--stream-rate", type=float, default=2e6, help="paced rate (frags/s) of the latency run")
     ap.add_argument("--stream-lat-tiles", type=int, default=2,
@@ -213,20 +216,22 @@ def main():
     if args.stream_frags != 0:
         from firedancer_amd import vtile
         off, psz = desc["payload_off"], desc["payload_sz"]
+        zc = not args.stream_copy
         if args.stream_frags > 0:
             n_max = n_pace = args.stream_frags
         else:                                   # sustained runs of --stream-seconds each
             barrier()
             cal = vtile.stream_bench(payload, off, psz, n_frags=2_000_000, tiles=args.stream_tiles,
-                                     batch_txn=args.stream_batch, max_inflight=2)
+                                     batch_txn=args.stream_batch, max_inflight=2, mcache_depth=1 << 18, zero_copy=zc)
             n_max = int(1.2 * cal["frags_per_s"] * args.stream_seconds)   # short runs under-read the rate
             n_pace = int(args.stream_rate * args.stream_seconds)
         barrier()
         smax = vtile.stream_bench(payload, off, psz, n_frags=n_max, tiles=args.stream_tiles,
-                                  batch_txn=args.stream_batch, max_inflight=2)
+                                  batch_txn=args.stream_batch, max_inflight=2, mcache_depth=1 << 18, zero_copy=zc)
         barrier()
         slat = vtile.stream_bench(payload, off, psz, n_frags=n_pace, tiles=args.stream_lat_tiles,
-                                  batch_txn=args.stream_batch, max_inflight=2, rate_fps=args.stream_rate)
+                                  batch_txn=args.stream_batch, max_inflight=2, rate_fps=args.stream_rate,
+                                  mcache_depth=1 << 18, zero_copy=zc)
         ok_s = (smax["metrics"][:4] == [0, 0, 0, 0] and smax["published"] == n_max
                 and slat["metrics"][:4] == [0, 0, 0, 0] and slat["published"] == n_pace)
         sig_tot, t_max, _ = shard.reduce_sum_max(dist if world > 1 else None, smax["sigs"], smax["seconds"], "cuda")
@@ -234,6 +239,8 @@ def main():
                               "(device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> out dcache",
                   "sigs_per_s": sig_tot / t_max, "per_gpu_sigs_per_s": smax["sigs_per_s"], "n_gpus": world,
                   "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch,
+                  "intake": "zero-copy (GPU gathers frags from the registered in dcache)" if zc
+                            else "host copy into the out dcache (reference during_frag)",
                   "max_rate": {"frags": n_max, "seconds": smax["seconds"], "p50_us": smax["lat_p50_us"],
                                "p99_us": smax["lat_p99_us"], "tile_host_ns_per_frag":
                                    [round(x / max(n_max, 1), 1) for x in smax["tile_ns"]]},

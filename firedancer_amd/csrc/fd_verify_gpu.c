@@ -261,6 +261,13 @@ fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ul
   /* staging arena of a batch = its range of the out dcache (in-place submits): up to
      batch_txn records of at most VT_RESERVE_MAX bytes (rounded to chunk pairs) */
   vt->ctx = fdgpu_ed25519_ctx_new( device, batch_txn, 16UL*batch_txn, batch_txn*2304UL + 1024UL, semantics );
+  /* adaptive batching launches a partial batch when the GPU has room (low
+     load: the latency path) and a full one when frags back up (high load:
+     the throughput path, whose per-signature work is 0.5x the 4-lane DSM's) */
+  if( vt->ctx ) {
+    ulong sm = fdgpu_ed25519_set_small_batch_max( vt->ctx, 0UL );
+    fdgpu_ed25519_set_small_batch_max( vt->ctx, sm < batch_txn/2UL ? sm : batch_txn/2UL );
+  }
   vt->tcache = fdgpu_tcache_new( tcache_depth );
   ulong nchunk = ( out_dcache_bytes / FDGPU_CHUNK_SZ ) & ~1UL;
   vt->dcache = (uchar *)fdgpu_host_alloc( nchunk * FDGPU_CHUNK_SZ );   /* pinned: batches upload from it in place */
