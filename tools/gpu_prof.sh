@@ -3,7 +3,7 @@
 # HBM-resident bench (no stream leg, no CPU baseline).
 # usage: gpurun --timeout 900 -- 'bash tools/gpu_prof.sh <tag>'
 tag="${1:-run}"
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-batch 0 --stream-frags 0"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
 P="timeout -s KILL 90 rocprofv3 --kernel-include-regex fd_ -f csv"
 bash "$(dirname "$0")/gpu_job.sh" \
   "stats:180:rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_${tag}/stats -o run -- $B" \

@@ -3,7 +3,7 @@
 # then separate PMC passes on the bench (one counter group per pass).
 # usage (from the container): gpurun --timeout 1100 -- 'bash tools/gpu_round.sh [tag]'
 tag="${1:-run}"
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-batch 0 --stream-frags 0"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
 P="timeout -s KILL 90 rocprofv3 --kernel-include-regex fd_ -f csv"
 exec_specs=(
   "tests:420:python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread"
