@@ -9,7 +9,7 @@ exec_specs=(
   "tests:420:python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread"
   "smoke:120:python -u -c 'import __graft_entry__ as g; g.smoke()'"
   "bench:300:python -u bench.py > gpurun_out/bench_${tag}.json"
-  "stats:180:rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_${tag}/stats -o run -- $B"
+  "stats:180:mkdir -p gpurun_out/prof_${tag} && rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof_${tag}/stats -o run -- $B > gpurun_out/prof_${tag}/bench_under_rocprof.log 2>&1"
   "pmc_fetch:120:$P --pmc FETCH_SIZE -d gpurun_out/prof_${tag}/fetch -o run -- $B"
   "pmc_write:120:$P --pmc WRITE_SIZE -d gpurun_out/prof_${tag}/write -o run -- $B"
   "pmc_sq:120:$P --pmc SQ_INSTS_VALU SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE -d gpurun_out/prof_${tag}/sq -o run -- $B"

@@ -45,6 +45,22 @@ json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1, sort_
 stats = os.path.join(src, "stats", "run_kernel_stats.csv")
 if os.path.exists(stats):
     shutil.copy(stats, os.path.join(dst, "kernel_stats.csv"))
+# the bench line printed by the profiled run itself: its HIP-event kernel_ms must agree with
+# rocprof's average duration of the same launches
+blog = os.path.join(src, "bench_under_rocprof.log")
+if os.path.exists(blog):
+    for line in open(blog):
+        if line.startswith('{"metric"'):
+            b = json.loads(line)
+            agree = {"bench_hip_event_dsm_ms": b["kernel_ms"]["dsm"]}
+            if os.path.exists(stats):
+                for r in csv.DictReader(open(stats)):
+                    if r["Name"].split("(")[0] == "fd_dsm_kernel":
+                        agree["rocprof_avg_dsm_ms"] = float(r["AverageNs"]) / 1e6
+                        agree["rocprof_calls"] = int(r["Calls"])
+            b["rocprof_agreement"] = agree
+            json.dump(b, open(os.path.join(dst, "bench_under_rocprof.json"), "w"), indent=1)
+            print("agreement", agree)
 d = out.get("fd_dsm_kernel")
 if d and "hbm_read_bytes" in d:
     json.dump({"kernel": "fd_dsm_kernel", "source": dst,
