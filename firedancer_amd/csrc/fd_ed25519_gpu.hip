@@ -1061,6 +1061,22 @@ fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__
   for( u32 i=threadIdx.x; i<(r.sz >> 4); i+=64u ) { uint4 v = src[i]; a[i] = v; o[i] = v; }
 }
 
+/* Gathered raw batches: the fd_txn_t image of each parsed transaction
+   goes straight into the caller's out region behind its payload, at the
+   next 2-byte boundary (where the tile publishes it,
+   fd_verify_tile.c:131-134), in 2-byte stores of one 64-lane group. */
+__global__ void __launch_bounds__( 64 )
+fd_img_scatter_kernel( fdgpu_txn_raw_t const * __restrict__ raw, unsigned char const * __restrict__ img, u32 stride,
+                       unsigned short const * __restrict__ fp, unsigned char * __restrict__ out ) {
+  u32 t = blockIdx.x;
+  u32 n = fp[t];
+  fdgpu_txn_raw_t r = raw[t];
+  unsigned char * dst = out + ( ( r.payload_off + (u32)r.payload_sz + 1u ) & ~1u );
+  unsigned short const * s16 = (unsigned short const *)( img + (size_t)t*stride );
+  for( u32 i=threadIdx.x; i<(n >> 1); i+=64u ) ((unsigned short *)dst)[i] = s16[i];
+  if( ( n & 1u ) && threadIdx.x==0u ) dst[n-1u] = img[(size_t)t*stride + n - 1u];
+}
+
 /* ==================================================================
    Host runtime: C ABI (include/fd_ed25519_gpu.h)
    ================================================================== */
@@ -1629,7 +1645,13 @@ static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
          : launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
   if( rc ) return rc;
   HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
-  if( sl.mode ) {   /* raw and in-place raw */
+  if( sl.mode==3 ) {   /* gathered: the images go into the out region, only the footprints come back */
+    hipLaunchKernelGGL( fd_img_scatter_kernel, dim3( (unsigned)sl.txn_cnt ), dim3( 64 ), 0, st,
+                        (fdgpu_txn_raw_t const *)sl.d_desc, sl.d_img, (u32)FDGPU_TXN_IMG_STRIDE, sl.d_fp,
+                        sl.ref_dev + sl.ref_lo );
+    HIPCHK( hipGetLastError(), -2 );
+    HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
+  } else if( sl.mode ) {   /* raw and in-place raw */
     HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
     HIPCHK( hipMemcpyAsync( sl.h_img, sl.d_img, sl.txn_cnt * FDGPU_TXN_IMG_STRIDE, hipMemcpyDeviceToHost, st ), -2 );
   }
@@ -1865,7 +1887,7 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
       out_tags[n+t]  = sl.h_tags[u];
       out_codes[n+t] = sl.h_txn_out[u];
       if( out_fp )  out_fp[n+t] = sl.mode ? sl.h_fp[u] : 0;
-      if( out_img && sl.mode ) {
+      if( out_img && sl.mode && sl.mode != 3 ) {   /* mode 3: the image is in the caller's out region */
         unsigned fp = sl.h_fp[u];
         memcpy( out_img + (n+t)*FDGPU_TXN_IMG_STRIDE, sl.h_img + u*FDGPU_TXN_IMG_STRIDE, fp );
       }

@@ -379,6 +379,9 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
     vt->metrics[0]++;
     return FDGPU_VTILE_PARSE_FAIL;
   }
+  /* zero-copy: the GPU already wrote the fd_txn_t image behind the payload */
+  ulong t_off = ( FDGPU_TXNM_HDR_SZ + txnm->payload_sz + 1UL ) & ~1UL;
+  if( vt->zc ) img = (uchar const *)txnm + t_off;
   /* fd_txn_verify (fd_verify_tile.h:59-108): dedup query, verify, insert */
   unsigned sig_off = (unsigned)img[2] | ((unsigned)img[3] << 8);
   ulong tag = xxh64_64( vt->seed, payload + sig_off );
@@ -393,8 +396,7 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
     return FDGPU_VTILE_VERIFY_FAIL;
   }
   /* publish: fd_txn_t behind the payload at a 2-byte boundary */
-  ulong t_off = ( FDGPU_TXNM_HDR_SZ + txnm->payload_sz + 1UL ) & ~1UL;
-  memcpy( (uchar *)txnm + t_off, img, fp );
+  if( !vt->zc ) memcpy( (uchar *)txnm + t_off, img, fp );
   d->sz = t_off + fp;                                  /* fd_txn_m_realized_footprint( txnm, 1, 0 ) */
   d->tag = is_bundle ? 0UL : tag;
   vt->metrics[4]++;
@@ -408,9 +410,20 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
   while( n < max && vt->pend_head < vt->pend_tail ) {
     ulong want = max - n;
     if( want > vt->batch ) want = vt->batch;
-    ulong k = fdgpu_ed25519_poll_raw( vt->ctx, vt->p_tags, vt->p_codes, vt->p_img, vt->p_fp, want, blocking );
+    ulong k = fdgpu_ed25519_poll_raw( vt->ctx, vt->p_tags, vt->p_codes, vt->zc ? NULL : vt->p_img, vt->p_fp, want, blocking );
     if( !k ) break;
     for( ulong i=0; i<k; i++ ) {
+      /* the records were written by the GPU / by non-temporal stores, so they are not in
+         this core's caches: prefetch a few frags ahead -- header + first signature lines at
+         distance 8, the fd_txn_t line (its offset needs the header) at distance 4 */
+      if( vt->pend_head + 8UL < vt->pend_tail ) {
+        uchar const * r = vt->dcache + vt->pend[ ( vt->pend_head + 8UL ) % vt->pend_cap ].chunk * FDGPU_CHUNK_SZ;
+        __builtin_prefetch( r ); __builtin_prefetch( r + 64 ); __builtin_prefetch( r + 128 );
+      }
+      if( vt->pend_head + 4UL < vt->pend_tail ) {
+        uchar const * r = vt->dcache + vt->pend[ ( vt->pend_head + 4UL ) % vt->pend_cap ].chunk * FDGPU_CHUNK_SZ;
+        __builtin_prefetch( r + ( ( FDGPU_TXNM_HDR_SZ + ((fdgpu_txnm_t const *)r)->payload_sz + 1UL ) & ~1UL ) );
+      }
       vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
       /* tags are the pending counter: completions come back in order */
       out[n].result = vt_after( vt, p, (int)vt->p_codes[i], vt->p_img + i*FDGPU_TXN_IMG_STRIDE, vt->p_fp[i], &out[n] );

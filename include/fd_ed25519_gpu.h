@@ -360,7 +360,11 @@ void   fdgpu_host_unregister( void * p );
    77-79).  Records of one batch lie at increasing dst addresses of one
    region (a lower one starts a new batch), 16-B aligned, with room for
    copy_sz rounded up to 16 at dst; src must stay valid until the batch
-   is launched (the caller checks for overruns after the verdict). */
+   is launched (the caller checks for overruns after the verdict).  The
+   GPU also writes each parsed transaction's fd_txn_t image into the out
+   region, behind the payload at the next 2-byte boundary (where the
+   tile publishes it), so poll_raw returns footprints but leaves out_img
+   untouched for these transactions; leave room for 852 bytes there. */
 int
 fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx,
                                  unsigned char const * src,
