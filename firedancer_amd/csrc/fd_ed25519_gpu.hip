@@ -1399,6 +1399,8 @@ fdgpu_ed25519_verify_txns_device( fdgpu_ed25519_ctx_t * ctx, unsigned char const
                        stream ? (hipStream_t)stream : ctx->stream );
 }
 
+static unsigned char * region_dev( void const * p, unsigned long sz );
+
 /* Host-side validation of a batch before staging: payload bounds and
    the sig_base prefix (the device kernels additionally bound-check every
    transaction against its own payload). */
@@ -1429,12 +1431,19 @@ fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
   hipStream_t st = ctx->stream;
   memcpy( sl.h_desc, desc, txn_cnt * sizeof(fdgpu_txn_desc_t) );
   HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
+  if( region_dev( payload, payload_bytes ) ) {
+    /* the caller's payload is already pinned (fdgpu_host_alloc / fdgpu_host_register, e.g. a
+       registered dcache): one DMA straight from it, no staging copy; the slack is zeroed on the device */
+    HIPCHK( hipMemcpyAsync( sl.d_payload, payload, payload_bytes, hipMemcpyHostToDevice, st ), -2 );
+    HIPCHK( hipMemsetAsync( sl.d_payload + payload_bytes, 0, FD_ARENA_SLACK, st ), -2 );
+  } else {
   /* stage in chunks: the DMA of chunk i overlaps the host copy of chunk i+1 */
   memset( sl.h_payload + payload_bytes, 0, FD_ARENA_SLACK );
   for( unsigned long off=0UL; off<payload_bytes+FD_ARENA_SLACK; off+=FD_STAGE_CHUNK ) {
     unsigned long end = off + FD_STAGE_CHUNK < payload_bytes + FD_ARENA_SLACK ? off + FD_STAGE_CHUNK : payload_bytes + FD_ARENA_SLACK;
     if( off < payload_bytes ) memcpy( sl.h_payload + off, payload + off, ( end < payload_bytes ? end : payload_bytes ) - off );
     HIPCHK( hipMemcpyAsync( sl.d_payload + off, sl.h_payload + off, end - off, hipMemcpyHostToDevice, st ), -2 );
+  }
   }
   int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, txn_cnt, nsig, sl.d_txn_out, NULL, st );
   if( rc ) return rc;

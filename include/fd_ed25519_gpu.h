@@ -174,7 +174,10 @@ fdgpu_ed25519_verify_txns_device( fdgpu_ed25519_ctx_t *    ctx,
                                   void *                   stream );
 
 /* fdgpu_ed25519_verify_txns_host: same from host memory; stages through
-   the ctx's pinned buffers, runs, and waits.  Synchronous. */
+   the ctx's pinned buffers, runs, and waits.  Synchronous.  A payload
+   that lies inside one fdgpu_host_alloc / fdgpu_host_register-ed region
+   (a pinned dcache) is DMA'd to the device directly, with no staging
+   copy. */
 int
 fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t *    ctx,
                                 unsigned char const *    payload,

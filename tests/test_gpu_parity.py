@@ -186,3 +186,30 @@ def test_verify_many_golden(fa, golden, sem, key):
     got = eng.verify_many(msgs, [v["sig"][i].tobytes() for i in range(n)], [v["pub"][i].tobytes() for i in range(n)])
     eng.close()
     np.testing.assert_array_equal(got, v[key])
+
+
+def _aligned_copy(a: np.ndarray) -> np.ndarray:
+    raw = np.zeros(a.nbytes + 8192, dtype=np.uint8)
+    o = (-raw.ctypes.data) % 4096
+    b = raw[o:o + a.nbytes]
+    b[:] = a.view(np.uint8)
+    return b
+
+
+@pytest.mark.parametrize("sem,sfx", [(0, "avx"), (1, "ref")])
+def test_pinned_payload_direct_dma(fa, golden, sem, sfx):
+    """A payload in a registered (pinned) host buffer is DMA'd without staging: same codes as staged."""
+    from firedancer_amd import engine
+    t = golden["txns"]
+    payload, desc, nsig = txns_fixture(t)
+    pinned = _aligned_copy(payload)
+    engine.host_register(pinned)
+    try:
+        eng = _engine(fa, len(desc), nsig, payload.nbytes, sem)
+        for _ in range(2):     # twice: the device slack must be re-zeroed, not left from the first batch
+            txn, sig = eng.verify_txns_host(pinned, desc)
+            np.testing.assert_array_equal(txn, t[f"txn_code_{sfx}"])
+            np.testing.assert_array_equal(sig, t[f"sig_code_{sfx}"])
+        eng.close()
+    finally:
+        engine.host_unregister(pinned)
