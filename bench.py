@@ -322,7 +322,14 @@ def main():
                                          f"S=44 M=72 MAC)",
                          "peak_source": "fdgpu_mad_peak_per_s: measured v_mad_u64_u32 throughput, this device (max of 3)",
                          "valu_busy": valu_busy,
-                         "valu_busy_source": "profiles/dsm_pmc.json: SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE/8)"},
+                         "valu_busy_source": "profiles/dsm_pmc.json: SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE/8)",
+                         # the same kernel against the HBM roofline: PMC bytes per launch / this run's launch time
+                         "hbm": ({"achieved": traffic * nsig / (1 << 20) / (dom_ms * 1e-3) / 1e9, "peak": 8000.0,
+                                  "unit": "GB/s",
+                                  "frac": traffic * nsig / (1 << 20) / (dom_ms * 1e-3) / 8e12,
+                                  "note": "PMC bytes (FETCH_SIZE x1024 x2 + WRITE_SIZE x1024) per 1M-sig launch, "
+                                          "scaled to this launch; L2/MALL-resident tables, not HBM-bound"}
+                                 if traffic else None)},
             "cpu_baseline": cpu,
             "per_gpu": per_gpu,
             "latency": lat,
