@@ -114,9 +114,17 @@ def main():
 
     env = shard.dist_env()
     world, rank, local_rank = env.world, env.rank, env.local_rank
-    torch.cuda.set_device(local_rank)
+    # rehearsal knobs for the N>1 flow on a one-GPU box: FDGPU_BENCH_BACKEND=gloo (collectives on CPU
+    # tensors) and FDGPU_BENCH_ONE_DEVICE=1 (every rank on GPU 0).  The driver's runs use neither.
+    backend = os.environ.get("FDGPU_BENCH_BACKEND", "nccl")
+    dev = 0 if os.environ.get("FDGPU_BENCH_ONE_DEVICE") == "1" else local_rank
+    red_dev = "cuda" if backend == "nccl" else "cpu"
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
 
     def barrier():
         if world > 1:
@@ -132,7 +140,7 @@ def main():
     pay_d = torch.from_numpy(payload).cuda()
     desc_d = torch.from_numpy(desc.view(np.uint8)).cuda()
     out_d = torch.empty(n, dtype=torch.int8, device="cuda")
-    eng = Engine(device=local_rank, max_txn=n, max_sig=nsig)
+    eng = Engine(device=dev, max_txn=n, max_sig=nsig)
     st = torch.cuda.current_stream().cuda_stream
 
     def step():
@@ -148,7 +156,7 @@ def main():
 
     got = out_d.cpu().numpy()
     ok = bool(np.array_equal(got, expect))
-    dt_max, all_ok = shard.reduce_max_min(dist if world > 1 else None, dt, ok, "cuda")
+    dt_max, all_ok = shard.reduce_max_min(dist if world > 1 else None, dt, ok, red_dev)
 
     # BASELINE configs[0] / [2] / [3] on the same device path, rank 0 only:
     # throughput with HBM-resident input plus a check of every result code
@@ -161,7 +169,7 @@ def main():
                                         ("configs2_adversarial_10pct", synth.LARGE_NOOP, 1 << 20, 1, 0.1),
                                         ("configs3_multisig_1to12", synth.MULTI, 1 << 18, 12, 0.1)):
             xp, xd, xe, xn = synth.make_batch(nt, kind, ms, inv, seed=shard.shard_seed(4321, rank), threads=gen_threads)
-            xe_d = Engine(device=local_rank, max_txn=nt, max_sig=xn)
+            xe_d = Engine(device=dev, max_txn=nt, max_sig=xn)
             xpd = torch.from_numpy(xp).cuda()
             xdd = torch.from_numpy(xd.view(np.uint8)).cuda()
             xo = torch.empty(nt, dtype=torch.int8, device="cuda")
@@ -181,7 +189,7 @@ def main():
         # p99 batch latency: host-staged batches (H2D + kernels + D2H), submit -> verdict
         lb = min(args.latency_batch, n)
         lpay = payload[: int(desc["payload_off"][lb - 1]) + 1232 + 64]
-        leng = Engine(device=local_rank, max_txn=lb, max_sig=lb, max_payload=lpay.nbytes)
+        leng = Engine(device=dev, max_txn=lb, max_sig=lb, max_payload=lpay.nbytes)
         ld = desc[:lb].copy()
         leng.verify_txns_host(lpay, ld, want_sig_codes=False)
         times = []
@@ -239,19 +247,19 @@ def main():
         else:                                   # sustained runs of --stream-seconds each
             barrier()
             cal = vtile.stream_bench(payload, off, psz, n_frags=2_000_000, tiles=args.stream_tiles,
-                                     batch_txn=args.stream_batch, max_inflight=2, mcache_depth=1 << 18, zero_copy=zc)
+                                     batch_txn=args.stream_batch, max_inflight=2, mcache_depth=1 << 18, zero_copy=zc, device=dev)
             n_max = int(1.2 * cal["frags_per_s"] * args.stream_seconds)   # short runs under-read the rate
             n_pace = int(args.stream_rate * args.stream_seconds)
         barrier()
         smax = vtile.stream_bench(payload, off, psz, n_frags=n_max, tiles=args.stream_tiles,
-                                  batch_txn=args.stream_batch, max_inflight=2, mcache_depth=1 << 18, zero_copy=zc)
+                                  batch_txn=args.stream_batch, max_inflight=2, mcache_depth=1 << 18, zero_copy=zc, device=dev)
         barrier()
         slat = vtile.stream_bench(payload, off, psz, n_frags=n_pace, tiles=args.stream_lat_tiles,
                                   batch_txn=args.stream_batch, max_inflight=2, rate_fps=args.stream_rate,
-                                  mcache_depth=1 << 18, zero_copy=zc)
+                                  mcache_depth=1 << 18, zero_copy=zc, device=dev)
         ok_s = (smax["metrics"][:4] == [0, 0, 0, 0] and smax["published"] == n_max
                 and slat["metrics"][:4] == [0, 0, 0, 0] and slat["published"] == n_pace)
-        sig_tot, t_max, _ = shard.reduce_sum_max(dist if world > 1 else None, smax["sigs"], smax["seconds"], "cuda")
+        sig_tot, t_max, _ = shard.reduce_sum_max(dist if world > 1 else None, smax["sigs"], smax["seconds"], red_dev)
         stream = {"workload": "BASELINE configs[4]: 1232-byte txns through mcache/dcache -> GPU verify tiles "
                               "(device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> out dcache",
                   "sigs_per_s": sig_tot / t_max, "per_gpu_sigs_per_s": smax["sigs_per_s"], "n_gpus": world,
@@ -273,9 +281,9 @@ def main():
     L = load_library()
     L.fdgpu_mad_peak_per_s.restype = ctypes.c_double
     L.fdgpu_mad_peak_per_s.argtypes = [ctypes.c_int]
-    my_peak = max(float(L.fdgpu_mad_peak_per_s(local_rank)) for _ in range(3))
+    my_peak = max(float(L.fdgpu_mad_peak_per_s(dev)) for _ in range(3))
     my_ach = DSM_MAC * nsig / (ms_dsm * 1e-3)
-    rows = shard.gather_rows(dist if world > 1 else None, [rank, ms_dsm, ms_prep, my_ach, my_peak, dt], "cuda")
+    rows = shard.gather_rows(dist if world > 1 else None, [rank, ms_dsm, ms_prep, my_ach, my_peak, dt], red_dev)
     per_gpu = [{"rank": int(r[0]), "dsm_ms": r[1], "prep_ms": r[2], "achieved_gmac_s": r[3] / 1e9,
                 "peak_gmac_s": r[4] / 1e9, "frac": r[3] / r[4] if r[4] > 0 else None,
                 "sigs_per_s": nsig * args.steps / r[5]} for r in rows]
