@@ -100,6 +100,9 @@ def main():
                     help="stream tiles copy each frag into the out dcache on the host (the reference tile's "
                          "during_frag) instead of the zero-copy intake (GPU gathers from the registered in dcache)")
     ap.add_argument("--stream-batch", type=int, default=8192)
+    ap.add_argument("--stream-inflight", type=int, default=1,
+                    help="batches a tile keeps launched on its GPU stream before it launches the filling one "
+                         "(1: a frag waits for at most the running batch; tools/stream_sweep.py, s13)")
     ap.add_argument("--stream-rate", type=float, default=2e6, help="paced rate (frags/s) of the latency run")
     ap.add_argument("--stream-lat-tiles", type=int, default=2,
                     help="verify tiles of the paced latency run (fewer tiles = fewer HIP streams sharing the "
@@ -263,15 +266,15 @@ def main():
         else:                                   # sustained runs of --stream-seconds each
             barrier()
             cal = vtile.stream_bench(payload, off, psz, n_frags=2_000_000, tiles=args.stream_tiles,
-                                     batch_txn=args.stream_batch, max_inflight=2, mcache_depth=1 << 18, zero_copy=zc, device=dev)
+                                     batch_txn=args.stream_batch, max_inflight=args.stream_inflight, mcache_depth=1 << 18, zero_copy=zc, device=dev)
             n_max = int(1.2 * cal["frags_per_s"] * args.stream_seconds)   # short runs under-read the rate
             n_pace = int(args.stream_rate * args.stream_seconds)
         barrier()
         smax = vtile.stream_bench(payload, off, psz, n_frags=n_max, tiles=args.stream_tiles,
-                                  batch_txn=args.stream_batch, max_inflight=2, mcache_depth=1 << 18, zero_copy=zc, device=dev)
+                                  batch_txn=args.stream_batch, max_inflight=args.stream_inflight, mcache_depth=1 << 18, zero_copy=zc, device=dev)
         barrier()
         slat = vtile.stream_bench(payload, off, psz, n_frags=n_pace, tiles=args.stream_lat_tiles,
-                                  batch_txn=args.stream_batch, max_inflight=2, rate_fps=args.stream_rate,
+                                  batch_txn=args.stream_batch, max_inflight=args.stream_inflight, rate_fps=args.stream_rate,
                                   mcache_depth=1 << 18, zero_copy=zc, device=dev)
         ok_s = (smax["metrics"][:4] == [0, 0, 0, 0] and smax["published"] == n_max
                 and slat["metrics"][:4] == [0, 0, 0, 0] and slat["published"] == n_pace)
@@ -280,6 +283,7 @@ def main():
                               "(device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> out dcache",
                   "sigs_per_s": sig_tot / t_max, "per_gpu_sigs_per_s": smax["sigs_per_s"], "n_gpus": world,
                   "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch,
+                  "max_inflight": args.stream_inflight,
                   "intake": "zero-copy (GPU gathers frags from the registered in dcache)" if zc
                             else "host copy into the out dcache (reference during_frag)",
                   "max_rate": {"frags": n_max, "seconds": smax["seconds"], "p50_us": smax["lat_p50_us"],

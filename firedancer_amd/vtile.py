@@ -184,7 +184,7 @@ class VTile:
 
 
 def stream_bench(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,
-                 batch_txn: int = 4096, max_inflight: int = 2, mcache_depth: int = 1 << 16, rate_fps: float = 0.0,
+                 batch_txn: int = 4096, max_inflight: int = 1, mcache_depth: int = 1 << 16, rate_fps: float = 0.0,
                  device: int = 0, zero_copy: bool = False) -> dict:
     L = load()
     payload = np.ascontiguousarray(payload, np.uint8)
