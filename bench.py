@@ -284,6 +284,7 @@ def main():
                   "sigs_per_s": sig_tot / t_max, "per_gpu_sigs_per_s": smax["sigs_per_s"], "n_gpus": world,
                   "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch,
                   "max_inflight": args.stream_inflight,
+                  "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
                   "intake": "zero-copy (GPU gathers frags from the registered in dcache)" if zc
                             else "host copy into the out dcache (reference during_frag)",
                   "max_rate": {"frags": n_max, "seconds": smax["seconds"], "p50_us": smax["lat_p50_us"],

@@ -226,11 +226,25 @@ vt_fence( void ) {
 
 typedef struct {
   ulong seq, tsorig, chunk;
+  int   k;                               /* engine context the frag's batch went to */
 } vt_pend_t;
+
+/* Engine contexts per tile (env FDGPU_VTILE_CTX, 1..VT_NCTX_MAX, default 2).
+   A context runs its batches in order on one HIP stream, so with one
+   context a frag that arrives while a batch runs waits for all of it.
+   With several, the tile fills them in turn and launches staggered by
+   the batch duration / nctx, so batches overlap on the GPU and a frag
+   waits for at most that stagger before its batch starts.  Completions
+   are merged back into frag order in after_frags. */
+#define VT_NCTX_MAX 3
 
 struct fdgpu_vtile {
   /* (fields below; ctx first so the watchdog can report pipeline state) */
-  fdgpu_ed25519_ctx_t * ctx;
+  fdgpu_ed25519_ctx_t * ctx[ VT_NCTX_MAX ];
+  int                   nctx, fill;      /* contexts, the one taking frags */
+  ulong                 launch_ns[ VT_NCTX_MAX ];
+  int                   busy[ VT_NCTX_MAX ];
+  double                batch_ns;        /* EWMA of launch -> drained */
   fdgpu_tcache_t *      tcache;
   ulong                 seed;
   uchar *               dcache;
@@ -260,13 +274,21 @@ fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ul
   if( !vt ) return NULL;
   /* staging arena of a batch = its range of the out dcache (in-place submits): up to
      batch_txn records of at most VT_RESERVE_MAX bytes (rounded to chunk pairs) */
-  vt->ctx = fdgpu_ed25519_ctx_new( device, batch_txn, 16UL*batch_txn, batch_txn*2304UL + 1024UL, semantics );
-  /* adaptive batching launches a partial batch when the GPU has room (low
-     load: the latency path) and a full one when frags back up (high load:
-     the throughput path, whose per-signature work is 0.5x the 4-lane DSM's) */
-  if( vt->ctx ) {
-    ulong sm = fdgpu_ed25519_set_small_batch_max( vt->ctx, 0UL );
-    fdgpu_ed25519_set_small_batch_max( vt->ctx, sm < batch_txn/2UL ? sm : batch_txn/2UL );
+  char const * ne = getenv( "FDGPU_VTILE_CTX" );
+  vt->nctx = ne ? atoi( ne ) : 2;
+  if( vt->nctx < 1 ) vt->nctx = 1;
+  if( vt->nctx > VT_NCTX_MAX ) vt->nctx = VT_NCTX_MAX;
+  vt->batch_ns = 500e3;
+  int ctx_ok = 1;
+  for( int k=0; k<vt->nctx; k++ ) {
+    vt->ctx[k] = fdgpu_ed25519_ctx_new( device, batch_txn, 16UL*batch_txn, batch_txn*2304UL + 1024UL, semantics );
+    /* adaptive batching launches a partial batch when the GPU has room (low
+       load: the latency path) and a full one when frags back up (high load:
+       the throughput path, whose per-signature work is 0.5x the 4-lane DSM's) */
+    if( vt->ctx[k] ) {
+      ulong sm = fdgpu_ed25519_set_small_batch_max( vt->ctx[k], 0UL );
+      fdgpu_ed25519_set_small_batch_max( vt->ctx[k], sm < batch_txn/2UL ? sm : batch_txn/2UL );
+    } else ctx_ok = 0;
   }
   vt->tcache = fdgpu_tcache_new( tcache_depth );
   ulong nchunk = ( out_dcache_bytes / FDGPU_CHUNK_SZ ) & ~1UL;
@@ -282,7 +304,7 @@ fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ul
   vt->p_codes = (signed char *)malloc( batch_txn );
   vt->p_img = (uchar *)malloc( batch_txn * FDGPU_TXN_IMG_STRIDE );
   vt->p_fp = (unsigned short *)malloc( batch_txn * sizeof(unsigned short) );
-  if( !vt->ctx || !vt->tcache || !vt->dcache || !vt->pend || !vt->p_tags || !vt->p_codes || !vt->p_img || !vt->p_fp ) {
+  if( !ctx_ok || !vt->tcache || !vt->dcache || !vt->pend || !vt->p_tags || !vt->p_codes || !vt->p_img || !vt->p_fp ) {
     fdgpu_vtile_delete( vt );
     return NULL;
   }
@@ -292,7 +314,7 @@ fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ul
 void
 fdgpu_vtile_delete( fdgpu_vtile_t * vt ) {
   if( !vt ) return;
-  if( vt->ctx ) fdgpu_ed25519_ctx_delete( vt->ctx );
+  for( int k=0; k<VT_NCTX_MAX; k++ ) if( vt->ctx[k] ) fdgpu_ed25519_ctx_delete( vt->ctx[k] );
   fdgpu_tcache_delete( vt->tcache );
   fdgpu_host_free( vt->dcache ); free( vt->pend ); free( vt->p_tags ); free( vt->p_codes ); free( vt->p_img ); free( vt->p_fp );
   free( vt );
@@ -301,7 +323,30 @@ fdgpu_vtile_delete( fdgpu_vtile_t * vt ) {
 uchar * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt ) { return vt->dcache; }
 ulong   fdgpu_vtile_pending( fdgpu_vtile_t const * vt ) { return vt->pend_tail - vt->pend_head; }
 void    fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, ulong out[ 5 ] ) { memcpy( out, vt->metrics, sizeof(vt->metrics) ); }
-int     fdgpu_vtile_flush( fdgpu_vtile_t * vt ) { vt_fence(); return fdgpu_ed25519_flush( vt->ctx ); }
+int
+fdgpu_vtile_flush( fdgpu_vtile_t * vt ) {
+  vt_fence();
+  int rc = 0;
+  for( int i=0; i<vt->nctx; i++ ) {            /* oldest first: the fill context's batch is the newest */
+    int k = ( vt->fill + 1 + i ) % vt->nctx;
+    ulong filling, inflight;
+    fdgpu_ed25519_pipeline_state( vt->ctx[k], &filling, &inflight );
+    if( !filling ) continue;
+    if( fdgpu_ed25519_flush( vt->ctx[k] ) ) rc = -1;
+    else { vt->launch_ns[k] = now_ns(); vt->busy[k] = 1; }
+  }
+  return rc;
+}
+
+void
+fdgpu_vtile_pipeline_state( fdgpu_vtile_t const * vt, ulong * filling, ulong * inflight ) {
+  *filling = 0UL; *inflight = 0UL;
+  for( int k=0; k<vt->nctx; k++ ) {
+    ulong f, i;
+    fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i );
+    *filling += f; *inflight += i;
+  }
+}
 ulong   fdgpu_vtile_overruns( fdgpu_vtile_t const * vt ) { return vt->overruns; }
 
 int
@@ -318,15 +363,34 @@ fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt ) {
 
 int
 fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
-  ulong filling, inflight;
-  fdgpu_ed25519_pipeline_state( vt->ctx, &filling, &inflight );
+  ulong filling, inflight, now = now_ns();
+  /* batch duration: a context's batches have drained (inflight counts
+     launched slots not yet fully polled) */
+  for( int k=0; k<vt->nctx; k++ ) {
+    if( !vt->busy[k] ) continue;
+    ulong f, i;
+    fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i );
+    if( !i ) { vt->busy[k] = 0; vt->batch_ns = 0.875*vt->batch_ns + 0.125*(double)( now - vt->launch_ns[k] ); }
+  }
+  int f = vt->fill;
+  fdgpu_ed25519_pipeline_state( vt->ctx[f], &filling, &inflight );
   /* keep at least one staging slot free to accumulate in: with every slot
      in flight, each freed slot would be relaunched after a handful of
      frags and the pipeline would degenerate into tiny batches */
   if( max_inflight > 3UL ) max_inflight = 3UL;
   if( !filling || inflight >= max_inflight ) return 0;
+  if( vt->nctx > 1 && filling < vt->batch ) {
+    /* stagger: launch once every other context's newest batch has run
+       batch_ns / nctx (or that context is idle) */
+    ulong stagger = (ulong)( vt->batch_ns / (double)vt->nctx );
+    for( int k=0; k<vt->nctx; k++ )
+      if( k != f && vt->busy[k] && now - vt->launch_ns[k] < stagger ) return 0;
+  }
   vt_fence();
-  return fdgpu_ed25519_flush( vt->ctx ) ? 0 : 1;
+  if( fdgpu_ed25519_flush( vt->ctx[f] ) ) return 0;
+  vt->launch_ns[f] = now; vt->busy[f] = 1;
+  vt->fill = ( f + 1 ) % vt->nctx;
+  return 1;
 }
 
 int
@@ -336,20 +400,20 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
      the payload must fit the MTU (the reference FD_LOG_ERRs) */
   if( sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U || FDGPU_TXNM_HDR_SZ + in->payload_sz > sz ) return -4;
   vt_fence();
-  if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_ed25519_flush( vt->ctx ); return -2; }
+  if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_vtile_flush( vt ); return -2; }
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
   int rc;
   if( vt->zc ) {   /* the GPU copies the frag into dst itself (no host copy) */
-    rc = fdgpu_ed25519_submit_raw_gather( vt->ctx, (uchar const *)frag, vt->dcache, dst,
+    rc = fdgpu_ed25519_submit_raw_gather( vt->ctx[ vt->fill ], (uchar const *)frag, vt->dcache, dst,
                                           (unsigned short)( FDGPU_TXNM_HDR_SZ + in->payload_sz ),
                                           (unsigned short)FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
   } else {
     vt_copy( dst, (uchar const *)frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
-    rc = fdgpu_ed25519_submit_raw_ref( vt->ctx, vt->dcache, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
+    rc = fdgpu_ed25519_submit_raw_ref( vt->ctx[ vt->fill ], vt->dcache, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
   }
   if( rc ) return rc;
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
-  p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk;
+  p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill;
   vt->pend_tail++;
   ulong reserve = ( ( FDGPU_TXNM_HDR_SZ + in->payload_sz + 1UL ) & ~1UL ) + 852UL;
   vt->out_chunk = fdgpu_dcache_compact_next( vt->out_chunk, reserve, vt->chunk0, vt->wmark );
@@ -406,11 +470,17 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
 ulong
 fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max, int blocking ) {
   ulong n = 0UL;
-  if( blocking ) { vt_fence(); fdgpu_ed25519_flush( vt->ctx ); }   /* a blocking drain must not wait on an unlaunched batch */
+  if( blocking ) fdgpu_vtile_flush( vt );      /* a blocking drain must not wait on an unlaunched batch */
   while( n < max && vt->pend_head < vt->pend_tail ) {
-    ulong want = max - n;
-    if( want > vt->batch ) want = vt->batch;
-    ulong k = fdgpu_ed25519_poll_raw( vt->ctx, vt->p_tags, vt->p_codes, vt->zc ? NULL : vt->p_img, vt->p_fp, want, blocking );
+    /* the next completions in frag order: the run of pending frags from
+       the head that went to the same context (each context completes in
+       its own submission order) */
+    int c = vt->pend[ vt->pend_head % vt->pend_cap ].k;
+    ulong want = 1UL, lim = max - n;
+    if( lim > vt->batch ) lim = vt->batch;
+    while( want < lim && vt->pend_head + want < vt->pend_tail &&
+           vt->pend[ ( vt->pend_head + want ) % vt->pend_cap ].k == c ) want++;
+    ulong k = fdgpu_ed25519_poll_raw( vt->ctx[c], vt->p_tags, vt->p_codes, vt->zc ? NULL : vt->p_img, vt->p_fp, want, blocking );
     if( !k ) break;
     for( ulong i=0; i<k; i++ ) {
       /* the records were written by the GPU / by non-temporal stores, so they are not in
@@ -574,7 +644,7 @@ static void * sb_tile( void * _a ) {
     if( seq != last_seq || got != last_got ) { last_seq = seq; last_got = got; t_prog = t0; }
     else if( t0 - t_prog > 30000000000UL ) {                      /* watchdog: 30 s without progress */
       ulong filling = 0, inflight = 0;
-      fdgpu_ed25519_pipeline_state( vt->ctx, &filling, &inflight );
+      fdgpu_vtile_pipeline_state( vt, &filling, &inflight );
       fprintf( stderr, "fdgpu_stream_bench: tile %d stalled: seq %lu got %lu/%lu pending %lu filling %lu inflight %lu\n",
                idx, seq, got, mine, fdgpu_vtile_pending( vt ), filling, inflight );
       atomic_store( &s->fail, 5 ); break;

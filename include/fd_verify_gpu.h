@@ -150,8 +150,15 @@ int             fdgpu_vtile_set_in_link( fdgpu_vtile_t * vt, fdgpu_mcache_t cons
 unsigned long   fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt );
 /* frags dropped as FDGPU_VTILE_OVERRUN */
 unsigned long   fdgpu_vtile_overruns( fdgpu_vtile_t const * vt );
-/* launch the partially filled batch (call when the input is idle) */
+/* launch the partially filled batches (call when the input is idle) */
 int             fdgpu_vtile_flush( fdgpu_vtile_t * vt );
+/* transactions waiting in unlaunched batches, and launched batches not yet
+   drained, summed over the tile's engine contexts (env FDGPU_VTILE_CTX,
+   1..3, default 2: batches of consecutive frags go to the contexts in
+   turn, launched staggered by a fraction of the batch duration so a frag
+   does not wait for a whole running batch before its own starts) */
+void            fdgpu_vtile_pipeline_state( fdgpu_vtile_t const * vt, unsigned long * filling,
+                                            unsigned long * inflight );
 /* adaptive batching, for the tile's housekeeping / before_credit hook:
    launch the filling batch when fewer than max_inflight batches are on
    the GPU -- batches stay small (low latency) while the GPU keeps up and
