@@ -82,6 +82,52 @@ def cpu_baseline(payload, desc, nsig_total, threads, target_s=1.5):
                     if kind == "reference" else "oracle/fd_ed25519_oracle.c portable C restatement"}
 
 
+
+def stream_runs(args, payload, desc, dev) -> dict:
+    """BASELINE configs[4]: the payloads streamed through GPU verify tiles (tango mcache/dcache in,
+    fd_txn_parse + verify on the GPU, in-order after_frag, out dcache): a calibration run, then
+    --stream-seconds at the maximum rate on --stream-tiles tiles, then paced on --stream-lat-tiles."""
+    from firedancer_amd import vtile
+    off, psz = desc["payload_off"], desc["payload_sz"]
+    zc = not args.stream_copy
+    kw = dict(batch_txn=args.stream_batch, max_inflight=args.stream_inflight, mcache_depth=1 << 18,
+              zero_copy=zc, device=dev)
+    if args.stream_frags > 0:
+        n_max = n_pace = args.stream_frags
+    else:
+        cal = vtile.stream_bench(payload, off, psz, n_frags=2_000_000, tiles=args.stream_tiles, **kw)
+        n_max = int(1.2 * cal["frags_per_s"] * args.stream_seconds)   # short runs under-read the rate
+        n_pace = int(args.stream_rate * args.stream_seconds)
+    smax = vtile.stream_bench(payload, off, psz, n_frags=n_max, tiles=args.stream_tiles, **kw)
+    slat = vtile.stream_bench(payload, off, psz, n_frags=n_pace, tiles=args.stream_lat_tiles,
+                              rate_fps=args.stream_rate, **kw)
+    return {"smax": smax, "slat": slat, "n_max": n_max, "n_pace": n_pace}
+
+
+def stream_child_main(args) -> None:
+    """--stream-child: regenerate this rank's workload (same seed) and run the stream legs; no torch GPU context."""
+    from firedancer_amd import synth
+    payload, desc, _, _ = synth.make_batch(args.txns, synth.LARGE_NOOP, seed=args.stream_seed,
+                                           threads=min(16, os.cpu_count() or 1))
+    print(json.dumps(stream_runs(args, payload, desc, args.stream_device)), flush=True)
+
+
+def run_stream_child(args, dev, seed, n) -> dict:
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--stream-child", "--stream-device", str(dev),
+           "--stream-seed", str(seed), "--txns", str(n), "--stream-frags", str(args.stream_frags),
+           "--stream-seconds", str(args.stream_seconds), "--stream-tiles", str(args.stream_tiles),
+           "--stream-batch", str(args.stream_batch), "--stream-rate", str(args.stream_rate),
+           "--stream-lat-tiles", str(args.stream_lat_tiles), "--stream-inflight", str(args.stream_inflight)]
+    if args.stream_copy:
+        cmd.append("--stream-copy")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode or not lines:
+        raise RuntimeError(f"stream child rc={r.returncode}: {r.stderr[-1500:]}")
+    return json.loads(lines[-1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -109,7 +155,13 @@ def main():
                          "device's hardware queues; 2 tiles carry 2M frags/s)")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="skip the BASELINE configs[0,2,3] side measurements (small / adversarial / multi-sig)")
+    ap.add_argument("--stream-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--stream-device", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--stream-seed", type=int, default=1234, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.stream_child:
+        stream_child_main(args)
+        return
 
     import torch
     import torch.distributed as dist
@@ -243,44 +295,40 @@ def main():
     # after_frag, out dcache).  Every rank streams its own shard at once.
     stream = None
     if args.stream_frags != 0:
-        from firedancer_amd import vtile
-        off, psz = desc["payload_off"], desc["payload_sz"]
+        # The tiles run in a child process that never initialises torch's GPU context: a verify tile is a
+        # plain C process, and torch's context in this one measurably inflates the tiles' tail latency
+        # (tools/stream_seq.py, TORCH=1: paced p99 1.2 -> 2.2 ms).  Every rank streams its own shard at once.
+        barrier()
         zc = not args.stream_copy
-        if args.stream_frags > 0:
-            n_max = n_pace = args.stream_frags
-        else:                                   # sustained runs of --stream-seconds each
-            barrier()
-            cal = vtile.stream_bench(payload, off, psz, n_frags=2_000_000, tiles=args.stream_tiles,
-                                     batch_txn=args.stream_batch, max_inflight=args.stream_inflight, mcache_depth=1 << 18, zero_copy=zc, device=dev)
-            n_max = int(1.2 * cal["frags_per_s"] * args.stream_seconds)   # short runs under-read the rate
-            n_pace = int(args.stream_rate * args.stream_seconds)
+        try:
+            res = run_stream_child(args, dev, shard.shard_seed(1234, rank), n)
+        except Exception as e:      # keep the headline line even if the stream leg fails
+            res = None
+            stream = {"error": str(e)[-2000:]}
         barrier()
-        smax = vtile.stream_bench(payload, off, psz, n_frags=n_max, tiles=args.stream_tiles,
-                                  batch_txn=args.stream_batch, max_inflight=args.stream_inflight, mcache_depth=1 << 18, zero_copy=zc, device=dev)
-        barrier()
-        slat = vtile.stream_bench(payload, off, psz, n_frags=n_pace, tiles=args.stream_lat_tiles,
-                                  batch_txn=args.stream_batch, max_inflight=args.stream_inflight, rate_fps=args.stream_rate,
-                                  mcache_depth=1 << 18, zero_copy=zc, device=dev)
-        ok_s = (smax["metrics"][:4] == [0, 0, 0, 0] and smax["published"] == n_max
-                and slat["metrics"][:4] == [0, 0, 0, 0] and slat["published"] == n_pace)
-        sig_tot, t_max, _ = shard.reduce_sum_max(dist if world > 1 else None, smax["sigs"], smax["seconds"], red_dev)
-        stream = {"workload": "BASELINE configs[4]: 1232-byte txns through mcache/dcache -> GPU verify tiles "
-                              "(device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> out dcache",
-                  "sigs_per_s": sig_tot / t_max, "per_gpu_sigs_per_s": smax["sigs_per_s"], "n_gpus": world,
-                  "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch,
-                  "max_inflight": args.stream_inflight,
-                  "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
-                  "intake": "zero-copy (GPU gathers frags from the registered in dcache)" if zc
-                            else "host copy into the out dcache (reference during_frag)",
-                  "max_rate": {"frags": n_max, "seconds": smax["seconds"], "p50_us": smax["lat_p50_us"],
-                               "p99_us": smax["lat_p99_us"], "tile_host_ns_per_frag":
-                                   [round(x / max(n_max, 1), 1) for x in smax["tile_ns"]]},
-                  "paced": {"frags": n_pace, "seconds": slat["seconds"], "rate_frags_per_s": args.stream_rate,
-                            "tiles_per_gpu": args.stream_lat_tiles,
-                            "achieved": slat["frags_per_s"], "p50_us": slat["lat_p50_us"],
-                            "p99_us": slat["lat_p99_us"], "max_us": slat["lat_max_us"]},
-                  "all_published": bool(ok_s),
-                  "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
+        if res is not None:
+            smax, slat, n_max, n_pace = res["smax"], res["slat"], res["n_max"], res["n_pace"]
+            ok_s = (smax["metrics"][:4] == [0, 0, 0, 0] and smax["published"] == n_max
+                    and slat["metrics"][:4] == [0, 0, 0, 0] and slat["published"] == n_pace)
+            sig_tot, t_max, _ = shard.reduce_sum_max(dist if world > 1 else None, smax["sigs"], smax["seconds"], red_dev)
+            stream = {"workload": "BASELINE configs[4]: 1232-byte txns through mcache/dcache -> GPU verify tiles "
+                                  "(device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> out dcache",
+                      "sigs_per_s": sig_tot / t_max, "per_gpu_sigs_per_s": smax["sigs_per_s"], "n_gpus": world,
+                      "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch,
+                      "max_inflight": args.stream_inflight,
+                      "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
+                      "process": "tiles in a child process without a torch GPU context (as a C verify tile)",
+                      "intake": "zero-copy (GPU gathers frags from the registered in dcache)" if zc
+                                else "host copy into the out dcache (reference during_frag)",
+                      "max_rate": {"frags": n_max, "seconds": smax["seconds"], "p50_us": smax["lat_p50_us"],
+                                   "p99_us": smax["lat_p99_us"], "tile_host_ns_per_frag":
+                                       [round(x / max(n_max, 1), 1) for x in smax["tile_ns"]]},
+                      "paced": {"frags": n_pace, "seconds": slat["seconds"], "rate_frags_per_s": args.stream_rate,
+                                "tiles_per_gpu": args.stream_lat_tiles,
+                                "achieved": slat["frags_per_s"], "p50_us": slat["lat_p50_us"],
+                                "p99_us": slat["lat_p99_us"], "max_us": slat["lat_max_us"]},
+                      "all_published": bool(ok_s),
+                      "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
 
     if lat is not None:
         # after the stream leg: the drop-in's process-wide context (and its stream) lives until exit
