@@ -514,6 +514,9 @@ fd_dsm_kernel( u32                      nsig,
    compiler's own lowering of __builtin_amdgcn_update_dpp gave wrong
    results here on gfx950 -- measured: every valid signature rejected --
    while these moves and a ds_swizzle __shfl_xor agree with the oracle.) */
+#ifndef FD_DSM4_FUSED
+#define FD_DSM4_FUSED 1      /* 4-lane DSM: broadcasts fused into VOP2 DPP adds/subs (0: separate moves, for A/B) */
+#endif
 #define FD_DPP_MOV( d, a, PERM ) "v_mov_b32_dpp %" #d ", %" #a " " PERM " row_mask:0xf bank_mask:0xf\n\t"
 /* r = a as seen through one quad_perm (10 moves, one asm block) */
 #define FD_DEF_FE_DPP( name, PERM )                                                        \
@@ -543,6 +546,52 @@ FD_DEF_FE_DPP( fe_bcast3, "quad_perm:[3,3,3,3]" )
 FD_DEF_FE_DPP( fe_swap23, "quad_perm:[0,1,3,2]" )       /* lanes 2 and 3 trade */
 FD_DEF_U32_DPP( fd_bcast0, "quad_perm:[0,0,0,0]" )
 FD_DEF_U32_DPP( fd_bcast1, "quad_perm:[1,1,1,1]" )
+
+/* Broadcast fused into the arithmetic: r = OP( quad lane k's a, this lane's b ),
+   one VOP2 DPP instruction per limb (the DPP applies to src0).  v_add_u32 is
+   a + b, v_subrev_u32 is b - a; limbs wrap mod 2^32 exactly as the unfused
+   forms do, so every result is bit-identical to bcast-then-op. */
+#define FD_DPP_OP( OP, d, a, b, PERM ) OP "_dpp %" #d ", %" #a ", %" #b " " PERM " row_mask:0xf bank_mask:0xf\n\t"
+#define FD_DEF_FE_DPP_OP( name, OP, PERM )                                                     \
+FD_DEV void name( fe & r, fe const & a, fe const & b ) {                                       \
+  asm volatile( "s_nop 1\n\t"                                                                  \
+                FD_DPP_OP( OP, 0, 10, 20, PERM ) FD_DPP_OP( OP, 1, 11, 21, PERM )              \
+                FD_DPP_OP( OP, 2, 12, 22, PERM ) FD_DPP_OP( OP, 3, 13, 23, PERM )              \
+                FD_DPP_OP( OP, 4, 14, 24, PERM ) FD_DPP_OP( OP, 5, 15, 25, PERM )              \
+                FD_DPP_OP( OP, 6, 16, 26, PERM ) FD_DPP_OP( OP, 7, 17, 27, PERM )              \
+                FD_DPP_OP( OP, 8, 18, 28, PERM ) FD_DPP_OP( OP, 9, 19, 29, PERM )              \
+                : "=&v"( r.v[0] ), "=&v"( r.v[1] ), "=&v"( r.v[2] ), "=&v"( r.v[3] ), "=&v"( r.v[4] ), \
+                  "=&v"( r.v[5] ), "=&v"( r.v[6] ), "=&v"( r.v[7] ), "=&v"( r.v[8] ), "=&v"( r.v[9] ) \
+                : "v"( a.v[0] ), "v"( a.v[1] ), "v"( a.v[2] ), "v"( a.v[3] ), "v"( a.v[4] ),      \
+                  "v"( a.v[5] ), "v"( a.v[6] ), "v"( a.v[7] ), "v"( a.v[8] ), "v"( a.v[9] ),      \
+                  "v"( b.v[0] ), "v"( b.v[1] ), "v"( b.v[2] ), "v"( b.v[3] ), "v"( b.v[4] ),      \
+                  "v"( b.v[5] ), "v"( b.v[6] ), "v"( b.v[7] ), "v"( b.v[8] ), "v"( b.v[9] ) );    \
+}
+FD_DEF_FE_DPP_OP( fe_add_q0,    "v_add_u32",    "quad_perm:[0,0,0,0]" )   /* a[0] + b */
+FD_DEF_FE_DPP_OP( fe_add_q1,    "v_add_u32",    "quad_perm:[1,1,1,1]" )   /* a[1] + b */
+FD_DEF_FE_DPP_OP( fe_add_q2,    "v_add_u32",    "quad_perm:[2,2,2,2]" )   /* a[2] + b */
+FD_DEF_FE_DPP_OP( fe_add_q3,    "v_add_u32",    "quad_perm:[3,3,3,3]" )   /* a[3] + b */
+FD_DEF_FE_DPP_OP( fe_sub_q0,    "v_sub_u32",    "quad_perm:[0,0,0,0]" )   /* a[0] - b */
+FD_DEF_FE_DPP_OP( fe_sub_q1,    "v_sub_u32",    "quad_perm:[1,1,1,1]" )   /* a[1] - b */
+FD_DEF_FE_DPP_OP( fe_sub_q3,    "v_sub_u32",    "quad_perm:[3,3,3,3]" )   /* a[3] - b */
+/* (not v_subrev_u32_dpp: measured on gfx950, tools/dppprobe, it applies the
+   lane permutation to the other operand) */
+
+/* limb-wise bias constants of fe_sub / fe_sub4 */
+FD_DEV u32 fe_twop( int i )  { return (i==0) ? 0x7ffffdau : ( (i & 1) ? 0x3fffffeu : 0x7fffffeu ); }
+FD_DEV u32 fe_fourp( int i ) { return (i==0) ? 0xfffffb4u : ( (i & 1) ? 0x7fffffcu : 0xffffffcu ); }
+FD_DEV void fe_addc( fe & r, fe const & a, int four ) {       /* r = a + 2p (four=0) or 4p */
+#pragma unroll
+  for( int i=0; i<10; i++ ) r.v[i] = a.v[i] + ( four ? fe_fourp( i ) : fe_twop( i ) );
+}
+FD_DEV void fe_subc( fe & r, fe const & a ) {                 /* r = a - 2p (wraps; only ever subtracted) */
+#pragma unroll
+  for( int i=0; i<10; i++ ) r.v[i] = a.v[i] - fe_twop( i );
+}
+FD_DEV void fe_csub4( fe & r, fe const & a ) {                /* r = 4p - a */
+#pragma unroll
+  for( int i=0; i<10; i++ ) r.v[i] = fe_fourp( i ) - a.v[i];
+}
 
 /* M-step: from completed (E, F, G, H) on both lanes to lane 0 (m0, m1) =
    (X3, T3), lane 1 (m0, m1) = (Y3, Z3); E, F, G, H T or L */
@@ -695,6 +744,18 @@ FD_DEV void quad_mstep( fe & m, int q, fe const & E, fe const & F, fe const & G,
 }
 
 FD_DEV void quad_dbl( fe & E, fe & F, fe & G, fe & H, int q, fe const & m ) {
+#if FD_DSM4_FUSED
+  fe y, a, sq, XX, YY, t, t2;
+  fe_bcast1( y, m );
+  fe_add_q0( t, m, y );                              /* X + Y */
+  fe_sel( a, q==3, t, m );                           /* X, Y, Z, X+Y */
+  fe_sqr( sq, a );
+  fe_bcast0( XX, sq ); fe_bcast1( YY, sq );
+  fe_add( H, YY, XX );                               /* H = YY+XX (L) */
+  fe_sub( G, YY, XX );                               /* G = YY-XX (L) */
+  fe_sub_q3( t, sq, H ); fe_addc( E, t, 1 ); fe_wcarry( E, E );   /* E = SS-H+4p = 2XY */
+  fe_csub4( t, G ); fe_add_q2( t2, sq, t ); fe_add_q2( F, sq, t2 ); fe_wcarry( F, F );   /* F = 2ZZ-G+4p */
+#else
   fe x, y, a, sq, XX, YY, ZZ, SS, t;
   fe_bcast0( x, m ); fe_bcast1( y, m );
   fe_add( t, x, y );
@@ -705,11 +766,27 @@ FD_DEV void quad_dbl( fe & E, fe & F, fe & G, fe & H, int q, fe const & m ) {
   fe_sub( G, YY, XX );                               /* G = YY-XX (L) */
   fe_sub4( E, SS, H ); fe_wcarry( E, E );            /* E = SS-H = 2XY */
   fe_add( t, ZZ, ZZ ); fe_sub4( F, t, G ); fe_wcarry( F, F );   /* F = 2ZZ-G */
+#endif
 }
 
 /* P + Q; lane q passes the coordinate of Q it multiplies by (Y2+X2,
    Y2-X2, 2dT2, Z2), already conditionally negated */
 FD_DEV void quad_add( fe & E, fe & F, fe & G, fe & H, int q, fe const & m, fe const & c ) {
+#if FD_DSM4_FUSED
+  fe x, w, a, b, u, n, B, C, D, D2, t;
+  fe_bcast0( x, m ); fe_swap23( w, m );              /* lane 2: T, lane 3: Z */
+  fe_add_q1( a, m, x );                              /* Y+X */
+  fe_subc( t, x ); fe_sub_q1( b, m, t );             /* Y-(X-2p) = Y-X+2p */
+  fe_sel( u, q==1, b, a );
+  fe_sel( u, q>=2, w, u );
+  fe_mul( n, u, c );
+  fe_bcast1( B, n );
+  fe_add_q0( H, n, B );                              /* H = A+B */
+  fe_subc( t, B ); fe_sub_q0( E, n, t );             /* E = A-(B-2p) = A-B+2p */
+  fe_bcast3( D, n ); fe_add_q3( D2, n, D );          /* D2 = 2 Z Z2 (L) */
+  fe_add_q2( G, n, D2 );                             /* G = D2+C */
+  fe_bcast2( C, n ); fe_sub4( F, D2, C ); fe_wcarry( F, F );        /* F = D2-C+4p */
+#else
   fe x, y, w, a, b, u, n, A, B, C, D;
   fe_bcast0( x, m ); fe_bcast1( y, m ); fe_swap23( w, m );   /* lane 2: T, lane 3: Z */
   fe_add( a, y, x );
@@ -723,6 +800,7 @@ FD_DEV void quad_add( fe & E, fe & F, fe & G, fe & H, int q, fe const & m, fe co
   fe_add( H, A, B );
   fe_add( G, D, C );
   fe_sub4( F, D, C ); fe_wcarry( F, F );
+#endif
 }
 
 __global__ void __launch_bounds__( FD_WG )
