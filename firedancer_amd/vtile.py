@@ -79,6 +79,7 @@ def load():
         L.fdgpu_vtile_during_frag.argtypes = [vp, vp, ul, ul, ul]
         L.fdgpu_vtile_flush.argtypes = [vp]
         L.fdgpu_vtile_housekeep.argtypes = [vp, ul]
+        L.fdgpu_vtile_housekeep.restype = ctypes.c_int
         L.fdgpu_vtile_after_frags.restype = ul
         L.fdgpu_vtile_after_frags.argtypes = [vp, ctypes.POINTER(Done), ul, ctypes.c_int]
         L.fdgpu_vtile_pending.restype = ul
@@ -154,6 +155,10 @@ class VTile:
 
     def flush(self):
         return self.L.fdgpu_vtile_flush(self.p)
+
+    def housekeep(self, max_inflight: int = 1) -> int:
+        """fdgpu_vtile_housekeep: adaptive batching (launch the filling batch when there is room)."""
+        return int(self.L.fdgpu_vtile_housekeep(self.p, max_inflight))
 
     def after_frags(self, max_n: int = 4096, blocking: bool = False):
         out = (Done * max_n)()

@@ -7,6 +7,7 @@ with valid / invalid signatures, parse failures, HA duplicates (incl.
 tcache eviction) and bundles with failing members."""
 import os
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -147,6 +148,69 @@ def test_vtile_vs_model(oracle, batch, depth, zero_copy):
     assert vt.metrics() == want_m
     assert bad == []
     assert sum(want_m[:4]) > 100 and want_m[2] > 10 and want_m[3] > 0
+    vt.close()
+    if zero_copy:
+        engine.host_unregister(buf)
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
+@pytest.mark.parametrize("nctx", [1, 2, 3])
+def test_vtile_multictx_vs_model(oracle, nctx, zero_copy):
+    """Adaptive batching over FDGPU_VTILE_CTX engine contexts (housekeep launches batches into the
+    contexts in turn, staggered): completions merged back into frag order must give exactly the
+    model's per-frag outcomes, metrics and published records."""
+    pytest.importorskip("xxhash")
+    from firedancer_amd import engine, vtile
+    frags = make_stream(seed=12)
+    seed, depth = 0x5eedbeef, 1 << 12
+    want_res, want_m, want_recs = model(oracle, frags, seed, depth)
+    old = os.environ.get("FDGPU_VTILE_CTX")
+    os.environ["FDGPU_VTILE_CTX"] = str(nctx)
+    try:
+        vt = vtile.VTile(device=0, batch_txn=128, tcache_depth=depth, seed=seed)
+    finally:
+        if old is None:
+            del os.environ["FDGPU_VTILE_CTX"]
+        else:
+            os.environ["FDGPU_VTILE_CTX"] = old
+    if zero_copy:
+        fbs = [vtile.frag_bytes(p, b) for p, b in frags]
+        buf, offs = in_dcache(fbs)
+        engine.host_register(buf)
+        assert vt.set_in_link(None) == 0
+    got, bad, launched = [], [], 0
+
+    def drain(blocking):
+        out = vt.after_frags(blocking=blocking)
+        for seq, r, chunk, sz, tag in out:
+            if r == vtile.PUBLISH:
+                head, timg = want_recs.get(seq, (b"", b""))
+                rec = vt.record(chunk, sz)
+                if rec[: len(head)] != head or rec[(len(head) + 1) & ~1:] != timg or sz != ((len(head) + 1) & ~1) + len(timg):
+                    bad.append(seq)
+        return out
+
+    for seq, (p, b) in enumerate(frags):
+        fb = vtile.frag_bytes(p, b)
+        while True:
+            rc = vt.during_frag_at(buf.ctypes.data + offs[seq], len(fb), seq) if zero_copy else vt.during_frag(fb, seq)
+            if rc != -2:
+                break
+            got += drain(True)
+        assert rc == 0, rc
+        if seq % 5 == 0:
+            launched += vt.housekeep(1)
+            time.sleep(3e-4)              # let batches finish between launches: many small staggered batches
+        if seq % 11 == 0:
+            got += drain(False)
+    vt.flush()
+    while vt.pending():
+        got += drain(True)
+    assert [g[0] for g in got] == list(range(len(frags)))
+    assert [g[1] for g in got] == want_res
+    assert vt.metrics() == want_m
+    assert bad == []
+    assert launched > 20
     vt.close()
     if zero_copy:
         engine.host_unregister(buf)
