@@ -38,6 +38,9 @@ MAC_PER_MUL, MAC_PER_SQR = 72, 44
 DSM_MUL, DSM_SQR = 1341, 1008          # wNAF DSM (1008 S + 1339 M) + eq (2 M)
 PREP_MUL, PREP_SQR = 38, 510           # decode of A and R: 2 x (255 S + 19 M)
 DSM_MAC = DSM_MUL * MAC_PER_MUL + DSM_SQR * MAC_PER_SQR
+# MI355X_MICROARCH.md: 157.3 TF FP32 vector FMA = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz x 2 flops, i.e. a
+# wave64 VALU instruction issues in 2 cycles per SIMD: 78.6 T lane-instructions/s for the whole chip
+GUIDE_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
 PREP_MAC = PREP_MUL * MAC_PER_MUL + PREP_SQR * MAC_PER_SQR
 
 
@@ -51,8 +54,24 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def usable_cores() -> tuple[int, dict]:
+    """Host cores this process may use: its affinity mask, capped by a cgroup CPU quota if one is set
+    (the GPU box's share of a larger host)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(quota)))
+    return n, {"affinity": aff, "cgroup_quota": quota}
+
+
 def cpu_baseline(payload, desc, nsig_total, threads, target_s=1.5):
-    """Time the reference (or the port) on a bounded prefix of the same workload."""
+    """Time the reference (or the port) on a bounded prefix of the same workload, every signature verified
+    once (fd_txn_verify's batch call; no separate per-signature pass)."""
     from oracle.oracle import Oracle, Reference, cpu_has_avx512_ifma
     kind, impl = "port", None
     ref_path = os.path.join(ROOT, "oracle", "_ref", "libfdref_avx512.so")
@@ -60,65 +79,158 @@ def cpu_baseline(payload, desc, nsig_total, threads, target_s=1.5):
         impl, kind = Reference("avx512"), "reference"
     else:
         impl = Oracle()
-    # calibrate on a small prefix, then size the sample for ~target_s wall (~10-30 CPU-s)
-    def run(n):
+
+    def run(n, t):
         d = desc[:n]
         ns = int(d["sig_cnt"].astype(np.int64).sum())
         t0 = time.perf_counter()
         if kind == "reference":
-            out, _ = impl.verify_txns(payload, d, ns, threads=threads)
+            out, _ = impl.verify_txns(payload, d, ns, threads=t, want_sig_codes=False)
         else:
-            out, _ = impl.verify_txns(payload, d, ns, threads=threads)
+            out, _ = impl.verify_txns(payload, d, ns, threads=t)
         return time.perf_counter() - t0, ns, out
-    dt, ns, _ = run(min(len(desc), 2048 * threads))
+    # calibrate on a small prefix, then size the sample for ~target_s wall (~10-30 CPU-s)
+    dt, ns, _ = run(min(len(desc), 2048 * threads), threads)
     rate = ns / dt
     n = int(min(len(desc), max(2048 * threads, rate * target_s)))
-    dt, ns, out = run(n)
+    dt, ns, out = run(n, threads)
     assert (out == 0).all(), "CPU baseline rejected valid signatures"
     return {"value": ns / dt, "unit": "sigs/s", "cores": threads, "kind": kind,
             "sample": f"first {n} txns ({ns} sigs) of the same 1232-byte workload, {threads} threads, "
                       f"{dt:.2f} s wall; host CPU: {cpu_model()}",
             "impl": "reference fd_ed25519_verify_batch_single_msg, AVX-512 r43x6 build (oracle/_ref)"
-                    if kind == "reference" else "oracle/fd_ed25519_oracle.c portable C restatement"}
+                    if kind == "reference" else "oracle/fd_ed25519_oracle.c portable C restatement"}, impl, kind
 
 
+def cpu_sweep_configs0(impl, kind, max_threads, gen_threads, point_s=0.6):
+    """BASELINE configs[0] on the host: 64K single-signature txns with 200-byte messages, all valid, the
+    reference timed at 1, 2, 4, ... up to max_threads threads (SURVEY.md §6 measured 29.8K/s on 1 thread and
+    211K/s on 8 of the survey box).  Each point is a bounded prefix sized to ~point_s of wall time."""
+    from firedancer_amd import synth
+    payload, desc, _, nsig = synth.make_batch(1 << 16, synth.SMALL_MSG, seed=77, threads=gen_threads)
+    ts = sorted({t for t in (1, 2, 4, 8, 16, 32, 64, 128) if t <= max_threads} | {max_threads})
+    pts = []
+    for t in ts:
+        n = min(len(desc), 512 * t)
+        for _ in range(2):          # calibrate, then the sized run
+            t0 = time.perf_counter()
+            if kind == "reference":
+                out, _ = impl.verify_txns(payload, desc[:n], n, threads=t, want_sig_codes=False)
+            else:
+                out, _ = impl.verify_txns(payload, desc[:n], n, threads=t)
+            dt = time.perf_counter() - t0
+            assert (out == 0).all()
+            rate = n / dt
+            n2 = int(min(len(desc), max(512 * t, rate * point_s)))
+            if n2 <= n:
+                break
+            n = n2
+        pts.append({"threads": t, "sigs_per_s": rate, "sigs": n})
+    return {"workload": "BASELINE configs[0]: 65,536 single-sig txns, 200-byte messages, all valid",
+            "points": pts}
 
-def stream_runs(args, payload, desc, dev) -> dict:
-    """BASELINE configs[4]: the payloads streamed through GPU verify tiles (tango mcache/dcache in,
-    fd_txn_parse + verify on the GPU, in-order after_frag, out dcache): a calibration run, then
-    --stream-seconds at the maximum rate on --stream-tiles tiles, then paced on --stream-lat-tiles."""
-    from firedancer_amd import vtile
-    off, psz = desc["payload_off"], desc["payload_sz"]
-    zc = not args.stream_copy
-    kw = dict(batch_txn=args.stream_batch, max_inflight=args.stream_inflight, mcache_depth=1 << 18,
-              zero_copy=zc, device=dev)
-    if args.stream_frags > 0:
-        n_max = n_pace = args.stream_frags
-    else:
-        cal = vtile.stream_bench(payload, off, psz, n_frags=2_000_000, tiles=args.stream_tiles, **kw)
-        n_max = int(1.2 * cal["frags_per_s"] * args.stream_seconds)   # short runs under-read the rate
-        n_pace = int(args.stream_rate * args.stream_seconds)
-    smax = vtile.stream_bench(payload, off, psz, n_frags=n_max, tiles=args.stream_tiles, **kw)
-    slat = vtile.stream_bench(payload, off, psz, n_frags=n_pace, tiles=args.stream_lat_tiles,
-                              rate_fps=args.stream_rate, **kw)
-    return {"smax": smax, "slat": slat, "n_max": n_max, "n_pace": n_pace}
+
+# ---- BASELINE configs[4]: the verify stage as the reference wires it ------------------------------------
+# One producer link (mcache + in dcache) read by T = tiles_per_gpu x G verify tiles; tile i takes
+# seq % T == i (before_frag, fd_verify_tile.c:47-48) and drives GPU i % G from that GPU's process.  With
+# G > 1 the link lives in a /dev/shm file that rank 0's child creates and the other ranks' children join.
+
+STREAM_LEGS = ("cal", "max", "paced", "unrel")
+
+
+def _leg_cfg(args, leg, procs, cal_fps):
+    T, Tl = args.stream_tiles * procs, args.stream_lat_tiles * procs
+    base = dict(batch_txn=args.stream_batch, max_inflight=args.stream_inflight, zero_copy=not args.stream_copy,
+                gpus=procs, mcache_depth=1 << 18)
+    if leg == "cal":
+        return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
+                    rate_fps=0.0, reliable=True)
+    if leg == "max":            # credit-based: the sustained rate with no frag lost
+        n = args.stream_frags if args.stream_frags > 0 else int(1.2 * cal_fps * args.stream_seconds)
+        return dict(base, tiles=T, n_frags=n, rate_fps=0.0, reliable=True)
+    if leg == "paced":          # the reference's unreliable link at a fixed offered load
+        rate = args.stream_rate * procs
+        n = args.stream_frags if args.stream_frags > 0 else int(rate * args.stream_seconds)
+        return dict(base, tiles=Tl, n_frags=n, rate_fps=rate, reliable=False)
+    # unreliable, producer unthrottled: tiles that fall a lap behind are overrun and skip frags
+    n = args.stream_frags if args.stream_frags > 0 else int(cal_fps * args.stream_unrel_seconds)
+    return dict(base, tiles=T, n_frags=n, rate_fps=0.0, reliable=False)
+
+
+def _leg_summary(st: dict, cfg: dict) -> dict:
+    n = max(st["verdicts"], 1)
+    hist = st["gpu_lat_hist"]
+    tot = sum(hist)
+
+    def hq(q):   # GPU batch latency quantile from the log2 histogram: bucket upper edge, us
+        c = 0
+        for i, h in enumerate(hist):
+            c += h
+            if tot and c > q * tot:
+                return float(2 ** (i + 1))
+        return None
+    return {"tiles": cfg["tiles"], "gpus": cfg["gpus"], "reliable": bool(cfg["reliable"]),
+            "rate_fps": cfg["rate_fps"] or None, "frags": st["frags"], "verdicts": st["verdicts"],
+            "lost": st["lost"], "overruns_at_verdict": st["overruns"],
+            "lost_per_frag": st["lost"] / max(st["frags"], 1),
+            "seconds": st["seconds"], "frags_per_s": st["frags_per_s"], "sigs_per_s": st["sigs_per_s"],
+            "p50_us": st["lat_p50_us"], "p99_us": st["lat_p99_us"], "max_us": st["lat_max_us"],
+            "published": st["published"], "metrics": st["metrics"],
+            "tile_host_ns_per_frag": [round(x / n, 1) for x in st["tile_ns"]],
+            "batches": st["batches"], "mean_batch_txns": st["batch_txns"] / max(st["batches"], 1),
+            "inflight_max": st["inflight_max"], "gpu_batch_lat_p50_us_le": hq(0.5),
+            "gpu_batch_lat_p99_us_le": hq(0.99)}
 
 
 def stream_child_main(args) -> None:
-    """--stream-child: regenerate this rank's workload (same seed) and run the stream legs; no torch GPU context."""
-    from firedancer_amd import synth
-    payload, desc, _, _ = synth.make_batch(args.txns, synth.LARGE_NOOP, seed=args.stream_seed,
-                                           threads=min(16, os.cpu_count() or 1))
-    print(json.dumps(stream_runs(args, payload, desc, args.stream_device)), flush=True)
+    """--stream-child: the configs[4] legs for one process (one GPU); no torch GPU context here.  Process 0
+    regenerates the payloads (same seed), creates each leg's link and runs the producer; the others join."""
+    from firedancer_amd import vtile
+    proc, procs, dev = args.stream_proc, args.stream_procs, args.stream_device
+    out, cal_fps = {}, 0.0
+    payload = desc = None
+    if proc == 0:
+        from firedancer_amd import synth
+        payload, desc, _, _ = synth.make_batch(args.txns, synth.LARGE_NOOP, seed=args.stream_seed,
+                                               threads=min(16, os.cpu_count() or 1))
+    for leg in STREAM_LEGS:
+        path = f"/dev/shm/fdgpu_link_{args.stream_token}_{leg}" if procs > 1 else None
+        if proc == 0:
+            cfg = _leg_cfg(args, leg, procs, cal_fps)
+            link = vtile.Link(path, create=True, payload=payload, off=desc["payload_off"], sz=desc["payload_sz"], **cfg)
+            try:
+                rc = link.run(0, dev, True)
+                if rc:
+                    raise RuntimeError(f"leg {leg}: fdgpu_link_run {rc}")
+                st = link.result(timeout_s=120.0)
+            finally:
+                link.close()
+                if path and os.path.exists(path):
+                    os.unlink(path)
+            if leg == "cal":
+                cal_fps = st["frags_per_s"]
+            else:
+                out[leg] = _leg_summary(st, cfg)
+        else:
+            link = vtile.Link(path, create=False, timeout_s=600.0 if leg == "cal" else 300.0)
+            try:
+                rc = link.run(proc, dev, False)
+            finally:
+                link.close()
+            if rc:
+                raise RuntimeError(f"leg {leg}: fdgpu_link_run {rc} (process {proc})")
+    print(json.dumps({"legs": out, "cal_frags_per_s": cal_fps}), flush=True)
 
 
-def run_stream_child(args, dev, seed, n) -> dict:
+def run_stream_child(args, dev, proc, procs, token) -> dict:
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--stream-child", "--stream-device", str(dev),
-           "--stream-seed", str(seed), "--txns", str(n), "--stream-frags", str(args.stream_frags),
-           "--stream-seconds", str(args.stream_seconds), "--stream-tiles", str(args.stream_tiles),
-           "--stream-batch", str(args.stream_batch), "--stream-rate", str(args.stream_rate),
-           "--stream-lat-tiles", str(args.stream_lat_tiles), "--stream-inflight", str(args.stream_inflight)]
+           "--stream-proc", str(proc), "--stream-procs", str(procs), "--stream-token", token,
+           "--stream-seed", "1234", "--txns", str(args.txns), "--stream-frags", str(args.stream_frags),
+           "--stream-seconds", str(args.stream_seconds), "--stream-unrel-seconds", str(args.stream_unrel_seconds),
+           "--stream-tiles", str(args.stream_tiles), "--stream-batch", str(args.stream_batch),
+           "--stream-rate", str(args.stream_rate), "--stream-lat-tiles", str(args.stream_lat_tiles),
+           "--stream-inflight", str(args.stream_inflight)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -137,11 +249,13 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-batch", type=int, default=8192)
     ap.add_argument("--stream-frags", type=int, default=-1,
-                    help="BASELINE configs[4]: frags per stream run through the GPU verify tiles "
-                         "(0 = skip; default: sized to --stream-seconds from a short calibration run)")
+                    help="BASELINE configs[4]: frags per stream leg (0 = skip the stream; default: sized to "
+                         "--stream-seconds from a short calibration leg)")
     ap.add_argument("--stream-seconds", type=float, default=10.0,
-                    help="sustained length of each stream run (max rate, then paced)")
-    ap.add_argument("--stream-tiles", type=int, default=6)
+                    help="sustained length of the reliable max-rate leg and of the paced leg")
+    ap.add_argument("--stream-unrel-seconds", type=float, default=4.0,
+                    help="frags of the unreliable unthrottled leg, in seconds of the calibrated rate")
+    ap.add_argument("--stream-tiles", type=int, default=6, help="verify tiles per GPU (max-rate legs)")
     ap.add_argument("--stream-copy", action="store_true",
                     help="stream tiles copy each frag into the out dcache on the host (the reference tile's "
                          "during_frag) instead of the zero-copy intake (GPU gathers from the registered in dcache)")
@@ -149,14 +263,17 @@ def main():
     ap.add_argument("--stream-inflight", type=int, default=1,
                     help="batches a tile keeps launched on its GPU stream before it launches the filling one "
                          "(1: a frag waits for at most the running batch; tools/stream_sweep.py, s13)")
-    ap.add_argument("--stream-rate", type=float, default=2e6, help="paced rate (frags/s) of the latency run")
+    ap.add_argument("--stream-rate", type=float, default=2e6, help="paced leg: offered frags/s per GPU")
     ap.add_argument("--stream-lat-tiles", type=int, default=2,
-                    help="verify tiles of the paced latency run (fewer tiles = fewer HIP streams sharing the "
+                    help="verify tiles per GPU of the paced leg (fewer tiles = fewer HIP streams sharing the "
                          "device's hardware queues; 2 tiles carry 2M frags/s)")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="skip the BASELINE configs[0,2,3] side measurements (small / adversarial / multi-sig)")
     ap.add_argument("--stream-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--stream-device", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--stream-proc", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--stream-procs", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--stream-token", default="x", help=argparse.SUPPRESS)
     ap.add_argument("--stream-seed", type=int, default=1234, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.stream_child:
@@ -169,17 +286,14 @@ def main():
 
     env = shard.dist_env()
     world, rank, local_rank = env.world, env.rank, env.local_rank
-    # rehearsal knobs for the N>1 flow on a one-GPU box: FDGPU_BENCH_BACKEND=gloo (collectives on CPU
-    # tensors) and FDGPU_BENCH_ONE_DEVICE=1 (every rank on GPU 0).  The driver's runs use neither.
-    backend = os.environ.get("FDGPU_BENCH_BACKEND", "nccl")
+    # rehearsal knob for the N>1 flow on a one-GPU box: FDGPU_BENCH_ONE_DEVICE=1 puts every rank on GPU 0
     dev = 0 if os.environ.get("FDGPU_BENCH_ONE_DEVICE") == "1" else local_rank
-    red_dev = "cuda" if backend == "nccl" else "cpu"
     torch.cuda.set_device(dev)
+    # The data path has no collective (independent shards); the measurement reductions (MAX of time, MIN of
+    # the results flag, SUM of signatures) are a few scalars, so they go over gloo on CPU tensors: no RCCL.
     if world > 1:
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(backend)
+        dist.init_process_group("gloo")
+    dd = dist if world > 1 else None
 
     def barrier():
         if world > 1:
@@ -211,7 +325,7 @@ def main():
 
     got = out_d.cpu().numpy()
     ok = bool(np.array_equal(got, expect))
-    dt_max, all_ok = shard.reduce_max_min(dist if world > 1 else None, dt, ok, red_dev)
+    dt_max, all_ok = shard.reduce_max_min(dd, dt, ok, "cpu")
 
     # BASELINE configs[0] / [2] / [3] on the same device path, rank 0 only:
     # throughput with HBM-resident input plus a check of every result code
@@ -289,46 +403,73 @@ def main():
                               "one direct H2D DMA, no staging copy",
                "samples": len(times)}
 
+    # configs[1] from host memory: the whole 1M-txn batch handed over in a pinned host buffer each step
+    # (chunked H2D on a copy stream overlapped with the kernels, fdgpu_ed25519_verify_txns_host) --
+    # the PCIe-inclusive rate, next to the HBM-resident headline
+    host_staged = None
+    if rank == 0 and not args.no_extra_configs:
+        from firedancer_amd import engine as _engine
+        heng = Engine(device=dev, max_txn=n, max_sig=nsig, max_payload=payload.nbytes)
+        hpay = np.array(payload, copy=True)
+        _engine.host_register(hpay)
+        try:
+            heng.verify_txns_host(hpay, desc, want_sig_codes=False)
+            hts = []
+            for _ in range(5):
+                t1 = time.perf_counter()
+                ho, _ = heng.verify_txns_host(hpay, desc, want_sig_codes=False)
+                hts.append(time.perf_counter() - t1)
+            hok = bool(np.array_equal(ho, expect))
+        finally:
+            _engine.host_unregister(hpay)
+        heng.close()
+        host_staged = {"sigs_per_s": nsig / float(np.median(hts)), "ms_per_batch": 1e3 * float(np.median(hts)),
+                       "batch_txns": n, "bytes_per_batch": int(payload.nbytes), "results_ok": hok,
+                       "path": "payload in a registered (pinned) host buffer -> H2D in 1-MB chunks on a copy stream, "
+                               "kernels on the compute stream, verdicts D2H; synchronous per batch"}
+
     eng.close()     # the headline context's stream is idle from here: free it before the tiles open theirs
-    # BASELINE configs[4]: the same payloads streamed through GPU verify tiles
-    # (tango mcache/dcache in, fd_txn_parse + verify on the GPU, in-order
-    # after_frag, out dcache).  Every rank streams its own shard at once.
+    # BASELINE configs[4]: the same 1232-byte payloads through the verify stage as the reference wires it
+    # (one producer link, T = tiles x G verify tiles, tile i -> GPU i % G), in a child process per GPU that
+    # never initialises torch's GPU context: a verify tile is a plain C process, and torch's context in this
+    # one measurably inflates the tiles' tail latency (tools/stream_seq.py, TORCH=1: paced p99 1.2 -> 2.2 ms).
     stream = None
     if args.stream_frags != 0:
-        # The tiles run in a child process that never initialises torch's GPU context: a verify tile is a
-        # plain C process, and torch's context in this one measurably inflates the tiles' tail latency
-        # (tools/stream_seq.py, TORCH=1: paced p99 1.2 -> 2.2 ms).  Every rank streams its own shard at once.
         barrier()
-        zc = not args.stream_copy
+        token = f"{os.getpid()}_{int(time.time())}" if rank == 0 else ""
+        if world > 1:
+            obj = [token]
+            dist.broadcast_object_list(obj, src=0)
+            token = obj[0]
+        res, err = None, None
         try:
-            res = run_stream_child(args, dev, shard.shard_seed(1234, rank), n)
+            res = run_stream_child(args, dev, rank, world, token)
         except Exception as e:      # keep the headline line even if the stream leg fails
-            res = None
-            stream = {"error": str(e)[-2000:]}
-        barrier()
-        if res is not None:
-            smax, slat, n_max, n_pace = res["smax"], res["slat"], res["n_max"], res["n_pace"]
-            ok_s = (smax["metrics"][:4] == [0, 0, 0, 0] and smax["published"] == n_max
-                    and slat["metrics"][:4] == [0, 0, 0, 0] and slat["published"] == n_pace)
-            sig_tot, t_max, _ = shard.reduce_sum_max(dist if world > 1 else None, smax["sigs"], smax["seconds"], red_dev)
-            stream = {"workload": "BASELINE configs[4]: 1232-byte txns through mcache/dcache -> GPU verify tiles "
-                                  "(device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> out dcache",
-                      "sigs_per_s": sig_tot / t_max, "per_gpu_sigs_per_s": smax["sigs_per_s"], "n_gpus": world,
-                      "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch,
-                      "max_inflight": args.stream_inflight,
-                      "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
-                      "process": "tiles in a child process without a torch GPU context (as a C verify tile)",
-                      "intake": "zero-copy (GPU gathers frags from the registered in dcache)" if zc
-                                else "host copy into the out dcache (reference during_frag)",
-                      "max_rate": {"frags": n_max, "seconds": smax["seconds"], "p50_us": smax["lat_p50_us"],
-                                   "p99_us": smax["lat_p99_us"], "tile_host_ns_per_frag":
-                                       [round(x / max(n_max, 1), 1) for x in smax["tile_ns"]]},
-                      "paced": {"frags": n_pace, "seconds": slat["seconds"], "rate_frags_per_s": args.stream_rate,
-                                "tiles_per_gpu": args.stream_lat_tiles,
-                                "achieved": slat["frags_per_s"], "p50_us": slat["lat_p50_us"],
-                                "p99_us": slat["lat_p99_us"], "max_us": slat["lat_max_us"]},
-                      "all_published": bool(ok_s),
-                      "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
+            err = str(e)[-2000:]
+        # every rank takes part in the same collective, whatever happened locally
+        _, stream_ok = shard.reduce_max_min(dd, 0.0, err is None, "cpu")
+        if rank == 0:
+            if res is not None and stream_ok:
+                legs = res["legs"]
+                mx, pc, ur = legs["max"], legs["paced"], legs["unrel"]
+                ok_s = (mx["metrics"][:4] == [0, 0, 0, 0] and mx["published"] == mx["frags"] and mx["lost"] == 0
+                        and pc["metrics"][:4] == [0, 0, 0, 0])
+                stream = {"workload": "BASELINE configs[4]: 1232-byte txns, one producer mcache/dcache link -> "
+                                      "T verify tiles (seq % T round robin, tile i -> GPU i % G; device fd_txn_parse "
+                                      "+ verify, in-order after_frag, dedup tcache) -> out dcache",
+                          "sigs_per_s": mx["sigs_per_s"], "per_gpu_sigs_per_s": mx["sigs_per_s"] / world,
+                          "n_gpus": world, "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch,
+                          "max_inflight": args.stream_inflight,
+                          "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
+                          "process": "one tile process per GPU without a torch GPU context (as a C verify tile); "
+                                     "link in /dev/shm when G > 1",
+                          "intake": "zero-copy (GPU gathers frags from the registered in dcache)"
+                                    if not args.stream_copy else "host copy into the out dcache (reference during_frag)",
+                          "max_rate": mx, "paced": pc, "unreliable_max": ur,
+                          "all_published": bool(ok_s),
+                          "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
+            else:
+                stream = {"error": err or "a stream child failed on another rank"}
 
     if lat is not None:
         # after the stream leg: the drop-in's process-wide context (and its stream) lives until exit
@@ -356,9 +497,10 @@ def main():
     L.fdgpu_mad_peak_per_s.argtypes = [ctypes.c_int]
     my_peak = max(float(L.fdgpu_mad_peak_per_s(dev)) for _ in range(3))
     my_ach = DSM_MAC * nsig / (ms_dsm * 1e-3)
-    rows = shard.gather_rows(dist if world > 1 else None, [rank, ms_dsm, ms_prep, my_ach, my_peak, dt], red_dev)
+    rows = shard.gather_rows(dd, [rank, ms_dsm, ms_prep, my_ach, my_peak, dt], "cpu")
     per_gpu = [{"rank": int(r[0]), "dsm_ms": r[1], "prep_ms": r[2], "achieved_gmac_s": r[3] / 1e9,
                 "peak_gmac_s": r[4] / 1e9, "frac": r[3] / r[4] if r[4] > 0 else None,
+                "frac_guide": r[3] / GUIDE_VALU_LANE_OPS if r[3] > 0 else None,
                 "sigs_per_s": nsig * args.steps / r[5]} for r in rows]
 
     if rank == 0:
@@ -376,7 +518,10 @@ def main():
                 traffic = None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(payload, desc, nsig, threads=gen_threads)
+            cores, core_src = usable_cores()
+            cpu, impl, kind = cpu_baseline(payload, desc, nsig, threads=cores)
+            cpu["cores_source"] = dict(core_src, used=cores)
+            cpu["sweep_configs0"] = cpu_sweep_configs0(impl, kind, cores, gen_threads)
         value = shard.aggregate_rate(world, nsig, args.steps, dt_max)
         rec = {
             "metric": "ed25519 verified sigs/sec at 1/8 MI355X vs host AVX-512; p99 batch latency",
@@ -402,8 +547,15 @@ def main():
                          "work_per_sig": f"{DSM_MAC} v_mad_u64_u32 (1008 S + 1341 M of the reference wNAF DSM, "
                                          f"S=44 M=72 MAC)",
                          "peak_source": "fdgpu_mad_peak_per_s: measured v_mad_u64_u32 throughput, this device (max of 3)",
+                         # the same achieved rate against MI355X_MICROARCH.md's VALU issue rate (157.3 TF FP32
+                         # vector = 78.6 T wave64 lane-instructions/s), one MAC priced as one lane-instruction
+                         "peak_guide": GUIDE_VALU_LANE_OPS / 1e9,
+                         "frac_guide": achieved / GUIDE_VALU_LANE_OPS,
+                         "peak_guide_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T "
+                                              "lane-ops/s (157.3 TF FP32 FMA / 2); profiles/r02/ROOFLINE.md",
                          "valu_busy": valu_busy,
-                         "valu_busy_source": "profiles/dsm_pmc.json: SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE/8)",
+                         "valu_busy_source": "profiles/dsm_pmc.json (see profiles/r02/ROOFLINE.md for the measured "
+                                             "per-instruction cost form)",
                          # the same kernel against the HBM roofline: PMC bytes per launch / this run's launch time
                          "hbm": ({"achieved": traffic * nsig / (1 << 20) / (dom_ms * 1e-3) / 1e9, "peak": 8000.0,
                                   "unit": "GB/s",
@@ -414,6 +566,7 @@ def main():
             "cpu_baseline": cpu,
             "per_gpu": per_gpu,
             "latency": lat,
+            "host_staged": host_staged,
             "stream": stream,
             "extra_configs": extra,
             "gen_s": t_gen,

@@ -81,6 +81,8 @@
 #define FD_DSM4_MAX 16384UL          /* latency path: four lanes per signature up to here, then two */
 #endif
 #define FD_STAGE_CHUNK ( 1UL << 20 )   /* host-staged batches: bytes per memcpy / H2D step */
+#define FD_PIPE_SUB    ( 1UL << 17 )   /* host batches of >= 2 FD_PIPE_SUB txns: sub-batches overlap H2D and kernels */
+#define FD_PIPE_MAX    16UL
 #define FD_PEND_ASMALL 2           /* per-signature code in flight: A small order, R's decode picks ERR_SIG / ERR_PUBKEY */
 #define FD_PEND_REQ    3           /* per-signature code in flight: P's encoding != R's bytes -> decode R, compare */
 
@@ -290,7 +292,8 @@ FD_DEV int result_code( int code, u32 pa, u32 pr, int semantics, int defer ) {
 FD_DEV void hash_one( unsigned char const * __restrict__ payload, fdgpu_txn_desc_t const * __restrict__ desc,
                       u32 const * __restrict__ map, u32 s, size_t n, int semantics, int defer,
                       unsigned char const * __restrict__ pstat, i8 * __restrict__ code_out,
-                      i8 * __restrict__ digA, short * __restrict__ digB, uint4 * __restrict__ Rraw ) {
+                      i8 * __restrict__ digA, short * __restrict__ digB, uint4 * __restrict__ Rraw,
+                      uint4 const * __restrict__ khash ) {
   u32 m = map[s];
   u32 t = m & 0xffffffu, j = m >> 24;
   fdgpu_txn_desc_t d = desc[t];
@@ -312,7 +315,10 @@ FD_DEV void hash_one( unsigned char const * __restrict__ payload, fdgpu_txn_desc
   }
   fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
   u32 h[16], k[8];
-  fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
+  if( khash ) {                                  /* digest computed beforehand (messages beyond the descriptor range) */
+#pragma unroll
+    for( int i=0; i<4; i++ ) { uint4 v = khash[4*(size_t)s + i]; h[4*i] = v.x; h[4*i+1] = v.y; h[4*i+2] = v.z; h[4*i+3] = v.w; }
+  } else fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
   sc_reduce( k, h );
   store_digits( k, Sw, s, n, digA, digB );
 }
@@ -328,17 +334,18 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
                 i8 *                     __restrict__ code_out,
                 i8 *                     __restrict__ digA,
                 short *                  __restrict__ digB,
-                uint4 *                  __restrict__ Rraw ) {
+                uint4 *                  __restrict__ Rraw,
+                uint4 const *            __restrict__ khash ) {
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
   if( !defer ) {                                 /* FD_DEFER_R=0 builds: both points decoded already */
-    hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rraw );
+    hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rraw, khash );
     int c = code_out[s];
     if( c==FD_ED25519_SUCCESS || c==FD_ED25519_ERR_SIG )
       code_out[s] = (i8)result_code( c, pstat[2*s], pstat[2*s+1], semantics, 0 );
     return;
   }
-  hash_one( payload, desc, map, s, nsig, semantics, 1, pstat, code_out, digA, digB, Rraw );
+  hash_one( payload, desc, map, s, nsig, semantics, 1, pstat, code_out, digA, digB, Rraw, khash );
 }
 
 /* Small batches (latency): the three independent parts of the prep in
@@ -359,7 +366,8 @@ fd_prep_kernel( unsigned char const *    __restrict__ payload,
                 i8 *                     __restrict__ code_out,
                 i8 *                     __restrict__ digA,
                 short *                  __restrict__ digB,
-                uint4 *                  __restrict__ tab ) {
+                uint4 *                  __restrict__ tab,
+                uint4 const *            __restrict__ khash ) {
   u32 role = blockIdx.x / sg, b = blockIdx.x - role*sg;
   u32 s = b * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
@@ -369,7 +377,7 @@ fd_prep_kernel( unsigned char const *    __restrict__ payload,
        decoded; fd_dsm2_kernel applies the result-code procedure) */
     if( tab && role==0u && ( pstat[2u*s] & 3u )==0u ) atab_build( tab, s, Axy );
   }
-  else hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rxy );
+  else hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rxy, khash );
 }
 
 /* Stage 3 -- table [0..8](-A) in cached form (fd_ed25519_point_neg + the
@@ -1049,6 +1057,31 @@ fd_reduce_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 n
    pflag makes the reduce kernel report FDGPU_ERR_PARSE.  A parsed
    transaction with more than 16 signatures gets sig_cnt = 0 (no lanes;
    the reduce kernel's batch-size rule gives ERR_SIG). */
+/* XXH64 (the published algorithm) of the 64 bytes at p, seed: the HA
+   dedup tag fd_txn_verify computes on the host, fd_hash( seed, sig0, 64 )
+   (src/disco/verify/fd_verify_tile.h:79, src/util/fd_hash.c) */
+#define FD_XXP1 0x9E3779B185EBCA87UL
+#define FD_XXP2 0xC2B2AE3D27D4EB4FUL
+#define FD_XXP3 0x165667B19E3779F9UL
+#define FD_XXP4 0x85EBCA77C2B2AE63UL
+FD_DEV u64 fd_rotl64( u64 x, int r ) { return (x << r) | (x >> (64 - r)); }
+FD_DEV u64 fd_xxh_round( u64 acc, u64 in ) { acc += in * FD_XXP2; acc = fd_rotl64( acc, 31 ); return acc * FD_XXP1; }
+FD_DEV u64 fd_xxh64_64( u64 seed, unsigned char const * p ) {
+  u32 w[16];
+  fd_load_words<16>( w, p );
+  u64 v[4] = { seed + FD_XXP1 + FD_XXP2, seed + FD_XXP2, seed, seed - FD_XXP1 };
+#pragma unroll
+  for( int blk=0; blk<2; blk++ )
+#pragma unroll
+    for( int i=0; i<4; i++ ) v[i] = fd_xxh_round( v[i], ((u64)w[8*blk + 2*i + 1] << 32) | (u64)w[8*blk + 2*i] );
+  u64 h = fd_rotl64( v[0], 1 ) + fd_rotl64( v[1], 7 ) + fd_rotl64( v[2], 12 ) + fd_rotl64( v[3], 18 );
+#pragma unroll
+  for( int i=0; i<4; i++ ) { h ^= fd_xxh_round( 0UL, v[i] ); h = h * FD_XXP1 + FD_XXP4; }
+  h += 64UL;
+  h ^= h >> 33; h *= FD_XXP2; h ^= h >> 29; h *= FD_XXP3; h ^= h >> 32;
+  return h;
+}
+
 __global__ void __launch_bounds__( FD_WG )
 fd_parse_kernel( unsigned char const *    __restrict__ payload,
                  fdgpu_txn_raw_t const *  __restrict__ raw,
@@ -1057,7 +1090,9 @@ fd_parse_kernel( unsigned char const *    __restrict__ payload,
                  unsigned char *          __restrict__ pflag,
                  unsigned char *          __restrict__ img,
                  u32                                    img_stride,
-                 unsigned short *         __restrict__ fp_out ) {
+                 unsigned short *         __restrict__ fp_out,
+                 u64                                    dedup_seed,
+                 u64 *                    __restrict__ dtag_out ) {
   u32 t = blockIdx.x * FD_WG + threadIdx.x;
   if( t >= txn_cnt ) return;
   fdgpu_txn_raw_t r = raw[t];
@@ -1065,6 +1100,9 @@ fd_parse_kernel( unsigned char const *    __restrict__ payload,
   u32 fp = fd_txn_parse_dev( payload + r.payload_off, (u32)r.payload_sz,
                              img ? img + (size_t)t*img_stride : (unsigned char *)0, h );
   if( fp_out ) fp_out[t] = (unsigned short)fp;
+  /* the HA dedup tag of a parsed transaction (its first signature), so the
+     tile's after_frag never reads the payload */
+  if( dtag_out ) dtag_out[t] = fp ? fd_xxh64_64( dedup_seed, payload + r.payload_off + h.sig_off ) : 0UL;
   if( !desc_out ) return;
   fdgpu_txn_desc_t d;
   d.payload_off = r.payload_off; d.sig_base = r.sig_base;
@@ -1145,11 +1183,14 @@ fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__
    fd_verify_tile.c:131-134), in 2-byte stores of one 64-lane group. */
 __global__ void __launch_bounds__( 64 )
 fd_img_scatter_kernel( fdgpu_txn_raw_t const * __restrict__ raw, unsigned char const * __restrict__ img, u32 stride,
-                       unsigned short const * __restrict__ fp, unsigned char * __restrict__ out ) {
+                       unsigned short const * __restrict__ fp, unsigned char * __restrict__ out, int rec_fp_off ) {
   u32 t = blockIdx.x;
   u32 n = fp[t];
   fdgpu_txn_raw_t r = raw[t];
   unsigned char * dst = out + ( ( r.payload_off + (u32)r.payload_sz + 1u ) & ~1u );
+  /* the footprint into the record header too (fd_txn_m_t txn_t_sz): _pad[0] = the payload's offset in its record */
+  if( rec_fp_off >= 0 && threadIdx.x==0u )
+    *(unsigned short *)( out + r.payload_off - (u32)r._pad[0] + (u32)rec_fp_off ) = (unsigned short)n;
   unsigned short const * s16 = (unsigned short const *)( img + (size_t)t*stride );
   for( u32 i=threadIdx.x; i<(n >> 1); i+=64u ) ((unsigned short *)dst)[i] = s16[i];
   if( ( n & 1u ) && threadIdx.x==0u ) dst[n-1u] = img[(size_t)t*stride + n - 1u];
@@ -1174,6 +1215,8 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   fdgpu_txn_desc_t * d_desc;
   i8 *               d_txn_out;
   unsigned short *   h_fp;     /* raw mode: footprints + fd_txn_t images (allocated on first raw use) */
+  unsigned long *    h_dtag;   /* raw mode, dedup tags on: XXH64 of each parsed transaction's first signature */
+  unsigned long *    d_dtag;
   unsigned char *    h_img;
   unsigned short *   d_fp;
   unsigned char *    d_img;
@@ -1196,6 +1239,8 @@ struct fdgpu_ed25519_ctx {
   int device, semantics, timing;
   unsigned long max_txn, max_sig, max_payload;
   hipStream_t stream;
+  hipStream_t cstream;           /* copy stream of large host batches (verify_host_pipelined) */
+  hipEvent_t  pipe_ev[ FD_PIPE_MAX ];
   /* scratch */
   u32 *   d_map;
   i8 *    d_code;
@@ -1214,6 +1259,7 @@ struct fdgpu_ed25519_ctx {
   u32 *   d_O;                   /*             product of the block's other Z, planar [10][max_sig] */
   u32 *   d_blk;                 /*             per 256-signature block: product of Z, then its inverse */
   u32 *   d_slow;                /*             signatures needing R's full decode, [max_sig] + count */
+  uint4 * d_khash;               /* NULL, or (drop-in, long messages) SHA-512(R||A||M) per signature, computed beforehand */
   hipEvent_t ev[4];
   enum { NRING = 64 };
   hipEvent_t ring[ NRING ][ 4 ];  /* per-batch kernel boundaries while timing is on */
@@ -1223,6 +1269,9 @@ struct fdgpu_ed25519_ctx {
   fd_slot slot[ NSLOT ];
   int cur;                       /* slot being filled */
   int fault;                     /* a batch failed on the device: the pipeline refuses new work */
+  int dedup;                     /* raw batches also return HA dedup tags (fdgpu_ed25519_set_dedup) */
+  unsigned long dedup_seed;
+  int rec_fp_off;                /* gathered records: offset of a u16 footprint field, -1 = none */
   std::deque<int> inflight;      /* slot order */
 };
 
@@ -1269,7 +1318,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       int d2 = lanes > 1;
       hipLaunchKernelGGL( fd_prep_kernel, dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, (u32)sg,
                           ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
-                          d2 ? ctx->d_tab : (uint4 *)NULL );
+                          d2 ? ctx->d_tab : (uint4 *)NULL, (uint4 const *)ctx->d_khash );
       if( !d2 )
         hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, ctx->d_pstat, code,
                             ctx->d_Axy, ctx->d_tab );
@@ -1278,7 +1327,8 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, !defer,
                           ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy );
       hipLaunchKernelGGL( fd_hash_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
-                          ctx->semantics, defer, ctx->d_pstat, code, ctx->d_digA, ctx->d_digB, ctx->d_Rxy );
+                          ctx->semantics, defer, ctx->d_pstat, code, ctx->d_digA, ctx->d_digB, ctx->d_Rxy,
+                          (uint4 const *)ctx->d_khash );
       hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics,
                           (unsigned char const *)NULL, code, ctx->d_Axy, ctx->d_tab );
     }
@@ -1311,6 +1361,24 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
 
 extern "C" void fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx );
 
+/* staging + device buffers of async slot i (once) */
+static int
+slot_bufs( fdgpu_ed25519_ctx_t * ctx, int i ) {
+  fd_slot & sl = ctx->slot[i];
+  if( sl.h_payload ) return 0;
+  unsigned long mp = ctx->max_payload, mt = ctx->max_txn;
+  HIPCHK( hipSetDevice( ctx->device ), -1 );
+  HIPCHK( hipHostMalloc( (void**)&sl.h_payload, mp + FD_ARENA_SLACK, hipHostMallocDefault ), -1 );
+  HIPCHK( hipHostMalloc( (void**)&sl.h_desc, mt * sizeof(fdgpu_txn_desc_t), hipHostMallocDefault ), -1 );
+  HIPCHK( hipHostMalloc( (void**)&sl.h_txn_out, mt, hipHostMallocDefault ), -1 );
+  HIPCHK( hipHostMalloc( (void**)&sl.h_tags, mt * sizeof(unsigned long), hipHostMallocDefault ), -1 );
+  HIPCHK( hipMalloc( &sl.d_payload, mp + FD_ARENA_SLACK ), -1 );
+  HIPCHK( hipMalloc( &sl.d_desc, mt * sizeof(fdgpu_txn_desc_t) ), -1 );
+  HIPCHK( hipMalloc( &sl.d_txn_out, mt ), -1 );
+  memset( sl.h_payload, 0, FD_ARENA_SLACK );
+  return 0;
+}
+
 /* allocations of a new context; on failure the caller deletes the
    partially built context (every handle starts NULL) */
 static int
@@ -1320,6 +1388,8 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->max_txn = max_txn; ctx->max_sig = max_sig; ctx->max_payload = max_payload_bytes;
   size_t ns = max_sig;
   HIPCHK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ), -1 );
+  HIPCHK( hipStreamCreateWithFlags( &ctx->cstream, hipStreamNonBlocking ), -1 );
+  for( unsigned long i=0; i<FD_PIPE_MAX; i++ ) HIPCHK( hipEventCreateWithFlags( &ctx->pipe_ev[i], hipEventDisableTiming ), -1 );
   HIPCHK( hipMalloc( &ctx->d_map,  ns * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_code, ns ), -1 );
   HIPCHK( hipMalloc( &ctx->d_pstat, 2*ns ), -1 );
@@ -1344,21 +1414,11 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->ring_cnt = 0;
   hipLaunchKernelGGL( fd_btab_kernel, dim3((FD_BTAB_ENTRIES + 255)/256), dim3(256), 0, ctx->stream, ctx->d_btab );
   HIPCHK( hipGetLastError(), -1 );
-  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
-    fd_slot & sl = ctx->slot[i];
-    if( max_payload_bytes ) {
-      HIPCHK( hipHostMalloc( (void**)&sl.h_payload, max_payload_bytes + FD_ARENA_SLACK, hipHostMallocDefault ), -1 );
-      HIPCHK( hipHostMalloc( (void**)&sl.h_desc, max_txn * sizeof(fdgpu_txn_desc_t), hipHostMallocDefault ), -1 );
-      HIPCHK( hipHostMalloc( (void**)&sl.h_txn_out, max_txn, hipHostMallocDefault ), -1 );
-      HIPCHK( hipHostMalloc( (void**)&sl.h_tags, max_txn * sizeof(unsigned long), hipHostMallocDefault ), -1 );
-      HIPCHK( hipMalloc( &sl.d_payload, max_payload_bytes + FD_ARENA_SLACK ), -1 );
-      HIPCHK( hipMalloc( &sl.d_desc, max_txn * sizeof(fdgpu_txn_desc_t) ), -1 );
-      HIPCHK( hipMalloc( &sl.d_txn_out, max_txn ), -1 );
-      memset( sl.h_payload, 0, max_payload_bytes + FD_ARENA_SLACK );
-    }
-    HIPCHK( hipEventCreateWithFlags( &sl.done, hipEventDisableTiming ), -1 );
-  }
-  ctx->cur = 0;
+  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) HIPCHK( hipEventCreateWithFlags( &ctx->slot[i].done, hipEventDisableTiming ), -1 );
+  /* slot 0 now (the synchronous host calls stage through it); the async
+     pipeline's other slots on first use (slot_bufs) */
+  if( max_payload_bytes && slot_bufs( ctx, 0 ) ) return -1;
+  ctx->cur = 0; ctx->rec_fp_off = -1;
   HIPCHK( hipStreamSynchronize( ctx->stream ), -1 );
   return 0;
 }
@@ -1398,11 +1458,15 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
     if( sl.h_tags    ) (void)hipHostFree( sl.h_tags );
     if( sl.h_img     ) (void)hipHostFree( sl.h_img );
     if( sl.h_fp      ) (void)hipHostFree( sl.h_fp );
+    if( sl.h_dtag    ) (void)hipHostFree( sl.h_dtag );
+    (void)hipFree( sl.d_dtag );
     if( sl.h_gat     ) (void)hipHostFree( sl.h_gat );
     (void)hipFree( sl.d_payload ); (void)hipFree( sl.d_desc ); (void)hipFree( sl.d_txn_out );
     (void)hipFree( sl.d_img ); (void)hipFree( sl.d_fp ); (void)hipFree( sl.d_gat );
     if( sl.done ) (void)hipEventDestroy( sl.done );
   }
+  if( ctx->cstream ) { (void)hipStreamSynchronize( ctx->cstream ); (void)hipStreamDestroy( ctx->cstream ); }
+  for( unsigned long i=0; i<FD_PIPE_MAX; i++ ) if( ctx->pipe_ev[i] ) (void)hipEventDestroy( ctx->pipe_ev[i] );
   if( ctx->stream ) (void)hipStreamDestroy( ctx->stream );
   delete ctx;
 }
@@ -1494,6 +1558,59 @@ static int check_batch( fdgpu_txn_desc_t const * desc, unsigned long txn_cnt, un
   return 0;
 }
 
+/* Large host batches: sub-batches of ~FD_PIPE_SUB transactions.  The
+   payload bytes of sub-batch i go up on the copy stream (straight from a
+   pinned region, or through the pinned staging slot) while the kernels of
+   sub-batch i-1 run on the compute stream, which waits for copy i by an
+   event.  Only the compute stream waits, and only on copies enqueued
+   before the wait; the copy stream never waits (no write-after-read on
+   its buffers: every sub-batch has its own range of one arena), so no
+   cycle of cross-queue waits can form whatever hardware queues the two
+   streams share. */
+static int
+verify_host_pipelined( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload, unsigned long payload_bytes,
+                       fdgpu_txn_desc_t const * desc, unsigned long txn_cnt, unsigned long nsig,
+                       signed char * txn_out, signed char * sig_out ) {
+  fd_slot & sl = ctx->slot[0];
+  hipStream_t st = ctx->stream, cs = ctx->cstream;
+  unsigned long nsub = txn_cnt / FD_PIPE_SUB;
+  if( nsub > FD_PIPE_MAX ) nsub = FD_PIPE_MAX;
+  int pinned = region_dev( payload, payload_bytes ) != NULL;
+  /* descriptors with each sub-batch's sig_base rebased to its first signature */
+  unsigned long sig_lo[ FD_PIPE_MAX + 1 ], txn_lo[ FD_PIPE_MAX + 1 ];
+  for( unsigned long i=0; i<=nsub; i++ ) txn_lo[i] = txn_cnt * i / nsub;
+  for( unsigned long i=0; i<nsub; i++ ) {
+    sig_lo[i] = desc[ txn_lo[i] ].sig_base;
+    for( unsigned long t=txn_lo[i]; t<txn_lo[i+1]; t++ ) { sl.h_desc[t] = desc[t]; sl.h_desc[t].sig_base -= (unsigned)sig_lo[i]; }
+  }
+  sig_lo[nsub] = nsig;
+  HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, cs ), -2 );
+  HIPCHK( hipMemsetAsync( sl.d_payload + payload_bytes, 0, FD_ARENA_SLACK, cs ), -2 );
+  for( unsigned long i=0; i<nsub; i++ ) {
+    unsigned long lo = ~0UL, hi = 0UL;
+    for( unsigned long t=txn_lo[i]; t<txn_lo[i+1]; t++ ) {
+      unsigned long a = desc[t].payload_off, b = a + desc[t].payload_sz;
+      if( a < lo ) lo = a;
+      if( b > hi ) hi = b;
+    }
+    if( hi > lo ) {
+      unsigned char const * src = payload + lo;
+      if( !pinned ) { memcpy( sl.h_payload + lo, payload + lo, hi - lo ); src = sl.h_payload + lo; }
+      HIPCHK( hipMemcpyAsync( sl.d_payload + lo, src, hi - lo, hipMemcpyHostToDevice, cs ), -2 );
+    }
+    HIPCHK( hipEventRecord( ctx->pipe_ev[i], cs ), -2 );
+    HIPCHK( hipStreamWaitEvent( st, ctx->pipe_ev[i], 0 ), -2 );
+    int rc = launch_batch( ctx, sl.d_payload, sl.d_desc + txn_lo[i], txn_lo[i+1] - txn_lo[i], sig_lo[i+1] - sig_lo[i],
+                           sl.d_txn_out + txn_lo[i], ctx->d_code + sig_lo[i], st );
+    if( rc ) return rc;
+  }
+  HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
+  if( sig_out && nsig ) HIPCHK( hipMemcpyAsync( sig_out, ctx->d_code, nsig, hipMemcpyDeviceToHost, st ), -2 );
+  HIPCHK( hipStreamSynchronize( st ), -2 );
+  memcpy( txn_out, sl.h_txn_out, txn_cnt );
+  return 0;
+}
+
 extern "C" int
 fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload, unsigned long payload_bytes,
                                 fdgpu_txn_desc_t const * desc, unsigned long txn_cnt,
@@ -1507,6 +1624,7 @@ fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
   fd_slot & sl = ctx->slot[0];
   if( async_busy( ctx ) ) { fd_err = "async batches pending or in flight"; return -1; }
   hipStream_t st = ctx->stream;
+  if( txn_cnt >= 2UL*FD_PIPE_SUB ) return verify_host_pipelined( ctx, payload, payload_bytes, desc, txn_cnt, nsig, txn_out, sig_out );
   memcpy( sl.h_desc, desc, txn_cnt * sizeof(fdgpu_txn_desc_t) );
   HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
   if( region_dev( payload, payload_bytes ) ) {
@@ -1625,18 +1743,18 @@ fdgpu_txn_parse_device( unsigned char const * d_payload, fdgpu_txn_raw_t const *
   if( txn_cnt >= (1UL<<31) || ( d_img && ( img_stride < 852UL || img_stride > 0xffffffffUL ) ) ) { fd_err = "bad arguments"; return -1; }
   unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, (hipStream_t)stream, d_payload, d_raw, (u32)txn_cnt,
-                      (fdgpu_txn_desc_t *)NULL, (unsigned char *)NULL, d_img, (u32)img_stride, d_fp );
+                      (fdgpu_txn_desc_t *)NULL, (unsigned char *)NULL, d_img, (u32)img_stride, d_fp, 0UL, (u64 *)NULL );
   HIPCHK( hipGetLastError(), -3 );
   return 0;
 }
 
 static int launch_raw( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_raw_t const * d_raw,
                        unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, unsigned char * d_img,
-                       unsigned long img_stride, unsigned short * d_fp, hipStream_t st ) {
+                       unsigned long img_stride, unsigned short * d_fp, hipStream_t st, u64 * d_dtag = NULL ) {
   if( !txn_cnt ) return 0;
   unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, st, d_payload, d_raw, (u32)txn_cnt,
-                      ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp );
+                      ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp, (u64)ctx->dedup_seed, d_dtag );
   HIPCHK( hipGetLastError(), -3 );
   return launch_batch( ctx, d_payload, ctx->d_rdesc, txn_cnt, sig_cnt, d_txn_out, NULL, st, ctx->d_pflag );
 }
@@ -1728,31 +1846,37 @@ static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
   HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
   int rc = sl.mode
          ? launch_raw( ctx, sl.d_payload, (fdgpu_txn_raw_t const *)sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out,
-                       sl.d_img, FDGPU_TXN_IMG_STRIDE, sl.d_fp, st )
+                       sl.d_img, FDGPU_TXN_IMG_STRIDE, sl.d_fp, st, ctx->dedup ? (u64 *)sl.d_dtag : (u64 *)NULL )
          : launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
   if( rc ) return rc;
   HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
   if( sl.mode==3 ) {   /* gathered: the images go into the out region, only the footprints come back */
     hipLaunchKernelGGL( fd_img_scatter_kernel, dim3( (unsigned)sl.txn_cnt ), dim3( 64 ), 0, st,
                         (fdgpu_txn_raw_t const *)sl.d_desc, sl.d_img, (u32)FDGPU_TXN_IMG_STRIDE, sl.d_fp,
-                        sl.ref_dev + sl.ref_lo );
+                        sl.ref_dev + sl.ref_lo, ctx->rec_fp_off );
     HIPCHK( hipGetLastError(), -2 );
     HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
   } else if( sl.mode ) {   /* raw and in-place raw */
     HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
     HIPCHK( hipMemcpyAsync( sl.h_img, sl.d_img, sl.txn_cnt * FDGPU_TXN_IMG_STRIDE, hipMemcpyDeviceToHost, st ), -2 );
   }
+  if( sl.mode && ctx->dedup )
+    HIPCHK( hipMemcpyAsync( sl.h_dtag, sl.d_dtag, sl.txn_cnt * sizeof(unsigned long), hipMemcpyDeviceToHost, st ), -2 );
   HIPCHK( hipEventRecord( sl.done, st ), -2 );
   sl.state = 1; sl.cursor = 0;
   ctx->inflight.push_back( i );
   return 0;
 }
 
-/* make ctx->cur a free slot; -2 if every slot is in flight */
+/* make ctx->cur a free slot; -2 if every slot is in flight, -3 if its
+   buffers cannot be allocated */
 static int next_free( fdgpu_ed25519_ctx_t * ctx ) {
   for( int k=0; k<fdgpu_ed25519_ctx_t::NSLOT; k++ ) {
     int i = (ctx->cur + k) % fdgpu_ed25519_ctx_t::NSLOT;
-    if( ctx->slot[i].state==0 ) { ctx->cur = i; return 0; }
+    if( ctx->slot[i].state==0 ) {
+      if( slot_bufs( ctx, i ) ) return -3;
+      ctx->cur = i; return 0;
+    }
   }
   return -2;
 }
@@ -1774,12 +1898,15 @@ static fd_slot * slot_for( fdgpu_ed25519_ctx_t * ctx, unsigned long payload_sz, 
   *rc = 0;
   if( ctx->fault ) { fd_err = "ctx faulted (see the poll error); delete and recreate it"; *rc = -3; return NULL; }
   if( !ctx->slot[0].h_payload ) { fd_err = "ctx has no staging buffers (max_payload_bytes==0)"; *rc = -3; return NULL; }
-  if( next_free( ctx ) ) { *rc = -2; return NULL; }
+  if( ( *rc = next_free( ctx ) ) ) return NULL;
+  /* a record that cannot fit an empty slot's arena is refused outright (it
+     would overrun the staging and device arenas) */
+  if( payload_sz + 8UL > ctx->max_payload ) { fd_err = "record larger than the ctx payload arena"; *rc = FDGPU_ERR_TOO_LONG; return NULL; }
   fd_slot * sl = &ctx->slot[ ctx->cur ];
   if( sl->txn_cnt && ( sl->mode != mode || sl->txn_cnt + 1 > ctx->max_txn || sl->sig_cnt + sig_cnt > ctx->max_sig
                        || sl->payload_used + payload_sz + 8 > ctx->max_payload ) ) {
     if( ( *rc = fdgpu_ed25519_flush( ctx ) ) ) return NULL;
-    if( next_free( ctx ) ) { *rc = -2; return NULL; }
+    if( ( *rc = next_free( ctx ) ) ) return NULL;
     sl = &ctx->slot[ ctx->cur ];
   }
   if( sl->txn_cnt==0 ) sl->mode = mode;
@@ -1811,6 +1938,8 @@ static int slot_raw_bufs( fdgpu_ed25519_ctx_t * ctx, fd_slot * sl ) {
   HIPCHK( hipHostMalloc( (void **)&sl->h_fp, ctx->max_txn * sizeof(unsigned short), hipHostMallocDefault ), -3 );
   HIPCHK( hipMalloc( (void **)&sl->d_img, ctx->max_txn * FDGPU_TXN_IMG_STRIDE ), -3 );
   HIPCHK( hipMalloc( (void **)&sl->d_fp, ctx->max_txn * sizeof(unsigned short) ), -3 );
+  HIPCHK( hipHostMalloc( (void **)&sl->h_dtag, ctx->max_txn * sizeof(unsigned long), hipHostMallocDefault ), -3 );
+  HIPCHK( hipMalloc( (void **)&sl->d_dtag, ctx->max_txn * sizeof(unsigned long) ), -3 );
   HIPCHK( hipHostMalloc( (void **)&sl->h_gat, ctx->max_txn * sizeof(fd_gather), hipHostMallocDefault ), -3 );
   HIPCHK( hipMalloc( (void **)&sl->d_gat, ctx->max_txn * sizeof(fd_gather) ), -3 );
   return 0;
@@ -1845,11 +1974,11 @@ fdgpu_ed25519_submit_raw_ref( fdgpu_ed25519_ctx_t * ctx, unsigned char const * b
   unsigned b0 = payload_sz ? payload[0] : 0u;
   unsigned lanes = ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u;
   size_t off = (size_t)( payload - base );
-  int rc; fd_slot * sl = slot_for( ctx, 0UL, lanes, 2, &rc );
+  int rc; fd_slot * sl = slot_for( ctx, payload_sz, lanes, 2, &rc );
   if( !sl ) return rc;
   if( sl->txn_cnt && ( sl->ref_base != base || off < sl->ref_hi || off + payload_sz - sl->ref_lo + 8UL > ctx->max_payload ) ) {
     if( ( rc = fdgpu_ed25519_flush( ctx ) ) ) return rc;
-    if( !( sl = slot_for( ctx, 0UL, lanes, 2, &rc ) ) ) return rc;
+    if( !( sl = slot_for( ctx, payload_sz, lanes, 2, &rc ) ) ) return rc;
   }
   if( slot_raw_bufs( ctx, sl ) ) return -3;
   if( !sl->txn_cnt ) { sl->ref_base = base; sl->ref_lo = off; }
@@ -1921,7 +2050,8 @@ extern "C" int
 fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char * dst_base,
                                  unsigned char * dst, unsigned short copy_sz, unsigned short payload_off,
                                  unsigned short payload_sz, unsigned long tag ) {
-  if( (unsigned)payload_off + payload_sz > copy_sz || ( (uintptr_t)src & 15 ) || ( (uintptr_t)( dst - dst_base ) & 15 ) ) {
+  if( (unsigned)payload_off + payload_sz > copy_sz || ( (uintptr_t)src & 15 ) || ( (uintptr_t)( dst - dst_base ) & 15 ) ||
+      ( ctx->rec_fp_off >= 0 && ( payload_off > 255u || (unsigned)ctx->rec_fp_off + 2u > payload_off ) ) ) {
     fd_err = "fdgpu_ed25519_submit_raw_gather: bad record"; return -1;
   }
   unsigned long csz = ( (unsigned long)copy_sz + 15UL ) & ~15UL;
@@ -1930,11 +2060,11 @@ fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const 
   unsigned b0 = payload_sz ? src[ payload_off ] : 0u;
   unsigned lanes = ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u;
   size_t off = (size_t)( dst - dst_base );
-  int rc; fd_slot * sl = slot_for( ctx, 0UL, lanes, 3, &rc );
+  int rc; fd_slot * sl = slot_for( ctx, csz, lanes, 3, &rc );
   if( !sl ) return rc;
   if( sl->txn_cnt && ( sl->ref_base != dst_base || off < sl->ref_hi || off + csz - sl->ref_lo + 8UL > ctx->max_payload ) ) {
     if( ( rc = fdgpu_ed25519_flush( ctx ) ) ) return rc;
-    if( !( sl = slot_for( ctx, 0UL, lanes, 3, &rc ) ) ) return rc;
+    if( !( sl = slot_for( ctx, csz, lanes, 3, &rc ) ) ) return rc;
   }
   if( slot_raw_bufs( ctx, sl ) ) return -3;
   if( !sl->txn_cnt ) {
@@ -1945,6 +2075,7 @@ fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const 
   fdgpu_txn_raw_t & r = ((fdgpu_txn_raw_t *)sl->h_desc)[ sl->txn_cnt ];
   r.payload_off = (unsigned)( off - sl->ref_lo + payload_off ); r.sig_base = (unsigned)sl->sig_cnt;
   r.payload_sz = payload_sz; r.sig_lanes = (unsigned char)lanes;
+  r._pad[0] = (unsigned char)payload_off;      /* fd_img_scatter_kernel finds the record header from it */
   fd_gather & g = sl->h_gat[ sl->txn_cnt ];
   g.src = (unsigned long)dsrc; g.dst = (unsigned)( off - sl->ref_lo ); g.sz = (unsigned)csz;
   sl->h_tags[ sl->txn_cnt ] = tag;
@@ -1956,7 +2087,8 @@ fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const 
 /* Drain completed slots in submission order, at most max results. */
 static unsigned long
 poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes, unsigned char * out_img,
-          unsigned short * out_fp, unsigned long max, int blocking ) {
+          unsigned short * out_fp, unsigned long * out_dtag, unsigned long max, int blocking ) {
+  if( ctx->fault ) return 0;             /* faulted: nothing more completes (never block on it) */
   hipSetDevice( ctx->device );
   unsigned long n = 0;
   while( n < max && !ctx->inflight.empty() ) {
@@ -1974,6 +2106,7 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
       out_tags[n+t]  = sl.h_tags[u];
       out_codes[n+t] = sl.h_txn_out[u];
       if( out_fp )  out_fp[n+t] = sl.mode ? sl.h_fp[u] : 0;
+      if( out_dtag ) out_dtag[n+t] = ( sl.mode && ctx->dedup ) ? sl.h_dtag[u] : 0UL;
       if( out_img && sl.mode && sl.mode != 3 ) {   /* mode 3: the image is in the caller's out region */
         unsigned fp = sl.h_fp[u];
         memcpy( out_img + (n+t)*FDGPU_TXN_IMG_STRIDE, sl.h_img + u*FDGPU_TXN_IMG_STRIDE, fp );
@@ -1988,6 +2121,16 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
   return n;
 }
 
+extern "C" int fdgpu_ed25519_faulted( fdgpu_ed25519_ctx_t const * ctx ) { return ctx ? ctx->fault : 1; }
+
+/* host-side test hook: the context behaves exactly as after a failed batch */
+extern "C" void
+fdgpu_ed25519_debug_fault( fdgpu_ed25519_ctx_t * ctx ) {
+  if( !ctx ) return;
+  ctx->fault = 1;
+  fd_err = "fdgpu_ed25519_poll: batch failed: injected by fdgpu_ed25519_debug_fault";
+}
+
 extern "C" void
 fdgpu_ed25519_pipeline_state( fdgpu_ed25519_ctx_t const * ctx, unsigned long * filling, unsigned long * inflight ) {
   *filling  = ctx->slot[ ctx->cur ].state==0 ? ctx->slot[ ctx->cur ].txn_cnt : 0UL;
@@ -1997,13 +2140,26 @@ fdgpu_ed25519_pipeline_state( fdgpu_ed25519_ctx_t const * ctx, unsigned long * f
 extern "C" unsigned long
 fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes,
                     unsigned long max, int blocking ) {
-  return poll_any( ctx, out_tags, out_codes, NULL, NULL, max, blocking );
+  return poll_any( ctx, out_tags, out_codes, NULL, NULL, NULL, max, blocking );
 }
 
 extern "C" unsigned long
 fdgpu_ed25519_poll_raw( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes,
-                        unsigned char * out_img, unsigned short * out_fp, unsigned long max, int blocking ) {
-  return poll_any( ctx, out_tags, out_codes, out_img, out_fp, max, blocking );
+                        unsigned char * out_img, unsigned short * out_fp, unsigned long * out_dedup, unsigned long max,
+                        int blocking ) {
+  return poll_any( ctx, out_tags, out_codes, out_img, out_fp, out_dedup, max, blocking );
+}
+
+extern "C" void
+fdgpu_ed25519_set_dedup( fdgpu_ed25519_ctx_t * ctx, int enable, unsigned long seed ) {
+  ctx->dedup = enable ? 1 : 0; ctx->dedup_seed = seed;
+}
+
+extern "C" int
+fdgpu_ed25519_set_record_fp_off( fdgpu_ed25519_ctx_t * ctx, int off ) {
+  if( off < -1 || off > 253 ) { fd_err = "bad record footprint offset"; return -1; }
+  ctx->rec_fp_off = off;
+  return 0;
 }
 
 /* ---- drop-in synchronous API (fd_ed25519.h) ------------------------- */
@@ -2020,6 +2176,40 @@ static fdgpu_ed25519_ctx_t * global_ctx( void ) {
   return g_ctx;
 }
 
+/* drop-in for messages whose descriptor would pass 64 KiB: digests first
+   (fd_sha512_batch_kernel over n staged R_j||A_j||M copies), then the batch
+   with an empty message and the digests in ctx->d_khash.  Returns the
+   code, or 1 on a GPU error. */
+static int
+verify_long( fdgpu_ed25519_ctx_t * ctx, unsigned char const * msg, unsigned long msg_sz,
+             unsigned char const * sigs, unsigned char const * pubs, unsigned long n ) {
+  size_t one = 64UL + msg_sz, tot = n*one;
+  std::vector<unsigned char> buf( tot );
+  std::vector<unsigned long> off( n );
+  std::vector<unsigned int>  hsz( n );
+  for( unsigned long j=0; j<n; j++ ) {
+    unsigned char * b = buf.data() + j*one;
+    memcpy( b, sigs + 64*j, 32 ); memcpy( b + 32, pubs + 32*j, 32 );
+    if( msg_sz ) memcpy( b + 64, msg, msg_sz );
+    off[j] = j*one; hsz[j] = (unsigned)one;
+  }
+  if( tot > 0xffffffffUL ) { fd_err = "message too long"; return 1; }
+  std::vector<unsigned char> dig( 64*n );
+  if( fdgpu_sha512_batch_host( ctx->device, buf.data(), tot, off.data(), hsz.data(), n, dig.data() ) ) return 1;
+  unsigned char pl[ 96*16 ];
+  memcpy( pl, sigs, 64*n ); memcpy( pl + 64*n, pubs, 32*n );
+  fdgpu_txn_desc_t d;
+  d.payload_off = 0; d.sig_base = 0; d.payload_sz = (unsigned short)(96*n); d.message_off = (unsigned short)(96*n);
+  d.acct_addr_off = (unsigned short)(64*n); d.signature_off = 0; d.sig_cnt = (unsigned char)n;
+  if( hipSetDevice( ctx->device ) != hipSuccess || hipMalloc( (void **)&ctx->d_khash, 64*n ) != hipSuccess ) { fd_err = "hipMalloc"; return 1; }
+  int rc = 1;
+  signed char out = 0;
+  if( hipMemcpy( ctx->d_khash, dig.data(), 64*n, hipMemcpyHostToDevice ) == hipSuccess &&
+      !fdgpu_ed25519_verify_txns_host( ctx, pl, 96*n, &d, 1, &out, NULL ) ) rc = out;
+  (void)hipFree( ctx->d_khash ); ctx->d_khash = NULL;
+  return rc;
+}
+
 extern "C" int
 fd_ed25519_verify_batch_single_msg( unsigned char const msg[], unsigned long const msg_sz,
                                     unsigned char const signatures[ 64 ], unsigned char const pubkeys[ 32 ],
@@ -2028,10 +2218,16 @@ fd_ed25519_verify_batch_single_msg( unsigned char const msg[], unsigned long con
   if( batch_sz==0 || batch_sz>16 ) return FD_ED25519_ERR_SIG;   /* fd_ed25519_user.c:238-241 */
   unsigned long n = batch_sz;
   unsigned long sz = 96UL*n + msg_sz;
-  if( sz > 0xffffUL ) return FDGPU_ERR_TOO_LONG; /* beyond the 64 KiB descriptor limit: see fd_ed25519_gpu.h */
   std::lock_guard<std::mutex> lk( g_mu );
   fdgpu_ed25519_ctx_t * ctx = global_ctx();
   if( !ctx ) { fprintf( stderr, "fdgpu: no GPU context: %s\n", fdgpu_last_error() ); abort(); }
+  if( sz > 0xffffUL ) {
+    /* beyond the 16-bit descriptor: k = SHA-512(R||A||M) by the batch SHA-512 kernel first, then the same
+       verify with the digests handed in (same codes as the reference for any message length) */
+    int r = verify_long( ctx, msg, msg_sz, signatures, pubkeys, n );
+    if( r > 0 ) { fprintf( stderr, "fdgpu: verify failed: %s\n", fdgpu_last_error() ); abort(); }
+    return r;
+  }
   std::vector<unsigned char> buf( sz );
   memcpy( buf.data(), signatures, 64*n );
   memcpy( buf.data() + 64*n, pubkeys, 32*n );

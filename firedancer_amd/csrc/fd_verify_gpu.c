@@ -7,8 +7,12 @@
 #include "../../include/fd_verify_gpu.h"
 #include "../../include/fd_ed25519_gpu.h"
 
+#include <fcntl.h>
 #include <pthread.h>
 #include <stdio.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <stdatomic.h>
 #include <stdint.h>
 #include <stdlib.h>
@@ -95,6 +99,15 @@ static int tc_find( fdgpu_tcache_t const * tc, ulong tag, ulong * idx ) {
   }
 }
 
+/* start the map lines a query / insert of tag will touch, and the map line
+   of the tag an insert `ahead` inserts from now would evict */
+static inline void tc_prefetch( fdgpu_tcache_t const * tc, ulong tag, ulong ahead ) {
+  __builtin_prefetch( &tc->map[ tc_slot( tag, tc->map_cnt ) ] );
+  ulong o = tc->oldest + ahead; if( o >= tc->depth ) o %= tc->depth;
+  ulong old = tc->ring[ o ];
+  if( old ) __builtin_prefetch( &tc->map[ tc_slot( old, tc->map_cnt ) ], 1 );
+}
+
 int fdgpu_tcache_query( fdgpu_tcache_t const * tc, ulong tag ) {
   if( !tag ) return 1;
   ulong i; return tc_find( tc, tag, &i );
@@ -129,60 +142,86 @@ int fdgpu_tcache_insert( fdgpu_tcache_t * tc, ulong tag ) {
 }
 
 /* ---- mcache / dcache -------------------------------------------------
-   An mcache is a ring of frag metadata indexed by seq & (depth-1); the
-   producer writes the entry and then its seq (release); a consumer
-   waiting for seq reads the entry between two acquire loads of its seq
-   field and classifies: equal = ready, behind = not yet published,
-   ahead = overrun (src/tango/mcache/fd_mcache.h:288-325 semantics). */
+   An mcache is a ring of 32-byte frag metadata lines indexed by seq &
+   (depth-1), laid out as fd_frag_meta_t (src/tango/fd_tango_base.h:
+   146-203): seq, sig, chunk, sz, ctl, tsorig, tspub, the timestamps
+   compressed to their low 32 bits (fd_frag_meta_ts_comp).  The producer
+   marks the line in progress (seq-1), writes the fields and publishes seq
+   (release); a consumer reads seq, the fields, then seq again (src/tango/
+   mcache/fd_mcache.h:288-325 semantics): equal = ready, behind = not yet
+   published, ahead = overrun. */
 
 typedef struct {
-  _Atomic ulong     seq;
-  fdgpu_frag_meta_t m;
+  _Atomic ulong  seq;
+  ulong          sig;
+  unsigned       chunk;
+  unsigned short sz, ctl;
+  unsigned       tsorig, tspub;
 } mc_line_t;
 
 struct fdgpu_mcache {
   ulong       depth;
   mc_line_t * line;
+  int         own;          /* line[] allocated here (else it lives in a shared link) */
 };
+
+static void mc_init_lines( mc_line_t * line, ulong depth, ulong seq0 ) {
+  memset( (void *)line, 0, depth * sizeof(mc_line_t) );
+  /* every line starts "one lap behind" so seq0.. read as not yet published */
+  for( ulong i=0; i<depth; i++ ) atomic_store_explicit( &line[ (seq0 + i) & (depth - 1UL) ].seq, seq0 + i - depth, memory_order_relaxed );
+}
 
 fdgpu_mcache_t *
 fdgpu_mcache_new( ulong depth, ulong seq0 ) {
   if( !depth || (depth & (depth - 1UL)) ) return NULL;
   fdgpu_mcache_t * mc = (fdgpu_mcache_t *)calloc( 1, sizeof(fdgpu_mcache_t) );
   if( !mc ) return NULL;
-  mc->depth = depth;
+  mc->depth = depth; mc->own = 1;
   mc->line = (mc_line_t *)aligned_alloc( 64, depth * sizeof(mc_line_t) + 64 );
   if( !mc->line ) { free( mc ); return NULL; }
-  memset( mc->line, 0, depth * sizeof(mc_line_t) );
-  /* every line starts "one lap behind" so seq0.. read as not yet published */
-  for( ulong i=0; i<depth; i++ ) atomic_store_explicit( &mc->line[i].seq, seq0 + i - depth, memory_order_relaxed );
+  mc_init_lines( mc->line, depth, seq0 );
   return mc;
 }
 
-void fdgpu_mcache_delete( fdgpu_mcache_t * mc ) { if( mc ) { free( mc->line ); free( mc ); } }
+void fdgpu_mcache_delete( fdgpu_mcache_t * mc ) { if( mc ) { if( mc->own ) free( mc->line ); free( mc ); } }
+
+static inline void
+mc_publish( mc_line_t * l, ulong seq, ulong sig, unsigned chunk, unsigned sz, unsigned tsorig, unsigned tspub ) {
+  atomic_store_explicit( &l->seq, seq - 1UL, memory_order_relaxed );   /* mark in-progress */
+  atomic_thread_fence( memory_order_release );
+  l->sig = sig; l->chunk = chunk; l->sz = (unsigned short)sz; l->ctl = 0; l->tsorig = tsorig; l->tspub = tspub;
+  atomic_store_explicit( &l->seq, seq, memory_order_release );
+}
 
 void
 fdgpu_mcache_publish( fdgpu_mcache_t * mc, ulong seq, ulong sig, unsigned chunk, unsigned sz, ulong tsorig, ulong tspub ) {
-  mc_line_t * l = &mc->line[ seq & (mc->depth - 1UL) ];
-  atomic_store_explicit( &l->seq, seq - 1UL, memory_order_relaxed );   /* mark in-progress */
-  atomic_thread_fence( memory_order_release );
-  l->m.seq = seq; l->m.sig = sig; l->m.chunk = chunk; l->m.sz = sz; l->m.tsorig = tsorig; l->m.tspub = tspub;
-  atomic_store_explicit( &l->seq, seq, memory_order_release );
+  mc_publish( &mc->line[ seq & (mc->depth - 1UL) ], seq, sig, chunk, sz, (unsigned)tsorig, (unsigned)tspub );
+}
+
+/* 0 ready (copied to *out), 1 not yet published, -1 overrun; *found = the
+   seq the line held (where an overrun consumer resumes, fd_stem.c:590-596) */
+static inline int
+mc_poll( mc_line_t const * l, ulong seq, fdgpu_frag_meta_t * out, ulong * found ) {
+  ulong s0 = atomic_load_explicit( (_Atomic ulong *)&l->seq, memory_order_acquire );
+  *found = s0;
+  if( (long)(s0 - seq) < 0 ) return 1;
+  if( s0 != seq ) return -1;
+  out->seq = seq; out->sig = l->sig; out->chunk = l->chunk; out->sz = l->sz; out->tsorig = l->tsorig; out->tspub = l->tspub;
+  atomic_thread_fence( memory_order_acquire );
+  ulong s1 = atomic_load_explicit( (_Atomic ulong *)&l->seq, memory_order_relaxed );
+  *found = s1;
+  return s1 == seq ? 0 : -1;                 /* overrun while reading */
 }
 
 int
 fdgpu_mcache_poll( fdgpu_mcache_t const * mc, ulong seq, fdgpu_frag_meta_t * out ) {
-  mc_line_t const * l = &mc->line[ seq & (mc->depth - 1UL) ];
-  ulong s0 = atomic_load_explicit( (_Atomic ulong *)&l->seq, memory_order_acquire );
-  if( (long)(s0 - seq) < 0 ) return 1;
-  if( s0 != seq ) return -1;
-  fdgpu_frag_meta_t m = l->m;
-  atomic_thread_fence( memory_order_acquire );
-  ulong s1 = atomic_load_explicit( (_Atomic ulong *)&l->seq, memory_order_relaxed );
-  if( s1 != seq ) return -1;
-  *out = m;
-  return 0;
+  ulong found;
+  return mc_poll( &mc->line[ seq & (mc->depth - 1UL) ], seq, out, &found );
 }
+
+/* fd_frag_meta_ts_decomp: the full timestamp nearest below-or-at now whose
+   low 32 bits are ts (valid for ages < 2^31 ns) */
+static inline ulong ts_decomp( unsigned ts, ulong now ) { return now - (ulong)(unsigned)( (unsigned)now - ts ); }
 
 /* fd_dcache_compact_next (src/tango/dcache/fd_dcache.h:263-269): advance
    by whole 128-byte chunk pairs, wrap to chunk0 past wmark */
@@ -226,6 +265,8 @@ vt_fence( void ) {
 
 typedef struct {
   ulong seq, tsorig, chunk;
+  ulong bundle_id;                       /* from the frag header, read in during_frag */
+  unsigned short payload_sz;
   int   k;                               /* engine context the frag's batch went to */
 } vt_pend_t;
 
@@ -238,9 +279,20 @@ typedef struct {
    are merged back into frag order in after_frags. */
 #define VT_NCTX_MAX 3
 
+/* GPU batch latency histogram: bucket i counts launch -> drained in
+   [2^i, 2^(i+1)) us (bucket 0 also takes < 1 us, the last one overflow) */
+static ulong vt_lat_bucket( ulong ns ) {
+  ulong us = ns / 1000UL;
+  ulong b = us ? 63UL - (ulong)__builtin_clzl( us ) : 0UL;
+  return b < FDGPU_VTILE_LAT_BUCKETS ? b : FDGPU_VTILE_LAT_BUCKETS - 1UL;
+}
+
 struct fdgpu_vtile {
   /* (fields below; ctx first so the watchdog can report pipeline state) */
   fdgpu_ed25519_ctx_t * ctx[ VT_NCTX_MAX ];
+  int                   device, semantics;   /* to recreate a faulted context */
+  int                   fault_seen[ VT_NCTX_MAX ];
+  fdgpu_vtile_gpu_metrics_t gm;
   int                   nctx, fill;      /* contexts, the one taking frags */
   ulong                 launch_ns[ VT_NCTX_MAX ];
   int                   busy[ VT_NCTX_MAX ];
@@ -262,10 +314,30 @@ struct fdgpu_vtile {
   /* poll scratch */
   ulong                 batch;
   ulong *               p_tags;
+  ulong *               p_dtag;          /* GPU-computed HA dedup tags */
   signed char *         p_codes;
   uchar *               p_img;
   unsigned short *      p_fp;
 };
+
+/* one engine context of the tile.  Adaptive batching launches a partial
+   batch when the GPU has room (low load: the latency path) and a full one
+   when frags back up (high load: the throughput path, whose per-signature
+   work is 0.5x the 4-lane DSM's). */
+static fdgpu_ed25519_ctx_t *
+vt_ctx_new( fdgpu_vtile_t const * vt ) {
+  ulong b = vt->batch;
+  fdgpu_ed25519_ctx_t * c = fdgpu_ed25519_ctx_new( vt->device, b, 16UL*b, b*2304UL + 1024UL, vt->semantics );
+  if( c ) {
+    ulong sm = fdgpu_ed25519_set_small_batch_max( c, 0UL );
+    fdgpu_ed25519_set_small_batch_max( c, sm < b/2UL ? sm : b/2UL );
+    /* the GPU computes the HA dedup tags and, for gathered records, stores
+       txn_t_sz: after_frag then touches neither payload nor record */
+    fdgpu_ed25519_set_dedup( c, 1, vt->seed );
+    fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
+  }
+  return c;
+}
 
 fdgpu_vtile_t *
 fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ulong out_dcache_bytes, int semantics ) {
@@ -279,17 +351,9 @@ fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ul
   if( vt->nctx < 1 ) vt->nctx = 1;
   if( vt->nctx > VT_NCTX_MAX ) vt->nctx = VT_NCTX_MAX;
   vt->batch_ns = 500e3;
+  vt->device = device; vt->semantics = semantics; vt->batch = batch_txn; vt->seed = seed;
   int ctx_ok = 1;
-  for( int k=0; k<vt->nctx; k++ ) {
-    vt->ctx[k] = fdgpu_ed25519_ctx_new( device, batch_txn, 16UL*batch_txn, batch_txn*2304UL + 1024UL, semantics );
-    /* adaptive batching launches a partial batch when the GPU has room (low
-       load: the latency path) and a full one when frags back up (high load:
-       the throughput path, whose per-signature work is 0.5x the 4-lane DSM's) */
-    if( vt->ctx[k] ) {
-      ulong sm = fdgpu_ed25519_set_small_batch_max( vt->ctx[k], 0UL );
-      fdgpu_ed25519_set_small_batch_max( vt->ctx[k], sm < batch_txn/2UL ? sm : batch_txn/2UL );
-    } else ctx_ok = 0;
-  }
+  for( int k=0; k<vt->nctx; k++ ) if( !( vt->ctx[k] = vt_ctx_new( vt ) ) ) ctx_ok = 0;
   vt->tcache = fdgpu_tcache_new( tcache_depth );
   ulong nchunk = ( out_dcache_bytes / FDGPU_CHUNK_SZ ) & ~1UL;
   vt->dcache = (uchar *)fdgpu_host_alloc( nchunk * FDGPU_CHUNK_SZ );   /* pinned: batches upload from it in place */
@@ -299,12 +363,12 @@ fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ul
   vt->pend_cap = nchunk / rchunk - 2UL;
   vt->pend = (vt_pend_t *)calloc( vt->pend_cap, sizeof(vt_pend_t) );
   vt->seed = seed;
-  vt->batch = batch_txn;
   vt->p_tags = (ulong *)malloc( batch_txn * sizeof(ulong) );
+  vt->p_dtag = (ulong *)malloc( batch_txn * sizeof(ulong) );
   vt->p_codes = (signed char *)malloc( batch_txn );
   vt->p_img = (uchar *)malloc( batch_txn * FDGPU_TXN_IMG_STRIDE );
   vt->p_fp = (unsigned short *)malloc( batch_txn * sizeof(unsigned short) );
-  if( !ctx_ok || !vt->tcache || !vt->dcache || !vt->pend || !vt->p_tags || !vt->p_codes || !vt->p_img || !vt->p_fp ) {
+  if( !ctx_ok || !vt->tcache || !vt->dcache || !vt->pend || !vt->p_tags || !vt->p_dtag || !vt->p_codes || !vt->p_img || !vt->p_fp ) {
     fdgpu_vtile_delete( vt );
     return NULL;
   }
@@ -316,13 +380,24 @@ fdgpu_vtile_delete( fdgpu_vtile_t * vt ) {
   if( !vt ) return;
   for( int k=0; k<VT_NCTX_MAX; k++ ) if( vt->ctx[k] ) fdgpu_ed25519_ctx_delete( vt->ctx[k] );
   fdgpu_tcache_delete( vt->tcache );
-  fdgpu_host_free( vt->dcache ); free( vt->pend ); free( vt->p_tags ); free( vt->p_codes ); free( vt->p_img ); free( vt->p_fp );
+  fdgpu_host_free( vt->dcache ); free( vt->pend ); free( vt->p_tags ); free( vt->p_dtag ); free( vt->p_codes ); free( vt->p_img );
+  free( vt->p_fp );
   free( vt );
 }
 
 uchar * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt ) { return vt->dcache; }
 ulong   fdgpu_vtile_pending( fdgpu_vtile_t const * vt ) { return vt->pend_tail - vt->pend_head; }
 void    fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, ulong out[ 5 ] ) { memcpy( out, vt->metrics, sizeof(vt->metrics) ); }
+/* bookkeeping of a batch launch on context k (filling txns) */
+static void
+vt_launched( fdgpu_vtile_t * vt, int k, ulong now, ulong filling ) {
+  vt->launch_ns[k] = now; vt->busy[k] = 1;
+  vt->gm.batches++; vt->gm.batch_txns += filling;
+  ulong f, infl = 0UL;
+  for( int j=0; j<vt->nctx; j++ ) { ulong i; fdgpu_ed25519_pipeline_state( vt->ctx[j], &f, &i ); infl += i; }
+  if( infl > vt->gm.inflight_max ) vt->gm.inflight_max = infl;
+}
+
 int
 fdgpu_vtile_flush( fdgpu_vtile_t * vt ) {
   vt_fence();
@@ -330,10 +405,11 @@ fdgpu_vtile_flush( fdgpu_vtile_t * vt ) {
   for( int i=0; i<vt->nctx; i++ ) {            /* oldest first: the fill context's batch is the newest */
     int k = ( vt->fill + 1 + i ) % vt->nctx;
     ulong filling, inflight;
+    if( fdgpu_ed25519_faulted( vt->ctx[k] ) ) continue;
     fdgpu_ed25519_pipeline_state( vt->ctx[k], &filling, &inflight );
     if( !filling ) continue;
     if( fdgpu_ed25519_flush( vt->ctx[k] ) ) rc = -1;
-    else { vt->launch_ns[k] = now_ns(); vt->busy[k] = 1; }
+    else vt_launched( vt, k, now_ns(), filling );
   }
   return rc;
 }
@@ -348,6 +424,39 @@ fdgpu_vtile_pipeline_state( fdgpu_vtile_t const * vt, ulong * filling, ulong * i
   }
 }
 ulong   fdgpu_vtile_overruns( fdgpu_vtile_t const * vt ) { return vt->overruns; }
+
+int
+fdgpu_vtile_faulted( fdgpu_vtile_t const * vt ) {
+  int n = 0;
+  for( int k=0; k<vt->nctx; k++ ) n += fdgpu_ed25519_faulted( vt->ctx[k] ) != 0;
+  return n;
+}
+
+int
+fdgpu_vtile_recover( fdgpu_vtile_t * vt ) {
+  for( int k=0; k<vt->nctx; k++ ) {
+    if( !fdgpu_ed25519_faulted( vt->ctx[k] ) ) continue;
+    for( ulong q=vt->pend_head; q<vt->pend_tail; q++ ) if( vt->pend[ q % vt->pend_cap ].k == k ) return -1;
+    fdgpu_ed25519_ctx_delete( vt->ctx[k] );
+    vt->ctx[k] = vt_ctx_new( vt );
+    vt->busy[k] = 0; vt->fault_seen[k] = 0;
+    if( !vt->ctx[k] ) return -2;
+  }
+  return 0;
+}
+
+void
+fdgpu_vtile_debug_fault( fdgpu_vtile_t * vt, int k ) { if( k >= 0 && k < vt->nctx ) fdgpu_ed25519_debug_fault( vt->ctx[k] ); }
+
+void
+fdgpu_vtile_gpu_metrics( fdgpu_vtile_t const * vt, fdgpu_vtile_gpu_metrics_t * out ) {
+  *out = vt->gm;
+  ulong f, i, infl = 0UL;
+  for( int k=0; k<vt->nctx; k++ ) { fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i ); infl += i; }
+  out->inflight = infl;
+  out->pending = vt->pend_tail - vt->pend_head;
+  out->overruns = vt->overruns;
+}
 
 int
 fdgpu_vtile_set_in_link( fdgpu_vtile_t * vt, fdgpu_mcache_t const * in_mc ) {
@@ -370,9 +479,13 @@ fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
     if( !vt->busy[k] ) continue;
     ulong f, i;
     fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i );
-    if( !i ) { vt->busy[k] = 0; vt->batch_ns = 0.875*vt->batch_ns + 0.125*(double)( now - vt->launch_ns[k] ); }
+    if( !i ) {
+      vt->busy[k] = 0; vt->batch_ns = 0.875*vt->batch_ns + 0.125*(double)( now - vt->launch_ns[k] );
+      vt->gm.lat_hist[ vt_lat_bucket( now - vt->launch_ns[k] ) ]++;
+    }
   }
   int f = vt->fill;
+  if( fdgpu_ed25519_faulted( vt->ctx[f] ) ) return 0;
   fdgpu_ed25519_pipeline_state( vt->ctx[f], &filling, &inflight );
   /* keep at least one staging slot free to accumulate in: with every slot
      in flight, each freed slot would be relaunched after a handful of
@@ -388,7 +501,7 @@ fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
   }
   vt_fence();
   if( fdgpu_ed25519_flush( vt->ctx[f] ) ) return 0;
-  vt->launch_ns[f] = now; vt->busy[f] = 1;
+  vt_launched( vt, f, now, filling );
   vt->fill = ( f + 1 ) % vt->nctx;
   return 1;
 }
@@ -401,6 +514,9 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   if( sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U || FDGPU_TXNM_HDR_SZ + in->payload_sz > sz ) return -4;
   vt_fence();
   if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_vtile_flush( vt ); return -2; }
+  /* a faulted context takes no more frags: fill the next healthy one (none: -3) */
+  for( int i=0; i<vt->nctx && fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ); i++ ) vt->fill = ( vt->fill + 1 ) % vt->nctx;
+  if( fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ) ) return -3;
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
   int rc;
   if( vt->zc ) {   /* the GPU copies the frag into dst itself (no host copy) */
@@ -414,17 +530,21 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   if( rc ) return rc;
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
   p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill;
+  p->bundle_id = in->bundle_id; p->payload_sz = in->payload_sz;
   vt->pend_tail++;
   ulong reserve = ( ( FDGPU_TXNM_HDR_SZ + in->payload_sz + 1UL ) & ~1UL ) + 852UL;
   vt->out_chunk = fdgpu_dcache_compact_next( vt->out_chunk, reserve, vt->chunk0, vt->wmark );
   return 0;
 }
 
-/* after_frag (fd_verify_tile.c:103-157) for one completed frag */
+/* after_frag (fd_verify_tile.c:103-157) for one completed frag.  The GPU
+   returned the code, the footprint and the dedup tag; with zero-copy intake
+   it also wrote the record (payload, txn_t_sz, fd_txn_t image) into the out
+   dcache, so this touches only the tcache and, for the overrun check, the
+   in mcache line. */
 static int
-vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, unsigned fp, fdgpu_vtile_done_t * d ) {
-  fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( vt->dcache + p->chunk * FDGPU_CHUNK_SZ );
-  uchar * payload = (uchar *)txnm + FDGPU_TXNM_HDR_SZ;
+vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, unsigned fp, ulong tag,
+          fdgpu_vtile_done_t * d ) {
   d->seq = p->seq; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
   if( vt->zc && vt->in_mc ) {
     /* zero-copy: the GPU read the frag at batch launch, after during_frag.
@@ -434,21 +554,17 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
     fdgpu_frag_meta_t m;
     if( fdgpu_mcache_poll( vt->in_mc, p->seq, &m ) != 0 ) { vt->overruns++; return FDGPU_VTILE_OVERRUN; }
   }
-  txnm->txn_t_sz = (unsigned short)fp;
-  int is_bundle = txnm->bundle_id != 0UL;
-  if( is_bundle && txnm->bundle_id != vt->bundle_id ) { vt->bundle_failed = 0; vt->bundle_id = txnm->bundle_id; }
+  fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( vt->dcache + p->chunk * FDGPU_CHUNK_SZ );
+  if( !vt->zc ) txnm->txn_t_sz = (unsigned short)fp;
+  int is_bundle = p->bundle_id != 0UL;
+  if( is_bundle && p->bundle_id != vt->bundle_id ) { vt->bundle_failed = 0; vt->bundle_id = p->bundle_id; }
   if( is_bundle && vt->bundle_failed ) { vt->metrics[3]++; return FDGPU_VTILE_BUNDLE_PEER_FAIL; }
   if( code == FDGPU_ERR_PARSE ) {
     if( is_bundle ) vt->bundle_failed = 1;
     vt->metrics[0]++;
     return FDGPU_VTILE_PARSE_FAIL;
   }
-  /* zero-copy: the GPU already wrote the fd_txn_t image behind the payload */
-  ulong t_off = ( FDGPU_TXNM_HDR_SZ + txnm->payload_sz + 1UL ) & ~1UL;
-  if( vt->zc ) img = (uchar const *)txnm + t_off;
   /* fd_txn_verify (fd_verify_tile.h:59-108): dedup query, verify, insert */
-  unsigned sig_off = (unsigned)img[2] | ((unsigned)img[3] << 8);
-  ulong tag = xxh64_64( vt->seed, payload + sig_off );
   int res = 0;   /* 0 success, 1 verify failed, 2 dedup */
   if( !is_bundle && fdgpu_tcache_query( vt->tcache, tag ) ) res = 2;
   else if( code != 0 ) res = 1;
@@ -460,6 +576,7 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
     return FDGPU_VTILE_VERIFY_FAIL;
   }
   /* publish: fd_txn_t behind the payload at a 2-byte boundary */
+  ulong t_off = ( FDGPU_TXNM_HDR_SZ + p->payload_sz + 1UL ) & ~1UL;
   if( !vt->zc ) memcpy( (uchar *)txnm + t_off, img, fp );
   d->sz = t_off + fp;                                  /* fd_txn_m_realized_footprint( txnm, 1, 0 ) */
   d->tag = is_bundle ? 0UL : tag;
@@ -480,23 +597,49 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
     if( lim > vt->batch ) lim = vt->batch;
     while( want < lim && vt->pend_head + want < vt->pend_tail &&
            vt->pend[ ( vt->pend_head + want ) % vt->pend_cap ].k == c ) want++;
-    ulong k = fdgpu_ed25519_poll_raw( vt->ctx[c], vt->p_tags, vt->p_codes, vt->zc ? NULL : vt->p_img, vt->p_fp, want, blocking );
-    if( !k ) break;
-    for( ulong i=0; i<k; i++ ) {
-      /* the records were written by the GPU / by non-temporal stores, so they are not in
-         this core's caches: prefetch a few frags ahead -- header + first signature lines at
-         distance 8, the fd_txn_t line (its offset needs the header) at distance 4 */
-      if( vt->pend_head + 8UL < vt->pend_tail ) {
-        uchar const * r = vt->dcache + vt->pend[ ( vt->pend_head + 8UL ) % vt->pend_cap ].chunk * FDGPU_CHUNK_SZ;
-        __builtin_prefetch( r ); __builtin_prefetch( r + 64 ); __builtin_prefetch( r + 128 );
+    if( fdgpu_ed25519_faulted( vt->ctx[c] ) ) {
+      /* the context's batches failed on the device: its frags will never get a
+         verdict.  Complete them, in order, as FDGPU_VTILE_GPU_FAULT (never
+         published, never blocked on); the caller treats that as the
+         reference's FD_LOG_ERR or recreates the context (fdgpu_vtile_recover). */
+      if( !vt->fault_seen[c] ) { vt->fault_seen[c] = 1; vt->gm.faults++; }
+      for( ulong i=0; i<want; i++ ) {
+        vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
+        fdgpu_vtile_done_t * d = &out[n];
+        d->seq = p->seq; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
+        d->result = FDGPU_VTILE_GPU_FAULT;
+        vt->gm.gpu_fault_frags++;
+        vt->pend_head++; n++;
       }
-      if( vt->pend_head + 4UL < vt->pend_tail ) {
-        uchar const * r = vt->dcache + vt->pend[ ( vt->pend_head + 4UL ) % vt->pend_cap ].chunk * FDGPU_CHUNK_SZ;
-        __builtin_prefetch( r + ( ( FDGPU_TXNM_HDR_SZ + ((fdgpu_txnm_t const *)r)->payload_sz + 1UL ) & ~1UL ) );
+      continue;
+    }
+    ulong k = fdgpu_ed25519_poll_raw( vt->ctx[c], vt->p_tags, vt->p_codes, vt->zc ? NULL : vt->p_img, vt->p_fp, vt->p_dtag,
+                                      want, blocking );
+    if( !k ) {
+      if( fdgpu_ed25519_faulted( vt->ctx[c] ) ) continue;   /* failed just now: complete its frags above */
+      break;
+    }
+    for( ulong i=0; i<k; i++ ) {
+      if( vt->p_tags[i] != vt->pend_head ) {   /* completions must come back in submission order */
+        fprintf( stderr, "fdgpu_vtile_after_frags: completion tag %lu != pending frag %lu\n", vt->p_tags[i], vt->pend_head );
+        abort();
+      }
+      /* the random accesses of after_frag are the tcache map slots (of this tag, and of the
+         tag the insert evicts) and, with an in link, the frag's mcache line: start them a
+         few completions ahead */
+      if( i + 8UL < k ) {
+        tc_prefetch( vt->tcache, vt->p_dtag[ i + 8UL ], 8UL );
+        if( vt->in_mc ) __builtin_prefetch( &vt->in_mc->line[ vt->pend[ ( vt->pend_head + 8UL ) % vt->pend_cap ].seq
+                                                               & ( vt->in_mc->depth - 1UL ) ] );
+      }
+      if( !vt->zc && vt->pend_head + 4UL < vt->pend_tail ) {   /* host-copied records: the header line */
+        uchar * r = vt->dcache + vt->pend[ ( vt->pend_head + 4UL ) % vt->pend_cap ].chunk * FDGPU_CHUNK_SZ;
+        __builtin_prefetch( r, 1 );
       }
       vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
       /* tags are the pending counter: completions come back in order */
-      out[n].result = vt_after( vt, p, (int)vt->p_codes[i], vt->p_img + i*FDGPU_TXN_IMG_STRIDE, vt->p_fp[i], &out[n] );
+      out[n].result = vt_after( vt, p, (int)vt->p_codes[i], vt->p_img + i*FDGPU_TXN_IMG_STRIDE, vt->p_fp[i],
+                                vt->p_dtag[i], &out[n] );
       vt->pend_head++; n++;
     }
     blocking = 0;
@@ -504,81 +647,25 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
   return n;
 }
 
-/* ---- streaming benchmark -------------------------------------------- */
+/* ---- the configs[4] stream: one producer link, T verify tiles ----------
+   The reference wires the verify stage as one QUIC out link read by every
+   verify tile: tile i takes the frags with seq % T == i (before_frag,
+   fd_verify_tile.c:47-48) over an UNRELIABLE, overrunnable in link
+   (topology.c:167-170).  Here the link -- mcache, in dcache prefilled with
+   one fd_txn_m_t record per distinct payload (what QUIC reassembly leaves),
+   the per-tile fseqs and the per-tile results -- is one memory region: a
+   shared file (/dev/shm) when the tiles live in several processes (one per
+   GPU; tile i drives GPU i % G, so process g runs the tiles i % G == g), or
+   private memory for a single process.  The producer (a thread of the
+   creating process) stands in for the QUIC tiles: the timed loop only
+   publishes metadata, frag seq pointing at payload seq % n_payload.
+   Reliable links (credit based: the producer stays depth/2 ahead of the
+   slowest tile) lose nothing; unreliable ones never wait and a tile that
+   falls a lap behind is overrun: it resumes at the seq it found
+   (fd_stem.c:590-596, 676-688) and the frags it skipped are counted. */
 
-typedef struct {
-  /* shared */
-  fdgpu_mcache_t *       mc;
-  uchar *                in_dcache;
-  ulong                  in_chunk0, in_wmark;
-  ulong                  n_frags;
-  int                    tiles;
-  struct { _Atomic ulong v; uchar pad[56]; } * fseq;   /* per tile, own cache line: next seq it has yet to consume */
-  _Atomic int            go, fail, ready;
-  ulong *                lh;          /* merged latency histogram (lh_idx buckets) */
-  ulong                  lmax;        /* max latency, ns */
-  unsigned char const *  payload; unsigned int const * off; unsigned short const * sz; ulong n_payload;
-  ulong *                frag_chunk;  /* in dcache chunk of payload p's prefilled frag record */
-  double                 rate_fps;
-  ulong                  depth;
-  ulong                  t_start, t_end;
-  _Atomic ulong          t_last;
-  _Atomic ulong          sigs, published, overruns;
-  _Atomic ulong          ns[4];        /* summed over tiles: during_frag, after_frags, housekeep, loop total */
-  ulong                  metrics[5];
-  pthread_mutex_t        mu;
-  int                    device; ulong batch_txn, max_inflight;
-  int                    zc;          /* zero-copy intake: tiles leave frags in the in dcache */
-} sb_t;
-
-/* The producer stands in for the QUIC tiles: every distinct payload is
-   written once, before the run, into the in dcache as an fd_txn_m_t frag
-   record (as the NIC / QUIC reassembly would have left it), and the
-   timed loop only publishes metadata -- frag seq points at payload
-   seq % n_payload.  The link is reliable (credit based): the producer
-   runs at most depth/2 frags ahead of the slowest tile, re-reading the
-   tiles' fseqs only when its cached credits run out. */
-static void * sb_producer( void * _s ) {
-  sb_t * s = (sb_t *)_s;
-  while( !atomic_load( &s->go ) ) ;
-  ulong t0 = now_ns();
-  s->t_start = t0;
-  ulong cr_until = 0UL;                     /* may publish seq < cr_until */
-  for( ulong seq=0; seq<s->n_frags; seq++ ) {
-    ulong t_wait = 0UL;
-    while( seq >= cr_until ) {
-      if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) return NULL;
-      if( !t_wait ) t_wait = now_ns();
-      else if( now_ns() - t_wait > 30000000000UL ) {            /* watchdog: 30 s without credits */
-        fprintf( stderr, "fdgpu_stream_bench: producer starved of credits at seq %lu\n", seq );
-        atomic_store( &s->fail, 4 ); return NULL;
-      }
-      ulong lo = ~0UL;
-      for( int t=0; t<s->tiles; t++ ) { ulong f = atomic_load_explicit( &s->fseq[t].v, memory_order_acquire ); if( f < lo ) lo = f; }
-      cr_until = lo + s->depth/2;
-    }
-    if( s->rate_fps > 0. ) {
-      ulong due = t0 + (ulong)( (double)seq * 1e9 / s->rate_fps );
-      while( now_ns() < due ) ;
-    }
-    ulong p = seq % s->n_payload;
-    ulong ts = now_ns();
-    fdgpu_mcache_publish( s->mc, seq, 0UL, (unsigned)s->frag_chunk[p], (unsigned)( FDGPU_TXNM_HDR_SZ + s->sz[p] ), ts, ts );
-  }
-  return NULL;
-}
-
-typedef struct { sb_t * s; int idx; } sb_tile_arg_t;
-
-/* credit a tile returns to the producer: every seq below it may be
-   overwritten.  With zero-copy intake a frag's bytes must survive until
-   the GPU has read them, so the credit stops at the oldest frag still
-   pending in the tile. */
-static void sb_credit( sb_t * s, int idx, fdgpu_vtile_t const * vt, ulong seq ) {
-  ulong c = seq;
-  if( s->zc ) { ulong o = fdgpu_vtile_oldest_pending_seq( vt ); if( o < c ) c = o; }
-  atomic_store_explicit( &s->fseq[idx].v, c, memory_order_release );
-}
+#define LINK_MAGIC    0xfd6e11c0ffee0002UL
+#define LINK_TILE_MAX 64
 
 /* Latency histogram (per tile, merged at the end): log-linear buckets,
    64 per octave (< 1.6 % wide), exact below 64 ns. */
@@ -602,8 +689,237 @@ static double lh_quantile( ulong const * h, ulong tot, double q ) {
   return lh_val( LH_N - 1UL );
 }
 
-static void sb_account( sb_t * s, fdgpu_vtile_t * vt, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs,
-                        ulong * lh, ulong * lmax ) {
+typedef struct {                 /* one tile's results, written once when it finishes */
+  ulong verdicts;                /* own frags returned by after_frags (any result) */
+  ulong lost;                    /* own frags skipped by polling / reading overruns (unreliable link) */
+  ulong overruns;                /* of the verdicts: FDGPU_VTILE_OVERRUN (overwritten before the GPU read it) */
+  ulong sigs, t_last, lmax;
+  ulong metrics[5];
+  ulong ns[4];                   /* during_frag intake (mcache polls + submit), after_frags, housekeep, whole loop */
+  fdgpu_vtile_gpu_metrics_t gm;
+  ulong device;
+} link_res_t;
+
+typedef struct {
+  _Atomic ulong magic;           /* set last by the creator (release) */
+  ulong         total_sz;
+  fdgpu_stream_cfg_t cfg;
+  ulong         depth, n_payload, in_bytes;
+  ulong         off_mcache, off_dcache, off_chunk, off_sz, off_res, off_hist;
+  _Atomic ulong joined, tiles_ready, tiles_done, go, fail;
+  ulong         t_start;
+  struct { _Atomic ulong v; uchar pad[56]; } fseq[ LINK_TILE_MAX ];   /* next seq each tile has yet to consume */
+} link_hdr_t;
+
+struct fdgpu_link {
+  link_hdr_t *     h;
+  uchar *          base;
+  ulong            sz;
+  int              shared, registered;
+  mc_line_t *      line;
+  uchar *          dcache;
+  unsigned *       chunk;
+  unsigned short * psz;
+  link_res_t *     res;
+  ulong *          hist;
+  fdgpu_mcache_t   mc;           /* local view of the shared lines (the tiles' in_mc) */
+};
+
+static ulong al64( ulong x ) { return ( x + 63UL ) & ~63UL; }
+
+static void link_view( fdgpu_link_t * l ) {
+  link_hdr_t * h = l->h;
+  l->line   = (mc_line_t *)( l->base + h->off_mcache );
+  l->dcache = l->base + h->off_dcache;
+  l->chunk  = (unsigned *)( l->base + h->off_chunk );
+  l->psz    = (unsigned short *)( l->base + h->off_sz );
+  l->res    = (link_res_t *)( l->base + h->off_res );
+  l->hist   = (ulong *)( l->base + h->off_hist );
+  l->mc.depth = h->depth; l->mc.line = l->line; l->mc.own = 0;
+}
+
+fdgpu_link_t *
+fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const * payload, unsigned const * off,
+                unsigned short const * sz, ulong n_payload, ulong mcache_depth ) {
+  if( !cfg || cfg->tiles < 1 || cfg->tiles > LINK_TILE_MAX || cfg->gpus < 1 || cfg->gpus > cfg->tiles || !n_payload ||
+      !cfg->n_frags || !cfg->batch_txn || mcache_depth < 64 ) return NULL;
+  ulong depth = pow2_up( mcache_depth );
+  ulong in_bytes = 0UL;
+  for( ulong p=0; p<n_payload; p++ ) {
+    if( sz[p] > 1232U ) return NULL;
+    in_bytes += ( ( FDGPU_TXNM_HDR_SZ + sz[p] + 127UL ) >> 7 ) << 7;
+  }
+  ulong T = (ulong)cfg->tiles;
+  ulong o = al64( sizeof(link_hdr_t) );
+  ulong off_mcache = o;  o = al64( o + depth * sizeof(mc_line_t) );
+  ulong off_chunk  = o;  o = al64( o + n_payload * sizeof(unsigned) );
+  ulong off_sz     = o;  o = al64( o + n_payload * sizeof(unsigned short) );
+  ulong off_res    = o;  o = al64( o + T * sizeof(link_res_t) );
+  ulong off_hist   = o;  o = al64( o + T * LH_N * sizeof(ulong) );
+  o = ( o + 4095UL ) & ~4095UL;
+  ulong off_dcache = o;  o += in_bytes + 4096UL;
+  ulong total = ( o + 4095UL ) & ~4095UL;
+  uchar * base;
+  int shared = path != NULL;
+  if( shared ) {
+    int fd = open( path, O_RDWR | O_CREAT | O_EXCL, 0600 );
+    if( fd < 0 ) return NULL;
+    if( ftruncate( fd, (off_t)total ) ) { close( fd ); unlink( path ); return NULL; }
+    base = (uchar *)mmap( NULL, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0 );
+    close( fd );
+    if( base == MAP_FAILED ) { unlink( path ); return NULL; }
+  } else {
+    base = (uchar *)mmap( NULL, total, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0 );
+    if( base == MAP_FAILED ) return NULL;
+  }
+  fdgpu_link_t * l = (fdgpu_link_t *)calloc( 1, sizeof(fdgpu_link_t) );
+  if( !l ) { munmap( base, total ); return NULL; }
+  l->base = base; l->sz = total; l->shared = shared; l->h = (link_hdr_t *)base;
+  link_hdr_t * h = l->h;
+  memset( (void *)h, 0, sizeof(link_hdr_t) );
+  h->total_sz = total; h->cfg = *cfg; h->depth = depth; h->n_payload = n_payload; h->in_bytes = in_bytes;
+  h->off_mcache = off_mcache; h->off_dcache = off_dcache; h->off_chunk = off_chunk; h->off_sz = off_sz;
+  h->off_res = off_res; h->off_hist = off_hist;
+  link_view( l );
+  mc_init_lines( l->line, depth, 0UL );
+  memset( (void *)l->res, 0, T * sizeof(link_res_t) );
+  memset( (void *)l->hist, 0, T * LH_N * sizeof(ulong) );
+  for( ulong p=0, c=0; p<n_payload; p++ ) {
+    fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( l->dcache + c * FDGPU_CHUNK_SZ );
+    memset( txnm, 0, FDGPU_TXNM_HDR_SZ );
+    txnm->payload_sz = sz[p];
+    memcpy( (uchar *)txnm + FDGPU_TXNM_HDR_SZ, payload + off[p], sz[p] );
+    l->chunk[p] = (unsigned)c; l->psz[p] = sz[p];
+    c = fdgpu_dcache_compact_next( c, FDGPU_TXNM_HDR_SZ + sz[p], 0UL, ~0UL );
+  }
+  atomic_store_explicit( &h->joined, 1UL, memory_order_relaxed );
+  atomic_store_explicit( &h->magic, LINK_MAGIC, memory_order_release );
+  return l;
+}
+
+fdgpu_link_t *
+fdgpu_link_join( char const * path, double timeout_s ) {
+  ulong t0 = now_ns(), lim = (ulong)( timeout_s * 1e9 );
+  int fd = -1;
+  for(;;) {                                    /* the creator may not have made the file yet */
+    fd = open( path, O_RDWR );
+    if( fd >= 0 ) {
+      struct stat st;
+      if( !fstat( fd, &st ) && (ulong)st.st_size >= sizeof(link_hdr_t) ) {
+        link_hdr_t * h = (link_hdr_t *)mmap( NULL, sizeof(link_hdr_t), PROT_READ, MAP_SHARED, fd, 0 );
+        if( h != MAP_FAILED ) {
+          int ok = atomic_load_explicit( &h->magic, memory_order_acquire ) == LINK_MAGIC;
+          ulong total = h->total_sz;
+          munmap( (void *)h, sizeof(link_hdr_t) );
+          if( ok && (ulong)st.st_size >= total ) {
+            uchar * base = (uchar *)mmap( NULL, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0 );
+            close( fd );
+            if( base == MAP_FAILED ) return NULL;
+            fdgpu_link_t * l = (fdgpu_link_t *)calloc( 1, sizeof(fdgpu_link_t) );
+            if( !l ) { munmap( base, total ); return NULL; }
+            l->base = base; l->sz = total; l->shared = 1; l->h = (link_hdr_t *)base;
+            link_view( l );
+            atomic_fetch_add( &l->h->joined, 1UL );
+            return l;
+          }
+        }
+      }
+      close( fd );
+    }
+    if( now_ns() - t0 > lim ) return NULL;
+    usleep( 2000 );
+  }
+}
+
+void
+fdgpu_link_delete( fdgpu_link_t * l ) {
+  if( !l ) return;
+  if( l->registered ) fdgpu_host_unregister( l->dcache );
+  munmap( l->base, l->sz );
+  free( l );
+}
+
+ulong fdgpu_link_joined( fdgpu_link_t const * l ) { return atomic_load( &l->h->joined ); }
+fdgpu_mcache_t * fdgpu_link_mcache( fdgpu_link_t * l ) { return &l->mc; }
+unsigned char *  fdgpu_link_dcache( fdgpu_link_t * l ) { return l->dcache; }
+
+/* the reference's verify-tile -> GPU binding: tile i drives GPU i % G and
+   runs in that GPU's process; the tiles of process proc, ascending */
+int
+fdgpu_link_tiles_of( int tiles, int gpus, int proc, int * out ) {
+  int n = 0;
+  if( tiles < 1 || gpus < 1 || proc < 0 || proc >= gpus ) return 0;
+  for( int i=0; i<tiles; i++ ) if( i % gpus == proc ) out[n++] = i;
+  return n;
+}
+void  fdgpu_link_cfg( fdgpu_link_t const * l, fdgpu_stream_cfg_t * cfg ) { *cfg = l->h->cfg; }
+
+static void * link_producer( void * _l ) {
+  fdgpu_link_t * l = (fdgpu_link_t *)_l;
+  link_hdr_t * h = l->h;
+  fdgpu_stream_cfg_t const * c = &h->cfg;
+  ulong T = (ulong)c->tiles, mask = h->depth - 1UL;
+  ulong t_wait0 = now_ns();
+  while( atomic_load( &h->tiles_ready ) < T ) {   /* every tile has its GPU context */
+    if( atomic_load( &h->fail ) ) return NULL;
+    if( now_ns() - t_wait0 > 300000000000UL ) {
+      fprintf( stderr, "fdgpu_link: producer waited 300 s for %lu tiles (%lu ready)\n", T, atomic_load( &h->tiles_ready ) );
+      atomic_store( &h->fail, 6 ); return NULL;
+    }
+  }
+  ulong t0 = now_ns();
+  h->t_start = t0;
+  atomic_store_explicit( &h->go, 1UL, memory_order_release );
+  ulong cr_until = 0UL;                     /* may publish seq < cr_until */
+  for( ulong seq=0; seq<c->n_frags; seq++ ) {
+    if( c->reliable ) {
+      ulong t_wait = 0UL;
+      while( seq >= cr_until ) {
+        if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) return NULL;
+        if( !t_wait ) t_wait = now_ns();
+        else if( now_ns() - t_wait > 30000000000UL ) {            /* watchdog: 30 s without credits */
+          fprintf( stderr, "fdgpu_link: producer starved of credits at seq %lu\n", seq );
+          atomic_store( &h->fail, 4 ); return NULL;
+        }
+        ulong lo = ~0UL;
+        for( ulong t=0; t<T; t++ ) { ulong f = atomic_load_explicit( &h->fseq[t].v, memory_order_acquire ); if( f < lo ) lo = f; }
+        cr_until = lo + h->depth/2;
+      }
+    }
+    if( c->rate_fps > 0. ) {
+      ulong due = t0 + (ulong)( (double)seq * 1e9 / c->rate_fps );
+      while( now_ns() < due ) ;
+    }
+    ulong p = seq % h->n_payload;
+    unsigned ts = (unsigned)now_ns();
+    mc_publish( &l->line[ seq & mask ], seq, 0UL, l->chunk[p], (unsigned)( FDGPU_TXNM_HDR_SZ + l->psz[p] ), ts, ts );
+  }
+  return NULL;
+}
+
+typedef struct { fdgpu_link_t * l; int idx, device; } link_tile_arg_t;
+
+/* credit a tile returns to the producer: every seq below it may be
+   overwritten.  With zero-copy intake a frag's bytes must survive until
+   the GPU has read them, so the credit stops at the oldest frag still
+   pending in the tile. */
+static void link_credit( link_hdr_t * h, int idx, fdgpu_vtile_t const * vt, ulong seq ) {
+  ulong c = seq;
+  if( h->cfg.zero_copy ) { ulong o = fdgpu_vtile_oldest_pending_seq( vt ); if( o < c ) c = o; }
+  atomic_store_explicit( &h->fseq[idx].v, c, memory_order_release );
+}
+
+/* own frags (q % T == idx) in [a, b) */
+static ulong own_in( ulong a, ulong b, ulong T, ulong idx ) {
+  if( b <= a ) return 0UL;
+  ulong ca = a > idx ? ( a - idx + T - 1UL ) / T : 0UL;   /* #own q < a */
+  ulong cb = b > idx ? ( b - idx + T - 1UL ) / T : 0UL;   /* #own q < b */
+  return cb - ca;
+}
+
+static void
+link_account( fdgpu_link_t * l, fdgpu_vtile_t * vt, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs, ulong * lh,
+              ulong * lmax, ulong * t_last ) {
   ulong t = now_ns();
   for( ulong i=0; i<n; i++ ) {
     ulong lat = t - d[i].tsorig;
@@ -614,70 +930,85 @@ static void sb_account( sb_t * s, fdgpu_vtile_t * vt, fdgpu_vtile_done_t const *
       *sigs += pl[0];
     }
   }
-  if( n ) {
-    ulong prev = atomic_load( &s->t_last );
-    while( t > prev && !atomic_compare_exchange_weak( &s->t_last, &prev, t ) ) ;
-  }
+  (void)l;
+  if( n ) *t_last = t;
 }
 
-static void * sb_tile( void * _a ) {
-  sb_tile_arg_t * a = (sb_tile_arg_t *)_a;
-  sb_t * s = a->s;
+static void * link_tile( void * _a ) {
+  link_tile_arg_t * a = (link_tile_arg_t *)_a;
+  fdgpu_link_t * l = a->l;
+  link_hdr_t * h = l->h;
+  fdgpu_stream_cfg_t const * c = &h->cfg;
   int idx = a->idx;
-  fdgpu_vtile_t * vt = fdgpu_vtile_new( s->device, s->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
-                                        ( 6UL*s->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
-  if( !vt ) { atomic_store( &s->fail, 1 ); return NULL; }
-  if( s->zc && fdgpu_vtile_set_in_link( vt, s->mc ) ) { atomic_store( &s->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL; }
-  atomic_fetch_add( &s->ready, 1 );              /* the producer starts once every tile has its GPU context */
+  ulong const T = (ulong)c->tiles, mask = h->depth - 1UL, n_frags = c->n_frags;
+  fdgpu_vtile_t * vt = fdgpu_vtile_new( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
+                                        ( 6UL*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
+  if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
+  if( c->zero_copy && fdgpu_vtile_set_in_link( vt, &l->mc ) ) { atomic_store( &h->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL; }
+  atomic_fetch_add( &h->tiles_ready, 1UL );    /* the producer starts once every tile has its GPU context */
+  while( !atomic_load_explicit( &h->go, memory_order_acquire ) ) if( atomic_load( &h->fail ) ) { fdgpu_vtile_delete( vt ); return NULL; }
   ulong dcap = 4096UL;
   fdgpu_vtile_done_t * done = (fdgpu_vtile_done_t *)malloc( dcap * sizeof(fdgpu_vtile_done_t) );
-  ulong * lh = (ulong *)calloc( LH_N, sizeof(ulong) ), lmax = 0UL;
-  ulong const T = (ulong)s->tiles;
-  ulong sigs = 0UL, mine = 0UL, got = 0UL;
-  for( ulong q=0; q<s->n_frags; q++ ) mine += ( q % T ) == (ulong)idx;
+  ulong * lh = (ulong *)calloc( LH_N, sizeof(ulong) ), lmax = 0UL, t_last = 0UL;
+  ulong sigs = 0UL, got = 0UL, lost = 0UL;
+  ulong mine = own_in( 0UL, n_frags, T, (ulong)idx );
   ulong seq = 0UL;
   ulong last_seq = ~0UL, last_got = ~0UL, t_prog = now_ns();
   ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, t_begin = now_ns();
-  while( got < mine ) {
-    if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) break;
+  while( got + lost < mine ) {
+    if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
     ulong t0 = now_ns();
     if( seq != last_seq || got != last_got ) { last_seq = seq; last_got = got; t_prog = t0; }
     else if( t0 - t_prog > 30000000000UL ) {                      /* watchdog: 30 s without progress */
       ulong filling = 0, inflight = 0;
       fdgpu_vtile_pipeline_state( vt, &filling, &inflight );
-      fprintf( stderr, "fdgpu_stream_bench: tile %d stalled: seq %lu got %lu/%lu pending %lu filling %lu inflight %lu\n",
-               idx, seq, got, mine, fdgpu_vtile_pending( vt ), filling, inflight );
-      atomic_store( &s->fail, 5 ); break;
+      fprintf( stderr, "fdgpu_link: tile %d stalled: seq %lu got %lu lost %lu / %lu pending %lu filling %lu inflight %lu\n",
+               idx, seq, got, lost, mine, fdgpu_vtile_pending( vt ), filling, inflight );
+      atomic_store( &h->fail, 5 ); break;
     }
-    /* intake: up to 64 frags per pass.  Every seq's mcache line is read, as
-       the stem loop does; before_frag keeps seq % tiles == idx. */
+    /* intake: up to 64 lines per pass.  Every seq's line is read, as the stem
+       loop does; before_frag keeps seq % T == idx. */
     int drain = 0;
-    for( int k=0; k<64 && seq < s->n_frags; k++ ) {
-      fdgpu_frag_meta_t m;
-      int r = fdgpu_mcache_poll( s->mc, seq, &m );
+    for( int k=0; k<64 && seq < n_frags; k++ ) {
+      mc_line_t const * ln = &l->line[ seq & mask ];
+      if( ( seq % T ) != (ulong)idx ) {                             /* before_frag filters: the seq alone decides */
+        ulong s0 = atomic_load_explicit( (_Atomic ulong *)&ln->seq, memory_order_acquire );
+        if( s0 == seq ) { seq++; continue; }
+        if( (long)( s0 - seq ) < 0 ) break;                         /* not yet published */
+        if( c->reliable ) { atomic_store( &h->fail, 3 ); break; }
+        lost += own_in( seq, s0, T, (ulong)idx ); seq = s0;          /* overrun while polling: resume there */
+        continue;
+      }
+      fdgpu_frag_meta_t m; ulong found;
+      int r = mc_poll( ln, seq, &m, &found );
       if( r > 0 ) break;
-      if( r < 0 ) { atomic_fetch_add( &s->overruns, 1 ); atomic_store( &s->fail, 3 ); break; }
-      if( ( seq % T ) == (ulong)idx ) {                             /* before_frag round robin */
-        int rc = fdgpu_vtile_during_frag( vt, s->in_dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, seq, m.tsorig );
-        if( rc == -2 ) { drain = 1; break; }                        /* staging full: drain, retry this seq */
-        if( rc ) { atomic_store( &s->fail, 2 ); break; }
-        /* this tile's next frag is usually published already: start its cold lines */
-        fdgpu_frag_meta_t nx;
-        if( seq + T < s->n_frags && !fdgpu_mcache_poll( s->mc, seq + T, &nx ) ) {
-          uchar const * pf = s->in_dcache + (ulong)nx.chunk * FDGPU_CHUNK_SZ;
-          for( ulong o=0UL; o<nx.sz; o+=64UL ) __builtin_prefetch( pf + o );
+      if( r < 0 ) {
+        if( c->reliable ) { atomic_store( &h->fail, 3 ); break; }
+        lost += own_in( seq, found, T, (ulong)idx ); seq = found;    /* overrun while polling / reading */
+        continue;
+      }
+      int rc = fdgpu_vtile_during_frag( vt, l->dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, seq,
+                                        ts_decomp( m.tsorig, now_ns() ) );
+      if( rc == -2 ) { drain = 1; break; }                          /* staging full: drain, retry this seq */
+      if( rc ) { fprintf( stderr, "fdgpu_link: tile %d during_frag %d\n", idx, rc ); atomic_store( &h->fail, 2 ); break; }
+      /* this tile's next frag is usually published already: start its cold lines */
+      if( seq + T < n_frags ) {
+        mc_line_t const * nl = &l->line[ ( seq + T ) & mask ];
+        if( atomic_load_explicit( (_Atomic ulong *)&nl->seq, memory_order_relaxed ) == seq + T ) {
+          uchar const * pf = l->dcache + (ulong)nl->chunk * FDGPU_CHUNK_SZ;
+          __builtin_prefetch( pf ); __builtin_prefetch( pf + 64 );
         }
       }
       seq++;
-      if( !(seq & 63UL) || seq==s->n_frags ) sb_credit( s, idx, vt, seq );   /* batched credit return */
+      if( c->reliable && ( !(seq & 63UL) || seq == n_frags ) ) link_credit( h, idx, vt, seq );   /* batched credit return */
     }
     ulong t1 = now_ns();
     ns_in += t1 - t0;
-    if( atomic_load_explicit( &s->fail, memory_order_relaxed ) ) break;
-    if( drain ) {
+    if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
+    if( drain || ( seq >= n_frags && fdgpu_vtile_pending( vt ) ) ) {
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
-      sb_account( s, vt, done, n, &sigs, lh, &lmax ); got += n;
-      if( s->zc ) sb_credit( s, idx, vt, seq );
+      link_account( l, vt, done, n, &sigs, lh, &lmax, &t_last ); got += n;
+      if( c->reliable && c->zero_copy ) link_credit( h, idx, vt, seq );
       ns_after += now_ns() - t1;
       continue;
     }
@@ -685,89 +1016,115 @@ static void * sb_tile( void * _a ) {
        (the HIP runtime calls behind them take locks shared by all tiles) */
     if( t1 - t_hk >= 10000UL ) {
       t_hk = t1;
-      fdgpu_vtile_housekeep( vt, s->max_inflight );                 /* adaptive batching */
+      fdgpu_vtile_housekeep( vt, c->max_inflight );                 /* adaptive batching */
       ulong t2 = now_ns();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
-      sb_account( s, vt, done, n, &sigs, lh, &lmax ); got += n;
-      if( s->zc && n ) sb_credit( s, idx, vt, seq );
+      link_account( l, vt, done, n, &sigs, lh, &lmax, &t_last ); got += n;
+      if( c->reliable && c->zero_copy && n ) link_credit( h, idx, vt, seq );
       ns_hk += t2 - t1; ns_after += now_ns() - t2;
     }
   }
   ulong t_end = now_ns();
-  atomic_fetch_add( &s->ns[0], ns_in );     atomic_fetch_add( &s->ns[1], ns_after );
-  atomic_fetch_add( &s->ns[2], ns_hk );     atomic_fetch_add( &s->ns[3], t_end - t_begin );
-  ulong m5[5]; fdgpu_vtile_metrics( vt, m5 );
-  atomic_fetch_add( &s->overruns, fdgpu_vtile_overruns( vt ) );
-  pthread_mutex_lock( &s->mu );
-  for( int i=0; i<5; i++ ) s->metrics[i] += m5[i];
-  for( ulong i=0UL; i<LH_N; i++ ) s->lh[i] += lh[i];
-  if( lmax > s->lmax ) s->lmax = lmax;
-  pthread_mutex_unlock( &s->mu );
-  atomic_fetch_add( &s->sigs, sigs );
+  link_res_t * r = &l->res[idx];
+  r->verdicts = got; r->lost = lost; r->overruns = fdgpu_vtile_overruns( vt );
+  r->sigs = sigs; r->t_last = t_last; r->lmax = lmax;
+  fdgpu_vtile_metrics( vt, r->metrics );
+  r->ns[0] = ns_in; r->ns[1] = ns_after; r->ns[2] = ns_hk; r->ns[3] = t_end - t_begin;
+  fdgpu_vtile_gpu_metrics( vt, &r->gm );
+  r->device = (ulong)a->device;
+  memcpy( l->hist + (ulong)idx * LH_N, lh, LH_N * sizeof(ulong) );
+  atomic_fetch_add_explicit( &h->tiles_done, 1UL, memory_order_release );
   free( done ); free( lh );
   fdgpu_vtile_delete( vt );
   return NULL;
 }
 
 int
+fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
+  link_hdr_t * h = l->h;
+  fdgpu_stream_cfg_t const * c = &h->cfg;
+  if( proc < 0 || proc >= c->gpus ) return -1;
+  if( c->zero_copy && !l->registered ) {
+    if( fdgpu_host_register( l->dcache, h->in_bytes + 4096UL ) ) { atomic_store( &h->fail, 7 ); return -3; }
+    l->registered = 1;
+  }
+  pthread_t prod, th[ LINK_TILE_MAX ];
+  link_tile_arg_t args[ LINK_TILE_MAX ];
+  int mine[ LINK_TILE_MAX ];
+  int nt = fdgpu_link_tiles_of( c->tiles, c->gpus, proc, mine );   /* tile i drives GPU i % G: this process's tiles */
+  for( int t=0; t<nt; t++ ) {
+    args[t].l = l; args[t].idx = mine[t]; args[t].device = device;
+    pthread_create( &th[t], NULL, link_tile, &args[t] );
+  }
+  if( run_producer ) pthread_create( &prod, NULL, link_producer, l );
+  if( run_producer ) pthread_join( prod, NULL );
+  for( int t=0; t<nt; t++ ) pthread_join( th[t], NULL );
+  int rc = (int)atomic_load( &h->fail );
+  return rc ? -rc - 10 : 0;
+}
+
+int
+fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st ) {
+  link_hdr_t * h = l->h;
+  fdgpu_stream_cfg_t const * c = &h->cfg;
+  ulong T = (ulong)c->tiles, t0 = now_ns(), lim = (ulong)( timeout_s * 1e9 );
+  while( atomic_load_explicit( &h->tiles_done, memory_order_acquire ) < T ) {
+    if( atomic_load( &h->fail ) ) return -(int)atomic_load( &h->fail ) - 10;
+    if( now_ns() - t0 > lim ) return -2;
+    usleep( 1000 );
+  }
+  memset( st, 0, sizeof(*st) );
+  ulong * lh = (ulong *)calloc( LH_N, sizeof(ulong) );
+  if( !lh ) return -3;
+  ulong t_end = 0UL, lmax = 0UL;
+  for( ulong i=0; i<T; i++ ) {
+    link_res_t const * r = &l->res[i];
+    st->sigs += r->sigs; st->verdicts += r->verdicts; st->lost += r->lost; st->overruns += r->overruns;
+    for( int k=0; k<5; k++ ) st->metrics[k] += r->metrics[k];
+    for( int k=0; k<4; k++ ) st->tile_ns[k] += r->ns[k];
+    st->batches += r->gm.batches; st->batch_txns += r->gm.batch_txns;
+    if( r->gm.inflight_max > st->inflight_max ) st->inflight_max = r->gm.inflight_max;
+    for( ulong k=0; k<FDGPU_VTILE_LAT_BUCKETS; k++ ) st->gpu_lat_hist[k] += r->gm.lat_hist[k];
+    if( r->t_last > t_end ) t_end = r->t_last;
+    if( r->lmax > lmax ) lmax = r->lmax;
+    for( ulong k=0UL; k<LH_N; k++ ) lh[k] += l->hist[ i*LH_N + k ];
+  }
+  st->seconds = t_end > h->t_start ? (double)( t_end - h->t_start ) * 1e-9 : 0.;
+  st->frags = c->n_frags;
+  st->published = st->metrics[4];
+  st->frags_per_s = st->seconds > 0. ? (double)st->verdicts / st->seconds : 0.;
+  st->sigs_per_s  = st->seconds > 0. ? (double)st->sigs / st->seconds : 0.;
+  ulong tot = 0UL;
+  for( ulong k=0UL; k<LH_N; k++ ) tot += lh[k];
+  st->lat_p50_us = tot ? lh_quantile( lh, tot, 0.50 ) * 1e-3 : 0.;
+  st->lat_p99_us = tot ? lh_quantile( lh, tot, 0.99 ) * 1e-3 : 0.;
+  st->lat_max_us = (double)lmax * 1e-3;
+  st->tiles = c->tiles; st->gpus = c->gpus;
+  free( lh );
+  return 0;
+}
+
+/* private link, producer + every tile in this process on one device (G = 1) */
+int
+fdgpu_stream_run( int device, fdgpu_stream_cfg_t const * cfg, uchar const * payload, unsigned const * off,
+                  unsigned short const * sz, ulong n_payload, ulong mcache_depth, fdgpu_stream_stats_t * st ) {
+  fdgpu_stream_cfg_t c = *cfg;
+  c.gpus = 1;
+  fdgpu_link_t * l = fdgpu_link_new( NULL, &c, payload, off, sz, n_payload, mcache_depth );
+  if( !l ) return -1;
+  int rc = fdgpu_link_run( l, 0, device, 1 );
+  if( !rc ) rc = fdgpu_link_result( l, 60., st );
+  fdgpu_link_delete( l );
+  return rc;
+}
+
+int
 fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, unsigned short const * sz, ulong n_payload,
                     ulong n_frags, int tiles, ulong batch_txn, ulong max_inflight, ulong mcache_depth, double rate_fps,
                     int zero_copy, fdgpu_stream_stats_t * st ) {
-  if( tiles < 1 || tiles > 64 || !n_frags || !n_payload || !batch_txn || mcache_depth < 64 ) return -1;
-  sb_t * s = (sb_t *)calloc( 1, sizeof(sb_t) );
-  s->depth = pow2_up( mcache_depth );
-  s->mc = fdgpu_mcache_new( s->depth, 0UL );
-  /* in dcache: one prefilled fd_txn_m_t frag record per distinct payload */
-  ulong in_bytes = 0UL;
-  for( ulong p=0; p<n_payload; p++ ) in_bytes += ( ( FDGPU_TXNM_HDR_SZ + sz[p] + 127UL ) >> 7 ) << 7;
-  s->in_dcache = (uchar *)aligned_alloc( 128, in_bytes + 128UL );
-  s->frag_chunk = (ulong *)malloc( n_payload * sizeof(ulong) );
-  if( !s->in_dcache || !s->frag_chunk ) { free( s->in_dcache ); free( s->frag_chunk ); fdgpu_mcache_delete( s->mc ); free( s ); return -2; }
-  for( ulong p=0, c=0; p<n_payload; p++ ) {
-    fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( s->in_dcache + c * FDGPU_CHUNK_SZ );
-    memset( txnm, 0, FDGPU_TXNM_HDR_SZ );
-    txnm->payload_sz = sz[p];
-    memcpy( (uchar *)txnm + FDGPU_TXNM_HDR_SZ, payload + off[p], sz[p] );
-    s->frag_chunk[p] = c;
-    c = fdgpu_dcache_compact_next( c, FDGPU_TXNM_HDR_SZ + sz[p], 0UL, ~0UL );
-  }
-  s->n_frags = n_frags; s->tiles = tiles;
-  s->fseq = calloc( (size_t)tiles, sizeof(*s->fseq) );
-  s->lh = (ulong *)calloc( LH_N, sizeof(ulong) );
-  s->payload = payload; s->off = off; s->sz = sz; s->n_payload = n_payload; s->rate_fps = rate_fps;
-  s->device = device; s->batch_txn = batch_txn; s->max_inflight = max_inflight ? max_inflight : 2UL;
-  s->zc = zero_copy;
-  if( zero_copy && fdgpu_host_register( s->in_dcache, in_bytes + 128UL ) ) {
-    fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( s->frag_chunk ); free( (void *)s->fseq ); free( s->lh );
-    free( s ); return -3;
-  }
-  pthread_mutex_init( &s->mu, NULL );
-  pthread_t prod, th[64]; sb_tile_arg_t args[64];
-  for( int t=0; t<tiles; t++ ) { args[t].s = s; args[t].idx = t; pthread_create( &th[t], NULL, sb_tile, &args[t] ); }
-  pthread_create( &prod, NULL, sb_producer, s );
-  while( atomic_load( &s->ready ) < tiles && !atomic_load( &s->fail ) ) ;
-  atomic_store( &s->go, 1 );
-  pthread_join( prod, NULL );
-  for( int t=0; t<tiles; t++ ) pthread_join( th[t], NULL );
-  int rc = atomic_load( &s->fail );
-  memset( st, 0, sizeof(*st) );
-  if( !rc ) {
-    st->seconds = (double)( atomic_load( &s->t_last ) - s->t_start ) * 1e-9;
-    st->frags = n_frags; st->sigs = atomic_load( &s->sigs ); st->published = s->metrics[4];
-    st->frags_per_s = (double)n_frags / st->seconds;
-    st->sigs_per_s = (double)st->sigs / st->seconds;
-    ulong tot = 0UL;
-    for( ulong i=0UL; i<LH_N; i++ ) tot += s->lh[i];
-    st->lat_p50_us = tot ? lh_quantile( s->lh, tot, 0.50 ) * 1e-3 : 0.;
-    st->lat_p99_us = tot ? lh_quantile( s->lh, tot, 0.99 ) * 1e-3 : 0.;
-    st->lat_max_us = (double)s->lmax * 1e-3;
-    memcpy( st->metrics, s->metrics, sizeof(st->metrics) );
-    st->overruns = atomic_load( &s->overruns );
-    for( int i=0; i<4; i++ ) st->tile_ns[i] = atomic_load( &s->ns[i] );
-  }
-  if( zero_copy ) fdgpu_host_unregister( s->in_dcache );
-  fdgpu_mcache_delete( s->mc ); free( s->in_dcache ); free( s->frag_chunk ); free( (void *)s->fseq ); free( s->lh );
-  pthread_mutex_destroy( &s->mu );
-  free( s );
-  return rc ? -rc - 10 : 0;
+  fdgpu_stream_cfg_t c;
+  memset( &c, 0, sizeof(c) );
+  c.n_frags = n_frags; c.batch_txn = batch_txn; c.max_inflight = max_inflight ? max_inflight : 2UL; c.rate_fps = rate_fps;
+  c.tiles = tiles; c.gpus = 1; c.zero_copy = zero_copy; c.reliable = 1;
+  return fdgpu_stream_run( device, &c, payload, off, sz, n_payload, mcache_depth, st );
 }

@@ -47,7 +47,8 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_host_alloc", "fdgpu_host_free", "fdgpu_host_register", "fdgpu_host_unregister",
            "fdgpu_ed25519_submit_raw_gather",
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
-           "fdgpu_last_error")
+           "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_set_dedup",
+           "fdgpu_ed25519_set_record_fp_off", "fdgpu_last_error")
 
 _lib = None
 _lock = threading.Lock()
@@ -118,12 +119,28 @@ def load_library():
         L.fdgpu_ed25519_submit_raw.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ushort, ctypes.c_ulong]
         L.fdgpu_ed25519_poll_raw.restype = ctypes.c_ulong
         L.fdgpu_ed25519_poll_raw.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                             ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int]
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int]
+        L.fdgpu_ed25519_set_dedup.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_ulong]
+        L.fdgpu_ed25519_set_record_fp_off.restype = ctypes.c_int
+        L.fdgpu_ed25519_set_record_fp_off.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.fdgpu_ed25519_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.fdgpu_ed25519_set_small_batch_max.restype = ctypes.c_ulong
         L.fdgpu_ed25519_set_small_batch_max.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
         L.fdgpu_ed25519_kernel_ms.restype = ctypes.c_float
         L.fdgpu_ed25519_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.fdgpu_ed25519_pipeline_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.fdgpu_ed25519_faulted.restype = ctypes.c_int
+        L.fdgpu_ed25519_faulted.argtypes = [ctypes.c_void_p]
+        L.fdgpu_ed25519_debug_fault.argtypes = [ctypes.c_void_p]
+        L.fdgpu_ed25519_submit_raw_ref.restype = ctypes.c_int
+        L.fdgpu_ed25519_submit_raw_ref.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ushort,
+                                                   ctypes.c_ulong]
+        L.fdgpu_ed25519_submit_raw_gather.restype = ctypes.c_int
+        L.fdgpu_ed25519_submit_raw_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_ushort, ctypes.c_ushort, ctypes.c_ushort, ctypes.c_ulong]
+        L.fdgpu_host_alloc.restype = ctypes.c_void_p
+        L.fdgpu_host_alloc.argtypes = [ctypes.c_ulong]
+        L.fdgpu_host_free.argtypes = [ctypes.c_void_p]
         L.fdgpu_last_error.restype = ctypes.c_char_p
         _lib = L
         return L
@@ -325,15 +342,29 @@ class Engine:
             raise RuntimeError(f"fdgpu_ed25519_submit_raw: {rc} {last_error()}")
         return rc
 
-    def poll_raw(self, max_n: int = 4096, blocking: bool = False):
-        """Completed raw submissions in order: (tags, codes, footprints, images)."""
+    def set_dedup(self, enable: bool, seed: int = 0):
+        """Raw batches also return the HA dedup tag (XXH64 of the first signature) computed on the GPU."""
+        self.L.fdgpu_ed25519_set_dedup(self.ctx, 1 if enable else 0, seed)
+
+    def poll_raw(self, max_n: int = 4096, blocking: bool = False, dedup: bool = False):
+        """Completed raw submissions in order: (tags, codes, footprints, images[, dedup tags])."""
         tags = np.zeros(max_n, np.uint64)
         codes = np.zeros(max_n, np.int8)
         fp = np.zeros(max_n, np.uint16)
         img = np.zeros((max_n, TXN_IMG_STRIDE), np.uint8)
+        dt = np.zeros(max_n, np.uint64)
         n = self.L.fdgpu_ed25519_poll_raw(self.ctx, tags.ctypes.data, codes.ctypes.data, img.ctypes.data,
-                                          fp.ctypes.data, max_n, 1 if blocking else 0)
+                                          fp.ctypes.data, dt.ctypes.data, max_n, 1 if blocking else 0)
+        if dedup:
+            return tags[:n], codes[:n], fp[:n], img[:n], dt[:n]
         return tags[:n], codes[:n], fp[:n], img[:n]
+
+    def faulted(self) -> bool:
+        return bool(self.L.fdgpu_ed25519_faulted(self.ctx))
+
+    def debug_fault(self):
+        """Host-side test hook: the context behaves as after a failed batch."""
+        self.L.fdgpu_ed25519_debug_fault(self.ctx)
 
     def poll(self, max_n: int = 4096, blocking: bool = False):
         tags = np.zeros(max_n, np.uint64)

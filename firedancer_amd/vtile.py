@@ -14,14 +14,18 @@ from .engine import PKG_DIR, load_library as load_engine
 LIB_PATH = os.path.join(PKG_DIR, "libfdgpu_vtile.so")
 TXNM_HDR_SZ = 80
 CHUNK_SZ = 64
-PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL, OVERRUN = range(6)
+PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL, OVERRUN, GPU_FAULT = range(7)
+LAT_BUCKETS = 20
 
 EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
            "fdgpu_mcache_new", "fdgpu_mcache_delete", "fdgpu_mcache_publish", "fdgpu_mcache_poll",
            "fdgpu_dcache_compact_next", "fdgpu_vtile_new", "fdgpu_vtile_delete", "fdgpu_vtile_out_dcache",
            "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_housekeep", "fdgpu_vtile_pipeline_state", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
            "fdgpu_vtile_metrics", "fdgpu_vtile_set_in_link", "fdgpu_vtile_oldest_pending_seq", "fdgpu_vtile_overruns",
-           "fdgpu_stream_bench")
+           "fdgpu_vtile_faulted", "fdgpu_vtile_recover", "fdgpu_vtile_debug_fault", "fdgpu_vtile_gpu_metrics",
+           "fdgpu_link_new", "fdgpu_link_join", "fdgpu_link_delete", "fdgpu_link_joined", "fdgpu_link_cfg",
+           "fdgpu_link_run", "fdgpu_link_tiles_of", "fdgpu_link_mcache", "fdgpu_link_dcache", "fdgpu_link_result",
+           "fdgpu_stream_run", "fdgpu_stream_bench")
 
 TXNM_DTYPE = np.dtype([("reference_slot", "<u8"), ("payload_sz", "<u2"), ("txn_t_sz", "<u2"), ("source_ipv4", "<u4"),
                        ("source_tpu", "u1"), ("_pad0", "u1", (7,)), ("bundle_id", "<u8"), ("bundle_txn_cnt", "<u8"),
@@ -39,11 +43,37 @@ class Done(ctypes.Structure):
                 ("tag", ctypes.c_ulong), ("result", ctypes.c_int)]
 
 
+class GpuMetrics(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_ulong), ("batch_txns", ctypes.c_ulong), ("inflight", ctypes.c_ulong),
+                ("inflight_max", ctypes.c_ulong), ("pending", ctypes.c_ulong), ("overruns", ctypes.c_ulong),
+                ("gpu_fault_frags", ctypes.c_ulong), ("faults", ctypes.c_ulong),
+                ("lat_hist", ctypes.c_ulong * LAT_BUCKETS)]
+
+    def as_dict(self) -> dict:
+        return {k: (list(getattr(self, k)) if k == "lat_hist" else int(getattr(self, k))) for k, _ in self._fields_}
+
+
+class StreamCfg(ctypes.Structure):
+    _fields_ = [("n_frags", ctypes.c_ulong), ("batch_txn", ctypes.c_ulong), ("max_inflight", ctypes.c_ulong),
+                ("rate_fps", ctypes.c_double), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int),
+                ("zero_copy", ctypes.c_int), ("reliable", ctypes.c_int)]
+
+
 class StreamStats(ctypes.Structure):
     _fields_ = [("seconds", ctypes.c_double), ("frags", ctypes.c_ulong), ("sigs", ctypes.c_ulong),
                 ("published", ctypes.c_ulong), ("frags_per_s", ctypes.c_double), ("sigs_per_s", ctypes.c_double),
                 ("lat_p50_us", ctypes.c_double), ("lat_p99_us", ctypes.c_double), ("lat_max_us", ctypes.c_double),
-                ("metrics", ctypes.c_ulong * 5), ("overruns", ctypes.c_ulong), ("tile_ns", ctypes.c_ulong * 4)]
+                ("metrics", ctypes.c_ulong * 5), ("overruns", ctypes.c_ulong), ("tile_ns", ctypes.c_ulong * 4),
+                ("verdicts", ctypes.c_ulong), ("lost", ctypes.c_ulong), ("batches", ctypes.c_ulong),
+                ("batch_txns", ctypes.c_ulong), ("inflight_max", ctypes.c_ulong),
+                ("gpu_lat_hist", ctypes.c_ulong * LAT_BUCKETS), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int)]
+
+    def as_dict(self) -> dict:
+        out = {}
+        for k, _ in self._fields_:
+            v = getattr(self, k)
+            out[k] = list(v) if k in ("metrics", "tile_ns", "gpu_lat_hist") else v
+        return out
 
 
 _lib = None
@@ -90,6 +120,27 @@ def load():
         L.fdgpu_vtile_oldest_pending_seq.argtypes = [vp]
         L.fdgpu_vtile_overruns.restype = ul
         L.fdgpu_vtile_overruns.argtypes = [vp]
+        L.fdgpu_vtile_faulted.argtypes = [vp]
+        L.fdgpu_vtile_recover.argtypes = [vp]
+        L.fdgpu_vtile_debug_fault.argtypes = [vp, ctypes.c_int]
+        L.fdgpu_vtile_gpu_metrics.argtypes = [vp, ctypes.POINTER(GpuMetrics)]
+        L.fdgpu_link_new.restype = vp
+        L.fdgpu_link_new.argtypes = [ctypes.c_char_p, ctypes.POINTER(StreamCfg), vp, vp, vp, ul, ul]
+        L.fdgpu_link_join.restype = vp
+        L.fdgpu_link_join.argtypes = [ctypes.c_char_p, ctypes.c_double]
+        L.fdgpu_link_delete.argtypes = [vp]
+        L.fdgpu_link_joined.restype = ul
+        L.fdgpu_link_joined.argtypes = [vp]
+        L.fdgpu_link_cfg.argtypes = [vp, ctypes.POINTER(StreamCfg)]
+        L.fdgpu_link_run.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.fdgpu_link_tiles_of.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        L.fdgpu_link_mcache.restype = vp
+        L.fdgpu_link_mcache.argtypes = [vp]
+        L.fdgpu_link_dcache.restype = vp
+        L.fdgpu_link_dcache.argtypes = [vp]
+        L.fdgpu_link_result.argtypes = [vp, ctypes.c_double, ctypes.POINTER(StreamStats)]
+        L.fdgpu_stream_run.argtypes = [ctypes.c_int, ctypes.POINTER(StreamCfg), vp, vp, vp, ul, ul,
+                                       ctypes.POINTER(StreamStats)]
         L.fdgpu_stream_bench.argtypes = [ctypes.c_int, vp, vp, vp, ul, ul, ctypes.c_int, ul, ul, ul, ctypes.c_double,
                                          ctypes.c_int, ctypes.POINTER(StreamStats)]
         _lib = L
@@ -173,6 +224,20 @@ class VTile:
         self.L.fdgpu_vtile_metrics(self.p, m)
         return list(m)
 
+    def gpu_metrics(self) -> dict:
+        m = GpuMetrics()
+        self.L.fdgpu_vtile_gpu_metrics(self.p, ctypes.byref(m))
+        return m.as_dict()
+
+    def faulted(self) -> int:
+        return int(self.L.fdgpu_vtile_faulted(self.p))
+
+    def recover(self) -> int:
+        return int(self.L.fdgpu_vtile_recover(self.p))
+
+    def debug_fault(self, k: int):
+        self.L.fdgpu_vtile_debug_fault(self.p, k)
+
     def record(self, chunk: int, sz: int) -> bytes:
         return ctypes.string_at(self.dcache + chunk * CHUNK_SZ, sz)
 
@@ -200,7 +265,89 @@ def stream_bench(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: 
                               batch_txn, max_inflight, mcache_depth, rate_fps, 1 if zero_copy else 0, ctypes.byref(st))
     if rc:
         raise RuntimeError(f"fdgpu_stream_bench: {rc} " + load_engine().fdgpu_last_error().decode())
-    return {"seconds": st.seconds, "frags": st.frags, "sigs": st.sigs, "published": st.published,
-            "frags_per_s": st.frags_per_s, "sigs_per_s": st.sigs_per_s, "lat_p50_us": st.lat_p50_us,
-            "lat_p99_us": st.lat_p99_us, "lat_max_us": st.lat_max_us, "metrics": list(st.metrics),
-            "overruns": st.overruns, "tile_ns": list(st.tile_ns)}
+    return st.as_dict()
+
+
+def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
+    """The verify tiles process `proc` runs (tile i drives GPU i % gpus)."""
+    out = (ctypes.c_int * max(tiles, 1))()
+    n = load().fdgpu_link_tiles_of(tiles, gpus, proc, out)
+    return list(out[:n])
+
+
+def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable) -> StreamCfg:
+    return StreamCfg(n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
+                     gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0)
+
+
+def stream_run(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,
+               batch_txn: int = 4096, max_inflight: int = 1, mcache_depth: int = 1 << 16, rate_fps: float = 0.0,
+               device: int = 0, zero_copy: bool = True, reliable: bool = True) -> dict:
+    """One process: producer + `tiles` verify tiles on `device` over a private link (G = 1)."""
+    L = load()
+    payload = np.ascontiguousarray(payload, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    sz = np.ascontiguousarray(sz, np.uint16)
+    cfg = _cfg(n_frags, tiles, 1, batch_txn, max_inflight, rate_fps, zero_copy, reliable)
+    st = StreamStats()
+    rc = L.fdgpu_stream_run(device, ctypes.byref(cfg), payload.ctypes.data, off.ctypes.data, sz.ctypes.data, len(off),
+                            mcache_depth, ctypes.byref(st))
+    if rc:
+        raise RuntimeError(f"fdgpu_stream_run: {rc} " + load_engine().fdgpu_last_error().decode())
+    return st.as_dict()
+
+
+class Link:
+    """The configs[4] link shared by several processes (fdgpu_link_t): create (with the payloads) or join."""
+
+    def __init__(self, path: str | None, *, create: bool, payload=None, off=None, sz=None, n_frags: int = 0,
+                 tiles: int = 1, gpus: int = 1, batch_txn: int = 8192, max_inflight: int = 1, rate_fps: float = 0.0,
+                 zero_copy: bool = True, reliable: bool = True, mcache_depth: int = 1 << 18, timeout_s: float = 300.0):
+        self.L = load()
+        self.path = path
+        if create:
+            payload = np.ascontiguousarray(payload, np.uint8)
+            off = np.ascontiguousarray(off, np.uint32)
+            sz = np.ascontiguousarray(sz, np.uint16)
+            cfg = _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable)
+            self.p = self.L.fdgpu_link_new(path.encode() if path else None, ctypes.byref(cfg), payload.ctypes.data,
+                                           off.ctypes.data, sz.ctypes.data, len(off), mcache_depth)
+        else:
+            self.p = self.L.fdgpu_link_join(path.encode(), timeout_s)
+        if not self.p:
+            raise RuntimeError(f"fdgpu_link_{'new' if create else 'join'}({path}) failed")
+
+    def cfg(self) -> dict:
+        c = StreamCfg()
+        self.L.fdgpu_link_cfg(self.p, ctypes.byref(c))
+        return {k: getattr(c, k) for k, _ in c._fields_}
+
+    def joined(self) -> int:
+        return int(self.L.fdgpu_link_joined(self.p))
+
+    def mcache(self):
+        return self.L.fdgpu_link_mcache(self.p)
+
+    def dcache(self) -> int:
+        return int(self.L.fdgpu_link_dcache(self.p))
+
+    def run(self, proc: int, device: int, run_producer: bool) -> int:
+        return int(self.L.fdgpu_link_run(self.p, proc, device, 1 if run_producer else 0))
+
+    def result(self, timeout_s: float = 120.0) -> dict:
+        st = StreamStats()
+        rc = self.L.fdgpu_link_result(self.p, timeout_s, ctypes.byref(st))
+        if rc:
+            raise RuntimeError(f"fdgpu_link_result: {rc}")
+        return st.as_dict()
+
+    def close(self):
+        if getattr(self, "p", None):
+            self.L.fdgpu_link_delete(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

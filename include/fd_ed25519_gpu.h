@@ -23,10 +23,14 @@
       The fd_sha512_t * arguments are accepted and ignored (the GPU
       computes SHA-512 itself); they are kept so the prototypes are
       identical.  These calls each run one GPU round trip, so they are
-      correct but latency-bound; throughput comes from layer 2.  One
-      limit the reference does not have: 96*batch_sz + msg_sz must fit
-      the 16-bit descriptor (<= 65535 bytes; every verify-path message is
-      <= 1232), else the call returns FDGPU_ERR_TOO_LONG.
+      correct but latency-bound; throughput comes from layer 2.  Any
+      message length is accepted, as in the reference: when 96*batch_sz +
+      msg_sz passes the 16-bit descriptor range (every verify-path message
+      is <= 1232 bytes) the digests SHA-512(R||A||M) are computed by the
+      batch SHA-512 kernel first and handed to the verify kernels.  Codes
+      are always FD_ED25519_*; a GPU runtime failure aborts the process
+      (the reference has no such failure mode; a verify tile's failure
+      is an FD_LOG_ERR, fd_verify_tile.c:74-84).
 
    2. Batch / async API (new; prefix fdgpu_).  A batch is a set of
       transactions described by fdgpu_txn_desc_t records (the fields
@@ -84,7 +88,7 @@ fd_ed25519_strerror( int err );
    AVX-512 and ERR_PUBKEY on ref, and an encoding with x==0 and the
    sign bit set is rejected at decode by AVX-512 only.  AVX-512 is the
    default (it is the north-star CPU baseline). */
-#define FDGPU_ERR_TOO_LONG     (-4)   /* drop-in call beyond the 64 KiB descriptor limit */
+#define FDGPU_ERR_TOO_LONG     (-4)   /* submit: the record cannot fit the ctx payload arena (not queued) */
 
 #define FDGPU_SEMANTICS_AVX512 (0)
 #define FDGPU_SEMANTICS_REF    (1)
@@ -281,7 +285,9 @@ fdgpu_sha512_batch_host( int                   device,
    out_codes[i] the fd_ed25519_verify_batch_single_msg code.  Returns
    the number written (<= max).  submit returns 0 on success, -1 if
    the transaction is malformed (it is then completed with ERR_SIG),
-   -2 if all slots are in flight (caller should poll). */
+   -2 if all slots are in flight (caller should poll), -3 if the ctx has
+   faulted, FDGPU_ERR_TOO_LONG if the record (payload_sz + 8 bytes)
+   exceeds max_payload_bytes (nothing is queued). */
 int
 fdgpu_ed25519_submit( fdgpu_ed25519_ctx_t * ctx,
                       unsigned char const * payload,
@@ -294,6 +300,17 @@ fdgpu_ed25519_submit( fdgpu_ed25519_ctx_t * ctx,
 
 int
 fdgpu_ed25519_flush( fdgpu_ed25519_ctx_t * ctx );
+
+/* 1 once a batch of ctx has failed on the device (poll then returns 0
+   without blocking and every submit returns -3: the in-flight
+   transactions are lost; delete and recreate the ctx). */
+int
+fdgpu_ed25519_faulted( fdgpu_ed25519_ctx_t const * ctx );
+
+/* Test hook (host side only): ctx behaves from now on exactly as after a
+   failed batch. */
+void
+fdgpu_ed25519_debug_fault( fdgpu_ed25519_ctx_t * ctx );
 
 unsigned long
 fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx,
@@ -378,14 +395,32 @@ fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx,
                                  unsigned short        payload_sz,
                                  unsigned long         tag );
 
+/* out_dedup (may be NULL): with fdgpu_ed25519_set_dedup on, the HA dedup
+   tag of each parsed transaction (XXH64 of its first signature with the
+   set seed, exactly fd_txn_verify's fd_hash( seed, sig0, 64 ),
+   fd_verify_tile.h:79; 0 for a rejected payload), computed on the GPU so
+   the tile never reads the payload bytes on the host. */
 unsigned long
 fdgpu_ed25519_poll_raw( fdgpu_ed25519_ctx_t * ctx,
                         unsigned long *       out_tags,
                         signed char *         out_codes,
                         unsigned char *       out_img,
                         unsigned short *      out_fp,
+                        unsigned long *       out_dedup,
                         unsigned long         max,
                         int                   blocking );
+
+void
+fdgpu_ed25519_set_dedup( fdgpu_ed25519_ctx_t * ctx, int enable, unsigned long seed );
+
+/* Gathered records (fdgpu_ed25519_submit_raw_gather) whose header holds a
+   u16 footprint field at byte `off` (fd_txn_m_t txn_t_sz: 10): the GPU
+   stores each footprint there as well, next to the fd_txn_t image, so
+   the tile never writes the record either.  -1 (default) = none.  Needs
+   payload_off <= 255 and off + 2 <= payload_off in every gathered
+   record. */
+int
+fdgpu_ed25519_set_record_fp_off( fdgpu_ed25519_ctx_t * ctx, int off );
 
 /* Batches of at most small_max signatures take the latency path: one
    launch decodes A, decodes R and hashes side by side, and R is compared

@@ -91,7 +91,9 @@ void             fdgpu_mcache_delete ( fdgpu_mcache_t * mc );
 void             fdgpu_mcache_publish( fdgpu_mcache_t * mc, unsigned long seq, unsigned long sig, unsigned int chunk,
                                        unsigned int sz, unsigned long tsorig, unsigned long tspub );
 /* consumer: 0 = frag seq copied to *out; 1 = not yet published; -1 = overrun
-   (the producer has lapped seq) */
+   (the producer has lapped seq).  Lines are fd_frag_meta_t's 32 bytes: out
+   tsorig / tspub are the compressed low 32 bits of the timestamps given to
+   publish (fd_frag_meta_ts_comp). */
 int              fdgpu_mcache_poll   ( fdgpu_mcache_t const * mc, unsigned long seq, fdgpu_frag_meta_t * out );
 
 /* next chunk after a frag of sz bytes at chunk, wrapping to chunk0 past
@@ -107,6 +109,8 @@ unsigned long    fdgpu_dcache_compact_next( unsigned long chunk, unsigned long s
 #define FDGPU_VTILE_DEDUP_FAIL       (3)
 #define FDGPU_VTILE_BUNDLE_PEER_FAIL (4)
 #define FDGPU_VTILE_OVERRUN          (5)   /* zero-copy intake: the frag was overwritten before the GPU read it */
+#define FDGPU_VTILE_GPU_FAULT        (6)   /* the frag's GPU batch failed: no verdict, never published (the
+                                              reference tile would FD_LOG_ERR, fd_verify_tile.c:74-84) */
 
 typedef struct fdgpu_vtile_done {
   unsigned long seq;      /* as given to during_frag */
@@ -118,6 +122,23 @@ typedef struct fdgpu_vtile_done {
 } fdgpu_vtile_done_t;
 
 typedef struct fdgpu_vtile fdgpu_vtile_t;
+
+/* GPU-side metrics of a tile (batches submitted, in-flight
+   depth, GPU verify latency histogram; plus overruns and faults), next to
+   the reference's verify counters of fdgpu_vtile_metrics. */
+#define FDGPU_VTILE_LAT_BUCKETS (20UL)
+typedef struct fdgpu_vtile_gpu_metrics {
+  unsigned long batches;          /* batches launched */
+  unsigned long batch_txns;       /* transactions in them (batches / batch_txns = mean batch) */
+  unsigned long inflight;         /* launched batches not yet drained, now */
+  unsigned long inflight_max;     /* high-water mark of inflight */
+  unsigned long pending;          /* frags between during_frag and after_frags, now */
+  unsigned long overruns;         /* frags returned as FDGPU_VTILE_OVERRUN */
+  unsigned long gpu_fault_frags;  /* frags returned as FDGPU_VTILE_GPU_FAULT */
+  unsigned long faults;           /* engine contexts seen faulted */
+  unsigned long lat_hist[ FDGPU_VTILE_LAT_BUCKETS ];  /* batch launch -> drained: bucket i = [2^i, 2^(i+1)) us
+                                                         (bucket 0 includes < 1 us, the last one overflow) */
+} fdgpu_vtile_gpu_metrics_t;
 
 /* device: HIP device; batch_txn: transactions per GPU batch (staging
    slot); tcache_depth: HA dedup depth (verify.tcache_depth); seed: the
@@ -166,38 +187,97 @@ void            fdgpu_vtile_pipeline_state( fdgpu_vtile_t const * vt, unsigned l
    less than the engine's 4 staging slots).  Returns 1 if it launched. */
 int             fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, unsigned long max_inflight );
 /* after_frag for completed frags, in during_frag order: at most max
-   records to out[]; blocking waits for the oldest batch. */
+   records to out[]; blocking waits for the oldest batch (never for a
+   faulted one).  Out-dcache records are reused once after_frags has
+   returned them and the ring wraps: as in the reference stem, the caller
+   publishes only within its out-link credits and must not call
+   during_frag while a reliable consumer still lags a full out-dcache ring
+   behind (the ring holds fdgpu_vtile_pending()-bounded frags; size it to
+   the consumers' depth). */
 unsigned long   fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, unsigned long max, int blocking );
 /* frags submitted but not yet returned by after_frags */
 unsigned long   fdgpu_vtile_pending( fdgpu_vtile_t const * vt );
+/* Fault path.  When a batch fails on the device its engine context stops:
+   after_frags never blocks on it and returns each of its pending frags, in
+   frag order, as FDGPU_VTILE_GPU_FAULT; during_frag moves on to the tile's
+   other contexts (-3 once none is left).  fdgpu_vtile_faulted counts the
+   faulted contexts; fdgpu_vtile_recover recreates them once after_frags
+   has returned all their frags (0; -1 while some are pending, -2 if a new
+   context could not be created).  A stem integration either treats a
+   nonzero fdgpu_vtile_faulted as the reference's FD_LOG_ERR or recovers. */
+int             fdgpu_vtile_faulted( fdgpu_vtile_t const * vt );
+int             fdgpu_vtile_recover( fdgpu_vtile_t * vt );
+/* host-side test hook: engine context k of the tile fails (fdgpu_ed25519_debug_fault) */
+void            fdgpu_vtile_debug_fault( fdgpu_vtile_t * vt, int k );
+void            fdgpu_vtile_gpu_metrics( fdgpu_vtile_t const * vt, fdgpu_vtile_gpu_metrics_t * out );
 /* metrics: [0] parse_fail [1] verify_fail [2] dedup_fail
    [3] bundle_peer_fail [4] published (fd_verify_tile.c:29-34) */
 void            fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, unsigned long out[ 5 ] );
 
-/* ---- streaming benchmark (BASELINE configs[4]) --------------------- */
+/* ---- the configs[4] stream (BASELINE configs[4]) ------------------- */
+
+typedef struct fdgpu_stream_cfg {
+  unsigned long n_frags;         /* frags the producer publishes (seq 0 .. n_frags-1) */
+  unsigned long batch_txn;       /* transactions per GPU batch of a tile */
+  unsigned long max_inflight;    /* fdgpu_vtile_housekeep( max_inflight ) */
+  double        rate_fps;        /* producer pacing, frags/s (0 = as fast as it can) */
+  int           tiles;           /* T verify tiles: tile i takes seq % T == i (fd_verify_tile.c:47-48) */
+  int           gpus;            /* G: tile i drives GPU i % G, run by process i % G (one process per GPU) */
+  int           zero_copy;       /* tiles leave frags in the in dcache, the GPU gathers them */
+  int           reliable;        /* 1: credit-based link (the producer waits for the slowest tile);
+                                    0: unreliable, as the reference's quic_verify link (topology.c:167-170):
+                                    the producer never waits, a lagging tile is overrun and skips frags */
+} fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
   double        seconds;         /* first frag published by the producer -> last verdict */
   unsigned long frags, sigs, published;
-  double        frags_per_s, sigs_per_s;
+  double        frags_per_s, sigs_per_s;  /* verdicts / s and verified signatures / s */
   double        lat_p50_us, lat_p99_us, lat_max_us;   /* tsorig (producer publish) -> after_frag verdict */
   unsigned long metrics[ 5 ];
-  unsigned long overruns;        /* producer lapped a tile (frags lost, as in tango) */
-  unsigned long tile_ns[ 4 ];    /* host time summed over tiles: frag intake (mcache polls +
-                                    during_frag), after_frags, housekeep, whole tile loop */
+  unsigned long overruns;        /* frags the GPU read after the producer had reused their line (FDGPU_VTILE_OVERRUN) */
+  unsigned long tile_ns[ 4 ];    /* host time summed over tiles: frag intake (mcache polls + during_frag),
+                                    after_frags, housekeep, whole tile loop */
+  unsigned long verdicts;        /* frags that reached after_frag (any result) */
+  unsigned long lost;            /* frags skipped by overrun tiles (unreliable link): verdicts + lost = frags */
+  unsigned long batches, batch_txns, inflight_max;
+  unsigned long gpu_lat_hist[ FDGPU_VTILE_LAT_BUCKETS ];   /* batch launch -> drained, summed over tiles */
+  int           tiles, gpus;
 } fdgpu_stream_stats_t;
 
-/* A producer thread publishes n_frags frags built from the payload
-   arena (payload t at payload + off[t], sz[t] bytes, cycling over
-   n_payload) into an in mcache / dcache (depth mcache_depth), paced to
-   at most rate_fps frags/s (0 = as fast as possible); tiles verify
-   tiles (one host thread each, before_frag's seq % tiles round robin,
-   each with its own GPU context on `device`, batches of at most
-   batch_txn launched by fdgpu_vtile_housekeep( max_inflight )) consume
-   it.  zero_copy: the in dcache is registered with the GPU and the tiles
-   take frags by fdgpu_vtile_set_in_link (no host copy); each tile's
-   credit then stops at its oldest pending frag.  Returns 0 and fills
-   *st. */
+/* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per
+   distinct payload), per-tile fseqs and results -- in one memory region:
+   a shared file at `path` (e.g. /dev/shm/...; the creator makes it, the
+   other processes fdgpu_link_join it; unlink it once fdgpu_link_joined
+   reaches the process count) or, path NULL, private memory for one
+   process.  The producer is a thread of whichever process passes
+   run_producer to fdgpu_link_run; each process runs the tiles i % G ==
+   proc on its `device`.  fdgpu_link_run returns once this process's
+   tiles (and producer) are done; fdgpu_link_result then waits for every
+   tile of every process and merges their results. */
+typedef struct fdgpu_link fdgpu_link_t;
+
+fdgpu_link_t *  fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, unsigned char const * payload,
+                                unsigned int const * off, unsigned short const * sz, unsigned long n_payload,
+                                unsigned long mcache_depth );
+fdgpu_link_t *  fdgpu_link_join( char const * path, double timeout_s );
+void            fdgpu_link_delete( fdgpu_link_t * link );
+unsigned long   fdgpu_link_joined( fdgpu_link_t const * link );
+void            fdgpu_link_cfg( fdgpu_link_t const * link, fdgpu_stream_cfg_t * cfg );
+int             fdgpu_link_run( fdgpu_link_t * link, int proc, int device, int run_producer );
+/* tile -> GPU binding: the tiles of process proc (i % gpus == proc), ascending, into out; returns the count */
+int             fdgpu_link_tiles_of( int tiles, int gpus, int proc, int * out );
+/* this process's view of the link's in mcache and in dcache (chunk c at dcache + 64 c) */
+fdgpu_mcache_t * fdgpu_link_mcache( fdgpu_link_t * link );
+unsigned char *  fdgpu_link_dcache( fdgpu_link_t * link );
+int             fdgpu_link_result( fdgpu_link_t * link, double timeout_s, fdgpu_stream_stats_t * st );
+
+/* one process, private link, every tile on `device` (G = 1) */
+int             fdgpu_stream_run( int device, fdgpu_stream_cfg_t const * cfg, unsigned char const * payload,
+                                  unsigned int const * off, unsigned short const * sz, unsigned long n_payload,
+                                  unsigned long mcache_depth, fdgpu_stream_stats_t * st );
+
+/* the same with a reliable link (kept for existing callers) */
 int             fdgpu_stream_bench( int device, unsigned char const * payload, unsigned int const * off,
                                     unsigned short const * sz, unsigned long n_payload, unsigned long n_frags,
                                     int tiles, unsigned long batch_txn, unsigned long max_inflight,

@@ -216,9 +216,12 @@ class Reference:
         self.lib.ref_sha512(_ptr(self._b(data)), len(data), _ptr(out))
         return out.tobytes()
 
-    def verify_txns(self, payload: np.ndarray, desc: np.ndarray, sig_cnt_total: int, threads: int = 1):
+    def verify_txns(self, payload: np.ndarray, desc: np.ndarray, sig_cnt_total: int, threads: int = 1,
+                    want_sig_codes: bool = True):
+        """(txn codes, per-signature codes or None).  want_sig_codes=False verifies every signature once
+        (only the batch call, as fd_txn_verify does): the form the CPU baseline times."""
         txn_out = np.zeros(len(desc), dtype=np.int8)
-        sig_out = np.zeros(max(sig_cnt_total, 1), dtype=np.int8)
+        sig_out = np.zeros(max(sig_cnt_total, 1), dtype=np.int8) if want_sig_codes else None
         self.lib.ref_verify_txns(_ptr(payload), desc.ctypes.data, len(desc), _ptr(txn_out, _i8p),
-                                 _ptr(sig_out, _i8p), threads)
-        return txn_out, sig_out[:sig_cnt_total]
+                                 _ptr(sig_out, _i8p) if sig_out is not None else None, threads)
+        return txn_out, (sig_out[:sig_cnt_total] if sig_out is not None else None)

@@ -46,7 +46,8 @@ ref_sha512( uchar const * in, ulong sz, uchar * out ) {
 /* Batch driver with the layout of include/fd_ed25519_gpu.h.  txn code =
    fd_ed25519_verify_batch_single_msg exactly as fd_txn_verify calls it
    (src/disco/verify/fd_verify_tile.h:59-92); per-signature codes (if
-   sig_out) = fd_ed25519_verify of each signature alone. */
+   sig_out; NULL for the timed CPU baseline, which then verifies each
+   signature once) = fd_ed25519_verify of each signature alone. */
 
 typedef struct {
   uchar const * payload; fdgpu_txn_desc_t const * desc; ulong lo, hi;

@@ -1,4 +1,6 @@
 """Helpers to turn tests/golden fixtures into batch inputs (payload arena + descriptors)."""
+import os
+
 import numpy as np
 
 DESC_DTYPE = np.dtype([("payload_off", "<u4"), ("sig_base", "<u4"), ("payload_sz", "<u2"),
@@ -25,3 +27,7 @@ def vectors_as_txns(v, idx=None):
 def txns_fixture(t):
     desc = t["desc"].reshape(-1).view(DESC_DTYPE).copy()
     return t["payload"].copy(), desc, int(t["sig_total"][0])
+
+
+def load_vectors():
+    return dict(np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "vectors.npz")))
