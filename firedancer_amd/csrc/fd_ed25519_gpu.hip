@@ -39,6 +39,7 @@
 #include <mutex>
 #include <string.h>
 #include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string>
 #include <vector>
@@ -1201,6 +1202,11 @@ fd_img_scatter_kernel( fdgpu_txn_raw_t const * __restrict__ raw, unsigned char c
    ================================================================== */
 
 static thread_local std::string fd_err;
+
+static unsigned long fd_now_ns( void ) {
+  timespec ts; clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (unsigned long)ts.tv_sec * 1000000000UL + (unsigned long)ts.tv_nsec;
+}
 static void set_err( char const * what, hipError_t e ) {
   fd_err = std::string( what ) + ": " + hipGetErrorString( e );
 }
@@ -1224,6 +1230,7 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   unsigned long      txn_cnt, sig_cnt;
   unsigned long      cursor;   /* results already handed out by poll */
   hipEvent_t         done;
+  unsigned long      launch_ns;   /* host time of slot_launch, for the batch latency histogram */
   int                state;    /* 0 filling, 1 in flight / draining */
   int                mode;     /* 0 desc (fdgpu_ed25519_submit), 1 raw (fdgpu_ed25519_submit_raw),
                                   2 raw in place (fdgpu_ed25519_submit_raw_ref),
@@ -1272,6 +1279,8 @@ struct fdgpu_ed25519_ctx {
   int dedup;                     /* raw batches also return HA dedup tags (fdgpu_ed25519_set_dedup) */
   unsigned long dedup_seed;
   int rec_fp_off;                /* gathered records: offset of a u16 footprint field, -1 = none */
+  unsigned long n_batches, n_txns;                /* async batches launched, transactions in them */
+  unsigned long lat_hist[ FDGPU_LAT_BUCKETS ];    /* launch -> verdicts seen by poll, quarter-octave buckets */
   std::deque<int> inflight;      /* slot order */
 };
 
@@ -1864,6 +1873,8 @@ static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
     HIPCHK( hipMemcpyAsync( sl.h_dtag, sl.d_dtag, sl.txn_cnt * sizeof(unsigned long), hipMemcpyDeviceToHost, st ), -2 );
   HIPCHK( hipEventRecord( sl.done, st ), -2 );
   sl.state = 1; sl.cursor = 0;
+  sl.launch_ns = fd_now_ns();
+  ctx->n_batches++; ctx->n_txns += sl.txn_cnt;
   ctx->inflight.push_back( i );
   return 0;
 }
@@ -2098,6 +2109,7 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
       hipError_t e = blocking ? hipEventSynchronize( sl.done ) : hipEventQuery( sl.done );
       if( e == hipErrorNotReady ) break;
       if( e != hipSuccess ) { set_err( "fdgpu_ed25519_poll: batch failed", e ); ctx->fault = 1; break; }
+      ctx->lat_hist[ fdgpu_lat_bucket( fd_now_ns() - sl.launch_ns ) ]++;
     }
     unsigned long k = sl.txn_cnt - sl.cursor;
     if( k > max - n ) k = max - n;
@@ -2122,6 +2134,13 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
 }
 
 extern "C" int fdgpu_ed25519_faulted( fdgpu_ed25519_ctx_t const * ctx ) { return ctx ? ctx->fault : 1; }
+
+extern "C" void
+fdgpu_ed25519_batch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * batches, unsigned long * txns,
+                           unsigned long hist[ FDGPU_LAT_BUCKETS ] ) {
+  *batches = ctx->n_batches; *txns = ctx->n_txns;
+  if( hist ) memcpy( hist, ctx->lat_hist, sizeof(ctx->lat_hist) );
+}
 
 /* host-side test hook: the context behaves exactly as after a failed batch */
 extern "C" void

@@ -279,19 +279,12 @@ typedef struct {
    are merged back into frag order in after_frags. */
 #define VT_NCTX_MAX 3
 
-/* GPU batch latency histogram: bucket i counts launch -> drained in
-   [2^i, 2^(i+1)) us (bucket 0 also takes < 1 us, the last one overflow) */
-static ulong vt_lat_bucket( ulong ns ) {
-  ulong us = ns / 1000UL;
-  ulong b = us ? 63UL - (ulong)__builtin_clzl( us ) : 0UL;
-  return b < FDGPU_VTILE_LAT_BUCKETS ? b : FDGPU_VTILE_LAT_BUCKETS - 1UL;
-}
-
 struct fdgpu_vtile {
   /* (fields below; ctx first so the watchdog can report pipeline state) */
   fdgpu_ed25519_ctx_t * ctx[ VT_NCTX_MAX ];
   int                   device, semantics;   /* to recreate a faulted context */
   int                   fault_seen[ VT_NCTX_MAX ];
+  int                   gpu_tag;         /* HA dedup tags from the GPU (env FDGPU_VTILE_GPU_TAG, default 1) */
   fdgpu_vtile_gpu_metrics_t gm;
   int                   nctx, fill;      /* contexts, the one taking frags */
   ulong                 launch_ns[ VT_NCTX_MAX ];
@@ -333,7 +326,7 @@ vt_ctx_new( fdgpu_vtile_t const * vt ) {
     fdgpu_ed25519_set_small_batch_max( c, sm < b/2UL ? sm : b/2UL );
     /* the GPU computes the HA dedup tags and, for gathered records, stores
        txn_t_sz: after_frag then touches neither payload nor record */
-    fdgpu_ed25519_set_dedup( c, 1, vt->seed );
+    fdgpu_ed25519_set_dedup( c, vt->gpu_tag, vt->seed );
     fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
   }
   return c;
@@ -352,6 +345,7 @@ fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ul
   if( vt->nctx > VT_NCTX_MAX ) vt->nctx = VT_NCTX_MAX;
   vt->batch_ns = 500e3;
   vt->device = device; vt->semantics = semantics; vt->batch = batch_txn; vt->seed = seed;
+  { char const * g = getenv( "FDGPU_VTILE_GPU_TAG" ); vt->gpu_tag = g ? atoi( g ) != 0 : 1; }
   int ctx_ok = 1;
   for( int k=0; k<vt->nctx; k++ ) if( !( vt->ctx[k] = vt_ctx_new( vt ) ) ) ctx_ok = 0;
   vt->tcache = fdgpu_tcache_new( tcache_depth );
@@ -391,8 +385,8 @@ void    fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, ulong out[ 5 ] ) { memcpy
 /* bookkeeping of a batch launch on context k (filling txns) */
 static void
 vt_launched( fdgpu_vtile_t * vt, int k, ulong now, ulong filling ) {
+  (void)filling;
   vt->launch_ns[k] = now; vt->busy[k] = 1;
-  vt->gm.batches++; vt->gm.batch_txns += filling;
   ulong f, infl = 0UL;
   for( int j=0; j<vt->nctx; j++ ) { ulong i; fdgpu_ed25519_pipeline_state( vt->ctx[j], &f, &i ); infl += i; }
   if( infl > vt->gm.inflight_max ) vt->gm.inflight_max = infl;
@@ -452,7 +446,16 @@ void
 fdgpu_vtile_gpu_metrics( fdgpu_vtile_t const * vt, fdgpu_vtile_gpu_metrics_t * out ) {
   *out = vt->gm;
   ulong f, i, infl = 0UL;
-  for( int k=0; k<vt->nctx; k++ ) { fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i ); infl += i; }
+  memset( out->lat_hist, 0, sizeof(out->lat_hist) );
+  out->batches = out->batch_txns = 0UL;
+  for( int k=0; k<vt->nctx; k++ ) {
+    fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i ); infl += i;
+    /* the engine counts every launch (a full slot launches inside submit) and times each batch */
+    ulong b, t, h[ FDGPU_LAT_BUCKETS ];
+    fdgpu_ed25519_batch_stats( vt->ctx[k], &b, &t, h );
+    out->batches += b; out->batch_txns += t;
+    for( int j=0; j<FDGPU_LAT_BUCKETS; j++ ) out->lat_hist[j] += h[j];
+  }
   out->inflight = infl;
   out->pending = vt->pend_tail - vt->pend_head;
   out->overruns = vt->overruns;
@@ -481,7 +484,6 @@ fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
     fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i );
     if( !i ) {
       vt->busy[k] = 0; vt->batch_ns = 0.875*vt->batch_ns + 0.125*(double)( now - vt->launch_ns[k] );
-      vt->gm.lat_hist[ vt_lat_bucket( now - vt->launch_ns[k] ) ]++;
     }
   }
   int f = vt->fill;
@@ -564,6 +566,11 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
     vt->metrics[0]++;
     return FDGPU_VTILE_PARSE_FAIL;
   }
+  if( !vt->gpu_tag ) {        /* host XXH64 of the first signature (A/B knob; reads payload and image) */
+    uchar const * payload = (uchar const *)txnm + FDGPU_TXNM_HDR_SZ;
+    uchar const * im = vt->zc ? (uchar const *)txnm + ( ( FDGPU_TXNM_HDR_SZ + p->payload_sz + 1UL ) & ~1UL ) : img;
+    tag = xxh64_64( vt->seed, payload + ( (unsigned)im[2] | ((unsigned)im[3] << 8) ) );
+  }
   /* fd_txn_verify (fd_verify_tile.h:59-108): dedup query, verify, insert */
   int res = 0;   /* 0 success, 1 verify failed, 2 dedup */
   if( !is_bundle && fdgpu_tcache_query( vt->tcache, tag ) ) res = 2;
@@ -628,7 +635,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
          tag the insert evicts) and, with an in link, the frag's mcache line: start them a
          few completions ahead */
       if( i + 8UL < k ) {
-        tc_prefetch( vt->tcache, vt->p_dtag[ i + 8UL ], 8UL );
+        if( vt->gpu_tag ) tc_prefetch( vt->tcache, vt->p_dtag[ i + 8UL ], 8UL );
         if( vt->in_mc ) __builtin_prefetch( &vt->in_mc->line[ vt->pend[ ( vt->pend_head + 8UL ) % vt->pend_cap ].seq
                                                                & ( vt->in_mc->depth - 1UL ) ] );
       }

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(PKG_DIR, "libfdgpu_vtile.so")
 TXNM_HDR_SZ = 80
 CHUNK_SZ = 64
 PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL, OVERRUN, GPU_FAULT = range(7)
-LAT_BUCKETS = 20
+LAT_BUCKETS = 40
 
 EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
            "fdgpu_mcache_new", "fdgpu_mcache_delete", "fdgpu_mcache_publish", "fdgpu_mcache_poll",

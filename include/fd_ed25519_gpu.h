@@ -301,6 +301,25 @@ fdgpu_ed25519_submit( fdgpu_ed25519_ctx_t * ctx,
 int
 fdgpu_ed25519_flush( fdgpu_ed25519_ctx_t * ctx );
 
+/* Batch latency histogram buckets (async pipeline: slot launch -> the
+   verdicts seen by poll): bucket 0 < 32 us, bucket i in 1..38 covers
+   [32 us * 2^((i-1)/4), 32 us * 2^(i/4)) (quarter octaves up to ~23 ms),
+   bucket 39 the rest. */
+#define FDGPU_LAT_BUCKETS (40)
+static inline int fdgpu_lat_bucket( unsigned long ns ) {
+  if( ns < 32000UL ) return 0;
+  int oct = 63 - __builtin_clzl( ns / 32000UL );            /* ns / 32 us in [2^oct, 2^(oct+1)) */
+  unsigned long base = 32000UL << oct;
+  int quarter = ( ns*10000UL >= base*11892UL ) + ( ns*10000UL >= base*14142UL ) + ( ns*10000UL >= base*16818UL );
+  int b = 1 + 4*oct + quarter;
+  return b < FDGPU_LAT_BUCKETS - 1 ? b : FDGPU_LAT_BUCKETS - 1;
+}
+/* counters of ctx's async pipeline: batches launched, transactions in them,
+   and (hist, may be NULL) the latency histogram above */
+void
+fdgpu_ed25519_batch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * batches, unsigned long * txns,
+                           unsigned long hist[ FDGPU_LAT_BUCKETS ] );
+
 /* 1 once a batch of ctx has failed on the device (poll then returns 0
    without blocking and every submit returns -3: the in-flight
    transactions are lost; delete and recreate the ctx). */

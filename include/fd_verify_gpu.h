@@ -29,6 +29,8 @@
    insert/evict semantics (src/tango/tcache/fd_tcache.h:281-404), used
    by the tile and by the streaming benchmark (BASELINE configs[4]). */
 
+#include "fd_ed25519_gpu.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -126,7 +128,7 @@ typedef struct fdgpu_vtile fdgpu_vtile_t;
 /* GPU-side metrics of a tile (batches submitted, in-flight
    depth, GPU verify latency histogram; plus overruns and faults), next to
    the reference's verify counters of fdgpu_vtile_metrics. */
-#define FDGPU_VTILE_LAT_BUCKETS (20UL)
+#define FDGPU_VTILE_LAT_BUCKETS ((unsigned long)FDGPU_LAT_BUCKETS)
 typedef struct fdgpu_vtile_gpu_metrics {
   unsigned long batches;          /* batches launched */
   unsigned long batch_txns;       /* transactions in them (batches / batch_txns = mean batch) */
@@ -136,8 +138,8 @@ typedef struct fdgpu_vtile_gpu_metrics {
   unsigned long overruns;         /* frags returned as FDGPU_VTILE_OVERRUN */
   unsigned long gpu_fault_frags;  /* frags returned as FDGPU_VTILE_GPU_FAULT */
   unsigned long faults;           /* engine contexts seen faulted */
-  unsigned long lat_hist[ FDGPU_VTILE_LAT_BUCKETS ];  /* batch launch -> drained: bucket i = [2^i, 2^(i+1)) us
-                                                         (bucket 0 includes < 1 us, the last one overflow) */
+  unsigned long lat_hist[ FDGPU_VTILE_LAT_BUCKETS ];  /* per batch, launch -> verdicts polled, summed over the
+                                                         tile's engine contexts (buckets: fdgpu_lat_bucket) */
 } fdgpu_vtile_gpu_metrics_t;
 
 /* device: HIP device; batch_txn: transactions per GPU batch (staging

@@ -12,6 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def _header_functions():
     txt = open(os.path.join(ROOT, "include", "fd_ed25519_gpu.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    txt = re.sub(r"static inline[^{]*\{.*?\n\}", "", txt, flags=re.S)    # header-only helpers, not exports
     return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", txt)) - {"sizeof"})
 
 
