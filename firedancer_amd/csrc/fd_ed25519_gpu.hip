@@ -397,6 +397,26 @@ fd_table_kernel( u32 nsig, int semantics, unsigned char const * __restrict__ pst
   atab_build( tab, s, Axy );
 }
 
+/* FD_CLOCK_PROBE builds (tools/clock_probe.py): lane 0 of every
+   fd_dsm_kernel block records the shader clock counter (s_memtime) and the
+   100 MHz real-time counter (s_memrealtime) at its start and end, so the
+   clock the kernel actually ran at is measured, not assumed. */
+#ifndef FD_CLOCK_PROBE
+#define FD_CLOCK_PROBE 0
+#endif
+#if FD_CLOCK_PROBE
+#define FD_CLK_BLOCKS 16384
+__device__ unsigned long long fd_clk_buf[ FD_CLK_BLOCKS ][ 4 ];
+#define FD_CLK_BEGIN unsigned long long fd_c0 = __builtin_amdgcn_s_memtime(), fd_r0 = __builtin_amdgcn_s_memrealtime();
+#define FD_CLK_END if( threadIdx.x == 0 && blockIdx.x < FD_CLK_BLOCKS ) {                                         \
+    unsigned long long fd_c1 = __builtin_amdgcn_s_memtime(), fd_r1 = __builtin_amdgcn_s_memrealtime();            \
+    fd_clk_buf[ blockIdx.x ][0] = fd_c0; fd_clk_buf[ blockIdx.x ][1] = fd_c1;                                      \
+    fd_clk_buf[ blockIdx.x ][2] = fd_r0; fd_clk_buf[ blockIdx.x ][3] = fd_r1; }
+#else
+#define FD_CLK_BEGIN
+#define FD_CLK_END
+#endif
+
 __global__ void __launch_bounds__( FD_WG )
 fd_dsm_kernel( u32                      nsig,
                uint4 const * __restrict__ tab,
@@ -413,6 +433,7 @@ fd_dsm_kernel( u32                      nsig,
   __syncthreads();
 #endif
 
+  FD_CLK_BEGIN
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
   if( code[s] != FD_ED25519_SUCCESS ) return;
@@ -485,6 +506,7 @@ fd_dsm_kernel( u32                      nsig,
     fe_store_planar( Pbuf + s, n, P2.X );
     fe_store_planar( Pbuf + 10*n + s, n, P2.Y );
     fe_store_planar( Pbuf + 20*n + s, n, P2.Z );
+    FD_CLK_END
     return;
   }
   /* R decoded up front (small batches): fd_ed25519_point_eq_z1,
@@ -1397,8 +1419,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->max_txn = max_txn; ctx->max_sig = max_sig; ctx->max_payload = max_payload_bytes;
   size_t ns = max_sig;
   HIPCHK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ), -1 );
-  HIPCHK( hipStreamCreateWithFlags( &ctx->cstream, hipStreamNonBlocking ), -1 );
-  for( unsigned long i=0; i<FD_PIPE_MAX; i++ ) HIPCHK( hipEventCreateWithFlags( &ctx->pipe_ev[i], hipEventDisableTiming ), -1 );
+
   HIPCHK( hipMalloc( &ctx->d_map,  ns * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_code, ns ), -1 );
   HIPCHK( hipMalloc( &ctx->d_pstat, 2*ns ), -1 );
@@ -1520,6 +1541,25 @@ fd_mad_probe_kernel( u32 iters, u32 seed, u64 * out ) {
   if( x == 0x1234567ull ) out[0] = x;
 }
 
+#if FD_CLOCK_PROBE
+/* mean shader clock (MHz) over the blocks of the last fd_dsm_kernel launch
+   that recorded (sum of s_memtime deltas / sum of s_memrealtime deltas x
+   100 MHz), and those blocks' count */
+extern "C" double
+fdgpu_debug_dsm_clock_mhz( unsigned long nblocks, unsigned long * recorded ) {
+  static unsigned long long h[ FD_CLK_BLOCKS ][ 4 ];
+  if( nblocks > FD_CLK_BLOCKS ) nblocks = FD_CLK_BLOCKS;
+  if( hipMemcpyFromSymbol( h, HIP_SYMBOL( fd_clk_buf ), nblocks * 4 * sizeof(unsigned long long) ) != hipSuccess ) return -1.;
+  double dc = 0., dr = 0.; unsigned long k = 0;
+  for( unsigned long b=0; b<nblocks; b++ ) {
+    if( h[b][3] <= h[b][2] || h[b][1] <= h[b][0] ) continue;
+    dc += (double)( h[b][1] - h[b][0] ); dr += (double)( h[b][3] - h[b][2] ); k++;
+  }
+  *recorded = k;
+  return dr > 0. ? dc / dr * 100. : -1.;
+}
+#endif
+
 extern "C" double
 fdgpu_mad_peak_per_s( int device ) {
   if( hipSetDevice( device ) != hipSuccess ) return -1.;
@@ -1581,6 +1621,12 @@ verify_host_pipelined( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload,
                        fdgpu_txn_desc_t const * desc, unsigned long txn_cnt, unsigned long nsig,
                        signed char * txn_out, signed char * sig_out ) {
   fd_slot & sl = ctx->slot[0];
+  if( !ctx->cstream ) {
+    /* created on first use: every stream of the process takes a place in the runtime's
+       stream -> hardware queue assignment, and the tiles' contexts never need this one */
+    HIPCHK( hipStreamCreateWithFlags( &ctx->cstream, hipStreamNonBlocking ), -2 );
+    for( unsigned long i=0; i<FD_PIPE_MAX; i++ ) HIPCHK( hipEventCreateWithFlags( &ctx->pipe_ev[i], hipEventDisableTiming ), -2 );
+  }
   hipStream_t st = ctx->stream, cs = ctx->cstream;
   unsigned long nsub = txn_cnt / FD_PIPE_SUB;
   if( nsub > FD_PIPE_MAX ) nsub = FD_PIPE_MAX;

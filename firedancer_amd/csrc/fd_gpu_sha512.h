@@ -67,14 +67,29 @@ FD_DEV u64 fd_maj64( u64 x, u64 y, u64 z ) {
 /* Load n32 consecutive little-endian 32-bit words starting at an
    arbitrary byte address p: aligned dword loads + v_alignbyte_b32.  Reads
    up to 4 bytes past p + 4*n32 (the batch arena carries tail slack). */
+/* FD_SHA_LOAD (A/B knob): 0 loads with the non-temporal hint (round-1
+   form), 1 plain loads.  Either way the compiler merges the dword-aligned
+   word loads into global_load_dwordx4 (dword alignment suffices). */
+#ifndef FD_SHA_LOAD
+#define FD_SHA_LOAD 0
+#endif
 template<int N32>
 FD_DEV void fd_load_words( u32 w[ N32 ], unsigned char const * p ) {
   uintptr_t a  = (uintptr_t)p;
-  u32 const * q = (u32 const *)( a & ~(uintptr_t)3 );
   u32 sh = (u32)( a & 3 );
+  /* global address space: the caller's pointer is generic, and generic loads become flat_load
+     (which wait on both the vector-memory and the LDS counters) */
+  typedef __attribute__(( address_space( 1 ) )) u32 const gu32;
+  gu32 * q = (gu32 *)( a & ~(uintptr_t)3 );
   u32 d[ N32 + 1 ];
 #pragma unroll
-  for( int i=0; i<N32+1; i++ ) d[i] = __builtin_nontemporal_load( q + i );
+  for( int i=0; i<N32+1; i++ ) {
+#if FD_SHA_LOAD==0
+    d[i] = __builtin_nontemporal_load( q + i );
+#else
+    d[i] = q[i];
+#endif
+  }
 #pragma unroll
   for( int i=0; i<N32; i++ ) w[i] = __builtin_amdgcn_alignbyte( d[i+1], d[i], sh );
 }

@@ -980,7 +980,11 @@ static void * link_tile( void * _a ) {
       mc_line_t const * ln = &l->line[ seq & mask ];
       if( ( seq % T ) != (ulong)idx ) {                             /* before_frag filters: the seq alone decides */
         ulong s0 = atomic_load_explicit( (_Atomic ulong *)&ln->seq, memory_order_acquire );
-        if( s0 == seq ) { seq++; continue; }
+        if( s0 == seq ) {
+          seq++;
+          if( c->reliable && ( !(seq & 63UL) || seq == n_frags ) ) link_credit( h, idx, vt, seq );   /* batched credit return */
+          continue;
+        }
         if( (long)( s0 - seq ) < 0 ) break;                         /* not yet published */
         if( c->reliable ) { atomic_store( &h->fail, 3 ); break; }
         lost += own_in( seq, s0, T, (ulong)idx ); seq = s0;          /* overrun while polling: resume there */

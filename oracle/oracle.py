@@ -161,6 +161,45 @@ class RefTxn:
         return _parse_batch(self.lib.ref_txn_parse_batch, arena, off, sz, stride)
 
 
+class RefTile:
+    """The reference verify tile's per-frag decision (oracle/_ref/libfdref_tile.so: fd_txn_verify, the
+    tcache macros, fd_hash, fd_txn_parse and the AVX-512 verify compiled in place; after_frag's bundle
+    bookkeeping restated in ref_tile_harness.c)."""
+
+    REC_STRIDE = 1232 + 1024
+
+    def __init__(self):
+        path = os.path.join(HERE, "_ref", "libfdref_tile.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        if not cpu_has_avx512_ifma():
+            raise RuntimeError("host CPU lacks AVX-512 IFMA; cannot run the AVX-512 reference build")
+        self.lib = L = ctypes.CDLL(path)
+        L.ref_tile_run.restype = ctypes.c_int
+        L.ref_tile_run.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_ulong, ctypes.c_ulong, ctypes.c_ulong] + \
+            [ctypes.c_void_p] * 3 + [ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p]
+
+    def run(self, frags, depth: int, seed: int):
+        """frags: [(payload bytes, bundle_id)].  Returns (results, metrics[5], {i: record bytes}, tags)."""
+        n = len(frags)
+        sz = np.array([len(p) for p, _ in frags], np.uint16)
+        off = np.concatenate([[0], np.cumsum(sz.astype(np.int64))[:-1]]).astype(np.uint32) if n else np.zeros(0, np.uint32)
+        arena = np.frombuffer(b"".join(bytes(p) for p, _ in frags) + bytes(64), np.uint8).copy()
+        bid = np.array([b for _, b in frags], np.uint64)
+        res = np.zeros(n, np.int32)
+        rec_sz = np.zeros(n, np.uint64)
+        rec = np.zeros((n, self.REC_STRIDE), np.uint8)
+        tag = np.zeros(n, np.uint64)
+        metrics = np.zeros(5, np.uint64)
+        rc = self.lib.ref_tile_run(arena.ctypes.data, off.ctypes.data, sz.ctypes.data, bid.ctypes.data, n, depth, seed,
+                                   res.ctypes.data, rec_sz.ctypes.data, rec.ctypes.data, self.REC_STRIDE,
+                                   tag.ctypes.data, metrics.ctypes.data)
+        if rc:
+            raise RuntimeError(f"ref_tile_run: {rc}")
+        recs = {i: rec[i, : int(rec_sz[i])].tobytes() for i in range(n) if res[i] == 0}
+        return [int(x) for x in res], [int(x) for x in metrics], recs, [int(x) for x in tag]
+
+
 def cpu_has_avx512_ifma() -> bool:
     try:
         with open("/proc/cpuinfo") as f:

@@ -1,10 +1,13 @@
-"""GPU: the verify tile over the engine (libfdgpu_vtile.so) against a
-sequential model of the reference tile's after_frag
-(src/disco/verify/fd_verify_tile.c:103-157 + fd_txn_verify,
-fd_verify_tile.h:59-108): same per-frag outcome, same metrics, same
-published fd_txn_m_t records (payload + fd_txn_t image), over a stream
-with valid / invalid signatures, parse failures, HA duplicates (incl.
-tcache eviction) and bundles with failing members."""
+"""GPU: the verify tile over the engine (libfdgpu_vtile.so) against the
+reference tile's own per-frag decision (oracle/_ref/libfdref_tile.so:
+fd_txn_verify, the tcache, fd_hash, fd_txn_parse and the AVX-512 verify
+compiled in place from the reference, src/disco/verify/fd_verify_tile.c:
+103-157 + fd_verify_tile.h:59-108): same per-frag outcome, same metrics,
+same published fd_txn_m_t records (payload + fd_txn_t image) and same HA
+dedup tags, over a stream with valid / invalid signatures, parse
+failures, HA duplicates (incl. tcache eviction) and bundles with failing
+members.  Without the reference build, the sequential model below (which
+tests/test_ref_tile.py pins to it) is the expectation."""
 import os
 import sys
 import time
@@ -88,6 +91,22 @@ def model(oracle, frags, seed, depth):
     return res, metrics, recs
 
 
+def expectation(oracle, frags, seed, depth):
+    """(per-frag results, metrics, {i: (record head, fd_txn_t bytes)}, {i: tag}) of the reference tile."""
+    from oracle.oracle import RefTile
+    try:
+        ref = RefTile()
+    except (FileNotFoundError, RuntimeError):
+        res, m, recs = model(oracle, frags, seed, depth)
+        return res, m, recs, None
+    res, m, recs, tags = ref.run(frags, depth, seed)
+    out = {}
+    for i, r in recs.items():
+        hl = 80 + len(frags[i][0])
+        out[i] = (r[:hl], r[(hl + 1) & ~1:])
+    return res, m, out, {i: tags[i] for i in recs}
+
+
 def in_dcache(frag_list):
     """The frags as fd_txn_m_t records in one 64-B-chunked in dcache (numpy, page-locked by the caller)."""
     offs, pos = [], 0
@@ -110,7 +129,7 @@ def test_vtile_vs_model(oracle, batch, depth, zero_copy):
     from firedancer_amd import engine, vtile
     frags = make_stream()
     seed = 0x1234abcd
-    want_res, want_m, want_recs = model(oracle, frags, seed, depth)
+    want_res, want_m, want_recs, want_tags = expectation(oracle, frags, seed, depth)
     vt = vtile.VTile(device=0, batch_txn=batch, tcache_depth=depth, seed=seed)
     if zero_copy:
         fbs = [vtile.frag_bytes(p, b) for p, b in frags]
@@ -128,6 +147,8 @@ def test_vtile_vs_model(oracle, batch, depth, zero_copy):
                 rec = vt.record(chunk, sz)
                 if rec[: len(head)] != head or rec[(len(head) + 1) & ~1:] != timg or sz != ((len(head) + 1) & ~1) + len(timg):
                     bad.append(seq)
+                if want_tags is not None and tag != want_tags.get(seq):
+                    bad.append(("tag", seq))
         return out
 
     for seq, (p, b) in enumerate(frags):
@@ -163,7 +184,7 @@ def test_vtile_multictx_vs_model(oracle, nctx, zero_copy):
     from firedancer_amd import engine, vtile
     frags = make_stream(seed=12)
     seed, depth = 0x5eedbeef, 1 << 12
-    want_res, want_m, want_recs = model(oracle, frags, seed, depth)
+    want_res, want_m, want_recs, want_tags = expectation(oracle, frags, seed, depth)
     old = os.environ.get("FDGPU_VTILE_CTX")
     os.environ["FDGPU_VTILE_CTX"] = str(nctx)
     try:
@@ -188,6 +209,8 @@ def test_vtile_multictx_vs_model(oracle, nctx, zero_copy):
                 rec = vt.record(chunk, sz)
                 if rec[: len(head)] != head or rec[(len(head) + 1) & ~1:] != timg or sz != ((len(head) + 1) & ~1) + len(timg):
                     bad.append(seq)
+                if want_tags is not None and tag != want_tags.get(seq):
+                    bad.append(("tag", seq))
         return out
 
     for seq, (p, b) in enumerate(frags):

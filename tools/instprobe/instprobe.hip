@@ -44,6 +44,10 @@ DEF_K( k_lshladd,asm volatile( "v_lshl_add_u32 %0, %0, 4, %1" : "+v"( v[c] ) : "
 DEF_K( k_fma,    asm volatile( "v_fma_f32 %0, %0, %1, %1" : "+v"( v[c] ) : "v"( seed ) ) )
 DEF_K( k_addf,   asm volatile( "v_add_f32 %0, %0, %1" : "+v"( v[c] ) : "v"( seed ) ) )
 DEF_K( k_mul24,  asm volatile( "v_mul_u32_u24 %0, %0, %1" : "+v"( v[c] ) : "v"( seed ) ) )
+DEF_K( k_sub,    asm volatile( "v_sub_u32 %0, %1, %0" : "+v"( v[c] ) : "v"( seed ) ) )
+DEF_K( k_mov,    asm volatile( "v_mov_b32 %0, %1" : "=v"( v[c] ) : "v"( v[(c+1)%CH] ) ) )
+DEF_K( k_lshr,   asm volatile( "v_lshrrev_b32 %0, 3, %0" : "+v"( v[c] ) ) )
+DEF_K( k_snop,   asm volatile( "s_nop 0" ::: ); v[c] ^= seed )
 
 __global__ void __launch_bounds__( 256 ) k_mad64( unsigned iters, unsigned seed, unsigned * out, unsigned long long * clk ) {
   CLK_START
@@ -55,6 +59,32 @@ __global__ void __launch_bounds__( 256 ) k_mad64( unsigned iters, unsigned seed,
   }
   uint64_t r = 0; for( int c=0; c<CH/2; c++ ) r ^= v[c];
   if( r == 0x12345678u ) out[0] = (unsigned)r;
+  CLK_END
+}
+__global__ void __launch_bounds__( 256 ) k_lshladd64( unsigned iters, unsigned seed, unsigned * out, unsigned long long * clk ) {
+  CLK_START
+  uint64_t v[CH / 2];
+  for( int c=0; c<CH/2; c++ ) v[c] = seed + threadIdx.x * 7u + c;
+  uint64_t sv = seed;
+  for( unsigned i=0; i<iters; i++ ) {
+#pragma unroll
+    for( int c=0; c<CH/2; c++ ) asm volatile( "v_lshl_add_u64 %0, %0, 1, %1" : "+v"( v[c] ) : "v"( sv ) );
+  }
+  uint64_t r = 0; for( int c=0; c<CH/2; c++ ) r ^= v[c];
+  if( r == 0x12345678u ) out[0] = (unsigned)r;
+  CLK_END
+}
+__global__ void __launch_bounds__( 256 ) k_fma64( unsigned iters, unsigned seed, unsigned * out, unsigned long long * clk ) {
+  CLK_START
+  double v[CH / 2];
+  for( int c=0; c<CH/2; c++ ) v[c] = (double)( seed + threadIdx.x * 7u + c );
+  double sv = (double)seed * 1e-9;
+  for( unsigned i=0; i<iters; i++ ) {
+#pragma unroll
+    for( int c=0; c<CH/2; c++ ) asm volatile( "v_fma_f64 %0, %0, %1, %1" : "+v"( v[c] ) : "v"( sv ) );
+  }
+  double r = 0; for( int c=0; c<CH/2; c++ ) r += v[c];
+  if( r == 0.125 ) out[0] = 1u;
   CLK_END
 }
 __global__ void __launch_bounds__( 256 ) k_lshr64( unsigned iters, unsigned seed, unsigned * out, unsigned long long * clk ) {
@@ -78,7 +108,9 @@ int main() {
     { "v_alignbit_b32",    k_align,   CH }, { "v_bitop3_b32",    k_bitop3,  CH }, { "v_cmp+v_cndmask", k_cndmask, CH },
     { "sel (compiler)", k_cndsel, CH }, { "v_mov_b32_dpp", k_dpp, CH }, { "v_lshl_add_u32", k_lshladd, CH },
     { "v_mad_u64_u32",     k_mad64, CH/2 }, { "v_lshrrev_b64",   k_lshr64, CH/2 },
-    { "v_fma_f32",         k_fma,   CH }, { "v_add_f32",       k_addf,    CH }, { "v_mul_u32_u24", k_mul24, CH } };
+    { "v_fma_f32",         k_fma,   CH }, { "v_add_f32",       k_addf,    CH }, { "v_mul_u32_u24", k_mul24, CH },
+    { "v_sub_u32",         k_sub,   CH }, { "v_mov_b32",       k_mov,     CH }, { "v_lshrrev_b32", k_lshr, CH },
+    { "s_nop 0 (+v_xor)",  k_snop,  CH }, { "v_lshl_add_u64",  k_lshladd64, CH/2 }, { "v_fma_f64", k_fma64, CH/2 } };
   int ncu = 0; hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, 0 );
   unsigned * out; hipMalloc( &out, 4 );
   unsigned iters = 4096; int blocks = ncu * 8;        /* 8 x 256 threads per CU = 8 waves per SIMD */
