@@ -162,12 +162,12 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
     hist = st["gpu_lat_hist"]
     tot = sum(hist)
 
-    def hq(q):   # GPU batch latency quantile from the log2 histogram: bucket upper edge, us
+    def hq(q):   # GPU batch latency quantile: upper edge of the quarter-octave bucket (fdgpu_lat_bucket), us
         c = 0
         for i, h in enumerate(hist):
             c += h
             if tot and c > q * tot:
-                return float(2 ** (i + 1))
+                return round(32.0 * 2 ** (i / 4), 1)
         return None
     return {"tiles": cfg["tiles"], "gpus": cfg["gpus"], "reliable": bool(cfg["reliable"]),
             "rate_fps": cfg["rate_fps"] or None, "frags": st["frags"], "verdicts": st["verdicts"],

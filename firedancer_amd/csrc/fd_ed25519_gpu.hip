@@ -36,6 +36,7 @@
 #include "../../include/fd_ed25519_gpu.h"
 
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <mutex>
 #include <string.h>
 #include <stdio.h>
@@ -1180,6 +1181,15 @@ __global__ void __launch_bounds__( 256 ) fd_btab_kernel( uint4 * out ) {
   fe_store_packed( o + 4, xy );
 }
 
+/* Last launch of an async batch: stores the slot's token into its
+   completion flag in pinned host memory (system scope, release), after
+   every earlier command of the stream -- copies included -- completed.
+   The tile polls that word with a plain load instead of a HIP call per
+   poll (hipEventQuery takes runtime locks every tile thread shares). */
+__global__ void fd_done_kernel( unsigned long * flag, unsigned long token ) {
+  __hip_atomic_store( flag, token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM );
+}
+
 struct fd_gather {             /* mode 3: copy sz bytes from src (host, device view) to arena / region offset dst */
   unsigned long src;
   unsigned int  dst;
@@ -1253,6 +1263,8 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   unsigned long      cursor;   /* results already handed out by poll */
   hipEvent_t         done;
   unsigned long      launch_ns;   /* host time of slot_launch, for the batch latency histogram */
+  unsigned long      token;       /* value fd_done_kernel writes to the slot's completion flag */
+  unsigned long      last_query;  /* host time of the last error check by hipEventQuery */
   int                state;    /* 0 filling, 1 in flight / draining */
   int                mode;     /* 0 desc (fdgpu_ed25519_submit), 1 raw (fdgpu_ed25519_submit_raw),
                                   2 raw in place (fdgpu_ed25519_submit_raw_ref),
@@ -1302,6 +1314,8 @@ struct fdgpu_ed25519_ctx {
   unsigned long dedup_seed;
   int rec_fp_off;                /* gathered records: offset of a u16 footprint field, -1 = none */
   unsigned long n_batches, n_txns;                /* async batches launched, transactions in them */
+  unsigned long volatile * h_flag;                /* per slot: completion token written by fd_done_kernel (pinned) */
+  unsigned long * d_flag;
   unsigned long lat_hist[ FDGPU_LAT_BUCKETS ];    /* launch -> verdicts seen by poll, quarter-octave buckets */
   std::deque<int> inflight;      /* slot order */
 };
@@ -1445,6 +1459,9 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   hipLaunchKernelGGL( fd_btab_kernel, dim3((FD_BTAB_ENTRIES + 255)/256), dim3(256), 0, ctx->stream, ctx->d_btab );
   HIPCHK( hipGetLastError(), -1 );
   for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) HIPCHK( hipEventCreateWithFlags( &ctx->slot[i].done, hipEventDisableTiming ), -1 );
+  HIPCHK( hipHostMalloc( (void **)&ctx->h_flag, fdgpu_ed25519_ctx_t::NSLOT * sizeof(unsigned long), hipHostMallocDefault ), -1 );
+  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) ctx->h_flag[i] = 0UL;
+  HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_flag, (void *)ctx->h_flag, 0 ), -1 );
   /* slot 0 now (the synchronous host calls stage through it); the async
      pipeline's other slots on first use (slot_bufs) */
   if( max_payload_bytes && slot_bufs( ctx, 0 ) ) return -1;
@@ -1496,6 +1513,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
     if( sl.done ) (void)hipEventDestroy( sl.done );
   }
   if( ctx->cstream ) { (void)hipStreamSynchronize( ctx->cstream ); (void)hipStreamDestroy( ctx->cstream ); }
+  if( ctx->h_flag ) (void)hipHostFree( (void *)ctx->h_flag );
   for( unsigned long i=0; i<FD_PIPE_MAX; i++ ) if( ctx->pipe_ev[i] ) (void)hipEventDestroy( ctx->pipe_ev[i] );
   if( ctx->stream ) (void)hipStreamDestroy( ctx->stream );
   delete ctx;
@@ -1917,9 +1935,12 @@ static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
   }
   if( sl.mode && ctx->dedup )
     HIPCHK( hipMemcpyAsync( sl.h_dtag, sl.d_dtag, sl.txn_cnt * sizeof(unsigned long), hipMemcpyDeviceToHost, st ), -2 );
+  sl.token++;
+  hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + i, sl.token );
+  HIPCHK( hipGetLastError(), -2 );
   HIPCHK( hipEventRecord( sl.done, st ), -2 );
   sl.state = 1; sl.cursor = 0;
-  sl.launch_ns = fd_now_ns();
+  sl.launch_ns = sl.last_query = fd_now_ns();
   ctx->n_batches++; ctx->n_txns += sl.txn_cnt;
   ctx->inflight.push_back( i );
   return 0;
@@ -2051,24 +2072,43 @@ fdgpu_ed25519_submit_raw_ref( fdgpu_ed25519_ctx_t * ctx, unsigned char const * b
 /* Host regions the GPU may read or write directly (fdgpu_host_alloc
    allocations and fdgpu_host_register-ed ranges): host base -> device
    address, for the gather path. */
-struct fd_region { unsigned char const * h; unsigned char * d; unsigned long sz; };
+/* A fixed table read without a lock (every tile thread looks its frags up
+   here in during_frag; a global mutex there was contended by all of them):
+   writers (register / unregister, rare) serialise on a mutex, fill an
+   entry's fields and then publish it with a release store of its size; a
+   removed entry's size drops to 0 first. */
+#define FD_REGION_MAX 256
+struct fd_region { unsigned char const * h; unsigned char * d; std::atomic<unsigned long> sz; };
 static std::mutex g_reg_mu;
-static std::vector<fd_region> g_regions;
+static fd_region g_regions[ FD_REGION_MAX ];
+static std::atomic<int> g_region_cnt{ 0 };
 
 static void region_add( void * h, void * d, unsigned long sz ) {
   std::lock_guard<std::mutex> lk( g_reg_mu );
-  g_regions.push_back( fd_region{ (unsigned char const *)h, (unsigned char *)d, sz } );
+  int n = g_region_cnt.load( std::memory_order_relaxed ), i = 0;
+  while( i < n && g_regions[i].sz.load( std::memory_order_relaxed ) ) i++;     /* reuse a removed entry */
+  if( i == FD_REGION_MAX ) return;
+  g_regions[i].h = (unsigned char const *)h; g_regions[i].d = (unsigned char *)d;
+  g_regions[i].sz.store( sz, std::memory_order_release );
+  if( i == n ) g_region_cnt.store( n + 1, std::memory_order_release );
 }
 static void region_del( void * h ) {
   std::lock_guard<std::mutex> lk( g_reg_mu );
-  for( size_t i=0; i<g_regions.size(); i++ ) if( g_regions[i].h == (unsigned char const *)h ) { g_regions.erase( g_regions.begin() + (long)i ); return; }
+  int n = g_region_cnt.load( std::memory_order_relaxed );
+  for( int i=0; i<n; i++ )
+    if( g_regions[i].h == (unsigned char const *)h && g_regions[i].sz.load( std::memory_order_relaxed ) ) {
+      g_regions[i].sz.store( 0UL, std::memory_order_release ); return;
+    }
 }
 /* device address of [p, p+sz) if it lies inside one registered region, else NULL */
 static unsigned char * region_dev( void const * p, unsigned long sz ) {
-  std::lock_guard<std::mutex> lk( g_reg_mu );
   unsigned char const * q = (unsigned char const *)p;
-  for( fd_region const & r : g_regions )
-    if( q >= r.h && q + sz <= r.h + r.sz ) return r.d + ( q - r.h );
+  int n = g_region_cnt.load( std::memory_order_acquire );
+  for( int i=0; i<n; i++ ) {
+    unsigned long rs = g_regions[i].sz.load( std::memory_order_acquire );
+    unsigned char const * h = g_regions[i].h;
+    if( rs && q >= h && q + sz <= h + rs ) return g_regions[i].d + ( q - h );
+  }
   return NULL;
 }
 
@@ -2152,9 +2192,25 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
     int i = ctx->inflight.front();
     fd_slot & sl = ctx->slot[i];
     if( sl.cursor==0 ) {
-      hipError_t e = blocking ? hipEventSynchronize( sl.done ) : hipEventQuery( sl.done );
-      if( e == hipErrorNotReady ) break;
-      if( e != hipSuccess ) { set_err( "fdgpu_ed25519_poll: batch failed", e ); ctx->fault = 1; break; }
+      /* ready when fd_done_kernel has stored the slot's token; a batch that failed never
+         stores it, so the stream's event is asked (a HIP call, with runtime locks) only
+         after 2 ms without the token and then once per ms */
+      int ready = 0;
+      for(;;) {
+        if( ctx->h_flag[i] == sl.token ) { ready = 1; break; }
+        unsigned long now = fd_now_ns();
+        if( now - sl.launch_ns > 2000000UL && now - sl.last_query > 1000000UL ) {
+          sl.last_query = now;
+          hipError_t e = hipEventQuery( sl.done );
+          if( e != hipSuccess && e != hipErrorNotReady ) { set_err( "fdgpu_ed25519_poll: batch failed", e ); ctx->fault = 1; break; }
+          if( e == hipSuccess && ctx->h_flag[i] == sl.token ) { ready = 1; break; }
+        }
+        if( !blocking ) break;
+        __builtin_ia32_pause();
+      }
+      if( ctx->fault ) break;
+      if( !ready ) break;
+      std::atomic_thread_fence( std::memory_order_acquire );
       ctx->lat_hist[ fdgpu_lat_bucket( fd_now_ns() - sl.launch_ns ) ]++;
     }
     unsigned long k = sl.txn_cnt - sl.cursor;

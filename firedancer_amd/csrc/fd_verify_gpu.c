@@ -999,7 +999,7 @@ static void * link_tile( void * _a ) {
         continue;
       }
       int rc = fdgpu_vtile_during_frag( vt, l->dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, seq,
-                                        ts_decomp( m.tsorig, now_ns() ) );
+                                        ts_decomp( m.tsorig, t0 ) );   /* the pass's start is "now" to 2^31 ns */
       if( rc == -2 ) { drain = 1; break; }                          /* staging full: drain, retry this seq */
       if( rc ) { fprintf( stderr, "fdgpu_link: tile %d during_frag %d\n", idx, rc ); atomic_store( &h->fail, 2 ); break; }
       /* this tile's next frag is usually published already: start its cold lines */
