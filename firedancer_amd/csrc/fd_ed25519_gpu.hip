@@ -1768,6 +1768,51 @@ fdgpu_ed25519_verify_many_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
   return 0;
 }
 
+/* Transactions scattered in host memory, each already parsed (the replay
+   path: fd_executor_txn_verify, src/flamenco/runtime/fd_executor.c:
+   1550-1574, once per transaction of a block, each over its own
+   txn_ctx->_txn_raw->raw).  desc[i] holds transaction i's fd_txn_t fields
+   (signature_off, acct_addr_off, message_off, sig_cnt) and payload_sz;
+   payload_off / sig_base are ignored.  out[i] = the
+   fd_ed25519_verify_batch_single_msg code of transaction i.  Chunks of up
+   to max_txn transactions / max_sig signatures / max_payload bytes. */
+extern "C" int
+fdgpu_ed25519_verify_txn_ptrs( fdgpu_ed25519_ctx_t * ctx, unsigned char const * const * payloads,
+                               fdgpu_txn_desc_t const * desc, unsigned long cnt, signed char * out ) {
+  if( !ctx ) { fd_err = "NULL ctx"; return -1; }
+  if( !ctx->slot[0].h_payload ) { fd_err = "ctx has no staging buffers (max_payload_bytes==0)"; return -3; }
+  if( async_busy( ctx ) ) { fd_err = "async batches pending or in flight"; return -1; }
+  for( unsigned long i=0; i<cnt; i++ )
+    if( (unsigned long)desc[i].payload_sz + 8UL > ctx->max_payload || desc[i].sig_cnt > ctx->max_sig ) {
+      fd_err = "transaction larger than the ctx"; return -1;
+    }
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  fd_slot & sl = ctx->slot[0];
+  hipStream_t st = ctx->stream;
+  unsigned long done = 0;
+  while( done < cnt ) {
+    unsigned long n = 0, nsig = 0; size_t used = 0;
+    while( done + n < cnt && n < ctx->max_txn ) {
+      fdgpu_txn_desc_t d = desc[ done + n ];
+      if( used + d.payload_sz + 8UL > ctx->max_payload || nsig + d.sig_cnt > ctx->max_sig ) break;
+      memcpy( sl.h_payload + used, payloads[ done + n ], d.payload_sz );
+      d.payload_off = (unsigned)used; d.sig_base = (unsigned)nsig;
+      sl.h_desc[n] = d;
+      used = ( used + d.payload_sz + 7UL ) & ~(size_t)7; nsig += d.sig_cnt; n++;
+    }
+    memset( sl.h_payload + used, 0, FD_ARENA_SLACK );
+    HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
+    HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, n * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
+    int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, n, nsig, sl.d_txn_out, NULL, st );
+    if( rc ) return rc;
+    HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, n, hipMemcpyDeviceToHost, st ), -2 );
+    HIPCHK( hipStreamSynchronize( st ), -2 );
+    memcpy( out + done, sl.h_txn_out, n );
+    done += n;
+  }
+  return 0;
+}
+
 /* ---- batch SHA-512 ---------------------------------------------------- */
 
 extern "C" int

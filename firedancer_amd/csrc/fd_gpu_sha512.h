@@ -67,11 +67,15 @@ FD_DEV u64 fd_maj64( u64 x, u64 y, u64 z ) {
 /* Load n32 consecutive little-endian 32-bit words starting at an
    arbitrary byte address p: aligned dword loads + v_alignbyte_b32.  Reads
    up to 4 bytes past p + 4*n32 (the batch arena carries tail slack). */
-/* FD_SHA_LOAD (A/B knob): 0 loads with the non-temporal hint (round-1
-   form), 1 plain loads.  Either way the compiler merges the dword-aligned
-   word loads into global_load_dwordx4 (dword alignment suffices). */
+/* FD_SHA_LOAD (A/B knob): 1 plain loads, 0 loads with the non-temporal
+   hint (the round-1 form).  Either way the compiler merges the
+   dword-aligned word loads into global_load_dwordx4 (dword alignment
+   suffices).  Measured on fd_hash_kernel, 1M x 1232-byte txns
+   (profiles/r02/sha_ab): non-temporal 1.239 ms, FETCH_SIZE 1.60 GB (x2
+   gfx950 correction: 3.27 GB = 2.5x the payload); plain 1.177 ms, 1.00 GB
+   (2.05 GB = 1.6x): the hint let lines go before the lane's next quads. */
 #ifndef FD_SHA_LOAD
-#define FD_SHA_LOAD 0
+#define FD_SHA_LOAD 1
 #endif
 template<int N32>
 FD_DEV void fd_load_words( u32 w[ N32 ], unsigned char const * p ) {

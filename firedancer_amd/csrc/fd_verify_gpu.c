@@ -219,9 +219,9 @@ fdgpu_mcache_poll( fdgpu_mcache_t const * mc, ulong seq, fdgpu_frag_meta_t * out
   return mc_poll( &mc->line[ seq & (mc->depth - 1UL) ], seq, out, &found );
 }
 
-/* fd_frag_meta_ts_decomp: the full timestamp nearest below-or-at now whose
-   low 32 bits are ts (valid for ages < 2^31 ns) */
-static inline ulong ts_decomp( unsigned ts, ulong now ) { return now - (ulong)(unsigned)( (unsigned)now - ts ); }
+/* fd_frag_meta_ts_decomp: the full timestamp nearest to now whose low 32
+   bits are ts (ts may lie up to 2^31 ns before or after now) */
+static inline ulong ts_decomp( unsigned ts, ulong now ) { return now + (ulong)(long)(int)( ts - (unsigned)now ); }
 
 /* fd_dcache_compact_next (src/tango/dcache/fd_dcache.h:263-269): advance
    by whole 128-byte chunk pairs, wrap to chunk0 past wmark */

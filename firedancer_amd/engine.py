@@ -48,7 +48,8 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_submit_raw_gather",
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_set_dedup",
-           "fdgpu_ed25519_set_record_fp_off", "fdgpu_ed25519_batch_stats", "fdgpu_last_error")
+           "fdgpu_ed25519_set_record_fp_off", "fdgpu_ed25519_batch_stats", "fdgpu_ed25519_verify_txn_ptrs",
+           "fdgpu_last_error")
 
 _lib = None
 _lock = threading.Lock()
@@ -129,6 +130,8 @@ def load_library():
         L.fdgpu_ed25519_kernel_ms.restype = ctypes.c_float
         L.fdgpu_ed25519_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.fdgpu_ed25519_pipeline_state.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.fdgpu_ed25519_verify_txn_ptrs.restype = ctypes.c_int
+        L.fdgpu_ed25519_verify_txn_ptrs.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_ulong, ctypes.c_void_p]
         L.fdgpu_ed25519_faulted.restype = ctypes.c_int
         L.fdgpu_ed25519_faulted.argtypes = [ctypes.c_void_p]
         L.fdgpu_ed25519_debug_fault.argtypes = [ctypes.c_void_p]
@@ -291,6 +294,19 @@ class Engine:
                                                    out.ctypes.data)
         if rc:
             raise RuntimeError(f"fdgpu_ed25519_verify_many_host: {rc} {last_error()}")
+        return out
+
+    def verify_txn_ptrs(self, payloads, desc: np.ndarray) -> np.ndarray:
+        """Codes of pre-parsed transactions scattered in host memory (fdgpu_ed25519_verify_txn_ptrs):
+        payloads[i] is transaction i's bytes, desc[i] its fd_txn_t offsets (payload_off/sig_base ignored)."""
+        keep = [np.frombuffer(bytes(p) + b"\0", np.uint8) for p in payloads]
+        ptrs = np.array([k.ctypes.data for k in keep], np.uint64)
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        out = np.zeros(len(keep), np.int8)
+        rc = self.L.fdgpu_ed25519_verify_txn_ptrs(self.ctx, ptrs.ctypes.data, desc.ctypes.data, len(keep),
+                                                  out.ctypes.data)
+        if rc:
+            raise RuntimeError(f"fdgpu_ed25519_verify_txn_ptrs: {rc} {last_error()}")
         return out
 
     # -- raw payloads: device fd_txn_parse + verify ---------------------------

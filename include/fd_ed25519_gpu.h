@@ -253,6 +253,21 @@ fdgpu_ed25519_verify_many_host( fdgpu_ed25519_ctx_t *         ctx,
                                 unsigned long                 cnt,
                                 signed char *                 out );
 
+/* fdgpu_ed25519_verify_txn_ptrs: out[i] = the fd_ed25519_verify_batch_
+   single_msg code of transaction i, whose payload is at payloads[i] (any
+   host memory) and whose fd_txn_t fields are in desc[i] (signature_off,
+   acct_addr_off, message_off, sig_cnt, payload_sz; payload_off and
+   sig_base ignored).  The replay path's batched fd_executor_txn_verify
+   (src/flamenco/runtime/fd_executor.c:1550-1574): one call per block
+   instead of one CPU verify per transaction.  Synchronous; needs a ctx
+   with staging. */
+int
+fdgpu_ed25519_verify_txn_ptrs( fdgpu_ed25519_ctx_t *         ctx,
+                               unsigned char const * const * payloads,
+                               fdgpu_txn_desc_t const *      desc,
+                               unsigned long                 cnt,
+                               signed char *                 out );
+
 /* Batch SHA-512 (replaces fd_sha512_batch_init / add / fini,
    src/ballet/sha512/fd_sha512.h:234-419, for any number of messages):
    hash[64 t, 64 t + 64) = SHA-512 of the sz[t] bytes at data + off[t].
