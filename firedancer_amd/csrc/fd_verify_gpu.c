@@ -948,8 +948,11 @@ static void * link_tile( void * _a ) {
   fdgpu_stream_cfg_t const * c = &h->cfg;
   int idx = a->idx;
   ulong const T = (ulong)c->tiles, mask = h->depth - 1UL, n_frags = c->n_frags;
+  /* out dcache: room for the frags a tile can have pending (its contexts' launched and filling
+     batches); large throughput batches get 3 batches' worth, small latency batches 6 */
+  ulong mult = c->batch_txn >= 32768UL ? 3UL : 6UL;
   fdgpu_vtile_t * vt = fdgpu_vtile_new( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
-                                        ( 6UL*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
+                                        ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
   if( c->zero_copy && fdgpu_vtile_set_in_link( vt, &l->mc ) ) { atomic_store( &h->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL; }
   atomic_fetch_add( &h->tiles_ready, 1UL );    /* the producer starts once every tile has its GPU context */
