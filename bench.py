@@ -140,8 +140,10 @@ STREAM_LEGS = ("cal", "max", "paced", "unrel")
 
 def _leg_cfg(args, leg, procs, cal_fps):
     T, Tl = args.stream_tiles * procs, args.stream_lat_tiles * procs
-    base = dict(batch_txn=args.stream_batch, max_inflight=args.stream_inflight, zero_copy=not args.stream_copy,
-                gpus=procs, mcache_depth=1 << 18)
+    # the max-rate legs batch for throughput (a GPU batch under one wave per SIMD costs about one wave's
+    # DSM chain, ~1 ms, whatever its size), the paced leg for latency
+    base = dict(batch_txn=args.stream_max_batch if leg != "paced" else args.stream_batch,
+                max_inflight=args.stream_inflight, zero_copy=not args.stream_copy, gpus=procs, mcache_depth=1 << 18)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -229,6 +231,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-seed", "1234", "--txns", str(args.txns), "--stream-frags", str(args.stream_frags),
            "--stream-seconds", str(args.stream_seconds), "--stream-unrel-seconds", str(args.stream_unrel_seconds),
            "--stream-tiles", str(args.stream_tiles), "--stream-batch", str(args.stream_batch),
+           "--stream-max-batch", str(args.stream_max_batch),
            "--stream-rate", str(args.stream_rate), "--stream-lat-tiles", str(args.stream_lat_tiles),
            "--stream-inflight", str(args.stream_inflight)]
     if args.stream_copy:
@@ -255,11 +258,16 @@ def main():
                     help="sustained length of the reliable max-rate leg and of the paced leg")
     ap.add_argument("--stream-unrel-seconds", type=float, default=4.0,
                     help="frags of the unreliable unthrottled leg, in seconds of the calibrated rate")
-    ap.add_argument("--stream-tiles", type=int, default=6, help="verify tiles per GPU (max-rate legs)")
+    ap.add_argument("--stream-tiles", type=int, default=2,
+                    help="verify tiles per GPU of the max-rate legs (profiles/r02/stream/sweep_*: 2 tiles 12.4M, "
+                         "4 tiles 9.8-12.5M, 6 tiles 9.3M sigs/s -- more tiles, more HIP streams on 4 hardware queues)")
     ap.add_argument("--stream-copy", action="store_true",
                     help="stream tiles copy each frag into the out dcache on the host (the reference tile's "
                          "during_frag) instead of the zero-copy intake (GPU gathers from the registered in dcache)")
-    ap.add_argument("--stream-batch", type=int, default=8192)
+    ap.add_argument("--stream-batch", type=int, default=8192, help="GPU batch (txns) of the paced latency leg")
+    ap.add_argument("--stream-max-batch", type=int, default=65536,
+                    help="GPU batch limit (txns) of the max-rate legs (profiles/r02/stream: batches of 8192 give "
+                         "7.2M, of up to 32768 13.7M sigs/s on 2 tiles)")
     ap.add_argument("--stream-inflight", type=int, default=1,
                     help="batches a tile keeps launched on its GPU stream before it launches the filling one "
                          "(1: a frag waits for at most the running batch; tools/stream_sweep.py, s13)")
@@ -458,7 +466,8 @@ def main():
                                       "T verify tiles (seq % T round robin, tile i -> GPU i % G; device fd_txn_parse "
                                       "+ verify, in-order after_frag, dedup tcache) -> out dcache",
                           "sigs_per_s": mx["sigs_per_s"], "per_gpu_sigs_per_s": mx["sigs_per_s"] / world,
-                          "n_gpus": world, "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_batch,
+                          "n_gpus": world, "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_max_batch,
+                          "batch_paced": args.stream_batch,
                           "max_inflight": args.stream_inflight,
                           "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
                           "process": "one tile process per GPU without a torch GPU context (as a C verify tile); "
