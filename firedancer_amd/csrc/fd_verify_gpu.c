@@ -322,8 +322,10 @@ vt_ctx_new( fdgpu_vtile_t const * vt ) {
   ulong b = vt->batch;
   fdgpu_ed25519_ctx_t * c = fdgpu_ed25519_ctx_new( vt->device, b, 16UL*b, b*2304UL + 1024UL, vt->semantics );
   if( c ) {
+    /* latency path for batches up to half the batch limit (env FDGPU_VTILE_SMALL_MAX overrides) */
     ulong sm = fdgpu_ed25519_set_small_batch_max( c, 0UL );
-    fdgpu_ed25519_set_small_batch_max( c, sm < b/2UL ? sm : b/2UL );
+    char const * e = getenv( "FDGPU_VTILE_SMALL_MAX" );
+    fdgpu_ed25519_set_small_batch_max( c, e ? strtoul( e, NULL, 0 ) : ( sm < b/2UL ? sm : b/2UL ) );
     /* the GPU computes the HA dedup tags and, for gathered records, stores
        txn_t_sz: after_frag then touches neither payload nor record */
     fdgpu_ed25519_set_dedup( c, vt->gpu_tag, vt->seed );
