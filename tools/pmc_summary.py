@@ -8,8 +8,11 @@ Corrections (MI355X_MICROARCH.md, HBM section):
   * gfx950 FETCH_SIZE counts 128-B requests as 64 B for wide streaming
     reads: hbm_read_bytes = 2 x FETCH_SIZE x 1024 (an upper estimate for
     the DSM's 16-B-per-lane gathers, which are not calibrated).
-  * GRBM_GUI_ACTIVE is summed over the 8 XCDs; VALU busy =
-    SQ_ACTIVE_INST_VALU x 4 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8).
+  * GRBM_GUI_ACTIVE is summed over the 8 XCDs; valu_busy_flat4 =
+    SQ_ACTIVE_INST_VALU x 4 cycles / (1024 SIMDs x GRBM_GUI_ACTIVE / 8) -- a
+    flat 4-cycle price per instruction, kept for comparison with round 1.
+    The measured-cost form is tools/dsm_issue_model.py (profiles/r02/
+    roofline/issue_model.json), which dsm_pmc.json carries as valu_busy.
 usage: tools/pmc_summary.py gpurun_out/prof_<tag> profiles/<round>/<tag>
 """
 import collections
@@ -37,7 +40,7 @@ for k, c in per.items():
     if "WRITE_SIZE" in m:
         e["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
     if "SQ_ACTIVE_INST_VALU" in m and m.get("GRBM_GUI_ACTIVE"):
-        e["valu_busy"] = m["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * m["GRBM_GUI_ACTIVE"] / 8)
+        e["valu_busy_flat4"] = m["SQ_ACTIVE_INST_VALU"] * 4 / (1024 * m["GRBM_GUI_ACTIVE"] / 8)
     if "SQ_INSTS_VALU" in m and m.get("SQ_WAVES"):
         e["valu_insts_per_wave"] = m["SQ_INSTS_VALU"] / m["SQ_WAVES"]
     out[k] = e
@@ -48,6 +51,8 @@ if os.path.exists(stats):
 # the bench line printed by the profiled run itself: its HIP-event kernel_ms must agree with
 # rocprof's average duration of the same launches
 blog = os.path.join(src, "bench_under_rocprof.log")
+if not os.path.exists(blog):
+    blog = os.path.join(src, "bench_under_rocprof.json")
 if os.path.exists(blog):
     for line in open(blog):
         if line.startswith('{"metric"'):
@@ -63,9 +68,12 @@ if os.path.exists(blog):
             print("agreement", agree)
 d = out.get("fd_dsm_kernel")
 if d and "hbm_read_bytes" in d:
+    im = os.path.join(os.path.dirname(dst.rstrip("/")), "roofline", "issue_model.json")
+    busy = json.load(open(im))["valu_busy_model"] if os.path.exists(im) else None
     json.dump({"kernel": "fd_dsm_kernel", "source": dst,
                "hbm_bytes_per_launch": d["hbm_read_bytes"] + d.get("hbm_write_bytes", 0),
-               "valu_busy": d.get("valu_busy"), "valu_insts_per_wave": d.get("valu_insts_per_wave")},
+               "valu_busy": busy, "valu_busy_source": im if busy is not None else None,
+               "valu_busy_flat4": d.get("valu_busy_flat4"), "valu_insts_per_wave": d.get("valu_insts_per_wave")},
               open(os.path.join(os.path.dirname(dst.rstrip("/")), "..", "dsm_pmc.json"), "w"), indent=1)
 for k, e in sorted(out.items()):
     print(k, {x: (round(y, 3) if isinstance(y, float) else y) for x, y in e.items() if x != "counters_mean_per_launch"})
