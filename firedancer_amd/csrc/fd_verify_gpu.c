@@ -285,6 +285,7 @@ struct fdgpu_vtile {
   int                   device, semantics;   /* to recreate a faulted context */
   int                   fault_seen[ VT_NCTX_MAX ];
   int                   gpu_tag;         /* HA dedup tags from the GPU (env FDGPU_VTILE_GPU_TAG, default 1) */
+  ulong                 min_batch, max_wait_ns, fill_t0;   /* see fdgpu_vtile_housekeep */
   fdgpu_vtile_gpu_metrics_t gm;
   int                   nctx, fill;      /* contexts, the one taking frags */
   ulong                 launch_ns[ VT_NCTX_MAX ];
@@ -348,6 +349,8 @@ fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ul
   vt->batch_ns = 500e3;
   vt->device = device; vt->semantics = semantics; vt->batch = batch_txn; vt->seed = seed;
   { char const * g = getenv( "FDGPU_VTILE_GPU_TAG" ); vt->gpu_tag = g ? atoi( g ) != 0 : 1; }
+  { char const * m = getenv( "FDGPU_VTILE_MIN_BATCH" ); vt->min_batch = m ? strtoul( m, NULL, 0 ) : 0UL;
+    char const * w = getenv( "FDGPU_VTILE_MAX_WAIT_US" ); vt->max_wait_ns = 1000UL * ( w ? strtoul( w, NULL, 0 ) : 2000UL ); }
   int ctx_ok = 1;
   for( int k=0; k<vt->nctx; k++ ) if( !( vt->ctx[k] = vt_ctx_new( vt ) ) ) ctx_ok = 0;
   vt->tcache = fdgpu_tcache_new( tcache_depth );
@@ -496,6 +499,9 @@ fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
      frags and the pipeline would degenerate into tiny batches */
   if( max_inflight > 3UL ) max_inflight = 3UL;
   if( !filling || inflight >= max_inflight ) return 0;
+  /* throughput knob (env FDGPU_VTILE_MIN_BATCH / _MAX_WAIT_US): a partial batch smaller than
+     min_batch waits until its oldest frag has waited max_wait -- bigger GPU batches under load */
+  if( filling < vt->min_batch && now - vt->fill_t0 < vt->max_wait_ns ) return 0;
   if( vt->nctx > 1 && filling < vt->batch ) {
     /* stagger: launch once every other context's newest batch has run
        batch_ns / nctx (or that context is idle) */
@@ -534,6 +540,10 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   if( rc ) return rc;
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
   p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill;
+  if( vt->min_batch ) {                          /* first frag of the filling batch: its wait starts */
+    ulong f, i; fdgpu_ed25519_pipeline_state( vt->ctx[ vt->fill ], &f, &i );
+    if( f == 1UL ) vt->fill_t0 = now_ns();
+  }
   p->bundle_id = in->bundle_id; p->payload_sz = in->payload_sz;
   vt->pend_tail++;
   ulong reserve = ( ( FDGPU_TXNM_HDR_SZ + in->payload_sz + 1UL ) & ~1UL ) + 852UL;
