@@ -179,6 +179,7 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
             "p50_us": st["lat_p50_us"], "p99_us": st["lat_p99_us"], "max_us": st["lat_max_us"],
             "published": st["published"], "metrics": st["metrics"],
             "tile_host_ns_per_frag": [round(x / n, 1) for x in st["tile_ns"]],
+            "tile_after_split_ns_per_frag": {k: round(st[k] / n, 1) for k in ("gpu_wait_ns", "poll_ns", "after_ns", "launch_ns")},
             "batches": st["batches"], "mean_batch_txns": st["batch_txns"] / max(st["batches"], 1),
             "inflight_max": st["inflight_max"], "gpu_batch_lat_p50_us_le": hq(0.5),
             "gpu_batch_lat_p99_us_le": hq(0.99)}

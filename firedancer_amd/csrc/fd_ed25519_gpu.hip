@@ -1314,6 +1314,7 @@ struct fdgpu_ed25519_ctx {
   unsigned long dedup_seed;
   int rec_fp_off;                /* gathered records: offset of a u16 footprint field, -1 = none */
   unsigned long n_batches, n_txns;                /* async batches launched, transactions in them */
+  unsigned long launch_ns;                        /* host time inside slot_launch */
   unsigned long volatile * h_flag;                /* per slot: completion token written by fd_done_kernel (pinned) */
   unsigned long * d_flag;
   unsigned long lat_hist[ FDGPU_LAT_BUCKETS ];    /* launch -> verdicts seen by poll, quarter-octave buckets */
@@ -1947,7 +1948,14 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
    ahead of the work it waits for in a shared queue.  Overlap of one
    context's upload with another's kernels comes from running several
    contexts, one per verify tile.) */
+static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i );
 static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
+  unsigned long t0 = fd_now_ns();
+  int rc = slot_launch_( ctx, i );
+  ctx->launch_ns += fd_now_ns() - t0;
+  return rc;
+}
+static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
   fd_slot & sl = ctx->slot[i];
   hipStream_t st = ctx->stream;
   if( sl.mode==2 ) {   /* in place: one upload of the caller's region range, no host copy */
@@ -2182,6 +2190,21 @@ fdgpu_host_register( void * p, unsigned long sz ) {
 extern "C" void
 fdgpu_host_unregister( void * p ) { if( p ) { region_del( p ); (void)hipHostUnregister( p ); } }
 
+extern "C" int
+fdgpu_device_numa_node( int device ) {
+  char bus[ 64 ];
+  if( hipDeviceGetPCIBusId( bus, (int)sizeof(bus), device ) != hipSuccess ) return -1;
+  for( char * c = bus; *c; c++ ) if( *c >= 'A' && *c <= 'F' ) *c = (char)( *c - 'A' + 'a' );
+  char path[ 128 ];
+  snprintf( path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus );
+  FILE * f = fopen( path, "r" );
+  if( !f ) return -1;
+  int node = -1;
+  if( fscanf( f, "%d", &node ) != 1 ) node = -1;
+  fclose( f );
+  return node;
+}
+
 /* Gathered raw submission: the record (copy_sz bytes at src, the payload
    at src + payload_off) stays where the caller's producer wrote it, in a
    registered host region; the batch's gather kernel copies it into the
@@ -2281,6 +2304,11 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
 }
 
 extern "C" int fdgpu_ed25519_faulted( fdgpu_ed25519_ctx_t const * ctx ) { return ctx ? ctx->fault : 1; }
+
+extern "C" void
+fdgpu_ed25519_launch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * launch_ns, unsigned long * launches ) {
+  *launch_ns = ctx->launch_ns; *launches = ctx->n_batches;
+}
 
 extern "C" void
 fdgpu_ed25519_batch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * batches, unsigned long * txns,

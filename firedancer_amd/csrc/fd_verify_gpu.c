@@ -9,6 +9,7 @@
 
 #include <fcntl.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -452,12 +453,13 @@ fdgpu_vtile_gpu_metrics( fdgpu_vtile_t const * vt, fdgpu_vtile_gpu_metrics_t * o
   *out = vt->gm;
   ulong f, i, infl = 0UL;
   memset( out->lat_hist, 0, sizeof(out->lat_hist) );
-  out->batches = out->batch_txns = 0UL;
+  out->batches = out->batch_txns = out->launch_ns = 0UL;
   for( int k=0; k<vt->nctx; k++ ) {
     fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i ); infl += i;
     /* the engine counts every launch (a full slot launches inside submit) and times each batch */
     ulong b, t, h[ FDGPU_LAT_BUCKETS ];
     fdgpu_ed25519_batch_stats( vt->ctx[k], &b, &t, h );
+    ulong lns, nl; fdgpu_ed25519_launch_stats( vt->ctx[k], &lns, &nl ); out->launch_ns += lns;
     out->batches += b; out->batch_txns += t;
     for( int j=0; j<FDGPU_LAT_BUCKETS; j++ ) out->lat_hist[j] += h[j];
   }
@@ -632,8 +634,11 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
       }
       continue;
     }
+    ulong tw = now_ns();
     ulong k = fdgpu_ed25519_poll_raw( vt->ctx[c], vt->p_tags, vt->p_codes, vt->zc ? NULL : vt->p_img, vt->p_fp, vt->p_dtag,
                                       want, blocking );
+    ulong tp = now_ns();
+    if( blocking ) vt->gm.wait_ns += tp - tw; else vt->gm.poll_ns += tp - tw;
     if( !k ) {
       if( fdgpu_ed25519_faulted( vt->ctx[c] ) ) continue;   /* failed just now: complete its frags above */
       break;
@@ -661,6 +666,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
                                 vt->p_dtag[i], &out[n] );
       vt->pend_head++; n++;
     }
+    vt->gm.after_ns += now_ns() - tp;
     blocking = 0;
   }
   return n;
@@ -683,7 +689,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
    falls a lap behind is overrun: it resumes at the seq it found
    (fd_stem.c:590-596, 676-688) and the frags it skipped are counted. */
 
-#define LINK_MAGIC    0xfd6e11c0ffee0002UL
+#define LINK_MAGIC    0xfd6e11c0ffee0003UL
 #define LINK_TILE_MAX 64
 
 /* Latency histogram (per tile, merged at the end): log-linear buckets,
@@ -724,7 +730,7 @@ typedef struct {
   ulong         total_sz;
   fdgpu_stream_cfg_t cfg;
   ulong         depth, n_payload, in_bytes;
-  ulong         off_mcache, off_dcache, off_chunk, off_sz, off_res, off_hist;
+  ulong         off_mcache, off_dcache, off_chunk, off_sz, off_psig, off_res, off_hist;
   _Atomic ulong joined, tiles_ready, tiles_done, go, fail;
   ulong         t_start;
   struct { _Atomic ulong v; uchar pad[56]; } fseq[ LINK_TILE_MAX ];   /* next seq each tile has yet to consume */
@@ -739,9 +745,11 @@ struct fdgpu_link {
   uchar *          dcache;
   unsigned *       chunk;
   unsigned short * psz;
+  uchar *          psig;         /* signatures of each payload (the first byte), for the stream's sigs/s */
   link_res_t *     res;
   ulong *          hist;
   fdgpu_mcache_t   mc;           /* local view of the shared lines (the tiles' in_mc) */
+  int              prod_cpu;     /* the producer thread's CPU (-1: not pinned) */
 };
 
 static ulong al64( ulong x ) { return ( x + 63UL ) & ~63UL; }
@@ -752,6 +760,7 @@ static void link_view( fdgpu_link_t * l ) {
   l->dcache = l->base + h->off_dcache;
   l->chunk  = (unsigned *)( l->base + h->off_chunk );
   l->psz    = (unsigned short *)( l->base + h->off_sz );
+  l->psig   = l->base + h->off_psig;
   l->res    = (link_res_t *)( l->base + h->off_res );
   l->hist   = (ulong *)( l->base + h->off_hist );
   l->mc.depth = h->depth; l->mc.line = l->line; l->mc.own = 0;
@@ -773,6 +782,7 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   ulong off_mcache = o;  o = al64( o + depth * sizeof(mc_line_t) );
   ulong off_chunk  = o;  o = al64( o + n_payload * sizeof(unsigned) );
   ulong off_sz     = o;  o = al64( o + n_payload * sizeof(unsigned short) );
+  ulong off_psig   = o;  o = al64( o + n_payload );
   ulong off_res    = o;  o = al64( o + T * sizeof(link_res_t) );
   ulong off_hist   = o;  o = al64( o + T * LH_N * sizeof(ulong) );
   o = ( o + 4095UL ) & ~4095UL;
@@ -797,7 +807,7 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   link_hdr_t * h = l->h;
   memset( (void *)h, 0, sizeof(link_hdr_t) );
   h->total_sz = total; h->cfg = *cfg; h->depth = depth; h->n_payload = n_payload; h->in_bytes = in_bytes;
-  h->off_mcache = off_mcache; h->off_dcache = off_dcache; h->off_chunk = off_chunk; h->off_sz = off_sz;
+  h->off_mcache = off_mcache; h->off_dcache = off_dcache; h->off_chunk = off_chunk; h->off_sz = off_sz; h->off_psig = off_psig;
   h->off_res = off_res; h->off_hist = off_hist;
   link_view( l );
   mc_init_lines( l->line, depth, 0UL );
@@ -809,6 +819,7 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
     txnm->payload_sz = sz[p];
     memcpy( (uchar *)txnm + FDGPU_TXNM_HDR_SZ, payload + off[p], sz[p] );
     l->chunk[p] = (unsigned)c; l->psz[p] = sz[p];
+    l->psig[p] = sz[p] ? payload[ off[p] ] : (uchar)0;
     c = fdgpu_dcache_compact_next( c, FDGPU_TXNM_HDR_SZ + sz[p], 0UL, ~0UL );
   }
   atomic_store_explicit( &h->joined, 1UL, memory_order_relaxed );
@@ -873,8 +884,10 @@ fdgpu_link_tiles_of( int tiles, int gpus, int proc, int * out ) {
 }
 void  fdgpu_link_cfg( fdgpu_link_t const * l, fdgpu_stream_cfg_t * cfg ) { *cfg = l->h->cfg; }
 
+static void link_pin( int cpu );
 static void * link_producer( void * _l ) {
   fdgpu_link_t * l = (fdgpu_link_t *)_l;
+  link_pin( l->prod_cpu );
   link_hdr_t * h = l->h;
   fdgpu_stream_cfg_t const * c = &h->cfg;
   ulong T = (ulong)c->tiles, mask = h->depth - 1UL;
@@ -916,7 +929,82 @@ static void * link_producer( void * _l ) {
   return NULL;
 }
 
-typedef struct { fdgpu_link_t * l; int idx, device; } link_tile_arg_t;
+/* CPU placement of the link's threads.  The reference pins every tile to
+   a core of its own (the [layout] affinity); here, by default, the
+   producer and this process's tiles take one hardware thread each of
+   distinct physical cores, on the GPU's NUMA node, filling one L3 (CCD)
+   before the next -- the mcache lines the producer writes and every tile
+   polls then move between cores that share an L3.  Process proc starts
+   at the L3 group proc % groups, so the processes of a multi-GPU run do
+   not share cores.  Env FDGPU_LINK_PIN: 0 = no pinning, an explicit
+   comma list of CPUs (producer first, then the tiles), else automatic. */
+#define LINK_CPU_MAX 1024
+static int cpulist_read( char const * path, uchar * set ) {
+  FILE * f = fopen( path, "r" );
+  if( !f ) return -1;
+  char buf[ 4096 ]; size_t n = fread( buf, 1, sizeof(buf)-1, f ); fclose( f ); buf[n] = 0;
+  char * c = buf;
+  while( *c ) {
+    char * e; long a = strtol( c, &e, 10 ), b = a;
+    if( e == c ) break;
+    if( *e == '-' ) { c = e + 1; b = strtol( c, &e, 10 ); }
+    for( long i=a; i<=b && i<LINK_CPU_MAX; i++ ) if( i >= 0 ) set[i] = 1;
+    c = e; if( *c == ',' ) c++; else break;
+  }
+  return 0;
+}
+static int cpu_first_of( char const * fmt, int cpu ) {          /* lowest CPU of a sysfs cpulist */
+  char path[ 160 ]; snprintf( path, sizeof(path), fmt, cpu );
+  static __thread uchar set[ LINK_CPU_MAX ];
+  memset( set, 0, sizeof(set) );
+  if( cpulist_read( path, set ) ) return cpu;
+  for( int i=0; i<LINK_CPU_MAX; i++ ) if( set[i] ) return i;
+  return cpu;
+}
+static int
+link_pick_cpus( int device, int proc, int n, int * out ) {
+  char const * env = getenv( "FDGPU_LINK_PIN" );
+  if( env && !strcmp( env, "0" ) ) return 0;
+  int got = 0;
+  if( env && *env >= '0' && *env <= '9' ) {                      /* explicit list (anything else: automatic) */
+    char const * c = env;
+    while( *c && got < n ) { char * e; long v = strtol( c, &e, 10 ); if( e == c ) break; out[got++] = (int)v; c = *e ? e + 1 : e; }
+    return got;
+  }
+  cpu_set_t aff; CPU_ZERO( &aff );
+  if( sched_getaffinity( 0, sizeof(aff), &aff ) ) return 0;
+  static uchar node_set[ LINK_CPU_MAX ];
+  memset( node_set, 0, sizeof(node_set) );
+  int node = fdgpu_device_numa_node( device ), use_node = 0;
+  if( node >= 0 ) {
+    char path[ 96 ]; snprintf( path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node );
+    use_node = !cpulist_read( path, node_set );
+  }
+  /* candidate cores: one hardware thread (the lowest sibling) of each allowed core */
+  int cand[ LINK_CPU_MAX ], grp[ LINK_CPU_MAX ], nc = 0;
+  for( int pass=0; pass<2 && !nc; pass++ )                       /* pass 1: ignore the node if it has no allowed CPU */
+    for( int c=0; c<LINK_CPU_MAX && c<CPU_SETSIZE; c++ ) {
+      if( !CPU_ISSET( c, &aff ) || ( pass==0 && use_node && !node_set[c] ) ) continue;
+      if( cpu_first_of( "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c ) != c ) continue;
+      cand[nc] = c; grp[nc] = cpu_first_of( "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", c ); nc++;
+    }
+  if( !nc ) return 0;
+  int gid[ LINK_CPU_MAX ], ng = 0;                               /* L3 groups in CPU order */
+  for( int i=0; i<nc; i++ ) { int k=0; while( k<ng && gid[k] != grp[i] ) k++; if( k==ng ) gid[ng++] = grp[i]; }
+  for( int r=0; r<ng && got<n; r++ ) {
+    int g = gid[ ( proc + r ) % ng ];
+    for( int i=0; i<nc && got<n; i++ ) if( grp[i] == g ) out[got++] = cand[i];
+  }
+  return got;
+}
+static void link_pin( int cpu ) {
+  if( cpu < 0 ) return;
+  cpu_set_t s; CPU_ZERO( &s ); CPU_SET( cpu, &s );
+  if( pthread_setaffinity_np( pthread_self(), sizeof(s), &s ) )
+    fprintf( stderr, "fdgpu_link: could not pin to CPU %d\n", cpu );
+}
+
+typedef struct { fdgpu_link_t * l; int idx, device, cpu; } link_tile_arg_t;
 
 /* credit a tile returns to the producer: every seq below it may be
    overwritten.  With zero-copy intake a frag's bytes must survive until
@@ -937,24 +1025,24 @@ static ulong own_in( ulong a, ulong b, ulong T, ulong idx ) {
 }
 
 static void
-link_account( fdgpu_link_t * l, fdgpu_vtile_t * vt, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs, ulong * lh,
-              ulong * lmax, ulong * t_last ) {
-  ulong t = now_ns();
+link_account( fdgpu_link_t * l, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs, ulong * lh, ulong * lmax,
+              ulong * t_last ) {
+  /* bench accounting only (not after_frag): the signature count comes from
+     the link's per-payload table, not from the (cold) record in the out dcache */
+  ulong t = now_ns(), np = l->h->n_payload;
   for( ulong i=0; i<n; i++ ) {
     ulong lat = t - d[i].tsorig;
     lh[ lh_idx( lat ) ]++;
     if( lat > *lmax ) *lmax = lat;
-    if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL ) {
-      uchar const * pl = fdgpu_vtile_out_dcache( vt ) + d[i].chunk * FDGPU_CHUNK_SZ + FDGPU_TXNM_HDR_SZ;
-      *sigs += pl[0];
-    }
+    if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL )
+      *sigs += l->psig[ d[i].seq % np ];
   }
-  (void)l;
   if( n ) *t_last = t;
 }
 
 static void * link_tile( void * _a ) {
   link_tile_arg_t * a = (link_tile_arg_t *)_a;
+  link_pin( a->cpu );                          /* before any allocation: first touch on the tile's node */
   fdgpu_link_t * l = a->l;
   link_hdr_t * h = l->h;
   fdgpu_stream_cfg_t const * c = &h->cfg;
@@ -974,7 +1062,7 @@ static void * link_tile( void * _a ) {
   ulong * lh = (ulong *)calloc( LH_N, sizeof(ulong) ), lmax = 0UL, t_last = 0UL;
   ulong sigs = 0UL, got = 0UL, lost = 0UL;
   ulong mine = own_in( 0UL, n_frags, T, (ulong)idx );
-  ulong seq = 0UL;
+  ulong seq = 0UL, credited = 0UL;
   ulong last_seq = ~0UL, last_got = ~0UL, t_prog = now_ns();
   ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, t_begin = now_ns();
   while( got + lost < mine ) {
@@ -988,52 +1076,48 @@ static void * link_tile( void * _a ) {
                idx, seq, got, lost, mine, fdgpu_vtile_pending( vt ), filling, inflight );
       atomic_store( &h->fail, 5 ); break;
     }
-    /* intake: up to 64 lines per pass.  Every seq's line is read, as the stem
-       loop does; before_frag keeps seq % T == idx. */
+    /* intake: up to 64 own frags per pass.  The stem loop reads every seq's
+       line and before_frag drops seq % T != idx; with the link's single
+       in-order producer a published line of seq implies every earlier seq
+       is published, so the tile reads only its own lines (the same frags,
+       without T-1 cross-core line transfers per own frag) */
     int drain = 0;
     for( int k=0; k<64 && seq < n_frags; k++ ) {
-      mc_line_t const * ln = &l->line[ seq & mask ];
-      if( ( seq % T ) != (ulong)idx ) {                             /* before_frag filters: the seq alone decides */
-        ulong s0 = atomic_load_explicit( (_Atomic ulong *)&ln->seq, memory_order_acquire );
-        if( s0 == seq ) {
-          seq++;
-          if( c->reliable && ( !(seq & 63UL) || seq == n_frags ) ) link_credit( h, idx, vt, seq );   /* batched credit return */
-          continue;
-        }
-        if( (long)( s0 - seq ) < 0 ) break;                         /* not yet published */
-        if( c->reliable ) { atomic_store( &h->fail, 3 ); break; }
-        lost += own_in( seq, s0, T, (ulong)idx ); seq = s0;          /* overrun while polling: resume there */
-        continue;
-      }
+      ulong own = seq + ( ( (ulong)idx + T - seq % T ) % T );      /* next seq with seq % T == idx */
+      if( own >= n_frags ) { seq = n_frags; break; }
+      mc_line_t const * ln = &l->line[ own & mask ];
       fdgpu_frag_meta_t m; ulong found;
-      int r = mc_poll( ln, seq, &m, &found );
-      if( r > 0 ) break;
+      int r = mc_poll( ln, own, &m, &found );
+      if( r > 0 ) break;                                            /* not yet published */
       if( r < 0 ) {
         if( c->reliable ) { atomic_store( &h->fail, 3 ); break; }
-        lost += own_in( seq, found, T, (ulong)idx ); seq = found;    /* overrun while polling / reading */
+        lost += own_in( own, found, T, (ulong)idx ); seq = found;    /* overrun while polling / reading: resume there */
         continue;
       }
-      int rc = fdgpu_vtile_during_frag( vt, l->dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, seq,
+      int rc = fdgpu_vtile_during_frag( vt, l->dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, own,
                                         ts_decomp( m.tsorig, t0 ) );   /* the pass's start is "now" to 2^31 ns */
-      if( rc == -2 ) { drain = 1; break; }                          /* staging full: drain, retry this seq */
+      if( rc == -2 ) { drain = 1; seq = own; break; }               /* staging full: drain, retry this seq */
       if( rc ) { fprintf( stderr, "fdgpu_link: tile %d during_frag %d\n", idx, rc ); atomic_store( &h->fail, 2 ); break; }
       /* this tile's next frag is usually published already: start its cold lines */
-      if( seq + T < n_frags ) {
-        mc_line_t const * nl = &l->line[ ( seq + T ) & mask ];
-        if( atomic_load_explicit( (_Atomic ulong *)&nl->seq, memory_order_relaxed ) == seq + T ) {
+      if( own + T < n_frags ) {
+        mc_line_t const * nl = &l->line[ ( own + T ) & mask ];
+        __builtin_prefetch( nl );
+        if( atomic_load_explicit( (_Atomic ulong *)&nl->seq, memory_order_relaxed ) == own + T ) {
           uchar const * pf = l->dcache + (ulong)nl->chunk * FDGPU_CHUNK_SZ;
           __builtin_prefetch( pf ); __builtin_prefetch( pf + 64 );
         }
       }
-      seq++;
-      if( c->reliable && ( !(seq & 63UL) || seq == n_frags ) ) link_credit( h, idx, vt, seq );   /* batched credit return */
+      seq = own + 1UL;
+      if( seq == n_frags ) seq = n_frags;
+      if( c->reliable && ( seq - credited >= 64UL || seq >= n_frags ) ) { link_credit( h, idx, vt, seq ); credited = seq; }   /* batched credit return */
     }
+    if( seq >= n_frags && c->reliable && credited < n_frags ) { link_credit( h, idx, vt, n_frags ); credited = n_frags; }
     ulong t1 = now_ns();
     ns_in += t1 - t0;
     if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
     if( drain || ( seq >= n_frags && fdgpu_vtile_pending( vt ) ) ) {
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
-      link_account( l, vt, done, n, &sigs, lh, &lmax, &t_last ); got += n;
+      link_account( l, done, n, &sigs, lh, &lmax, &t_last ); got += n;
       if( c->reliable && c->zero_copy ) link_credit( h, idx, vt, seq );
       ns_after += now_ns() - t1;
       continue;
@@ -1045,7 +1129,7 @@ static void * link_tile( void * _a ) {
       fdgpu_vtile_housekeep( vt, c->max_inflight );                 /* adaptive batching */
       ulong t2 = now_ns();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
-      link_account( l, vt, done, n, &sigs, lh, &lmax, &t_last ); got += n;
+      link_account( l, done, n, &sigs, lh, &lmax, &t_last ); got += n;
       if( c->reliable && c->zero_copy && n ) link_credit( h, idx, vt, seq );
       ns_hk += t2 - t1; ns_after += now_ns() - t2;
     }
@@ -1078,8 +1162,17 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   link_tile_arg_t args[ LINK_TILE_MAX ];
   int mine[ LINK_TILE_MAX ];
   int nt = fdgpu_link_tiles_of( c->tiles, c->gpus, proc, mine );   /* tile i drives GPU i % G: this process's tiles */
+  int cpus[ LINK_TILE_MAX + 1 ], np = run_producer ? 1 : 0;
+  int ncpu = link_pick_cpus( device, proc, nt + np, cpus );
+  l->prod_cpu = run_producer && ncpu > 0 ? cpus[0] : -1;
+  if( getenv( "FDGPU_LINK_VERBOSE" ) ) {
+    fprintf( stderr, "fdgpu_link: proc %d device %d numa %d cpus:", proc, device, fdgpu_device_numa_node( device ) );
+    for( int i=0; i<ncpu; i++ ) fprintf( stderr, " %d", cpus[i] );
+    fprintf( stderr, "\n" );
+  }
   for( int t=0; t<nt; t++ ) {
     args[t].l = l; args[t].idx = mine[t]; args[t].device = device;
+    args[t].cpu = np + t < ncpu ? cpus[ np + t ] : -1;
     pthread_create( &th[t], NULL, link_tile, &args[t] );
   }
   if( run_producer ) pthread_create( &prod, NULL, link_producer, l );
@@ -1111,6 +1204,8 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     st->batches += r->gm.batches; st->batch_txns += r->gm.batch_txns;
     if( r->gm.inflight_max > st->inflight_max ) st->inflight_max = r->gm.inflight_max;
     for( ulong k=0; k<FDGPU_VTILE_LAT_BUCKETS; k++ ) st->gpu_lat_hist[k] += r->gm.lat_hist[k];
+    st->gpu_wait_ns += r->gm.wait_ns; st->poll_ns += r->gm.poll_ns; st->after_ns += r->gm.after_ns;
+    st->launch_ns += r->gm.launch_ns;
     if( r->t_last > t_end ) t_end = r->t_last;
     if( r->lmax > lmax ) lmax = r->lmax;
     for( ulong k=0UL; k<LH_N; k++ ) lh[k] += l->hist[ i*LH_N + k ];

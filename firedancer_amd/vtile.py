@@ -47,7 +47,9 @@ class GpuMetrics(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_ulong), ("batch_txns", ctypes.c_ulong), ("inflight", ctypes.c_ulong),
                 ("inflight_max", ctypes.c_ulong), ("pending", ctypes.c_ulong), ("overruns", ctypes.c_ulong),
                 ("gpu_fault_frags", ctypes.c_ulong), ("faults", ctypes.c_ulong),
-                ("lat_hist", ctypes.c_ulong * LAT_BUCKETS)]
+                ("lat_hist", ctypes.c_ulong * LAT_BUCKETS), ("wait_ns", ctypes.c_ulong),
+                ("poll_ns", ctypes.c_ulong), ("after_ns", ctypes.c_ulong),
+                ("launch_ns", ctypes.c_ulong)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if k == "lat_hist" else int(getattr(self, k))) for k, _ in self._fields_}
@@ -66,7 +68,9 @@ class StreamStats(ctypes.Structure):
                 ("metrics", ctypes.c_ulong * 5), ("overruns", ctypes.c_ulong), ("tile_ns", ctypes.c_ulong * 4),
                 ("verdicts", ctypes.c_ulong), ("lost", ctypes.c_ulong), ("batches", ctypes.c_ulong),
                 ("batch_txns", ctypes.c_ulong), ("inflight_max", ctypes.c_ulong),
-                ("gpu_lat_hist", ctypes.c_ulong * LAT_BUCKETS), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int)]
+                ("gpu_lat_hist", ctypes.c_ulong * LAT_BUCKETS), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int),
+                ("gpu_wait_ns", ctypes.c_ulong), ("poll_ns", ctypes.c_ulong), ("after_ns", ctypes.c_ulong),
+                ("launch_ns", ctypes.c_ulong)]
 
     def as_dict(self) -> dict:
         out = {}

@@ -335,6 +335,11 @@ void
 fdgpu_ed25519_batch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * batches, unsigned long * txns,
                            unsigned long hist[ FDGPU_LAT_BUCKETS ] );
 
+/* host time the caller's thread spent inside ctx's batch launches (the
+   HIP calls that queue a batch's copies and kernels), ns, and how many */
+void
+fdgpu_ed25519_launch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * launch_ns, unsigned long * launches );
+
 /* 1 once a batch of ctx has failed on the device (poll then returns 0
    without blocking and every submit returns -3: the in-flight
    transactions are lost; delete and recreate the ctx). */
@@ -401,6 +406,11 @@ void   fdgpu_host_free ( void * p );
    success. */
 int    fdgpu_host_register  ( void * p, unsigned long sz );
 void   fdgpu_host_unregister( void * p );
+
+/* NUMA node of HIP device `device` (its PCI function's numa_node in
+   sysfs), -1 if unknown: where the threads that drive it and their pinned
+   buffers belong. */
+int    fdgpu_device_numa_node( int device );
 
 /* Gathered form (no host copy at all; the zero-copy staging of SURVEY.md
    §8f rank 2): the record -- copy_sz bytes at src, 16-B aligned, inside

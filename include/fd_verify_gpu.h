@@ -140,6 +140,10 @@ typedef struct fdgpu_vtile_gpu_metrics {
   unsigned long faults;           /* engine contexts seen faulted */
   unsigned long lat_hist[ FDGPU_VTILE_LAT_BUCKETS ];  /* per batch, launch -> verdicts polled, summed over the
                                                          tile's engine contexts (buckets: fdgpu_lat_bucket) */
+  unsigned long wait_ns;          /* host time after_frags spent blocked on a batch not yet complete */
+  unsigned long poll_ns;          /* ... in non-blocking completion polls (fdgpu_ed25519_poll_raw) */
+  unsigned long after_ns;         /* ... in after_frag proper (dedup, overrun check, publish) */
+  unsigned long launch_ns;        /* host time inside batch launches (in during_frag, housekeep or a drain) */
 } fdgpu_vtile_gpu_metrics_t;
 
 /* device: HIP device; batch_txn: transactions per GPU batch (staging
@@ -245,6 +249,9 @@ typedef struct fdgpu_stream_stats {
   unsigned long batches, batch_txns, inflight_max;
   unsigned long gpu_lat_hist[ FDGPU_VTILE_LAT_BUCKETS ];   /* batch launch -> drained, summed over tiles */
   int           tiles, gpus;
+  unsigned long gpu_wait_ns;     /* of tile_ns[1]: time blocked on batches not yet complete, summed over tiles */
+  unsigned long poll_ns, after_ns;   /* of tile_ns[1]: non-blocking completion polls; after_frag proper */
+  unsigned long launch_ns;       /* host time inside batch launches, summed over tiles (part of tile_ns[0..2]) */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per

@@ -322,3 +322,25 @@ def test_stream_bench_small(zero_copy):
     # 4096 distinct payloads cycled: the first copy of each publishes per tile, repeats are HA duplicates
     assert m[0] == 0 and m[1] == 0 and m[4] + m[2] == 50000 and m[4] >= 4096
     assert st["lat_p99_us"] > 0
+
+
+@pytest.mark.parametrize("tiles,reliable,zero_copy", [(3, True, True), (1, True, True), (2, True, False), (4, False, True)])
+def test_stream_run_link(tiles, reliable, zero_copy):
+    """The configs[4] link (fdgpu_stream_run): tile i takes seq % T == i, each tile polling its own
+    lines only.  Reliable: every frag gets exactly one verdict and the signature count is that of the
+    frags' payloads; unreliable: verdicts + frags lost to overruns = frags published."""
+    from firedancer_amd import synth, vtile
+    payload, desc, _, _ = synth.make_batch(3000, synth.MULTI, seed=21)
+    n = 40000 + tiles                                   # not a multiple of T: ragged last round
+    st = vtile.stream_run(payload, desc["payload_off"], desc["payload_sz"], n_frags=n, tiles=tiles, batch_txn=2048,
+                          mcache_depth=16384 if reliable else 4096, zero_copy=zero_copy, reliable=reliable)
+    assert st["frags"] == n
+    assert st["verdicts"] + st["lost"] == n
+    sig_cnt = np.array([payload[o] for o in desc["payload_off"]], np.uint64)
+    if reliable:
+        assert st["lost"] == 0 and st["verdicts"] == n and st["overruns"] == 0
+        assert st["sigs"] == int(sig_cnt[np.arange(n) % len(desc)].sum())
+        m = st["metrics"]
+        assert m[0] == 0 and m[1] == 0 and sum(m) == n          # no parse / verify failures in valid txns
+    else:
+        assert st["verdicts"] > 0

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Sweep the configs[4] verify stage on one GPU (fdgpu_stream_run: one producer link, T verify tiles,
 tile i -> GPU 0): one JSON line per point.  Env: TILES, RATE (frags/s, 0 = max), REL (1 reliable /
-0 unreliable), SECONDS, BATCH, INFL, ZC, VARIANTS (comma list of env assignments applied per point,
+0 unreliable), SECONDS, BATCH, INFL, ZC, DEPTH (mcache lines), VARIANTS (comma list of env assignments applied per point,
 e.g. "FDGPU_VTILE_GPU_TAG=1,FDGPU_VTILE_GPU_TAG=0"), NPAY (distinct payloads)."""
 import json
 import os
@@ -38,14 +38,14 @@ for var in variants:
                 nf = int((rate or 8e6) * secs)
                 st = vtile.stream_run(payload, desc["payload_off"], desc["payload_sz"], n_frags=nf, tiles=tiles,
                                       batch_txn=int(os.environ.get("BATCH", 8192)),
-                                      max_inflight=int(os.environ.get("INFL", 1)), mcache_depth=1 << 18,
+                                      max_inflight=int(os.environ.get("INFL", 1)), mcache_depth=int(os.environ.get("DEPTH", 1 << 18)),
                                       rate_fps=rate, zero_copy=bool(int(os.environ.get("ZC", 1))), reliable=bool(rel))
                 n = max(st["verdicts"], 1)
                 print(json.dumps({"variant": var, "reliable": rel, "tiles": tiles, "rate": rate, "frags": st["frags"],
                                   "verdicts": st["verdicts"], "lost": st["lost"], "overruns": st["overruns"],
                                   "sigs_per_s": round(st["sigs_per_s"]), "p50_us": st["lat_p50_us"],
                                   "p99_us": st["lat_p99_us"], "max_us": st["lat_max_us"],
-                                  "host_ns": [round(x / n, 1) for x in st["tile_ns"]],
+                                  "host_ns": [round(x / n, 1) for x in st["tile_ns"]], "wait_poll_after_ns": [round(st[k] / n, 1) for k in ("gpu_wait_ns", "poll_ns", "after_ns", "launch_ns")],
                                   "batches": st["batches"], "mean_batch": round(st["batch_txns"] / max(st["batches"], 1)),
                                   "inflight_max": st["inflight_max"], "gpu_lat_p50_us": lat_q(st["gpu_lat_hist"], .5),
                                   "gpu_lat_p99_us": lat_q(st["gpu_lat_hist"], .99), "metrics": st["metrics"]}),
