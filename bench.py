@@ -143,7 +143,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
     # the max-rate legs batch for throughput (a GPU batch under one wave per SIMD costs about one wave's
     # DSM chain, ~1 ms, whatever its size), the paced leg for latency
     base = dict(batch_txn=args.stream_max_batch if leg != "paced" else args.stream_batch,
-                max_inflight=args.stream_inflight, zero_copy=not args.stream_copy, gpus=procs, mcache_depth=1 << 18)
+                max_inflight=args.stream_inflight, zero_copy=not args.stream_copy, gpus=procs,
+                mcache_depth=args.stream_depth if leg != "paced" else 1 << 18)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -180,6 +181,8 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
             "published": st["published"], "metrics": st["metrics"],
             "tile_host_ns_per_frag": [round(x / n, 1) for x in st["tile_ns"]],
             "tile_after_split_ns_per_frag": {k: round(st[k] / n, 1) for k in ("gpu_wait_ns", "poll_ns", "after_ns", "launch_ns")},
+            "tile_idle_ns_per_frag": round(st["tile_idle_ns"] / n, 1), "producer_seconds": st["prod_seconds"],
+            "producer_credit_wait_s": st["prod_wait_ns"] * 1e-9,
             "batches": st["batches"], "mean_batch_txns": st["batch_txns"] / max(st["batches"], 1),
             "inflight_max": st["inflight_max"], "gpu_batch_lat_p50_us_le": hq(0.5),
             "gpu_batch_lat_p99_us_le": hq(0.99)}
@@ -234,7 +237,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-tiles", str(args.stream_tiles), "--stream-batch", str(args.stream_batch),
            "--stream-max-batch", str(args.stream_max_batch),
            "--stream-rate", str(args.stream_rate), "--stream-lat-tiles", str(args.stream_lat_tiles),
-           "--stream-inflight", str(args.stream_inflight)]
+           "--stream-inflight", str(args.stream_inflight), "--stream-depth", str(args.stream_depth)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -260,8 +263,8 @@ def main():
     ap.add_argument("--stream-unrel-seconds", type=float, default=4.0,
                     help="frags of the unreliable unthrottled leg, in seconds of the calibrated rate")
     ap.add_argument("--stream-tiles", type=int, default=2,
-                    help="verify tiles per GPU of the max-rate legs (profiles/r02/stream/sweep_*: 2 tiles 12.4M, "
-                         "4 tiles 9.8-12.5M, 6 tiles 9.3M sigs/s -- more tiles, more HIP streams on 4 hardware queues)")
+                    help="verify tiles per GPU of the max-rate legs (profiles/r02/stream/sweep_depth.md: at depth 2^20 "
+                         "2 tiles 16.2-17.6M, 3 tiles 15-17.3M, 4 tiles 13.1-16.1M, 6 tiles 12.4-14.1M sigs/s)")
     ap.add_argument("--stream-copy", action="store_true",
                     help="stream tiles copy each frag into the out dcache on the host (the reference tile's "
                          "during_frag) instead of the zero-copy intake (GPU gathers from the registered in dcache)")
@@ -269,9 +272,14 @@ def main():
     ap.add_argument("--stream-max-batch", type=int, default=65536,
                     help="GPU batch limit (txns) of the max-rate legs (profiles/r02/stream: batches of 8192 give "
                          "7.2M, of up to 32768 13.7M sigs/s on 2 tiles)")
-    ap.add_argument("--stream-inflight", type=int, default=1,
-                    help="batches a tile keeps launched on its GPU stream before it launches the filling one "
-                         "(1: a frag waits for at most the running batch; tools/stream_sweep.py, s13)")
+    ap.add_argument("--stream-inflight", type=int, default=2,
+                    help="batches a tile's engine context keeps launched before housekeeping launches its filling "
+                         "one (a full batch launches regardless); 2: 17.5M vs 16.8M sigs/s at 1 on 2 tiles "
+                         "(profiles/r02/stream/sweep_depth.md)")
+    ap.add_argument("--stream-depth", type=int, default=1 << 20,
+                    help="mcache lines of the max-rate legs' link: a reliable producer runs depth/2 ahead of the "
+                         "oldest frag a tile still holds, so the depth bounds the frags in flight (2^18: 13.8M, "
+                         "2^20: 16-17.6M sigs/s on 2 tiles, profiles/r02/stream/sweep_depth.log)")
     ap.add_argument("--stream-rate", type=float, default=2e6, help="paced leg: offered frags/s per GPU")
     ap.add_argument("--stream-lat-tiles", type=int, default=2,
                     help="verify tiles per GPU of the paced leg (fewer tiles = fewer HIP streams sharing the "

@@ -2325,6 +2325,13 @@ fdgpu_ed25519_debug_fault( fdgpu_ed25519_ctx_t * ctx ) {
   fd_err = "fdgpu_ed25519_poll: batch failed: injected by fdgpu_ed25519_debug_fault";
 }
 
+extern "C" unsigned long
+fdgpu_ed25519_front_remaining( fdgpu_ed25519_ctx_t const * ctx ) {
+  if( ctx->inflight.empty() ) return 0UL;
+  fd_slot const & sl = ctx->slot[ ctx->inflight.front() ];
+  return sl.txn_cnt - sl.cursor;
+}
+
 extern "C" void
 fdgpu_ed25519_pipeline_state( fdgpu_ed25519_ctx_t const * ctx, unsigned long * filling, unsigned long * inflight ) {
   *filling  = ctx->slot[ ctx->cur ].state==0 ? ctx->slot[ ctx->cur ].txn_cnt : 0UL;

@@ -10,6 +10,7 @@
 #include <fcntl.h>
 #include <pthread.h>
 #include <sched.h>
+#include <x86intrin.h>
 #include <stdio.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -614,11 +615,11 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
        the head that went to the same context (each context completes in
        its own submission order) */
     int c = vt->pend[ vt->pend_head % vt->pend_cap ].k;
-    ulong want = 1UL, lim = max - n;
-    if( lim > vt->batch ) lim = vt->batch;
-    while( want < lim && vt->pend_head + want < vt->pend_tail &&
-           vt->pend[ ( vt->pend_head + want ) % vt->pend_cap ].k == c ) want++;
+    ulong want, lim = max - n;
     if( fdgpu_ed25519_faulted( vt->ctx[c] ) ) {
+      want = 1UL;
+      while( want < lim && vt->pend_head + want < vt->pend_tail &&
+             vt->pend[ ( vt->pend_head + want ) % vt->pend_cap ].k == c ) want++;
       /* the context's batches failed on the device: its frags will never get a
          verdict.  Complete them, in order, as FDGPU_VTILE_GPU_FAULT (never
          published, never blocked on); the caller treats that as the
@@ -634,6 +635,12 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
       }
       continue;
     }
+    /* the frag at the head is the next verdict of context c's oldest launched batch, whose
+       frags are contiguous in the pending ring: poll at most what that batch has left (0: the
+       head frag's batch is still filling) */
+    want = fdgpu_ed25519_front_remaining( vt->ctx[c] );
+    if( want > lim ) want = lim;
+    if( !want ) break;                         /* (a blocking call launched every filling batch above) */
     ulong tw = now_ns();
     ulong k = fdgpu_ed25519_poll_raw( vt->ctx[c], vt->p_tags, vt->p_codes, vt->zc ? NULL : vt->p_img, vt->p_fp, vt->p_dtag,
                                       want, blocking );
@@ -721,6 +728,8 @@ typedef struct {                 /* one tile's results, written once when it fin
   ulong sigs, t_last, lmax;
   ulong metrics[5];
   ulong ns[4];                   /* during_frag intake (mcache polls + submit), after_frags, housekeep, whole loop */
+  ulong ns_idle;                 /* of ns[0]: intake passes that found nothing published */
+  ulong prof[ 8 ];               /* FDGPU_LINK_PROF=1: section times, ns (fdgpu_stream_stats_t prof_ns) */
   fdgpu_vtile_gpu_metrics_t gm;
   ulong device;
 } link_res_t;
@@ -733,6 +742,7 @@ typedef struct {
   ulong         off_mcache, off_dcache, off_chunk, off_sz, off_psig, off_res, off_hist;
   _Atomic ulong joined, tiles_ready, tiles_done, go, fail;
   ulong         t_start;
+  ulong         prod_end, prod_wait_ns;   /* producer: last publish, time waiting for credits */
   struct { _Atomic ulong v; uchar pad[56]; } fseq[ LINK_TILE_MAX ];   /* next seq each tile has yet to consume */
 } link_hdr_t;
 
@@ -906,10 +916,10 @@ static void * link_producer( void * _l ) {
   for( ulong seq=0; seq<c->n_frags; seq++ ) {
     if( c->reliable ) {
       ulong t_wait = 0UL;
+      if( seq >= cr_until ) t_wait = now_ns();
       while( seq >= cr_until ) {
         if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) return NULL;
-        if( !t_wait ) t_wait = now_ns();
-        else if( now_ns() - t_wait > 30000000000UL ) {            /* watchdog: 30 s without credits */
+        if( now_ns() - t_wait > 30000000000UL ) {                  /* watchdog: 30 s without credits */
           fprintf( stderr, "fdgpu_link: producer starved of credits at seq %lu\n", seq );
           atomic_store( &h->fail, 4 ); return NULL;
         }
@@ -917,6 +927,7 @@ static void * link_producer( void * _l ) {
         for( ulong t=0; t<T; t++ ) { ulong f = atomic_load_explicit( &h->fseq[t].v, memory_order_acquire ); if( f < lo ) lo = f; }
         cr_until = lo + h->depth/2;
       }
+      if( t_wait ) h->prod_wait_ns += now_ns() - t_wait;
     }
     if( c->rate_fps > 0. ) {
       ulong due = t0 + (ulong)( (double)seq * 1e9 / c->rate_fps );
@@ -926,6 +937,7 @@ static void * link_producer( void * _l ) {
     unsigned ts = (unsigned)now_ns();
     mc_publish( &l->line[ seq & mask ], seq, 0UL, l->chunk[p], (unsigned)( FDGPU_TXNM_HDR_SZ + l->psz[p] ), ts, ts );
   }
+  h->prod_end = now_ns();
   return NULL;
 }
 
@@ -1064,7 +1076,14 @@ static void * link_tile( void * _a ) {
   ulong mine = own_in( 0UL, n_frags, T, (ulong)idx );
   ulong seq = 0UL, credited = 0UL;
   ulong last_seq = ~0UL, last_got = ~0UL, t_prog = now_ns();
-  ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, t_begin = now_ns();
+  ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, ns_idle = 0UL, t_begin = now_ns();
+  /* FDGPU_LINK_PROF=1: rdtsc section profile (mcache poll, during_frag, prefetch + credit, drain
+     after_frags, housekeep after_frags, link_account, credit after a drain, housekeep) */
+  char const * pe = getenv( "FDGPU_LINK_PROF" );
+  int prof = pe && atoi( pe );
+  ulong pc[ 8 ] = { 0 }, c_begin = __rdtsc(), cx = 0UL;
+#define PROF_T0()    do { if( prof ) cx = __rdtsc(); } while( 0 )
+#define PROF_ADD(i)  do { if( prof ) { ulong cy_ = __rdtsc(); pc[i] += cy_ - cx; cx = cy_; } } while( 0 )
   while( got + lost < mine ) {
     if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
     ulong t0 = now_ns();
@@ -1082,13 +1101,16 @@ static void * link_tile( void * _a ) {
        is published, so the tile reads only its own lines (the same frags,
        without T-1 cross-core line transfers per own frag) */
     int drain = 0;
+    ulong seq_pass0 = seq;
     for( int k=0; k<64 && seq < n_frags; k++ ) {
       ulong own = seq + ( ( (ulong)idx + T - seq % T ) % T );      /* next seq with seq % T == idx */
       if( own >= n_frags ) { seq = n_frags; break; }
       mc_line_t const * ln = &l->line[ own & mask ];
       fdgpu_frag_meta_t m; ulong found;
+      PROF_T0();
       int r = mc_poll( ln, own, &m, &found );
       if( r > 0 ) break;                                            /* not yet published */
+      PROF_ADD( 0 );
       if( r < 0 ) {
         if( c->reliable ) { atomic_store( &h->fail, 3 ); break; }
         lost += own_in( own, found, T, (ulong)idx ); seq = found;    /* overrun while polling / reading: resume there */
@@ -1096,6 +1118,7 @@ static void * link_tile( void * _a ) {
       }
       int rc = fdgpu_vtile_during_frag( vt, l->dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, own,
                                         ts_decomp( m.tsorig, t0 ) );   /* the pass's start is "now" to 2^31 ns */
+      PROF_ADD( 1 );
       if( rc == -2 ) { drain = 1; seq = own; break; }               /* staging full: drain, retry this seq */
       if( rc ) { fprintf( stderr, "fdgpu_link: tile %d during_frag %d\n", idx, rc ); atomic_store( &h->fail, 2 ); break; }
       /* this tile's next frag is usually published already: start its cold lines */
@@ -1110,15 +1133,21 @@ static void * link_tile( void * _a ) {
       seq = own + 1UL;
       if( seq == n_frags ) seq = n_frags;
       if( c->reliable && ( seq - credited >= 64UL || seq >= n_frags ) ) { link_credit( h, idx, vt, seq ); credited = seq; }   /* batched credit return */
+      PROF_ADD( 2 );
     }
     if( seq >= n_frags && c->reliable && credited < n_frags ) { link_credit( h, idx, vt, n_frags ); credited = n_frags; }
     ulong t1 = now_ns();
     ns_in += t1 - t0;
+    if( seq == seq_pass0 && !drain ) ns_idle += t1 - t0;
     if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
     if( drain || ( seq >= n_frags && fdgpu_vtile_pending( vt ) ) ) {
+      PROF_T0();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
+      PROF_ADD( 3 );
       link_account( l, done, n, &sigs, lh, &lmax, &t_last ); got += n;
+      PROF_ADD( 5 );
       if( c->reliable && c->zero_copy ) link_credit( h, idx, vt, seq );
+      PROF_ADD( 6 );
       ns_after += now_ns() - t1;
       continue;
     }
@@ -1126,20 +1155,30 @@ static void * link_tile( void * _a ) {
        (the HIP runtime calls behind them take locks shared by all tiles) */
     if( t1 - t_hk >= 10000UL ) {
       t_hk = t1;
+      PROF_T0();
       fdgpu_vtile_housekeep( vt, c->max_inflight );                 /* adaptive batching */
+      PROF_ADD( 7 );
       ulong t2 = now_ns();
+      PROF_T0();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
+      PROF_ADD( 4 );
       link_account( l, done, n, &sigs, lh, &lmax, &t_last ); got += n;
+      PROF_ADD( 5 );
       if( c->reliable && c->zero_copy && n ) link_credit( h, idx, vt, seq );
+      PROF_ADD( 6 );
       ns_hk += t2 - t1; ns_after += now_ns() - t2;
     }
   }
   ulong t_end = now_ns();
   link_res_t * r = &l->res[idx];
+  double cyc_per_ns = (double)( __rdtsc() - c_begin ) / (double)( t_end - t_begin + 1UL );
+  for( int i=0; i<8; i++ ) r->prof[i] = prof ? (ulong)( (double)pc[i] / cyc_per_ns ) : 0UL;
+#undef PROF_T0
+#undef PROF_ADD
   r->verdicts = got; r->lost = lost; r->overruns = fdgpu_vtile_overruns( vt );
   r->sigs = sigs; r->t_last = t_last; r->lmax = lmax;
   fdgpu_vtile_metrics( vt, r->metrics );
-  r->ns[0] = ns_in; r->ns[1] = ns_after; r->ns[2] = ns_hk; r->ns[3] = t_end - t_begin;
+  r->ns[0] = ns_in; r->ns[1] = ns_after; r->ns[2] = ns_hk; r->ns[3] = t_end - t_begin; r->ns_idle = ns_idle;
   fdgpu_vtile_gpu_metrics( vt, &r->gm );
   r->device = (ulong)a->device;
   memcpy( l->hist + (ulong)idx * LH_N, lh, LH_N * sizeof(ulong) );
@@ -1206,11 +1245,15 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     for( ulong k=0; k<FDGPU_VTILE_LAT_BUCKETS; k++ ) st->gpu_lat_hist[k] += r->gm.lat_hist[k];
     st->gpu_wait_ns += r->gm.wait_ns; st->poll_ns += r->gm.poll_ns; st->after_ns += r->gm.after_ns;
     st->launch_ns += r->gm.launch_ns;
+    st->tile_idle_ns += r->ns_idle;
+    for( int k=0; k<8; k++ ) st->prof_ns[k] += r->prof[k];
     if( r->t_last > t_end ) t_end = r->t_last;
     if( r->lmax > lmax ) lmax = r->lmax;
     for( ulong k=0UL; k<LH_N; k++ ) lh[k] += l->hist[ i*LH_N + k ];
   }
   st->seconds = t_end > h->t_start ? (double)( t_end - h->t_start ) * 1e-9 : 0.;
+  st->prod_seconds = h->prod_end > h->t_start ? (double)( h->prod_end - h->t_start ) * 1e-9 : 0.;
+  st->prod_wait_ns = h->prod_wait_ns;
   st->frags = c->n_frags;
   st->published = st->metrics[4];
   st->frags_per_s = st->seconds > 0. ? (double)st->verdicts / st->seconds : 0.;

@@ -70,13 +70,14 @@ class StreamStats(ctypes.Structure):
                 ("batch_txns", ctypes.c_ulong), ("inflight_max", ctypes.c_ulong),
                 ("gpu_lat_hist", ctypes.c_ulong * LAT_BUCKETS), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int),
                 ("gpu_wait_ns", ctypes.c_ulong), ("poll_ns", ctypes.c_ulong), ("after_ns", ctypes.c_ulong),
-                ("launch_ns", ctypes.c_ulong)]
+                ("launch_ns", ctypes.c_ulong), ("tile_idle_ns", ctypes.c_ulong), ("prod_seconds", ctypes.c_double),
+                ("prod_wait_ns", ctypes.c_ulong), ("prof_ns", ctypes.c_ulong * 8)]
 
     def as_dict(self) -> dict:
         out = {}
         for k, _ in self._fields_:
             v = getattr(self, k)
-            out[k] = list(v) if k in ("metrics", "tile_ns", "gpu_lat_hist") else v
+            out[k] = list(v) if k in ("metrics", "tile_ns", "gpu_lat_hist", "prof_ns") else v
         return out
 
 

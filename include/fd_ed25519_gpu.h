@@ -358,6 +358,12 @@ fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx,
                     unsigned long         max,
                     int                   blocking );
 
+/* transactions of ctx's oldest launched batch not yet returned by a poll
+   (0 if none is in flight): the most one poll can return without moving
+   on to the next batch */
+unsigned long
+fdgpu_ed25519_front_remaining( fdgpu_ed25519_ctx_t const * ctx );
+
 /* Pipeline occupancy: transactions in the slot being filled, and
    launched slots not yet fully drained by poll.  Lets a caller launch
    early when the GPU is idle and let batches grow while it is busy. */

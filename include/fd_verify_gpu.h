@@ -252,6 +252,12 @@ typedef struct fdgpu_stream_stats {
   unsigned long gpu_wait_ns;     /* of tile_ns[1]: time blocked on batches not yet complete, summed over tiles */
   unsigned long poll_ns, after_ns;   /* of tile_ns[1]: non-blocking completion polls; after_frag proper */
   unsigned long launch_ns;       /* host time inside batch launches, summed over tiles (part of tile_ns[0..2]) */
+  unsigned long tile_idle_ns;    /* of tile_ns[0]: intake passes that found no frag published yet */
+  double        prod_seconds;    /* producer: first -> last publish */
+  unsigned long prod_wait_ns;    /* producer: time waiting for credits (reliable links) */
+  unsigned long prof_ns[ 8 ];    /* env FDGPU_LINK_PROF=1, summed over tiles: mcache poll, during_frag, prefetch +
+                                    credit, drain after_frags, housekeep after_frags, accounting, credit after
+                                    after_frags, housekeep (launch decisions) */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per

@@ -45,7 +45,9 @@ for var in variants:
                                   "verdicts": st["verdicts"], "lost": st["lost"], "overruns": st["overruns"],
                                   "sigs_per_s": round(st["sigs_per_s"]), "p50_us": st["lat_p50_us"],
                                   "p99_us": st["lat_p99_us"], "max_us": st["lat_max_us"],
-                                  "host_ns": [round(x / n, 1) for x in st["tile_ns"]], "wait_poll_after_ns": [round(st[k] / n, 1) for k in ("gpu_wait_ns", "poll_ns", "after_ns", "launch_ns")],
+                                  "host_ns": [round(x / n, 1) for x in st["tile_ns"]], "wait_poll_after_ns": [round(st[k] / n, 1) for k in ("gpu_wait_ns", "poll_ns", "after_ns", "launch_ns")], "idle_ns": round(st["tile_idle_ns"] / n, 1),
+                                  "prod_s": round(st["prod_seconds"], 3), "prod_wait_s": round(st["prod_wait_ns"] * 1e-9, 3),
+                                  "seconds": round(st["seconds"], 3), "prof_ns": [round(x / n, 1) for x in st["prof_ns"]],
                                   "batches": st["batches"], "mean_batch": round(st["batch_txns"] / max(st["batches"], 1)),
                                   "inflight_max": st["inflight_max"], "gpu_lat_p50_us": lat_q(st["gpu_lat_hist"], .5),
                                   "gpu_lat_p99_us": lat_q(st["gpu_lat_hist"], .99), "metrics": st["metrics"]}),

@@ -101,6 +101,24 @@ def main():
         out["queue_gap_us"] = {"p50": gaps[len(gaps) // 2] / 1e3, "p90": gaps[int(len(gaps) * .9)] / 1e3,
                                "sum_ms": sum(gaps) / 1e6}
     out["queues"] = len(byq)
+    # which kernel families run beside a DSM kernel, as a fraction of the DSM's time
+    qstream = defaultdict(set)
+    for r in ks:
+        qstream[r.get("Queue_Id", "?")].add(r.get("Stream_Id", "?"))
+    out["streams_per_queue"] = {q: sorted(v) for q, v in qstream.items()}
+    beside = defaultdict(int)
+    tot = 0
+    kev_s = sorted(kev)
+    for d in dsm:
+        s0, e0 = d[0], d[1]
+        tot += e0 - s0
+        for s, e, n, q in kev_s:
+            if s >= e0:
+                break
+            if e <= s0 or (s, e, n, q) == d:
+                continue
+            beside[n] += min(e, e0) - max(s, s0)
+    out["beside_dsm_frac"] = {n: round(v / max(tot, 1), 3) for n, v in sorted(beside.items(), key=lambda kv: -kv[1])}
     print(json.dumps(out, indent=1))
 
 
