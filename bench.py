@@ -143,7 +143,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
     # the max-rate legs batch for throughput (a GPU batch under one wave per SIMD costs about one wave's
     # DSM chain, ~1 ms, whatever its size), the paced leg for latency
     base = dict(batch_txn=args.stream_max_batch if leg != "paced" else args.stream_batch,
-                max_inflight=args.stream_inflight, zero_copy=not args.stream_copy, gpus=procs,
+                max_inflight=args.stream_inflight if leg != "paced" else args.stream_lat_inflight,
+                zero_copy=not args.stream_copy, gpus=procs,
                 mcache_depth=args.stream_depth if leg != "paced" else 1 << 18)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
@@ -237,7 +238,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-tiles", str(args.stream_tiles), "--stream-batch", str(args.stream_batch),
            "--stream-max-batch", str(args.stream_max_batch),
            "--stream-rate", str(args.stream_rate), "--stream-lat-tiles", str(args.stream_lat_tiles),
-           "--stream-inflight", str(args.stream_inflight), "--stream-depth", str(args.stream_depth)]
+           "--stream-inflight", str(args.stream_inflight), "--stream-depth", str(args.stream_depth),
+           "--stream-lat-inflight", str(args.stream_lat_inflight)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -276,6 +278,9 @@ def main():
                     help="batches a tile's engine context keeps launched before housekeeping launches its filling "
                          "one (a full batch launches regardless); 2: 17.5M vs 16.8M sigs/s at 1 on 2 tiles "
                          "(profiles/r02/stream/sweep_depth.md)")
+    ap.add_argument("--stream-lat-inflight", type=int, default=1,
+                    help="--stream-inflight of the paced leg (1: few, larger batches; 2 gave p50/p99 0.82/1.53 ms "
+                         "against 0.72/1.02 ms at 1, with 277-txn mean batches)")
     ap.add_argument("--stream-depth", type=int, default=1 << 20,
                     help="mcache lines of the max-rate legs' link: a reliable producer runs depth/2 ahead of the "
                          "oldest frag a tile still holds, so the depth bounds the frags in flight (2^18: 13.8M, "
@@ -477,7 +482,8 @@ def main():
                           "sigs_per_s": mx["sigs_per_s"], "per_gpu_sigs_per_s": mx["sigs_per_s"] / world,
                           "n_gpus": world, "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_max_batch,
                           "batch_paced": args.stream_batch,
-                          "max_inflight": args.stream_inflight,
+                          "max_inflight": args.stream_inflight, "max_inflight_paced": args.stream_lat_inflight,
+                          "link_depth": args.stream_depth,
                           "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
                           "process": "one tile process per GPU without a torch GPU context (as a C verify tile); "
                                      "link in /dev/shm when G > 1",
