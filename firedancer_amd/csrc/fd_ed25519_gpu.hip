@@ -418,7 +418,17 @@ __device__ unsigned long long fd_clk_buf[ FD_CLK_BLOCKS ][ 4 ];
 #define FD_CLK_END
 #endif
 
+/* FD_DSM_MINW: minimum waves per SIMD asked of the compiler for
+   fd_dsm_kernel (0: none; the register count then decides, 162 VGPRs ->
+   3 waves) */
+#ifndef FD_DSM_MINW
+#define FD_DSM_MINW 0
+#endif
+#if FD_DSM_MINW
+__global__ void __launch_bounds__( FD_WG, FD_DSM_MINW )
+#else
 __global__ void __launch_bounds__( FD_WG )
+#endif
 fd_dsm_kernel( u32                      nsig,
                uint4 const * __restrict__ tab,
                uint4 const * __restrict__ Rxy,

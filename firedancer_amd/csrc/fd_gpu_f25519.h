@@ -162,7 +162,7 @@ FD_DEV void fe_carry64( fe & r, u64 h[ 10 ] ) {
       COL( s_, ca );     r.v[s_]   = (u32)ca & FE_M(s_);   ca >>= FE_W(s_);  \
       COL( s_+5, cb );   r.v[s_+5] = (u32)cb & FE_M(s_+5); cb >>= FE_W(s_+5);\
     }                                                                        \
-    u64 t5_ = (u64)r.v[5] + ca;                                              \
+    u64 t5_ = fd_add32( ca, r.v[5] );                                         \
     r.v[5] = (u32)t5_ & FE_M(5); r.v[6] += (u32)( t5_ >> 25 );                \
     u64 t0_ = (u64)r.v[0] + cb * 19u;                                        \
     r.v[0] = (u32)t0_ & FE_M(0); r.v[1] += (u32)( t0_ >> 26 );                \
@@ -174,6 +174,37 @@ FD_DEV void fe_carry64( fe & r, u64 h[ 10 ] ) {
    instead of re-deriving it at every use (VALU-issue bound: every
    instruction counts). */
 #define FD_KEEP( x ) asm( "" : "+v"( x ) )
+
+/* 2x as x + x: on gfx950 v_add_u32 issues in 2.9 cycles per wave64 and
+   v_lshlrev_b32 (what the compiler emits for 2x) in 4.75 (tools/instprobe,
+   profiles/r02/roofline/instprobe.log); the asm also keeps the multiple in
+   one register like FD_KEEP.  FD_ADD2=0: the compiler's shift. */
+#ifndef FD_ADD2
+#define FD_ADD2 1
+#endif
+FD_DEV u32 fd_x2( u32 x ) {
+#if FD_ADD2
+  u32 r; asm( "v_add_u32 %0, %1, %1" : "=v"( r ) : "v"( x ) ); return r;
+#else
+  u32 r = 2u * x; FD_KEEP( r ); return r;
+#endif
+}
+
+/* acc + x for a 32-bit x as one v_mad_u64_u32 (x * 1 + acc, 4.66 cycles)
+   instead of zero-extending x (v_mov_b32) and a 64-bit add
+   (v_lshl_add_u64): 7.5 cycles.  FD_MAD1=0: the plain add. */
+#ifndef FD_MAD1
+#define FD_MAD1 1
+#endif
+FD_DEV u64 fd_add32( u64 acc, u32 x ) {
+#if FD_MAD1
+  u64 r, cy;   /* (the compiler folds a C multiply by 1 back into the add: spell the instruction) */
+  asm( "v_mad_u64_u32 %0, %1, %2, 1, %3" : "=v"( r ), "=s"( cy ) : "v"( x ), "v"( acc ) );
+  return r;
+#else
+  return acc + (u64)x;
+#endif
+}
 
 /* 19 g_j for j = 1..9 (the wrapped columns of a product with g) */
 struct fe19 { u32 v[10]; };
@@ -191,7 +222,7 @@ FD_DEV void fe_x19( fe19 & r, fe const & g ) {
 FD_DEV void fe_mul19( fe & r, fe const & f, fe const & g, fe19 const & g19 ) {
   u32 f2[10];
 #pragma unroll
-  for( int i=0; i<10; i++ ) { f2[i] = f.v[i]; if( i & 1 ) { f2[i] = 2u * f.v[i]; FD_KEEP( f2[i] ); } }
+  for( int i=0; i<10; i++ ) { f2[i] = f.v[i]; if( i & 1 ) f2[i] = fd_x2( f.v[i] ); }
 #define FE_MUL_COL( k, acc ) do {                                      \
     _Pragma("unroll") for( int i=0; i<10; i++ ) {                       \
       int j = (k) - i, wrap = j < 0;                                    \
@@ -225,7 +256,7 @@ FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
    multiples.  Largest operand 38f_odd < 2^31.9 (L input). */
 #define FE_SQR_OPERANDS( f )                                                  \
   u32 f2[10], fw[10];                                                         \
-  _Pragma("unroll") for( int i=0; i<9; i++ ) { f2[i] = 2u * f.v[i]; FD_KEEP( f2[i] ); } \
+  _Pragma("unroll") for( int i=0; i<9; i++ ) f2[i] = fd_x2( f.v[i] );          \
   f2[9] = 0u;                                                                 \
   _Pragma("unroll") for( int j=0; j<10; j++ ) {                               \
     fw[j] = 0u;                                                               \
@@ -283,7 +314,7 @@ FD_DEV void fe_sqr( fe & r, fe const & f ) {
 FD_DEV void fe_sqr_sub( fe & r, fe const & f, fe const & b ) {
   FE_SQR_OPERANDS( f );
 #if FD_CARRY_FOLD
-#define FE_SQR_SUB_COL( k, acc ) do { acc += (u64)( FE_4P(k) - b.v[k] ); FE_SQR_COL( k, acc ); } while(0)
+#define FE_SQR_SUB_COL( k, acc ) do { acc = fd_add32( acc, FE_4P(k) - b.v[k] ); FE_SQR_COL( k, acc ); } while(0)
   u64 ca = 0, cb = 0; fe o;
   FE_FOLD_CHAINS( o, FE_SQR_SUB_COL, ca, cb );
   r = o;
@@ -297,16 +328,63 @@ FD_DEV void fe_sqr_sub( fe & r, fe const & f, fe const & b ) {
   FD_SCHED_FENCE();
 }
 
-/* r = 2 f^2 + 4p - b (b L) -> T */
+/* r = 2 f^2 + 4p - b (b L) -> T.  FD_SQR2_PRE: f must be T (every caller
+   passes a point's Z straight from a multiply); the factor 2 rides in the
+   operands -- multiples f, 2f, 4f (limbs 1, 3), 38f (even j >= 6) and 76f
+   (odd j >= 5), all < 2^31.3 for T limbs -- so each column accumulates into
+   the carry chain directly instead of a separate sum doubled into it
+   (v_lshl_add_u64 per column).  Column sums stay < 2^62. */
+#ifndef FD_SQR2_PRE
+#define FD_SQR2_PRE 1
+#endif
+#define FE_SQR2_OPERANDS( f )                                                 \
+  u32 g2[10], g4[4], gw[10];                                                  \
+  _Pragma("unroll") for( int i=0; i<10; i++ ) g2[i] = fd_x2( f.v[i] );        \
+  g4[0] = g4[2] = 0u; g4[1] = fd_x2( g2[1] ); g4[3] = fd_x2( g2[3] );         \
+  _Pragma("unroll") for( int j=0; j<10; j++ ) {                               \
+    gw[j] = 0u;                                                               \
+    if( j >= 5 ) { gw[j] = ( (j & 1) ? 76u : 38u ) * f.v[j]; FD_KEEP( gw[j] ); } \
+  }
+#define FE_SQR2_COL( k, acc ) do {                                            \
+    _Pragma("unroll") for( int i=0; i<10; i++ ) {                              \
+      _Pragma("unroll") for( int j=i; j<10; j++ ) {                            \
+        if( ( (i + j) % 10 ) != (k) ) continue;                                \
+        int odd2 = (i & 1) && (j & 1);                                         \
+        int pair = i < j;                                                      \
+        int wrap = i + j >= 10;                                                \
+        u32 a_, b_;                                                            \
+        if( !wrap ) {         /* 2c = 2, 4 or 8 */                             \
+          int c = 2 * (pair ? 2 : 1) * (odd2 ? 2 : 1);                         \
+          a_ = c==8 ? g4[i & 3] : g2[i];                                       \
+          b_ = c==2 ? f.v[j] : g2[j];                                          \
+        } else if( j & 1 ) {  /* b = 76 f_j: 2c/76 = 1 or 2 */                 \
+          a_ = ( pair && odd2 ) ? g2[i] : f.v[i];                              \
+          b_ = gw[j];                                                          \
+        } else {              /* b = 38 f_j: 2c/38 = 1 (i == j) or 2 */        \
+          a_ = pair ? g2[i] : f.v[i];                                          \
+          b_ = gw[j];                                                          \
+        }                                                                      \
+        acc = FD_COL_MAD( a_, b_, acc );                                       \
+      }                                                                        \
+    } } while(0)
+
 FD_DEV void fe_sqr2_sub( fe & r, fe const & f, fe const & b ) {
+#if FD_CARRY_FOLD && FD_SQR2_PRE
+  FE_SQR2_OPERANDS( f );
+#define FE_SQR2P_SUB_COL( k, acc ) do { acc = fd_add32( acc, FE_4P(k) - b.v[k] ); FE_SQR2_COL( k, acc ); } while(0)
+  u64 ca = 0, cb = 0; fe o;
+  FE_FOLD_CHAINS( o, FE_SQR2P_SUB_COL, ca, cb );
+  r = o;
+#undef FE_SQR2P_SUB_COL
+#elif FD_CARRY_FOLD
   FE_SQR_OPERANDS( f );
-#if FD_CARRY_FOLD
 #define FE_SQR2_SUB_COL( k, acc ) do { u64 h_ = 0; FE_SQR_COL( k, h_ ); acc = ( h_ << 1 ) + acc + (u64)( FE_4P(k) - b.v[k] ); } while(0)
   u64 ca = 0, cb = 0; fe o;
   FE_FOLD_CHAINS( o, FE_SQR2_SUB_COL, ca, cb );
   r = o;
 #undef FE_SQR2_SUB_COL
 #else
+  FE_SQR_OPERANDS( f );
   u64 h[10];
 #pragma unroll
   for( int k=0; k<10; k++ ) { u64 acc = 0; FE_SQR_COL( k, acc ); h[k] = ( acc << 1 ) + (u64)( FE_4P(k) - b.v[k] ); }
