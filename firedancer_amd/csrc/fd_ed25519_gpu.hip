@@ -77,10 +77,19 @@
    (fd_prep_kernel, R decoded up front): they cannot fill the GPU, so
    per-wave instruction streams, not total work, set their time. */
 #ifndef FD_SMALL_BATCH_MAX
-#define FD_SMALL_BATCH_MAX 32768UL
+#define FD_SMALL_BATCH_MAX 65536UL
+#endif
+/* fd_dsm_kernel without the carry fold (fd_gpu_f25519.h) for batches of at
+   most this many signatures: <= 2 waves per SIMD, where the per-wave chain
+   latency, not the instruction count, sets the time */
+#ifndef FD_NOFOLD_MAX
+#define FD_NOFOLD_MAX 131072UL
 #endif
 #ifndef FD_DSM4_MAX
-#define FD_DSM4_MAX 16384UL          /* latency path: four lanes per signature up to here, then two */
+#define FD_DSM4_MAX 16384UL          /* latency path: four lanes per signature up to here, */
+#endif
+#ifndef FD_DSM2_MAX
+#define FD_DSM2_MAX 32768UL          /* then two up to here, then one (fd_dsm_kernel, R compared at its end) */
 #endif
 #define FD_STAGE_CHUNK ( 1UL << 20 )   /* host-staged batches: bytes per memcpy / H2D step */
 #define FD_PIPE_SUB    ( 1UL << 17 )   /* host batches of >= 2 FD_PIPE_SUB txns: sub-batches overlap H2D and kernels */
@@ -164,6 +173,7 @@ fd_expand_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 *
 }
 
 /* [0..8](-A) in cached form from A's canonical affine coordinates */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void atab_build( uint4 * __restrict__ tab, u32 s, uint4 const * __restrict__ Axy ) {
   uint4 const * ap = Axy + (size_t)s*4;
   ge_p3 A;
@@ -171,19 +181,19 @@ FD_DEV void atab_build( uint4 * __restrict__ tab, u32 s, uint4 const * __restric
   fe_from_quads( A.Y, ap[2], ap[3] );
   A.Z = fe_one();
   fe_neg( A.X, A.X ); fe_wcarry( A.X, A.X );              /* -A */
-  fe_mul( A.T, A.X, A.Y );
+  fe_mul<FM>( A.T, A.X, A.Y );
   ge_cached c1, c;
   c.YpX = fe_one(); c.YmX = fe_one(); c.Z = fe_one(); c.T2d = fe_zero();
   atab_store( tab, s, 0, c );
-  ge_p3_to_cached( c1, A );
+  ge_p3_to_cached<FM>( c1, A );
   atab_store( tab, s, 1, c1 );
   ge_p3 cur = A;
 #pragma unroll 1
   for( int e=2; e<FD_ATAB_ENTRIES; e++ ) {
     ge_p1p1 tt;
-    ge_add_cached( tt, cur, c1 );
-    ge_p1p1_to_p3( cur, tt );
-    ge_p3_to_cached( c, cur );
+    ge_add_cached<FM>( tt, cur, c1 );
+    ge_p1p1_to_p3<FM>( cur, tt );
+    ge_p3_to_cached<FM>( c, cur );
     atab_store( tab, s, e, c );
   }
 }
@@ -202,6 +212,7 @@ FD_DEV int txn_desc_ok( fdgpu_txn_desc_t const & d ) {
    or its R (is_r 1).  Status byte rc | small_order<<2 (rc: 0 ok, 1 not
    a square, 2 x==0 with sign set), 0xff if the transaction is
    malformed; the canonical affine point goes to Axy / Rxy. */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void decode_one( unsigned char const * __restrict__ payload, fdgpu_txn_desc_t const * __restrict__ desc,
                         u32 const * __restrict__ map, u32 s, u32 is_r, unsigned char * __restrict__ pstat,
                         uint4 * __restrict__ Rxy, uint4 * __restrict__ Axy ) {
@@ -213,7 +224,7 @@ FD_DEV void decode_one( unsigned char const * __restrict__ payload, fdgpu_txn_de
   u32 w[8];
   fd_load_words<8>( w, base + ( is_r ? (u32)d.signature_off + 64u*j : (u32)d.acct_addr_off + 32u*j ) );
   ge_p3 P; int rc;
-  ge_decode1( P, rc, w );
+  ge_decode1<FM>( P, rc, w );
   int so = ge_affine_is_small_order( P );
   pstat[2u*s + is_r] = (unsigned char)( rc | (so << 2) );
   u32 x[8], y[8];
@@ -355,6 +366,7 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
    check S and hash -- so a batch that cannot fill the GPU pays the
    longest of them instead of their sum.  Every block has one role, so
    no wave diverges. */
+template<int FM>
 __global__ void __launch_bounds__( FD_WG )
 fd_prep_kernel( unsigned char const *    __restrict__ payload,
                 fdgpu_txn_desc_t const * __restrict__ desc,
@@ -374,10 +386,10 @@ fd_prep_kernel( unsigned char const *    __restrict__ payload,
   u32 s = b * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
   if( role < 2u ) {
-    decode_one( payload, desc, map, s, role, pstat, Rxy, Axy );
+    decode_one<FM>( payload, desc, map, s, role, pstat, Rxy, Axy );
     /* tab != NULL: the A lane goes on to the -A table (for every A that
        decoded; fd_dsm2_kernel applies the result-code procedure) */
-    if( tab && role==0u && ( pstat[2u*s] & 3u )==0u ) atab_build( tab, s, Axy );
+    if( tab && role==0u && ( pstat[2u*s] & 3u )==0u ) atab_build<FM>( tab, s, Axy );
   }
   else hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rxy, khash );
 }
@@ -424,6 +436,7 @@ __device__ unsigned long long fd_clk_buf[ FD_CLK_BLOCKS ][ 4 ];
 #ifndef FD_DSM_MINW
 #define FD_DSM_MINW 0
 #endif
+template<int FM>
 #if FD_DSM_MINW
 __global__ void __launch_bounds__( FD_WG, FD_DSM_MINW )
 #else
@@ -474,19 +487,19 @@ fd_dsm_kernel( u32                      nsig,
     ge_p1p1 t;
     if( w != 63 ) {
 #pragma unroll 1
-      for( int r=0; r<3; r++ ) { ge_dbl( t, P2 ); ge_p1p1_to_p2( P2, t ); }
-      ge_dbl( t, P2 ); ge_p1p1_to_p3( P, t );
+      for( int r=0; r<3; r++ ) { ge_dbl<FM>( t, P2 ); ge_p1p1_to_p2<FM>( P2, t ); }
+      ge_dbl<FM>( t, P2 ); ge_p1p1_to_p3<FM>( P, t );
     }
     {
 #if !FD_DSM_PREFETCH
       atab_fetch( raw, tab, s, da < 0 ? -da : da );
 #endif
       ge_cached q; atab_unpack( q, raw ); ge_cached_cneg( q, da < 0 );
-      ge_add_cached( t, P, q );
+      ge_add_cached<FM>( t, P, q );
     }
 #if FD_BWIN==8
     if( !(w & 1) ) {
-      ge_p1p1_to_p3( P, t );
+      ge_p1p1_to_p3<FM>( P, t );
       int db = digB[ (size_t)(w>>1)*n + s ];
       int e = db < 0 ? -db : db;
       uint4 const * bp = btab + e*6;
@@ -495,20 +508,20 @@ fd_dsm_kernel( u32                      nsig,
       fe_from_quads( bq.ymx,  bp[2], bp[3] );
       fe_from_quads( bq.xy2d, bp[4], bp[5] );
       ge_precomp_cneg( bq, db < 0 );
-      ge_add_precomp( t, P, bq );
+      ge_add_precomp<FM>( t, P, bq );
     }
 #else
     if( !(w & 3) ) {
-      ge_p1p1_to_p3( P, t );
+      ge_p1p1_to_p3<FM>( P, t );
       ge_precomp bq;
       fe_from_quads( bq.ypx,  braw[0], braw[1] );
       fe_from_quads( bq.ymx,  braw[2], braw[3] );
       fe_from_quads( bq.xy2d, braw[4], braw[5] );
       ge_precomp_cneg( bq, db < 0 );
-      ge_add_precomp( t, P, bq );
+      ge_add_precomp<FM>( t, P, bq );
     }
 #endif
-    ge_p1p1_to_p2( P2, t );
+    ge_p1p1_to_p2<FM>( P2, t );
     if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
   }
 
@@ -526,8 +539,8 @@ fd_dsm_kernel( u32                      nsig,
   fe x, y, u;
   fe_from_quads( x, rp[0], rp[1] );
   fe_from_quads( y, rp[2], rp[3] );
-  fe_mul( u, x, P2.Z ); int okx = fe_eq( u, P2.X );
-  fe_mul( u, y, P2.Z ); int oky = fe_eq( u, P2.Y );
+  fe_mul<FM>( u, x, P2.Z ); int okx = fe_eq( u, P2.X );
+  fe_mul<FM>( u, y, P2.Z ); int oky = fe_eq( u, P2.Y );
   code[s] = (okx & oky) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
@@ -637,24 +650,26 @@ FD_DEV void fe_csub4( fe & r, fe const & a ) {                /* r = 4p - a */
 
 /* M-step: from completed (E, F, G, H) on both lanes to lane 0 (m0, m1) =
    (X3, T3), lane 1 (m0, m1) = (Y3, Z3); E, F, G, H T or L */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void pair_mstep( fe & m0, fe & m1, int h, fe const & E, fe const & F, fe const & G, fe const & H ) {
   fe u, v0, v1;
   fe_sel( u,  h, G, E );
   fe_sel( v0, h, H, F );
   fe_sel( v1, h, F, H );
-  fe_mul( m0, u, v0 );
-  fe_mul( m1, u, v1 );
+  fe_mul<FM>( m0, u, v0 );
+  fe_mul<FM>( m1, u, v1 );
 }
 
 /* doubling of the point held as M-step output -> completed (E,F,G,H) on
    both lanes */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void pair_dbl( fe & E, fe & F, fe & G, fe & H, int h, fe const & m0, fe const & m1 ) {
   fe s, a1, q0, q1, p0, p1, XX, YY, SS, ZZ, t;
   fe_xchg( s, m0 );                                  /* lane 0: Y, lane 1: X */
   fe_add( t, m0, s );                                /* X + Y */
   fe_sel( a1, h, m1, t );                            /* lane 0: X+Y, lane 1: Z */
-  fe_sqr( q0, m0 );                                  /* lane 0: XX, lane 1: YY */
-  fe_sqr( q1, a1 );                                  /* lane 0: SS, lane 1: ZZ */
+  fe_sqr<FM>( q0, m0 );                                  /* lane 0: XX, lane 1: YY */
+  fe_sqr<FM>( q1, a1 );                                  /* lane 0: SS, lane 1: ZZ */
   fe_xchg( p0, q0 ); fe_xchg( p1, q1 );
   fe_sel( XX, h, p0, q0 ); fe_sel( YY, h, q0, p0 );
   fe_sel( SS, h, p1, q1 ); fe_sel( ZZ, h, q1, p1 );
@@ -667,6 +682,7 @@ FD_DEV void pair_dbl( fe & E, fe & F, fe & G, fe & H, int h, fe const & m0, fe c
 /* P + Q from the M-step output; each lane passes the two coordinates of Q
    it multiplies by (lane 0: Y2+X2 and 2dT2, lane 1: Y2-X2 and Z2), already
    conditionally negated -> completed (E,F,G,H) on both lanes */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void pair_add( fe & E, fe & F, fe & G, fe & H, int h, fe const & m0, fe const & m1,
                       fe const & q0, fe const & q1 ) {
   fe s, a, b, u, n0, n1, x0, x1, A, B, C, D;
@@ -674,8 +690,8 @@ FD_DEV void pair_add( fe & E, fe & F, fe & G, fe & H, int h, fe const & m0, fe c
   fe_add( a, m0, s );                                /* lane 0: X+Y          */
   fe_sub( b, m0, s );                                /* lane 1: Y-X          */
   fe_sel( u, h, b, a );
-  fe_mul( n0, u, q0 );                               /* lane 0: A, lane 1: B */
-  fe_mul( n1, m1, q1 );                              /* lane 0: C, lane 1: Z Z2 */
+  fe_mul<FM>( n0, u, q0 );                               /* lane 0: A, lane 1: B */
+  fe_mul<FM>( n1, m1, q1 );                              /* lane 0: C, lane 1: Z Z2 */
   fe_xchg( x0, n0 ); fe_xchg( x1, n1 );
   fe_sel( A, h, x0, n0 ); fe_sel( B, h, n0, x0 );
   fe_sel( C, h, x1, n1 ); fe_sel( D, h, n1, x1 );
@@ -686,6 +702,7 @@ FD_DEV void pair_add( fe & E, fe & F, fe & G, fe & H, int h, fe const & m0, fe c
   fe_sub4( F, D, C ); fe_wcarry( F, F );             /* F = D-C (T) */
 }
 
+template<int FM>
 __global__ void __launch_bounds__( FD_WG )
 fd_dsm2_kernel( u32                      nsig,
                 uint4 const * __restrict__ tab,
@@ -732,13 +749,13 @@ fd_dsm2_kernel( u32                      nsig,
     }
     if( w != 63 ) {
 #pragma unroll 1
-      for( int r=0; r<4; r++ ) { pair_dbl( E, F, G, H, h, m0, m1 ); pair_mstep( m0, m1, h, E, F, G, H ); }
+      for( int r=0; r<4; r++ ) { pair_dbl<FM>( E, F, G, H, h, m0, m1 ); pair_mstep<FM>( m0, m1, h, E, F, G, H ); }
     }
     fe_from_quads( q0, araw[0], araw[1] );
     fe_from_quads( q1, araw[2], araw[3] );
     { fe nq; fe_neg( nq, q1 ); fe_sel( q1, !h && da < 0, nq, q1 ); }
-    pair_add( E, F, G, H, h, m0, m1, q0, q1 );
-    pair_mstep( m0, m1, h, E, F, G, H );
+    pair_add<FM>( E, F, G, H, h, m0, m1, q0, q1 );
+    pair_mstep<FM>( m0, m1, h, E, F, G, H );
     if( !(w & 3) ) {
       fe_from_quads( q0, braw[0], braw[1] );
       if( h ) q1 = one;
@@ -746,8 +763,8 @@ fd_dsm2_kernel( u32                      nsig,
         fe_from_quads( q1, braw[2], braw[3] );
         fe nq; fe_neg( nq, q1 ); fe_sel( q1, db < 0, nq, q1 );
       }
-      pair_add( E, F, G, H, h, m0, m1, q0, q1 );
-      pair_mstep( m0, m1, h, E, F, G, H );
+      pair_add<FM>( E, F, G, H, h, m0, m1, q0, q1 );
+      pair_mstep<FM>( m0, m1, h, E, F, G, H );
     }
     if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
   }
@@ -757,7 +774,7 @@ fd_dsm2_kernel( u32                      nsig,
   fe_sel( z, h, m1, z );
   uint4 const * rp = Rxy + (size_t)s*4 + 2*h;
   fe_from_quads( r, rp[0], rp[1] );
-  fe_mul( u, r, z );
+  fe_mul<FM>( u, r, z );
   u32 ok = (u32)fe_eq( u, m0 );
   ok &= fd_pair_xchg( ok );
   if( !h ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
@@ -778,20 +795,22 @@ fd_dsm2_kernel( u32                      nsig,
    for 2.1x the total work of fd_dsm_kernel. */
 
 /* M-step: E, F, G, H (T or L) on all lanes -> coordinate q of the point */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void quad_mstep( fe & m, int q, fe const & E, fe const & F, fe const & G, fe const & H ) {
   fe u, v;
   fe_sel( u, q==0 || q==3, E, G );
   fe_sel( v, q & 1, H, F );
-  fe_mul( m, u, v );
+  fe_mul<FM>( m, u, v );
 }
 
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void quad_dbl( fe & E, fe & F, fe & G, fe & H, int q, fe const & m ) {
 #if FD_DSM4_FUSED
   fe y, a, sq, XX, YY, t, t2;
   fe_bcast1( y, m );
   fe_add_q0( t, m, y );                              /* X + Y */
   fe_sel( a, q==3, t, m );                           /* X, Y, Z, X+Y */
-  fe_sqr( sq, a );
+  fe_sqr<FM>( sq, a );
   fe_bcast0( XX, sq ); fe_bcast1( YY, sq );
   fe_add( H, YY, XX );                               /* H = YY+XX (L) */
   fe_sub( G, YY, XX );                               /* G = YY-XX (L) */
@@ -802,7 +821,7 @@ FD_DEV void quad_dbl( fe & E, fe & F, fe & G, fe & H, int q, fe const & m ) {
   fe_bcast0( x, m ); fe_bcast1( y, m );
   fe_add( t, x, y );
   fe_sel( a, q==3, t, m );                           /* X, Y, Z, X+Y */
-  fe_sqr( sq, a );
+  fe_sqr<FM>( sq, a );
   fe_bcast0( XX, sq ); fe_bcast1( YY, sq ); fe_bcast2( ZZ, sq ); fe_bcast3( SS, sq );
   fe_add( H, YY, XX );                               /* H = YY+XX (L) */
   fe_sub( G, YY, XX );                               /* G = YY-XX (L) */
@@ -813,6 +832,7 @@ FD_DEV void quad_dbl( fe & E, fe & F, fe & G, fe & H, int q, fe const & m ) {
 
 /* P + Q; lane q passes the coordinate of Q it multiplies by (Y2+X2,
    Y2-X2, 2dT2, Z2), already conditionally negated */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void quad_add( fe & E, fe & F, fe & G, fe & H, int q, fe const & m, fe const & c ) {
 #if FD_DSM4_FUSED
   fe x, w, a, b, u, n, B, C, D, D2, t;
@@ -821,7 +841,7 @@ FD_DEV void quad_add( fe & E, fe & F, fe & G, fe & H, int q, fe const & m, fe co
   fe_subc( t, x ); fe_sub_q1( b, m, t );             /* Y-(X-2p) = Y-X+2p */
   fe_sel( u, q==1, b, a );
   fe_sel( u, q>=2, w, u );
-  fe_mul( n, u, c );
+  fe_mul<FM>( n, u, c );
   fe_bcast1( B, n );
   fe_add_q0( H, n, B );                              /* H = A+B */
   fe_subc( t, B ); fe_sub_q0( E, n, t );             /* E = A-(B-2p) = A-B+2p */
@@ -835,7 +855,7 @@ FD_DEV void quad_add( fe & E, fe & F, fe & G, fe & H, int q, fe const & m, fe co
   fe_sub( b, y, x );
   fe_sel( u, q==1, b, a );
   fe_sel( u, q>=2, w, u );
-  fe_mul( n, u, c );
+  fe_mul<FM>( n, u, c );
   fe_bcast0( A, n ); fe_bcast1( B, n ); fe_bcast2( C, n ); fe_bcast3( D, n );
   fe_add( D, D, D );                                 /* D = 2 Z Z2 (L) */
   fe_sub( E, A, B );
@@ -845,6 +865,7 @@ FD_DEV void quad_add( fe & E, fe & F, fe & G, fe & H, int q, fe const & m, fe co
 #endif
 }
 
+template<int FM>
 __global__ void __launch_bounds__( FD_WG )
 fd_dsm4_kernel( u32                      nsig,
                 uint4 const * __restrict__ tab,
@@ -887,20 +908,20 @@ fd_dsm4_kernel( u32                      nsig,
     }
     if( w != 63 ) {
 #pragma unroll 1
-      for( int r=0; r<4; r++ ) { quad_dbl( E, F, G, H, q, m ); quad_mstep( m, q, E, F, G, H ); }
+      for( int r=0; r<4; r++ ) { quad_dbl<FM>( E, F, G, H, q, m ); quad_mstep<FM>( m, q, E, F, G, H ); }
     }
     fe_from_quads( c, araw[0], araw[1] );
     { fe nc; fe_neg( nc, c ); fe_sel( c, q==2 && da < 0, nc, c ); }
-    quad_add( E, F, G, H, q, m, c );
-    quad_mstep( m, q, E, F, G, H );
+    quad_add<FM>( E, F, G, H, q, m, c );
+    quad_mstep<FM>( m, q, E, F, G, H );
     if( !(w & 3) ) {
       if( q == 3 ) c = one;
       else {
         fe_from_quads( c, braw[0], braw[1] );
         fe nc; fe_neg( nc, c ); fe_sel( c, q==2 && db < 0, nc, c );
       }
-      quad_add( E, F, G, H, q, m, c );
-      quad_mstep( m, q, E, F, G, H );
+      quad_add<FM>( E, F, G, H, q, m, c );
+      quad_mstep<FM>( m, q, E, F, G, H );
     }
     if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
   }
@@ -909,7 +930,7 @@ fd_dsm4_kernel( u32                      nsig,
   fe_bcast2( z, m );
   uint4 const * rp = Rxy + (size_t)s*4 + 2*( q & 1 );
   fe_from_quads( r, rp[0], rp[1] );
-  fe_mul( u, r, z );
+  fe_mul<FM>( u, r, z );
   u32 ok = (u32)fe_eq( u, m );
   ok = fd_bcast0( ok ) & fd_bcast1( ok );
   if( !q ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
@@ -1306,6 +1327,7 @@ struct fdgpu_ed25519_ctx {
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
   int dsm_lanes;                 /* latency path: lanes per signature in the DSM, 0 = by batch size (env FDGPU_DSM_LANES) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
+  unsigned long nofold_max;      /* fd_dsm_kernel<0> (no carry fold) for batches of at most this many signatures */
   u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
   u32 *   d_O;                   /*             product of the block's other Z, planar [10][max_sig] */
   u32 *   d_blk;                 /*             per 256-signature block: product of Z, then its inverse */
@@ -1369,10 +1391,11 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     int defer = FD_DEFER_R && !small;
     if( small ) {
       /* lanes per signature in the DSM: 4 while a quad per signature still fits one wave per
-         SIMD (n <= 16K), else 2 */
-      lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM4_MAX ? 4 : 2 );
+         SIMD (n <= 16K), 2 while a pair does (n <= 32K), else 1 (configs[0]'s 64K: 0.88 ms
+         against 0.92 on the throughput path and 1.08 with two lanes, tools/configs0_ab.py) */
+      lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM4_MAX ? 4 : nsig <= FD_DSM2_MAX ? 2 : 1 );
       int d2 = lanes > 1;
-      hipLaunchKernelGGL( fd_prep_kernel, dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, (u32)sg,
+      hipLaunchKernelGGL( fd_prep_kernel<0>, dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, (u32)sg,
                           ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
                           d2 ? ctx->d_tab : (uint4 *)NULL, (uint4 const *)ctx->d_khash );
       if( !d2 )
@@ -1390,13 +1413,16 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     }
     if( ctx->timing ) hipEventRecord( ev[1], st );
     if( small && lanes==4 )
-      hipLaunchKernelGGL( fd_dsm4_kernel, dim3(4*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
+      hipLaunchKernelGGL( fd_dsm4_kernel<0>, dim3(4*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                           ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat );
     else if( small && lanes==2 )
-      hipLaunchKernelGGL( fd_dsm2_kernel, dim3(2*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
+      hipLaunchKernelGGL( fd_dsm2_kernel<0>, dim3(2*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                           ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat );
+    else if( nsig <= ctx->nofold_max )         /* <= 2 waves per SIMD: latency-bound, independent column chains */
+      hipLaunchKernelGGL( fd_dsm_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
+                          ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P, defer );
     else
-      hipLaunchKernelGGL( fd_dsm_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
+      hipLaunchKernelGGL( fd_dsm_kernel<1>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                           ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P, defer );
     if( ctx->timing ) hipEventRecord( ev[2], st );
     if( defer ) {
@@ -1463,7 +1489,9 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   { char const * e = getenv( "FDGPU_SMALL_BATCH_MAX" );   /* A/B knob: signatures at or below take the latency path */
     ctx->small_max = e ? strtoul( e, NULL, 0 ) : FD_SMALL_BATCH_MAX;
     char const * dl = getenv( "FDGPU_DSM_LANES" );
-    ctx->dsm_lanes = dl ? atoi( dl ) : 0; }
+    ctx->dsm_lanes = dl ? atoi( dl ) : 0;
+    char const * nf = getenv( "FDGPU_NOFOLD_MAX" );   /* A/B knob: fd_dsm_kernel<0> (no carry fold) up to here */
+    ctx->nofold_max = nf ? strtoul( nf, NULL, 0 ) : FD_NOFOLD_MAX; }
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;

@@ -25,41 +25,45 @@ FD_DEV void ge_p3_identity( ge_p3 & p ) { p.X = fe_zero(); p.Y = fe_one(); p.Z =
 
 /* The completed -> projective/extended conversions share the 19x
    multiples of the operand used twice (T, and Y for p3). */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void ge_p1p1_to_p2( ge_p2 & r, ge_p1p1 const & p ) {
   fe19 t19; fe_x19( t19, p.T );
-  fe_mul19( r.X, p.X, p.T, t19 ); fe_mul( r.Y, p.Y, p.Z ); fe_mul19( r.Z, p.Z, p.T, t19 );
+  fe_mul19<FM>( r.X, p.X, p.T, t19 ); fe_mul<FM>( r.Y, p.Y, p.Z ); fe_mul19<FM>( r.Z, p.Z, p.T, t19 );
 }
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void ge_p1p1_to_p3( ge_p3 & r, ge_p1p1 const & p ) {
   fe19 t19; fe_x19( t19, p.T );
-  fe_mul19( r.X, p.X, p.T, t19 ); fe_mul19( r.Z, p.Z, p.T, t19 );
+  fe_mul19<FM>( r.X, p.X, p.T, t19 ); fe_mul19<FM>( r.Z, p.Z, p.T, t19 );
   fe19 y19; fe_x19( y19, p.Y );
-  fe_mul19( r.Y, p.Z, p.Y, y19 ); fe_mul19( r.T, p.X, p.Y, y19 );
+  fe_mul19<FM>( r.Y, p.Z, p.Y, y19 ); fe_mul19<FM>( r.T, p.X, p.Y, y19 );
 }
 
 /* 2P for a=-1 twisted Edwards from (X:Y:Z) T -- eprint 2008/522 §4.4:
    4 squarings.  Out: X=E (T), Y=H (L), Z=G (L), T=F (T).  E = (X+Y)^2-H
    and F = 2Z^2-G are folded into their squarings' carry chains. */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void ge_dbl( ge_p1p1 & r, ge_p2 const & p ) {
   fe xx, yy, s;
-  fe_sqr( xx, p.X );                  /* XX (T)               */
-  fe_sqr( yy, p.Y );                  /* YY (T)               */
+  fe_sqr<FM>( xx, p.X );                  /* XX (T)               */
+  fe_sqr<FM>( yy, p.Y );                  /* YY (T)               */
   fe_add( r.Y, yy, xx );              /* H = YY+XX (L)        */
   fe_sub( r.Z, yy, xx );              /* G = YY-XX (L)        */
   fe_add( s, p.X, p.Y );              /* X+Y (L)              */
-  fe_sqr_sub( r.X, s, r.Y );          /* E = (X+Y)^2-H = 2XY  */
-  fe_sqr2_sub( r.T, p.Z, r.Z );       /* F = 2ZZ-G            */
+  fe_sqr_sub<FM>( r.X, s, r.Y );          /* E = (X+Y)^2-H = 2XY  */
+  fe_sqr2_sub<FM>( r.T, p.Z, r.Z );       /* F = 2ZZ-G            */
 }
 
 /* P + Q, P T, Q cached (already negated by the caller if needed)
    (eprint 2008/522 §4.2, 4 mul).  Out: X=E, Y=H, Z=G (L), T=F (T). */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void ge_add_cached( ge_p1p1 & r, ge_p3 const & p, ge_cached const & q ) {
   fe a, b, c, d;
   fe_add( a, p.Y, p.X );
   fe_sub( b, p.Y, p.X );
-  fe_mul( a, a, q.YpX );              /* A (T) */
-  fe_mul( b, b, q.YmX );              /* B (T) */
-  fe_mul( c, q.T2d, p.T );            /* C (T) */
-  fe_mul( d, p.Z, q.Z );
+  fe_mul<FM>( a, a, q.YpX );              /* A (T) */
+  fe_mul<FM>( b, b, q.YmX );              /* B (T) */
+  fe_mul<FM>( c, q.T2d, p.T );            /* C (T) */
+  fe_mul<FM>( d, p.Z, q.Z );
   fe_add( d, d, d );                  /* D = 2 Z1 Z2 (L) */
   fe_sub( r.X, a, b );                /* E (L) */
   fe_add( r.Y, a, b );                /* H (L) */
@@ -69,13 +73,14 @@ FD_DEV void ge_add_cached( ge_p1p1 & r, ge_p3 const & p, ge_cached const & q ) {
 }
 
 /* P + Q, Q affine precomputed (Z=1), already negated if needed (3 mul). */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void ge_add_precomp( ge_p1p1 & r, ge_p3 const & p, ge_precomp const & q ) {
   fe a, b, c, d;
   fe_add( a, p.Y, p.X );
   fe_sub( b, p.Y, p.X );
-  fe_mul( a, a, q.ypx );
-  fe_mul( b, b, q.ymx );
-  fe_mul( c, q.xy2d, p.T );
+  fe_mul<FM>( a, a, q.ypx );
+  fe_mul<FM>( b, b, q.ymx );
+  fe_mul<FM>( c, q.xy2d, p.T );
   fe_add( d, p.Z, p.Z );
   fe_sub( r.X, a, b );
   fe_add( r.Y, a, b );
@@ -103,22 +108,25 @@ FD_DEV void ge_precomp_cneg( ge_precomp & q, int neg ) {
 }
 
 /* p T */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void ge_p3_to_cached( ge_cached & r, ge_p3 const & p ) {
   fe_add( r.YpX, p.Y, p.X );
   fe_sub( r.YmX, p.Y, p.X );
   r.Z = p.Z;
   fe d2 = fe_d2();
-  fe_mul( r.T2d, p.T, d2 );
+  fe_mul<FM>( r.T2d, p.T, d2 );
 }
 
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void ge_p3_dbl( ge_p3 & r, ge_p3 const & p ) {
   ge_p2 q; q.X = p.X; q.Y = p.Y; q.Z = p.Z;
-  ge_p1p1 t; ge_dbl( t, q ); ge_p1p1_to_p3( r, t );
+  ge_p1p1 t; ge_dbl<FM>( t, q ); ge_p1p1_to_p3<FM>( r, t );
 }
 
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void ge_p3_add( ge_p3 & r, ge_p3 const & p, ge_p3 const & q ) {
-  ge_cached c; ge_p3_to_cached( c, q );
-  ge_p1p1 t; ge_add_cached( t, p, c ); ge_p1p1_to_p3( r, t );
+  ge_cached c; ge_p3_to_cached<FM>( c, q );
+  ge_p1p1 t; ge_add_cached<FM>( t, p, c ); ge_p1p1_to_p3<FM>( r, t );
 }
 
 /* canonicalise in place (pack + unpack): any value with limbs < 2^31 -> T canonical */
@@ -134,34 +142,36 @@ FD_DEV void fe_canon( fe & a ) { u32 w[8]; fe_pack( w, a ); fe_unpack( a, w ); }
    (the AVX-512 decode rejects this, avx512/fd_r43x6_ge.c:230-232; the
    portable decode negates 0 and accepts, fd_curve25519.c:41-43 -- the
    caller decides).  Outputs are canonical T with Z=1, T=xy. */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void fe_decode_uv( fe & u, fe & v, fe const & y ) {
   fe one = fe_one(), d = fe_d();
-  fe_sqr( u, y );
-  fe_mul( v, u, d );
+  fe_sqr<FM>( u, y );
+  fe_mul<FM>( v, u, d );
   fe_sub( u, u, one );           /* u = y^2-1 (L) */
   fe_add( v, v, one );           /* v = dy^2+1 (L) */
 }
 
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void ge_decode1( ge_p3 & P, int & rc, u32 const w[ 8 ] ) {
   fe y; fe_unpack( y, w );
   int sgn = (int)(w[7] >> 31);
   fe u, v, t, x;
-  fe_decode_uv( u, v, y );
-  fe_sqr( t, v );
-  fe_mul( t, t, v );             /* v^3 */
-  fe_sqr( t, t );
-  fe_mul( t, t, v );             /* v^7 */
-  fe_mul( t, u, t );             /* u v^7 */
-  fe_pow22523( x, t );
+  fe_decode_uv<FM>( u, v, y );
+  fe_sqr<FM>( t, v );
+  fe_mul<FM>( t, t, v );             /* v^3 */
+  fe_sqr<FM>( t, t );
+  fe_mul<FM>( t, t, v );             /* v^7 */
+  fe_mul<FM>( t, u, t );             /* u v^7 */
+  fe_pow22523<FM>( x, t );
   /* u, v and u v^3 are recomputed rather than held across the 265-op
      chain: +5 field ops, -30 VGPRs */
-  fe_decode_uv( u, v, y );
-  fe_sqr( t, v );
-  fe_mul( t, t, v );             /* v^3 */
-  fe_mul( t, u, t );             /* u v^3 */
-  fe_mul( x, x, t );
-  fe_sqr( t, x );
-  fe_mul( t, t, v );             /* v x^2 (T) */
+  fe_decode_uv<FM>( u, v, y );
+  fe_sqr<FM>( t, v );
+  fe_mul<FM>( t, t, v );             /* v^3 */
+  fe_mul<FM>( t, u, t );             /* u v^3 */
+  fe_mul<FM>( x, x, t );
+  fe_sqr<FM>( t, x );
+  fe_mul<FM>( t, t, v );             /* v x^2 (T) */
   u32 wt[8], wu[8], wn[8];
   fe n; fe_add( n, t, u );       /* v x^2 + u */
   fe_pack( wt, t ); fe_pack( wu, u ); fe_pack( wn, n );
@@ -170,7 +180,7 @@ FD_DEV void ge_decode1( ge_p3 & P, int & rc, u32 const w[ 8 ] ) {
   for( int k=0; k<8; k++ ) { ne |= wt[k] ^ wu[k]; nz |= wn[k]; }
   int ok = ne==0u, flip = nz==0u;
   fe i = fe_sqrtm1();
-  fe_mul( t, x, i );
+  fe_mul<FM>( t, x, i );
   fe_sel( x, !ok, t, x );
   u32 wx[8]; fe_pack( wx, x );
   u32 z = 0;
@@ -180,7 +190,7 @@ FD_DEV void ge_decode1( ge_p3 & P, int & rc, u32 const w[ 8 ] ) {
   fe_neg( t, x ); fe_canon( t );
   fe_sel( x, (int)(wx[0] & 1u) != sgn, t, x );
   rc = ( ok | flip ) ? ( ( z==0u && sgn ) ? 2 : 0 ) : 1;
-  P.X = x; P.Y = y; P.Z = fe_one(); fe_mul( P.T, x, y );
+  P.X = x; P.Y = y; P.Z = fe_one(); fe_mul<FM>( P.T, x, y );
 }
 
 /* fd_ed25519_affine_is_small_order (fd_curve25519.h:88-118): on a decoded

@@ -148,15 +148,22 @@ FD_DEV void fe_carry64( fe & r, u64 h[ 10 ] ) {
    and a mask but no 64-bit add (≈10 fewer VALU instructions per
    multiply).  The chains meet at limb 5 (carry out of 4) and limb 0
    (19 x carry out of 9), each a short second step.  Output T:
-   r5 and r0 are re-masked, r6 and r1 take carries < 2^12 and < 2^15. */
+   r5 and r0 are re-masked, r6 and r1 take carries < 2^12 and < 2^15.
+
+   The fold serialises each half's 50 multiplies through one accumulator:
+   the fewest instructions, for kernels with waves enough per SIMD to hide
+   the latency.  A kernel that runs one wave per SIMD (a batch of <= 64K
+   signatures) finishes sooner with ten independent column chains (F = 0:
+   more instructions, more VGPRs, 4x the ILP) -- profiles/r02/dsm_ab.  The
+   multiply family below is templated on F; FD_CARRY_FOLD is the default. */
 #ifndef FD_CARRY_FOLD
 #define FD_CARRY_FOLD 1
 #endif
-#if FD_CARRY_FOLD
-#define FD_COL_MAD fd_mad_a
-#else
-#define FD_COL_MAD fd_mad
-#endif
+template<int F> FD_DEV u64 fd_col_mad( u32 a, u32 b, u64 c ) {
+  if constexpr( F != 0 ) return fd_mad_a( a, b, c );
+  else                   return fd_mad( a, b, c );
+}
+#define FD_COL_MAD fd_col_mad<FM>
 #define FE_FOLD_CHAINS( r, COL, ca, cb ) do {                               \
     _Pragma("unroll") for( int s_=0; s_<5; s_++ ) {                          \
       COL( s_, ca );     r.v[s_]   = (u32)ca & FE_M(s_);   ca >>= FE_W(s_);  \
@@ -219,6 +226,7 @@ FD_DEV void fe_x19( fe19 & r, fe const & g ) {
    i+j == k (mod 10); weight 2 when i and j are both odd
    (ceil(25.5i)+ceil(25.5j) = ceil(25.5(i+j)) + 1), weight 19 when
    i+j >= 10 (2^255 = 19).  100 v_mad_u64_u32 + 5 doublings. */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void fe_mul19( fe & r, fe const & f, fe const & g, fe19 const & g19 ) {
   u32 f2[10];
 #pragma unroll
@@ -231,23 +239,24 @@ FD_DEV void fe_mul19( fe & r, fe const & f, fe const & g, fe19 const & g19 ) {
       u32 b_ = wrap ? g19.v[j] : g.v[j];                                \
       acc = FD_COL_MAD( a_, b_, acc );                                  \
     } } while(0)
-#if FD_CARRY_FOLD
-  u64 ca = 0, cb = 0; fe o;   /* o: r may alias f or g */
-  FE_FOLD_CHAINS( o, FE_MUL_COL, ca, cb );
-  r = o;
-#else
-  u64 h[10];
+  if constexpr( FM != 0 ) {
+    u64 ca = 0, cb = 0; fe o;   /* o: r may alias f or g */
+    FE_FOLD_CHAINS( o, FE_MUL_COL, ca, cb );
+    r = o;
+  } else {
+    u64 h[10];
 #pragma unroll
-  for( int k=0; k<10; k++ ) { u64 acc = 0; FE_MUL_COL( k, acc ); h[k] = acc; }
-  fe_carry64( r, h );
-#endif
+    for( int k=0; k<10; k++ ) { u64 acc = 0; FE_MUL_COL( k, acc ); h[k] = acc; }
+    fe_carry64( r, h );
+  }
 #undef FE_MUL_COL
   FD_SCHED_FENCE();
 }
 
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
   fe19 g19; fe_x19( g19, g );
-  fe_mul19( r, f, g, g19 );
+  fe_mul19<FM>( r, f, g, g19 );
 }
 
 /* r = f^2; f L -> r T.  55 products; coefficient c = (i<j ? 2 : 1) x
@@ -290,18 +299,19 @@ FD_DEV void fe_mul( fe & r, fe const & f, fe const & g ) {
    (i, j both odd ? 2 : 1) x (i+j >= 10 ? 19 : 1) is carried by the
    operands f, 2f (i<=8), 38f (odd j>=5) and 19f (even j>=6) -- 14
    multiples.  Largest operand 38f_odd < 2^31.9 (L input). */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void fe_sqr( fe & r, fe const & f ) {
   FE_SQR_OPERANDS( f );
-#if FD_CARRY_FOLD
-  u64 ca = 0, cb = 0; fe o;
-  FE_FOLD_CHAINS( o, FE_SQR_COL, ca, cb );
-  r = o;
-#else
-  u64 h[10];
+  if constexpr( FM != 0 ) {
+    u64 ca = 0, cb = 0; fe o;
+    FE_FOLD_CHAINS( o, FE_SQR_COL, ca, cb );
+    r = o;
+  } else {
+    u64 h[10];
 #pragma unroll
-  for( int k=0; k<10; k++ ) { u64 acc = 0; FE_SQR_COL( k, acc ); h[k] = acc; }
-  fe_carry64( r, h );
-#endif
+    for( int k=0; k<10; k++ ) { u64 acc = 0; FE_SQR_COL( k, acc ); h[k] = acc; }
+    fe_carry64( r, h );
+  }
   FD_SCHED_FENCE();
 }
 
@@ -311,20 +321,21 @@ FD_DEV void fe_sqr( fe & r, fe const & f ) {
 
 /* r = f^2 + 4p - b (b L) -> T: the subtraction rides on the squaring's
    carry chain instead of a separate biased sub + fe_wcarry */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void fe_sqr_sub( fe & r, fe const & f, fe const & b ) {
   FE_SQR_OPERANDS( f );
-#if FD_CARRY_FOLD
+  if constexpr( FM != 0 ) {
 #define FE_SQR_SUB_COL( k, acc ) do { acc = fd_add32( acc, FE_4P(k) - b.v[k] ); FE_SQR_COL( k, acc ); } while(0)
-  u64 ca = 0, cb = 0; fe o;
-  FE_FOLD_CHAINS( o, FE_SQR_SUB_COL, ca, cb );
-  r = o;
+    u64 ca = 0, cb = 0; fe o;
+    FE_FOLD_CHAINS( o, FE_SQR_SUB_COL, ca, cb );
+    r = o;
 #undef FE_SQR_SUB_COL
-#else
-  u64 h[10];
+  } else {
+    u64 h[10];
 #pragma unroll
-  for( int k=0; k<10; k++ ) { u64 acc = 0; FE_SQR_COL( k, acc ); h[k] = acc + (u64)( FE_4P(k) - b.v[k] ); }
-  fe_carry64( r, h );
-#endif
+    for( int k=0; k<10; k++ ) { u64 acc = (u64)( FE_4P(k) - b.v[k] ); FE_SQR_COL( k, acc ); h[k] = acc; }
+    fe_carry64( r, h );
+  }
   FD_SCHED_FENCE();
 }
 
@@ -368,36 +379,46 @@ FD_DEV void fe_sqr_sub( fe & r, fe const & f, fe const & b ) {
       }                                                                        \
     } } while(0)
 
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void fe_sqr2_sub( fe & r, fe const & f, fe const & b ) {
-#if FD_CARRY_FOLD && FD_SQR2_PRE
+#if FD_SQR2_PRE
   FE_SQR2_OPERANDS( f );
+  if constexpr( FM != 0 ) {
 #define FE_SQR2P_SUB_COL( k, acc ) do { acc = fd_add32( acc, FE_4P(k) - b.v[k] ); FE_SQR2_COL( k, acc ); } while(0)
-  u64 ca = 0, cb = 0; fe o;
-  FE_FOLD_CHAINS( o, FE_SQR2P_SUB_COL, ca, cb );
-  r = o;
+    u64 ca = 0, cb = 0; fe o;
+    FE_FOLD_CHAINS( o, FE_SQR2P_SUB_COL, ca, cb );
+    r = o;
 #undef FE_SQR2P_SUB_COL
-#elif FD_CARRY_FOLD
-  FE_SQR_OPERANDS( f );
-#define FE_SQR2_SUB_COL( k, acc ) do { u64 h_ = 0; FE_SQR_COL( k, h_ ); acc = ( h_ << 1 ) + acc + (u64)( FE_4P(k) - b.v[k] ); } while(0)
-  u64 ca = 0, cb = 0; fe o;
-  FE_FOLD_CHAINS( o, FE_SQR2_SUB_COL, ca, cb );
-  r = o;
-#undef FE_SQR2_SUB_COL
+  } else {
+    u64 h[10];
+#pragma unroll
+    for( int k=0; k<10; k++ ) { u64 acc = (u64)( FE_4P(k) - b.v[k] ); FE_SQR2_COL( k, acc ); h[k] = acc; }
+    fe_carry64( r, h );
+  }
 #else
   FE_SQR_OPERANDS( f );
-  u64 h[10];
+  if constexpr( FM != 0 ) {
+#define FE_SQR2_SUB_COL( k, acc ) do { u64 h_ = 0; FE_SQR_COL( k, h_ ); acc = ( h_ << 1 ) + acc + (u64)( FE_4P(k) - b.v[k] ); } while(0)
+    u64 ca = 0, cb = 0; fe o;
+    FE_FOLD_CHAINS( o, FE_SQR2_SUB_COL, ca, cb );
+    r = o;
+#undef FE_SQR2_SUB_COL
+  } else {
+    u64 h[10];
 #pragma unroll
-  for( int k=0; k<10; k++ ) { u64 acc = 0; FE_SQR_COL( k, acc ); h[k] = ( acc << 1 ) + (u64)( FE_4P(k) - b.v[k] ); }
-  fe_carry64( r, h );
+    for( int k=0; k<10; k++ ) { u64 acc = 0; FE_SQR_COL( k, acc ); h[k] = ( acc << 1 ) + (u64)( FE_4P(k) - b.v[k] ); }
+    fe_carry64( r, h );
+  }
 #endif
   FD_SCHED_FENCE();
 }
 
 /* r = a^(2^n) */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void fe_sqrn( fe & r, fe const & a, int n ) {
-  fe_sqr( r, a );
+  fe_sqr<FM>( r, a );
 #pragma unroll 1
-  for( int i=1; i<n; i++ ) fe_sqr( r, r );
+  for( int i=1; i<n; i++ ) fe_sqr<FM>( r, r );
 }
 
 /* ---- packed 8 x 32-bit form (canonical) ---------------------------------- */
@@ -473,49 +494,51 @@ FD_DEV void fe_sel( fe & r, int c, fe const & a, fe const & b ) { /* r = c ? a :
 
 /* r = a^(2^252-3): the addition chain of fd_f25519_pow22523
    (src/ballet/ed25519/fd_f25519.c:10-59). */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void fe_pow22523( fe & r, fe const & a ) {
   fe t0, t1, t2;
-  fe_sqr ( t0, a );
-  fe_sqrn( t1, t0, 2 );
-  fe_mul ( t1, a, t1 );
-  fe_mul ( t0, t0, t1 );
-  fe_sqr ( t0, t0 );
-  fe_mul ( t0, t1, t0 );
-  fe_sqrn( t1, t0, 5 );
-  fe_mul ( t0, t1, t0 );
-  fe_sqrn( t1, t0, 10 );
-  fe_mul ( t1, t1, t0 );
-  fe_sqrn( t2, t1, 20 );
-  fe_mul ( t1, t2, t1 );
-  fe_sqrn( t1, t1, 10 );
-  fe_mul ( t0, t1, t0 );
-  fe_sqrn( t1, t0, 50 );
-  fe_mul ( t1, t1, t0 );
-  fe_sqrn( t2, t1, 100 );
-  fe_mul ( t1, t2, t1 );
-  fe_sqrn( t1, t1, 50 );
-  fe_mul ( t0, t1, t0 );
-  fe_sqrn( t0, t0, 2 );
-  fe_mul ( r, t0, a );
+  fe_sqr<FM>( t0, a );
+  fe_sqrn<FM>( t1, t0, 2 );
+  fe_mul<FM>( t1, a, t1 );
+  fe_mul<FM>( t0, t0, t1 );
+  fe_sqr<FM>( t0, t0 );
+  fe_mul<FM>( t0, t1, t0 );
+  fe_sqrn<FM>( t1, t0, 5 );
+  fe_mul<FM>( t0, t1, t0 );
+  fe_sqrn<FM>( t1, t0, 10 );
+  fe_mul<FM>( t1, t1, t0 );
+  fe_sqrn<FM>( t2, t1, 20 );
+  fe_mul<FM>( t1, t2, t1 );
+  fe_sqrn<FM>( t1, t1, 10 );
+  fe_mul<FM>( t0, t1, t0 );
+  fe_sqrn<FM>( t1, t0, 50 );
+  fe_mul<FM>( t1, t1, t0 );
+  fe_sqrn<FM>( t2, t1, 100 );
+  fe_mul<FM>( t1, t2, t1 );
+  fe_sqrn<FM>( t1, t1, 50 );
+  fe_mul<FM>( t0, t1, t0 );
+  fe_sqrn<FM>( t0, t0, 2 );
+  fe_mul<FM>( r, t0, a );
 }
 
 /* r = a^(p-2) = a^-1: the addition chain of fd_f25519_inv
    (src/ballet/ed25519/fd_f25519.c:62-103).  Off the hot path. */
+template<int FM = FD_CARRY_FOLD>
 FD_DEV void fe_invert( fe & r, fe const & z ) {
   fe t0, t1, t2, t3;
-  fe_sqr ( t0, z );
-  fe_sqrn( t1, t0, 2 );
-  fe_mul ( t1, z, t1 );
-  fe_mul ( t0, t0, t1 );
-  fe_sqr ( t2, t0 );
-  fe_mul ( t1, t1, t2 );
-  fe_sqrn( t2, t1, 5 );   fe_mul( t1, t2, t1 );
-  fe_sqrn( t2, t1, 10 );  fe_mul( t2, t2, t1 );
-  fe_sqrn( t3, t2, 20 );  fe_mul( t2, t3, t2 );
-  fe_sqrn( t2, t2, 10 );  fe_mul( t1, t2, t1 );
-  fe_sqrn( t2, t1, 50 );  fe_mul( t2, t2, t1 );
-  fe_sqrn( t3, t2, 100 ); fe_mul( t2, t3, t2 );
-  fe_sqrn( t2, t2, 50 );  fe_mul( t1, t2, t1 );
-  fe_sqrn( t1, t1, 5 );
-  fe_mul ( r, t1, t0 );
+  fe_sqr<FM>( t0, z );
+  fe_sqrn<FM>( t1, t0, 2 );
+  fe_mul<FM>( t1, z, t1 );
+  fe_mul<FM>( t0, t0, t1 );
+  fe_sqr<FM>( t2, t0 );
+  fe_mul<FM>( t1, t1, t2 );
+  fe_sqrn<FM>( t2, t1, 5 );   fe_mul<FM>( t1, t2, t1 );
+  fe_sqrn<FM>( t2, t1, 10 );  fe_mul<FM>( t2, t2, t1 );
+  fe_sqrn<FM>( t3, t2, 20 );  fe_mul<FM>( t2, t3, t2 );
+  fe_sqrn<FM>( t2, t2, 10 );  fe_mul<FM>( t1, t2, t1 );
+  fe_sqrn<FM>( t2, t1, 50 );  fe_mul<FM>( t2, t2, t1 );
+  fe_sqrn<FM>( t3, t2, 100 ); fe_mul<FM>( t2, t3, t2 );
+  fe_sqrn<FM>( t2, t2, 50 );  fe_mul<FM>( t1, t2, t1 );
+  fe_sqrn<FM>( t1, t1, 5 );
+  fe_mul<FM>( r, t1, t0 );
 }
