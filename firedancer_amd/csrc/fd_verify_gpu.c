@@ -1061,8 +1061,10 @@ static void * link_tile( void * _a ) {
   int idx = a->idx;
   ulong const T = (ulong)c->tiles, mask = h->depth - 1UL, n_frags = c->n_frags;
   /* out dcache: room for the frags a tile can have pending (its contexts' launched and filling
-     batches); large throughput batches get 3 batches' worth, small latency batches 6 */
-  ulong mult = c->batch_txn >= 32768UL ? 3UL : 6UL;
+     batches), 6 batch limits' worth: with 3 a 2-tile max-rate run blocked in drains (16.7M vs
+     18.8M sigs/s, profiles/r02/stream/sweep_depth.md) */
+  ulong mult = 6UL;
+  { char const * e = getenv( "FDGPU_LINK_OUT_MULT" ); if( e && atoi( e ) > 0 ) mult = (ulong)atoi( e ); }   /* A/B knob */
   fdgpu_vtile_t * vt = fdgpu_vtile_new( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                         ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
