@@ -2194,11 +2194,19 @@ static void region_del( void * h ) {
 /* device address of [p, p+sz) if it lies inside one registered region, else NULL */
 static unsigned char * region_dev( void const * p, unsigned long sz ) {
   unsigned char const * q = (unsigned char const *)p;
+  /* a tile's frags come from one region: try the thread's last hit first (re-validated like
+     any entry, so a removed or reused entry is never trusted) */
+  static thread_local int hint = 0;
   int n = g_region_cnt.load( std::memory_order_acquire );
+  if( hint < n ) {
+    unsigned long rs = g_regions[hint].sz.load( std::memory_order_acquire );
+    unsigned char const * h = g_regions[hint].h;
+    if( rs && q >= h && q + sz <= h + rs ) return g_regions[hint].d + ( q - h );
+  }
   for( int i=0; i<n; i++ ) {
     unsigned long rs = g_regions[i].sz.load( std::memory_order_acquire );
     unsigned char const * h = g_regions[i].h;
-    if( rs && q >= h && q + sz <= h + rs ) return g_regions[i].d + ( q - h );
+    if( rs && q >= h && q + sz <= h + rs ) { hint = i; return g_regions[i].d + ( q - h ); }
   }
   return NULL;
 }

@@ -1068,7 +1068,11 @@ static void * link_tile( void * _a ) {
   fdgpu_vtile_t * vt = fdgpu_vtile_new( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                         ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
-  if( c->zero_copy && fdgpu_vtile_set_in_link( vt, &l->mc ) ) { atomic_store( &h->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL; }
+  /* zero-copy intake; the overrun check only on an unreliable link (a reliable producer never
+     reuses a line before the tile's credit passes its oldest pending frag) */
+  if( c->zero_copy && fdgpu_vtile_set_in_link( vt, c->reliable ? NULL : &l->mc ) ) {
+    atomic_store( &h->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL;
+  }
   atomic_fetch_add( &h->tiles_ready, 1UL );    /* the producer starts once every tile has its GPU context */
   while( !atomic_load_explicit( &h->go, memory_order_acquire ) ) if( atomic_load( &h->fail ) ) { fdgpu_vtile_delete( vt ); return NULL; }
   ulong dcap = 4096UL;
