@@ -145,7 +145,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
     base = dict(batch_txn=args.stream_max_batch if leg != "paced" else args.stream_batch,
                 max_inflight=args.stream_inflight if leg != "paced" else args.stream_lat_inflight,
                 zero_copy=not args.stream_copy, gpus=procs,
-                mcache_depth=args.stream_depth if leg != "paced" else 1 << 18)
+                mcache_depth=args.stream_depth * procs if leg != "paced" else 1 << 18)   # the window scales with the tiles
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -198,7 +198,12 @@ def stream_child_main(args) -> None:
     payload = desc = None
     if proc == 0:
         from firedancer_amd import synth
-        payload, desc, _, _ = synth.make_batch(args.txns, synth.LARGE_NOOP, seed=args.stream_seed,
+        # distinct payloads: every tile's share must exceed its HA dedup depth (1 << 16), or each
+        # payload's second round through the link would be dropped as a duplicate (correct dedup,
+        # but then the legs would verify-and-drop instead of verify-and-publish)
+        tiles = max(args.stream_tiles, args.stream_lat_tiles) * procs
+        n_pay = max(args.txns, 2 * tiles * (1 << 16))
+        payload, desc, _, _ = synth.make_batch(n_pay, synth.LARGE_NOOP, seed=args.stream_seed,
                                                threads=min(16, os.cpu_count() or 1))
     for leg in STREAM_LEGS:
         path = f"/dev/shm/fdgpu_link_{args.stream_token}_{leg}" if procs > 1 else None
