@@ -574,7 +574,7 @@ def main():
             "kernel_ms": {"prep": ms_prep, "dsm": ms_dsm, "reduce": ms_red},
             "roofline": {"bound": "valu", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GMAC/s",
                          "frac": achieved / peak if peak > 0 else None, "traffic": traffic,
-                         "kernel": "fd_dsm_kernel",
+                         "kernel": "fd_dsm_kernel<1>",   # rocprof name of the 1M launch (carry-fold instantiation)
                          "work_per_sig": f"{DSM_MAC} v_mad_u64_u32 (1008 S + 1341 M of the reference wNAF DSM, "
                                          f"S=44 M=72 MAC)",
                          "peak_source": "fdgpu_mad_peak_per_s: measured v_mad_u64_u32 throughput, this device (max of 3)",
