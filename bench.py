@@ -224,7 +224,7 @@ def stream_child_main(args) -> None:
             else:
                 out[leg] = _leg_summary(st, cfg)
         else:
-            link = vtile.Link(path, create=False, timeout_s=600.0 if leg == "cal" else 300.0)
+            link = vtile.Link(path, create=False, timeout_s=180.0 if leg == "cal" else 120.0)   # bounded if process 0 failed
             try:
                 rc = link.run(proc, dev, False)
             finally:

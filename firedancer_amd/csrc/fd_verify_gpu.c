@@ -904,8 +904,8 @@ static void * link_producer( void * _l ) {
   ulong t_wait0 = now_ns();
   while( atomic_load( &h->tiles_ready ) < T ) {   /* every tile has its GPU context */
     if( atomic_load( &h->fail ) ) return NULL;
-    if( now_ns() - t_wait0 > 300000000000UL ) {
-      fprintf( stderr, "fdgpu_link: producer waited 300 s for %lu tiles (%lu ready)\n", T, atomic_load( &h->tiles_ready ) );
+    if( now_ns() - t_wait0 > 120000000000UL ) {
+      fprintf( stderr, "fdgpu_link: producer waited 120 s for %lu tiles (%lu ready)\n", T, atomic_load( &h->tiles_ready ) );
       atomic_store( &h->fail, 6 ); return NULL;
     }
   }
