@@ -1074,7 +1074,16 @@ static void * link_tile( void * _a ) {
     atomic_store( &h->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL;
   }
   atomic_fetch_add( &h->tiles_ready, 1UL );    /* the producer starts once every tile has its GPU context */
-  while( !atomic_load_explicit( &h->go, memory_order_acquire ) ) if( atomic_load( &h->fail ) ) { fdgpu_vtile_delete( vt ); return NULL; }
+  {
+    ulong t_go = now_ns();                       /* bounded: the producer's process may have died */
+    while( !atomic_load_explicit( &h->go, memory_order_acquire ) ) {
+      if( atomic_load( &h->fail ) ) { fdgpu_vtile_delete( vt ); return NULL; }
+      if( now_ns() - t_go > 180000000000UL ) {
+        fprintf( stderr, "fdgpu_link: tile %d waited 180 s for the producer\n", idx );
+        atomic_store( &h->fail, 8 ); fdgpu_vtile_delete( vt ); return NULL;
+      }
+    }
+  }
   ulong dcap = 4096UL;
   fdgpu_vtile_done_t * done = (fdgpu_vtile_done_t *)malloc( dcap * sizeof(fdgpu_vtile_done_t) );
   ulong * lh = (ulong *)calloc( LH_N, sizeof(ulong) ), lmax = 0UL, t_last = 0UL;
