@@ -145,6 +145,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
     base = dict(batch_txn=args.stream_max_batch if leg != "paced" else args.stream_batch,
                 max_inflight=args.stream_inflight if leg != "paced" else args.stream_lat_inflight,
                 zero_copy=not args.stream_copy, gpus=procs,
+                producers=args.stream_producers * procs,   # the reference's QUIC tiles: producer q in process q % G
                 mcache_depth=args.stream_depth * procs if leg != "paced" else 1 << 18)   # the window scales with the tiles
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
@@ -226,7 +227,7 @@ def stream_child_main(args) -> None:
         else:
             link = vtile.Link(path, create=False, timeout_s=180.0 if leg == "cal" else 120.0)   # bounded if process 0 failed
             try:
-                rc = link.run(proc, dev, False)
+                rc = link.run(proc, dev, True)          # its producers: q % G == proc
             finally:
                 link.close()
             if rc:
@@ -244,7 +245,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-max-batch", str(args.stream_max_batch),
            "--stream-rate", str(args.stream_rate), "--stream-lat-tiles", str(args.stream_lat_tiles),
            "--stream-inflight", str(args.stream_inflight), "--stream-depth", str(args.stream_depth),
-           "--stream-lat-inflight", str(args.stream_lat_inflight)]
+           "--stream-lat-inflight", str(args.stream_lat_inflight), "--stream-producers", str(args.stream_producers)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -283,6 +284,8 @@ def main():
                     help="batches a tile's engine context keeps launched before housekeeping launches its filling "
                          "one (a full batch launches regardless); 2: 17.5M vs 16.8M sigs/s at 1 on 2 tiles "
                          "(profiles/r02/stream/sweep_depth.md)")
+    ap.add_argument("--stream-producers", type=int, default=1,
+                    help="producer links (the reference's QUIC tiles) per GPU; every tile reads every link")
     ap.add_argument("--stream-lat-inflight", type=int, default=1,
                     help="--stream-inflight of the paced leg (1: few, larger batches; 2 gave p50/p99 0.82/1.53 ms "
                          "against 0.72/1.02 ms at 1, with 277-txn mean batches)")
@@ -483,14 +486,16 @@ def main():
                 mx, pc, ur = legs["max"], legs["paced"], legs["unrel"]
                 ok_s = (mx["metrics"][:4] == [0, 0, 0, 0] and mx["published"] == mx["frags"] and mx["lost"] == 0
                         and pc["metrics"][:4] == [0, 0, 0, 0])
-                stream = {"workload": "BASELINE configs[4]: 1232-byte txns, one producer mcache/dcache link -> "
-                                      "T verify tiles (seq % T round robin, tile i -> GPU i % G; device fd_txn_parse "
-                                      "+ verify, in-order after_frag, dedup tcache) -> out dcache",
+                stream = {"workload": "BASELINE configs[4]: 1232-byte txns, Q producer mcache links over one in dcache "
+                                      "-> T verify tiles reading every link (seq % T round robin per link, tile i -> "
+                                      "GPU i % G; device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> "
+                                      "out dcache",
                           "sigs_per_s": mx["sigs_per_s"], "per_gpu_sigs_per_s": mx["sigs_per_s"] / world,
                           "n_gpus": world, "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_max_batch,
                           "batch_paced": args.stream_batch,
                           "max_inflight": args.stream_inflight, "max_inflight_paced": args.stream_lat_inflight,
-                          "link_depth": args.stream_depth,
+                          "link_depth": args.stream_depth * world,
+                          "producers": args.stream_producers * world,
                           "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
                           "process": "one tile process per GPU without a torch GPU context (as a C verify tile); "
                                      "link in /dev/shm when G > 1",

@@ -305,7 +305,9 @@ struct fdgpu_vtile {
   /* zero-copy intake (fdgpu_vtile_set_in_link): frags stay in the in
      dcache, the GPU gathers them; in_mc (optional) for the overrun check */
   int                   zc;
-  fdgpu_mcache_t const * in_mc;
+  fdgpu_mcache_t const * in_mc;          /* (the single-link form: in_mcs[0]) */
+  fdgpu_mcache_t const * in_mcs[ FDGPU_VTILE_IN_MAX ];
+  int                   n_in;
   ulong                 overruns;
   /* poll scratch */
   ulong                 batch;
@@ -471,8 +473,16 @@ fdgpu_vtile_gpu_metrics( fdgpu_vtile_t const * vt, fdgpu_vtile_gpu_metrics_t * o
 
 int
 fdgpu_vtile_set_in_link( fdgpu_vtile_t * vt, fdgpu_mcache_t const * in_mc ) {
+  return fdgpu_vtile_set_in_links( vt, &in_mc, 1 );
+}
+
+int
+fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_mc, int n ) {
   if( vt->pend_tail != vt->pend_head ) return -1;       /* switch only while idle */
-  vt->zc = 1; vt->in_mc = in_mc;
+  if( n < 1 || n > FDGPU_VTILE_IN_MAX ) return -1;
+  vt->zc = 1; vt->n_in = n; vt->in_mc = NULL;
+  for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) vt->in_mcs[i] = i < n ? in_mc[i] : NULL;
+  for( int i=0; i<n; i++ ) if( in_mc[i] ) vt->in_mc = in_mc[i];   /* any overrun check at all */
   return 0;
 }
 
@@ -568,8 +578,9 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
        If the producer has since reused the frag's mcache line, its dcache
        bytes may have been overwritten before that read: drop it, as the
        stem loop drops a frag overrun during its copy. */
+    fdgpu_mcache_t const * mc = vt->in_mcs[ FDGPU_VTILE_SEQ_LINK( p->seq ) & ( FDGPU_VTILE_IN_MAX - 1 ) ];
     fdgpu_frag_meta_t m;
-    if( fdgpu_mcache_poll( vt->in_mc, p->seq, &m ) != 0 ) { vt->overruns++; return FDGPU_VTILE_OVERRUN; }
+    if( mc && fdgpu_mcache_poll( mc, FDGPU_VTILE_SEQ_SEQ( p->seq ), &m ) != 0 ) { vt->overruns++; return FDGPU_VTILE_OVERRUN; }
   }
   fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( vt->dcache + p->chunk * FDGPU_CHUNK_SZ );
   if( !vt->zc ) txnm->txn_t_sz = (unsigned short)fp;
@@ -660,8 +671,11 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
          few completions ahead */
       if( i + 8UL < k ) {
         if( vt->gpu_tag ) tc_prefetch( vt->tcache, vt->p_dtag[ i + 8UL ], 8UL );
-        if( vt->in_mc ) __builtin_prefetch( &vt->in_mc->line[ vt->pend[ ( vt->pend_head + 8UL ) % vt->pend_cap ].seq
-                                                               & ( vt->in_mc->depth - 1UL ) ] );
+        if( vt->in_mc ) {
+          ulong s8 = vt->pend[ ( vt->pend_head + 8UL ) % vt->pend_cap ].seq;
+          fdgpu_mcache_t const * mc = vt->in_mcs[ FDGPU_VTILE_SEQ_LINK( s8 ) & ( FDGPU_VTILE_IN_MAX - 1 ) ];
+          if( mc ) __builtin_prefetch( &mc->line[ FDGPU_VTILE_SEQ_SEQ( s8 ) & ( mc->depth - 1UL ) ] );
+        }
       }
       if( !vt->zc && vt->pend_head + 4UL < vt->pend_tail ) {   /* host-copied records: the header line */
         uchar * r = vt->dcache + vt->pend[ ( vt->pend_head + 4UL ) % vt->pend_cap ].chunk * FDGPU_CHUNK_SZ;
@@ -679,24 +693,26 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
   return n;
 }
 
-/* ---- the configs[4] stream: one producer link, T verify tiles ----------
-   The reference wires the verify stage as one QUIC out link read by every
-   verify tile: tile i takes the frags with seq % T == i (before_frag,
-   fd_verify_tile.c:47-48) over an UNRELIABLE, overrunnable in link
-   (topology.c:167-170).  Here the link -- mcache, in dcache prefilled with
-   one fd_txn_m_t record per distinct payload (what QUIC reassembly leaves),
-   the per-tile fseqs and the per-tile results -- is one memory region: a
-   shared file (/dev/shm) when the tiles live in several processes (one per
-   GPU; tile i drives GPU i % G, so process g runs the tiles i % G == g), or
-   private memory for a single process.  The producer (a thread of the
-   creating process) stands in for the QUIC tiles: the timed loop only
-   publishes metadata, frag seq pointing at payload seq % n_payload.
-   Reliable links (credit based: the producer stays depth/2 ahead of the
-   slowest tile) lose nothing; unreliable ones never wait and a tile that
-   falls a lap behind is overrun: it resumes at the seq it found
-   (fd_stem.c:590-596, 676-688) and the frags it skipped are counted. */
+/* ---- the configs[4] stream: Q producer links, T verify tiles -----------
+   The reference wires the verify stage as one out link per QUIC tile, each
+   read by every verify tile: tile i takes the frags with seq % T == i of
+   every link (before_frag, fd_verify_tile.c:47-48; topology.c:167-169) over
+   UNRELIABLE, overrunnable links.  Here the links -- Q mcaches, one in
+   dcache prefilled with one fd_txn_m_t record per distinct payload (what
+   QUIC reassembly leaves; producer q's frag s points at payload
+   (s Q + q) % n_payload), the per-link per-tile fseqs and the per-tile
+   results -- are one memory region: a shared file (/dev/shm) when the tiles
+   live in several processes (one per GPU; tile i drives GPU i % G, so
+   process g runs the tiles i % G == g and the producers q % G == g), or
+   private memory for a single process.  The producers (threads) stand in
+   for the QUIC tiles: their timed loops only publish metadata.  Reliable
+   links (credit based: a producer stays depth/2 ahead of the slowest tile
+   on its link) lose nothing; unreliable ones never wait and a tile that
+   falls a lap behind on a link is overrun: it resumes at the seq it found
+   (fd_stem.c:590-596, 676-688) and the frags it skipped are counted.  A
+   frag's seq as the tile hands it on carries its link (FDGPU_VTILE_SEQ). */
 
-#define LINK_MAGIC    0xfd6e11c0ffee0003UL
+#define LINK_MAGIC    0xfd6e11c0ffee0004UL
 #define LINK_TILE_MAX 64
 
 /* Latency histogram (per tile, merged at the end): log-linear buckets,
@@ -734,16 +750,18 @@ typedef struct {                 /* one tile's results, written once when it fin
   ulong device;
 } link_res_t;
 
+#define LINK_PROD_MAX FDGPU_VTILE_IN_MAX
+
 typedef struct {
   _Atomic ulong magic;           /* set last by the creator (release) */
   ulong         total_sz;
-  fdgpu_stream_cfg_t cfg;
+  fdgpu_stream_cfg_t cfg;        /* (cfg.producers normalised to 1..LINK_PROD_MAX) */
   ulong         depth, n_payload, in_bytes;
-  ulong         off_mcache, off_dcache, off_chunk, off_sz, off_psig, off_res, off_hist;
+  ulong         off_mcache[ LINK_PROD_MAX ], off_dcache, off_chunk, off_sz, off_psig, off_res, off_hist;
   _Atomic ulong joined, tiles_ready, tiles_done, go, fail;
   ulong         t_start;
-  ulong         prod_end, prod_wait_ns;   /* producer: last publish, time waiting for credits */
-  struct { _Atomic ulong v; uchar pad[56]; } fseq[ LINK_TILE_MAX ];   /* next seq each tile has yet to consume */
+  ulong         prod_end[ LINK_PROD_MAX ], prod_wait_ns[ LINK_PROD_MAX ];   /* per producer: last publish, credit waits */
+  struct { _Atomic ulong v; uchar pad[56]; } fseq[ LINK_PROD_MAX ][ LINK_TILE_MAX ];   /* per link: next seq each tile may lose */
 } link_hdr_t;
 
 struct fdgpu_link {
@@ -751,36 +769,42 @@ struct fdgpu_link {
   uchar *          base;
   ulong            sz;
   int              shared, registered;
-  mc_line_t *      line;
+  mc_line_t *      line[ LINK_PROD_MAX ];
   uchar *          dcache;
   unsigned *       chunk;
   unsigned short * psz;
   uchar *          psig;         /* signatures of each payload (the first byte), for the stream's sigs/s */
   link_res_t *     res;
   ulong *          hist;
-  fdgpu_mcache_t   mc;           /* local view of the shared lines (the tiles' in_mc) */
-  int              prod_cpu;     /* the producer thread's CPU (-1: not pinned) */
+  fdgpu_mcache_t   mc[ LINK_PROD_MAX ];   /* local views of the shared lines (the tiles' in links) */
 };
 
 static ulong al64( ulong x ) { return ( x + 63UL ) & ~63UL; }
 
 static void link_view( fdgpu_link_t * l ) {
   link_hdr_t * h = l->h;
-  l->line   = (mc_line_t *)( l->base + h->off_mcache );
+  for( int q=0; q<h->cfg.producers; q++ ) {
+    l->line[q] = (mc_line_t *)( l->base + h->off_mcache[q] );
+    l->mc[q].depth = h->depth; l->mc[q].line = l->line[q]; l->mc[q].own = 0;
+  }
   l->dcache = l->base + h->off_dcache;
   l->chunk  = (unsigned *)( l->base + h->off_chunk );
   l->psz    = (unsigned short *)( l->base + h->off_sz );
   l->psig   = l->base + h->off_psig;
   l->res    = (link_res_t *)( l->base + h->off_res );
   l->hist   = (ulong *)( l->base + h->off_hist );
-  l->mc.depth = h->depth; l->mc.line = l->line; l->mc.own = 0;
 }
+
+/* frags producer q of Q publishes: n / Q, the first n % Q producers one more */
+static ulong prod_frags( ulong n, ulong Q, ulong q ) { return n / Q + ( q < n % Q ? 1UL : 0UL ); }
 
 fdgpu_link_t *
 fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const * payload, unsigned const * off,
                 unsigned short const * sz, ulong n_payload, ulong mcache_depth ) {
   if( !cfg || cfg->tiles < 1 || cfg->tiles > LINK_TILE_MAX || cfg->gpus < 1 || cfg->gpus > cfg->tiles || !n_payload ||
-      !cfg->n_frags || !cfg->batch_txn || mcache_depth < 64 ) return NULL;
+      !cfg->n_frags || !cfg->batch_txn || mcache_depth < 64 || cfg->producers < 0 || cfg->producers > LINK_PROD_MAX )
+    return NULL;
+  ulong Q = cfg->producers ? (ulong)cfg->producers : 1UL;
   ulong depth = pow2_up( mcache_depth );
   ulong in_bytes = 0UL;
   for( ulong p=0; p<n_payload; p++ ) {
@@ -789,7 +813,8 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   }
   ulong T = (ulong)cfg->tiles;
   ulong o = al64( sizeof(link_hdr_t) );
-  ulong off_mcache = o;  o = al64( o + depth * sizeof(mc_line_t) );
+  ulong off_mcache[ LINK_PROD_MAX ] = { 0 };
+  for( ulong q=0; q<Q; q++ ) { off_mcache[q] = o;  o = al64( o + depth * sizeof(mc_line_t) ); }
   ulong off_chunk  = o;  o = al64( o + n_payload * sizeof(unsigned) );
   ulong off_sz     = o;  o = al64( o + n_payload * sizeof(unsigned short) );
   ulong off_psig   = o;  o = al64( o + n_payload );
@@ -816,11 +841,13 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   l->base = base; l->sz = total; l->shared = shared; l->h = (link_hdr_t *)base;
   link_hdr_t * h = l->h;
   memset( (void *)h, 0, sizeof(link_hdr_t) );
-  h->total_sz = total; h->cfg = *cfg; h->depth = depth; h->n_payload = n_payload; h->in_bytes = in_bytes;
-  h->off_mcache = off_mcache; h->off_dcache = off_dcache; h->off_chunk = off_chunk; h->off_sz = off_sz; h->off_psig = off_psig;
+  h->total_sz = total; h->cfg = *cfg; h->cfg.producers = (int)Q;
+  h->depth = depth; h->n_payload = n_payload; h->in_bytes = in_bytes;
+  for( ulong q=0; q<Q; q++ ) h->off_mcache[q] = off_mcache[q];
+  h->off_dcache = off_dcache; h->off_chunk = off_chunk; h->off_sz = off_sz; h->off_psig = off_psig;
   h->off_res = off_res; h->off_hist = off_hist;
   link_view( l );
-  mc_init_lines( l->line, depth, 0UL );
+  for( ulong q=0; q<Q; q++ ) mc_init_lines( l->line[q], depth, 0UL );
   memset( (void *)l->res, 0, T * sizeof(link_res_t) );
   memset( (void *)l->hist, 0, T * LH_N * sizeof(ulong) );
   for( ulong p=0, c=0; p<n_payload; p++ ) {
@@ -880,7 +907,7 @@ fdgpu_link_delete( fdgpu_link_t * l ) {
 }
 
 ulong fdgpu_link_joined( fdgpu_link_t const * l ) { return atomic_load( &l->h->joined ); }
-fdgpu_mcache_t * fdgpu_link_mcache( fdgpu_link_t * l ) { return &l->mc; }
+fdgpu_mcache_t * fdgpu_link_mcache( fdgpu_link_t * l ) { return &l->mc[0]; }
 unsigned char *  fdgpu_link_dcache( fdgpu_link_t * l ) { return l->dcache; }
 
 /* the reference's verify-tile -> GPU binding: tile i drives GPU i % G and
@@ -894,50 +921,66 @@ fdgpu_link_tiles_of( int tiles, int gpus, int proc, int * out ) {
 }
 void  fdgpu_link_cfg( fdgpu_link_t const * l, fdgpu_stream_cfg_t * cfg ) { *cfg = l->h->cfg; }
 
+typedef struct { fdgpu_link_t * l; int q, cpu; } link_prod_arg_t;
+
 static void link_pin( int cpu );
-static void * link_producer( void * _l ) {
-  fdgpu_link_t * l = (fdgpu_link_t *)_l;
-  link_pin( l->prod_cpu );
+/* producer q (one of the reference's QUIC tiles): publishes its frags on its
+   own mcache, seq 0 .. n_q-1, frag s pointing at payload (s Q + q) % n_payload */
+static void * link_producer( void * _a ) {
+  link_prod_arg_t * a = (link_prod_arg_t *)_a;
+  link_pin( a->cpu );
+  fdgpu_link_t * l = a->l;
   link_hdr_t * h = l->h;
   fdgpu_stream_cfg_t const * c = &h->cfg;
-  ulong T = (ulong)c->tiles, mask = h->depth - 1UL;
+  ulong const q = (ulong)a->q, Q = (ulong)c->producers;
+  ulong T = (ulong)c->tiles, mask = h->depth - 1UL, n_q = prod_frags( c->n_frags, Q, q );
   ulong t_wait0 = now_ns();
-  while( atomic_load( &h->tiles_ready ) < T ) {   /* every tile has its GPU context */
-    if( atomic_load( &h->fail ) ) return NULL;
-    if( now_ns() - t_wait0 > 120000000000UL ) {
-      fprintf( stderr, "fdgpu_link: producer waited 120 s for %lu tiles (%lu ready)\n", T, atomic_load( &h->tiles_ready ) );
-      atomic_store( &h->fail, 6 ); return NULL;
+  if( q == 0UL ) {
+    while( atomic_load( &h->tiles_ready ) < T ) {   /* every tile has its GPU context */
+      if( atomic_load( &h->fail ) ) return NULL;
+      if( now_ns() - t_wait0 > 120000000000UL ) {
+        fprintf( stderr, "fdgpu_link: producer waited 120 s for %lu tiles (%lu ready)\n", T, atomic_load( &h->tiles_ready ) );
+        atomic_store( &h->fail, 6 ); return NULL;
+      }
+    }
+    h->t_start = now_ns();
+    atomic_store_explicit( &h->go, 1UL, memory_order_release );
+  } else {
+    while( !atomic_load_explicit( &h->go, memory_order_acquire ) ) {
+      if( atomic_load( &h->fail ) ) return NULL;
+      if( now_ns() - t_wait0 > 180000000000UL ) { atomic_store( &h->fail, 6 ); return NULL; }
     }
   }
   ulong t0 = now_ns();
-  h->t_start = t0;
-  atomic_store_explicit( &h->go, 1UL, memory_order_release );
-  ulong cr_until = 0UL;                     /* may publish seq < cr_until */
-  for( ulong seq=0; seq<c->n_frags; seq++ ) {
+  double rate = c->rate_fps > 0. ? c->rate_fps / (double)Q : 0.;   /* the offered load, split over the producers */
+  mc_line_t * line = l->line[q];
+  ulong cr_until = 0UL, wait_ns = 0UL;      /* may publish seq < cr_until */
+  for( ulong seq=0; seq<n_q; seq++ ) {
     if( c->reliable ) {
       ulong t_wait = 0UL;
       if( seq >= cr_until ) t_wait = now_ns();
       while( seq >= cr_until ) {
         if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) return NULL;
         if( now_ns() - t_wait > 30000000000UL ) {                  /* watchdog: 30 s without credits */
-          fprintf( stderr, "fdgpu_link: producer starved of credits at seq %lu\n", seq );
+          fprintf( stderr, "fdgpu_link: producer %lu starved of credits at seq %lu\n", q, seq );
           atomic_store( &h->fail, 4 ); return NULL;
         }
         ulong lo = ~0UL;
-        for( ulong t=0; t<T; t++ ) { ulong f = atomic_load_explicit( &h->fseq[t].v, memory_order_acquire ); if( f < lo ) lo = f; }
+        for( ulong t=0; t<T; t++ ) { ulong f = atomic_load_explicit( &h->fseq[q][t].v, memory_order_acquire ); if( f < lo ) lo = f; }
         cr_until = lo + h->depth/2;
       }
-      if( t_wait ) h->prod_wait_ns += now_ns() - t_wait;
+      if( t_wait ) wait_ns += now_ns() - t_wait;
     }
-    if( c->rate_fps > 0. ) {
-      ulong due = t0 + (ulong)( (double)seq * 1e9 / c->rate_fps );
+    if( rate > 0. ) {
+      ulong due = t0 + (ulong)( (double)seq * 1e9 / rate );
       while( now_ns() < due ) ;
     }
-    ulong p = seq % h->n_payload;
+    ulong p = ( seq * Q + q ) % h->n_payload;
     unsigned ts = (unsigned)now_ns();
-    mc_publish( &l->line[ seq & mask ], seq, 0UL, l->chunk[p], (unsigned)( FDGPU_TXNM_HDR_SZ + l->psz[p] ), ts, ts );
+    mc_publish( &line[ seq & mask ], seq, 0UL, l->chunk[p], (unsigned)( FDGPU_TXNM_HDR_SZ + l->psz[p] ), ts, ts );
   }
-  h->prod_end = now_ns();
+  h->prod_wait_ns[q] = wait_ns;
+  h->prod_end[q] = now_ns();
   return NULL;
 }
 
@@ -1018,14 +1061,24 @@ static void link_pin( int cpu ) {
 
 typedef struct { fdgpu_link_t * l; int idx, device, cpu; } link_tile_arg_t;
 
-/* credit a tile returns to the producer: every seq below it may be
+/* per-link state of a tile */
+typedef struct {
+  ulong seq;                     /* next seq of the link this tile has not consumed (own or not) */
+  ulong n;                       /* frags the link's producer publishes */
+  ulong credited;                /* last credit returned */
+  ulong app, fin;                /* own frags handed to during_frag / returned by after_frags */
+  ulong done_next;               /* 1 + the seq of the last frag of this link returned by after_frags */
+} link_in_t;
+
+/* credit a tile returns to producer q: every seq below it may be
    overwritten.  With zero-copy intake a frag's bytes must survive until
-   the GPU has read them, so the credit stops at the oldest frag still
-   pending in the tile. */
-static void link_credit( link_hdr_t * h, int idx, fdgpu_vtile_t const * vt, ulong seq ) {
-  ulong c = seq;
-  if( h->cfg.zero_copy ) { ulong o = fdgpu_vtile_oldest_pending_seq( vt ); if( o < c ) c = o; }
-  atomic_store_explicit( &h->fseq[idx].v, c, memory_order_release );
+   the GPU has read them, so while frags of the link are pending the credit
+   stops at the first seq after the link's last completed frag (its frags
+   complete in seq order, so that is at or below its oldest pending one). */
+static void link_credit( link_hdr_t * h, int q, int idx, link_in_t const * in ) {
+  ulong c = in->seq;
+  if( h->cfg.zero_copy && in->app != in->fin && in->done_next < c ) c = in->done_next;
+  atomic_store_explicit( &h->fseq[q][idx].v, c, memory_order_release );
 }
 
 /* own frags (q % T == idx) in [a, b) */
@@ -1038,16 +1091,19 @@ static ulong own_in( ulong a, ulong b, ulong T, ulong idx ) {
 
 static void
 link_account( fdgpu_link_t * l, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs, ulong * lh, ulong * lmax,
-              ulong * t_last ) {
+              ulong * t_last, link_in_t * in ) {
   /* bench accounting only (not after_frag): the signature count comes from
      the link's per-payload table, not from the (cold) record in the out dcache */
-  ulong t = now_ns(), np = l->h->n_payload;
+  ulong t = now_ns(), np = l->h->n_payload, Q = (ulong)l->h->cfg.producers;
   for( ulong i=0; i<n; i++ ) {
     ulong lat = t - d[i].tsorig;
     lh[ lh_idx( lat ) ]++;
     if( lat > *lmax ) *lmax = lat;
+    int q = FDGPU_VTILE_SEQ_LINK( d[i].seq ) & ( LINK_PROD_MAX - 1 );
+    ulong s = FDGPU_VTILE_SEQ_SEQ( d[i].seq );
+    in[q].fin++; in[q].done_next = s + 1UL;
     if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL )
-      *sigs += l->psig[ d[i].seq % np ];
+      *sigs += l->psig[ ( s * Q + (ulong)q ) % np ];
   }
   if( n ) *t_last = t;
 }
@@ -1059,7 +1115,7 @@ static void * link_tile( void * _a ) {
   link_hdr_t * h = l->h;
   fdgpu_stream_cfg_t const * c = &h->cfg;
   int idx = a->idx;
-  ulong const T = (ulong)c->tiles, mask = h->depth - 1UL, n_frags = c->n_frags;
+  ulong const T = (ulong)c->tiles, mask = h->depth - 1UL, Q = (ulong)c->producers;
   /* out dcache: room for the frags a tile can have pending (its contexts' launched and filling
      batches), 6 batch limits' worth: with 3 a 2-tile max-rate run blocked in drains (16.7M vs
      18.8M sigs/s, profiles/r02/stream/sweep_depth.md) */
@@ -1068,12 +1124,14 @@ static void * link_tile( void * _a ) {
   fdgpu_vtile_t * vt = fdgpu_vtile_new( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                         ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
-  /* zero-copy intake; the overrun check only on an unreliable link (a reliable producer never
-     reuses a line before the tile's credit passes its oldest pending frag) */
-  if( c->zero_copy && fdgpu_vtile_set_in_link( vt, c->reliable ? NULL : &l->mc ) ) {
-    atomic_store( &h->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL;
+  /* zero-copy intake from every producer's link; the overrun check only on unreliable links (a
+     reliable producer never reuses a line before the tile's credit passes its pending frags) */
+  if( c->zero_copy ) {
+    fdgpu_mcache_t const * mcs[ LINK_PROD_MAX ];
+    for( ulong q=0; q<Q; q++ ) mcs[q] = c->reliable ? NULL : &l->mc[q];
+    if( fdgpu_vtile_set_in_links( vt, mcs, (int)Q ) ) { atomic_store( &h->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL; }
   }
-  atomic_fetch_add( &h->tiles_ready, 1UL );    /* the producer starts once every tile has its GPU context */
+  atomic_fetch_add( &h->tiles_ready, 1UL );    /* the producers start once every tile has its GPU context */
   {
     ulong t_go = now_ns();                       /* bounded: the producer's process may have died */
     while( !atomic_load_explicit( &h->go, memory_order_acquire ) ) {
@@ -1087,10 +1145,12 @@ static void * link_tile( void * _a ) {
   ulong dcap = 4096UL;
   fdgpu_vtile_done_t * done = (fdgpu_vtile_done_t *)malloc( dcap * sizeof(fdgpu_vtile_done_t) );
   ulong * lh = (ulong *)calloc( LH_N, sizeof(ulong) ), lmax = 0UL, t_last = 0UL;
-  ulong sigs = 0UL, got = 0UL, lost = 0UL;
-  ulong mine = own_in( 0UL, n_frags, T, (ulong)idx );
-  ulong seq = 0UL, credited = 0UL;
-  ulong last_seq = ~0UL, last_got = ~0UL, t_prog = now_ns();
+  ulong sigs = 0UL, got = 0UL, lost = 0UL, mine = 0UL;
+  link_in_t in[ LINK_PROD_MAX ];
+  memset( in, 0, sizeof(in) );
+  for( ulong q=0; q<Q; q++ ) { in[q].n = prod_frags( c->n_frags, Q, q ); mine += own_in( 0UL, in[q].n, T, (ulong)idx ); }
+  ulong last_prog = ~0UL, t_prog = now_ns(), q0 = 0UL;
+  ulong per_link = Q > 1UL ? ( 64UL / Q > 8UL ? 64UL / Q : 8UL ) : 64UL;   /* own frags per link per pass */
   ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, ns_idle = 0UL, t_begin = now_ns();
   /* FDGPU_LINK_PROF=1: rdtsc section profile (mcache poll, during_frag, prefetch + credit, drain
      after_frags, housekeep after_frags, link_account, credit after a drain, housekeep) */
@@ -1102,66 +1162,79 @@ static void * link_tile( void * _a ) {
   while( got + lost < mine ) {
     if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
     ulong t0 = now_ns();
-    if( seq != last_seq || got != last_got ) { last_seq = seq; last_got = got; t_prog = t0; }
+    ulong prog = got;
+    for( ulong q=0; q<Q; q++ ) prog += in[q].seq;
+    if( prog != last_prog ) { last_prog = prog; t_prog = t0; }
     else if( t0 - t_prog > 30000000000UL ) {                      /* watchdog: 30 s without progress */
       ulong filling = 0, inflight = 0;
       fdgpu_vtile_pipeline_state( vt, &filling, &inflight );
-      fprintf( stderr, "fdgpu_link: tile %d stalled: seq %lu got %lu lost %lu / %lu pending %lu filling %lu inflight %lu\n",
-               idx, seq, got, lost, mine, fdgpu_vtile_pending( vt ), filling, inflight );
+      fprintf( stderr, "fdgpu_link: tile %d stalled: seq[0] %lu got %lu lost %lu / %lu pending %lu filling %lu inflight %lu\n",
+               idx, in[0].seq, got, lost, mine, fdgpu_vtile_pending( vt ), filling, inflight );
       atomic_store( &h->fail, 5 ); break;
     }
-    /* intake: up to 64 own frags per pass.  The stem loop reads every seq's
-       line and before_frag drops seq % T != idx; with the link's single
-       in-order producer a published line of seq implies every earlier seq
-       is published, so the tile reads only its own lines (the same frags,
-       without T-1 cross-core line transfers per own frag) */
-    int drain = 0;
-    ulong seq_pass0 = seq;
-    for( int k=0; k<64 && seq < n_frags; k++ ) {
-      ulong own = seq + ( ( (ulong)idx + T - seq % T ) % T );      /* next seq with seq % T == idx */
-      if( own >= n_frags ) { seq = n_frags; break; }
-      mc_line_t const * ln = &l->line[ own & mask ];
-      fdgpu_frag_meta_t m; ulong found;
-      PROF_T0();
-      int r = mc_poll( ln, own, &m, &found );
-      if( r > 0 ) break;                                            /* not yet published */
-      PROF_ADD( 0 );
-      if( r < 0 ) {
-        if( c->reliable ) { atomic_store( &h->fail, 3 ); break; }
-        lost += own_in( own, found, T, (ulong)idx ); seq = found;    /* overrun while polling / reading: resume there */
-        continue;
-      }
-      int rc = fdgpu_vtile_during_frag( vt, l->dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, own,
-                                        ts_decomp( m.tsorig, t0 ) );   /* the pass's start is "now" to 2^31 ns */
-      PROF_ADD( 1 );
-      if( rc == -2 ) { drain = 1; seq = own; break; }               /* staging full: drain, retry this seq */
-      if( rc ) { fprintf( stderr, "fdgpu_link: tile %d during_frag %d\n", idx, rc ); atomic_store( &h->fail, 2 ); break; }
-      /* this tile's next frag is usually published already: start its cold lines */
-      if( own + T < n_frags ) {
-        mc_line_t const * nl = &l->line[ ( own + T ) & mask ];
-        __builtin_prefetch( nl );
-        if( atomic_load_explicit( (_Atomic ulong *)&nl->seq, memory_order_relaxed ) == own + T ) {
-          uchar const * pf = l->dcache + (ulong)nl->chunk * FDGPU_CHUNK_SZ;
-          __builtin_prefetch( pf ); __builtin_prefetch( pf + 64 );
+    /* intake: up to per_link own frags from each link per pass, links in
+       turn.  The stem loop reads every seq's line and before_frag drops
+       seq % T != idx; with each link's single in-order producer a published
+       line of seq implies every earlier seq is published, so the tile reads
+       only its own lines (the same frags, without T-1 cross-core line
+       transfers per own frag) */
+    int drain = 0, all_done = 1;
+    ulong took = 0UL;
+    for( ulong qi=0; qi<Q && !drain; qi++ ) {
+      ulong q = ( q0 + qi ) % Q;
+      link_in_t * li = &in[q];
+      mc_line_t const * line = l->line[q];
+      for( ulong k=0; k<per_link && li->seq < li->n; k++ ) {
+        ulong own = li->seq + ( ( (ulong)idx + T - li->seq % T ) % T );   /* next seq with seq % T == idx */
+        if( own >= li->n ) { li->seq = li->n; break; }
+        mc_line_t const * ln = &line[ own & mask ];
+        fdgpu_frag_meta_t m; ulong found;
+        PROF_T0();
+        int r = mc_poll( ln, own, &m, &found );
+        if( r > 0 ) break;                                          /* not yet published */
+        PROF_ADD( 0 );
+        if( r < 0 ) {
+          if( c->reliable ) { atomic_store( &h->fail, 3 ); drain = 1; break; }
+          lost += own_in( own, found < li->n ? found : li->n, T, (ulong)idx );   /* overrun: resume there */
+          li->seq = found < li->n ? found : li->n;
+          continue;
         }
+        int rc = fdgpu_vtile_during_frag( vt, l->dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, FDGPU_VTILE_SEQ( q, own ),
+                                          ts_decomp( m.tsorig, t0 ) );   /* the pass's start is "now" to 2^31 ns */
+        PROF_ADD( 1 );
+        if( rc == -2 ) { drain = 1; li->seq = own; break; }         /* staging full: drain, retry this seq */
+        if( rc ) { fprintf( stderr, "fdgpu_link: tile %d during_frag %d\n", idx, rc ); atomic_store( &h->fail, 2 ); drain = 1; break; }
+        li->app++; took++;
+        /* this tile's next frag of the link is usually published already: start its cold lines */
+        if( own + T < li->n ) {
+          mc_line_t const * nl = &line[ ( own + T ) & mask ];
+          __builtin_prefetch( nl );
+          if( atomic_load_explicit( (_Atomic ulong *)&nl->seq, memory_order_relaxed ) == own + T ) {
+            uchar const * pf = l->dcache + (ulong)nl->chunk * FDGPU_CHUNK_SZ;
+            __builtin_prefetch( pf ); __builtin_prefetch( pf + 64 );
+          }
+        }
+        li->seq = own + 1UL;
+        if( c->reliable && ( li->seq - li->credited >= 64UL || li->seq >= li->n ) ) {   /* batched credit return */
+          link_credit( h, (int)q, idx, li ); li->credited = li->seq;
+        }
+        PROF_ADD( 2 );
       }
-      seq = own + 1UL;
-      if( seq == n_frags ) seq = n_frags;
-      if( c->reliable && ( seq - credited >= 64UL || seq >= n_frags ) ) { link_credit( h, idx, vt, seq ); credited = seq; }   /* batched credit return */
-      PROF_ADD( 2 );
+      if( li->seq >= li->n && c->reliable && li->credited < li->n ) { link_credit( h, (int)q, idx, li ); li->credited = li->n; }
     }
-    if( seq >= n_frags && c->reliable && credited < n_frags ) { link_credit( h, idx, vt, n_frags ); credited = n_frags; }
+    q0++;
+    for( ulong q=0; q<Q; q++ ) if( in[q].seq < in[q].n ) all_done = 0;
     ulong t1 = now_ns();
     ns_in += t1 - t0;
-    if( seq == seq_pass0 && !drain ) ns_idle += t1 - t0;
+    if( !took && !drain ) ns_idle += t1 - t0;
     if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
-    if( drain || ( seq >= n_frags && fdgpu_vtile_pending( vt ) ) ) {
+    if( drain || ( all_done && fdgpu_vtile_pending( vt ) ) ) {
       PROF_T0();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
       PROF_ADD( 3 );
-      link_account( l, done, n, &sigs, lh, &lmax, &t_last ); got += n;
+      link_account( l, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
       PROF_ADD( 5 );
-      if( c->reliable && c->zero_copy ) link_credit( h, idx, vt, seq );
+      if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q] );
       PROF_ADD( 6 );
       ns_after += now_ns() - t1;
       continue;
@@ -1177,9 +1250,9 @@ static void * link_tile( void * _a ) {
       PROF_T0();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
       PROF_ADD( 4 );
-      link_account( l, done, n, &sigs, lh, &lmax, &t_last ); got += n;
+      link_account( l, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
       PROF_ADD( 5 );
-      if( c->reliable && c->zero_copy && n ) link_credit( h, idx, vt, seq );
+      if( c->reliable && c->zero_copy && n ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q] );
       PROF_ADD( 6 );
       ns_hk += t2 - t1; ns_after += now_ns() - t2;
     }
@@ -1203,6 +1276,8 @@ static void * link_tile( void * _a ) {
   return NULL;
 }
 
+/* Each process runs its tiles (i % G == proc) and, with run_producer, its
+   producers (q % G == proc). */
 int
 fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   link_hdr_t * h = l->h;
@@ -1212,15 +1287,17 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
     if( fdgpu_host_register( l->dcache, h->in_bytes + 4096UL ) ) { atomic_store( &h->fail, 7 ); return -3; }
     l->registered = 1;
   }
-  pthread_t prod, th[ LINK_TILE_MAX ];
+  pthread_t prod[ LINK_PROD_MAX ], th[ LINK_TILE_MAX ];
   link_tile_arg_t args[ LINK_TILE_MAX ];
-  int mine[ LINK_TILE_MAX ];
+  link_prod_arg_t pargs[ LINK_PROD_MAX ];
+  int mine[ LINK_TILE_MAX ], myq[ LINK_PROD_MAX ], np = 0;
   int nt = fdgpu_link_tiles_of( c->tiles, c->gpus, proc, mine );   /* tile i drives GPU i % G: this process's tiles */
-  int cpus[ LINK_TILE_MAX + 1 ], np = run_producer ? 1 : 0;
+  if( run_producer ) for( int q=0; q<c->producers; q++ ) if( q % c->gpus == proc ) myq[np++] = q;
+  int cpus[ LINK_TILE_MAX + LINK_PROD_MAX ];
   int ncpu = link_pick_cpus( device, proc, nt + np, cpus );
-  l->prod_cpu = run_producer && ncpu > 0 ? cpus[0] : -1;
   if( getenv( "FDGPU_LINK_VERBOSE" ) ) {
-    fprintf( stderr, "fdgpu_link: proc %d device %d numa %d cpus:", proc, device, fdgpu_device_numa_node( device ) );
+    fprintf( stderr, "fdgpu_link: proc %d device %d numa %d producers %d tiles %d cpus:", proc, device,
+             fdgpu_device_numa_node( device ), np, nt );
     for( int i=0; i<ncpu; i++ ) fprintf( stderr, " %d", cpus[i] );
     fprintf( stderr, "\n" );
   }
@@ -1229,8 +1306,11 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
     args[t].cpu = np + t < ncpu ? cpus[ np + t ] : -1;
     pthread_create( &th[t], NULL, link_tile, &args[t] );
   }
-  if( run_producer ) pthread_create( &prod, NULL, link_producer, l );
-  if( run_producer ) pthread_join( prod, NULL );
+  for( int i=0; i<np; i++ ) {
+    pargs[i].l = l; pargs[i].q = myq[i]; pargs[i].cpu = i < ncpu ? cpus[i] : -1;
+    pthread_create( &prod[i], NULL, link_producer, &pargs[i] );
+  }
+  for( int i=0; i<np; i++ ) pthread_join( prod[i], NULL );
   for( int t=0; t<nt; t++ ) pthread_join( th[t], NULL );
   int rc = (int)atomic_load( &h->fail );
   return rc ? -rc - 10 : 0;
@@ -1266,9 +1346,13 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     if( r->lmax > lmax ) lmax = r->lmax;
     for( ulong k=0UL; k<LH_N; k++ ) lh[k] += l->hist[ i*LH_N + k ];
   }
+  ulong prod_end = 0UL;
+  for( int q=0; q<c->producers; q++ ) {
+    if( h->prod_end[q] > prod_end ) prod_end = h->prod_end[q];
+    st->prod_wait_ns += h->prod_wait_ns[q];
+  }
   st->seconds = t_end > h->t_start ? (double)( t_end - h->t_start ) * 1e-9 : 0.;
-  st->prod_seconds = h->prod_end > h->t_start ? (double)( h->prod_end - h->t_start ) * 1e-9 : 0.;
-  st->prod_wait_ns = h->prod_wait_ns;
+  st->prod_seconds = prod_end > h->t_start ? (double)( prod_end - h->t_start ) * 1e-9 : 0.;
   st->frags = c->n_frags;
   st->published = st->metrics[4];
   st->frags_per_s = st->seconds > 0. ? (double)st->verdicts / st->seconds : 0.;
@@ -1283,7 +1367,7 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
   return 0;
 }
 
-/* private link, producer + every tile in this process on one device (G = 1) */
+/* private link, producers + every tile in this process on one device (G = 1) */
 int
 fdgpu_stream_run( int device, fdgpu_stream_cfg_t const * cfg, uchar const * payload, unsigned const * off,
                   unsigned short const * sz, ulong n_payload, ulong mcache_depth, fdgpu_stream_stats_t * st ) {
@@ -1304,6 +1388,6 @@ fdgpu_stream_bench( int device, uchar const * payload, unsigned const * off, uns
   fdgpu_stream_cfg_t c;
   memset( &c, 0, sizeof(c) );
   c.n_frags = n_frags; c.batch_txn = batch_txn; c.max_inflight = max_inflight ? max_inflight : 2UL; c.rate_fps = rate_fps;
-  c.tiles = tiles; c.gpus = 1; c.zero_copy = zero_copy; c.reliable = 1;
+  c.tiles = tiles; c.gpus = 1; c.zero_copy = zero_copy; c.reliable = 1; c.producers = 1;
   return fdgpu_stream_run( device, &c, payload, off, sz, n_payload, mcache_depth, st );
 }

@@ -21,7 +21,7 @@ EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_
            "fdgpu_mcache_new", "fdgpu_mcache_delete", "fdgpu_mcache_publish", "fdgpu_mcache_poll",
            "fdgpu_dcache_compact_next", "fdgpu_vtile_new", "fdgpu_vtile_delete", "fdgpu_vtile_out_dcache",
            "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_housekeep", "fdgpu_vtile_pipeline_state", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
-           "fdgpu_vtile_metrics", "fdgpu_vtile_set_in_link", "fdgpu_vtile_oldest_pending_seq", "fdgpu_vtile_overruns",
+           "fdgpu_vtile_metrics", "fdgpu_vtile_set_in_link", "fdgpu_vtile_set_in_links", "fdgpu_vtile_oldest_pending_seq", "fdgpu_vtile_overruns",
            "fdgpu_vtile_faulted", "fdgpu_vtile_recover", "fdgpu_vtile_debug_fault", "fdgpu_vtile_gpu_metrics",
            "fdgpu_link_new", "fdgpu_link_join", "fdgpu_link_delete", "fdgpu_link_joined", "fdgpu_link_cfg",
            "fdgpu_link_run", "fdgpu_link_tiles_of", "fdgpu_link_mcache", "fdgpu_link_dcache", "fdgpu_link_result",
@@ -58,7 +58,7 @@ class GpuMetrics(ctypes.Structure):
 class StreamCfg(ctypes.Structure):
     _fields_ = [("n_frags", ctypes.c_ulong), ("batch_txn", ctypes.c_ulong), ("max_inflight", ctypes.c_ulong),
                 ("rate_fps", ctypes.c_double), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int),
-                ("zero_copy", ctypes.c_int), ("reliable", ctypes.c_int)]
+                ("zero_copy", ctypes.c_int), ("reliable", ctypes.c_int), ("producers", ctypes.c_int)]
 
 
 class StreamStats(ctypes.Structure):
@@ -121,6 +121,7 @@ def load():
         L.fdgpu_vtile_pending.argtypes = [vp]
         L.fdgpu_vtile_metrics.argtypes = [vp, ctypes.POINTER(ctypes.c_ulong)]
         L.fdgpu_vtile_set_in_link.argtypes = [vp, vp]
+        L.fdgpu_vtile_set_in_links.argtypes = [vp, vp, ctypes.c_int]
         L.fdgpu_vtile_oldest_pending_seq.restype = ul
         L.fdgpu_vtile_oldest_pending_seq.argtypes = [vp]
         L.fdgpu_vtile_overruns.restype = ul
@@ -280,20 +281,20 @@ def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
     return list(out[:n])
 
 
-def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable) -> StreamCfg:
+def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers=1) -> StreamCfg:
     return StreamCfg(n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
-                     gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0)
+                     gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0, producers=producers)
 
 
 def stream_run(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,
                batch_txn: int = 4096, max_inflight: int = 1, mcache_depth: int = 1 << 16, rate_fps: float = 0.0,
-               device: int = 0, zero_copy: bool = True, reliable: bool = True) -> dict:
-    """One process: producer + `tiles` verify tiles on `device` over a private link (G = 1)."""
+               device: int = 0, zero_copy: bool = True, reliable: bool = True, producers: int = 1) -> dict:
+    """One process: `producers` producer links + `tiles` verify tiles on `device`, private memory (G = 1)."""
     L = load()
     payload = np.ascontiguousarray(payload, np.uint8)
     off = np.ascontiguousarray(off, np.uint32)
     sz = np.ascontiguousarray(sz, np.uint16)
-    cfg = _cfg(n_frags, tiles, 1, batch_txn, max_inflight, rate_fps, zero_copy, reliable)
+    cfg = _cfg(n_frags, tiles, 1, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers)
     st = StreamStats()
     rc = L.fdgpu_stream_run(device, ctypes.byref(cfg), payload.ctypes.data, off.ctypes.data, sz.ctypes.data, len(off),
                             mcache_depth, ctypes.byref(st))
@@ -307,14 +308,15 @@ class Link:
 
     def __init__(self, path: str | None, *, create: bool, payload=None, off=None, sz=None, n_frags: int = 0,
                  tiles: int = 1, gpus: int = 1, batch_txn: int = 8192, max_inflight: int = 1, rate_fps: float = 0.0,
-                 zero_copy: bool = True, reliable: bool = True, mcache_depth: int = 1 << 18, timeout_s: float = 300.0):
+                 zero_copy: bool = True, reliable: bool = True, mcache_depth: int = 1 << 18, timeout_s: float = 300.0,
+                 producers: int = 1):
         self.L = load()
         self.path = path
         if create:
             payload = np.ascontiguousarray(payload, np.uint8)
             off = np.ascontiguousarray(off, np.uint32)
             sz = np.ascontiguousarray(sz, np.uint16)
-            cfg = _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable)
+            cfg = _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers)
             self.p = self.L.fdgpu_link_new(path.encode() if path else None, ctypes.byref(cfg), payload.ctypes.data,
                                            off.ctypes.data, sz.ctypes.data, len(off), mcache_depth)
         else:

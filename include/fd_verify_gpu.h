@@ -173,6 +173,16 @@ int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, 
    fdgpu_vtile_oldest_pending_seq has passed it (credits).  Call while no
    frag is pending; 0 on success. */
 int             fdgpu_vtile_set_in_link( fdgpu_vtile_t * vt, fdgpu_mcache_t const * in_mc );
+/* The same for a tile that reads n in links (the reference's verify tile
+   reads every QUIC tile's link, topology.c:167-169): the seq a frag is
+   handed to during_frag with carries its link in bits 56..63
+   (FDGPU_VTILE_SEQ( link, seq )), and after_frag checks the frag against
+   in_mc[ link ] (entries may be NULL).  n <= FDGPU_VTILE_IN_MAX. */
+#define FDGPU_VTILE_IN_MAX   16
+#define FDGPU_VTILE_SEQ( link, seq )  ( ( (unsigned long)(link) << 56 ) | (unsigned long)(seq) )
+#define FDGPU_VTILE_SEQ_LINK( s )     ( (int)( (s) >> 56 ) )
+#define FDGPU_VTILE_SEQ_SEQ( s )      ( (s) & ( ( 1UL << 56 ) - 1UL ) )
+int             fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_mc, int n );
 /* seq of the oldest frag not yet returned by after_frags (~0UL if none) */
 unsigned long   fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt );
 /* frags dropped as FDGPU_VTILE_OVERRUN */
@@ -233,6 +243,9 @@ typedef struct fdgpu_stream_cfg {
   int           reliable;        /* 1: credit-based link (the producer waits for the slowest tile);
                                     0: unreliable, as the reference's quic_verify link (topology.c:167-170):
                                     the producer never waits, a lagging tile is overrun and skips frags */
+  int           producers;       /* Q producer links (the reference's QUIC tiles, 0 = 1): producer q publishes
+                                    about n_frags / Q frags on its own mcache, every tile reads every link with
+                                    seq % T == i on each (topology.c:167-169); producer q runs in process q % G */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
@@ -253,8 +266,8 @@ typedef struct fdgpu_stream_stats {
   unsigned long poll_ns, after_ns;   /* of tile_ns[1]: non-blocking completion polls; after_frag proper */
   unsigned long launch_ns;       /* host time inside batch launches, summed over tiles (part of tile_ns[0..2]) */
   unsigned long tile_idle_ns;    /* of tile_ns[0]: intake passes that found no frag published yet */
-  double        prod_seconds;    /* producer: first -> last publish */
-  unsigned long prod_wait_ns;    /* producer: time waiting for credits (reliable links) */
+  double        prod_seconds;    /* producers: first -> last publish */
+  unsigned long prod_wait_ns;    /* producers: time waiting for credits (reliable links), summed */
   unsigned long prof_ns[ 8 ];    /* env FDGPU_LINK_PROF=1, summed over tiles: mcache poll, during_frag, prefetch +
                                     credit, drain after_frags, housekeep after_frags, accounting, credit after
                                     after_frags, housekeep (launch decisions) */

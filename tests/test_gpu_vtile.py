@@ -324,22 +324,27 @@ def test_stream_bench_small(zero_copy):
     assert st["lat_p99_us"] > 0
 
 
-@pytest.mark.parametrize("tiles,reliable,zero_copy", [(3, True, True), (1, True, True), (2, True, False), (4, False, True)])
-def test_stream_run_link(tiles, reliable, zero_copy):
-    """The configs[4] link (fdgpu_stream_run): tile i takes seq % T == i, each tile polling its own
-    lines only.  Reliable: every frag gets exactly one verdict and the signature count is that of the
+@pytest.mark.parametrize("tiles,reliable,zero_copy,producers", [(3, True, True, 1), (1, True, True, 1), (2, True, False, 1),
+                                                           (4, False, True, 1), (3, True, True, 2), (2, False, True, 3)])
+def test_stream_run_link(tiles, reliable, zero_copy, producers):
+    """The configs[4] link (fdgpu_stream_run): Q producer links, every tile reads every link and takes
+    seq % T == i of each, polling its own lines only.  Reliable: every frag gets exactly one verdict and the signature count is that of the
     frags' payloads; unreliable: verdicts + frags lost to overruns = frags published."""
     from firedancer_amd import synth, vtile
     payload, desc, _, _ = synth.make_batch(3000, synth.MULTI, seed=21)
     n = 40000 + tiles                                   # not a multiple of T: ragged last round
     st = vtile.stream_run(payload, desc["payload_off"], desc["payload_sz"], n_frags=n, tiles=tiles, batch_txn=2048,
-                          mcache_depth=16384 if reliable else 4096, zero_copy=zero_copy, reliable=reliable)
+                          mcache_depth=16384 if reliable else 4096, zero_copy=zero_copy, reliable=reliable,
+                          producers=producers)
     assert st["frags"] == n
     assert st["verdicts"] + st["lost"] == n
     sig_cnt = np.array([payload[o] for o in desc["payload_off"]], np.uint64)
     if reliable:
         assert st["lost"] == 0 and st["verdicts"] == n and st["overruns"] == 0
-        assert st["sigs"] == int(sig_cnt[np.arange(n) % len(desc)].sum())
+        # producer q of Q publishes n_q frags, frag s -> payload (s Q + q) % n_payload
+        nq = [n // producers + (q < n % producers) for q in range(producers)]
+        idx = np.concatenate([(np.arange(nq[q]) * producers + q) % len(desc) for q in range(producers)])
+        assert st["sigs"] == int(sig_cnt[idx].sum())
         m = st["metrics"]
         assert m[0] == 0 and m[1] == 0 and sum(m) == n          # no parse / verify failures in valid txns
     else:

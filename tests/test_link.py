@@ -109,3 +109,21 @@ def test_link_rejects_bad_config():
                    n_frags=10, tiles=1, gpus=1)
     with pytest.raises(RuntimeError):
         vtile.Link(os.path.join(_shm_dir(), "fdgpu_link_absent"), create=False, timeout_s=0.05)
+
+
+def test_link_producers_config():
+    """Q producer links (the reference's QUIC tiles): the count travels in the shared configuration;
+    the default is one; more than FDGPU_VTILE_IN_MAX (16) is refused."""
+    payload, off, sz = _payloads()
+    link = vtile.Link(None, create=True, payload=payload, off=off, sz=sz, n_frags=100, tiles=4, gpus=2, producers=3)
+    try:
+        assert link.cfg()["producers"] == 3 and link.mcache()
+    finally:
+        link.close()
+    link = vtile.Link(None, create=True, payload=payload, off=off, sz=sz, n_frags=100, tiles=2, gpus=1)
+    try:
+        assert link.cfg()["producers"] == 1
+    finally:
+        link.close()
+    with pytest.raises(RuntimeError):
+        vtile.Link(None, create=True, payload=payload, off=off, sz=sz, n_frags=10, tiles=2, gpus=1, producers=17)
