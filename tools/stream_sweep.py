@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Sweep the configs[4] verify stage on one GPU (fdgpu_stream_run: one producer link, T verify tiles,
 tile i -> GPU 0): one JSON line per point.  Env: TILES, RATE (frags/s, 0 = max), REL (1 reliable /
-0 unreliable), SECONDS, BATCH, INFL, ZC, DEPTH (mcache lines), VARIANTS (comma list of env assignments applied per point,
+0 unreliable), SECONDS, BATCH, INFL, ZC, DEPTH (mcache lines), PROD (producer links), VARIANTS (comma list of env assignments applied per point,
 e.g. "FDGPU_VTILE_GPU_TAG=1,FDGPU_VTILE_GPU_TAG=0"), NPAY (distinct payloads)."""
 import json
 import os
@@ -39,7 +39,8 @@ for var in variants:
                 st = vtile.stream_run(payload, desc["payload_off"], desc["payload_sz"], n_frags=nf, tiles=tiles,
                                       batch_txn=int(os.environ.get("BATCH", 8192)),
                                       max_inflight=int(os.environ.get("INFL", 1)), mcache_depth=int(os.environ.get("DEPTH", 1 << 18)),
-                                      rate_fps=rate, zero_copy=bool(int(os.environ.get("ZC", 1))), reliable=bool(rel))
+                                      rate_fps=rate, zero_copy=bool(int(os.environ.get("ZC", 1))), reliable=bool(rel),
+                                      producers=int(os.environ.get("PROD", 1)))
                 n = max(st["verdicts"], 1)
                 print(json.dumps({"variant": var, "reliable": rel, "tiles": tiles, "rate": rate, "frags": st["frags"],
                                   "verdicts": st["verdicts"], "lost": st["lost"], "overruns": st["overruns"],
