@@ -183,7 +183,8 @@ int             fdgpu_vtile_set_in_link( fdgpu_vtile_t * vt, fdgpu_mcache_t cons
 #define FDGPU_VTILE_SEQ_LINK( s )     ( (int)( (s) >> 56 ) )
 #define FDGPU_VTILE_SEQ_SEQ( s )      ( (s) & ( ( 1UL << 56 ) - 1UL ) )
 int             fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_mc, int n );
-/* seq of the oldest frag not yet returned by after_frags (~0UL if none) */
+/* seq of the oldest frag not yet returned by after_frags, as handed to
+   during_frag (link bits included, FDGPU_VTILE_SEQ); ~0UL if none */
 unsigned long   fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt );
 /* frags dropped as FDGPU_VTILE_OVERRUN */
 unsigned long   fdgpu_vtile_overruns( fdgpu_vtile_t const * vt );
