@@ -146,7 +146,9 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 max_inflight=args.stream_inflight if leg != "paced" else args.stream_lat_inflight,
                 zero_copy=not args.stream_copy, gpus=procs,
                 producers=args.stream_producers * procs,   # the reference's QUIC tiles: producer q in process q % G
-                mcache_depth=args.stream_depth * procs if leg != "paced" else 1 << 18)   # the window scales with the tiles
+                # per link: its producer runs depth/2 ahead of the slowest tile; with one producer per GPU a
+                # link carries 1/G of the frags but is read by all 2G tiles -> twice the single-GPU depth
+                mcache_depth=args.stream_depth * min(procs, 2) if leg != "paced" else 1 << 18)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -494,7 +496,7 @@ def main():
                           "n_gpus": world, "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_max_batch,
                           "batch_paced": args.stream_batch,
                           "max_inflight": args.stream_inflight, "max_inflight_paced": args.stream_lat_inflight,
-                          "link_depth": args.stream_depth * world,
+                          "link_depth": args.stream_depth * min(world, 2),
                           "producers": args.stream_producers * world,
                           "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
                           "process": "one tile process per GPU without a torch GPU context (as a C verify tile); "
