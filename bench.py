@@ -139,7 +139,11 @@ STREAM_LEGS = ("cal", "max", "paced", "unrel")
 
 
 def _leg_cfg(args, leg, procs, cal_fps):
-    T, Tl = args.stream_tiles * procs, args.stream_lat_tiles * procs
+    # every tile and producer thread spins on its core: keep them within the host cores this job may
+    # use (affinity and cgroup quota), split over the GPUs' processes
+    budget = max(2, usable_cores()[0] // procs)
+    T = min(args.stream_tiles, max(1, budget - args.stream_producers)) * procs
+    Tl = min(args.stream_lat_tiles, max(1, budget - args.stream_producers)) * procs
     # the max-rate legs batch for throughput (a GPU batch under one wave per SIMD costs about one wave's
     # DSM chain, ~1 ms, whatever its size), the paced leg for latency
     base = dict(batch_txn=args.stream_max_batch if leg != "paced" else args.stream_batch,
@@ -493,7 +497,7 @@ def main():
                                       "GPU i % G; device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> "
                                       "out dcache",
                           "sigs_per_s": mx["sigs_per_s"], "per_gpu_sigs_per_s": mx["sigs_per_s"] / world,
-                          "n_gpus": world, "tiles_per_gpu": args.stream_tiles, "batch_max": args.stream_max_batch,
+                          "n_gpus": world, "tiles_per_gpu": mx["tiles"] // world, "batch_max": args.stream_max_batch,
                           "batch_paced": args.stream_batch,
                           "max_inflight": args.stream_inflight, "max_inflight_paced": args.stream_lat_inflight,
                           "link_depth": args.stream_depth * min(world, 2),
