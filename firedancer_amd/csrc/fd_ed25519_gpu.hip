@@ -92,6 +92,11 @@
 #define FD_DSM2_MAX 32768UL          /* then two up to here, then one (fd_dsm_kernel, R compared at its end) */
 #endif
 #define FD_STAGE_CHUNK ( 1UL << 20 )   /* host-staged batches: bytes per memcpy / H2D step */
+/* gathered batches: the fd_txn_t image of the last record may end this far past its record */
+#define FD_IMG_TAIL    1024UL
+#ifndef FD_GATHER_DMA
+#define FD_GATHER_DMA  0
+#endif
 #define FD_PIPE_SUB    ( 1UL << 17 )   /* host batches of >= 2 FD_PIPE_SUB txns: sub-batches overlap H2D and kernels */
 #define FD_PIPE_MAX    16UL
 #define FD_PEND_ASMALL 2           /* per-signature code in flight: A small order, R's decode picks ERR_SIG / ERR_PUBKEY */
@@ -1238,7 +1243,7 @@ fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__
   uint4 const * src = (uint4 const *)r.src;
   uint4 * a = (uint4 *)( arena + r.dst );
   uint4 * o = (uint4 *)( out + r.dst );
-  for( u32 i=threadIdx.x; i<(r.sz >> 4); i+=64u ) { uint4 v = src[i]; a[i] = v; o[i] = v; }
+  for( u32 i=threadIdx.x; i<(r.sz >> 4); i+=64u ) { uint4 v = src[i]; a[i] = v; if( out ) o[i] = v; }
 }
 
 /* Gathered raw batches: the fd_txn_t image of each parsed transaction
@@ -1345,6 +1350,8 @@ struct fdgpu_ed25519_ctx {
   int dedup;                     /* raw batches also return HA dedup tags (fdgpu_ed25519_set_dedup) */
   unsigned long dedup_seed;
   int rec_fp_off;                /* gathered records: offset of a u16 footprint field, -1 = none */
+  int gather_dma;                /* gathered batches: records and images return to the out region by one D2H copy
+                                    of the arena range instead of kernel stores over PCIe (env FDGPU_GATHER_DMA) */
   unsigned long n_batches, n_txns;                /* async batches launched, transactions in them */
   unsigned long launch_ns;                        /* host time inside slot_launch */
   unsigned long volatile * h_flag;                /* per slot: completion token written by fd_done_kernel (pinned) */
@@ -1454,7 +1461,7 @@ slot_bufs( fdgpu_ed25519_ctx_t * ctx, int i ) {
   HIPCHK( hipHostMalloc( (void**)&sl.h_desc, mt * sizeof(fdgpu_txn_desc_t), hipHostMallocDefault ), -1 );
   HIPCHK( hipHostMalloc( (void**)&sl.h_txn_out, mt, hipHostMallocDefault ), -1 );
   HIPCHK( hipHostMalloc( (void**)&sl.h_tags, mt * sizeof(unsigned long), hipHostMallocDefault ), -1 );
-  HIPCHK( hipMalloc( &sl.d_payload, mp + FD_ARENA_SLACK ), -1 );
+  HIPCHK( hipMalloc( &sl.d_payload, mp + FD_ARENA_SLACK + FD_IMG_TAIL ), -1 );   /* + the last gathered record's image */
   HIPCHK( hipMalloc( &sl.d_desc, mt * sizeof(fdgpu_txn_desc_t) ), -1 );
   HIPCHK( hipMalloc( &sl.d_txn_out, mt ), -1 );
   memset( sl.h_payload, 0, FD_ARENA_SLACK );
@@ -1505,6 +1512,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
      pipeline's other slots on first use (slot_bufs) */
   if( max_payload_bytes && slot_bufs( ctx, 0 ) ) return -1;
   ctx->cur = 0; ctx->rec_fp_off = -1;
+  { char const * g = getenv( "FDGPU_GATHER_DMA" ); ctx->gather_dma = g ? atoi( g ) != 0 : FD_GATHER_DMA; }
   HIPCHK( hipStreamSynchronize( ctx->stream ), -1 );
   return 0;
 }
@@ -2001,7 +2009,7 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
   } else if( sl.mode==3 ) {   /* gathered: the GPU reads each record from the caller's in region */
     HIPCHK( hipMemcpyAsync( sl.d_gat, sl.h_gat, sl.txn_cnt * sizeof(fd_gather), hipMemcpyHostToDevice, st ), -2 );
     hipLaunchKernelGGL( fd_gather_kernel, dim3( (unsigned)sl.txn_cnt ), dim3( 64 ), 0, st, sl.d_gat, sl.d_payload,
-                        sl.ref_dev + sl.ref_lo );
+                        ctx->gather_dma ? (unsigned char *)NULL : sl.ref_dev + sl.ref_lo );
     HIPCHK( hipGetLastError(), -2 );
   } else {
     memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
@@ -2017,8 +2025,11 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
   if( sl.mode==3 ) {   /* gathered: the images go into the out region, only the footprints come back */
     hipLaunchKernelGGL( fd_img_scatter_kernel, dim3( (unsigned)sl.txn_cnt ), dim3( 64 ), 0, st,
                         (fdgpu_txn_raw_t const *)sl.d_desc, sl.d_img, (u32)FDGPU_TXN_IMG_STRIDE, sl.d_fp,
-                        sl.ref_dev + sl.ref_lo, ctx->rec_fp_off );
+                        ctx->gather_dma ? sl.d_payload : sl.ref_dev + sl.ref_lo, ctx->rec_fp_off );
     HIPCHK( hipGetLastError(), -2 );
+    if( ctx->gather_dma )   /* records + images, as laid out in the out region, in one DMA */
+      HIPCHK( hipMemcpyAsync( (unsigned char *)sl.ref_base + sl.ref_lo, sl.d_payload, sl.payload_used + 856UL,
+                              hipMemcpyDeviceToHost, st ), -2 );
     HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
   } else if( sl.mode ) {   /* raw and in-place raw */
     HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
