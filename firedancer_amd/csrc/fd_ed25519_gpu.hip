@@ -341,7 +341,15 @@ FD_DEV void hash_one( unsigned char const * __restrict__ payload, fdgpu_txn_desc
   store_digits( k, Sw, s, n, digA, digB );
 }
 
+/* FD_HASH_MINW: minimum waves per SIMD asked of the compiler for fd_hash_kernel (A/B; 0 = none) */
+#ifndef FD_HASH_MINW
+#define FD_HASH_MINW 0
+#endif
+#if FD_HASH_MINW
+__global__ void __launch_bounds__( FD_WG, FD_HASH_MINW )
+#else
 __global__ void __launch_bounds__( FD_WG )
+#endif
 fd_hash_kernel( unsigned char const *    __restrict__ payload,
                 fdgpu_txn_desc_t const * __restrict__ desc,
                 u32 const *              __restrict__ map,
