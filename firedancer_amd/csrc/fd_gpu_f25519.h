@@ -175,6 +175,33 @@ template<int F> FD_DEV u64 fd_col_mad( u32 a, u32 b, u64 c ) {
     r.v[0] = (u32)t0_ & FE_M(0); r.v[1] += (u32)( t0_ >> 26 );                \
   } while(0)
 
+/* FD_FOLD4: four chains (columns 0-2, 3-4, 5-7, 8-9) instead of two: twice the independent
+   accumulators, so consecutive multiply-adds of one chain are further apart (no wait state between
+   them), for two more carry junctions (limbs 3 and 8).  A/B knob. */
+#ifndef FD_FOLD4
+#define FD_FOLD4 0
+#endif
+#define FE_FOLD_CHAINS4( r, COL, ca, cb ) do {                              \
+    u64 cc = 0, cd = 0;                                                      \
+    _Pragma("unroll") for( int t_=0; t_<3; t_++ ) {                          \
+      COL( t_, ca );     r.v[t_]   = (u32)ca & FE_M(t_);   ca >>= FE_W(t_);  \
+      if( t_ < 2 ) { COL( t_+3, cb ); r.v[t_+3] = (u32)cb & FE_M(t_+3); cb >>= FE_W(t_+3); } \
+      COL( t_+5, cc );   r.v[t_+5] = (u32)cc & FE_M(t_+5); cc >>= FE_W(t_+5);\
+      if( t_ < 2 ) { COL( t_+8, cd ); r.v[t_+8] = (u32)cd & FE_M(t_+8); cd >>= FE_W(t_+8); } \
+    }                                                                        \
+    u64 t3_ = fd_add32( ca, r.v[3] );                                        \
+    r.v[3] = (u32)t3_ & FE_M(3); r.v[4] += (u32)( t3_ >> 25 );                \
+    u64 t5_ = fd_add32( cb, r.v[5] );                                        \
+    r.v[5] = (u32)t5_ & FE_M(5); r.v[6] += (u32)( t5_ >> 25 );                \
+    u64 t8_ = fd_add32( cc, r.v[8] );                                        \
+    r.v[8] = (u32)t8_ & FE_M(8); r.v[9] += (u32)( t8_ >> 26 );                \
+    u64 t0_ = (u64)r.v[0] + cd * 19u;                                        \
+    r.v[0] = (u32)t0_ & FE_M(0); r.v[1] += (u32)( t0_ >> 26 );                \
+  } while(0)
+#if FD_FOLD4
+#undef  FE_FOLD_CHAINS
+#define FE_FOLD_CHAINS FE_FOLD_CHAINS4
+#endif
 
 /* Operand multiples are formed only for the limbs that use them, each
    behind an empty asm so the compiler keeps one register per multiple
