@@ -224,11 +224,13 @@ FD_DEV u32 fd_x2( u32 x ) {
 #endif
 }
 
-/* acc + x for a 32-bit x as one v_mad_u64_u32 (x * 1 + acc, 4.66 cycles)
-   instead of zero-extending x (v_mov_b32) and a 64-bit add
-   (v_lshl_add_u64): 7.5 cycles.  FD_MAD1=0: the plain add. */
+/* acc + x for a 32-bit x.  FD_MAD1=1: as one v_mad_u64_u32 (x * 1 + acc, 4.66 cycles isolated)
+   instead of zero-extending x (v_mov_b32) and a 64-bit add (v_lshl_add_u64, 7.5 cycles together).
+   Off: the DSM's time follows its multiply-add count more than its other instructions (27 more
+   v_mad_u64_u32 per doubling measured 0.3 % slower, four carry chains with ~14 more 2.5-4 % slower,
+   profiles/r02/dsm_ab), so the add stays off the multiplier. */
 #ifndef FD_MAD1
-#define FD_MAD1 1
+#define FD_MAD1 0
 #endif
 FD_DEV u64 fd_add32( u64 acc, u32 x ) {
 #if FD_MAD1
