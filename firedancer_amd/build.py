@@ -14,7 +14,8 @@ CSRC = os.path.join(PKG, "csrc")
 ARCH = os.environ.get("FDGPU_ARCH", "gfx950")
 
 HIP_SRCS = ["fd_ed25519_gpu.hip"]
-HIP_DEPS = ["fd_gpu_f25519.h", "fd_gpu_sha512.h", "fd_gpu_curve.h", "fd_gpu_txn.h", "../../include/fd_ed25519_gpu.h"]
+HIP_DEPS = ["fd_gpu_f25519.h", "fd_gpu_sha512.h", "fd_gpu_curve.h", "fd_gpu_txn.h", "fd_gpu_lattice.h",
+            "../../include/fd_ed25519_gpu.h"]
 
 
 def _stale(out: str, deps: list[str]) -> bool:
@@ -52,8 +53,19 @@ def build_vtile(force: bool = False) -> str:
     return out
 
 
+def build_lattice_host(force: bool = False) -> str:
+    """libfdlat_host.so: the device half-size-scalar reduction (fd_gpu_lattice.h) compiled as host C,
+    for tests/test_lattice.py only (the product calls it inside fd_hashh_kernel)."""
+    out = os.path.join(PKG, "libfdlat_host.so")
+    if force or _stale(out, ["fd_lat_host.c", "fd_gpu_lattice.h"]):
+        subprocess.run(["gcc", "-std=gnu11", "-O2", "-Wall", "-Wno-unknown-pragmas", "-fPIC", "-shared", "-o", out,
+                        os.path.join(CSRC, "fd_lat_host.c")], check=True)
+    return out
+
+
 def build_all(force: bool = False) -> None:
     build_synth(force)
+    build_lattice_host(force)
     build_engine(force)
     build_vtile(force)
 

@@ -33,6 +33,7 @@
 #include "fd_gpu_sha512.h"
 #include "fd_gpu_curve.h"
 #include "fd_gpu_txn.h"
+#include "fd_gpu_lattice.h"
 #include "../../include/fd_ed25519_gpu.h"
 
 #include <hip/hip_runtime.h>
@@ -101,6 +102,14 @@
 #define FD_PIPE_MAX    16UL
 #define FD_PEND_ASMALL 2           /* per-signature code in flight: A small order, R's decode picks ERR_SIG / ERR_PUBKEY */
 #define FD_PEND_REQ    3           /* per-signature code in flight: P's encoding != R's bytes -> decode R, compare */
+#define FD_PEND_SLOW   4           /* per-signature code in flight: no half-size scalars, full 253-bit walk (fd_dsm_slow_kernel) */
+/* Throughput path with half-size scalars (fd_gpu_lattice.h): 128 doublings
+   instead of 252; 0 = the full-length walk with the deferred R check (A/B) */
+#ifndef FD_HALF
+#define FD_HALF 1
+#endif
+#define FD_HDIG 33                 /* signed radix-16 digits of c0, c1 (< 2^131) */
+#define FD_PSTAT_SLOW 0x80u        /* A-status bit: the signature is on the half-size path's slow list */
 
 typedef signed char i8;
 
@@ -167,8 +176,10 @@ FD_DEV void atab_unpack( ge_cached & c, atab_raw const & r ) {
 /* ------------------------------------------------------------------ */
 
 __global__ void __launch_bounds__( FD_WG )
-fd_expand_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 * __restrict__ map, u32 nsig ) {
+fd_expand_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 * __restrict__ map, u32 nsig,
+                  u32 * __restrict__ zero_word ) {
   u32 t = blockIdx.x * FD_WG + threadIdx.x;
+  if( zero_word && t == 0u ) *zero_word = 0u;        /* the batch's slow-list count (half-size path) */
   if( t >= txn_cnt ) return;
   fdgpu_txn_desc_t d = desc[t];
   for( u32 j=0; j<d.sig_cnt; j++ ) {
@@ -277,6 +288,91 @@ FD_DEV void store_digits( u32 const k[ 8 ], u32 const Sw[ 8 ], u32 s, size_t n,
   }
 }
 
+/* ---- half-size scalars (fd_gpu_lattice.h) ------------------------------ */
+
+/* a (5 words) x b (8 words) -> 16 words (the top 3 zero), for sc_reduce */
+FD_DEV void sc_mul_5x8( u32 out[ 16 ], u32 const a[ 5 ], u32 const b[ 8 ] ) {
+  u32 r[ 16 ];
+#pragma unroll
+  for( int i=0; i<16; i++ ) r[i] = 0u;
+#pragma unroll
+  for( int i=0; i<5; i++ ) {
+    u64 c = 0;
+#pragma unroll
+    for( int j=0; j<8; j++ ) { u64 t = (u64)a[i] * (u64)b[j] + (u64)r[i+j] + c; r[i+j] = (u32)t; c = t >> 32; }
+    r[i+8] = (u32)c;
+  }
+#pragma unroll
+  for( int i=0; i<16; i++ ) out[i] = r[i];
+}
+
+/* k -> (c0, c1) with c0 == c1 k (mod 8l), re-checked here: mod 8 on the
+   low words, mod l through sc_reduce (c0, |c1| k mod l < l); then
+   s' = c1 S mod l.  0: no such pair within FD_LAT_BITS (full walk). */
+FD_DEV int hs_prepare( u32 const k[ 8 ], u32 const Sw[ 8 ], u32 c0[ 5 ], u32 c1m[ 5 ], int & c1neg, u32 sp[ 8 ] ) {
+  int ng = 0;
+  if( !fd_lat_halfsize( c0, c1m, &ng, k ) ) return 0;
+  c1neg = ng;
+  u32 c1lo = ng ? 0u - c1m[0] : c1m[0];
+  if( ( c0[0] - c1lo * k[0] ) & 7u ) return 0;                       /* mod 8 */
+  u32 const lw[8] = { 0x5cf5d3edu, 0x5812631au, 0xa2f79cd6u, 0x14def9deu, 0u, 0u, 0u, 0x10000000u };
+  u32 prod[ 16 ], x[ 8 ];
+  sc_mul_5x8( prod, c1m, k ); sc_reduce( x, prod );                  /* |c1| k mod l */
+  u32 diff = 0u;
+  if( !ng ) {                                                          /* c0 == |c1| k */
+#pragma unroll
+    for( int i=0; i<8; i++ ) diff |= x[i] ^ ( i < 5 ? c0[i] : 0u );
+  } else {                                                             /* c0 + |c1| k == 0 or l */
+    u64 c = 0; u32 z = 0u, e = 0u;
+#pragma unroll
+    for( int i=0; i<8; i++ ) {
+      u64 v = (u64)x[i] + (u64)( i < 5 ? c0[i] : 0u ) + c; c = v >> 32;
+      z |= (u32)v; e |= (u32)v ^ lw[i];
+    }
+    diff = ( z != 0u ) & ( e != 0u );
+  }
+  if( diff ) return 0;                                                 /* mod l */
+  sc_mul_5x8( prod, c1m, Sw ); sc_reduce( x, prod );                 /* |c1| S mod l */
+  u32 nz = 0u;
+#pragma unroll
+  for( int i=0; i<8; i++ ) nz |= x[i];
+  if( ng && nz ) {                                                     /* s' = l - x */
+    i64 br = 0;
+#pragma unroll
+    for( int i=0; i<8; i++ ) { i64 t = (i64)lw[i] - (i64)x[i] + br; sp[i] = (u32)t; br = t >> 32; }
+  } else {
+#pragma unroll
+    for( int i=0; i<8; i++ ) sp[i] = x[i];
+  }
+  return 1;
+}
+
+/* signed radix-16 digits of c0 and c1 (sign folded in: [c1](-R) =
+   sum d_i 16^i (-R)), digA / digR [FD_HDIG][n]; s' as digB */
+FD_DEV void hs_store_digits( u32 const c0[ 5 ], u32 const c1m[ 5 ], int c1neg, u32 const sp[ 8 ], u32 s, size_t n,
+                             i8 * __restrict__ digA, i8 * __restrict__ digR, short * __restrict__ digB ) {
+  int ca = 0, cr = 0;
+#pragma unroll
+  for( int i=0; i<FD_HDIG; i++ ) {
+    int va = (int)( ( c0[i>>3]  >> (4*(i&7)) ) & 15u ) + ca;
+    int vr = (int)( ( c1m[i>>3] >> (4*(i&7)) ) & 15u ) + cr;
+    /* digits in [-8,8); the top one (bits 128-131 plus the carry, <= 8 for
+       values < 2^131) is kept as is: the tables hold [0..8] */
+    ca = i < FD_HDIG-1 ? ( va + 8 ) >> 4 : 0; cr = i < FD_HDIG-1 ? ( vr + 8 ) >> 4 : 0;
+    int dr = vr - ( cr << 4 );
+    digA[(size_t)i*n + s] = (i8)( va - ( ca << 4 ) );
+    digR[(size_t)i*n + s] = (i8)( c1neg ? -dr : dr );
+  }
+  int carry = 0;
+#pragma unroll
+  for( int i=0; i<FD_BDIG; i++ ) {
+    int bit = FD_BWIN*i;
+    int v = (int)((sp[bit>>5] >> (bit&31)) & ((1u<<FD_BWIN)-1u)) + carry;
+    carry = (v + (1<<(FD_BWIN-1))) >> FD_BWIN;
+    digB[(size_t)i*n + s] = (short)(v - (carry << FD_BWIN));
+  }
+}
+
 /* The result-code procedure of fd_ed25519_verify (fd_ed25519_user.c:
    174-199) from S's check (code so far: SUCCESS or
    ERR_SIG) and the point statuses pa (A) and pr (R).  defer: R has not
@@ -374,6 +470,60 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
   hash_one( payload, desc, map, s, nsig, semantics, 1, pstat, code_out, digA, digB, Rraw, khash );
 }
 
+/* Half-size path, after the decode of A and R: the full result-code
+   procedure, then for the signatures still pending k = SHA-512(R||A||M)
+   mod l, the reduction to (c0, c1) and s' = c1 S mod l, stored as digits.
+   A signature without a short pair keeps the digits of k and S and goes
+   on the slow list (FD_PEND_SLOW). */
+__global__ void __launch_bounds__( FD_WG )
+fd_hashh_kernel( unsigned char const *    __restrict__ payload,
+                 fdgpu_txn_desc_t const * __restrict__ desc,
+                 u32 const *              __restrict__ map,
+                 u32                                   nsig,
+                 int                                   semantics,
+                 unsigned char *          __restrict__ pstat,
+                 i8 *                     __restrict__ code_out,
+                 i8 *                     __restrict__ digA,
+                 i8 *                     __restrict__ digR,
+                 short *                  __restrict__ digB,
+                 u32 *                    __restrict__ slow,
+                 u32 *                    __restrict__ slow_cnt,
+                 uint4 const *            __restrict__ khash,
+                 u32                                   force_slow ) {
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  u32 m = map[s];
+  u32 t = m & 0xffffffu, j = m >> 24;
+  fdgpu_txn_desc_t d = desc[t];
+  if( !txn_desc_ok( d ) ) { code_out[s] = FD_ED25519_ERR_SIG; return; }
+  unsigned char const * base = payload + d.payload_off;
+  u32 Sw[8];
+  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
+  int code = sc_is_canonical( Sw ) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_SIG;
+  code = result_code( code, pstat[2*s], pstat[2*s+1], semantics, 0 );
+  if( code != FD_ED25519_SUCCESS ) { code_out[s] = (i8)code; return; }
+  u32 Rw[8], Aw[8];
+  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
+  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
+  u32 h[16], k[8];
+  if( khash ) {
+#pragma unroll
+    for( int i=0; i<4; i++ ) { uint4 v = khash[4*(size_t)s + i]; h[4*i] = v.x; h[4*i+1] = v.y; h[4*i+2] = v.z; h[4*i+3] = v.w; }
+  } else fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
+  sc_reduce( k, h );
+  size_t n = nsig;
+  u32 c0[5], c1m[5], sp[8]; int c1neg = 0;
+  if( !( force_slow && s % force_slow == 0u ) && hs_prepare( k, Sw, c0, c1m, c1neg, sp ) ) {
+    hs_store_digits( c0, c1m, c1neg, sp, s, n, digA, digR, digB );
+    code_out[s] = FD_ED25519_SUCCESS;
+  } else {
+    store_digits( k, Sw, s, n, digA, digB );
+    code_out[s] = FD_PEND_SLOW;
+    pstat[2*s] |= FD_PSTAT_SLOW;       /* fd_dsmh_kernel's half-size blocks skip it even once its code is final */
+    slow[ atomicAdd( slow_cnt, 1u ) ] = s;
+  }
+}
+
 /* Small batches (latency): the three independent parts of the prep in
    ONE launch -- blocks [0,sg) decode A, [sg,2sg) decode R, [2sg,3sg)
    check S and hash -- so a batch that cannot fill the GPU pays the
@@ -449,33 +599,13 @@ __device__ unsigned long long fd_clk_buf[ FD_CLK_BLOCKS ][ 4 ];
 #ifndef FD_DSM_MINW
 #define FD_DSM_MINW 0
 #endif
+/* [k](-A) + [S]B for signature s (full-length signed fixed windows; body of
+   fd_dsm_kernel and of fd_dsm_slow_kernel).  defer: store P for the R-check
+   kernels; else compare with the decoded R and write the code. */
 template<int FM>
-#if FD_DSM_MINW
-__global__ void __launch_bounds__( FD_WG, FD_DSM_MINW )
-#else
-__global__ void __launch_bounds__( FD_WG )
-#endif
-fd_dsm_kernel( u32                      nsig,
-               uint4 const * __restrict__ tab,
-               uint4 const * __restrict__ Rxy,
-               i8 const *    __restrict__ digA,
-               short const * __restrict__ digB,
-               uint4 const * __restrict__ btab_g,
-               i8 *          __restrict__ code,
-               u32 *         __restrict__ Pbuf,
-               int                        defer ) {
-#if FD_BWIN==8
-  __shared__ uint4 btab[ FD_BTAB_ENTRIES * 6 ];
-  for( int i=threadIdx.x; i<FD_BTAB_ENTRIES*6; i+=FD_WG ) btab[i] = btab_g[i];
-  __syncthreads();
-#endif
-
-  FD_CLK_BEGIN
-  u32 s = blockIdx.x * FD_WG + threadIdx.x;
-  if( s >= nsig ) return;
-  if( code[s] != FD_ED25519_SUCCESS ) return;
-  size_t n = nsig;
-
+FD_DEV void dsm_one( u32 s, size_t n, uint4 const * __restrict__ tab, uint4 const * __restrict__ Rxy,
+                     i8 const * __restrict__ digA, short const * __restrict__ digB, uint4 const * btab,
+                     i8 * __restrict__ code, u32 * __restrict__ Pbuf, int defer ) {
   ge_p3 P; ge_p3_identity( P );
   ge_p2 P2;
   atab_raw raw;
@@ -492,7 +622,7 @@ fd_dsm_kernel( u32                      nsig,
 #if FD_BWIN==16
     if( !(w & 3) ) {                                 /* base-point entry, also in flight */
       db = digB[ (size_t)(w>>2)*n + s ];
-      uint4 const * bp = btab_g + (size_t)( db < 0 ? -db : db )*6;
+      uint4 const * bp = btab + (size_t)( db < 0 ? -db : db )*6;
 #pragma unroll
       for( int i=0; i<6; i++ ) braw[i] = bp[i];
     }
@@ -543,7 +673,6 @@ fd_dsm_kernel( u32                      nsig,
     fe_store_planar( Pbuf + s, n, P2.X );
     fe_store_planar( Pbuf + 10*n + s, n, P2.Y );
     fe_store_planar( Pbuf + 20*n + s, n, P2.Z );
-    FD_CLK_END
     return;
   }
   /* R decoded up front (small batches): fd_ed25519_point_eq_z1,
@@ -555,6 +684,170 @@ fd_dsm_kernel( u32                      nsig,
   fe_mul<FM>( u, x, P2.Z ); int okx = fe_eq( u, P2.X );
   fe_mul<FM>( u, y, P2.Z ); int oky = fe_eq( u, P2.Y );
   code[s] = (okx & oky) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+template<int FM>
+#if FD_DSM_MINW
+__global__ void __launch_bounds__( FD_WG, FD_DSM_MINW )
+#else
+__global__ void __launch_bounds__( FD_WG )
+#endif
+fd_dsm_kernel( u32                      nsig,
+               uint4 const * __restrict__ tab,
+               uint4 const * __restrict__ Rxy,
+               i8 const *    __restrict__ digA,
+               short const * __restrict__ digB,
+               uint4 const * __restrict__ btab_g,
+               i8 *          __restrict__ code,
+               u32 *         __restrict__ Pbuf,
+               int                        defer ) {
+#if FD_BWIN==8
+  __shared__ uint4 btab[ FD_BTAB_ENTRIES * 6 ];
+  for( int i=threadIdx.x; i<FD_BTAB_ENTRIES*6; i+=FD_WG ) btab[i] = btab_g[i];
+  __syncthreads();
+#else
+  uint4 const * btab = btab_g;
+#endif
+  FD_CLK_BEGIN
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  if( code[s] != FD_ED25519_SUCCESS ) return;
+  dsm_one<FM>( s, nsig, tab, Rxy, digA, digB, btab, code, Pbuf, defer );
+  FD_CLK_END
+}
+
+/* Half-size path: the signatures on the slow list (no short (c0, c1)) take
+   the full 253-bit walk over k's and S's digits, R compared at its end,
+   compacted into whole waves.  fd_dsmh_kernel's first blocks take the head
+   of the list; this kernel the rest (normally nothing: ~0.2 % of
+   signatures, more only for inputs ground to defeat the reduction). */
+template<int FM>
+__global__ void __launch_bounds__( FD_WG )
+fd_dsm_slow_kernel( u32 nsig, uint4 const * __restrict__ tab, uint4 const * __restrict__ Rxy,
+                    i8 const * __restrict__ digA, short const * __restrict__ digB, uint4 const * __restrict__ btab,
+                    i8 * __restrict__ code, u32 const * __restrict__ slow, u32 const * __restrict__ slow_cnt,
+                    u32 first ) {
+  u32 i = first + blockIdx.x * FD_WG + threadIdx.x;
+  if( i < *slow_cnt ) dsm_one<FM>( slow[i], nsig, tab, Rxy, digA, digB, btab, code, (u32 *)0, 0 );
+}
+
+/* Half-size path tables: blocks [0,sg) build [0..8](-A) for every pending
+   signature (also the slow ones), blocks [sg,2sg) [0..8](-R) for the
+   half-size ones. */
+__global__ void __launch_bounds__( FD_WG, 3 )
+fd_tableh_kernel( u32 nsig, u32 sg, i8 const * __restrict__ code, uint4 const * __restrict__ Axy,
+                  uint4 const * __restrict__ Rxy, uint4 * __restrict__ tabA, uint4 * __restrict__ tabR ) {
+  u32 role = blockIdx.x >= sg, b = blockIdx.x - role*sg;
+  u32 s = b * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  int c = code[s];
+  if( !role ) { if( c == FD_ED25519_SUCCESS || c == FD_PEND_SLOW ) atab_build( tabA, s, Axy ); }
+  else if( c == FD_ED25519_SUCCESS ) atab_build( tabR, s, Rxy );
+}
+
+/* Half-size DSM: Q = [s']B + [c0](-A) + [c1](-R) by a joint signed
+   fixed-window walk over FD_HDIG = 33 windows of 4 bits -- 128 doublings,
+   33 -A adds and 33 -R adds (both tables gathered from HBM, the -A entry
+   across the window's doublings), and the 16 radix-2^16 digits of s' as one
+   base-point add per even window from [0..32768]B (digits 0-7) and
+   [0..32768](2^120 B) (digits 8-15).
+   Q == O (X == 0, Y == Z)  <=>  R == [S]B - [k]A  (fd_gpu_lattice.h). */
+/* FD_DSMH_MINW: waves per SIMD asked of the compiler (3: <= 168 VGPRs) */
+#ifndef FD_DSMH_MINW
+#define FD_DSMH_MINW 3
+#endif
+#ifndef FD_DSMH_RLATE
+#define FD_DSMH_RLATE 0      /* 1: issue the -R gather after the -A add (fewer VGPRs live across it) */
+#endif
+template<int FM>
+__global__ void __launch_bounds__( FD_WG, FM ? FD_DSMH_MINW : 1 )
+fd_dsmh_kernel( u32                      nsig,
+                uint4 const * __restrict__ tabA,
+                uint4 const * __restrict__ tabR,
+                i8 const *    __restrict__ digA,
+                i8 const *    __restrict__ digR,
+                short const * __restrict__ digB,
+                uint4 const * __restrict__ btab,
+                uint4 const * __restrict__ btab2,
+                i8 *          __restrict__ code,
+                uint4 const * __restrict__ Rxy,
+                u32 const *   __restrict__ slow,
+                u32 const *   __restrict__ slow_cnt,
+                u32                        nslowblk,
+                unsigned char const * __restrict__ pstat ) {
+  size_t n = nsig;
+  if( blockIdx.x < nslowblk ) {
+    /* the first blocks take the head of the slow list (full 253-bit walk,
+       about twice a half-size walk): dispatched first, they run beside the
+       half-size waves instead of after them; fd_dsm_slow_kernel takes the rest */
+    u32 i = blockIdx.x * FD_WG + threadIdx.x;
+    if( i < *slow_cnt ) dsm_one<FM>( slow[i], n, tabA, Rxy, digA, digB, btab, code, (u32 *)0, 0 );
+    return;
+  }
+  u32 s = ( blockIdx.x - nslowblk ) * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  /* a slow-list signature's code may already be final (SUCCESS) when this
+     block starts: the flag, not the code, keeps it out */
+  if( code[s] != FD_ED25519_SUCCESS || ( pstat[2*s] & FD_PSTAT_SLOW ) ) return;
+  ge_p3 P; ge_p3_identity( P );
+  ge_p2 P2;
+  atab_raw ra, rr;
+  int da = digA[ (size_t)(FD_HDIG-1)*n + s ], dr = digR[ (size_t)(FD_HDIG-1)*n + s ];
+#pragma unroll 1
+  for( int w=FD_HDIG-1; w>=0; w-- ) {
+    atab_fetch( ra, tabA, s, da < 0 ? -da : da );    /* in flight during the doublings */
+    ge_p1p1 t;
+    if( w != FD_HDIG-1 ) {
+#pragma unroll 1
+      for( int r=0; r<3; r++ ) { ge_dbl<FM>( t, P2 ); ge_p1p1_to_p2<FM>( P2, t ); }
+      ge_dbl<FM>( t, P2 ); ge_p1p1_to_p3<FM>( P, t );
+    }
+    /* the -R entry and the base-point entries are issued after the
+       doublings (in flight during the -A add): prefetching all of them
+       across the doublings costs 206 VGPRs, 2 waves per SIMD */
+#if FD_DSMH_RLATE
+    {
+      ge_cached q; atab_unpack( q, ra ); ge_cached_cneg( q, da < 0 );
+      ge_add_cached<FM>( t, P, q );
+    }
+    atab_fetch( rr, tabR, s, dr < 0 ? -dr : dr );   /* in flight during the P3 conversion */
+    ge_p1p1_to_p3<FM>( P, t );
+#else
+    atab_fetch( rr, tabR, s, dr < 0 ? -dr : dr );
+    {
+      ge_cached q; atab_unpack( q, ra ); ge_cached_cneg( q, da < 0 );
+      ge_add_cached<FM>( t, P, q ); ge_p1p1_to_p3<FM>( P, t );
+    }
+#endif
+    /* base-point digit j (bits 16j..16j+15 of s') at window 4j from [0..32768]B,
+       digit j+8 (bits 16j+128..) at window 4j+2 from [0..32768](2^120 B):
+       one base-point add per even window */
+    int bw = !(w & 1) && w < 32;
+    int db = bw ? digB[ (size_t)( (w>>2) + ( (w & 2) ? 8 : 0 ) )*n + s ] : 0;
+    {
+      ge_cached q; atab_unpack( q, rr ); ge_cached_cneg( q, dr < 0 );
+      ge_add_cached<FM>( t, P, q );
+    }
+    if( bw ) {
+      uint4 braw[6];                                 /* in flight during the P3 conversion (across the
+                                                        -R add it cost the 3rd wave) */
+      uint4 const * bp = ( (w & 2) ? btab2 : btab ) + (size_t)( db < 0 ? -db : db )*6;
+#pragma unroll
+      for( int i=0; i<6; i++ ) braw[i] = bp[i];
+      ge_precomp bq;
+      ge_p1p1_to_p3<FM>( P, t );
+      fe_from_quads( bq.ypx,  braw[0], braw[1] );
+      fe_from_quads( bq.ymx,  braw[2], braw[3] );
+      fe_from_quads( bq.xy2d, braw[4], braw[5] );
+      ge_precomp_cneg( bq, db < 0 );
+      ge_add_precomp<FM>( t, P, bq );
+    }
+    ge_p1p1_to_p2<FM>( P2, t );
+    if( w > 0 ) { da = digA[ (size_t)(w-1)*n + s ]; dr = digR[ (size_t)(w-1)*n + s ]; }
+  }
+  /* Q == O: X == 0 and Y == Z (Z != 0: complete formulas) */
+  int ok = fe_is_zero( P2.X ) & fe_eq( P2.Y, P2.Z );
+  code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
 /* ---- latency path: two lanes per signature ------------------------------
@@ -1201,14 +1494,17 @@ fd_sha512_batch_kernel( unsigned char const * __restrict__ data, unsigned long c
   for( int i=0; i<4; i++ ) o[i] = make_uint4( h[4*i], h[4*i+1], h[4*i+2], h[4*i+3] );
 }
 
-/* [e]B for e in [0,FD_BTAB_ENTRIES), affine precomputed (y+x, y-x, 2dxy),
+/* [e]B (or [e](2^dbl B)) for e in [0,FD_BTAB_ENTRIES), affine precomputed (y+x, y-x, 2dxy),
    canonical, packed 8x32.  Generated on the device at context creation
    (the GPU analogue of table/fd_curve25519_table_*.c
    fd_ed25519_base_point_wnaf_table). */
-__global__ void __launch_bounds__( 256 ) fd_btab_kernel( uint4 * out ) {
+__global__ void __launch_bounds__( 256 ) fd_btab_kernel( uint4 * out, int dbl ) {
   int e = blockIdx.x * blockDim.x + threadIdx.x;
   if( e >= FD_BTAB_ENTRIES ) return;
   ge_p3 B; B.X = fe_Bx(); B.Y = fe_By(); B.Z = fe_one(); fe_mul( B.T, B.X, B.Y );
+  /* dbl = 120: the table of 2^120 B (the half-size path's digits 8-15 of s') */
+#pragma unroll 1
+  for( int i=0; i<dbl; i++ ) ge_p3_dbl( B, B );
   ge_p3 acc; ge_p3_identity( acc );
 #pragma unroll 1
   for( int b=FD_BWIN; b>=0; b-- ) {
@@ -1344,7 +1640,13 @@ struct fdgpu_ed25519_ctx {
   u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
   u32 *   d_O;                   /*             product of the block's other Z, planar [10][max_sig] */
   u32 *   d_blk;                 /*             per 256-signature block: product of Z, then its inverse */
-  u32 *   d_slow;                /*             signatures needing R's full decode, [max_sig] + count */
+  u32 *   d_slow;                /*             signatures needing R's full decode, [max_sig] + count
+                                    (half-size path: signatures without a short (c0, c1)) */
+  int     half;                  /* throughput path with half-size scalars (env FDGPU_HALF, default FD_HALF) */
+  u32     half_force_slow;       /* tests: signatures with s % m == 0 take the full walk (env FDGPU_HALF_FORCE_SLOW) */
+  uint4 * d_tabR;                /* half-size path: [0..8](-R), layout of d_tab */
+  i8 *    d_digR;                /*                 signed radix-16 digits of c1, [FD_HDIG][max_sig] */
+  uint4 * d_btab2;               /*                 [0..32768](2^120 B) */
   uint4 * d_khash;               /* NULL, or (drop-in, long messages) SHA-512(R||A||M) per signature, computed beforehand */
   hipEvent_t ev[4];
   enum { NRING = 64 };
@@ -1397,13 +1699,15 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
   unsigned tg = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   unsigned sg = (unsigned)( (sig_cnt + FD_WG - 1) / FD_WG );
   if( nsig ) {
-    hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig );
+    hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig,
+                        ctx->d_slow + ctx->max_sig );
     if( ctx->timing ) hipEventRecord( ev[0], st );
     /* small batch: cannot fill the GPU, so latency is the sum of the kernels' per-wave
        instruction streams -- decode A, decode R and hash side by side in one launch,
        R compared at the end of the DSM (no R-check chain and its inversion) */
     int small = nsig <= ctx->small_max, lanes = 1;
-    int defer = FD_DEFER_R && !small;
+    int half = ctx->half && !small;
+    int defer = FD_DEFER_R && !small && !half;
     if( small ) {
       /* lanes per signature in the DSM: 4 while a quad per signature still fits one wave per
          SIMD (n <= 16K), 2 while a pair does (n <= 32K), else 1 (configs[0]'s 64K: 0.88 ms
@@ -1416,6 +1720,16 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       if( !d2 )
         hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, ctx->d_pstat, code,
                             ctx->d_Axy, ctx->d_tab );
+    } else if( half ) {
+      /* half-size scalars: decode A and R, result codes + hash + (c0, c1, s'), both tables */
+      unsigned pg = (unsigned)( ( 2UL*sig_cnt + FD_WG - 1) / FD_WG );
+      hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, 1,
+                          ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy );
+      hipLaunchKernelGGL( fd_hashh_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+                          ctx->semantics, ctx->d_pstat, code, ctx->d_digA, ctx->d_digR, ctx->d_digB, ctx->d_slow,
+                          ctx->d_slow + ctx->max_sig, (uint4 const *)ctx->d_khash, ctx->half_force_slow );
+      hipLaunchKernelGGL( fd_tableh_kernel, dim3(2*sg), dim3(FD_WG), 0, st, nsig, (u32)sg, code, ctx->d_Axy, ctx->d_Rxy,
+                          ctx->d_tab, ctx->d_tabR );
     } else {
       unsigned pg = (unsigned)( ( (defer ? 1UL : 2UL)*sig_cnt + FD_WG - 1) / FD_WG );
       hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, !defer,
@@ -1433,13 +1747,34 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     else if( small && lanes==2 )
       hipLaunchKernelGGL( fd_dsm2_kernel<0>, dim3(2*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                           ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat );
+    else if( half ) {
+      /* slow list: its head in fd_dsmh_kernel's first nsb blocks (room for 1/64 of the batch), the
+         rest (if any) in fd_dsm_slow_kernel */
+      unsigned nsb = ( sg + 63u ) / 64u;
+      u32 * slow_cnt = ctx->d_slow + ctx->max_sig;
+      if( nsig <= ctx->nofold_max ) {
+        hipLaunchKernelGGL( fd_dsmh_kernel<0>, dim3(nsb + sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
+                            ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->d_Rxy, ctx->d_slow, slow_cnt, nsb,
+                            ctx->d_pstat );
+        if( ctx->timing ) hipEventRecord( ev[2], st );
+        hipLaunchKernelGGL( fd_dsm_slow_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy, ctx->d_digA,
+                            ctx->d_digB, ctx->d_btab, code, ctx->d_slow, slow_cnt, nsb * FD_WG );
+      } else {
+        hipLaunchKernelGGL( fd_dsmh_kernel<1>, dim3(nsb + sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
+                            ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->d_Rxy, ctx->d_slow, slow_cnt, nsb,
+                            ctx->d_pstat );
+        if( ctx->timing ) hipEventRecord( ev[2], st );
+        hipLaunchKernelGGL( fd_dsm_slow_kernel<1>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy, ctx->d_digA,
+                            ctx->d_digB, ctx->d_btab, code, ctx->d_slow, slow_cnt, nsb * FD_WG );
+      }
+    }
     else if( nsig <= ctx->nofold_max )         /* <= 2 waves per SIMD: latency-bound, independent column chains */
       hipLaunchKernelGGL( fd_dsm_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                           ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P, defer );
     else
       hipLaunchKernelGGL( fd_dsm_kernel<1>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                           ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P, defer );
-    if( ctx->timing ) hipEventRecord( ev[2], st );
+    if( ctx->timing && !half ) hipEventRecord( ev[2], st );
     if( defer ) {
       u32 * slow_cnt = ctx->d_slow + ctx->max_sig;
       hipLaunchKernelGGL( fd_rprod_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_P, ctx->d_O, ctx->d_blk, slow_cnt );
@@ -1501,6 +1836,15 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   HIPCHK( hipMalloc( &ctx->d_O, ns * 10 * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_blk, ( ( ns + FD_WG - 1 ) / FD_WG ) * 10 * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_slow, ( ns + 1 ) * sizeof(u32) ), -1 );
+  { char const * h = getenv( "FDGPU_HALF" );                /* A/B knob: 0 = full-length walk + deferred R check */
+    ctx->half = h ? atoi( h ) : FD_HALF;
+    char const * fs = getenv( "FDGPU_HALF_FORCE_SLOW" );
+    ctx->half_force_slow = fs ? (u32)strtoul( fs, NULL, 0 ) : 0u; }
+  if( ctx->half ) {
+    HIPCHK( hipMalloc( &ctx->d_tabR, ns * FD_ATAB_ENTRIES * 8 * sizeof(uint4) ), -1 );
+    HIPCHK( hipMalloc( &ctx->d_digR, ns * FD_HDIG ), -1 );
+    HIPCHK( hipMalloc( &ctx->d_btab2, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), -1 );
+  }
   { char const * e = getenv( "FDGPU_SMALL_BATCH_MAX" );   /* A/B knob: signatures at or below take the latency path */
     ctx->small_max = e ? strtoul( e, NULL, 0 ) : FD_SMALL_BATCH_MAX;
     char const * dl = getenv( "FDGPU_DSM_LANES" );
@@ -1510,7 +1854,9 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
-  hipLaunchKernelGGL( fd_btab_kernel, dim3((FD_BTAB_ENTRIES + 255)/256), dim3(256), 0, ctx->stream, ctx->d_btab );
+  hipLaunchKernelGGL( fd_btab_kernel, dim3((FD_BTAB_ENTRIES + 255)/256), dim3(256), 0, ctx->stream, ctx->d_btab, 0 );
+  if( ctx->half )
+    hipLaunchKernelGGL( fd_btab_kernel, dim3((FD_BTAB_ENTRIES + 255)/256), dim3(256), 0, ctx->stream, ctx->d_btab2, 120 );
   HIPCHK( hipGetLastError(), -1 );
   for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) HIPCHK( hipEventCreateWithFlags( &ctx->slot[i].done, hipEventDisableTiming ), -1 );
   HIPCHK( hipHostMalloc( (void **)&ctx->h_flag, fdgpu_ed25519_ctx_t::NSLOT * sizeof(unsigned long), hipHostMallocDefault ), -1 );
@@ -1549,6 +1895,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   (void)hipFree( ctx->d_map ); (void)hipFree( ctx->d_code ); (void)hipFree( ctx->d_pstat ); (void)hipFree( ctx->d_tab );
   (void)hipFree( ctx->d_Rxy ); (void)hipFree( ctx->d_Axy ); (void)hipFree( ctx->d_digA ); (void)hipFree( ctx->d_digB );
   (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_rdesc ); (void)hipFree( ctx->d_pflag );
+  (void)hipFree( ctx->d_tabR ); (void)hipFree( ctx->d_digR ); (void)hipFree( ctx->d_btab2 );
   (void)hipFree( ctx->d_P ); (void)hipFree( ctx->d_O ); (void)hipFree( ctx->d_blk ); (void)hipFree( ctx->d_slow );
   for( int i=0; i<4; i++ ) if( ctx->ev[i] ) (void)hipEventDestroy( ctx->ev[i] );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) if( ctx->ring[r][i] ) (void)hipEventDestroy( ctx->ring[r][i] );

@@ -26,21 +26,25 @@ def golden():
 
 
 # Every GPU test runs on both engine paths (include/fd_ed25519_gpu.h,
-# fdgpu_ed25519_set_small_batch_max): "throughput" (R checked after one
-# batched inversion per 256 signatures) and "latencyN" (one fused prep
+# fdgpu_ed25519_set_small_batch_max): "throughput" (half-size scalars,
+# fd_gpu_lattice.h: R decoded, a 128-doubling walk, Q == O), "throughput_full"
+# (env FDGPU_HALF=0: the 252-doubling walk, R checked after one batched
+# inversion per 256 signatures) and "latencyN" (one fused prep
 # launch, R decoded up front, N = 4, 2 or 1 lanes per signature in the
 # DSM, env FDGPU_DSM_LANES).  The engine reads FDGPU_SMALL_BATCH_MAX
 # when a context is created, so the choice reaches contexts the verify
 # tile library creates too.
 def pytest_generate_tests(metafunc):
     if metafunc.definition.get_closest_marker("gpu") is not None and "engine_path" in metafunc.fixturenames:
-        metafunc.parametrize("engine_path", ["throughput", "latency4", "latency2", "latency1"], indirect=True)
+        metafunc.parametrize("engine_path", ["throughput", "throughput_full", "latency4", "latency2", "latency1"],
+                            indirect=True)
 
 
 @pytest.fixture(autouse=True)
 def engine_path(request, monkeypatch):
     path = getattr(request, "param", None)
     if path is not None:
-        monkeypatch.setenv("FDGPU_SMALL_BATCH_MAX", "0" if path == "throughput" else str(2**63))
+        monkeypatch.setenv("FDGPU_SMALL_BATCH_MAX", "0" if path.startswith("throughput") else str(2**63))
+        monkeypatch.setenv("FDGPU_HALF", "0" if path == "throughput_full" else "1")
         monkeypatch.setenv("FDGPU_DSM_LANES", path[-1] if path.startswith("latency") else "0")
     return path

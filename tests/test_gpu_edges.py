@@ -101,3 +101,25 @@ def test_r_check_slow_path(fa, oracle, frac):
     np.testing.assert_array_equal(t, want)
     ot, os_ = oracle.verify_txns(payload, desc, nsig, threads=16)
     np.testing.assert_array_equal(t, ot)
+
+
+@pytest.mark.parametrize("every,ntx", [(1, 3000), (3, 3000), (50, 200000), (97, 300000)])
+def test_half_size_slow_list(fa, oracle, monkeypatch, every, ntx):
+    """Half-size path: signatures without a short (c0, c1) take the full 253-bit walk off a compacted
+    list (the head in fd_dsmh_kernel's first blocks, the rest in fd_dsm_slow_kernel).  Forced here for
+    every / every 3rd / 50th / 97th signature (env FDGPU_HALF_FORCE_SLOW) in adversarial multi-signer
+    batches: codes equal the oracle's.  At 2 % (every 50th of ~500K signatures) the list overflows the
+    head into fd_dsm_slow_kernel, and a slow signature's code is final long before the last
+    half-size blocks start (they must not take it for a half-size one)."""
+    from firedancer_amd import synth
+    monkeypatch.setenv("FDGPU_HALF", "1")
+    monkeypatch.setenv("FDGPU_SMALL_BATCH_MAX", "0")
+    monkeypatch.setenv("FDGPU_HALF_FORCE_SLOW", str(every))
+    payload, desc, expect, nsig = synth.make_batch(ntx, synth.MULTI, max_signers=4, invalid_frac=0.3, seed=77 + every,
+                                                   threads=16)
+    eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    t, s = eng.verify_txns_host(payload, desc)
+    eng.close()
+    np.testing.assert_array_equal(t, expect)
+    ot, os_ = oracle.verify_txns(payload, desc, nsig, threads=16)
+    np.testing.assert_array_equal(s, os_)
