@@ -108,7 +108,7 @@
 #ifndef FD_HALF
 #define FD_HALF 1
 #endif
-#define FD_HDIG 33                 /* signed radix-16 digits of c0, c1 (< 2^131) */
+#define FD_HDIG 40                 /* signed radix-16 digits of c0, c1 (< 2^159); the walk stops at the wave's top one */
 #define FD_PSTAT_SLOW 0x80u        /* A-status bit: the signature is on the half-size path's slow list */
 
 typedef signed char i8;
@@ -350,19 +350,23 @@ FD_DEV int hs_prepare( u32 const k[ 8 ], u32 const Sw[ 8 ], u32 c0[ 5 ], u32 c1m
 /* signed radix-16 digits of c0 and c1 (sign folded in: [c1](-R) =
    sum d_i 16^i (-R)), digA / digR [FD_HDIG][n]; s' as digB */
 FD_DEV void hs_store_digits( u32 const c0[ 5 ], u32 const c1m[ 5 ], int c1neg, u32 const sp[ 8 ], u32 s, size_t n,
-                             i8 * __restrict__ digA, i8 * __restrict__ digR, short * __restrict__ digB ) {
-  int ca = 0, cr = 0;
+                             i8 * __restrict__ digA, i8 * __restrict__ digR, short * __restrict__ digB,
+                             unsigned char * __restrict__ htop ) {
+  int ca = 0, cr = 0, top = 0;
 #pragma unroll
   for( int i=0; i<FD_HDIG; i++ ) {
     int va = (int)( ( c0[i>>3]  >> (4*(i&7)) ) & 15u ) + ca;
     int vr = (int)( ( c1m[i>>3] >> (4*(i&7)) ) & 15u ) + cr;
-    /* digits in [-8,8); the top one (bits 128-131 plus the carry, <= 8 for
-       values < 2^131) is kept as is: the tables hold [0..8] */
+    /* digits in [-8,8); the top one (bits 156-159 plus the carry, <= 8 for
+       values < 2^159) is kept as is: the tables hold [0..8] */
     ca = i < FD_HDIG-1 ? ( va + 8 ) >> 4 : 0; cr = i < FD_HDIG-1 ? ( vr + 8 ) >> 4 : 0;
     int dr = vr - ( cr << 4 );
-    digA[(size_t)i*n + s] = (i8)( va - ( ca << 4 ) );
+    int da = va - ( ca << 4 );
+    digA[(size_t)i*n + s] = (i8)da;
     digR[(size_t)i*n + s] = (i8)( c1neg ? -dr : dr );
+    top = ( da | dr ) ? i : top;
   }
+  htop[s] = (unsigned char)top;                     /* highest window with a nonzero digit */
   int carry = 0;
 #pragma unroll
   for( int i=0; i<FD_BDIG; i++ ) {
@@ -489,7 +493,8 @@ fd_hashh_kernel( unsigned char const *    __restrict__ payload,
                  u32 *                    __restrict__ slow,
                  u32 *                    __restrict__ slow_cnt,
                  uint4 const *            __restrict__ khash,
-                 u32                                   force_slow ) {
+                 u32                                   force_slow,
+                 unsigned char *          __restrict__ htop ) {
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
   u32 m = map[s];
@@ -514,7 +519,7 @@ fd_hashh_kernel( unsigned char const *    __restrict__ payload,
   size_t n = nsig;
   u32 c0[5], c1m[5], sp[8]; int c1neg = 0;
   if( !( force_slow && s % force_slow == 0u ) && hs_prepare( k, Sw, c0, c1m, c1neg, sp ) ) {
-    hs_store_digits( c0, c1m, c1neg, sp, s, n, digA, digR, digB );
+    hs_store_digits( c0, c1m, c1neg, sp, s, n, digA, digR, digB, htop );
     code_out[s] = FD_ED25519_SUCCESS;
   } else {
     store_digits( k, Sw, s, n, digA, digB );
@@ -746,7 +751,7 @@ fd_tableh_kernel( u32 nsig, u32 sg, i8 const * __restrict__ code, uint4 const * 
 }
 
 /* Half-size DSM: Q = [s']B + [c0](-A) + [c1](-R) by a joint signed
-   fixed-window walk over FD_HDIG = 33 windows of 4 bits -- 128 doublings,
+   fixed-window walk over (normally) 33 windows of 4 bits -- 128 doublings,
    33 -A adds and 33 -R adds (both tables gathered from HBM, the -A entry
    across the window's doublings), and the 16 radix-2^16 digits of s' as one
    base-point add per even window from [0..32768]B (digits 0-7) and
@@ -755,6 +760,9 @@ fd_tableh_kernel( u32 nsig, u32 sg, i8 const * __restrict__ code, uint4 const * 
 /* FD_DSMH_MINW: waves per SIMD asked of the compiler (3: <= 168 VGPRs) */
 #ifndef FD_DSMH_MINW
 #define FD_DSMH_MINW 3
+#endif
+#ifndef FD_DSMH_RPRE
+#define FD_DSMH_RPRE 0       /* 1: the -R gather also in flight across the doublings (more VGPRs) */
 #endif
 #ifndef FD_DSMH_RLATE
 #define FD_DSMH_RLATE 0      /* 1: issue the -R gather after the -A add (fewer VGPRs live across it) */
@@ -774,7 +782,8 @@ fd_dsmh_kernel( u32                      nsig,
                 u32 const *   __restrict__ slow,
                 u32 const *   __restrict__ slow_cnt,
                 u32                        nslowblk,
-                unsigned char const * __restrict__ pstat ) {
+                unsigned char const * __restrict__ pstat,
+                unsigned char const * __restrict__ htop ) {
   size_t n = nsig;
   if( blockIdx.x < nslowblk ) {
     /* the first blocks take the head of the slow list (full 253-bit walk,
@@ -785,19 +794,27 @@ fd_dsmh_kernel( u32                      nsig,
     return;
   }
   u32 s = ( blockIdx.x - nslowblk ) * FD_WG + threadIdx.x;
-  if( s >= nsig ) return;
   /* a slow-list signature's code may already be final (SUCCESS) when this
      block starts: the flag, not the code, keeps it out */
-  if( code[s] != FD_ED25519_SUCCESS || ( pstat[2*s] & FD_PSTAT_SLOW ) ) return;
+  int pend = s < nsig && code[s] == FD_ED25519_SUCCESS && !( pstat[2*s] & FD_PSTAT_SLOW );
+  /* the walk starts at the wave's highest nonzero window (32 unless a lane's
+     scalar exceeds 2^131): every lane of the wave is still here */
+  int wtop = pend ? (int)htop[s] : 0;
+#pragma unroll
+  for( int o=32; o>0; o>>=1 ) { int v = __shfl_xor( wtop, o, 64 ); wtop = v > wtop ? v : wtop; }
+  if( !pend ) return;
   ge_p3 P; ge_p3_identity( P );
   ge_p2 P2;
   atab_raw ra, rr;
-  int da = digA[ (size_t)(FD_HDIG-1)*n + s ], dr = digR[ (size_t)(FD_HDIG-1)*n + s ];
+  int da = digA[ (size_t)wtop*n + s ], dr = digR[ (size_t)wtop*n + s ];
 #pragma unroll 1
-  for( int w=FD_HDIG-1; w>=0; w-- ) {
+  for( int w=wtop; w>=0; w-- ) {
     atab_fetch( ra, tabA, s, da < 0 ? -da : da );    /* in flight during the doublings */
+#if FD_DSMH_RPRE
+    atab_fetch( rr, tabR, s, dr < 0 ? -dr : dr );
+#endif
     ge_p1p1 t;
-    if( w != FD_HDIG-1 ) {
+    if( w != wtop ) {
 #pragma unroll 1
       for( int r=0; r<3; r++ ) { ge_dbl<FM>( t, P2 ); ge_p1p1_to_p2<FM>( P2, t ); }
       ge_dbl<FM>( t, P2 ); ge_p1p1_to_p3<FM>( P, t );
@@ -805,7 +822,12 @@ fd_dsmh_kernel( u32                      nsig,
     /* the -R entry and the base-point entries are issued after the
        doublings (in flight during the -A add): prefetching all of them
        across the doublings costs 206 VGPRs, 2 waves per SIMD */
-#if FD_DSMH_RLATE
+#if FD_DSMH_RPRE
+    {
+      ge_cached q; atab_unpack( q, ra ); ge_cached_cneg( q, da < 0 );
+      ge_add_cached<FM>( t, P, q ); ge_p1p1_to_p3<FM>( P, t );
+    }
+#elif FD_DSMH_RLATE
     {
       ge_cached q; atab_unpack( q, ra ); ge_cached_cneg( q, da < 0 );
       ge_add_cached<FM>( t, P, q );
@@ -1646,6 +1668,7 @@ struct fdgpu_ed25519_ctx {
   u32     half_force_slow;       /* tests: signatures with s % m == 0 take the full walk (env FDGPU_HALF_FORCE_SLOW) */
   uint4 * d_tabR;                /* half-size path: [0..8](-R), layout of d_tab */
   i8 *    d_digR;                /*                 signed radix-16 digits of c1, [FD_HDIG][max_sig] */
+  unsigned char * d_htop;        /*                 highest nonzero window of c0 / c1, [max_sig] */
   uint4 * d_btab2;               /*                 [0..32768](2^120 B) */
   uint4 * d_khash;               /* NULL, or (drop-in, long messages) SHA-512(R||A||M) per signature, computed beforehand */
   hipEvent_t ev[4];
@@ -1727,7 +1750,8 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
                           ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy );
       hipLaunchKernelGGL( fd_hashh_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
                           ctx->semantics, ctx->d_pstat, code, ctx->d_digA, ctx->d_digR, ctx->d_digB, ctx->d_slow,
-                          ctx->d_slow + ctx->max_sig, (uint4 const *)ctx->d_khash, ctx->half_force_slow );
+                          ctx->d_slow + ctx->max_sig, (uint4 const *)ctx->d_khash, ctx->half_force_slow,
+                          ctx->d_htop );
       hipLaunchKernelGGL( fd_tableh_kernel, dim3(2*sg), dim3(FD_WG), 0, st, nsig, (u32)sg, code, ctx->d_Axy, ctx->d_Rxy,
                           ctx->d_tab, ctx->d_tabR );
     } else {
@@ -1755,14 +1779,14 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       if( nsig <= ctx->nofold_max ) {
         hipLaunchKernelGGL( fd_dsmh_kernel<0>, dim3(nsb + sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
                             ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->d_Rxy, ctx->d_slow, slow_cnt, nsb,
-                            ctx->d_pstat );
+                            ctx->d_pstat, ctx->d_htop );
         if( ctx->timing ) hipEventRecord( ev[2], st );
         hipLaunchKernelGGL( fd_dsm_slow_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy, ctx->d_digA,
                             ctx->d_digB, ctx->d_btab, code, ctx->d_slow, slow_cnt, nsb * FD_WG );
       } else {
         hipLaunchKernelGGL( fd_dsmh_kernel<1>, dim3(nsb + sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
                             ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->d_Rxy, ctx->d_slow, slow_cnt, nsb,
-                            ctx->d_pstat );
+                            ctx->d_pstat, ctx->d_htop );
         if( ctx->timing ) hipEventRecord( ev[2], st );
         hipLaunchKernelGGL( fd_dsm_slow_kernel<1>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy, ctx->d_digA,
                             ctx->d_digB, ctx->d_btab, code, ctx->d_slow, slow_cnt, nsb * FD_WG );
@@ -1843,6 +1867,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   if( ctx->half ) {
     HIPCHK( hipMalloc( &ctx->d_tabR, ns * FD_ATAB_ENTRIES * 8 * sizeof(uint4) ), -1 );
     HIPCHK( hipMalloc( &ctx->d_digR, ns * FD_HDIG ), -1 );
+    HIPCHK( hipMalloc( &ctx->d_htop, ns ), -1 );
     HIPCHK( hipMalloc( &ctx->d_btab2, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), -1 );
   }
   { char const * e = getenv( "FDGPU_SMALL_BATCH_MAX" );   /* A/B knob: signatures at or below take the latency path */
@@ -1895,7 +1920,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   (void)hipFree( ctx->d_map ); (void)hipFree( ctx->d_code ); (void)hipFree( ctx->d_pstat ); (void)hipFree( ctx->d_tab );
   (void)hipFree( ctx->d_Rxy ); (void)hipFree( ctx->d_Axy ); (void)hipFree( ctx->d_digA ); (void)hipFree( ctx->d_digB );
   (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_rdesc ); (void)hipFree( ctx->d_pflag );
-  (void)hipFree( ctx->d_tabR ); (void)hipFree( ctx->d_digR ); (void)hipFree( ctx->d_btab2 );
+  (void)hipFree( ctx->d_tabR ); (void)hipFree( ctx->d_digR ); (void)hipFree( ctx->d_htop ); (void)hipFree( ctx->d_btab2 );
   (void)hipFree( ctx->d_P ); (void)hipFree( ctx->d_O ); (void)hipFree( ctx->d_blk ); (void)hipFree( ctx->d_slow );
   for( int i=0; i<4; i++ ) if( ctx->ev[i] ) (void)hipEventDestroy( ctx->ev[i] );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) if( ctx->ring[r][i] ) (void)hipEventDestroy( ctx->ring[r][i] );

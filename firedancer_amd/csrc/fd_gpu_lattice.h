@@ -11,7 +11,7 @@
    EdDSA signature verification") rewrites that check with two ~128-bit
    scalars, so the double-and-add walk needs 128 doublings instead of 252:
 
-     find c0, c1 with c0 == c1 k (mod 8 l), c1 odd, |c0|, |c1| < 2^131
+     find c0, c1 with c0 == c1 k (mod 8 l), c1 odd, |c0|, |c1| ~ 2^128
      Q = [c1 S mod l]B + [c0](-A) + [c1](-R)
 
    Then Q = [c1] D exactly:
@@ -29,8 +29,11 @@
    |t| <= 8l / r_prev < 2^127).  Every step is an integer row operation on
    the two lattice vectors, so c0 == c1 k (mod 8l) holds whatever the
    approximations decide; the caller re-checks the congruence anyway
-   (mod 8 and, with sc_reduce, mod l) and sends a signature whose
-   reduction fails any bound to the full 253-bit walk.
+   (mod 8 and, with sc_reduce, mod l).  For random k the pair fits 131
+   bits in 99.8 % of cases and ~140 in the rest (no short vector with c1
+   odd); the walk's length follows the largest scalar of each wave.  A
+   signature whose reduction fails a bound (not seen for hash-distributed
+   k; k = l - 1 is one) takes the full 253-bit walk.
 
    Each outer iteration takes the top 64 bits of both remainders and runs
    binary Euclid steps on them (a -= b << s), accumulating the 2x2
@@ -50,7 +53,7 @@
 
 #define FD_LAT_MAXIT  10      /* outer iterations (5 for all but rare k) */
 #define FD_LAT_MAXIN  64      /* 64-bit steps per outer iteration */
-#define FD_LAT_BITS   131     /* |c0|, |c1| < 2^131: 33 signed radix-16 digits */
+#define FD_LAT_BITS   159     /* |c0|, |c1| < 2^159 (40 signed radix-16 digits); typically < 2^131 */
 
 /* 8 l, little-endian words */
 #define FD_LAT_N8L { 0xe7ae9f68u, 0xc09318d2u, 0x17bce6b2u, 0xa6f7cef5u, 0u, 0u, 0u, 0x80000000u }

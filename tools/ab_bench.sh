@@ -1,0 +1,15 @@
+#!/bin/bash
+# Interleaved A/B of engine builds on the headline bench (HBM-resident configs[1]):
+# tools/ab_bench.sh <reps> <name=lib-or-env>...   e.g. base= v1=build/ab/v1.so full=FDGPU_HALF=0
+# Each run prints one line: name value dsm prep.
+reps="$1"; shift
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+B="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
+for r in $(seq "$reps"); do
+  for spec in "$@"; do
+    name="${spec%%=*}"; val="${spec#*=}"
+    if [[ "$val" == *.so ]]; then envs="FDGPU_LIB=$val"; else envs="$val"; fi
+    out=$(env $envs timeout -k 10 120 $B 2>/dev/null | tail -1)
+    python3 -c "import json,sys; d=json.loads(sys.argv[2]); k=d['kernel_ms']; print(sys.argv[1], round(d['value']/1e6,2), round(k['dsm'],3), round(k['prep'],3), d['results_ok'])" "$name" "$out" || echo "$name failed"
+  done
+done
