@@ -377,6 +377,15 @@ FD_DEV void hs_store_digits( u32 const c0[ 5 ], u32 const c1m[ 5 ], int c1neg, u
   }
 }
 
+/* The wave's top window (half-size walks): the largest htop of its pending
+   signatures, every lane of the wave still active */
+FD_DEV int hs_wave_top( int pend, unsigned char const * __restrict__ htop, u32 s ) {
+  int wtop = pend ? (int)htop[s] : 0;
+#pragma unroll
+  for( int o=32; o>0; o>>=1 ) { int v = __shfl_xor( wtop, o, 64 ); wtop = v > wtop ? v : wtop; }
+  return wtop;
+}
+
 /* The result-code procedure of fd_ed25519_verify (fd_ed25519_user.c:
    174-199) from S's check (code so far: SUCCESS or
    ERR_SIG) and the point statuses pa (A) and pr (R).  defer: R has not
@@ -479,6 +488,46 @@ fd_hash_kernel( unsigned char const *    __restrict__ payload,
    mod l, the reduction to (c0, c1) and s' = c1 S mod l, stored as digits.
    A signature without a short pair keeps the digits of k and S and goes
    on the slow list (FD_PEND_SLOW). */
+/* rc = 1 (throughput, after both decodes): the full result-code procedure
+   first, and a slow signature is flagged in pstat; rc = 0 (fd_prep_kernel,
+   beside the decodes): S's check only -- the DSM applies the rest. */
+FD_DEV void hashh_one( unsigned char const * __restrict__ payload, fdgpu_txn_desc_t const * __restrict__ desc,
+                       u32 const * __restrict__ map, u32 s, size_t n, int semantics, int rc,
+                       unsigned char * __restrict__ pstat, i8 * __restrict__ code_out, i8 * __restrict__ digA,
+                       i8 * __restrict__ digR, short * __restrict__ digB, u32 * __restrict__ slow,
+                       u32 * __restrict__ slow_cnt, uint4 const * __restrict__ khash, u32 force_slow,
+                       unsigned char * __restrict__ htop ) {
+  u32 m = map[s];
+  u32 t = m & 0xffffffu, j = m >> 24;
+  fdgpu_txn_desc_t d = desc[t];
+  if( !txn_desc_ok( d ) ) { code_out[s] = FD_ED25519_ERR_SIG; return; }
+  unsigned char const * base = payload + d.payload_off;
+  u32 Sw[8];
+  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
+  int code = sc_is_canonical( Sw ) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_SIG;
+  if( rc ) code = result_code( code, pstat[2*s], pstat[2*s+1], semantics, 0 );
+  if( code != FD_ED25519_SUCCESS ) { code_out[s] = (i8)code; return; }
+  u32 Rw[8], Aw[8];
+  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
+  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
+  u32 h[16], k[8];
+  if( khash ) {
+#pragma unroll
+    for( int i=0; i<4; i++ ) { uint4 v = khash[4*(size_t)s + i]; h[4*i] = v.x; h[4*i+1] = v.y; h[4*i+2] = v.z; h[4*i+3] = v.w; }
+  } else fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
+  sc_reduce( k, h );
+  u32 c0[5], c1m[5], sp[8]; int c1neg = 0;
+  if( !( force_slow && s % force_slow == 0u ) && hs_prepare( k, Sw, c0, c1m, c1neg, sp ) ) {
+    hs_store_digits( c0, c1m, c1neg, sp, s, n, digA, digR, digB, htop );
+    code_out[s] = FD_ED25519_SUCCESS;
+  } else {
+    store_digits( k, Sw, s, n, digA, digB );
+    code_out[s] = FD_PEND_SLOW;
+    if( rc ) pstat[2*s] |= FD_PSTAT_SLOW;          /* fd_dsmh_kernel's half-size blocks skip it even once its code is final */
+    slow[ atomicAdd( slow_cnt, 1u ) ] = s;
+  }
+}
+
 __global__ void __launch_bounds__( FD_WG )
 fd_hashh_kernel( unsigned char const *    __restrict__ payload,
                  fdgpu_txn_desc_t const * __restrict__ desc,
@@ -497,36 +546,8 @@ fd_hashh_kernel( unsigned char const *    __restrict__ payload,
                  unsigned char *          __restrict__ htop ) {
   u32 s = blockIdx.x * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
-  u32 m = map[s];
-  u32 t = m & 0xffffffu, j = m >> 24;
-  fdgpu_txn_desc_t d = desc[t];
-  if( !txn_desc_ok( d ) ) { code_out[s] = FD_ED25519_ERR_SIG; return; }
-  unsigned char const * base = payload + d.payload_off;
-  u32 Sw[8];
-  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
-  int code = sc_is_canonical( Sw ) ? FD_ED25519_SUCCESS : FD_ED25519_ERR_SIG;
-  code = result_code( code, pstat[2*s], pstat[2*s+1], semantics, 0 );
-  if( code != FD_ED25519_SUCCESS ) { code_out[s] = (i8)code; return; }
-  u32 Rw[8], Aw[8];
-  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
-  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
-  u32 h[16], k[8];
-  if( khash ) {
-#pragma unroll
-    for( int i=0; i<4; i++ ) { uint4 v = khash[4*(size_t)s + i]; h[4*i] = v.x; h[4*i+1] = v.y; h[4*i+2] = v.z; h[4*i+3] = v.w; }
-  } else fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
-  sc_reduce( k, h );
-  size_t n = nsig;
-  u32 c0[5], c1m[5], sp[8]; int c1neg = 0;
-  if( !( force_slow && s % force_slow == 0u ) && hs_prepare( k, Sw, c0, c1m, c1neg, sp ) ) {
-    hs_store_digits( c0, c1m, c1neg, sp, s, n, digA, digR, digB, htop );
-    code_out[s] = FD_ED25519_SUCCESS;
-  } else {
-    store_digits( k, Sw, s, n, digA, digB );
-    code_out[s] = FD_PEND_SLOW;
-    pstat[2*s] |= FD_PSTAT_SLOW;       /* fd_dsmh_kernel's half-size blocks skip it even once its code is final */
-    slow[ atomicAdd( slow_cnt, 1u ) ] = s;
-  }
+  hashh_one( payload, desc, map, s, nsig, semantics, 1, pstat, code_out, digA, digR, digB, slow, slow_cnt, khash,
+             force_slow, htop );
 }
 
 /* Small batches (latency): the three independent parts of the prep in
@@ -534,7 +555,7 @@ fd_hashh_kernel( unsigned char const *    __restrict__ payload,
    check S and hash -- so a batch that cannot fill the GPU pays the
    longest of them instead of their sum.  Every block has one role, so
    no wave diverges. */
-template<int FM>
+template<int FM, int HS>
 __global__ void __launch_bounds__( FD_WG )
 fd_prep_kernel( unsigned char const *    __restrict__ payload,
                 fdgpu_txn_desc_t const * __restrict__ desc,
@@ -549,16 +570,26 @@ fd_prep_kernel( unsigned char const *    __restrict__ payload,
                 i8 *                     __restrict__ digA,
                 short *                  __restrict__ digB,
                 uint4 *                  __restrict__ tab,
-                uint4 const *            __restrict__ khash ) {
+                uint4 const *            __restrict__ khash,
+                uint4 *                  __restrict__ tabR,
+                i8 *                     __restrict__ digR,
+                u32 *                    __restrict__ slow,
+                u32 *                    __restrict__ slow_cnt,
+                u32                                   force_slow,
+                unsigned char *          __restrict__ htop ) {
   u32 role = blockIdx.x / sg, b = blockIdx.x - role*sg;
   u32 s = b * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
   if( role < 2u ) {
     decode_one<FM>( payload, desc, map, s, role, pstat, Rxy, Axy );
     /* tab != NULL: the A lane goes on to the -A table (for every A that
-       decoded; fd_dsm2_kernel applies the result-code procedure) */
+       decoded; fd_dsm2_kernel applies the result-code procedure); HS: the R
+       lane to the -R table */
     if( tab && role==0u && ( pstat[2u*s] & 3u )==0u ) atab_build<FM>( tab, s, Axy );
+    if( HS && role==1u && ( pstat[2u*s+1u] & 3u )==0u ) atab_build<FM>( tabR, s, Rxy );
   }
+  else if( HS ) hashh_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digR, digB, slow, slow_cnt,
+                           khash, force_slow, htop );
   else hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rxy, khash );
 }
 
@@ -736,6 +767,23 @@ fd_dsm_slow_kernel( u32 nsig, uint4 const * __restrict__ tab, uint4 const * __re
   if( i < *slow_cnt ) dsm_one<FM>( slow[i], nsig, tab, Rxy, digA, digB, btab, code, (u32 *)0, 0 );
 }
 
+/* Latency half-size path: the slow list after the walks, the result-code
+   procedure first (fd_prep_kernel ran it beside the decodes: S only). */
+template<int FM>
+__global__ void __launch_bounds__( FD_WG )
+fd_dsm_slowl_kernel( u32 nsig, uint4 const * __restrict__ tab, uint4 const * __restrict__ Rxy,
+                     i8 const * __restrict__ digA, short const * __restrict__ digB, uint4 const * __restrict__ btab,
+                     i8 * __restrict__ code, u32 const * __restrict__ slow, u32 const * __restrict__ slow_cnt,
+                     int semantics, unsigned char const * __restrict__ pstat ) {
+  u32 i = blockIdx.x * FD_WG + threadIdx.x;
+  if( i >= *slow_cnt ) return;
+  u32 s = slow[i];
+  if( code[s] != FD_PEND_SLOW ) return;
+  int c = result_code( FD_ED25519_SUCCESS, pstat[2*s], pstat[2*s+1], semantics, 0 );
+  if( c != FD_ED25519_SUCCESS ) { code[s] = (i8)c; return; }
+  dsm_one<FM>( s, nsig, tab, Rxy, digA, digB, btab, code, (u32 *)0, 0 );
+}
+
 /* Half-size path tables: blocks [0,sg) build [0..8](-A) for every pending
    signature (also the slow ones), blocks [sg,2sg) [0..8](-R) for the
    half-size ones. */
@@ -783,7 +831,9 @@ fd_dsmh_kernel( u32                      nsig,
                 u32 const *   __restrict__ slow_cnt,
                 u32                        nslowblk,
                 unsigned char const * __restrict__ pstat,
-                unsigned char const * __restrict__ htop ) {
+                unsigned char const * __restrict__ htop,
+                int                        rc,
+                int                        semantics ) {
   size_t n = nsig;
   if( blockIdx.x < nslowblk ) {
     /* the first blocks take the head of the slow list (full 253-bit walk,
@@ -796,13 +846,15 @@ fd_dsmh_kernel( u32                      nsig,
   u32 s = ( blockIdx.x - nslowblk ) * FD_WG + threadIdx.x;
   /* a slow-list signature's code may already be final (SUCCESS) when this
      block starts: the flag, not the code, keeps it out */
-  int pend = s < nsig && code[s] == FD_ED25519_SUCCESS && !( pstat[2*s] & FD_PSTAT_SLOW );
+  /* rc (latency path, after fd_prep_kernel): the result-code procedure
+     here; slow signatures (FD_PEND_SLOW) are left to fd_dsm_slowl_kernel */
+  int c = s < nsig ? (int)code[s] : FD_ED25519_ERR_SIG;
+  if( rc && s < nsig ) c = result_code( c, pstat[2*s], pstat[2*s+1], semantics, 0 );
+  int pend = c == FD_ED25519_SUCCESS && !( pstat[2*s] & FD_PSTAT_SLOW );
   /* the walk starts at the wave's highest nonzero window (32 unless a lane's
      scalar exceeds 2^131): every lane of the wave is still here */
-  int wtop = pend ? (int)htop[s] : 0;
-#pragma unroll
-  for( int o=32; o>0; o>>=1 ) { int v = __shfl_xor( wtop, o, 64 ); wtop = v > wtop ? v : wtop; }
-  if( !pend ) return;
+  int wtop = hs_wave_top( pend, htop, s );
+  if( !pend ) { if( rc && s < nsig && c != FD_PEND_SLOW ) code[s] = (i8)c; return; }
   ge_p3 P; ge_p3_identity( P );
   ge_p2 P2;
   atab_raw ra, rr;
@@ -1030,7 +1082,12 @@ FD_DEV void pair_add( fe & E, fe & F, fe & G, fe & H, int h, fe const & m0, fe c
   fe_sub4( F, D, C ); fe_wcarry( F, F );             /* F = D-C (T) */
 }
 
-template<int FM>
+/* HS = 0: [k](-A) + [S]B over 64 windows, compared with R; HS = 1: the
+   half-size walk (fd_gpu_lattice.h) Q = [s']B + [c0](-A) + [c1](-R) from
+   the wave's top window, -A and -R added in every window, one base-point
+   entry per even window ([0..32768]B / 2^120 B), Q == O at the end.
+   Signatures on the slow list (FD_PEND_SLOW) are left to fd_dsm_slowl_kernel. */
+template<int FM, int HS>
 __global__ void __launch_bounds__( FD_WG )
 fd_dsm2_kernel( u32                      nsig,
                 uint4 const * __restrict__ tab,
@@ -1040,13 +1097,22 @@ fd_dsm2_kernel( u32                      nsig,
                 uint4 const * __restrict__ btab_g,
                 i8 *          __restrict__ code,
                 int                        semantics,
-                unsigned char const * __restrict__ pstat ) {
+                unsigned char const * __restrict__ pstat,
+                uint4 const * __restrict__ tabR,
+                i8 const *    __restrict__ digR,
+                uint4 const * __restrict__ btab2,
+                unsigned char const * __restrict__ htop ) {
   u32 gl = blockIdx.x * FD_WG + threadIdx.x;
   u32 s = gl >> 1;
   int h = (int)( gl & 1u );
-  if( s >= nsig ) return;                            /* both lanes of a pair leave together */
-  {                                                  /* fd_prep_kernel left S's check only */
-    int c = result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 );
+  int wtop = 63;
+  if( HS ) {
+    int c = s < nsig ? result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 ) : FD_ED25519_ERR_SIG;
+    wtop = hs_wave_top( c == FD_ED25519_SUCCESS, htop, s );
+    if( c != FD_ED25519_SUCCESS ) { if( s < nsig && !h && c != FD_PEND_SLOW ) code[s] = (i8)c; return; }
+  } else {
+    if( s >= nsig ) return;                          /* both lanes of a pair leave together */
+    int c = result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 );   /* fd_prep_kernel left S's check only */
     if( c != FD_ED25519_SUCCESS ) { if( !h ) code[s] = (i8)c; return; }
   }
   size_t n = nsig;
@@ -1055,11 +1121,11 @@ fd_dsm2_kernel( u32                      nsig,
   fe one = fe_one(), zero = fe_zero();
   fe_sel( m0, h, one, zero );                        /* identity: lane 0 X=0, T=0; lane 1 Y=1, Z=1 */
   m1 = m0;
-  int da = digA[ (size_t)63*n + s ];
-  uint4 araw[4], braw[4];
+  int da = digA[ (size_t)wtop*n + s ], dr = HS ? digR[ (size_t)wtop*n + s ] : 0;
+  uint4 araw[4], rraw[4], braw[4];
   int db = 0;
 #pragma unroll 1
-  for( int w=63; w>=0; w-- ) {
+  for( int w=wtop; w>=0; w-- ) {
     {                                                /* this lane's two coordinates of the -A entry */
       int neg = da < 0, e = neg ? -da : da;
       uint4 const * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8;
@@ -1067,15 +1133,22 @@ fd_dsm2_kernel( u32                      nsig,
       int c1 = h ? 2 : 3;                            /* lane 0 T2d, lane 1 Z */
       araw[0] = b[2*c0]; araw[1] = b[2*c0+1]; araw[2] = b[2*c1]; araw[3] = b[2*c1+1];
     }
-    if( !(w & 3) ) {
-      db = digB[ (size_t)(w>>2)*n + s ];
+    if( HS ) {                                       /* and of the -R entry */
+      int neg = dr < 0, e = neg ? -dr : dr;
+      uint4 const * b = tabR + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8;
+      int c0 = h ^ neg, c1 = h ? 2 : 3;
+      rraw[0] = b[2*c0]; rraw[1] = b[2*c0+1]; rraw[2] = b[2*c1]; rraw[3] = b[2*c1+1];
+    }
+    int bw = HS ? ( !(w & 1) && w < 32 ) : !(w & 3);
+    if( bw ) {
+      db = HS ? digB[ (size_t)( (w>>2) + ( (w & 2) ? 8 : 0 ) )*n + s ] : digB[ (size_t)(w>>2)*n + s ];
       int neg = db < 0, e = neg ? -db : db;
-      uint4 const * b = btab_g + (size_t)e*6;
+      uint4 const * b = ( HS && (w & 2) ? btab2 : btab_g ) + (size_t)e*6;
       int c0 = h ^ neg;                              /* 0 ypx, 1 ymx */
       braw[0] = b[2*c0]; braw[1] = b[2*c0+1];
       if( !h ) { braw[2] = b[4]; braw[3] = b[5]; }   /* lane 0 xy2d; lane 1 Z2 = 1 */
     }
-    if( w != 63 ) {
+    if( w != wtop ) {
 #pragma unroll 1
       for( int r=0; r<4; r++ ) { pair_dbl<FM>( E, F, G, H, h, m0, m1 ); pair_mstep<FM>( m0, m1, h, E, F, G, H ); }
     }
@@ -1084,7 +1157,14 @@ fd_dsm2_kernel( u32                      nsig,
     { fe nq; fe_neg( nq, q1 ); fe_sel( q1, !h && da < 0, nq, q1 ); }
     pair_add<FM>( E, F, G, H, h, m0, m1, q0, q1 );
     pair_mstep<FM>( m0, m1, h, E, F, G, H );
-    if( !(w & 3) ) {
+    if( HS ) {
+      fe_from_quads( q0, rraw[0], rraw[1] );
+      fe_from_quads( q1, rraw[2], rraw[3] );
+      { fe nq; fe_neg( nq, q1 ); fe_sel( q1, !h && dr < 0, nq, q1 ); }
+      pair_add<FM>( E, F, G, H, h, m0, m1, q0, q1 );
+      pair_mstep<FM>( m0, m1, h, E, F, G, H );
+    }
+    if( bw ) {
       fe_from_quads( q0, braw[0], braw[1] );
       if( h ) q1 = one;
       else {
@@ -1094,7 +1174,14 @@ fd_dsm2_kernel( u32                      nsig,
       pair_add<FM>( E, F, G, H, h, m0, m1, q0, q1 );
       pair_mstep<FM>( m0, m1, h, E, F, G, H );
     }
-    if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
+    if( w > 0 ) { da = digA[ (size_t)(w-1)*n + s ]; if( HS ) dr = digR[ (size_t)(w-1)*n + s ]; }
+  }
+  if( HS ) {
+    /* Q == O: lane 0 X == 0 (m0 = X), lane 1 Y == Z (m0 = Y, m1 = Z) */
+    u32 ok = h ? (u32)fe_eq( m0, m1 ) : (u32)fe_is_zero( m0 );
+    ok &= fd_pair_xchg( ok );
+    if( !h ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+    return;
   }
   /* fd_ed25519_point_eq_z1: lane 0 X == x_R Z, lane 1 Y == y_R Z */
   fe z, r, u;
@@ -1193,7 +1280,7 @@ FD_DEV void quad_add( fe & E, fe & F, fe & G, fe & H, int q, fe const & m, fe co
 #endif
 }
 
-template<int FM>
+template<int FM, int HS>
 __global__ void __launch_bounds__( FD_WG )
 fd_dsm4_kernel( u32                      nsig,
                 uint4 const * __restrict__ tab,
@@ -1203,38 +1290,54 @@ fd_dsm4_kernel( u32                      nsig,
                 uint4 const * __restrict__ btab_g,
                 i8 *          __restrict__ code,
                 int                        semantics,
-                unsigned char const * __restrict__ pstat ) {
+                unsigned char const * __restrict__ pstat,
+                uint4 const * __restrict__ tabR,
+                i8 const *    __restrict__ digR,
+                uint4 const * __restrict__ btab2,
+                unsigned char const * __restrict__ htop ) {
   u32 gl = blockIdx.x * FD_WG + threadIdx.x;
   u32 s = gl >> 2;
   int q = (int)( gl & 3u );
-  if( s >= nsig ) return;                            /* the four lanes of a quad leave together */
-  {                                                  /* fd_prep_kernel left S's check only */
-    int c = result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 );
+  int wtop = 63;
+  if( HS ) {                                         /* (fd_dsm2_kernel's HS = 1 walk, four lanes) */
+    int c = s < nsig ? result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 ) : FD_ED25519_ERR_SIG;
+    wtop = hs_wave_top( c == FD_ED25519_SUCCESS, htop, s );
+    if( c != FD_ED25519_SUCCESS ) { if( s < nsig && !q && c != FD_PEND_SLOW ) code[s] = (i8)c; return; }
+  } else {
+    if( s >= nsig ) return;                          /* the four lanes of a quad leave together */
+    int c = result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 );   /* fd_prep_kernel left S's check only */
     if( c != FD_ED25519_SUCCESS ) { if( !q ) code[s] = (i8)c; return; }
   }
   size_t n = nsig;
   fe m, E, F, G, H, c;
   fe one = fe_one(), zero = fe_zero();
   fe_sel( m, q==1 || q==2, one, zero );              /* identity (0 : 1 : 1 : 0) */
-  int da = digA[ (size_t)63*n + s ];
-  uint4 araw[2], braw[2];
+  int da = digA[ (size_t)wtop*n + s ], dr = HS ? digR[ (size_t)wtop*n + s ] : 0;
+  uint4 araw[2], rraw[2], braw[2];
   int db = 0;
 #pragma unroll 1
-  for( int w=63; w>=0; w-- ) {
+  for( int w=wtop; w>=0; w-- ) {
     {                                                /* this lane's coordinate of the -A entry */
       int neg = da < 0, e = neg ? -da : da;
       int ci = q < 2 ? ( q ^ neg ) : ( q==2 ? 3 : 2 );   /* YpX / YmX (swapped when negated), T2d, Z */
       uint4 const * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8 + 2*ci;
       araw[0] = b[0]; araw[1] = b[1];
     }
-    if( !(w & 3) ) {
-      db = digB[ (size_t)(w>>2)*n + s ];
+    if( HS ) {                                       /* and of the -R entry */
+      int neg = dr < 0, e = neg ? -dr : dr;
+      int ci = q < 2 ? ( q ^ neg ) : ( q==2 ? 3 : 2 );
+      uint4 const * b = tabR + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8 + 2*ci;
+      rraw[0] = b[0]; rraw[1] = b[1];
+    }
+    int bw = HS ? ( !(w & 1) && w < 32 ) : !(w & 3);
+    if( bw ) {
+      db = HS ? digB[ (size_t)( (w>>2) + ( (w & 2) ? 8 : 0 ) )*n + s ] : digB[ (size_t)(w>>2)*n + s ];
       int neg = db < 0, e = neg ? -db : db;
       int ci = q < 2 ? ( q ^ neg ) : 2;              /* ypx / ymx, xy2d; lane 3: Z2 = 1 */
-      uint4 const * b = btab_g + (size_t)e*6 + 2*ci;
+      uint4 const * b = ( HS && (w & 2) ? btab2 : btab_g ) + (size_t)e*6 + 2*ci;
       if( q < 3 ) { braw[0] = b[0]; braw[1] = b[1]; }
     }
-    if( w != 63 ) {
+    if( w != wtop ) {
 #pragma unroll 1
       for( int r=0; r<4; r++ ) { quad_dbl<FM>( E, F, G, H, q, m ); quad_mstep<FM>( m, q, E, F, G, H ); }
     }
@@ -1242,7 +1345,13 @@ fd_dsm4_kernel( u32                      nsig,
     { fe nc; fe_neg( nc, c ); fe_sel( c, q==2 && da < 0, nc, c ); }
     quad_add<FM>( E, F, G, H, q, m, c );
     quad_mstep<FM>( m, q, E, F, G, H );
-    if( !(w & 3) ) {
+    if( HS ) {
+      fe_from_quads( c, rraw[0], rraw[1] );
+      { fe nc; fe_neg( nc, c ); fe_sel( c, q==2 && dr < 0, nc, c ); }
+      quad_add<FM>( E, F, G, H, q, m, c );
+      quad_mstep<FM>( m, q, E, F, G, H );
+    }
+    if( bw ) {
       if( q == 3 ) c = one;
       else {
         fe_from_quads( c, braw[0], braw[1] );
@@ -1251,7 +1360,15 @@ fd_dsm4_kernel( u32                      nsig,
       quad_add<FM>( E, F, G, H, q, m, c );
       quad_mstep<FM>( m, q, E, F, G, H );
     }
-    if( w > 0 ) da = digA[ (size_t)(w-1)*n + s ];
+    if( w > 0 ) { da = digA[ (size_t)(w-1)*n + s ]; if( HS ) dr = digR[ (size_t)(w-1)*n + s ]; }
+  }
+  if( HS ) {
+    /* Q == O: lane 0 X == 0, lane 1 Y == Z (Z from lane 2) */
+    fe z; fe_bcast2( z, m );
+    u32 ok = q==0 ? (u32)fe_is_zero( m ) : ( q==1 ? (u32)fe_eq( m, z ) : 1u );
+    ok = fd_bcast0( ok ) & fd_bcast1( ok );
+    if( !q ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+    return;
   }
   /* fd_ed25519_point_eq_z1: lane 0 X == x_R Z, lane 1 Y == y_R Z */
   fe z, r, u;
@@ -1729,7 +1846,8 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
        instruction streams -- decode A, decode R and hash side by side in one launch,
        R compared at the end of the DSM (no R-check chain and its inversion) */
     int small = nsig <= ctx->small_max, lanes = 1;
-    int half = ctx->half && !small;
+    int hs = ctx->half && small;               /* half-size scalars on the latency path */
+    int half = ctx->half && !small;            /* ... on the throughput path */
     int defer = FD_DEFER_R && !small && !half;
     if( small ) {
       /* lanes per signature in the DSM: 4 while a quad per signature still fits one wave per
@@ -1737,12 +1855,20 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
          against 0.92 on the throughput path and 1.08 with two lanes, tools/configs0_ab.py) */
       lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM4_MAX ? 4 : nsig <= FD_DSM2_MAX ? 2 : 1 );
       int d2 = lanes > 1;
-      hipLaunchKernelGGL( fd_prep_kernel<0>, dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, (u32)sg,
-                          ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
-                          d2 ? ctx->d_tab : (uint4 *)NULL, (uint4 const *)ctx->d_khash );
-      if( !d2 )
-        hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, ctx->d_pstat, code,
-                            ctx->d_Axy, ctx->d_tab );
+      if( hs )      /* half-size: the A and R lanes build both tables, the hash lane (c0, c1, s') */
+        hipLaunchKernelGGL( (fd_prep_kernel<0,1>), dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+                            (u32)sg, ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
+                            ctx->d_tab, (uint4 const *)ctx->d_khash, ctx->d_tabR, ctx->d_digR, ctx->d_slow,
+                            ctx->d_slow + ctx->max_sig, ctx->half_force_slow, ctx->d_htop );
+      else {
+        hipLaunchKernelGGL( (fd_prep_kernel<0,0>), dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+                            (u32)sg, ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
+                            d2 ? ctx->d_tab : (uint4 *)NULL, (uint4 const *)ctx->d_khash, (uint4 *)NULL, (i8 *)NULL,
+                            (u32 *)NULL, (u32 *)NULL, 0u, (unsigned char *)NULL );
+        if( !d2 )
+          hipLaunchKernelGGL( fd_table_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->semantics, ctx->d_pstat, code,
+                              ctx->d_Axy, ctx->d_tab );
+      }
     } else if( half ) {
       /* half-size scalars: decode A and R, result codes + hash + (c0, c1, s'), both tables */
       unsigned pg = (unsigned)( ( 2UL*sig_cnt + FD_WG - 1) / FD_WG );
@@ -1766,11 +1892,17 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     }
     if( ctx->timing ) hipEventRecord( ev[1], st );
     if( small && lanes==4 )
-      hipLaunchKernelGGL( fd_dsm4_kernel<0>, dim3(4*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
-                          ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat );
+      hipLaunchKernelGGL( (hs ? fd_dsm4_kernel<0,1> : fd_dsm4_kernel<0,0>), dim3(4*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab,
+                          ctx->d_Rxy, ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat,
+                          ctx->d_tabR, ctx->d_digR, ctx->d_btab2, ctx->d_htop );
     else if( small && lanes==2 )
-      hipLaunchKernelGGL( fd_dsm2_kernel<0>, dim3(2*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
-                          ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat );
+      hipLaunchKernelGGL( (hs ? fd_dsm2_kernel<0,1> : fd_dsm2_kernel<0,0>), dim3(2*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab,
+                          ctx->d_Rxy, ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat,
+                          ctx->d_tabR, ctx->d_digR, ctx->d_btab2, ctx->d_htop );
+    else if( hs )                              /* one lane: the half-size walk, result codes at its start */
+      hipLaunchKernelGGL( fd_dsmh_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
+                          ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->d_Rxy, ctx->d_slow,
+                          ctx->d_slow + ctx->max_sig, 0u, ctx->d_pstat, ctx->d_htop, 1, ctx->semantics );
     else if( half ) {
       /* slow list: its head in fd_dsmh_kernel's first nsb blocks (room for 1/64 of the batch), the
          rest (if any) in fd_dsm_slow_kernel */
@@ -1779,14 +1911,14 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       if( nsig <= ctx->nofold_max ) {
         hipLaunchKernelGGL( fd_dsmh_kernel<0>, dim3(nsb + sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
                             ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->d_Rxy, ctx->d_slow, slow_cnt, nsb,
-                            ctx->d_pstat, ctx->d_htop );
+                            ctx->d_pstat, ctx->d_htop, 0, ctx->semantics );
         if( ctx->timing ) hipEventRecord( ev[2], st );
         hipLaunchKernelGGL( fd_dsm_slow_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy, ctx->d_digA,
                             ctx->d_digB, ctx->d_btab, code, ctx->d_slow, slow_cnt, nsb * FD_WG );
       } else {
         hipLaunchKernelGGL( fd_dsmh_kernel<1>, dim3(nsb + sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
                             ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->d_Rxy, ctx->d_slow, slow_cnt, nsb,
-                            ctx->d_pstat, ctx->d_htop );
+                            ctx->d_pstat, ctx->d_htop, 0, ctx->semantics );
         if( ctx->timing ) hipEventRecord( ev[2], st );
         hipLaunchKernelGGL( fd_dsm_slow_kernel<1>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy, ctx->d_digA,
                             ctx->d_digB, ctx->d_btab, code, ctx->d_slow, slow_cnt, nsb * FD_WG );
@@ -1799,6 +1931,10 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       hipLaunchKernelGGL( fd_dsm_kernel<1>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                           ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P, defer );
     if( ctx->timing && !half ) hipEventRecord( ev[2], st );
+    if( hs )                                   /* slow list (normally empty) */
+      hipLaunchKernelGGL( fd_dsm_slowl_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy, ctx->d_digA,
+                          ctx->d_digB, ctx->d_btab, code, ctx->d_slow, ctx->d_slow + ctx->max_sig, ctx->semantics,
+                          ctx->d_pstat );
     if( defer ) {
       u32 * slow_cnt = ctx->d_slow + ctx->max_sig;
       hipLaunchKernelGGL( fd_rprod_kernel, dim3(sg), dim3(FD_WG), 0, st, nsig, code, ctx->d_P, ctx->d_O, ctx->d_blk, slow_cnt );
