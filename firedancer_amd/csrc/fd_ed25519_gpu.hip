@@ -109,6 +109,13 @@
 #define FD_HALF 1
 #endif
 #define FD_HDIG 40                 /* signed radix-16 digits of c0, c1 (< 2^159); the walk stops at the wave's top one */
+/* carry-fold mode (fd_gpu_f25519.h) of the throughput path's decode and table kernels (A/B knobs) */
+#ifndef FD_DECODE_FM
+#define FD_DECODE_FM FD_CARRY_FOLD
+#endif
+#ifndef FD_TABLE_FM
+#define FD_TABLE_FM FD_CARRY_FOLD
+#endif
 #define FD_PSTAT_SLOW 0x80u        /* A-status bit: the signature is on the half-size path's slow list */
 
 typedef signed char i8;
@@ -264,7 +271,7 @@ fd_decode_kernel( unsigned char const *    __restrict__ payload,
   u32 p = blockIdx.x * FD_WG + threadIdx.x;
   if( p >= ( both ? 2u*nsig : nsig ) ) return;
   u32 s = both ? p >> 1 : p, is_r = both ? p & 1u : 0u;
-  decode_one( payload, desc, map, s, is_r, pstat, Rxy, Axy );
+  decode_one<FD_DECODE_FM>( payload, desc, map, s, is_r, pstat, Rxy, Axy );
 }
 
 /* Signed digits of k (radix 16, digA[64][n]) and S (radix 2^FD_BWIN,
@@ -794,8 +801,8 @@ fd_tableh_kernel( u32 nsig, u32 sg, i8 const * __restrict__ code, uint4 const * 
   u32 s = b * FD_WG + threadIdx.x;
   if( s >= nsig ) return;
   int c = code[s];
-  if( !role ) { if( c == FD_ED25519_SUCCESS || c == FD_PEND_SLOW ) atab_build( tabA, s, Axy ); }
-  else if( c == FD_ED25519_SUCCESS ) atab_build( tabR, s, Rxy );
+  if( !role ) { if( c == FD_ED25519_SUCCESS || c == FD_PEND_SLOW ) atab_build<FD_TABLE_FM>( tabA, s, Axy ); }
+  else if( c == FD_ED25519_SUCCESS ) atab_build<FD_TABLE_FM>( tabR, s, Rxy );
 }
 
 /* Half-size DSM: Q = [s']B + [c0](-A) + [c1](-R) by a joint signed
@@ -808,6 +815,9 @@ fd_tableh_kernel( u32 nsig, u32 sg, i8 const * __restrict__ code, uint4 const * 
 /* FD_DSMH_MINW: waves per SIMD asked of the compiler (3: <= 168 VGPRs) */
 #ifndef FD_DSMH_MINW
 #define FD_DSMH_MINW 3
+#endif
+#ifndef FD_DIAG_GATHER
+#define FD_DIAG_GATHER 0
 #endif
 #ifndef FD_DSMH_RPRE
 #define FD_DSMH_RPRE 0       /* 1: the -R gather also in flight across the doublings (more VGPRs) */
@@ -861,7 +871,11 @@ fd_dsmh_kernel( u32                      nsig,
   int da = digA[ (size_t)wtop*n + s ], dr = digR[ (size_t)wtop*n + s ];
 #pragma unroll 1
   for( int w=wtop; w>=0; w-- ) {
+#if FD_DIAG_GATHER                                   /* diagnostic builds only (wrong results): one fixed line per table */
+    atab_fetch( ra, tabA, s, 1 );
+#else
     atab_fetch( ra, tabA, s, da < 0 ? -da : da );    /* in flight during the doublings */
+#endif
 #if FD_DSMH_RPRE
     atab_fetch( rr, tabR, s, dr < 0 ? -dr : dr );
 #endif
@@ -887,7 +901,11 @@ fd_dsmh_kernel( u32                      nsig,
     atab_fetch( rr, tabR, s, dr < 0 ? -dr : dr );   /* in flight during the P3 conversion */
     ge_p1p1_to_p3<FM>( P, t );
 #else
+#if FD_DIAG_GATHER
+    atab_fetch( rr, tabR, s, 1 );
+#else
     atab_fetch( rr, tabR, s, dr < 0 ? -dr : dr );
+#endif
     {
       ge_cached q; atab_unpack( q, ra ); ge_cached_cneg( q, da < 0 );
       ge_add_cached<FM>( t, P, q ); ge_p1p1_to_p3<FM>( P, t );
