@@ -614,9 +614,9 @@ def main():
                          "peak_guide_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T "
                                               "lane-ops/s (157.3 TF FP32 FMA / 2); profiles/r02/ROOFLINE.md",
                          "valu_busy": valu_busy,
-                         "valu_busy_source": "profiles/dsm_pmc.json: issue cycles of fd_dsm_kernel's ISA priced at the "
-                                             "measured per-instruction costs (tools/dsm_issue_model.py, "
-                                             "profiles/r02/roofline/issue_model.json) / measured kernel cycles",
+                         "valu_busy_source": "profiles/dsm_pmc.json: issue cycles of the walk kernel's ISA priced at "
+                                             "the measured per-instruction costs (tools/dsm_issue_model.py, "
+                                             "profiles/r02/roofline/issue_model_dsmh.json) / measured kernel cycles",
                          # the same kernel against the HBM roofline: PMC bytes per launch / this run's launch time
                          "hbm": ({"achieved": traffic * nsig / (1 << 20) / (dom_ms * 1e-3) / 1e9, "peak": 8000.0,
                                   "unit": "GB/s",

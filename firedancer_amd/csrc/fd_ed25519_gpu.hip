@@ -865,6 +865,7 @@ fd_dsmh_kernel( u32                      nsig,
      scalar exceeds 2^131): every lane of the wave is still here */
   int wtop = hs_wave_top( pend, htop, s );
   if( !pend ) { if( rc && s < nsig && c != FD_PEND_SLOW ) code[s] = (i8)c; return; }
+  FD_CLK_BEGIN
   ge_p3 P; ge_p3_identity( P );
   ge_p2 P2;
   atab_raw ra, rr;
@@ -940,6 +941,7 @@ fd_dsmh_kernel( u32                      nsig,
   /* Q == O: X == 0 and Y == Z (Z != 0: complete formulas) */
   int ok = fe_is_zero( P2.X ) & fe_eq( P2.Y, P2.Z );
   code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+  FD_CLK_END
 }
 
 /* ---- latency path: two lanes per signature ------------------------------

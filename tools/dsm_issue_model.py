@@ -13,6 +13,7 @@
    fd_dsm_kernel time: their ratio is the VALU busy fraction under the measured costs.
 
 usage: dsm_issue_model.py instprobe.log --dsm-ms 9.57 --clock-mhz 2350 [--asm /tmp/isa/dsm.s] [--nsig 1048576]
+       [--kernel dsmh]   (the half-size walk: DSM_KERNEL=fd_dsmh_kernel tools/isa_hist.sh first)
 """
 import argparse
 import json
@@ -26,6 +27,15 @@ BLOCK_WEIGHTS = [("start", 0), ("bb0", 1), ("bb1", 1), ("bb2 prologue", 1), ("wi
                  ("inner loop: dbl -> P2", 189), ("dbl -> P3", 63), ("-A table add", 64), ("base-point add", 16),
                  ("-> P2", 64), ("next digit", 63), ("loop tail", 64), ("back edge", 64), ("exit", 1),
                  ("deferred-R store", 1), ("R compare (latency builds only)", 0), ("ret", 1), ("ret2", 1)]
+
+# fd_dsmh_kernel<1> (the half-size walk, wtop = 32: 33 windows, 32 with doublings, 16 base-point windows;
+# tools/isa_hist.sh with DSM_KERNEL=fd_dsmh_kernel); blocks 40-56 are the slow-list role (dsm_one), 0 here
+HS_BLOCK_WEIGHTS = ([(f"prologue {i}", 1) for i in range(26)] +
+                    [("walk prologue", 1), ("loop latch", 32), ("window header + -A gather", 33), ("dbl entry", 32),
+                     ("inner loop: dbl -> P2", 96), ("dbl -> P3", 32), ("-A add -> P3, -R gather", 33),
+                     ("base-point digit", 16), ("-R add", 33), ("base-point add", 16), ("-> P2, next", 33),
+                     ("digit loads", 32), ("identity check", 1), ("exit", 1)] +
+                    [(f"slow role {i}", 0) for i in range(19)])
 
 # instprobe row for each mnemonic family
 ROW = {"v_mad_u64_u32": "v_mad_u64_u32", "v_and_b32": "v_and_b32", "v_lshrrev_b64": "v_lshrrev_b64",
@@ -79,13 +89,15 @@ def main():
     ap.add_argument("--clock-mhz", type=float, required=True)
     ap.add_argument("--nsig", type=int, default=1 << 20)
     ap.add_argument("--pmc-valu-per-wave", type=float, default=338222.0)
+    ap.add_argument("--kernel", choices=("dsm", "dsmh"), default="dsm")
     a = ap.parse_args()
+    weights = HS_BLOCK_WEIGHTS if a.kernel == "dsmh" else BLOCK_WEIGHTS
     cyc = parse_probe(a.probe)
     blocks = blocks_of(a.asm)
-    if len(blocks) != len(BLOCK_WEIGHTS):
-        sys.exit(f"ISA has {len(blocks)} blocks, the weights describe {len(BLOCK_WEIGHTS)}: re-derive BLOCK_WEIGHTS")
+    if len(blocks) != len(weights):
+        sys.exit(f"ISA has {len(blocks)} blocks, the weights describe {len(weights)}: re-derive the weights")
     mix = {}
-    for (name, w), b in zip(BLOCK_WEIGHTS, blocks):
+    for (name, w), b in zip(weights, blocks):
         for k, c in b.items():
             mix[k] = mix.get(k, 0) + w * c
     valu = sum(c for k, c in mix.items() if k.startswith("v_"))

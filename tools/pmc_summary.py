@@ -23,7 +23,8 @@ import shutil
 import sys
 
 src, dst = sys.argv[1], sys.argv[2]
-DSM = ("fd_dsm_kernel<1>", "fd_dsm_kernel")   # the 1M launch: the carry-folded instantiation (round 2 late)
+# the 1M launch: the half-size walk (default), else the carry-folded full-length walk
+DSM = ("fd_dsmh_kernel<1>", "fd_dsm_kernel<1>", "fd_dsm_kernel")
 
 
 def norm(name):      # "void fd_dsm_kernel<1>(unsigned int, ...)" -> "fd_dsm_kernel<1>"
@@ -74,11 +75,13 @@ if os.path.exists(blog):
             b["rocprof_agreement"] = agree
             json.dump(b, open(os.path.join(dst, "bench_under_rocprof.json"), "w"), indent=1)
             print("agreement", agree)
-d = next((out[k] for k in DSM if k in out), None)
+dk = next((k for k in DSM if k in out), None)
+d = out.get(dk)
 if d and "hbm_read_bytes" in d:
-    im = os.path.join(os.path.dirname(dst.rstrip("/")), "roofline", "issue_model.json")
+    im = os.path.join(os.path.dirname(dst.rstrip("/")), "roofline",
+                      "issue_model_dsmh.json" if dk.startswith("fd_dsmh") else "issue_model.json")
     busy = json.load(open(im))["valu_busy_model"] if os.path.exists(im) else None
-    json.dump({"kernel": "fd_dsm_kernel", "source": dst,
+    json.dump({"kernel": dk, "source": dst,
                "hbm_bytes_per_launch": d["hbm_read_bytes"] + d.get("hbm_write_bytes", 0),
                "valu_busy": busy, "valu_busy_source": im if busy is not None else None,
                "valu_busy_flat4": d.get("valu_busy_flat4"), "valu_insts_per_wave": d.get("valu_insts_per_wave")},
