@@ -220,10 +220,14 @@ FD_DEV int sc_is_canonical( u32 const s[ 8 ] ) {
   return decided ? lt : 0; /* equal to l -> not canonical */
 }
 
+/* bits [bit, bit+nbits) of the 512-bit input (nbits <= 29, compile-time bit): one funnel
+   shift of two words (a 64-bit combine of the pair made the compiler spill the input to
+   scratch and reload it with unaligned 64-bit loads) */
 FD_DEV i64 sc_get21( u32 const w[ 16 ], int bit, int nbits ) {
   int wi = bit >> 5, sh = bit & 31;
-  u64 x = (u64)w[wi] | ( wi+1 < 16 ? ((u64)w[wi+1] << 32) : 0UL );
-  return (i64)( (x >> sh) & ((1UL << nbits) - 1UL) );
+  u32 hi = wi+1 < 16 ? w[wi+1] : 0u;
+  u32 x = __builtin_amdgcn_alignbit( hi, w[wi], (u32)sh );
+  return (i64)( x & ((1u << nbits) - 1u) );
 }
 
 FD_DEV void sc_fold( i64 * t, int j ) {
