@@ -116,6 +116,9 @@
 #ifndef FD_TABLE_FM
 #define FD_TABLE_FM FD_CARRY_FOLD
 #endif
+#ifndef FD_HALF_FUSED_TABLE
+#define FD_HALF_FUSED_TABLE 1      /* half-size throughput path: tables built by the decode lanes (0: fd_tableh_kernel) */
+#endif
 #define FD_PSTAT_SLOW 0x80u        /* A-status bit: the signature is on the half-size path's slow list */
 
 typedef signed char i8;
@@ -267,11 +270,17 @@ fd_decode_kernel( unsigned char const *    __restrict__ payload,
                   int                                   both,
                   unsigned char *          __restrict__ pstat,
                   uint4 *                  __restrict__ Rxy,
-                  uint4 *                  __restrict__ Axy ) {
+                  uint4 *                  __restrict__ Axy,
+                  uint4 *                  __restrict__ tabA,
+                  uint4 *                  __restrict__ tabR ) {
   u32 p = blockIdx.x * FD_WG + threadIdx.x;
   if( p >= ( both ? 2u*nsig : nsig ) ) return;
   u32 s = both ? p >> 1 : p, is_r = both ? p & 1u : 0u;
   decode_one<FD_DECODE_FM>( payload, desc, map, s, is_r, pstat, Rxy, Axy );
+  /* tabA != NULL (half-size path): each lane goes on to its point's table
+     when the point decoded, its table writes overlapping the other waves'
+     decodes (a separate table kernel is write-heavy: 2.3 KB per signature) */
+  if( tabA && ( pstat[2u*s + is_r] & 3u )==0u ) atab_build<FD_TABLE_FM>( is_r ? tabR : tabA, s, is_r ? Rxy : Axy );
 }
 
 /* Signed digits of k (radix 16, digA[64][n]) and S (radix 2^FD_BWIN,
@@ -1892,18 +1901,25 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     } else if( half ) {
       /* half-size scalars: decode A and R, result codes + hash + (c0, c1, s'), both tables */
       unsigned pg = (unsigned)( ( 2UL*sig_cnt + FD_WG - 1) / FD_WG );
+#if FD_HALF_FUSED_TABLE
       hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, 1,
-                          ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy );
+                          ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, ctx->d_tab, ctx->d_tabR );
+#else
+      hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, 1,
+                          ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, (uint4 *)NULL, (uint4 *)NULL );
+#endif
       hipLaunchKernelGGL( fd_hashh_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
                           ctx->semantics, ctx->d_pstat, code, ctx->d_digA, ctx->d_digR, ctx->d_digB, ctx->d_slow,
                           ctx->d_slow + ctx->max_sig, (uint4 const *)ctx->d_khash, ctx->half_force_slow,
                           ctx->d_htop );
+#if !FD_HALF_FUSED_TABLE
       hipLaunchKernelGGL( fd_tableh_kernel, dim3(2*sg), dim3(FD_WG), 0, st, nsig, (u32)sg, code, ctx->d_Axy, ctx->d_Rxy,
                           ctx->d_tab, ctx->d_tabR );
+#endif
     } else {
       unsigned pg = (unsigned)( ( (defer ? 1UL : 2UL)*sig_cnt + FD_WG - 1) / FD_WG );
       hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, !defer,
-                          ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy );
+                          ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, (uint4 *)NULL, (uint4 *)NULL );
       hipLaunchKernelGGL( fd_hash_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
                           ctx->semantics, defer, ctx->d_pstat, code, ctx->d_digA, ctx->d_digB, ctx->d_Rxy,
                           (uint4 const *)ctx->d_khash );
