@@ -153,12 +153,20 @@ int fdgpu_tcache_insert( fdgpu_tcache_t * tc, ulong tag ) {
    mcache/fd_mcache.h:288-325 semantics): equal = ready, behind = not yet
    published, ahead = overrun. */
 
+/* FDGPU_MC_PAD (A/B builds): pad each line to a 64-byte cache line, so the
+   tiles that read alternate seqs never share a line */
+#ifndef FDGPU_MC_PAD
+#define FDGPU_MC_PAD 0
+#endif
 typedef struct {
   _Atomic ulong  seq;
   ulong          sig;
   unsigned       chunk;
   unsigned short sz, ctl;
   unsigned       tsorig, tspub;
+#if FDGPU_MC_PAD
+  unsigned char  _pad[ 32 ];
+#endif
 } mc_line_t;
 
 struct fdgpu_mcache {

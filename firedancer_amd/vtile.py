@@ -11,7 +11,7 @@ import numpy as np
 
 from .engine import PKG_DIR, load_library as load_engine
 
-LIB_PATH = os.path.join(PKG_DIR, "libfdgpu_vtile.so")
+LIB_PATH = os.environ.get("FDGPU_VTILE_LIB") or os.path.join(PKG_DIR, "libfdgpu_vtile.so")   # env: A/B builds
 TXNM_HDR_SZ = 80
 CHUNK_SZ = 64
 PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL, OVERRUN, GPU_FAULT = range(7)
