@@ -49,6 +49,7 @@
 
 #define FD_WG 256
 #define FD_ATAB_ENTRIES 9          /* [0..8](-A), cached form, 128 B each */
+#define FD_ATAB_STORED  8          /* [1..8] stored per signature; [0] (the identity) is one shared constant line */
 /* Base-point window: FD_BWIN = 8 keeps [0..128]B (12.4 KB) in LDS and adds
    it every 2nd A window (32 adds); FD_BWIN = 16 keeps [0..32768]B (3.1 MB,
    L2 / Infinity-Cache resident) in HBM, gathered per lane one window
@@ -125,7 +126,7 @@ typedef signed char i8;
 
 /* ------------------------------------------------------------------ */
 /* scratch layout                                                      */
-/*   tab : uint4 [nsig][FD_ATAB_ENTRIES][8]  entry e of signature s =   */
+/*   tab : uint4 [nsig][FD_ATAB_STORED][8]   entry e >= 1 of signature s =*/
 /*         e*(-A) in cached form, 4 canonical field elements packed    */
 /*         8x32 (YpX, YmX, Z, T2d) = 128 B = one cache line, so the    */
 /*         per-lane gather of a random entry moves exactly one line    */
@@ -144,8 +145,17 @@ FD_DEV void fe_from_quads( fe & a, uint4 x, uint4 y ) {
   fe_unpack( a, w );
 }
 
-FD_DEV void atab_store( uint4 * tab, u32 s, int e, ge_cached const & c ) {
-  uint4 * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8;
+/* entry 0 = the identity in cached form (Y+X = Y-X = Z = 1, 2dT = 0), packed
+   like the stored entries: zero digits read this line instead of one per signature */
+__device__ __attribute__(( aligned( 16 ) )) unsigned const fd_atab_ident_w[ 32 ] = {
+  1u,0u,0u,0u, 0u,0u,0u,0u,  1u,0u,0u,0u, 0u,0u,0u,0u,  1u,0u,0u,0u, 0u,0u,0u,0u,  0u,0u,0u,0u, 0u,0u,0u,0u };
+
+FD_DEV uint4 const * atab_entry( uint4 const * tab, u32 s, int e ) {
+  return e ? tab + ((size_t)s * FD_ATAB_STORED + (size_t)( e - 1 )) * 8 : (uint4 const *)fd_atab_ident_w;
+}
+
+FD_DEV void atab_store( uint4 * tab, u32 s, int e, ge_cached const & c ) {   /* e >= 1 */
+  uint4 * b = tab + ((size_t)s * FD_ATAB_STORED + (size_t)( e - 1 )) * 8;
   fe_store_packed( b + 0, c.YpX );
   fe_store_packed( b + 2, c.YmX );
   fe_store_packed( b + 4, c.Z   );
@@ -155,7 +165,7 @@ FD_DEV void atab_store( uint4 * tab, u32 s, int e, ge_cached const & c ) {
 struct atab_raw { uint4 q[8]; };
 
 FD_DEV void atab_fetch( atab_raw & r, uint4 const * tab, u32 s, int e ) {
-  uint4 const * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8;
+  uint4 const * b = atab_entry( tab, s, e );
 #pragma unroll
   for( int i=0; i<8; i++ ) r.q[i] = b[i];
 }
@@ -209,8 +219,6 @@ FD_DEV void atab_build( uint4 * __restrict__ tab, u32 s, uint4 const * __restric
   fe_neg( A.X, A.X ); fe_wcarry( A.X, A.X );              /* -A */
   fe_mul<FM>( A.T, A.X, A.Y );
   ge_cached c1, c;
-  c.YpX = fe_one(); c.YmX = fe_one(); c.Z = fe_one(); c.T2d = fe_zero();
-  atab_store( tab, s, 0, c );
   ge_p3_to_cached<FM>( c1, A );
   atab_store( tab, s, 1, c1 );
   ge_p3 cur = A;
@@ -1157,14 +1165,14 @@ fd_dsm2_kernel( u32                      nsig,
   for( int w=wtop; w>=0; w-- ) {
     {                                                /* this lane's two coordinates of the -A entry */
       int neg = da < 0, e = neg ? -da : da;
-      uint4 const * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8;
+      uint4 const * b = atab_entry( tab, s, e );
       int c0 = h ^ neg;                              /* 0 YpX, 1 YmX (swapped when negated) */
       int c1 = h ? 2 : 3;                            /* lane 0 T2d, lane 1 Z */
       araw[0] = b[2*c0]; araw[1] = b[2*c0+1]; araw[2] = b[2*c1]; araw[3] = b[2*c1+1];
     }
     if( HS ) {                                       /* and of the -R entry */
       int neg = dr < 0, e = neg ? -dr : dr;
-      uint4 const * b = tabR + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8;
+      uint4 const * b = atab_entry( tabR, s, e );
       int c0 = h ^ neg, c1 = h ? 2 : 3;
       rraw[0] = b[2*c0]; rraw[1] = b[2*c0+1]; rraw[2] = b[2*c1]; rraw[3] = b[2*c1+1];
     }
@@ -1349,13 +1357,13 @@ fd_dsm4_kernel( u32                      nsig,
     {                                                /* this lane's coordinate of the -A entry */
       int neg = da < 0, e = neg ? -da : da;
       int ci = q < 2 ? ( q ^ neg ) : ( q==2 ? 3 : 2 );   /* YpX / YmX (swapped when negated), T2d, Z */
-      uint4 const * b = tab + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8 + 2*ci;
+      uint4 const * b = atab_entry( tab, s, e ) + 2*ci;
       araw[0] = b[0]; araw[1] = b[1];
     }
     if( HS ) {                                       /* and of the -R entry */
       int neg = dr < 0, e = neg ? -dr : dr;
       int ci = q < 2 ? ( q ^ neg ) : ( q==2 ? 3 : 2 );
-      uint4 const * b = tabR + ((size_t)s * FD_ATAB_ENTRIES + (size_t)e) * 8 + 2*ci;
+      uint4 const * b = atab_entry( tabR, s, e ) + 2*ci;
       rraw[0] = b[0]; rraw[1] = b[1];
     }
     int bw = HS ? ( !(w & 1) && w < 32 ) : !(w & 3);
@@ -2020,7 +2028,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   HIPCHK( hipMalloc( &ctx->d_map,  ns * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_code, ns ), -1 );
   HIPCHK( hipMalloc( &ctx->d_pstat, 2*ns ), -1 );
-  HIPCHK( hipMalloc( &ctx->d_tab,  ns * FD_ATAB_ENTRIES * 8 * sizeof(uint4) ), -1 );
+  HIPCHK( hipMalloc( &ctx->d_tab,  ns * FD_ATAB_STORED * 8 * sizeof(uint4) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_Rxy,  ns * 4 * sizeof(uint4) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_Axy,  ns * 4 * sizeof(uint4) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_digA, ns * 64 ), -1 );
@@ -2037,7 +2045,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
     char const * fs = getenv( "FDGPU_HALF_FORCE_SLOW" );
     ctx->half_force_slow = fs ? (u32)strtoul( fs, NULL, 0 ) : 0u; }
   if( ctx->half ) {
-    HIPCHK( hipMalloc( &ctx->d_tabR, ns * FD_ATAB_ENTRIES * 8 * sizeof(uint4) ), -1 );
+    HIPCHK( hipMalloc( &ctx->d_tabR, ns * FD_ATAB_STORED * 8 * sizeof(uint4) ), -1 );
     HIPCHK( hipMalloc( &ctx->d_digR, ns * FD_HDIG ), -1 );
     HIPCHK( hipMalloc( &ctx->d_htop, ns ), -1 );
     HIPCHK( hipMalloc( &ctx->d_btab2, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), -1 );
