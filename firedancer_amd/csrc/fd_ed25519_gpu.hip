@@ -833,15 +833,6 @@ fd_tableh_kernel( u32 nsig, u32 sg, i8 const * __restrict__ code, uint4 const * 
 #ifndef FD_DSMH_MINW
 #define FD_DSMH_MINW 3
 #endif
-#ifndef FD_DIAG_GATHER
-#define FD_DIAG_GATHER 0
-#endif
-#ifndef FD_DSMH_RPRE
-#define FD_DSMH_RPRE 0       /* 1: the -R gather also in flight across the doublings (more VGPRs) */
-#endif
-#ifndef FD_DSMH_RLATE
-#define FD_DSMH_RLATE 0      /* 1: issue the -R gather after the -A add (fewer VGPRs live across it) */
-#endif
 template<int FM>
 __global__ void __launch_bounds__( FD_WG, FM ? FD_DSMH_MINW : 1 )
 fd_dsmh_kernel( u32                      nsig,
@@ -889,46 +880,21 @@ fd_dsmh_kernel( u32                      nsig,
   int da = digA[ (size_t)wtop*n + s ], dr = digR[ (size_t)wtop*n + s ];
 #pragma unroll 1
   for( int w=wtop; w>=0; w-- ) {
-#if FD_DIAG_GATHER                                   /* diagnostic builds only (wrong results): one fixed line per table */
-    atab_fetch( ra, tabA, s, 1 );
-#else
     atab_fetch( ra, tabA, s, da < 0 ? -da : da );    /* in flight during the doublings */
-#endif
-#if FD_DSMH_RPRE
-    atab_fetch( rr, tabR, s, dr < 0 ? -dr : dr );
-#endif
     ge_p1p1 t;
     if( w != wtop ) {
 #pragma unroll 1
       for( int r=0; r<3; r++ ) { ge_dbl<FM>( t, P2 ); ge_p1p1_to_p2<FM>( P2, t ); }
       ge_dbl<FM>( t, P2 ); ge_p1p1_to_p3<FM>( P, t );
     }
-    /* the -R entry and the base-point entries are issued after the
-       doublings (in flight during the -A add): prefetching all of them
-       across the doublings costs 206 VGPRs, 2 waves per SIMD */
-#if FD_DSMH_RPRE
-    {
-      ge_cached q; atab_unpack( q, ra ); ge_cached_cneg( q, da < 0 );
-      ge_add_cached<FM>( t, P, q ); ge_p1p1_to_p3<FM>( P, t );
-    }
-#elif FD_DSMH_RLATE
-    {
-      ge_cached q; atab_unpack( q, ra ); ge_cached_cneg( q, da < 0 );
-      ge_add_cached<FM>( t, P, q );
-    }
-    atab_fetch( rr, tabR, s, dr < 0 ? -dr : dr );   /* in flight during the P3 conversion */
-    ge_p1p1_to_p3<FM>( P, t );
-#else
-#if FD_DIAG_GATHER
-    atab_fetch( rr, tabR, s, 1 );
-#else
+    /* the -R entry is issued after the doublings, in flight during the -A
+       add (prefetching it across the doublings as well, or issuing it after
+       the -A add: the same time, A/B 7.13-7.21 ms) */
     atab_fetch( rr, tabR, s, dr < 0 ? -dr : dr );
-#endif
     {
       ge_cached q; atab_unpack( q, ra ); ge_cached_cneg( q, da < 0 );
       ge_add_cached<FM>( t, P, q ); ge_p1p1_to_p3<FM>( P, t );
     }
-#endif
     /* base-point digit j (bits 16j..16j+15 of s') at window 4j from [0..32768]B,
        digit j+8 (bits 16j+128..) at window 4j+2 from [0..32768](2^120 B):
        one base-point add per even window */
