@@ -2909,6 +2909,15 @@ fdgpu_ed25519_debug_fault( fdgpu_ed25519_ctx_t * ctx ) {
 }
 
 extern "C" unsigned long
+fdgpu_ed25519_slow_count( fdgpu_ed25519_ctx_t * ctx ) {
+  if( !ctx || !ctx->half ) return 0UL;
+  if( hipSetDevice( ctx->device ) != hipSuccess || hipStreamSynchronize( ctx->stream ) != hipSuccess ) return ~0UL;
+  u32 cnt = 0u;
+  if( hipMemcpy( &cnt, ctx->d_slow + ctx->max_sig, sizeof(u32), hipMemcpyDeviceToHost ) != hipSuccess ) return ~0UL;
+  return (unsigned long)cnt;
+}
+
+extern "C" unsigned long
 fdgpu_ed25519_front_remaining( fdgpu_ed25519_ctx_t const * ctx ) {
   if( ctx->inflight.empty() ) return 0UL;
   fd_slot const & sl = ctx->slot[ ctx->inflight.front() ];

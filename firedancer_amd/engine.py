@@ -47,7 +47,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_host_alloc", "fdgpu_host_free", "fdgpu_host_register", "fdgpu_host_unregister", "fdgpu_device_numa_node",
            "fdgpu_ed25519_submit_raw_gather",
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
-           "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_set_dedup",
+           "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_slow_count", "fdgpu_ed25519_set_dedup",
            "fdgpu_ed25519_set_record_fp_off", "fdgpu_ed25519_batch_stats", "fdgpu_ed25519_launch_stats", "fdgpu_ed25519_front_remaining", "fdgpu_ed25519_verify_txn_ptrs",
            "fdgpu_last_error")
 
@@ -135,6 +135,8 @@ def load_library():
         L.fdgpu_ed25519_faulted.restype = ctypes.c_int
         L.fdgpu_ed25519_faulted.argtypes = [ctypes.c_void_p]
         L.fdgpu_ed25519_debug_fault.argtypes = [ctypes.c_void_p]
+        L.fdgpu_ed25519_slow_count.restype = ctypes.c_ulong
+        L.fdgpu_ed25519_slow_count.argtypes = [ctypes.c_void_p]
         L.fdgpu_ed25519_submit_raw_ref.restype = ctypes.c_int
         L.fdgpu_ed25519_submit_raw_ref.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_ushort,
                                                    ctypes.c_ulong]
@@ -381,6 +383,10 @@ class Engine:
     def debug_fault(self):
         """Host-side test hook: the context behaves as after a failed batch."""
         self.L.fdgpu_ed25519_debug_fault(self.ctx)
+
+    def slow_count(self) -> int:
+        """Signatures of the last batch that took the full-length walk (half-size path; 0 when it is off)."""
+        return int(self.L.fdgpu_ed25519_slow_count(self.ctx))
 
     def poll(self, max_n: int = 4096, blocking: bool = False):
         tags = np.zeros(max_n, np.uint64)

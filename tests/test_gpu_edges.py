@@ -123,3 +123,27 @@ def test_half_size_slow_list(fa, oracle, monkeypatch, every, ntx):
     np.testing.assert_array_equal(t, expect)
     ot, os_ = oracle.verify_txns(payload, desc, nsig, threads=16)
     np.testing.assert_array_equal(s, os_)
+
+
+@pytest.mark.parametrize("path", ["throughput", "latency"])
+def test_half_size_no_silent_fallback(fa, monkeypatch, path):
+    """Hash-distributed k always has a short (c0, c1) within 2^159: a valid batch takes the half-size walk
+    for every signature (slow list empty).  A device reduction that failed its own congruence check would
+    still verify correctly through the full walk -- only this count shows it.  The forced slow list counts
+    exactly the forced signatures."""
+    from firedancer_amd import synth
+    monkeypatch.setenv("FDGPU_HALF", "1")
+    monkeypatch.setenv("FDGPU_SMALL_BATCH_MAX", "0" if path == "throughput" else str(2**63))
+    payload, desc, expect, nsig = synth.make_batch(20000, synth.MULTI, max_signers=3, invalid_frac=0.0, seed=91,
+                                                   threads=16)
+    eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    t, _ = eng.verify_txns_host(payload, desc)
+    assert eng.slow_count() == 0
+    eng.close()
+    np.testing.assert_array_equal(t, expect)
+    monkeypatch.setenv("FDGPU_HALF_FORCE_SLOW", "7")
+    eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    t, _ = eng.verify_txns_host(payload, desc)
+    assert eng.slow_count() == (nsig + 6) // 7
+    eng.close()
+    np.testing.assert_array_equal(t, expect)
