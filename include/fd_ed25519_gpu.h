@@ -354,8 +354,9 @@ fdgpu_ed25519_debug_fault( fdgpu_ed25519_ctx_t * ctx );
 /* Signatures of the last batch launched on ctx that took the full 253-bit
    walk instead of the half-size one (no short (c0, c1) pair, or forced by
    env FDGPU_HALF_FORCE_SLOW); 0 when the half-size path is off.  Waits
-   for ctx's stream.  For tests and metrics: a device reduction that
-   silently failed would still verify correctly, only slower. */
+   for ctx's stream (a batch launched on a caller's stream must have
+   completed).  For tests and metrics: a device reduction that silently
+   failed would still verify correctly, only slower. */
 unsigned long
 fdgpu_ed25519_slow_count( fdgpu_ed25519_ctx_t * ctx );
 
