@@ -1807,11 +1807,42 @@ struct fdgpu_ed25519_ctx {
                                     of the arena range instead of kernel stores over PCIe (env FDGPU_GATHER_DMA) */
   unsigned long n_batches, n_txns;                /* async batches launched, transactions in them */
   unsigned long launch_ns;                        /* host time inside slot_launch */
-  unsigned long volatile * h_flag;                /* per slot: completion token written by fd_done_kernel (pinned) */
+  unsigned long volatile * h_flag;                /* per slot: completion token written by fd_done_kernel (pinned);
+                                                     [NSLOT]: the synchronous calls' (stream_wait) */
+  unsigned long sync_token;
   unsigned long * d_flag;
   unsigned long lat_hist[ FDGPU_LAT_BUCKETS ];    /* launch -> verdicts seen by poll, quarter-octave buckets */
   std::deque<int> inflight;      /* slot order */
 };
+
+/* Wait for everything queued on st in a synchronous host call.  A blocking
+   hipStreamSynchronize sleeps and now and then wakes late (the host-staged
+   8192-txn batch: p99 2x its p50); instead fd_done_kernel stores a fresh
+   token into a pinned word behind the batch and the host spins on it.  A
+   batch that failed never stores it: after FD_SYNC_SPIN_NS the call falls
+   back to hipStreamSynchronize, which waits or reports the error.  Only
+   for work whose results land in pinned memory: a copy into pageable host
+   memory may finish on the host after the stream (pageable = 1 waits the
+   HIP way). */
+#define FD_SYNC_SPIN_NS 20000000UL
+static int stream_wait( fdgpu_ed25519_ctx_t * ctx, hipStream_t st, int pageable ) {
+  if( !pageable ) {
+    unsigned long tok = ++ctx->sync_token;
+    hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT, tok );
+    if( hipGetLastError() == hipSuccess ) {
+      unsigned long t0 = fd_now_ns();
+      while( fd_now_ns() - t0 < FD_SYNC_SPIN_NS ) {
+        if( ctx->h_flag[ fdgpu_ed25519_ctx_t::NSLOT ] == tok ) return 0;
+#if defined(__x86_64__)
+        __builtin_ia32_pause();
+#endif
+      }
+    }
+  }
+  hipError_t e = hipStreamSynchronize( st );
+  if( e != hipSuccess ) { set_err( "hipStreamSynchronize", e ); return -2; }
+  return 0;
+}
 
 extern "C" unsigned long
 fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long small_max ) {
@@ -2030,8 +2061,8 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
     hipLaunchKernelGGL( fd_btab_kernel, dim3((FD_BTAB_ENTRIES + 255)/256), dim3(256), 0, ctx->stream, ctx->d_btab2, 120 );
   HIPCHK( hipGetLastError(), -1 );
   for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) HIPCHK( hipEventCreateWithFlags( &ctx->slot[i].done, hipEventDisableTiming ), -1 );
-  HIPCHK( hipHostMalloc( (void **)&ctx->h_flag, fdgpu_ed25519_ctx_t::NSLOT * sizeof(unsigned long), hipHostMallocDefault ), -1 );
-  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) ctx->h_flag[i] = 0UL;
+  HIPCHK( hipHostMalloc( (void **)&ctx->h_flag, ( fdgpu_ed25519_ctx_t::NSLOT + 1 ) * sizeof(unsigned long), hipHostMallocDefault ), -1 );
+  for( int i=0; i<=fdgpu_ed25519_ctx_t::NSLOT; i++ ) ctx->h_flag[i] = 0UL;   /* [NSLOT]: stream_wait's word */
   HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_flag, (void *)ctx->h_flag, 0 ), -1 );
   /* slot 0 now (the synchronous host calls stage through it); the async
      pipeline's other slots on first use (slot_bufs) */
@@ -2252,7 +2283,7 @@ verify_host_pipelined( fdgpu_ed25519_ctx_t * ctx, unsigned char const * payload,
   }
   HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
   if( sig_out && nsig ) HIPCHK( hipMemcpyAsync( sig_out, ctx->d_code, nsig, hipMemcpyDeviceToHost, st ), -2 );
-  HIPCHK( hipStreamSynchronize( st ), -2 );
+  if( stream_wait( ctx, st, sig_out && nsig ) ) return -2;
   memcpy( txn_out, sl.h_txn_out, txn_cnt );
   return 0;
 }
@@ -2291,7 +2322,7 @@ fdgpu_ed25519_verify_txns_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
   if( rc ) return rc;
   HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
   if( sig_out && nsig ) HIPCHK( hipMemcpyAsync( sig_out, ctx->d_code, nsig, hipMemcpyDeviceToHost, st ), -2 );
-  HIPCHK( hipStreamSynchronize( st ), -2 );
+  if( stream_wait( ctx, st, sig_out && nsig ) ) return -2;
   memcpy( txn_out, sl.h_txn_out, txn_cnt );
   return 0;
 }
@@ -2334,7 +2365,7 @@ fdgpu_ed25519_verify_many_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const *
     int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, n, n, sl.d_txn_out, NULL, st );
     if( rc ) return rc;
     HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, n, hipMemcpyDeviceToHost, st ), -2 );
-    HIPCHK( hipStreamSynchronize( st ), -2 );
+    if( stream_wait( ctx, st, 0 ) ) return -2;
     memcpy( out + done, sl.h_txn_out, n );
     done += n;
   }
@@ -2379,7 +2410,7 @@ fdgpu_ed25519_verify_txn_ptrs( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
     int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, n, nsig, sl.d_txn_out, NULL, st );
     if( rc ) return rc;
     HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, n, hipMemcpyDeviceToHost, st ), -2 );
-    HIPCHK( hipStreamSynchronize( st ), -2 );
+    if( stream_wait( ctx, st, 0 ) ) return -2;
     memcpy( out + done, sl.h_txn_out, n );
     done += n;
   }
@@ -2506,7 +2537,7 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
   HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
   if( img ) { HIPCHK( hipMemcpyAsync( img, d_img, txn_cnt * img_stride, hipMemcpyDeviceToHost, st ), -2 ); HIPCHK( hipFreeAsync( d_img, st ), -2 ); }
   if( fp  ) { HIPCHK( hipMemcpyAsync( fp, d_fp, txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 ); HIPCHK( hipFreeAsync( d_fp, st ), -2 ); }
-  HIPCHK( hipStreamSynchronize( st ), -2 );
+  if( stream_wait( ctx, st, img || fp ) ) return -2;
   memcpy( txn_out, sl.h_txn_out, txn_cnt );
   return 0;
 }
