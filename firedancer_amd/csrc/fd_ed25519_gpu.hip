@@ -1384,6 +1384,121 @@ fd_dsm4_kernel( u32                      nsig,
   if( !q ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
+/* ---- latency path: eight lanes per signature (half-size walk) -------------
+   For batches that leave SIMDs idle even at four lanes per signature
+   (<= FD_DSM8_MAX), the half-size walk's terms are split over two quads:
+   quad 0 walks [c0](-A) plus base-point digits 0-7, quad 1 [c1](-R) plus
+   digits 8-15, each with all 128 doublings but one variable-base add per
+   window instead of two and half the base-point adds (a shorter chain for
+   more total work).  At the end quad 1's point goes to quad 0 (row_shr:4 /
+   row_shl:4 moves: lanes 4-7 of each group of 8 to lanes 0-3), in cached
+   form (Y+X, Y-X, 2dT, Z; one multiplication), is added to quad 0's, and
+   the sum is tested for the identity.  Every lane of a group leaves
+   together (result codes first, like fd_dsm4_kernel<.,1>). */
+#ifndef FD_DSM8_MAX
+#define FD_DSM8_MAX 8192UL
+#endif
+FD_DEV void fe_from_upper_quad( fe & r, fe const & a ) {   /* lanes 0-3 of a group of 8 read lanes 4-7 */
+  asm volatile( "s_nop 1\n\t"
+                FD_DPP_MOV( 0, 10, "row_shl:4" ) FD_DPP_MOV( 1, 11, "row_shl:4" ) FD_DPP_MOV( 2, 12, "row_shl:4" )
+                FD_DPP_MOV( 3, 13, "row_shl:4" ) FD_DPP_MOV( 4, 14, "row_shl:4" ) FD_DPP_MOV( 5, 15, "row_shl:4" )
+                FD_DPP_MOV( 6, 16, "row_shl:4" ) FD_DPP_MOV( 7, 17, "row_shl:4" ) FD_DPP_MOV( 8, 18, "row_shl:4" )
+                FD_DPP_MOV( 9, 19, "row_shl:4" )
+                : "=&v"( r.v[0] ), "=&v"( r.v[1] ), "=&v"( r.v[2] ), "=&v"( r.v[3] ), "=&v"( r.v[4] ),
+                  "=&v"( r.v[5] ), "=&v"( r.v[6] ), "=&v"( r.v[7] ), "=&v"( r.v[8] ), "=&v"( r.v[9] )
+                : "v"( a.v[0] ), "v"( a.v[1] ), "v"( a.v[2] ), "v"( a.v[3] ), "v"( a.v[4] ),
+                  "v"( a.v[5] ), "v"( a.v[6] ), "v"( a.v[7] ), "v"( a.v[8] ), "v"( a.v[9] ) );
+}
+
+template<int FM>
+__global__ void __launch_bounds__( FD_WG )
+fd_dsm8_kernel( u32                      nsig,
+                uint4 const * __restrict__ tabA,
+                uint4 const * __restrict__ tabR,
+                i8 const *    __restrict__ digA,
+                i8 const *    __restrict__ digR,
+                short const * __restrict__ digB,
+                uint4 const * __restrict__ btab,
+                uint4 const * __restrict__ btab2,
+                i8 *          __restrict__ code,
+                int                        semantics,
+                unsigned char const * __restrict__ pstat,
+                unsigned char const * __restrict__ htop ) {
+  u32 gl = blockIdx.x * FD_WG + threadIdx.x;
+  u32 s = gl >> 3;
+  int half = (int)( ( gl >> 2 ) & 1u ), q = (int)( gl & 3u );
+  int c = s < nsig ? result_code( code[s], pstat[2*s], pstat[2*s+1], semantics, 0 ) : FD_ED25519_ERR_SIG;
+  int wtop = hs_wave_top( c == FD_ED25519_SUCCESS, htop, s );
+  if( c != FD_ED25519_SUCCESS ) { if( s < nsig && !half && !q && c != FD_PEND_SLOW ) code[s] = (i8)c; return; }
+  size_t n = nsig;
+  uint4 const * tab = half ? tabR : tabA;
+  i8 const *    dig = half ? digR : digA;
+  fe m, E, F, G, H, cc;
+  fe one = fe_one(), zero = fe_zero();
+  fe_sel( m, q==1 || q==2, one, zero );              /* identity (0 : 1 : 1 : 0) */
+  int da = dig[ (size_t)wtop*n + s ];
+  uint4 araw[2], braw[2];
+  int db = 0;
+#pragma unroll 1
+  for( int w=wtop; w>=0; w-- ) {
+    {                                                /* this lane's coordinate of its term's table entry */
+      int neg = da < 0, e = neg ? -da : da;
+      int ci = q < 2 ? ( q ^ neg ) : ( q==2 ? 3 : 2 );   /* YpX / YmX (swapped when negated), T2d, Z */
+      uint4 const * b = atab_entry( tab, s, e ) + 2*ci;
+      araw[0] = b[0]; araw[1] = b[1];
+    }
+    /* quad 0: digit j at window 4j from [0..32768]B; quad 1: digit j + 8 at window 4j + 2 from 2^120 B */
+    int bw = ( w & 3 ) == 2*half && w < 32;
+    if( bw ) {
+      db = digB[ (size_t)( (w>>2) + 8*half )*n + s ];
+      int neg = db < 0, e = neg ? -db : db;
+      int ci = q < 2 ? ( q ^ neg ) : 2;              /* ypx / ymx, xy2d; lane 3: Z2 = 1 */
+      uint4 const * b = ( half ? btab2 : btab ) + (size_t)e*6 + 2*ci;
+      if( q < 3 ) { braw[0] = b[0]; braw[1] = b[1]; }
+    }
+    if( w != wtop ) {
+#pragma unroll 1
+      for( int r=0; r<4; r++ ) { quad_dbl<FM>( E, F, G, H, q, m ); quad_mstep<FM>( m, q, E, F, G, H ); }
+    }
+    fe_from_quads( cc, araw[0], araw[1] );
+    { fe nc; fe_neg( nc, cc ); fe_sel( cc, q==2 && da < 0, nc, cc ); }
+    quad_add<FM>( E, F, G, H, q, m, cc );
+    quad_mstep<FM>( m, q, E, F, G, H );
+    if( bw ) {
+      if( q == 3 ) cc = one;
+      else {
+        fe_from_quads( cc, braw[0], braw[1] );
+        fe nc; fe_neg( nc, cc ); fe_sel( cc, q==2 && db < 0, nc, cc );
+      }
+      quad_add<FM>( E, F, G, H, q, m, cc );
+      quad_mstep<FM>( m, q, E, F, G, H );
+    }
+    if( w > 0 ) da = dig[ (size_t)(w-1)*n + s ];
+  }
+  /* quad 1's point in cached form: lane 0 Y+X, lane 1 Y-X, lane 2 2dT, lane 3 Z */
+  {
+    fe x, y, t, u;
+    fe_bcast0( x, m ); fe_bcast1( y, m );
+    fe_add( u, y, x );
+    fe_sub( t, y, x );
+    fe_sel( u, q==1, t, u );
+    fe d2 = fe_d2();
+    fe_mul<FM>( t, m, d2 );                          /* lane 3: T 2d (lane 2 keeps Z) */
+    fe_sel( u, q==2, m, u );                         /* Z on lane 2 ... */
+    fe_sel( u, q==3, t, u );                         /* ... 2dT on lane 3 */
+    fe_swap23( t, u );                               /* quad_add order: lane 2 2dT2, lane 3 Z2 */
+    fe_sel( u, q>=2, t, u );
+    fe_from_upper_quad( cc, u );                     /* quad 0 receives quad 1's */
+  }
+  /* all lanes take part in the moves above; quad 0 adds and tests */
+  quad_add<FM>( E, F, G, H, q, m, cc );
+  quad_mstep<FM>( m, q, E, F, G, H );
+  fe z; fe_bcast2( z, m );
+  u32 ok = q==0 ? (u32)fe_is_zero( m ) : ( q==1 ? (u32)fe_eq( m, z ) : 1u );
+  ok = fd_bcast0( ok ) & fd_bcast1( ok );
+  if( !half && !q ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
 /* ---- deferred R check (FD_DEFER_R) ---------------------------------------
    The signature's R is never decompressed on the common path.
    fd_dsm_kernel leaves P = [k](-A) + [S]B projective, and P's affine
@@ -1887,7 +2002,9 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       /* lanes per signature in the DSM: 4 while a quad per signature still fits one wave per
          SIMD (n <= 16K), 2 while a pair does (n <= 32K), else 1 (configs[0]'s 64K: 0.88 ms
          against 0.92 on the throughput path and 1.08 with two lanes, tools/configs0_ab.py) */
-      lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM4_MAX ? 4 : nsig <= FD_DSM2_MAX ? 2 : 1 );
+      lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM8_MAX && ctx->half ? 8 : nsig <= FD_DSM4_MAX ? 4 :
+                                                  nsig <= FD_DSM2_MAX ? 2 : 1 );
+      if( lanes == 8 && !ctx->half ) lanes = 4;       /* the term split needs the half-size walk */
       int d2 = lanes > 1;
       if( hs )      /* half-size: the A and R lanes build both tables, the hash lane (c0, c1, s') */
         hipLaunchKernelGGL( (fd_prep_kernel<0,1>), dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
@@ -1932,7 +2049,11 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
                           (unsigned char const *)NULL, code, ctx->d_Axy, ctx->d_tab );
     }
     if( ctx->timing ) hipEventRecord( ev[1], st );
-    if( small && lanes==4 )
+    if( small && lanes==8 )
+      hipLaunchKernelGGL( fd_dsm8_kernel<0>, dim3(8*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
+                          ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->semantics, ctx->d_pstat,
+                          ctx->d_htop );
+    else if( small && lanes==4 )
       hipLaunchKernelGGL( (hs ? fd_dsm4_kernel<0,1> : fd_dsm4_kernel<0,0>), dim3(4*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab,
                           ctx->d_Rxy, ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat,
                           ctx->d_tabR, ctx->d_digR, ctx->d_btab2, ctx->d_htop );

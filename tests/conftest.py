@@ -29,14 +29,16 @@ def golden():
 # fdgpu_ed25519_set_small_batch_max): "throughput" (half-size scalars,
 # fd_gpu_lattice.h: R decoded, a 128-doubling walk, Q == O), "throughput_full"
 # (env FDGPU_HALF=0: the 252-doubling walk, R checked after one batched
-# inversion per 256 signatures) and "latencyN" (one fused prep
+# inversion per 256 signatures) and "latencyN" (one fused prep; 8 = the
+# half-size walk's terms split over two quads
 # launch, R decoded up front, N = 4, 2 or 1 lanes per signature in the
 # DSM, env FDGPU_DSM_LANES).  The engine reads FDGPU_SMALL_BATCH_MAX
 # when a context is created, so the choice reaches contexts the verify
 # tile library creates too.
 def pytest_generate_tests(metafunc):
     if metafunc.definition.get_closest_marker("gpu") is not None and "engine_path" in metafunc.fixturenames:
-        metafunc.parametrize("engine_path", ["throughput", "throughput_full", "latency4", "latency2", "latency1"],
+        metafunc.parametrize("engine_path", ["throughput", "throughput_full", "latency8", "latency4", "latency2",
+                                            "latency1"],
                             indirect=True)
 
 

@@ -22,7 +22,7 @@ def main():
     nmax = max(sizes)
     payload, desc, expect, nsig = synth.make_batch(nmax, synth.LARGE_NOOP, seed=7, threads=16)
     out = {}
-    for n, path in [(n, p) for n in sizes for p in ("throughput", "latency4", "latency2")]:
+    for n, path in [(n, p) for n in sizes for p in ("throughput", "latency8", "latency4", "latency2")]:
         lpay = payload[: int(desc["payload_off"][n - 1]) + 1232 + 64]
         d = desc[:n].copy()
         os.environ["FDGPU_DSM_LANES"] = path[-1] if path.startswith("latency") else "0"   # read at ctx creation
