@@ -16,13 +16,14 @@ def cases():
     return torsion.make_cases(64)
 
 
-def test_torsion_signatures(cases, engine_path):
+@pytest.mark.parametrize("sem", [0, 1])            # AVX-512 and portable semantics: the same codes here
+def test_torsion_signatures(cases, engine_path, sem):
     import firedancer_amd as fa
     msgs = [c[0] for c in cases]
     sigs = [c[1] for c in cases]
     pubs = [c[2] for c in cases]
     want = np.array([c[3] for c in cases], np.int8)
-    eng = fa.Engine(device=0, max_txn=len(cases), max_sig=len(cases), max_payload=1 << 20)
+    eng = fa.Engine(device=0, max_txn=len(cases), max_sig=len(cases), max_payload=1 << 20, semantics=sem)
     try:
         got = np.asarray(eng.verify_many(msgs, sigs, pubs), np.int8)
     finally:
