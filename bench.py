@@ -221,6 +221,8 @@ def stream_child_main(args) -> None:
                                                threads=min(16, os.cpu_count() or 1))
     for leg in STREAM_LEGS:
         path = f"/dev/shm/fdgpu_link_{args.stream_token}_{leg}" if procs > 1 else None
+        # read by fdgpu_vtile_new (getenv) when link.run creates this process's tiles
+        os.environ["FDGPU_VTILE_CTX"] = str(args.stream_lat_ctx if leg == "paced" else args.stream_ctx)
         if proc == 0:
             cfg = _leg_cfg(args, leg, procs, cal_fps)
             link = vtile.Link(path, create=True, payload=payload, off=desc["payload_off"], sz=desc["payload_sz"], **cfg)
@@ -236,7 +238,7 @@ def stream_child_main(args) -> None:
             if leg == "cal":
                 cal_fps = st["frags_per_s"]
             else:
-                out[leg] = _leg_summary(st, cfg)
+                out[leg] = dict(_leg_summary(st, cfg), engine_contexts_per_tile=int(os.environ["FDGPU_VTILE_CTX"]))
         else:
             link = vtile.Link(path, create=False, timeout_s=180.0 if leg == "cal" else 120.0)   # bounded if process 0 failed
             try:
@@ -258,7 +260,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-max-batch", str(args.stream_max_batch),
            "--stream-rate", str(args.stream_rate), "--stream-lat-tiles", str(args.stream_lat_tiles),
            "--stream-inflight", str(args.stream_inflight), "--stream-depth", str(args.stream_depth),
-           "--stream-lat-inflight", str(args.stream_lat_inflight), "--stream-producers", str(args.stream_producers)]
+           "--stream-lat-inflight", str(args.stream_lat_inflight), "--stream-producers", str(args.stream_producers),
+           "--stream-ctx", str(args.stream_ctx), "--stream-lat-ctx", str(args.stream_lat_ctx)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -299,6 +302,12 @@ def main():
                          "(profiles/r02/stream/sweep_depth.md)")
     ap.add_argument("--stream-producers", type=int, default=1,
                     help="producer links (the reference's QUIC tiles) per GPU; every tile reads every link")
+    ap.add_argument("--stream-ctx", type=int, default=1,
+                    help="engine contexts per verify tile on the max-rate and unreliable legs (FDGPU_VTILE_CTX; "
+                         "1 beat 2 by 2.5-5.6 %% in 4 interleaved pairs, profiles/r02/stream/sweep_ctx_per_tile.md)")
+    ap.add_argument("--stream-lat-ctx", type=int, default=2,
+                    help="engine contexts per verify tile on the paced leg (staggered batches: one stages while "
+                         "the other runs)")
     ap.add_argument("--stream-lat-inflight", type=int, default=1,
                     help="--stream-inflight of the paced leg (1: few, larger batches; 2 gave p50/p99 0.82/1.53 ms "
                          "against 0.72/1.02 ms at 1, with 277-txn mean batches)")
@@ -512,7 +521,7 @@ def main():
                           "max_inflight": args.stream_inflight, "max_inflight_paced": args.stream_lat_inflight,
                           "link_depth": args.stream_depth * min(world, 2),
                           "producers": args.stream_producers * world,
-                          "engine_contexts_per_tile": int(os.environ.get("FDGPU_VTILE_CTX", "2")),
+                          "engine_contexts_per_tile": args.stream_ctx, "engine_contexts_per_tile_paced": args.stream_lat_ctx,
                           "process": "one tile process per GPU without a torch GPU context (as a C verify tile); "
                                      "link in /dev/shm when G > 1",
                           "intake": "zero-copy (GPU gathers frags from the registered in dcache)"
