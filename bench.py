@@ -38,7 +38,7 @@ MAC_PER_MUL, MAC_PER_SQR = 72, 44
 DSM_MUL, DSM_SQR = 1341, 1008          # wNAF DSM (1008 S + 1339 M) + eq (2 M)
 PREP_MUL, PREP_SQR = 38, 510           # decode of A and R: 2 x (255 S + 19 M)
 DSM_MAC = DSM_MUL * MAC_PER_MUL + DSM_SQR * MAC_PER_SQR
-# The half-size walk the engine runs by default (fd_gpu_lattice.h, fd_dsmh_kernel; env FDGPU_HALF=0 keeps
+# The half-size walk the engine runs by default (fd_gpu_lattice.h, fd_dsmh_kernel; bench.py with FDGPU_HALF=0 keeps
 # the 252-doubling walk): 128 doublings (4 S + 3 M), 66 variable-base adds (A and R, 4 M + 4 M to
 # extended), 16 base-point adds (3 M + 4 M), priced the same way.
 HS_MUL, HS_SQR = 128 * 3 + 66 * 8 + 16 * 7, 128 * 4
@@ -142,7 +142,20 @@ def cpu_sweep_configs0(impl, kind, max_threads, gen_threads, point_s=0.6):
 # seq % T == i (before_frag, fd_verify_tile.c:47-48) and drives GPU i % G from that GPU's process.  With
 # G > 1 the link lives in a /dev/shm file that rank 0's child creates and the other ranks' children join.
 
-STREAM_LEGS = ("cal", "max", "paced", "unrel")
+def stream_legs(args) -> list[str]:
+    """cal, max, one paced leg per --stream-rates entry (frags/s per GPU), unrel"""
+    return ["cal", "max"] + [f"paced@{r}" for r in _rates(args)] + ["unrel"]
+
+
+def _rates(args) -> list[float]:
+    return [float(x) for x in str(args.stream_rates).split(",") if x.strip()]
+
+
+def _pow2_clamp(x: float, lo: int, hi: int) -> int:
+    p = lo
+    while p < x and p < hi:
+        p *= 2
+    return p
 
 
 def _leg_cfg(args, leg, procs, cal_fps):
@@ -153,23 +166,29 @@ def _leg_cfg(args, leg, procs, cal_fps):
     Tl = min(args.stream_lat_tiles, max(1, budget - args.stream_producers)) * procs
     # the max-rate legs batch for throughput (a GPU batch under one wave per SIMD costs about one wave's
     # DSM chain, ~1 ms, whatever its size), the paced leg for latency
-    base = dict(batch_txn=args.stream_max_batch if leg != "paced" else args.stream_batch,
-                max_inflight=args.stream_inflight if leg != "paced" else args.stream_lat_inflight,
+    paced = leg.startswith("paced@")
+    rate = float(leg.split("@")[1]) if paced else 0.0
+    # paced legs: a batch limit of about 4 ms of one tile's share of the offered load (8K..64K), so batches
+    # stay small at low load (latency path) and can grow with it; adaptive launch sizes them below that
+    pb = _pow2_clamp(rate / max(1, args.stream_lat_tiles) * 4e-3, args.stream_batch, args.stream_max_batch)
+    base = dict(batch_txn=args.stream_max_batch if not paced else pb,
+                max_inflight=args.stream_inflight if not paced else args.stream_lat_inflight,
                 zero_copy=not args.stream_copy, gpus=procs,
                 producers=args.stream_producers * procs,   # the reference's QUIC tiles: producer q in process q % G
                 # per link: its producer runs depth/2 ahead of the slowest tile; with one producer per GPU a
                 # link carries 1/G of the frags but is read by all 2G tiles -> twice the single-GPU depth
-                mcache_depth=args.stream_depth * min(procs, 2) if leg != "paced" else 1 << 18)
+                mcache_depth=args.stream_depth * min(procs, 2) if not paced else 1 << 18,
+                nctx=args.stream_lat_ctx if paced else args.stream_ctx,
+                copy_wait_ns=int(args.stream_copy_wait_us * 1000))
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
     if leg == "max":            # credit-based: the sustained rate with no frag lost
         n = args.stream_frags if args.stream_frags > 0 else int(1.2 * cal_fps * args.stream_seconds)
         return dict(base, tiles=T, n_frags=n, rate_fps=0.0, reliable=True)
-    if leg == "paced":          # the reference's unreliable link at a fixed offered load
-        rate = args.stream_rate * procs
-        n = args.stream_frags if args.stream_frags > 0 else int(rate * args.stream_seconds)
-        return dict(base, tiles=Tl, n_frags=n, rate_fps=rate, reliable=False)
+    if paced:                   # the reference's unreliable link at a fixed offered load (per GPU)
+        n = args.stream_frags if args.stream_frags > 0 else int(rate * procs * args.stream_paced_seconds)
+        return dict(base, tiles=Tl, n_frags=n, rate_fps=rate * procs, reliable=False)
     # unreliable, producer unthrottled: tiles that fall a lap behind are overrun and skip frags
     n = args.stream_frags if args.stream_frags > 0 else int(cal_fps * args.stream_unrel_seconds)
     return dict(base, tiles=T, n_frags=n, rate_fps=0.0, reliable=False)
@@ -199,6 +218,10 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
             "tile_idle_ns_per_frag": round(st["tile_idle_ns"] / n, 1), "producer_seconds": st["prod_seconds"],
             "producer_credit_wait_s": st["prod_wait_ns"] * 1e-9,
             "batches": st["batches"], "mean_batch_txns": st["batch_txns"] / max(st["batches"], 1),
+            "batch_limit": cfg["batch_txn"], "engine_contexts_per_tile": cfg["nctx"],
+            # zero-copy intake: the GPU copies (the stem's during_frag copy, done by the GPU) started early
+            "copies": st["copies"], "copy_lat_mean_us": st["copy_lat_ns_sum"] / max(st["copy_lat_n"], 1) * 1e-3,
+            "copy_lat_max_us": st["copy_lat_ns_max"] * 1e-3,
             "inflight_max": st["inflight_max"], "gpu_batch_lat_p50_us_le": hq(0.5),
             "gpu_batch_lat_p99_us_le": hq(0.99)}
 
@@ -219,10 +242,8 @@ def stream_child_main(args) -> None:
         n_pay = max(args.txns, 2 * tiles * (1 << 16))
         payload, desc, _, _ = synth.make_batch(n_pay, synth.LARGE_NOOP, seed=args.stream_seed,
                                                threads=min(16, os.cpu_count() or 1))
-    for leg in STREAM_LEGS:
-        path = f"/dev/shm/fdgpu_link_{args.stream_token}_{leg}" if procs > 1 else None
-        # read by fdgpu_vtile_new (getenv) when link.run creates this process's tiles
-        os.environ["FDGPU_VTILE_CTX"] = str(args.stream_lat_ctx if leg == "paced" else args.stream_ctx)
+    for leg in stream_legs(args):
+        path = f"/dev/shm/fdgpu_link_{args.stream_token}_{leg.replace('@', '_')}" if procs > 1 else None
         if proc == 0:
             cfg = _leg_cfg(args, leg, procs, cal_fps)
             link = vtile.Link(path, create=True, payload=payload, off=desc["payload_off"], sz=desc["payload_sz"], **cfg)
@@ -238,7 +259,7 @@ def stream_child_main(args) -> None:
             if leg == "cal":
                 cal_fps = st["frags_per_s"]
             else:
-                out[leg] = dict(_leg_summary(st, cfg), engine_contexts_per_tile=int(os.environ["FDGPU_VTILE_CTX"]))
+                out[leg] = _leg_summary(st, cfg)
         else:
             link = vtile.Link(path, create=False, timeout_s=180.0 if leg == "cal" else 120.0)   # bounded if process 0 failed
             try:
@@ -258,10 +279,12 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-seconds", str(args.stream_seconds), "--stream-unrel-seconds", str(args.stream_unrel_seconds),
            "--stream-tiles", str(args.stream_tiles), "--stream-batch", str(args.stream_batch),
            "--stream-max-batch", str(args.stream_max_batch),
-           "--stream-rate", str(args.stream_rate), "--stream-lat-tiles", str(args.stream_lat_tiles),
+           "--stream-lat-tiles", str(args.stream_lat_tiles),
            "--stream-inflight", str(args.stream_inflight), "--stream-depth", str(args.stream_depth),
            "--stream-lat-inflight", str(args.stream_lat_inflight), "--stream-producers", str(args.stream_producers),
-           "--stream-ctx", str(args.stream_ctx), "--stream-lat-ctx", str(args.stream_lat_ctx)]
+           "--stream-ctx", str(args.stream_ctx), "--stream-lat-ctx", str(args.stream_lat_ctx),
+           "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
+           "--stream-copy-wait-us", str(args.stream_copy_wait_us)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -315,7 +338,13 @@ def main():
                     help="mcache lines of the max-rate legs' link: a reliable producer runs depth/2 ahead of the "
                          "oldest frag a tile still holds, so the depth bounds the frags in flight (2^18: 13.8M, "
                          "2^20: 16-17.6M sigs/s on 2 tiles, profiles/r02/stream/sweep_depth.log)")
-    ap.add_argument("--stream-rate", type=float, default=2e6, help="paced leg: offered frags/s per GPU")
+    ap.add_argument("--stream-rates", default="2e6,5e6,10e6,15e6",
+                    help="paced legs (the latency-under-load curve): offered frags/s per GPU, comma separated; "
+                         "stream.knee = the highest whose p99 is <= 1 ms with no frag lost")
+    ap.add_argument("--stream-paced-seconds", type=float, default=3.0, help="length of each paced leg")
+    ap.add_argument("--stream-copy-wait-us", type=float, default=0.0,
+                    help="zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
+                         "waited this long (0 = fdgpu_vtile default, FDGPU_VTILE_COPY_WAIT_NS)")
     ap.add_argument("--stream-lat-tiles", type=int, default=2,
                     help="verify tiles per GPU of the paced leg (fewer tiles = fewer HIP streams sharing the "
                          "device's hardware queues; 2 tiles carry 2M frags/s)")
@@ -361,6 +390,9 @@ def main():
     pay_d = torch.from_numpy(payload).cuda()
     desc_d = torch.from_numpy(desc.view(np.uint8)).cuda()
     out_d = torch.empty(n, dtype=torch.int8, device="cuda")
+    if not HALF:                 # A/B: the full-length walk (the engine's explicit test hook, not an env read)
+        from firedancer_amd import engine as _engine
+        _engine.debug_set_opts(half=0)
     eng = Engine(device=dev, max_txn=n, max_sig=nsig)
     st = torch.cuda.current_stream().cuda_stream
 
@@ -508,16 +540,24 @@ def main():
         if rank == 0:
             if res is not None and stream_ok:
                 legs = res["legs"]
-                mx, pc, ur = legs["max"], legs["paced"], legs["unrel"]
+                mx, ur = legs["max"], legs["unrel"]
+                curve = [dict(legs[f"paced@{r}"], offered_frags_per_s_per_gpu=r) for r in _rates(args)]
+                pc = curve[0]
                 ok_s = (mx["metrics"][:4] == [0, 0, 0, 0] and mx["published"] == mx["frags"] and mx["lost"] == 0
-                        and pc["metrics"][:4] == [0, 0, 0, 0])
+                        and all(c["metrics"][:4] == [0, 0, 0, 0] for c in curve))
+                # the knee: the highest offered rate whose p99 (tsorig -> verdict) stays within 1 ms with
+                # every frag verified (none lost to overruns, none overrun while copied)
+                within = [c["offered_frags_per_s_per_gpu"] for c in curve
+                          if c["p99_us"] <= 1000.0 and c["lost"] == 0 and c["overruns_at_verdict"] == 0]
+                knee = {"frags_per_s_per_gpu": max(within) if within else None, "p99_bound_us": 1000.0,
+                        "rates_tried": _rates(args)}
                 stream = {"workload": "BASELINE configs[4]: 1232-byte txns, Q producer mcache links over one in dcache "
                                       "-> T verify tiles reading every link (seq % T round robin per link, tile i -> "
                                       "GPU i % G; device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> "
                                       "out dcache",
                           "sigs_per_s": mx["sigs_per_s"], "per_gpu_sigs_per_s": mx["sigs_per_s"] / world,
                           "n_gpus": world, "tiles_per_gpu": mx["tiles"] // world, "batch_max": args.stream_max_batch,
-                          "batch_paced": args.stream_batch,
+                          "batch_paced": pc["batch_limit"],
                           "max_inflight": args.stream_inflight, "max_inflight_paced": args.stream_lat_inflight,
                           "link_depth": args.stream_depth * min(world, 2),
                           "producers": args.stream_producers * world,
@@ -526,7 +566,9 @@ def main():
                                      "link in /dev/shm when G > 1",
                           "intake": "zero-copy (GPU gathers frags from the registered in dcache)"
                                     if not args.stream_copy else "host copy into the out dcache (reference during_frag)",
-                          "max_rate": mx, "paced": pc, "unreliable_max": ur,
+                          "max_rate": mx, "paced": pc, "latency_curve": curve, "knee": knee, "unreliable_max": ur,
+                          # goodput of the reference's own link mode under overload, against the reliable max rate
+                          "unreliable_goodput_vs_max": ur["sigs_per_s"] / mx["sigs_per_s"] if mx["sigs_per_s"] else None,
                           "all_published": bool(ok_s),
                           "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
             else:

@@ -96,9 +96,6 @@
 #define FD_STAGE_CHUNK ( 1UL << 20 )   /* host-staged batches: bytes per memcpy / H2D step */
 /* gathered batches: the fd_txn_t image of the last record may end this far past its record */
 #define FD_IMG_TAIL    1024UL
-#ifndef FD_GATHER_DMA
-#define FD_GATHER_DMA  0
-#endif
 #define FD_PIPE_SUB    ( 1UL << 17 )   /* host batches of >= 2 FD_PIPE_SUB txns: sub-batches overlap H2D and kernels */
 #define FD_PIPE_MAX    16UL
 #define FD_PEND_ASMALL 2           /* per-signature code in flight: A small order, R's decode picks ERR_SIG / ERR_PUBKEY */
@@ -1653,7 +1650,7 @@ fd_reduce_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 n
   fdgpu_txn_desc_t d = desc[t];
   u32 cnt = d.sig_cnt;
   int r;
-  if( pflag && pflag[t] ) r = FDGPU_ERR_PARSE;               /* fd_verify_tile.c:127-131 */
+  if( pflag && pflag[t] ) r = pflag[t]==2u ? FDGPU_ERR_OVERRUN : FDGPU_ERR_PARSE;   /* fd_verify_tile.c:127-131 */
   else if( cnt==0u || cnt>16u ) r = FD_ED25519_ERR_SIG;      /* fd_ed25519_user.c:238-241 */
   else {
     int first = 0, any_msg = 0;
@@ -1710,10 +1707,22 @@ fd_parse_kernel( unsigned char const *    __restrict__ payload,
                  u32                                    img_stride,
                  unsigned short *         __restrict__ fp_out,
                  u64                                    dedup_seed,
-                 u64 *                    __restrict__ dtag_out ) {
+                 u64 *                    __restrict__ dtag_out,
+                 unsigned char const *    __restrict__ ovr ) {
   u32 t = blockIdx.x * FD_WG + threadIdx.x;
   if( t >= txn_cnt ) return;
   fdgpu_txn_raw_t r = raw[t];
+  if( ovr && ovr[t] ) {        /* overrun while gathered (fd_gather_kernel): never parsed, never verified */
+    if( fp_out ) fp_out[t] = 0;
+    if( dtag_out ) dtag_out[t] = 0UL;
+    if( !desc_out ) return;
+    fdgpu_txn_desc_t d;
+    d.payload_off = r.payload_off; d.sig_base = r.sig_base; d.payload_sz = 0; d.message_off = 0; d.acct_addr_off = 0;
+    d.signature_off = 0; d.sig_cnt = r.sig_lanes;
+    desc_out[t] = d;
+    pflag[t] = 2u;
+    return;
+  }
   fd_txn_hdr h;
   u32 fp = fd_txn_parse_dev( payload + r.payload_off, (u32)r.payload_sz,
                              img ? img + (size_t)t*img_stride : (unsigned char *)0, h );
@@ -1791,20 +1800,65 @@ struct fd_gather {             /* mode 3: copy sz bytes from src (host, device v
   unsigned long src;
   unsigned int  dst;
   unsigned int  sz;            /* multiple of 16 */
+  unsigned long seq_addr;      /* device view of the frag's in-mcache line seq word, 0 = no overrun check */
+  unsigned long seq;           /* the seq that line held when the tile took the frag */
 };
 
-/* Gathered raw batches (fdgpu_ed25519_submit_raw_gather): one 64-lane
-   group per record copies it, 16 B per lane, from the caller's in region
-   (host memory registered with the GPU, read over PCIe) into the batch
-   arena and into the record's place in the caller's out region -- the
-   host never touches the payload bytes. */
+/* Gathered raw batches (fdgpu_ed25519_submit_raw_gather) -- the GPU side of
+   the stem's during_frag copy (src/disco/stem/fd_stem.c:667-686): one
+   64-lane group per record copies it, 16 B per lane, from the caller's in
+   region (host memory registered with the GPU, read over PCIe) into the
+   batch arena and into the record's place in the caller's out region, then
+   re-reads the frag's in-mcache seq (a system-scope load, issued after
+   every lane's copy loads have returned).  A changed seq means the producer
+   reused the line while the record was being read: the record is flagged
+   (ovr[t] = 1) and the verify kernels report FDGPU_ERR_OVERRUN for it, the
+   stem's "overrun while reading" skip.  The check happens once, here; the
+   copy in the out region is what after_frag publishes.
+   Gathers of a context run on their own stream, ahead of the batch that
+   verifies them (the tile gathers while a batch fills): every block bumps a
+   device counter once its loads have returned, and the block that brings
+   it to `target` stores target into the pinned word `flag`, so the host
+   learns which records have been read -- and may be overwritten in the in
+   region -- without a HIP call.  The flag speaks for the loads only (the
+   copies' stores reach the host's out region before the batch's verdicts,
+   behind its completion token), so no release fence is needed: a
+   system-scope release per block wrote back the XCD's whole L2 each time,
+   under the verify kernels running beside it (2x slower stream). */
 __global__ void __launch_bounds__( 64 )
-fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__ arena, unsigned char * __restrict__ out ) {
+fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__ arena, unsigned char * __restrict__ out,
+                  unsigned char * __restrict__ ovr, unsigned long * cnt, unsigned long * flag, unsigned long target ) {
   fd_gather r = g[ blockIdx.x ];
   uint4 const * src = (uint4 const *)r.src;
   uint4 * a = (uint4 *)( arena + r.dst );
   uint4 * o = (uint4 *)( out + r.dst );
-  for( u32 i=threadIdx.x; i<(r.sz >> 4); i+=64u ) { uint4 v = src[i]; a[i] = v; if( out ) o[i] = v; }
+  u32 n16 = r.sz >> 4, i = threadIdx.x;
+  unsigned char bad = 0;
+  if( n16 <= 128u ) {          /* every fd_txn_m_t record (<= 80 + 1232 bytes): all loads, the re-check, then stores */
+    uint4 v0 = make_uint4( 0u, 0u, 0u, 0u ), v1 = v0;
+    if( i < n16 ) v0 = src[i];
+    if( i + 64u < n16 ) v1 = src[i + 64u];
+    if( r.seq_addr ) {
+      asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );     /* the copy's loads have all returned */
+      unsigned long s = __hip_atomic_load( (unsigned long *)r.seq_addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+      bad = s != r.seq;
+    }
+    if( i < n16 ) { a[i] = v0; o[i] = v0; }
+    if( i + 64u < n16 ) { a[i + 64u] = v1; o[i + 64u] = v1; }
+  } else {
+    for( ; i<n16; i+=64u ) { uint4 v = src[i]; a[i] = v; o[i] = v; }
+    if( r.seq_addr ) {
+      asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
+      unsigned long s = __hip_atomic_load( (unsigned long *)r.seq_addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+      bad = s != r.seq;
+    }
+  }
+  if( threadIdx.x == 0u ) ovr[ blockIdx.x ] = bad;
+  __syncthreads();                                          /* (one wave: every lane's loads have returned) */
+  if( threadIdx.x == 0u ) {
+    unsigned long old = __hip_atomic_fetch_add( cnt, 1UL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+    if( old + 1UL == target ) __hip_atomic_store( flag, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+  }
 }
 
 /* Gathered raw batches: the fd_txn_t image of each parsed transaction
@@ -1869,8 +1923,10 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   unsigned char const * ref_base; /* mode 2, 3: the caller's pinned region; payloads at [ref_lo, ref_hi) */
   size_t             ref_lo, ref_hi;
   unsigned char *    ref_dev;  /* mode 3: the device address of ref_base (the gather kernel writes the records back) */
-  struct fd_gather * h_gat;    /* mode 3: one gather record per transaction */
-  struct fd_gather * d_gat;
+  struct fd_gather * h_gat;    /* mode 3: one gather record per transaction (pinned; the kernel reads it over PCIe) */
+  struct fd_gather * g_dev;    /*         its device view */
+  unsigned char *    d_ovr;    /*         per transaction: 1 = overrun while gathered */
+  unsigned long      gathered; /*         records whose gather has been launched (fdgpu_ed25519_gather) */
 };
 
 struct fdgpu_ed25519_ctx {
@@ -1918,12 +1974,15 @@ struct fdgpu_ed25519_ctx {
   int dedup;                     /* raw batches also return HA dedup tags (fdgpu_ed25519_set_dedup) */
   unsigned long dedup_seed;
   int rec_fp_off;                /* gathered records: offset of a u16 footprint field, -1 = none */
-  int gather_dma;                /* gathered batches: records and images return to the out region by one D2H copy
-                                    of the arena range instead of kernel stores over PCIe (env FDGPU_GATHER_DMA) */
+  hipStream_t gstream;           /* gathered batches: the copies (fd_gather_kernel), ahead of the batch's kernels */
+  hipEvent_t  gev;               /*   recorded behind a batch's last gather; the ctx stream waits for it */
+  unsigned long * d_gcnt;        /*   gather blocks completed (device counter) */
+  unsigned long   g_launched;    /*   records whose gather has been launched, cumulative */
   unsigned long n_batches, n_txns;                /* async batches launched, transactions in them */
   unsigned long launch_ns;                        /* host time inside slot_launch */
   unsigned long volatile * h_flag;                /* per slot: completion token written by fd_done_kernel (pinned);
-                                                     [NSLOT]: the synchronous calls' (stream_wait) */
+                                                     [NSLOT]: the synchronous calls' (stream_wait);
+                                                     [NSLOT+1]: records gathered, cumulative (fd_gather_kernel) */
   unsigned long sync_token;
   unsigned long * d_flag;
   unsigned long lat_hist[ FDGPU_LAT_BUCKETS ];    /* launch -> verdicts seen by poll, quarter-octave buckets */
@@ -1947,7 +2006,12 @@ static int stream_wait( fdgpu_ed25519_ctx_t * ctx, hipStream_t st, int pageable 
     if( hipGetLastError() == hipSuccess ) {
       unsigned long t0 = fd_now_ns();
       while( fd_now_ns() - t0 < FD_SYNC_SPIN_NS ) {
-        if( ctx->h_flag[ fdgpu_ed25519_ctx_t::NSLOT ] == tok ) return 0;
+        if( ctx->h_flag[ fdgpu_ed25519_ctx_t::NSLOT ] == tok ) {
+          /* the results the caller reads next were stored before the token (fd_done_kernel's release):
+             keep those plain loads behind this volatile one */
+          std::atomic_thread_fence( std::memory_order_acquire );
+          return 0;
+        }
 #if defined(__x86_64__)
         __builtin_ia32_pause();
 #endif
@@ -2115,6 +2179,19 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
 
 extern "C" void fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx );
 
+/* Test / A/B options of contexts created from now on (fdgpu_debug_set_opts).
+   Process-wide, behind a mutex; the defaults are the product's choices. */
+static std::mutex g_dbg_mu;
+static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L };
+static void debug_opts_get( fdgpu_debug_opts_t * o ) { std::lock_guard<std::mutex> lk( g_dbg_mu ); *o = g_dbg; }
+
+extern "C" void
+fdgpu_debug_set_opts( fdgpu_debug_opts_t const * opts ) {
+  std::lock_guard<std::mutex> lk( g_dbg_mu );
+  if( opts ) g_dbg = *opts;
+  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L };
+}
+
 /* staging + device buffers of async slot i (once) */
 static int
 slot_bufs( fdgpu_ed25519_ctx_t * ctx, int i ) {
@@ -2158,22 +2235,18 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   HIPCHK( hipMalloc( &ctx->d_O, ns * 10 * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_blk, ( ( ns + FD_WG - 1 ) / FD_WG ) * 10 * sizeof(u32) ), -1 );
   HIPCHK( hipMalloc( &ctx->d_slow, ( ns + 1 ) * sizeof(u32) ), -1 );
-  { char const * h = getenv( "FDGPU_HALF" );                /* A/B knob: 0 = full-length walk + deferred R check */
-    ctx->half = h ? atoi( h ) : FD_HALF;
-    char const * fs = getenv( "FDGPU_HALF_FORCE_SLOW" );
-    ctx->half_force_slow = fs ? (u32)strtoul( fs, NULL, 0 ) : 0u; }
+  fdgpu_debug_opts_t dbg; debug_opts_get( &dbg );   /* test / A/B choices (fdgpu_debug_set_opts), never the environment */
+  ctx->half = dbg.half >= 0 ? dbg.half : FD_HALF;
+  ctx->half_force_slow = dbg.half_force_slow;
   if( ctx->half ) {
     HIPCHK( hipMalloc( &ctx->d_tabR, ns * FD_ATAB_STORED * 8 * sizeof(uint4) ), -1 );
     HIPCHK( hipMalloc( &ctx->d_digR, ns * FD_HDIG ), -1 );
     HIPCHK( hipMalloc( &ctx->d_htop, ns ), -1 );
     HIPCHK( hipMalloc( &ctx->d_btab2, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), -1 );
   }
-  { char const * e = getenv( "FDGPU_SMALL_BATCH_MAX" );   /* A/B knob: signatures at or below take the latency path */
-    ctx->small_max = e ? strtoul( e, NULL, 0 ) : FD_SMALL_BATCH_MAX;
-    char const * dl = getenv( "FDGPU_DSM_LANES" );
-    ctx->dsm_lanes = dl ? atoi( dl ) : 0;
-    char const * nf = getenv( "FDGPU_NOFOLD_MAX" );   /* A/B knob: fd_dsm_kernel<0> (no carry fold) up to here */
-    ctx->nofold_max = nf ? strtoul( nf, NULL, 0 ) : FD_NOFOLD_MAX; }
+  ctx->small_max  = dbg.small_batch_max >= 0 ? (unsigned long)dbg.small_batch_max : FD_SMALL_BATCH_MAX;
+  ctx->dsm_lanes  = dbg.dsm_lanes;
+  ctx->nofold_max = dbg.nofold_max >= 0 ? (unsigned long)dbg.nofold_max : FD_NOFOLD_MAX;
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
@@ -2182,14 +2255,15 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
     hipLaunchKernelGGL( fd_btab_kernel, dim3((FD_BTAB_ENTRIES + 255)/256), dim3(256), 0, ctx->stream, ctx->d_btab2, 120 );
   HIPCHK( hipGetLastError(), -1 );
   for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) HIPCHK( hipEventCreateWithFlags( &ctx->slot[i].done, hipEventDisableTiming ), -1 );
-  HIPCHK( hipHostMalloc( (void **)&ctx->h_flag, ( fdgpu_ed25519_ctx_t::NSLOT + 1 ) * sizeof(unsigned long), hipHostMallocDefault ), -1 );
-  for( int i=0; i<=fdgpu_ed25519_ctx_t::NSLOT; i++ ) ctx->h_flag[i] = 0UL;   /* [NSLOT]: stream_wait's word */
+  HIPCHK( hipHostMalloc( (void **)&ctx->h_flag, ( fdgpu_ed25519_ctx_t::NSLOT + 2 ) * sizeof(unsigned long), hipHostMallocDefault ), -1 );
+  for( int i=0; i<=fdgpu_ed25519_ctx_t::NSLOT+1; i++ ) ctx->h_flag[i] = 0UL;   /* [NSLOT]: stream_wait's word, [NSLOT+1]: gathers */
+  HIPCHK( hipMalloc( &ctx->d_gcnt, sizeof(unsigned long) ), -1 );
+  HIPCHK( hipMemsetAsync( ctx->d_gcnt, 0, sizeof(unsigned long), ctx->stream ), -1 );
   HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_flag, (void *)ctx->h_flag, 0 ), -1 );
   /* slot 0 now (the synchronous host calls stage through it); the async
      pipeline's other slots on first use (slot_bufs) */
   if( max_payload_bytes && slot_bufs( ctx, 0 ) ) return -1;
   ctx->cur = 0; ctx->rec_fp_off = -1;
-  { char const * g = getenv( "FDGPU_GATHER_DMA" ); ctx->gather_dma = g ? atoi( g ) != 0 : FD_GATHER_DMA; }
   HIPCHK( hipStreamSynchronize( ctx->stream ), -1 );
   return 0;
 }
@@ -2234,10 +2308,13 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
     (void)hipFree( sl.d_dtag );
     if( sl.h_gat     ) (void)hipHostFree( sl.h_gat );
     (void)hipFree( sl.d_payload ); (void)hipFree( sl.d_desc ); (void)hipFree( sl.d_txn_out );
-    (void)hipFree( sl.d_img ); (void)hipFree( sl.d_fp ); (void)hipFree( sl.d_gat );
+    (void)hipFree( sl.d_img ); (void)hipFree( sl.d_fp ); (void)hipFree( sl.d_ovr );
     if( sl.done ) (void)hipEventDestroy( sl.done );
   }
   if( ctx->cstream ) { (void)hipStreamSynchronize( ctx->cstream ); (void)hipStreamDestroy( ctx->cstream ); }
+  if( ctx->gstream ) { (void)hipStreamSynchronize( ctx->gstream ); (void)hipStreamDestroy( ctx->gstream ); }
+  if( ctx->gev ) (void)hipEventDestroy( ctx->gev );
+  (void)hipFree( ctx->d_gcnt );
   if( ctx->h_flag ) (void)hipHostFree( (void *)ctx->h_flag );
   for( unsigned long i=0; i<FD_PIPE_MAX; i++ ) if( ctx->pipe_ev[i] ) (void)hipEventDestroy( ctx->pipe_ev[i] );
   if( ctx->stream ) (void)hipStreamDestroy( ctx->stream );
@@ -2586,18 +2663,20 @@ fdgpu_txn_parse_device( unsigned char const * d_payload, fdgpu_txn_raw_t const *
   if( txn_cnt >= (1UL<<31) || ( d_img && ( img_stride < 852UL || img_stride > 0xffffffffUL ) ) ) { fd_err = "bad arguments"; return -1; }
   unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, (hipStream_t)stream, d_payload, d_raw, (u32)txn_cnt,
-                      (fdgpu_txn_desc_t *)NULL, (unsigned char *)NULL, d_img, (u32)img_stride, d_fp, 0UL, (u64 *)NULL );
+                      (fdgpu_txn_desc_t *)NULL, (unsigned char *)NULL, d_img, (u32)img_stride, d_fp, 0UL, (u64 *)NULL,
+                      (unsigned char const *)NULL );
   HIPCHK( hipGetLastError(), -3 );
   return 0;
 }
 
 static int launch_raw( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_raw_t const * d_raw,
                        unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, unsigned char * d_img,
-                       unsigned long img_stride, unsigned short * d_fp, hipStream_t st, u64 * d_dtag = NULL ) {
+                       unsigned long img_stride, unsigned short * d_fp, hipStream_t st, u64 * d_dtag = NULL,
+                       unsigned char const * d_ovr = NULL ) {
   if( !txn_cnt ) return 0;
   unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, st, d_payload, d_raw, (u32)txn_cnt,
-                      ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp, (u64)ctx->dedup_seed, d_dtag );
+                      ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp, (u64)ctx->dedup_seed, d_dtag, d_ovr );
   HIPCHK( hipGetLastError(), -3 );
   return launch_batch( ctx, d_payload, ctx->d_rdesc, txn_cnt, sig_cnt, d_txn_out, NULL, st, ctx->d_pflag );
 }
@@ -2672,6 +2751,24 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
    ahead of the work it waits for in a shared queue.  Overlap of one
    context's upload with another's kernels comes from running several
    contexts, one per verify tile.) */
+/* launch the gather of slot sl's records not yet gathered (mode 3) on the
+   context's gather stream; returns how many, or < 0 */
+static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
+  unsigned long n = sl.txn_cnt - sl.gathered;
+  if( !n ) return 0;
+  if( !ctx->gstream ) {
+    HIPCHK( hipStreamCreateWithFlags( &ctx->gstream, hipStreamNonBlocking ), -2 );
+    HIPCHK( hipEventCreateWithFlags( &ctx->gev, hipEventDisableTiming ), -2 );
+  }
+  unsigned long target = ctx->g_launched + n;
+  hipLaunchKernelGGL( fd_gather_kernel, dim3( (unsigned)n ), dim3( 64 ), 0, ctx->gstream, sl.g_dev + sl.gathered,
+                      sl.d_payload, sl.ref_dev + sl.ref_lo, sl.d_ovr + sl.gathered, ctx->d_gcnt,
+                      (unsigned long *)( ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT + 1 ), target );
+  HIPCHK( hipGetLastError(), -2 );
+  ctx->g_launched = target; sl.gathered = sl.txn_cnt;
+  return (int)n;
+}
+
 static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i );
 static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
   unsigned long t0 = fd_now_ns();
@@ -2684,11 +2781,11 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
   hipStream_t st = ctx->stream;
   if( sl.mode==2 ) {   /* in place: one upload of the caller's region range, no host copy */
     HIPCHK( hipMemcpyAsync( sl.d_payload, sl.ref_base + sl.ref_lo, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
-  } else if( sl.mode==3 ) {   /* gathered: the GPU reads each record from the caller's in region */
-    HIPCHK( hipMemcpyAsync( sl.d_gat, sl.h_gat, sl.txn_cnt * sizeof(fd_gather), hipMemcpyHostToDevice, st ), -2 );
-    hipLaunchKernelGGL( fd_gather_kernel, dim3( (unsigned)sl.txn_cnt ), dim3( 64 ), 0, st, sl.d_gat, sl.d_payload,
-                        ctx->gather_dma ? (unsigned char *)NULL : sl.ref_dev + sl.ref_lo );
-    HIPCHK( hipGetLastError(), -2 );
+  } else if( sl.mode==3 ) {   /* gathered: the rest of the records, then this stream waits for every gather */
+    int g = gather_launch( ctx, sl );
+    if( g < 0 ) return g;
+    HIPCHK( hipEventRecord( ctx->gev, ctx->gstream ), -2 );
+    HIPCHK( hipStreamWaitEvent( st, ctx->gev, 0 ), -2 );
   } else {
     memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
     HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
@@ -2696,18 +2793,16 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
   HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
   int rc = sl.mode
          ? launch_raw( ctx, sl.d_payload, (fdgpu_txn_raw_t const *)sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out,
-                       sl.d_img, FDGPU_TXN_IMG_STRIDE, sl.d_fp, st, ctx->dedup ? (u64 *)sl.d_dtag : (u64 *)NULL )
+                       sl.d_img, FDGPU_TXN_IMG_STRIDE, sl.d_fp, st, ctx->dedup ? (u64 *)sl.d_dtag : (u64 *)NULL,
+                       sl.mode==3 ? sl.d_ovr : (unsigned char const *)NULL )
          : launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
   if( rc ) return rc;
   HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
   if( sl.mode==3 ) {   /* gathered: the images go into the out region, only the footprints come back */
     hipLaunchKernelGGL( fd_img_scatter_kernel, dim3( (unsigned)sl.txn_cnt ), dim3( 64 ), 0, st,
                         (fdgpu_txn_raw_t const *)sl.d_desc, sl.d_img, (u32)FDGPU_TXN_IMG_STRIDE, sl.d_fp,
-                        ctx->gather_dma ? sl.d_payload : sl.ref_dev + sl.ref_lo, ctx->rec_fp_off );
+                        sl.ref_dev + sl.ref_lo, ctx->rec_fp_off );
     HIPCHK( hipGetLastError(), -2 );
-    if( ctx->gather_dma )   /* records + images, as laid out in the out region, in one DMA */
-      HIPCHK( hipMemcpyAsync( (unsigned char *)sl.ref_base + sl.ref_lo, sl.d_payload, sl.payload_used + 856UL,
-                              hipMemcpyDeviceToHost, st ), -2 );
     HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
   } else if( sl.mode ) {   /* raw and in-place raw */
     HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
@@ -2799,7 +2894,8 @@ static int slot_raw_bufs( fdgpu_ed25519_ctx_t * ctx, fd_slot * sl ) {
   HIPCHK( hipHostMalloc( (void **)&sl->h_dtag, ctx->max_txn * sizeof(unsigned long), hipHostMallocDefault ), -3 );
   HIPCHK( hipMalloc( (void **)&sl->d_dtag, ctx->max_txn * sizeof(unsigned long) ), -3 );
   HIPCHK( hipHostMalloc( (void **)&sl->h_gat, ctx->max_txn * sizeof(fd_gather), hipHostMallocDefault ), -3 );
-  HIPCHK( hipMalloc( (void **)&sl->d_gat, ctx->max_txn * sizeof(fd_gather) ), -3 );
+  HIPCHK( hipHostGetDevicePointer( (void **)&sl->g_dev, (void *)sl->h_gat, 0 ), -3 );
+  HIPCHK( hipMalloc( (void **)&sl->d_ovr, ctx->max_txn ), -3 );
   return 0;
 }
 
@@ -2947,16 +3043,22 @@ fdgpu_device_numa_node( int device ) {
    out region dst_base.  Records of one batch lie at increasing dst
    addresses (a lower one starts a new batch), chunk aligned. */
 extern "C" int
-fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char * dst_base,
-                                 unsigned char * dst, unsigned short copy_sz, unsigned short payload_off,
-                                 unsigned short payload_sz, unsigned long tag ) {
+fdgpu_ed25519_submit_raw_gather_chk( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char * dst_base,
+                                     unsigned char * dst, unsigned short copy_sz, unsigned short payload_off,
+                                     unsigned short payload_sz, unsigned long tag, unsigned long const * seq_addr,
+                                     unsigned long seq ) {
   if( (unsigned)payload_off + payload_sz > copy_sz || ( (uintptr_t)src & 15 ) || ( (uintptr_t)( dst - dst_base ) & 15 ) ||
-      ( ctx->rec_fp_off >= 0 && ( payload_off > 255u || (unsigned)ctx->rec_fp_off + 2u > payload_off ) ) ) {
+      ( ctx->rec_fp_off >= 0 && ( payload_off > 255u || (unsigned)ctx->rec_fp_off + 2u > payload_off ) ) ||
+      ( (uintptr_t)seq_addr & 7 ) ) {
     fd_err = "fdgpu_ed25519_submit_raw_gather: bad record"; return -1;
   }
   unsigned long csz = ( (unsigned long)copy_sz + 15UL ) & ~15UL;
   unsigned char * dsrc = region_dev( src, csz );
   if( !dsrc ) { fd_err = "fdgpu_ed25519_submit_raw_gather: src not in a registered region"; return -3; }
+  unsigned char * dseq = NULL;
+  if( seq_addr && !( dseq = region_dev( seq_addr, sizeof(unsigned long) ) ) ) {
+    fd_err = "fdgpu_ed25519_submit_raw_gather: seq_addr not in a registered region"; return -3;
+  }
   unsigned b0 = payload_sz ? src[ payload_off ] : 0u;
   unsigned lanes = ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u;
   size_t off = (size_t)( dst - dst_base );
@@ -2978,11 +3080,61 @@ fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const 
   r._pad[0] = (unsigned char)payload_off;      /* fd_img_scatter_kernel finds the record header from it */
   fd_gather & g = sl->h_gat[ sl->txn_cnt ];
   g.src = (unsigned long)dsrc; g.dst = (unsigned)( off - sl->ref_lo ); g.sz = (unsigned)csz;
+  g.seq_addr = (unsigned long)dseq; g.seq = seq;
   sl->h_tags[ sl->txn_cnt ] = tag;
   sl->txn_cnt++; sl->sig_cnt += lanes;
   sl->ref_hi = off + csz; sl->payload_used = sl->ref_hi - sl->ref_lo;
   return 0;
 }
+
+extern "C" int
+fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char * dst_base,
+                                 unsigned char * dst, unsigned short copy_sz, unsigned short payload_off,
+                                 unsigned short payload_sz, unsigned long tag ) {
+  return fdgpu_ed25519_submit_raw_gather_chk( ctx, src, dst_base, dst, copy_sz, payload_off, payload_sz, tag, NULL, 0UL );
+}
+
+extern "C" long
+fdgpu_ed25519_gather( fdgpu_ed25519_ctx_t * ctx ) {
+  if( !ctx || ctx->fault ) return -3;
+  fd_slot & sl = ctx->slot[ ctx->cur ];
+  if( sl.state != 0 || sl.mode != 3 || sl.gathered == sl.txn_cnt ) return 0;
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  unsigned long t0 = fd_now_ns();
+  int n = gather_launch( ctx, sl );
+  ctx->launch_ns += fd_now_ns() - t0;
+  return n;
+}
+
+extern "C" unsigned long
+fdgpu_ed25519_gathered( fdgpu_ed25519_ctx_t const * ctx ) {
+  unsigned long g = ctx->h_flag[ fdgpu_ed25519_ctx_t::NSLOT + 1 ];
+  std::atomic_thread_fence( std::memory_order_acquire );
+  return g;
+}
+
+extern "C" unsigned long
+fdgpu_ed25519_gather_launched( fdgpu_ed25519_ctx_t const * ctx ) { return ctx->g_launched; }
+
+extern "C" int
+fdgpu_ed25519_gather_wait( fdgpu_ed25519_ctx_t * ctx ) {
+  if( !ctx || ctx->fault ) return -3;
+  unsigned long t0 = fd_now_ns(), last = t0;
+  while( fdgpu_ed25519_gathered( ctx ) != ctx->g_launched ) {
+    unsigned long now = fd_now_ns();
+    if( now - last > 2000000UL ) {        /* a failed gather never stores its count: ask the stream */
+      last = now;
+      hipError_t e = hipStreamQuery( ctx->gstream );
+      if( e != hipSuccess && e != hipErrorNotReady ) { set_err( "fdgpu_ed25519_gather_wait", e ); ctx->fault = 1; return -3; }
+      if( e == hipSuccess && fdgpu_ed25519_gathered( ctx ) != ctx->g_launched ) { fd_err = "gather count lost"; return -2; }
+    }
+    __builtin_ia32_pause();
+  }
+  return 0;
+}
+
+extern "C" void *
+fdgpu_host_dev_ptr( void const * p, unsigned long sz ) { return region_dev( p, sz ); }
 
 /* Drain completed slots in submission order, at most max results. */
 static unsigned long
@@ -3032,7 +3184,7 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
     n += k; sl.cursor += k;
     if( sl.cursor==sl.txn_cnt ) {
       ctx->inflight.pop_front();
-      sl.txn_cnt = 0; sl.sig_cnt = 0; sl.payload_used = 0; sl.cursor = 0; sl.state = 0;
+      sl.txn_cnt = 0; sl.sig_cnt = 0; sl.payload_used = 0; sl.cursor = 0; sl.state = 0; sl.gathered = 0;
     }
   }
   return n;
@@ -3112,13 +3264,21 @@ fdgpu_ed25519_set_record_fp_off( fdgpu_ed25519_ctx_t * ctx, int off ) {
 static std::mutex g_mu;
 static fdgpu_ed25519_ctx_t * g_ctx = NULL;
 
+static int g_dropin_device = 0, g_dropin_semantics = FDGPU_SEMANTICS_AVX512;
+
 static fdgpu_ed25519_ctx_t * global_ctx( void ) {
   if( g_ctx ) return g_ctx;
-  char const * dev = getenv( "FDGPU_DEVICE" );
-  char const * sem = getenv( "FDGPU_SEMANTICS" );
-  g_ctx = fdgpu_ed25519_ctx_new( dev ? atoi( dev ) : 0, 64, 64, 1UL<<17,
-                                 ( sem && !strcmp( sem, "ref" ) ) ? FDGPU_SEMANTICS_REF : FDGPU_SEMANTICS_AVX512 );
+  g_ctx = fdgpu_ed25519_ctx_new( g_dropin_device, 64, 64, 1UL<<17, g_dropin_semantics );
   return g_ctx;
+}
+
+extern "C" int
+fdgpu_ed25519_dropin_init( int device, int semantics ) {
+  if( semantics!=FDGPU_SEMANTICS_AVX512 && semantics!=FDGPU_SEMANTICS_REF ) { fd_err = "bad semantics"; return -1; }
+  std::lock_guard<std::mutex> lk( g_mu );
+  if( g_ctx && ( g_ctx->device != device || g_ctx->semantics != semantics ) ) { fdgpu_ed25519_ctx_delete( g_ctx ); g_ctx = NULL; }
+  g_dropin_device = device; g_dropin_semantics = semantics;
+  return global_ctx() ? 0 : -2;
 }
 
 /* drop-in for messages whose descriptor would pass 64 KiB: digests first
@@ -3128,18 +3288,20 @@ static fdgpu_ed25519_ctx_t * global_ctx( void ) {
 static int
 verify_long( fdgpu_ed25519_ctx_t * ctx, unsigned char const * msg, unsigned long msg_sz,
              unsigned char const * sigs, unsigned char const * pubs, unsigned long n ) {
+  /* the batch SHA kernel takes 32-bit sizes: refuse before allocating anything */
+  if( msg_sz > 0xffffffffUL - 64UL || n * ( 64UL + msg_sz ) > 0xffffffffUL ) { fd_err = "message too long"; return 1; }
   size_t one = 64UL + msg_sz, tot = n*one;
-  std::vector<unsigned char> buf( tot );
-  std::vector<unsigned long> off( n );
-  std::vector<unsigned int>  hsz( n );
+  std::vector<unsigned char> buf, dig;
+  std::vector<unsigned long> off;
+  std::vector<unsigned int>  hsz;
+  try { buf.resize( tot ); off.resize( n ); hsz.resize( n ); dig.resize( 64*n ); }
+  catch( std::bad_alloc const & ) { fd_err = "verify_long: out of host memory"; return 1; }
   for( unsigned long j=0; j<n; j++ ) {
     unsigned char * b = buf.data() + j*one;
     memcpy( b, sigs + 64*j, 32 ); memcpy( b + 32, pubs + 32*j, 32 );
     if( msg_sz ) memcpy( b + 64, msg, msg_sz );
     off[j] = j*one; hsz[j] = (unsigned)one;
   }
-  if( tot > 0xffffffffUL ) { fd_err = "message too long"; return 1; }
-  std::vector<unsigned char> dig( 64*n );
   if( fdgpu_sha512_batch_host( ctx->device, buf.data(), tot, off.data(), hsz.data(), n, dig.data() ) ) return 1;
   unsigned char pl[ 96*16 ];
   memcpy( pl, sigs, 64*n ); memcpy( pl + 64*n, pubs, 32*n );

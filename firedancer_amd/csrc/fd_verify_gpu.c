@@ -173,7 +173,12 @@ struct fdgpu_mcache {
   ulong       depth;
   mc_line_t * line;
   int         own;          /* line[] allocated here (else it lives in a shared link) */
+  int         reg;          /* line[] registered with the GPU here (fdgpu_vtile_set_in_links) */
 };
+
+/* bytes of an mcache's lines, whole pages (page-aligned line arrays can be
+   registered with the GPU without sharing a page with anything else) */
+static ulong mc_bytes( ulong depth ) { return ( depth * sizeof(mc_line_t) + 4095UL ) & ~4095UL; }
 
 static void mc_init_lines( mc_line_t * line, ulong depth, ulong seq0 ) {
   memset( (void *)line, 0, depth * sizeof(mc_line_t) );
@@ -187,13 +192,18 @@ fdgpu_mcache_new( ulong depth, ulong seq0 ) {
   fdgpu_mcache_t * mc = (fdgpu_mcache_t *)calloc( 1, sizeof(fdgpu_mcache_t) );
   if( !mc ) return NULL;
   mc->depth = depth; mc->own = 1;
-  mc->line = (mc_line_t *)aligned_alloc( 64, depth * sizeof(mc_line_t) + 64 );
+  mc->line = (mc_line_t *)aligned_alloc( 4096, mc_bytes( depth ) );
   if( !mc->line ) { free( mc ); return NULL; }
   mc_init_lines( mc->line, depth, seq0 );
   return mc;
 }
 
-void fdgpu_mcache_delete( fdgpu_mcache_t * mc ) { if( mc ) { if( mc->own ) free( mc->line ); free( mc ); } }
+void fdgpu_mcache_delete( fdgpu_mcache_t * mc ) {
+  if( !mc ) return;
+  if( mc->reg ) fdgpu_host_unregister( mc->line );
+  if( mc->own ) free( mc->line );
+  free( mc );
+}
 
 static inline void
 mc_publish( mc_line_t * l, ulong seq, ulong sig, unsigned chunk, unsigned sz, unsigned tsorig, unsigned tspub ) {
@@ -276,11 +286,12 @@ vt_fence( void ) {
 typedef struct {
   ulong seq, tsorig, chunk;
   ulong bundle_id;                       /* from the frag header, read in during_frag */
+  ulong cidx;                            /* zero-copy: the frag's index among context k's gathered submissions */
   unsigned short payload_sz;
   int   k;                               /* engine context the frag's batch went to */
 } vt_pend_t;
 
-/* Engine contexts per tile (env FDGPU_VTILE_CTX, 1..VT_NCTX_MAX, default 2).
+/* Engine contexts per tile (fdgpu_vtile_opts_t.nctx, 1..VT_NCTX_MAX, default 2).
    A context runs its batches in order on one HIP stream, so with one
    context a frag that arrives while a batch runs waits for all of it.
    With several, the tile fills them in turn and launches staggered by
@@ -294,8 +305,17 @@ struct fdgpu_vtile {
   fdgpu_ed25519_ctx_t * ctx[ VT_NCTX_MAX ];
   int                   device, semantics;   /* to recreate a faulted context */
   int                   fault_seen[ VT_NCTX_MAX ];
-  int                   gpu_tag;         /* HA dedup tags from the GPU (env FDGPU_VTILE_GPU_TAG, default 1) */
+  fdgpu_vtile_opts_t    opt;             /* with the defaults filled in */
+  int                   gpu_tag;         /* HA dedup tags from the GPU (!opt.host_dedup_tag) */
   ulong                 min_batch, max_wait_ns, fill_t0;   /* see fdgpu_vtile_housekeep */
+  /* zero-copy intake: the GPU copies of the frags (fdgpu_ed25519_gather) */
+  ulong                 sub_cnt[ VT_NCTX_MAX ];            /* gathered submissions per context, cumulative */
+  ulong                 copy_cursor;     /* pending-ring counter: frags below it are known to be copied */
+  ulong                 copy_t0;         /* host time the oldest frag not yet given to a gather was taken (0: none) */
+  ulong                 uncopied[ FDGPU_VTILE_IN_MAX ];    /* per in link: frags taken and not yet known copied */
+  ulong                 copied_next[ FDGPU_VTILE_IN_MAX ]; /* per in link: 1 + seq of the last frag known copied */
+  struct { ulong target, t; } cq[ VT_NCTX_MAX ][ 8 ];     /* early copies in flight: gathered count they complete at */
+  ulong                 cq_head[ VT_NCTX_MAX ], cq_tail[ VT_NCTX_MAX ];
   fdgpu_vtile_gpu_metrics_t gm;
   int                   nctx, fill;      /* contexts, the one taking frags */
   ulong                 launch_ns[ VT_NCTX_MAX ];
@@ -313,7 +333,6 @@ struct fdgpu_vtile {
   /* zero-copy intake (fdgpu_vtile_set_in_link): frags stay in the in
      dcache, the GPU gathers them; in_mc (optional) for the overrun check */
   int                   zc;
-  fdgpu_mcache_t const * in_mc;          /* (the single-link form: in_mcs[0]) */
   fdgpu_mcache_t const * in_mcs[ FDGPU_VTILE_IN_MAX ];
   int                   n_in;
   ulong                 overruns;
@@ -335,10 +354,9 @@ vt_ctx_new( fdgpu_vtile_t const * vt ) {
   ulong b = vt->batch;
   fdgpu_ed25519_ctx_t * c = fdgpu_ed25519_ctx_new( vt->device, b, 16UL*b, b*2304UL + 1024UL, vt->semantics );
   if( c ) {
-    /* latency path for batches up to half the batch limit (env FDGPU_VTILE_SMALL_MAX overrides) */
+    /* latency path for batches up to half the batch limit (opt.small_max overrides) */
     ulong sm = fdgpu_ed25519_set_small_batch_max( c, 0UL );
-    char const * e = getenv( "FDGPU_VTILE_SMALL_MAX" );
-    fdgpu_ed25519_set_small_batch_max( c, e ? strtoul( e, NULL, 0 ) : ( sm < b/2UL ? sm : b/2UL ) );
+    fdgpu_ed25519_set_small_batch_max( c, vt->opt.small_max ? vt->opt.small_max : ( sm < b/2UL ? sm : b/2UL ) );
     /* the GPU computes the HA dedup tags and, for gathered records, stores
        txn_t_sz: after_frag then touches neither payload nor record */
     fdgpu_ed25519_set_dedup( c, vt->gpu_tag, vt->seed );
@@ -349,20 +367,30 @@ vt_ctx_new( fdgpu_vtile_t const * vt ) {
 
 fdgpu_vtile_t *
 fdgpu_vtile_new( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ulong out_dcache_bytes, int semantics ) {
+  return fdgpu_vtile_new_opts( device, batch_txn, tcache_depth, seed, out_dcache_bytes, semantics, NULL );
+}
+
+fdgpu_vtile_t *
+fdgpu_vtile_new_opts( int device, ulong batch_txn, ulong tcache_depth, ulong seed, ulong out_dcache_bytes, int semantics,
+                      fdgpu_vtile_opts_t const * opts ) {
   if( !batch_txn || !tcache_depth || out_dcache_bytes < 8UL*VT_RESERVE_MAX ) return NULL;
   fdgpu_vtile_t * vt = (fdgpu_vtile_t *)calloc( 1, sizeof(fdgpu_vtile_t) );
   if( !vt ) return NULL;
+  if( opts ) vt->opt = *opts;
+  if( !vt->opt.nctx )         vt->opt.nctx = 2;
+  if( !vt->opt.max_wait_ns )  vt->opt.max_wait_ns = 2000000UL;
+  if( !vt->opt.copy_wait_ns ) vt->opt.copy_wait_ns = FDGPU_VTILE_COPY_WAIT_NS;
+  if( !vt->opt.copy_min )     vt->opt.copy_min = FDGPU_VTILE_COPY_MIN;
   /* staging arena of a batch = its range of the out dcache (in-place submits): up to
      batch_txn records of at most VT_RESERVE_MAX bytes (rounded to chunk pairs) */
-  char const * ne = getenv( "FDGPU_VTILE_CTX" );
-  vt->nctx = ne ? atoi( ne ) : 2;
+  vt->nctx = vt->opt.nctx;
   if( vt->nctx < 1 ) vt->nctx = 1;
   if( vt->nctx > VT_NCTX_MAX ) vt->nctx = VT_NCTX_MAX;
+  vt->opt.nctx = vt->nctx;
   vt->batch_ns = 500e3;
   vt->device = device; vt->semantics = semantics; vt->batch = batch_txn; vt->seed = seed;
-  { char const * g = getenv( "FDGPU_VTILE_GPU_TAG" ); vt->gpu_tag = g ? atoi( g ) != 0 : 1; }
-  { char const * m = getenv( "FDGPU_VTILE_MIN_BATCH" ); vt->min_batch = m ? strtoul( m, NULL, 0 ) : 0UL;
-    char const * w = getenv( "FDGPU_VTILE_MAX_WAIT_US" ); vt->max_wait_ns = 1000UL * ( w ? strtoul( w, NULL, 0 ) : 2000UL ); }
+  vt->gpu_tag = !vt->opt.host_dedup_tag;
+  vt->min_batch = vt->opt.min_batch; vt->max_wait_ns = vt->opt.max_wait_ns;
   int ctx_ok = 1;
   for( int k=0; k<vt->nctx; k++ ) if( !( vt->ctx[k] = vt_ctx_new( vt ) ) ) ctx_ok = 0;
   vt->tcache = fdgpu_tcache_new( tcache_depth );
@@ -445,15 +473,20 @@ fdgpu_vtile_faulted( fdgpu_vtile_t const * vt ) {
 
 int
 fdgpu_vtile_recover( fdgpu_vtile_t * vt ) {
+  int rc = 0;
   for( int k=0; k<vt->nctx; k++ ) {
     if( !fdgpu_ed25519_faulted( vt->ctx[k] ) ) continue;
-    for( ulong q=vt->pend_head; q<vt->pend_tail; q++ ) if( vt->pend[ q % vt->pend_cap ].k == k ) return -1;
+    int busy = 0;
+    for( ulong q=vt->pend_head; q<vt->pend_tail && !busy; q++ ) busy = vt->pend[ q % vt->pend_cap ].k == k;
+    if( busy ) { rc = -1; continue; }
+    /* the replacement first: if it cannot be made, the faulted context stays (and stays skipped) */
+    fdgpu_ed25519_ctx_t * c = vt_ctx_new( vt );
+    if( !c ) { if( !rc ) rc = -2; continue; }
     fdgpu_ed25519_ctx_delete( vt->ctx[k] );
-    vt->ctx[k] = vt_ctx_new( vt );
-    vt->busy[k] = 0; vt->fault_seen[k] = 0;
-    if( !vt->ctx[k] ) return -2;
+    vt->ctx[k] = c;
+    vt->busy[k] = 0; vt->fault_seen[k] = 0; vt->sub_cnt[k] = 0UL; vt->cq_head[k] = vt->cq_tail[k] = 0UL;
   }
-  return 0;
+  return rc;
 }
 
 void
@@ -488,10 +521,79 @@ int
 fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_mc, int n ) {
   if( vt->pend_tail != vt->pend_head ) return -1;       /* switch only while idle */
   if( n < 1 || n > FDGPU_VTILE_IN_MAX ) return -1;
-  vt->zc = 1; vt->n_in = n; vt->in_mc = NULL;
+  /* the GPU re-reads each frag's mcache line after its copy: the lines must be mapped for it */
+  for( int i=0; i<n; i++ ) {
+    fdgpu_mcache_t * mc = (fdgpu_mcache_t *)in_mc[i];
+    if( !mc || fdgpu_host_dev_ptr( mc->line, mc->depth * sizeof(mc_line_t) ) ) continue;
+    if( fdgpu_host_register( mc->line, mc_bytes( mc->depth ) ) ) return -2;
+    mc->reg = 1;
+  }
+  vt->zc = 1; vt->n_in = n;
   for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) vt->in_mcs[i] = i < n ? in_mc[i] : NULL;
-  for( int i=0; i<n; i++ ) if( in_mc[i] ) vt->in_mc = in_mc[i];   /* any overrun check at all */
+  for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) { vt->uncopied[i] = 0UL; vt->copied_next[i] = 0UL; }
+  vt->copy_cursor = vt->pend_tail; vt->copy_t0 = 0UL;
   return 0;
+}
+
+/* a frag's copy has completed (or it left the pipeline without one) */
+static inline void vt_copied( fdgpu_vtile_t * vt, vt_pend_t const * p ) {
+  int l = FDGPU_VTILE_SEQ_LINK( p->seq );
+  vt->uncopied[l]--; vt->copied_next[l] = FDGPU_VTILE_SEQ_SEQ( p->seq ) + 1UL;
+}
+
+/* an early copy of context k was launched (for its latency metric) */
+static void vt_copy_launched( fdgpu_vtile_t * vt, int k ) {
+  vt->gm.copies++;
+  if( vt->cq_tail[k] - vt->cq_head[k] >= 8UL ) return;   /* (not timed) */
+  vt->cq[k][ vt->cq_tail[k] % 8UL ].target = fdgpu_ed25519_gather_launched( vt->ctx[k] );
+  vt->cq[k][ vt->cq_tail[k] % 8UL ].t = now_ns();
+  vt->cq_tail[k]++;
+}
+
+/* advance copy_cursor over the frags whose gathers have completed */
+static void vt_copy_poll( fdgpu_vtile_t * vt ) {
+  if( !vt->zc ) return;
+  ulong g[ VT_NCTX_MAX ], now = 0UL;
+  for( int k=0; k<vt->nctx; k++ ) {
+    g[k] = fdgpu_ed25519_gathered( vt->ctx[k] );
+    while( vt->cq_head[k] < vt->cq_tail[k] && vt->cq[k][ vt->cq_head[k] % 8UL ].target <= g[k] ) {
+      if( !now ) now = now_ns();
+      ulong lat = now - vt->cq[k][ vt->cq_head[k] % 8UL ].t;
+      vt->gm.copy_lat_ns_sum += lat; vt->gm.copy_lat_n++;
+      if( lat > vt->gm.copy_lat_ns_max ) vt->gm.copy_lat_ns_max = lat;
+      vt->cq_head[k]++;
+    }
+  }
+  if( vt->copy_cursor < vt->pend_head ) vt->copy_cursor = vt->pend_head;   /* (after_frags accounts those) */
+  while( vt->copy_cursor < vt->pend_tail ) {
+    vt_pend_t const * p = &vt->pend[ vt->copy_cursor % vt->pend_cap ];
+    if( p->cidx >= g[ p->k ] ) break;
+    vt_copied( vt, p );
+    vt->copy_cursor++;
+  }
+}
+
+int
+fdgpu_vtile_copy( fdgpu_vtile_t * vt, int blocking ) {
+  if( !vt->zc ) return 0;
+  int rc = 0;
+  for( int k=0; k<vt->nctx; k++ ) {
+    if( fdgpu_ed25519_faulted( vt->ctx[k] ) ) continue;
+    long n = fdgpu_ed25519_gather( vt->ctx[k] );
+    if( n < 0 ) { rc = (int)n; continue; }
+    if( n ) vt_copy_launched( vt, k );
+    if( blocking && fdgpu_ed25519_gather_wait( vt->ctx[k] ) ) rc = -3;
+  }
+  vt->copy_t0 = 0UL;
+  vt_copy_poll( vt );
+  return rc;
+}
+
+ulong
+fdgpu_vtile_copy_state( fdgpu_vtile_t const * vt, int link, ulong * copied_next ) {
+  if( link < 0 || link >= FDGPU_VTILE_IN_MAX ) { *copied_next = 0UL; return 0UL; }
+  *copied_next = vt->copied_next[link];
+  return vt->uncopied[link];
 }
 
 ulong
@@ -502,6 +604,19 @@ fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt ) {
 int
 fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
   ulong filling, inflight, now = now_ns();
+  if( vt->zc ) {
+    /* the GPU copy of the frags taken since the last one: once the oldest has waited copy_wait_ns or
+       copy_min are waiting -- what bounds a frag's exposure to a lapping producer (and a reliable
+       link's credit) to about copy_wait_ns plus one gather, whatever the batch size */
+    int f = vt->fill;
+    if( vt->copy_t0 && !fdgpu_ed25519_faulted( vt->ctx[f] ) &&
+        ( now - vt->copy_t0 >= vt->opt.copy_wait_ns ||
+          vt->sub_cnt[f] - fdgpu_ed25519_gather_launched( vt->ctx[f] ) >= vt->opt.copy_min ) ) {
+      if( fdgpu_ed25519_gather( vt->ctx[f] ) > 0 ) vt_copy_launched( vt, f );
+      vt->copy_t0 = 0UL;
+    }
+    vt_copy_poll( vt );
+  }
   /* batch duration: a context's batches have drained (inflight counts
      launched slots not yet fully polled) */
   for( int k=0; k<vt->nctx; k++ ) {
@@ -550,10 +665,15 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   if( fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ) ) return -3;
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
   int rc;
-  if( vt->zc ) {   /* the GPU copies the frag into dst itself (no host copy) */
-    rc = fdgpu_ed25519_submit_raw_gather( vt->ctx[ vt->fill ], (uchar const *)frag, vt->dcache, dst,
-                                          (unsigned short)( FDGPU_TXNM_HDR_SZ + in->payload_sz ),
-                                          (unsigned short)FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
+  int link = FDGPU_VTILE_SEQ_LINK( seq );
+  if( vt->zc ) {   /* the GPU copies the frag into dst itself (no host copy) and re-checks its mcache line */
+    if( link >= vt->n_in ) return -4;                   /* a link set_in_links was not told about */
+    fdgpu_mcache_t const * mc = vt->in_mcs[ link ];
+    ulong const * seq_addr = mc ? (ulong const *)&mc->line[ FDGPU_VTILE_SEQ_SEQ( seq ) & ( mc->depth - 1UL ) ].seq : NULL;
+    rc = fdgpu_ed25519_submit_raw_gather_chk( vt->ctx[ vt->fill ], (uchar const *)frag, vt->dcache, dst,
+                                              (unsigned short)( FDGPU_TXNM_HDR_SZ + in->payload_sz ),
+                                              (unsigned short)FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail,
+                                              seq_addr, FDGPU_VTILE_SEQ_SEQ( seq ) );
   } else {
     vt_copy( dst, (uchar const *)frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
     rc = fdgpu_ed25519_submit_raw_ref( vt->ctx[ vt->fill ], vt->dcache, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
@@ -561,6 +681,11 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   if( rc ) return rc;
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
   p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill;
+  if( vt->zc ) {
+    p->cidx = vt->sub_cnt[ vt->fill ]++;
+    vt->uncopied[ link ]++;
+    if( !vt->copy_t0 ) vt->copy_t0 = now_ns();
+  }
   if( vt->min_batch ) {                          /* first frag of the filling batch: its wait starts */
     ulong f, i; fdgpu_ed25519_pipeline_state( vt->ctx[ vt->fill ], &f, &i );
     if( f == 1UL ) vt->fill_t0 = now_ns();
@@ -581,15 +706,10 @@ static int
 vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, unsigned fp, ulong tag,
           fdgpu_vtile_done_t * d ) {
   d->seq = p->seq; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
-  if( vt->zc && vt->in_mc ) {
-    /* zero-copy: the GPU read the frag at batch launch, after during_frag.
-       If the producer has since reused the frag's mcache line, its dcache
-       bytes may have been overwritten before that read: drop it, as the
-       stem loop drops a frag overrun during its copy. */
-    fdgpu_mcache_t const * mc = vt->in_mcs[ FDGPU_VTILE_SEQ_LINK( p->seq ) & ( FDGPU_VTILE_IN_MAX - 1 ) ];
-    fdgpu_frag_meta_t m;
-    if( mc && fdgpu_mcache_poll( mc, FDGPU_VTILE_SEQ_SEQ( p->seq ), &m ) != 0 ) { vt->overruns++; return FDGPU_VTILE_OVERRUN; }
-  }
+  /* zero-copy: the GPU re-read the frag's mcache line right after copying it and found it reused
+     -- the stem's "overrun while reading" (fd_stem.c:667-686), decided at copy time: the frag
+     never reaches after_frag in the reference, so no bundle state or metric changes */
+  if( code == FDGPU_ERR_OVERRUN ) { vt->overruns++; return FDGPU_VTILE_OVERRUN; }
   fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( vt->dcache + p->chunk * FDGPU_CHUNK_SZ );
   if( !vt->zc ) txnm->txn_t_sz = (unsigned short)fp;
   int is_bundle = p->bundle_id != 0UL;
@@ -625,6 +745,12 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
   return FDGPU_VTILE_PUBLISH;
 }
 
+/* the frag at the head leaves the pending ring (a verdict implies its copy completed) */
+static inline void vt_pop( fdgpu_vtile_t * vt, vt_pend_t const * p ) {
+  if( vt->zc && vt->copy_cursor == vt->pend_head ) { vt_copied( vt, p ); vt->copy_cursor++; }
+  vt->pend_head++;
+}
+
 ulong
 fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max, int blocking ) {
   ulong n = 0UL;
@@ -650,7 +776,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
         d->seq = p->seq; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
         d->result = FDGPU_VTILE_GPU_FAULT;
         vt->gm.gpu_fault_frags++;
-        vt->pend_head++; n++;
+        vt_pop( vt, p ); n++;
       }
       continue;
     }
@@ -677,14 +803,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
       /* the random accesses of after_frag are the tcache map slots (of this tag, and of the
          tag the insert evicts) and, with an in link, the frag's mcache line: start them a
          few completions ahead */
-      if( i + 8UL < k ) {
-        if( vt->gpu_tag ) tc_prefetch( vt->tcache, vt->p_dtag[ i + 8UL ], 8UL );
-        if( vt->in_mc ) {
-          ulong s8 = vt->pend[ ( vt->pend_head + 8UL ) % vt->pend_cap ].seq;
-          fdgpu_mcache_t const * mc = vt->in_mcs[ FDGPU_VTILE_SEQ_LINK( s8 ) & ( FDGPU_VTILE_IN_MAX - 1 ) ];
-          if( mc ) __builtin_prefetch( &mc->line[ FDGPU_VTILE_SEQ_SEQ( s8 ) & ( mc->depth - 1UL ) ] );
-        }
-      }
+      if( i + 8UL < k && vt->gpu_tag ) tc_prefetch( vt->tcache, vt->p_dtag[ i + 8UL ], 8UL );
       if( !vt->zc && vt->pend_head + 4UL < vt->pend_tail ) {   /* host-copied records: the header line */
         uchar * r = vt->dcache + vt->pend[ ( vt->pend_head + 4UL ) % vt->pend_cap ].chunk * FDGPU_CHUNK_SZ;
         __builtin_prefetch( r, 1 );
@@ -693,7 +812,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
       /* tags are the pending counter: completions come back in order */
       out[n].result = vt_after( vt, p, (int)vt->p_codes[i], vt->p_img + i*FDGPU_TXN_IMG_STRIDE, vt->p_fp[i],
                                 vt->p_dtag[i], &out[n] );
-      vt->pend_head++; n++;
+      vt_pop( vt, p ); n++;
     }
     vt->gm.after_ns += now_ns() - tp;
     blocking = 0;
@@ -822,7 +941,8 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   ulong T = (ulong)cfg->tiles;
   ulong o = al64( sizeof(link_hdr_t) );
   ulong off_mcache[ LINK_PROD_MAX ] = { 0 };
-  for( ulong q=0; q<Q; q++ ) { off_mcache[q] = o;  o = al64( o + depth * sizeof(mc_line_t) ); }
+  o = ( o + 4095UL ) & ~4095UL;                /* page-aligned line arrays: registered with the GPU (overrun check) */
+  for( ulong q=0; q<Q; q++ ) { off_mcache[q] = o;  o += mc_bytes( depth ); }
   ulong off_chunk  = o;  o = al64( o + n_payload * sizeof(unsigned) );
   ulong off_sz     = o;  o = al64( o + n_payload * sizeof(unsigned short) );
   ulong off_psig   = o;  o = al64( o + n_payload );
@@ -909,7 +1029,10 @@ fdgpu_link_join( char const * path, double timeout_s ) {
 void
 fdgpu_link_delete( fdgpu_link_t * l ) {
   if( !l ) return;
-  if( l->registered ) fdgpu_host_unregister( l->dcache );
+  if( l->registered ) {
+    fdgpu_host_unregister( l->dcache );
+    for( int q=0; q<l->h->cfg.producers; q++ ) fdgpu_host_unregister( l->line[q] );
+  }
   munmap( l->base, l->sz );
   free( l );
 }
@@ -1075,17 +1198,18 @@ typedef struct {
   ulong n;                       /* frags the link's producer publishes */
   ulong credited;                /* last credit returned */
   ulong app, fin;                /* own frags handed to during_frag / returned by after_frags */
-  ulong done_next;               /* 1 + the seq of the last frag of this link returned by after_frags */
 } link_in_t;
 
 /* credit a tile returns to producer q: every seq below it may be
    overwritten.  With zero-copy intake a frag's bytes must survive until
-   the GPU has read them, so while frags of the link are pending the credit
-   stops at the first seq after the link's last completed frag (its frags
-   complete in seq order, so that is at or below its oldest pending one). */
-static void link_credit( link_hdr_t * h, int q, int idx, link_in_t const * in ) {
+   the GPU has copied them (the stem's during_frag copy, done by the GPU:
+   fdgpu_vtile_copy_state), so while frags of the link are not yet copied
+   the credit stops at the first seq after the link's last copied frag
+   (copies complete in seq order per link, so that is at or below the
+   oldest uncopied one).  The verdict does not hold the link. */
+static void link_credit( link_hdr_t * h, int q, int idx, link_in_t const * in, fdgpu_vtile_t const * vt ) {
   ulong c = in->seq;
-  if( h->cfg.zero_copy && in->app != in->fin && in->done_next < c ) c = in->done_next;
+  if( h->cfg.zero_copy ) { ulong cn; if( fdgpu_vtile_copy_state( vt, q, &cn ) && cn < c ) c = cn; }
   atomic_store_explicit( &h->fseq[q][idx].v, c, memory_order_release );
 }
 
@@ -1107,9 +1231,9 @@ link_account( fdgpu_link_t * l, fdgpu_vtile_done_t const * d, ulong n, ulong * s
     ulong lat = t - d[i].tsorig;
     lh[ lh_idx( lat ) ]++;
     if( lat > *lmax ) *lmax = lat;
-    int q = FDGPU_VTILE_SEQ_LINK( d[i].seq ) & ( LINK_PROD_MAX - 1 );
+    int q = FDGPU_VTILE_SEQ_LINK( d[i].seq );        /* < Q: the tile handed it over with its link */
     ulong s = FDGPU_VTILE_SEQ_SEQ( d[i].seq );
-    in[q].fin++; in[q].done_next = s + 1UL;
+    in[q].fin++;
     if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL )
       *sigs += l->psig[ ( s * Q + (ulong)q ) % np ];
   }
@@ -1127,10 +1251,12 @@ static void * link_tile( void * _a ) {
   /* out dcache: room for the frags a tile can have pending (its contexts' launched and filling
      batches), 6 batch limits' worth: with 3 a 2-tile max-rate run blocked in drains (16.7M vs
      18.8M sigs/s, profiles/r02/stream/sweep_depth.md) */
-  ulong mult = 6UL;
-  { char const * e = getenv( "FDGPU_LINK_OUT_MULT" ); if( e && atoi( e ) > 0 ) mult = (ulong)atoi( e ); }   /* A/B knob */
-  fdgpu_vtile_t * vt = fdgpu_vtile_new( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
-                                        ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512 );
+  ulong mult = c->out_mult ? c->out_mult : 6UL;
+  fdgpu_vtile_opts_t vo;
+  memset( &vo, 0, sizeof(vo) );
+  vo.nctx = c->nctx; vo.copy_wait_ns = c->copy_wait_ns; vo.copy_min = c->copy_min;
+  fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
+                                             ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
   /* zero-copy intake from every producer's link; the overrun check only on unreliable links (a
      reliable producer never reuses a line before the tile's credit passes its pending frags) */
@@ -1162,8 +1288,7 @@ static void * link_tile( void * _a ) {
   ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, ns_idle = 0UL, t_begin = now_ns();
   /* FDGPU_LINK_PROF=1: rdtsc section profile (mcache poll, during_frag, prefetch + credit, drain
      after_frags, housekeep after_frags, link_account, credit after a drain, housekeep) */
-  char const * pe = getenv( "FDGPU_LINK_PROF" );
-  int prof = pe && atoi( pe );
+  int prof = c->prof;
   ulong pc[ 8 ] = { 0 }, c_begin = __rdtsc(), cx = 0UL;
 #define PROF_T0()    do { if( prof ) cx = __rdtsc(); } while( 0 )
 #define PROF_ADD(i)  do { if( prof ) { ulong cy_ = __rdtsc(); pc[i] += cy_ - cx; cx = cy_; } } while( 0 )
@@ -1224,11 +1349,11 @@ static void * link_tile( void * _a ) {
         }
         li->seq = own + 1UL;
         if( c->reliable && ( li->seq - li->credited >= 64UL || li->seq >= li->n ) ) {   /* batched credit return */
-          link_credit( h, (int)q, idx, li ); li->credited = li->seq;
+          link_credit( h, (int)q, idx, li, vt ); li->credited = li->seq;
         }
         PROF_ADD( 2 );
       }
-      if( li->seq >= li->n && c->reliable && li->credited < li->n ) { link_credit( h, (int)q, idx, li ); li->credited = li->n; }
+      if( li->seq >= li->n && c->reliable && li->credited < li->n ) { link_credit( h, (int)q, idx, li, vt ); li->credited = li->n; }
     }
     q0++;
     for( ulong q=0; q<Q; q++ ) if( in[q].seq < in[q].n ) all_done = 0;
@@ -1242,7 +1367,7 @@ static void * link_tile( void * _a ) {
       PROF_ADD( 3 );
       link_account( l, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
       PROF_ADD( 5 );
-      if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q] );
+      if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );
       PROF_ADD( 6 );
       ns_after += now_ns() - t1;
       continue;
@@ -1260,7 +1385,7 @@ static void * link_tile( void * _a ) {
       PROF_ADD( 4 );
       link_account( l, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
       PROF_ADD( 5 );
-      if( c->reliable && c->zero_copy && n ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q] );
+      if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );
       PROF_ADD( 6 );
       ns_hk += t2 - t1; ns_after += now_ns() - t2;
     }
@@ -1293,6 +1418,8 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   if( proc < 0 || proc >= c->gpus ) return -1;
   if( c->zero_copy && !l->registered ) {
     if( fdgpu_host_register( l->dcache, h->in_bytes + 4096UL ) ) { atomic_store( &h->fail, 7 ); return -3; }
+    for( int q=0; q<c->producers; q++ )          /* the gather re-reads each frag's line after its copy */
+      if( fdgpu_host_register( l->line[q], mc_bytes( h->depth ) ) ) { atomic_store( &h->fail, 7 ); return -3; }
     l->registered = 1;
   }
   pthread_t prod[ LINK_PROD_MAX ], th[ LINK_TILE_MAX ];
@@ -1348,6 +1475,8 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     for( ulong k=0; k<FDGPU_VTILE_LAT_BUCKETS; k++ ) st->gpu_lat_hist[k] += r->gm.lat_hist[k];
     st->gpu_wait_ns += r->gm.wait_ns; st->poll_ns += r->gm.poll_ns; st->after_ns += r->gm.after_ns;
     st->launch_ns += r->gm.launch_ns;
+    st->copies += r->gm.copies; st->copy_lat_n += r->gm.copy_lat_n; st->copy_lat_ns_sum += r->gm.copy_lat_ns_sum;
+    if( r->gm.copy_lat_ns_max > st->copy_lat_ns_max ) st->copy_lat_ns_max = r->gm.copy_lat_ns_max;
     st->tile_idle_ns += r->ns_idle;
     for( int k=0; k<8; k++ ) st->prof_ns[k] += r->prof[k];
     if( r->t_last > t_end ) t_end = r->t_last;

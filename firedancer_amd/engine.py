@@ -36,6 +36,7 @@ RAW_DTYPE = np.dtype([("payload_off", "<u4"), ("sig_base", "<u4"), ("payload_sz"
                       ("_pad", "u1", (5,))])
 assert RAW_DTYPE.itemsize == 16
 FDGPU_ERR_PARSE = -16
+FDGPU_ERR_OVERRUN = -17
 TXN_IMG_STRIDE = 864
 
 # every symbol include/fd_ed25519_gpu.h declares
@@ -45,7 +46,9 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_verify_raw_host", "fdgpu_ed25519_submit", "fdgpu_ed25519_flush",
            "fdgpu_ed25519_poll", "fdgpu_ed25519_submit_raw", "fdgpu_ed25519_poll_raw", "fdgpu_ed25519_submit_raw_ref",
            "fdgpu_host_alloc", "fdgpu_host_free", "fdgpu_host_register", "fdgpu_host_unregister", "fdgpu_device_numa_node",
-           "fdgpu_ed25519_submit_raw_gather",
+           "fdgpu_ed25519_submit_raw_gather", "fdgpu_ed25519_submit_raw_gather_chk", "fdgpu_ed25519_gather",
+           "fdgpu_ed25519_gathered", "fdgpu_ed25519_gather_launched", "fdgpu_ed25519_gather_wait", "fdgpu_host_dev_ptr",
+           "fdgpu_ed25519_dropin_init", "fdgpu_debug_set_opts",
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_slow_count", "fdgpu_ed25519_set_dedup",
            "fdgpu_ed25519_set_record_fp_off", "fdgpu_ed25519_batch_stats", "fdgpu_ed25519_launch_stats", "fdgpu_ed25519_front_remaining", "fdgpu_ed25519_verify_txn_ptrs",
@@ -143,6 +146,23 @@ def load_library():
         L.fdgpu_ed25519_submit_raw_gather.restype = ctypes.c_int
         L.fdgpu_ed25519_submit_raw_gather.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                       ctypes.c_ushort, ctypes.c_ushort, ctypes.c_ushort, ctypes.c_ulong]
+        L.fdgpu_ed25519_submit_raw_gather_chk.restype = ctypes.c_int
+        L.fdgpu_ed25519_submit_raw_gather_chk.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                          ctypes.c_void_p, ctypes.c_ushort, ctypes.c_ushort,
+                                                          ctypes.c_ushort, ctypes.c_ulong, ctypes.c_void_p, ctypes.c_ulong]
+        L.fdgpu_ed25519_gather.restype = ctypes.c_long
+        L.fdgpu_ed25519_gather.argtypes = [ctypes.c_void_p]
+        L.fdgpu_ed25519_gathered.restype = ctypes.c_ulong
+        L.fdgpu_ed25519_gathered.argtypes = [ctypes.c_void_p]
+        L.fdgpu_ed25519_gather_launched.restype = ctypes.c_ulong
+        L.fdgpu_ed25519_gather_launched.argtypes = [ctypes.c_void_p]
+        L.fdgpu_ed25519_gather_wait.restype = ctypes.c_int
+        L.fdgpu_ed25519_gather_wait.argtypes = [ctypes.c_void_p]
+        L.fdgpu_host_dev_ptr.restype = ctypes.c_void_p
+        L.fdgpu_host_dev_ptr.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
+        L.fdgpu_ed25519_dropin_init.restype = ctypes.c_int
+        L.fdgpu_ed25519_dropin_init.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.fdgpu_debug_set_opts.argtypes = [ctypes.c_void_p]
         L.fdgpu_host_alloc.restype = ctypes.c_void_p
         L.fdgpu_host_alloc.argtypes = [ctypes.c_ulong]
         L.fdgpu_host_free.argtypes = [ctypes.c_void_p]
@@ -153,6 +173,32 @@ def load_library():
 
 def last_error() -> str:
     return load_library().fdgpu_last_error().decode()
+
+
+class DebugOpts(ctypes.Structure):
+    """fdgpu_debug_opts_t: test / A/B choices for engine contexts created afterwards."""
+    _fields_ = [("half", ctypes.c_int), ("half_force_slow", ctypes.c_uint), ("small_batch_max", ctypes.c_long),
+                ("dsm_lanes", ctypes.c_int), ("nofold_max", ctypes.c_long)]
+
+
+def debug_set_opts(half: int = -1, half_force_slow: int = 0, small_batch_max: int = -1, dsm_lanes: int = 0,
+                   nofold_max: int = -1) -> None:
+    """fdgpu_debug_set_opts: the engine path of every context created from now on (tests only; the
+    defaults restore the product's choices).  small_batch_max >= 2**63 means "always the latency path"."""
+    o = DebugOpts(half=half, half_force_slow=half_force_slow,
+                  small_batch_max=min(small_batch_max, 2**63 - 1), dsm_lanes=dsm_lanes, nofold_max=nofold_max)
+    load_library().fdgpu_debug_set_opts(ctypes.byref(o))
+
+
+def debug_reset_opts() -> None:
+    load_library().fdgpu_debug_set_opts(None)
+
+
+def dropin_init(device: int = 0, semantics: int = SEMANTICS_AVX512) -> None:
+    """fdgpu_ed25519_dropin_init: device and result-code semantics of the fd_ed25519_verify drop-ins."""
+    rc = load_library().fdgpu_ed25519_dropin_init(device, semantics)
+    if rc:
+        raise RuntimeError(f"fdgpu_ed25519_dropin_init: {rc} {last_error()}")
 
 
 def _buf(b: bytes):

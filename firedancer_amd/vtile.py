@@ -23,6 +23,7 @@ EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_
            "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_housekeep", "fdgpu_vtile_pipeline_state", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
            "fdgpu_vtile_metrics", "fdgpu_vtile_set_in_link", "fdgpu_vtile_set_in_links", "fdgpu_vtile_oldest_pending_seq", "fdgpu_vtile_overruns",
            "fdgpu_vtile_faulted", "fdgpu_vtile_recover", "fdgpu_vtile_debug_fault", "fdgpu_vtile_gpu_metrics",
+           "fdgpu_vtile_new_opts", "fdgpu_vtile_copy", "fdgpu_vtile_copy_state",
            "fdgpu_link_new", "fdgpu_link_join", "fdgpu_link_delete", "fdgpu_link_joined", "fdgpu_link_cfg",
            "fdgpu_link_run", "fdgpu_link_tiles_of", "fdgpu_link_mcache", "fdgpu_link_dcache", "fdgpu_link_result",
            "fdgpu_stream_run", "fdgpu_stream_bench")
@@ -49,16 +50,26 @@ class GpuMetrics(ctypes.Structure):
                 ("gpu_fault_frags", ctypes.c_ulong), ("faults", ctypes.c_ulong),
                 ("lat_hist", ctypes.c_ulong * LAT_BUCKETS), ("wait_ns", ctypes.c_ulong),
                 ("poll_ns", ctypes.c_ulong), ("after_ns", ctypes.c_ulong),
-                ("launch_ns", ctypes.c_ulong)]
+                ("launch_ns", ctypes.c_ulong), ("copies", ctypes.c_ulong), ("copy_lat_n", ctypes.c_ulong),
+                ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if k == "lat_hist" else int(getattr(self, k))) for k, _ in self._fields_}
 
 
+class VTileOpts(ctypes.Structure):
+    """fdgpu_vtile_opts_t (0 = default everywhere)."""
+    _fields_ = [("nctx", ctypes.c_int), ("host_dedup_tag", ctypes.c_int), ("small_max", ctypes.c_ulong),
+                ("min_batch", ctypes.c_ulong), ("max_wait_ns", ctypes.c_ulong), ("copy_wait_ns", ctypes.c_ulong),
+                ("copy_min", ctypes.c_ulong)]
+
+
 class StreamCfg(ctypes.Structure):
     _fields_ = [("n_frags", ctypes.c_ulong), ("batch_txn", ctypes.c_ulong), ("max_inflight", ctypes.c_ulong),
                 ("rate_fps", ctypes.c_double), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int),
-                ("zero_copy", ctypes.c_int), ("reliable", ctypes.c_int), ("producers", ctypes.c_int)]
+                ("zero_copy", ctypes.c_int), ("reliable", ctypes.c_int), ("producers", ctypes.c_int),
+                ("nctx", ctypes.c_int), ("prof", ctypes.c_int), ("out_mult", ctypes.c_ulong),
+                ("copy_wait_ns", ctypes.c_ulong), ("copy_min", ctypes.c_ulong)]
 
 
 class StreamStats(ctypes.Structure):
@@ -71,7 +82,8 @@ class StreamStats(ctypes.Structure):
                 ("gpu_lat_hist", ctypes.c_ulong * LAT_BUCKETS), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int),
                 ("gpu_wait_ns", ctypes.c_ulong), ("poll_ns", ctypes.c_ulong), ("after_ns", ctypes.c_ulong),
                 ("launch_ns", ctypes.c_ulong), ("tile_idle_ns", ctypes.c_ulong), ("prod_seconds", ctypes.c_double),
-                ("prod_wait_ns", ctypes.c_ulong), ("prof_ns", ctypes.c_ulong * 8)]
+                ("prod_wait_ns", ctypes.c_ulong), ("prof_ns", ctypes.c_ulong * 8), ("copies", ctypes.c_ulong),
+                ("copy_lat_n", ctypes.c_ulong), ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong)]
 
     def as_dict(self) -> dict:
         out = {}
@@ -108,6 +120,12 @@ def load():
         L.fdgpu_dcache_compact_next.argtypes = [ul, ul, ul, ul]
         L.fdgpu_vtile_new.restype = vp
         L.fdgpu_vtile_new.argtypes = [ctypes.c_int, ul, ul, ul, ul, ctypes.c_int]
+        L.fdgpu_vtile_new_opts.restype = vp
+        L.fdgpu_vtile_new_opts.argtypes = [ctypes.c_int, ul, ul, ul, ul, ctypes.c_int, ctypes.POINTER(VTileOpts)]
+        L.fdgpu_vtile_copy.restype = ctypes.c_int
+        L.fdgpu_vtile_copy.argtypes = [vp, ctypes.c_int]
+        L.fdgpu_vtile_copy_state.restype = ul
+        L.fdgpu_vtile_copy_state.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_ulong)]
         L.fdgpu_vtile_delete.argtypes = [vp]
         L.fdgpu_vtile_out_dcache.restype = vp
         L.fdgpu_vtile_out_dcache.argtypes = [vp]
@@ -186,10 +204,14 @@ class VTile:
     """One GPU verify tile (fdgpu_vtile_t)."""
 
     def __init__(self, device: int = 0, batch_txn: int = 1024, tcache_depth: int = 1 << 16, seed: int = 0x5eed,
-                 out_dcache_bytes: int | None = None, semantics: int = 0):
+                 out_dcache_bytes: int | None = None, semantics: int = 0, **opts):
+        """opts: fdgpu_vtile_opts_t fields (nctx, host_dedup_tag, small_max, min_batch, max_wait_ns,
+        copy_wait_ns, copy_min); 0 / absent = default."""
         self.L = load()
         out_dcache_bytes = out_dcache_bytes or (6 * batch_txn + 64) * 2304
-        self.p = self.L.fdgpu_vtile_new(device, batch_txn, tcache_depth, seed, out_dcache_bytes, semantics)
+        o = VTileOpts(**opts)
+        self.p = self.L.fdgpu_vtile_new_opts(device, batch_txn, tcache_depth, seed, out_dcache_bytes, semantics,
+                                             ctypes.byref(o))
         if not self.p:
             raise RuntimeError("fdgpu_vtile_new failed: " + load_engine().fdgpu_last_error().decode())
         self.seed = seed
@@ -209,6 +231,16 @@ class VTile:
 
     def overruns(self) -> int:
         return int(self.L.fdgpu_vtile_overruns(self.p))
+
+    def copy(self, blocking: bool = False) -> int:
+        """fdgpu_vtile_copy: start (and, blocking, wait for) the GPU copy of every frag taken so far."""
+        return int(self.L.fdgpu_vtile_copy(self.p, 1 if blocking else 0))
+
+    def copy_state(self, link: int = 0) -> tuple[int, int]:
+        """(frags of `link` not yet known copied, 1 + seq of its last frag known copied)."""
+        cn = ctypes.c_ulong(0)
+        n = self.L.fdgpu_vtile_copy_state(self.p, link, ctypes.byref(cn))
+        return int(n), int(cn.value)
 
     def flush(self):
         return self.L.fdgpu_vtile_flush(self.p)
@@ -281,20 +313,23 @@ def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
     return list(out[:n])
 
 
-def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers=1) -> StreamCfg:
+def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers=1, nctx=0, prof=0,
+         out_mult=0, copy_wait_ns=0, copy_min=0) -> StreamCfg:
     return StreamCfg(n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
-                     gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0, producers=producers)
+                     gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0, producers=producers,
+                     nctx=nctx, prof=prof, out_mult=out_mult, copy_wait_ns=copy_wait_ns, copy_min=copy_min)
 
 
 def stream_run(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,
                batch_txn: int = 4096, max_inflight: int = 1, mcache_depth: int = 1 << 16, rate_fps: float = 0.0,
-               device: int = 0, zero_copy: bool = True, reliable: bool = True, producers: int = 1) -> dict:
-    """One process: `producers` producer links + `tiles` verify tiles on `device`, private memory (G = 1)."""
+               device: int = 0, zero_copy: bool = True, reliable: bool = True, producers: int = 1, **tune) -> dict:
+    """One process: `producers` producer links + `tiles` verify tiles on `device`, private memory (G = 1).
+    tune: nctx, prof, out_mult, copy_wait_ns, copy_min (fdgpu_stream_cfg_t)."""
     L = load()
     payload = np.ascontiguousarray(payload, np.uint8)
     off = np.ascontiguousarray(off, np.uint32)
     sz = np.ascontiguousarray(sz, np.uint16)
-    cfg = _cfg(n_frags, tiles, 1, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers)
+    cfg = _cfg(n_frags, tiles, 1, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers, **tune)
     st = StreamStats()
     rc = L.fdgpu_stream_run(device, ctypes.byref(cfg), payload.ctypes.data, off.ctypes.data, sz.ctypes.data, len(off),
                             mcache_depth, ctypes.byref(st))
@@ -309,14 +344,14 @@ class Link:
     def __init__(self, path: str | None, *, create: bool, payload=None, off=None, sz=None, n_frags: int = 0,
                  tiles: int = 1, gpus: int = 1, batch_txn: int = 8192, max_inflight: int = 1, rate_fps: float = 0.0,
                  zero_copy: bool = True, reliable: bool = True, mcache_depth: int = 1 << 18, timeout_s: float = 300.0,
-                 producers: int = 1):
+                 producers: int = 1, **tune):
         self.L = load()
         self.path = path
         if create:
             payload = np.ascontiguousarray(payload, np.uint8)
             off = np.ascontiguousarray(off, np.uint32)
             sz = np.ascontiguousarray(sz, np.uint16)
-            cfg = _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers)
+            cfg = _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers, **tune)
             self.p = self.L.fdgpu_link_new(path.encode() if path else None, ctypes.byref(cfg), payload.ctypes.data,
                                            off.ctypes.data, sz.ctypes.data, len(off), mcache_depth)
         else:

@@ -136,6 +136,8 @@ typedef struct fdgpu_txn_raw {
 } fdgpu_txn_raw_t;
 
 #define FDGPU_ERR_PARSE        (-16)    /* fd_txn_parse returned 0 */
+#define FDGPU_ERR_OVERRUN      (-17)    /* gathered record: its in-mcache line was reused while the GPU copied it
+                                           (fdgpu_ed25519_submit_raw_gather_chk); never parsed or verified */
 #define FDGPU_TXN_IMG_STRIDE   (864UL)  /* >= FD_TXN_MAX_SZ (852), fd_txn.h:99 */
 
 /* A context is single-threaded (one per verify tile / thread); several
@@ -353,10 +355,11 @@ fdgpu_ed25519_debug_fault( fdgpu_ed25519_ctx_t * ctx );
 
 /* Signatures of the last batch launched on ctx that took the full 253-bit
    walk instead of the half-size one (no short (c0, c1) pair, or forced by
-   env FDGPU_HALF_FORCE_SLOW); 0 when the half-size path is off.  Waits
-   for ctx's stream (a batch launched on a caller's stream must have
-   completed).  For tests and metrics: a device reduction that silently
-   failed would still verify correctly, only slower. */
+   fdgpu_debug_opts_t.half_force_slow); 0 when the half-size path is off.
+   TEST-ONLY: it synchronises ctx's stream (stalling any async batch in
+   flight) and sees only the last batch launched, so it is not a metric a
+   tile loop can export.  A device reduction that silently failed would
+   still verify correctly, only slower. */
 unsigned long
 fdgpu_ed25519_slow_count( fdgpu_ed25519_ctx_t * ctx );
 
@@ -438,9 +441,9 @@ int    fdgpu_device_numa_node( int device );
    had copied it (the reference's during_frag copy, fd_verify_tile.c:
    77-79).  Records of one batch lie at increasing dst addresses of one
    region (a lower one starts a new batch), 16-B aligned, with room for
-   copy_sz rounded up to 16 at dst; src must stay valid until the batch
-   is launched (the caller checks for overruns after the verdict).  The
-   GPU also writes each parsed transaction's fd_txn_t image into the out
+   copy_sz rounded up to 16 at dst; src must stay valid until the record's
+   gather has completed (fdgpu_ed25519_gathered; at the latest, its
+   verdict).  The GPU also writes each parsed transaction's fd_txn_t image into the out
    region, behind the payload at the next 2-byte boundary (where the
    tile publishes it), so poll_raw returns footprints but leaves out_img
    untouched for these transactions; leave room for 852 bytes there. */
@@ -453,6 +456,47 @@ fdgpu_ed25519_submit_raw_gather( fdgpu_ed25519_ctx_t * ctx,
                                  unsigned short        payload_off,
                                  unsigned short        payload_sz,
                                  unsigned long         tag );
+
+/* The same with the stem's overrun check (src/disco/stem/fd_stem.c:667-686)
+   done by the GPU: seq_addr (NULL = no check; else 8-B aligned, inside a
+   registered range) is the seq word of the frag's line in the producer's
+   mcache, and seq the value it held when the caller took the frag.  Right
+   after copying the record the gather kernel re-reads that word (a
+   system-scope load behind every copy load); if it changed, the producer
+   reused the line while the record was being read, and the record's
+   verdict is FDGPU_ERR_OVERRUN.  The decision is made once, at copy time:
+   a lap after the gather has completed changes nothing. */
+int
+fdgpu_ed25519_submit_raw_gather_chk( fdgpu_ed25519_ctx_t * ctx,
+                                     unsigned char const * src,
+                                     unsigned char *       dst_base,
+                                     unsigned char *       dst,
+                                     unsigned short        copy_sz,
+                                     unsigned short        payload_off,
+                                     unsigned short        payload_sz,
+                                     unsigned long         tag,
+                                     unsigned long const * seq_addr,
+                                     unsigned long         seq );
+
+/* Early gather: launch now, on the context's gather stream, the copies of
+   every gathered record submitted to the filling batch and not yet
+   copied (the batch itself launches later; its kernels wait for these
+   copies).  This is what bounds how long a frag stays exposed to the
+   producer between during_frag and its copy.  Returns the number of
+   records launched (0: none pending), < 0 on error.
+   fdgpu_ed25519_gathered: records (all gathered submissions of ctx, in
+   submission order, counted from 0) whose copy has completed -- read from
+   a pinned word the last block of each gather stores; no HIP call.
+   fdgpu_ed25519_gather_launched: records whose copy has been launched. */
+long          fdgpu_ed25519_gather( fdgpu_ed25519_ctx_t * ctx );
+unsigned long fdgpu_ed25519_gathered( fdgpu_ed25519_ctx_t const * ctx );
+unsigned long fdgpu_ed25519_gather_launched( fdgpu_ed25519_ctx_t const * ctx );
+/* wait until every launched gather of ctx has completed: 0, or -3 (ctx faulted) */
+int           fdgpu_ed25519_gather_wait( fdgpu_ed25519_ctx_t * ctx );
+
+/* device address of the host range [p, p+sz) if it lies inside one range
+   given to fdgpu_host_register / fdgpu_host_alloc, else NULL */
+void * fdgpu_host_dev_ptr( void const * p, unsigned long sz );
 
 /* out_dedup (may be NULL): with fdgpu_ed25519_set_dedup on, the HA dedup
    tag of each parsed transaction (XXH64 of its first signature with the
@@ -486,8 +530,9 @@ fdgpu_ed25519_set_record_fp_off( fdgpu_ed25519_ctx_t * ctx, int off );
    at the end of the DSM.  Larger batches take the throughput path: R is
    not decompressed up front but checked against P's encoding after one
    batched inversion per 256 signatures.  Both give identical codes.
-   Default FD_SMALL_BATCH_MAX (env FDGPU_SMALL_BATCH_MAX at context
-   creation); 0 forces the throughput path, ~0UL the latency path.
+   Default FD_SMALL_BATCH_MAX (fdgpu_debug_set_opts can change the value
+   new contexts start with); 0 forces the throughput path, ~0UL the
+   latency path.
    Returns the previous value. */
 unsigned long
 fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long small_max );
@@ -510,6 +555,30 @@ fdgpu_ed25519_kernel_ms( fdgpu_ed25519_ctx_t * ctx, int idx );
    against; MI355X_MICROARCH.md has no integer-multiply row. */
 double
 fdgpu_mad_peak_per_s( int device );
+
+/* The drop-ins (fd_ed25519_verify, fd_ed25519_verify_batch_single_msg)
+   share one process-wide context, created on first use on device 0 with
+   FDGPU_SEMANTICS_AVX512.  Call this first to choose another device or
+   the portable codes (recreates the context if one exists).  0 on
+   success. */
+int
+fdgpu_ed25519_dropin_init( int device, int semantics );
+
+/* ---- test / A/B hooks (never read from the environment) ---------------
+   Options for engine contexts created after the call, process-wide
+   (contexts that already exist keep theirs).  NULL restores the
+   defaults.  The tests run every engine path through these; the product
+   never calls it. */
+typedef struct fdgpu_debug_opts {
+  int           half;             /* -1: default (half-size walk); 0: full-length walk + deferred R check; 1: half */
+  unsigned int  half_force_slow;  /* 0: off; m: signatures with S % m == 0 take the full-length walk (slow list) */
+  long          small_batch_max;  /* -1: default; else the initial fdgpu_ed25519_set_small_batch_max */
+  int           dsm_lanes;        /* latency path: lanes per signature in the DSM (1, 2, 4, 8); 0 = by batch size */
+  long          nofold_max;       /* -1: default; batches of at most this many signatures use the unfolded DSM */
+} fdgpu_debug_opts_t;
+
+void
+fdgpu_debug_set_opts( fdgpu_debug_opts_t const * opts );
 
 /* Last error string of the calling thread (never NULL). */
 char const *

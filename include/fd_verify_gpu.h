@@ -110,7 +110,7 @@ unsigned long    fdgpu_dcache_compact_next( unsigned long chunk, unsigned long s
 #define FDGPU_VTILE_VERIFY_FAIL      (2)
 #define FDGPU_VTILE_DEDUP_FAIL       (3)
 #define FDGPU_VTILE_BUNDLE_PEER_FAIL (4)
-#define FDGPU_VTILE_OVERRUN          (5)   /* zero-copy intake: the frag was overwritten before the GPU read it */
+#define FDGPU_VTILE_OVERRUN          (5)   /* zero-copy intake: the producer reused the frag's line while the GPU copied it */
 #define FDGPU_VTILE_GPU_FAULT        (6)   /* the frag's GPU batch failed: no verdict, never published (the
                                               reference tile would FD_LOG_ERR, fd_verify_tile.c:74-84) */
 
@@ -143,16 +143,38 @@ typedef struct fdgpu_vtile_gpu_metrics {
   unsigned long wait_ns;          /* host time after_frags spent blocked on a batch not yet complete */
   unsigned long poll_ns;          /* ... in non-blocking completion polls (fdgpu_ed25519_poll_raw) */
   unsigned long after_ns;         /* ... in after_frag proper (dedup, overrun check, publish) */
-  unsigned long launch_ns;        /* host time inside batch launches (in during_frag, housekeep or a drain) */
+  unsigned long launch_ns;        /* host time inside batch launches and early copies (in during_frag, housekeep or a drain) */
+  unsigned long copies;           /* zero-copy: early GPU copies started (housekeep, fdgpu_vtile_copy) */
+  unsigned long copy_lat_n, copy_lat_ns_sum, copy_lat_ns_max;   /* ... of them timed: launch -> completion seen */
 } fdgpu_vtile_gpu_metrics_t;
 
 /* device: HIP device; batch_txn: transactions per GPU batch (staging
    slot); tcache_depth: HA dedup depth (verify.tcache_depth); seed: the
    dedup hash seed (ctx->hashmap_seed); out_dcache_bytes: size of the
    tile's out dcache (fd_txn_m_t records, 64-B chunks);  semantics:
-   FDGPU_SEMANTICS_*.  NULL on failure (fdgpu_last_error). */
+   FDGPU_SEMANTICS_*.  NULL on failure (fdgpu_last_error).  Tuning comes
+   only through fdgpu_vtile_opts_t (fdgpu_vtile_new: every field 0 =
+   default); nothing is read from the environment. */
+#define FDGPU_VTILE_COPY_WAIT_NS (50000UL)   /* default copy_wait_ns */
+#define FDGPU_VTILE_COPY_MIN     (4096UL)    /* default copy_min */
+typedef struct fdgpu_vtile_opts {
+  int           nctx;            /* engine contexts per tile, 1..3 (0 = 2): batches of consecutive frags go to them in
+                                    turn, launched staggered, so a frag does not wait for a whole running batch */
+  int           host_dedup_tag;  /* 1: after_frag computes the HA dedup tag on the host (reads the payload; A/B only) */
+  unsigned long small_max;       /* batches of at most this many signatures take the engine's latency path
+                                    (0 = half the batch limit, at most the engine default) */
+  unsigned long min_batch;       /* housekeep: a partial batch below this many frags waits ... (0 = never waits) */
+  unsigned long max_wait_ns;     /* ... until its oldest frag has waited this long (0 = 2 ms) */
+  unsigned long copy_wait_ns;    /* zero-copy: housekeep starts the GPU copy of the frags taken since the last one
+                                    once the oldest has waited this long (0 = FDGPU_VTILE_COPY_WAIT_NS) ... */
+  unsigned long copy_min;        /* ... or once this many are waiting (0 = FDGPU_VTILE_COPY_MIN) */
+} fdgpu_vtile_opts_t;
+
 fdgpu_vtile_t * fdgpu_vtile_new( int device, unsigned long batch_txn, unsigned long tcache_depth, unsigned long seed,
                                  unsigned long out_dcache_bytes, int semantics );
+fdgpu_vtile_t * fdgpu_vtile_new_opts( int device, unsigned long batch_txn, unsigned long tcache_depth,
+                                      unsigned long seed, unsigned long out_dcache_bytes, int semantics,
+                                      fdgpu_vtile_opts_t const * opts );
 void            fdgpu_vtile_delete( fdgpu_vtile_t * vt );
 unsigned char * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt );   /* chunk c is at base + 64 c */
 
@@ -166,11 +188,17 @@ int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, 
    is -- frag must then lie in a range registered with
    fdgpu_host_register (the in dcache), 16-B aligned -- and the GPU
    copies it into the out dcache record itself
-   (fdgpu_ed25519_submit_raw_gather).  in_mc (may be NULL): the in link's
-   mcache; after the verdict, a frag whose mcache line the producer has
-   reused is reported FDGPU_VTILE_OVERRUN instead of published.  A
-   reliable producer must not reuse a frag's dcache bytes before
-   fdgpu_vtile_oldest_pending_seq has passed it (credits).  Call while no
+   (fdgpu_ed25519_submit_raw_gather_chk): the stem's during_frag copy,
+   done by the GPU shortly after during_frag (housekeep starts the copies,
+   see fdgpu_vtile_opts_t.copy_wait_ns; fdgpu_vtile_copy starts them now).
+   in_mc (may be NULL): the in link's mcache (its lines are registered
+   with the GPU here if they are not yet); right after copying a frag the
+   GPU re-reads its line, and a frag whose line the producer reused while
+   it was being copied is reported FDGPU_VTILE_OVERRUN instead of
+   published -- the stem's overrun check, at the same point
+   (src/disco/stem/fd_stem.c:667-686).  A lap after the copy changes
+   nothing.  A reliable producer must not reuse a frag's dcache bytes
+   before its copy has completed (fdgpu_vtile_copy_state).  Call while no
    frag is pending; 0 on success. */
 int             fdgpu_vtile_set_in_link( fdgpu_vtile_t * vt, fdgpu_mcache_t const * in_mc );
 /* The same for a tile that reads n in links (the reference's verify tile
@@ -186,12 +214,22 @@ int             fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t con
 /* seq of the oldest frag not yet returned by after_frags, as handed to
    during_frag (link bits included, FDGPU_VTILE_SEQ); ~0UL if none */
 unsigned long   fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt );
+/* Zero-copy intake: start the GPU copy of every frag taken and not yet
+   copied; blocking: wait until every copy has completed.  0, or < 0 if a
+   context failed (its frags come back as FDGPU_VTILE_GPU_FAULT). */
+int             fdgpu_vtile_copy( fdgpu_vtile_t * vt, int blocking );
+/* Zero-copy intake, per in link: the number of frags taken whose copy is
+   not known to have completed, and (copied_next) 1 + the seq of the
+   link's last frag known copied (0 if none).  While the count is nonzero
+   the producer must not reuse seqs >= copied_next (a reliable link's
+   credit).  Progress is picked up by housekeep, copy and after_frags. */
+unsigned long   fdgpu_vtile_copy_state( fdgpu_vtile_t const * vt, int link, unsigned long * copied_next );
 /* frags dropped as FDGPU_VTILE_OVERRUN */
 unsigned long   fdgpu_vtile_overruns( fdgpu_vtile_t const * vt );
 /* launch the partially filled batches (call when the input is idle) */
 int             fdgpu_vtile_flush( fdgpu_vtile_t * vt );
 /* transactions waiting in unlaunched batches, and launched batches not yet
-   drained, summed over the tile's engine contexts (env FDGPU_VTILE_CTX,
+   drained, summed over the tile's engine contexts (fdgpu_vtile_opts_t.nctx,
    1..3, default 2: batches of consecutive frags go to the contexts in
    turn, launched staggered by a fraction of the batch duration so a frag
    does not wait for a whole running batch before its own starts) */
@@ -247,6 +285,11 @@ typedef struct fdgpu_stream_cfg {
   int           producers;       /* Q producer links (the reference's QUIC tiles, 0 = 1): producer q publishes
                                     about n_frags / Q frags on its own mcache, every tile reads every link with
                                     seq % T == i on each (topology.c:167-169); producer q runs in process q % G */
+  int           nctx;            /* engine contexts per tile (fdgpu_vtile_opts_t.nctx; 0 = its default) */
+  int           prof;            /* 1: rdtsc section profile of the tile loop (fdgpu_stream_stats_t.prof_ns) */
+  unsigned long out_mult;        /* out dcache per tile, in batch limits (0 = 6) */
+  unsigned long copy_wait_ns;    /* zero-copy: fdgpu_vtile_opts_t.copy_wait_ns (0 = its default) */
+  unsigned long copy_min;        /* zero-copy: fdgpu_vtile_opts_t.copy_min (0 = its default) */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
@@ -269,9 +312,11 @@ typedef struct fdgpu_stream_stats {
   unsigned long tile_idle_ns;    /* of tile_ns[0]: intake passes that found no frag published yet */
   double        prod_seconds;    /* producers: first -> last publish */
   unsigned long prod_wait_ns;    /* producers: time waiting for credits (reliable links), summed */
-  unsigned long prof_ns[ 8 ];    /* env FDGPU_LINK_PROF=1, summed over tiles: mcache poll, during_frag, prefetch +
+  unsigned long prof_ns[ 8 ];    /* cfg.prof = 1, summed over tiles: mcache poll, during_frag, prefetch +
                                     credit, drain after_frags, housekeep after_frags, accounting, credit after
                                     after_frags, housekeep (launch decisions) */
+  unsigned long copies, copy_lat_n, copy_lat_ns_sum, copy_lat_ns_max;   /* zero-copy: early GPU copies (summed over
+                                    tiles; max over tiles), as fdgpu_vtile_gpu_metrics_t */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per

@@ -28,13 +28,13 @@ def golden():
 # Every GPU test runs on both engine paths (include/fd_ed25519_gpu.h,
 # fdgpu_ed25519_set_small_batch_max): "throughput" (half-size scalars,
 # fd_gpu_lattice.h: R decoded, a 128-doubling walk, Q == O), "throughput_full"
-# (env FDGPU_HALF=0: the 252-doubling walk, R checked after one batched
-# inversion per 256 signatures) and "latencyN" (one fused prep; 8 = the
-# half-size walk's terms split over two quads
-# launch, R decoded up front, N = 4, 2 or 1 lanes per signature in the
-# DSM, env FDGPU_DSM_LANES).  The engine reads FDGPU_SMALL_BATCH_MAX
-# when a context is created, so the choice reaches contexts the verify
-# tile library creates too.
+# (half = 0: the 252-doubling walk, R checked after one batched inversion per
+# 256 signatures) and "latencyN" (one fused prep, R decoded up front, N = 8,
+# 4, 2 or 1 lanes per signature in the DSM; 8 = the half-size walk's terms
+# split over two quads).  The choice goes through the engine's explicit test
+# hook, fdgpu_debug_set_opts, which every context created afterwards reads --
+# contexts the verify tile library creates too.  The product never reads
+# these from the environment.
 def pytest_generate_tests(metafunc):
     if metafunc.definition.get_closest_marker("gpu") is not None and "engine_path" in metafunc.fixturenames:
         metafunc.parametrize("engine_path", ["throughput", "throughput_full", "latency8", "latency4", "latency2",
@@ -42,11 +42,22 @@ def pytest_generate_tests(metafunc):
                             indirect=True)
 
 
+def engine_opts(path: str, **kw) -> dict:
+    """fdgpu_debug_opts_t fields selecting an engine path (see above)."""
+    o = dict(small_batch_max=0 if path.startswith("throughput") else 2**63,
+             half=0 if path == "throughput_full" else 1,
+             dsm_lanes=int(path[-1]) if path.startswith("latency") else 0)
+    o.update(kw)
+    return o
+
+
 @pytest.fixture(autouse=True)
-def engine_path(request, monkeypatch):
+def engine_path(request):
     path = getattr(request, "param", None)
     if path is not None:
-        monkeypatch.setenv("FDGPU_SMALL_BATCH_MAX", "0" if path.startswith("throughput") else str(2**63))
-        monkeypatch.setenv("FDGPU_HALF", "0" if path == "throughput_full" else "1")
-        monkeypatch.setenv("FDGPU_DSM_LANES", path[-1] if path.startswith("latency") else "0")
-    return path
+        from firedancer_amd import engine
+        engine.debug_set_opts(**engine_opts(path))
+        yield path
+        engine.debug_reset_opts()
+    else:
+        yield path

@@ -104,20 +104,22 @@ def test_r_check_slow_path(fa, oracle, frac):
 
 
 @pytest.mark.parametrize("every,ntx", [(1, 3000), (3, 3000), (50, 200000), (97, 300000)])
-def test_half_size_slow_list(fa, oracle, monkeypatch, every, ntx):
+def test_half_size_slow_list(fa, oracle, every, ntx):
     """Half-size path: signatures without a short (c0, c1) take the full 253-bit walk off a compacted
     list (the head in fd_dsmh_kernel's first blocks, the rest in fd_dsm_slow_kernel).  Forced here for
-    every / every 3rd / 50th / 97th signature (env FDGPU_HALF_FORCE_SLOW) in adversarial multi-signer
+    every / every 3rd / 50th / 97th signature (fdgpu_debug_opts_t.half_force_slow) in adversarial multi-signer
     batches: codes equal the oracle's.  At 2 % (every 50th of ~500K signatures) the list overflows the
     head into fd_dsm_slow_kernel, and a slow signature's code is final long before the last
     half-size blocks start (they must not take it for a half-size one)."""
     from firedancer_amd import synth
-    monkeypatch.setenv("FDGPU_HALF", "1")
-    monkeypatch.setenv("FDGPU_SMALL_BATCH_MAX", "0")
-    monkeypatch.setenv("FDGPU_HALF_FORCE_SLOW", str(every))
+    from firedancer_amd import engine
     payload, desc, expect, nsig = synth.make_batch(ntx, synth.MULTI, max_signers=4, invalid_frac=0.3, seed=77 + every,
                                                    threads=16)
-    eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    engine.debug_set_opts(half=1, small_batch_max=0, half_force_slow=every)
+    try:
+        eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    finally:
+        engine.debug_reset_opts()
     t, s = eng.verify_txns_host(payload, desc)
     eng.close()
     np.testing.assert_array_equal(t, expect)
@@ -126,23 +128,29 @@ def test_half_size_slow_list(fa, oracle, monkeypatch, every, ntx):
 
 
 @pytest.mark.parametrize("path", ["throughput", "latency"])
-def test_half_size_no_silent_fallback(fa, monkeypatch, path):
+def test_half_size_no_silent_fallback(fa, path):
     """Hash-distributed k always has a short (c0, c1) within 2^159: a valid batch takes the half-size walk
     for every signature (slow list empty).  A device reduction that failed its own congruence check would
     still verify correctly through the full walk -- only this count shows it.  The forced slow list counts
     exactly the forced signatures."""
-    from firedancer_amd import synth
-    monkeypatch.setenv("FDGPU_HALF", "1")
-    monkeypatch.setenv("FDGPU_SMALL_BATCH_MAX", "0" if path == "throughput" else str(2**63))
+    from firedancer_amd import engine, synth
+    sbm = 0 if path == "throughput" else 2**63
     payload, desc, expect, nsig = synth.make_batch(20000, synth.MULTI, max_signers=3, invalid_frac=0.0, seed=91,
                                                    threads=16)
-    eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    engine.debug_set_opts(half=1, small_batch_max=sbm)
+    try:
+        eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    finally:
+        engine.debug_reset_opts()
     t, _ = eng.verify_txns_host(payload, desc)
     assert eng.slow_count() == 0
     eng.close()
     np.testing.assert_array_equal(t, expect)
-    monkeypatch.setenv("FDGPU_HALF_FORCE_SLOW", "7")
-    eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    engine.debug_set_opts(half=1, small_batch_max=sbm, half_force_slow=7)
+    try:
+        eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    finally:
+        engine.debug_reset_opts()
     t, _ = eng.verify_txns_host(payload, desc)
     assert eng.slow_count() == (nsig + 6) // 7
     eng.close()

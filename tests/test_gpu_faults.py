@@ -95,15 +95,7 @@ def test_vtile_fault_path():
     from firedancer_amd import synth, vtile
     payload, desc, _, _ = synth.make_batch(96, synth.LARGE_NOOP, seed=31)
     frags = [vtile.frag_bytes(payload[d["payload_off"]: d["payload_off"] + d["payload_sz"]].tobytes()) for d in desc]
-    old = os.environ.get("FDGPU_VTILE_CTX")
-    os.environ["FDGPU_VTILE_CTX"] = "2"
-    try:
-        vt = vtile.VTile(device=0, batch_txn=32, tcache_depth=4096)
-    finally:
-        if old is None:
-            del os.environ["FDGPU_VTILE_CTX"]
-        else:
-            os.environ["FDGPU_VTILE_CTX"] = old
+    vt = vtile.VTile(device=0, batch_txn=32, tcache_depth=4096, nctx=2)
     # frags 0..31 -> context 0, 32..63 -> context 1 (full batches launch and move the fill on)
     for seq in range(64):
         assert vt.during_frag(frags[seq], seq) == 0

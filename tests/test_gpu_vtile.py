@@ -177,7 +177,7 @@ def test_vtile_vs_model(oracle, batch, depth, zero_copy):
 @pytest.mark.parametrize("zero_copy", [False, True])
 @pytest.mark.parametrize("nctx", [1, 2, 3])
 def test_vtile_multictx_vs_model(oracle, nctx, zero_copy):
-    """Adaptive batching over FDGPU_VTILE_CTX engine contexts (housekeep launches batches into the
+    """Adaptive batching over nctx engine contexts (fdgpu_vtile_opts_t) (housekeep launches batches into the
     contexts in turn, staggered): completions merged back into frag order must give exactly the
     model's per-frag outcomes, metrics and published records."""
     pytest.importorskip("xxhash")
@@ -185,15 +185,7 @@ def test_vtile_multictx_vs_model(oracle, nctx, zero_copy):
     frags = make_stream(seed=12)
     seed, depth = 0x5eedbeef, 1 << 12
     want_res, want_m, want_recs, want_tags = expectation(oracle, frags, seed, depth)
-    old = os.environ.get("FDGPU_VTILE_CTX")
-    os.environ["FDGPU_VTILE_CTX"] = str(nctx)
-    try:
-        vt = vtile.VTile(device=0, batch_txn=128, tcache_depth=depth, seed=seed)
-    finally:
-        if old is None:
-            del os.environ["FDGPU_VTILE_CTX"]
-        else:
-            os.environ["FDGPU_VTILE_CTX"] = old
+    vt = vtile.VTile(device=0, batch_txn=128, tcache_depth=depth, seed=seed, nctx=nctx)
     if zero_copy:
         fbs = [vtile.frag_bytes(p, b) for p, b in frags]
         buf, offs = in_dcache(fbs)
@@ -239,32 +231,84 @@ def test_vtile_multictx_vs_model(oracle, nctx, zero_copy):
         engine.host_unregister(buf)
 
 
-def test_vtile_zero_copy_overrun():
-    """Zero-copy intake: a frag whose in-link mcache line the producer reuses before the verdict is
-    reported OVERRUN (its bytes may have changed before the GPU read them); the others verify."""
+def _overrun_setup(n, depth, seed):
     from firedancer_amd import engine, synth, vtile
     L = vtile.load()
-    depth, n = 64, 64
-    payload, desc, _, _ = synth.make_batch(n, synth.LARGE_NOOP, seed=21)
+    payload, desc, _, _ = synth.make_batch(n, synth.LARGE_NOOP, seed=seed)
     fbs = [vtile.frag_bytes(payload[d["payload_off"]: d["payload_off"] + d["payload_sz"]].tobytes()) for d in desc]
     buf, offs = in_dcache(fbs)
     engine.host_register(buf)
     mc = L.fdgpu_mcache_new(depth, 0)
     for seq in range(n):
         L.fdgpu_mcache_publish(mc, seq, 0, seq, len(fbs[seq]), 0, 0)
-    vt = vtile.VTile(device=0, batch_txn=256, tcache_depth=1024)
-    assert vt.set_in_link(mc) == 0
-    for seq in range(n):
-        assert vt.during_frag_at(buf.ctypes.data + offs[seq], len(fbs[seq]), seq) == 0
-    for seq in range(n, n + 24):                       # the producer laps lines 0..23 before the verdicts
-        L.fdgpu_mcache_publish(mc, seq, 0, 0, 0, 0, 0)
+    return L, fbs, buf, offs, mc
+
+
+def _drain_all(vt):
     vt.flush()
     got = []
     while vt.pending():
         got += vt.after_frags(blocking=True)
+    return got
+
+
+def test_vtile_zero_copy_overrun():
+    """Zero-copy intake, lap BEFORE the copy: the producer reuses the mcache lines of frags 0..23
+    after during_frag took them but before the GPU copied them (the batch launch copies here).  The
+    gather kernel re-reads each line right after its copy (the stem's seq / copy / re-check,
+    fd_stem.c:667-686): those frags are OVERRUN, never parsed or published; the others publish."""
+    from firedancer_amd import engine, vtile
+    depth, n = 64, 64
+    L, fbs, buf, offs, mc = _overrun_setup(n, depth, 21)
+    vt = vtile.VTile(device=0, batch_txn=256, tcache_depth=1024)
+    assert vt.set_in_link(mc) == 0
+    for seq in range(n):
+        assert vt.during_frag_at(buf.ctypes.data + offs[seq], len(fbs[seq]), seq) == 0
+    assert vt.copy_state(0) == (n, 0)                  # nothing copied yet: a reliable credit would stop at 0
+    for seq in range(n, n + 24):                       # the producer laps lines 0..23 before the copy
+        L.fdgpu_mcache_publish(mc, seq, 0, 0, 0, 0, 0)
+    got = _drain_all(vt)
     assert [g[0] for g in got] == list(range(n))
     assert [g[1] for g in got] == [vtile.OVERRUN] * 24 + [vtile.PUBLISH] * (n - 24)
-    assert vt.overruns() == 24 and vt.metrics()[4] == n - 24
+    assert vt.overruns() == 24 and vt.metrics() == [0, 0, 0, 0, n - 24]
+    assert vt.copy_state(0) == (0, n)
+    vt.close()
+    L.fdgpu_mcache_delete(mc)
+    engine.host_unregister(buf)
+
+
+def test_vtile_zero_copy_lap_after_copy():
+    """Zero-copy intake, lap AFTER the copy: the reference decides an overrun once, right after
+    during_frag's copy; a lap after that changes nothing (the out-dcache copy is what it publishes).
+    Frags 0..31 are copied by the GPU (fdgpu_vtile_copy, waited for) before the producer laps lines
+    0..39: they PUBLISH, bit for bit the reference's records; frags 32..39, taken but not yet
+    copied when their lines were reused, are OVERRUN; 40..63 publish.  Round 2 checked at the
+    verdict and dropped 0..31 too."""
+    from firedancer_amd import engine, vtile
+    depth, n = 64, 64
+    L, fbs, buf, offs, mc = _overrun_setup(n, depth, 22)
+    vt = vtile.VTile(device=0, batch_txn=256, tcache_depth=1024)
+    assert vt.set_in_link(mc) == 0
+    for seq in range(32):
+        assert vt.during_frag_at(buf.ctypes.data + offs[seq], len(fbs[seq]), seq) == 0
+    assert vt.copy(blocking=True) == 0
+    assert vt.copy_state(0) == (0, 32)                 # 0..31 copied: a reliable credit may pass them
+    for seq in range(32, n):
+        assert vt.during_frag_at(buf.ctypes.data + offs[seq], len(fbs[seq]), seq) == 0
+    assert vt.copy_state(0) == (32, 32)
+    for seq in range(n, n + 40):                       # laps lines 0..39
+        L.fdgpu_mcache_publish(mc, seq, 0, 0, 0, 0, 0)
+    # the producer also rewrites the in-dcache bytes of frags 0..7 (their copies are already taken)
+    for seq in range(8):
+        buf[offs[seq] + 80: offs[seq] + 80 + 64] ^= 0xff
+    got = _drain_all(vt)
+    assert [g[0] for g in got] == list(range(n))
+    want = [vtile.PUBLISH] * 32 + [vtile.OVERRUN] * 8 + [vtile.PUBLISH] * (n - 40)
+    assert [g[1] for g in got] == want
+    assert vt.overruns() == 8 and vt.metrics() == [0, 0, 0, 0, n - 8]
+    for seq, r, chunk, sz, tag in got[:8]:             # published records hold the bytes copied before the rewrite
+        rec = vt.record(chunk, sz)
+        assert rec[:len(fbs[seq])][80:] == fbs[seq][80:]
     vt.close()
     L.fdgpu_mcache_delete(mc)
     engine.host_unregister(buf)
