@@ -179,7 +179,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 # link carries 1/G of the frags but is read by all 2G tiles -> twice the single-GPU depth
                 mcache_depth=args.stream_depth * min(procs, 2) if not paced else 1 << 18,
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
-                copy_wait_ns=int(args.stream_copy_wait_us * 1000))
+                copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -222,6 +222,12 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
             # zero-copy intake: the GPU copies (the stem's during_frag copy, done by the GPU) started early
             "copies": st["copies"], "copy_lat_mean_us": st["copy_lat_ns_sum"] / max(st["copy_lat_n"], 1) * 1e-3,
             "copy_lat_max_us": st["copy_lat_ns_max"] * 1e-3,
+            # every GPU copy on the GPU clock: host launch -> first block's start, start -> last block's end
+            "gather_gpu": {"n": st["gather_gpu"][0],
+                           "launch_to_start_mean_us": st["gather_gpu"][1] / max(st["gather_gpu"][0], 1) * 1e-3,
+                           "launch_to_start_max_us": st["gather_gpu"][2] * 1e-3,
+                           "run_mean_us": st["gather_gpu"][3] / max(st["gather_gpu"][0], 1) * 1e-3,
+                           "run_max_us": st["gather_gpu"][4] * 1e-3},
             "inflight_max": st["inflight_max"], "gpu_batch_lat_p50_us_le": hq(0.5),
             "gpu_batch_lat_p99_us_le": hq(0.99)}
 
@@ -284,7 +290,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-lat-inflight", str(args.stream_lat_inflight), "--stream-producers", str(args.stream_producers),
            "--stream-ctx", str(args.stream_ctx), "--stream-lat-ctx", str(args.stream_lat_ctx),
            "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
-           "--stream-copy-wait-us", str(args.stream_copy_wait_us)]
+           "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -342,6 +348,8 @@ def main():
                     help="paced legs (the latency-under-load curve): offered frags/s per GPU, comma separated; "
                          "stream.knee = the highest whose p99 is <= 1 ms with no frag lost")
     ap.add_argument("--stream-paced-seconds", type=float, default=3.0, help="length of each paced leg")
+    ap.add_argument("--stream-gather-cus", type=int, default=0,
+                    help="zero-copy intake: CUs each tile's engine contexts reserve for the copies (fdgpu_vtile_opts_t)")
     ap.add_argument("--stream-copy-wait-us", type=float, default=0.0,
                     help="zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
                          "waited this long (0 = fdgpu_vtile default, FDGPU_VTILE_COPY_WAIT_NS)")

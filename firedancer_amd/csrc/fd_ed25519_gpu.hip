@@ -1827,7 +1827,12 @@ struct fd_gather {             /* mode 3: copy sz bytes from src (host, device v
    under the verify kernels running beside it (2x slower stream). */
 __global__ void __launch_bounds__( 64 )
 fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__ arena, unsigned char * __restrict__ out,
-                  unsigned char * __restrict__ ovr, unsigned long * cnt, unsigned long * flag, unsigned long target ) {
+                  unsigned char * __restrict__ ovr, unsigned long * cnt, unsigned long * flag, unsigned long target,
+                  unsigned long * gtime ) {
+  /* gtime (pinned): the 100-MHz GPU clock when block 0 starts and when the last block ends -- the
+     engine's gather latency metric (fdgpu_ed25519_gather_stats) */
+  if( blockIdx.x == 0u && threadIdx.x == 0u )
+    __hip_atomic_store( gtime, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
   fd_gather r = g[ blockIdx.x ];
   uint4 const * src = (uint4 const *)r.src;
   uint4 * a = (uint4 *)( arena + r.dst );
@@ -1857,7 +1862,10 @@ fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__
   __syncthreads();                                          /* (one wave: every lane's loads have returned) */
   if( threadIdx.x == 0u ) {
     unsigned long old = __hip_atomic_fetch_add( cnt, 1UL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-    if( old + 1UL == target ) __hip_atomic_store( flag, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+    if( old + 1UL == target ) {
+      __hip_atomic_store( gtime + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+      __hip_atomic_store( flag, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+    }
   }
 }
 
@@ -1978,6 +1986,15 @@ struct fdgpu_ed25519_ctx {
   hipEvent_t  gev;               /*   recorded behind a batch's last gather; the ctx stream waits for it */
   unsigned long * d_gcnt;        /*   gather blocks completed (device counter) */
   unsigned long   g_launched;    /*   records whose gather has been launched, cumulative */
+  unsigned        gather_cus;    /*   CUs reserved for the gathers (fdgpu_ed25519_reserve_gather_cus), 0 = none */
+  enum { NGT = 64 };
+  unsigned long * h_gtime;       /*   pinned [NGT][2]: GPU clock (100 MHz ticks) at a gather's start / end */
+  unsigned long * d_gtime;
+  struct { unsigned long target, t_launch; } gt[ NGT ];   /* host side of those gathers: count they end at, launch ns */
+  unsigned long   gt_head, gt_tail;
+  double          gclk_off_ns;   /*   GPU clock ns - host CLOCK_MONOTONIC ns (calibrated once) */
+  int             gclk_ok;
+  unsigned long   gs_n, gs_start_sum, gs_start_max, gs_run_sum, gs_run_max;   /* fdgpu_ed25519_gather_stats */
   unsigned long n_batches, n_txns;                /* async batches launched, transactions in them */
   unsigned long launch_ns;                        /* host time inside slot_launch */
   unsigned long volatile * h_flag;                /* per slot: completion token written by fd_done_kernel (pinned);
@@ -2314,6 +2331,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   if( ctx->cstream ) { (void)hipStreamSynchronize( ctx->cstream ); (void)hipStreamDestroy( ctx->cstream ); }
   if( ctx->gstream ) { (void)hipStreamSynchronize( ctx->gstream ); (void)hipStreamDestroy( ctx->gstream ); }
   if( ctx->gev ) (void)hipEventDestroy( ctx->gev );
+  if( ctx->h_gtime ) (void)hipHostFree( ctx->h_gtime );
   (void)hipFree( ctx->d_gcnt );
   if( ctx->h_flag ) (void)hipHostFree( (void *)ctx->h_flag );
   for( unsigned long i=0; i<FD_PIPE_MAX; i++ ) if( ctx->pipe_ev[i] ) (void)hipEventDestroy( ctx->pipe_ev[i] );
@@ -2753,17 +2771,68 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
    contexts, one per verify tile.) */
 /* launch the gather of slot sl's records not yet gathered (mode 3) on the
    context's gather stream; returns how many, or < 0 */
+__global__ void fd_clock_kernel( unsigned long * out ) {
+  __hip_atomic_store( out, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+}
+
+/* GPU clock -> host clock offset, from one probe launch (error <= half its round trip, ~10 us) */
+static void gclk_calibrate( fdgpu_ed25519_ctx_t * ctx ) {
+  unsigned long volatile * w = (unsigned long volatile *)ctx->h_gtime;
+  w[0] = 0UL;
+  unsigned long t0 = fd_now_ns();
+  hipLaunchKernelGGL( fd_clock_kernel, dim3(1), dim3(1), 0, ctx->gstream, ctx->d_gtime );
+  if( hipStreamSynchronize( ctx->gstream ) != hipSuccess || !w[0] ) return;
+  unsigned long t1 = fd_now_ns();
+  ctx->gclk_off_ns = (double)w[0] * 10.0 - 0.5 * ( (double)t0 + (double)t1 );
+  ctx->gclk_ok = 1;
+}
+
+/* account the timed gathers whose count has been reached */
+static void gather_times( fdgpu_ed25519_ctx_t * ctx, unsigned long gathered ) {
+  while( ctx->gt_head < ctx->gt_tail && ctx->gt[ ctx->gt_head % fdgpu_ed25519_ctx_t::NGT ].target <= gathered ) {
+    unsigned long i = ctx->gt_head % fdgpu_ed25519_ctx_t::NGT;
+    unsigned long const volatile * w = (unsigned long const volatile *)( ctx->h_gtime + 2*i );
+    if( ctx->gclk_ok && w[0] && w[1] >= w[0] ) {
+      double st = (double)w[0] * 10.0 - ctx->gclk_off_ns - (double)ctx->gt[i].t_launch;
+      unsigned long sd = st > 0. ? (unsigned long)st : 0UL, rn = ( w[1] - w[0] ) * 10UL;
+      ctx->gs_n++; ctx->gs_start_sum += sd; ctx->gs_run_sum += rn;
+      if( sd > ctx->gs_start_max ) ctx->gs_start_max = sd;
+      if( rn > ctx->gs_run_max ) ctx->gs_run_max = rn;
+    }
+    ctx->gt_head++;
+  }
+}
+
 static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
   unsigned long n = sl.txn_cnt - sl.gathered;
   if( !n ) return 0;
+  if( !ctx->h_gtime ) {
+    HIPCHK( hipHostMalloc( (void **)&ctx->h_gtime, ( fdgpu_ed25519_ctx_t::NGT + 1 ) * 2 * sizeof(unsigned long), hipHostMallocDefault ), -2 );
+    HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_gtime, (void *)ctx->h_gtime, 0 ), -2 );
+  }
   if( !ctx->gstream ) {
-    HIPCHK( hipStreamCreateWithFlags( &ctx->gstream, hipStreamNonBlocking ), -2 );
+    /* the copies bound how long a frag stays exposed to a lapping producer: the highest stream
+       priority, so the dispatcher starts them ahead of queued verify work as CU slots free up */
+    int lo = 0, hi = 0;
+    HIPCHK( hipDeviceGetStreamPriorityRange( &lo, &hi ), -2 );
+    HIPCHK( hipStreamCreateWithPriority( &ctx->gstream, hipStreamNonBlocking, hi ), -2 );
     HIPCHK( hipEventCreateWithFlags( &ctx->gev, hipEventDisableTiming ), -2 );
   }
+  if( !ctx->gclk_ok && !ctx->g_launched ) gclk_calibrate( ctx );
   unsigned long target = ctx->g_launched + n;
+  /* time this gather if a ring entry is free (the ring is drained as gathers complete) */
+  unsigned long * gt = NULL;
+  gather_times( ctx, fdgpu_ed25519_gathered( ctx ) );
+  if( ctx->gt_tail - ctx->gt_head < fdgpu_ed25519_ctx_t::NGT ) {
+    unsigned long i = ctx->gt_tail % fdgpu_ed25519_ctx_t::NGT;
+    ctx->h_gtime[ 2*i ] = 0UL; ctx->h_gtime[ 2*i + 1 ] = 0UL;
+    ctx->gt[i].target = target; ctx->gt[i].t_launch = fd_now_ns();
+    ctx->gt_tail++;
+    gt = ctx->d_gtime + 2*i;
+  } else gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT;   /* untimed: a scratch entry */
   hipLaunchKernelGGL( fd_gather_kernel, dim3( (unsigned)n ), dim3( 64 ), 0, ctx->gstream, sl.g_dev + sl.gathered,
                       sl.d_payload, sl.ref_dev + sl.ref_lo, sl.d_ovr + sl.gathered, ctx->d_gcnt,
-                      (unsigned long *)( ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT + 1 ), target );
+                      (unsigned long *)( ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT + 1 ), target, gt );
   HIPCHK( hipGetLastError(), -2 );
   ctx->g_launched = target; sl.gathered = sl.txn_cnt;
   return (int)n;
@@ -3115,6 +3184,36 @@ fdgpu_ed25519_gathered( fdgpu_ed25519_ctx_t const * ctx ) {
 
 extern "C" unsigned long
 fdgpu_ed25519_gather_launched( fdgpu_ed25519_ctx_t const * ctx ) { return ctx->g_launched; }
+
+extern "C" void
+fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 5 ] ) {
+  gather_times( ctx, fdgpu_ed25519_gathered( ctx ) );
+  out[0] = ctx->gs_n; out[1] = ctx->gs_start_sum; out[2] = ctx->gs_start_max; out[3] = ctx->gs_run_sum; out[4] = ctx->gs_run_max;
+}
+
+extern "C" int
+fdgpu_ed25519_reserve_gather_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n ) {
+  if( !ctx || ctx->gstream || !ctx->inflight.empty() || ctx->slot[ ctx->cur ].txn_cnt ) {
+    fd_err = "fdgpu_ed25519_reserve_gather_cus: only on a fresh context"; return -1;
+  }
+  if( !n ) return 0;
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  int ncu = 0;
+  HIPCHK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, ctx->device ), -2 );
+  if( (int)n >= ncu ) { fd_err = "fdgpu_ed25519_reserve_gather_cus: n >= CUs"; return -1; }
+  std::vector<uint32_t> cm( (size_t)( ncu + 31 ) / 32, 0u ), gm( cm.size(), 0u );
+  for( int c=0; c<ncu; c++ ) ( c >= ncu - (int)n ? gm : cm )[ (size_t)c / 32 ] |= 1u << ( c % 32 );
+  hipStream_t s = NULL, g = NULL;
+  HIPCHK( hipExtStreamCreateWithCUMask( &s, (uint32_t)cm.size(), cm.data() ), -2 );
+  hipError_t e = hipExtStreamCreateWithCUMask( &g, (uint32_t)gm.size(), gm.data() );
+  if( e != hipSuccess ) { (void)hipStreamDestroy( s ); set_err( "hipExtStreamCreateWithCUMask", e ); return -2; }
+  e = hipEventCreateWithFlags( &ctx->gev, hipEventDisableTiming );
+  if( e != hipSuccess ) { (void)hipStreamDestroy( s ); (void)hipStreamDestroy( g ); set_err( "hipEventCreate", e ); return -2; }
+  (void)hipStreamSynchronize( ctx->stream );
+  (void)hipStreamDestroy( ctx->stream );
+  ctx->stream = s; ctx->gstream = g; ctx->gather_cus = n;
+  return 0;
+}
 
 extern "C" int
 fdgpu_ed25519_gather_wait( fdgpu_ed25519_ctx_t * ctx ) {

@@ -289,6 +289,7 @@ typedef struct {
   ulong cidx;                            /* zero-copy: the frag's index among context k's gathered submissions */
   unsigned short payload_sz;
   int   k;                               /* engine context the frag's batch went to */
+  int   ovr;                             /* the caller's seq re-check failed after during_frag's host copy */
 } vt_pend_t;
 
 /* Engine contexts per tile (fdgpu_vtile_opts_t.nctx, 1..VT_NCTX_MAX, default 2).
@@ -329,6 +330,7 @@ struct fdgpu_vtile {
   ulong                 pend_cap, pend_head, pend_tail;   /* monotonic counters */
   int                   bundle_failed;
   ulong                 bundle_id;
+  ulong                 rr_idx, rr_cnt;  /* before_frag's round robin (fdgpu_vtile_set_round_robin) */
   ulong                 metrics[5];
   /* zero-copy intake (fdgpu_vtile_set_in_link): frags stay in the in
      dcache, the GPU gathers them; in_mc (optional) for the overrun check */
@@ -360,6 +362,9 @@ vt_ctx_new( fdgpu_vtile_t const * vt ) {
     /* the GPU computes the HA dedup tags and, for gathered records, stores
        txn_t_sz: after_frag then touches neither payload nor record */
     fdgpu_ed25519_set_dedup( c, vt->gpu_tag, vt->seed );
+    if( vt->opt.gather_cus && fdgpu_ed25519_reserve_gather_cus( c, vt->opt.gather_cus ) ) {
+      fdgpu_ed25519_ctx_delete( c ); return NULL;
+    }
     fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
   }
   return c;
@@ -493,17 +498,22 @@ void
 fdgpu_vtile_debug_fault( fdgpu_vtile_t * vt, int k ) { if( k >= 0 && k < vt->nctx ) fdgpu_ed25519_debug_fault( vt->ctx[k] ); }
 
 void
-fdgpu_vtile_gpu_metrics( fdgpu_vtile_t const * vt, fdgpu_vtile_gpu_metrics_t * out ) {
+fdgpu_vtile_gpu_metrics( fdgpu_vtile_t * vt, fdgpu_vtile_gpu_metrics_t * out ) {
   *out = vt->gm;
   ulong f, i, infl = 0UL;
   memset( out->lat_hist, 0, sizeof(out->lat_hist) );
   out->batches = out->batch_txns = out->launch_ns = 0UL;
+  memset( out->gather_gpu, 0, sizeof(out->gather_gpu) );
   for( int k=0; k<vt->nctx; k++ ) {
     fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i ); infl += i;
     /* the engine counts every launch (a full slot launches inside submit) and times each batch */
     ulong b, t, h[ FDGPU_LAT_BUCKETS ];
     fdgpu_ed25519_batch_stats( vt->ctx[k], &b, &t, h );
     ulong lns, nl; fdgpu_ed25519_launch_stats( vt->ctx[k], &lns, &nl ); out->launch_ns += lns;
+    ulong gs[5]; fdgpu_ed25519_gather_stats( vt->ctx[k], gs );
+    out->gather_gpu[0] += gs[0]; out->gather_gpu[1] += gs[1]; out->gather_gpu[3] += gs[3];
+    if( gs[2] > out->gather_gpu[2] ) out->gather_gpu[2] = gs[2];
+    if( gs[4] > out->gather_gpu[4] ) out->gather_gpu[4] = gs[4];
     out->batches += b; out->batch_txns += t;
     for( int j=0; j<FDGPU_LAT_BUCKETS; j++ ) out->lat_hist[j] += h[j];
   }
@@ -601,22 +611,33 @@ fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt ) {
   return vt->pend_head < vt->pend_tail ? vt->pend[ vt->pend_head % vt->pend_cap ].seq : ~0UL;
 }
 
+/* launch decision of housekeep: 1 if context f's filling batch should go now */
+static int
+vt_should_launch( fdgpu_vtile_t * vt, int f, ulong max_inflight, ulong now, ulong * filling ) {
+  ulong inflight;
+  if( fdgpu_ed25519_faulted( vt->ctx[f] ) ) return 0;
+  fdgpu_ed25519_pipeline_state( vt->ctx[f], filling, &inflight );
+  /* keep at least one staging slot free to accumulate in: with every slot
+     in flight, each freed slot would be relaunched after a handful of
+     frags and the pipeline would degenerate into tiny batches */
+  if( max_inflight > 3UL ) max_inflight = 3UL;
+  if( !*filling || inflight >= max_inflight ) return 0;
+  /* throughput knob (opt.min_batch / max_wait_ns): a partial batch smaller than min_batch waits until
+     its oldest frag has waited max_wait -- bigger GPU batches under load */
+  if( *filling < vt->min_batch && now - vt->fill_t0 < vt->max_wait_ns ) return 0;
+  if( vt->nctx > 1 && *filling < vt->batch ) {
+    /* stagger: launch once every other context's newest batch has run
+       batch_ns / nctx (or that context is idle) */
+    ulong stagger = (ulong)( vt->batch_ns / (double)vt->nctx );
+    for( int k=0; k<vt->nctx; k++ )
+      if( k != f && vt->busy[k] && now - vt->launch_ns[k] < stagger ) return 0;
+  }
+  return 1;
+}
+
 int
 fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
-  ulong filling, inflight, now = now_ns();
-  if( vt->zc ) {
-    /* the GPU copy of the frags taken since the last one: once the oldest has waited copy_wait_ns or
-       copy_min are waiting -- what bounds a frag's exposure to a lapping producer (and a reliable
-       link's credit) to about copy_wait_ns plus one gather, whatever the batch size */
-    int f = vt->fill;
-    if( vt->copy_t0 && !fdgpu_ed25519_faulted( vt->ctx[f] ) &&
-        ( now - vt->copy_t0 >= vt->opt.copy_wait_ns ||
-          vt->sub_cnt[f] - fdgpu_ed25519_gather_launched( vt->ctx[f] ) >= vt->opt.copy_min ) ) {
-      if( fdgpu_ed25519_gather( vt->ctx[f] ) > 0 ) vt_copy_launched( vt, f );
-      vt->copy_t0 = 0UL;
-    }
-    vt_copy_poll( vt );
-  }
+  ulong filling, now = now_ns();
   /* batch duration: a context's batches have drained (inflight counts
      launched slots not yet fully polled) */
   for( int k=0; k<vt->nctx; k++ ) {
@@ -627,29 +648,69 @@ fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
       vt->busy[k] = 0; vt->batch_ns = 0.875*vt->batch_ns + 0.125*(double)( now - vt->launch_ns[k] );
     }
   }
-  int f = vt->fill;
-  if( fdgpu_ed25519_faulted( vt->ctx[f] ) ) return 0;
-  fdgpu_ed25519_pipeline_state( vt->ctx[f], &filling, &inflight );
-  /* keep at least one staging slot free to accumulate in: with every slot
-     in flight, each freed slot would be relaunched after a handful of
-     frags and the pipeline would degenerate into tiny batches */
-  if( max_inflight > 3UL ) max_inflight = 3UL;
-  if( !filling || inflight >= max_inflight ) return 0;
-  /* throughput knob (env FDGPU_VTILE_MIN_BATCH / _MAX_WAIT_US): a partial batch smaller than
-     min_batch waits until its oldest frag has waited max_wait -- bigger GPU batches under load */
-  if( filling < vt->min_batch && now - vt->fill_t0 < vt->max_wait_ns ) return 0;
-  if( vt->nctx > 1 && filling < vt->batch ) {
-    /* stagger: launch once every other context's newest batch has run
-       batch_ns / nctx (or that context is idle) */
-    ulong stagger = (ulong)( vt->batch_ns / (double)vt->nctx );
-    for( int k=0; k<vt->nctx; k++ )
-      if( k != f && vt->busy[k] && now - vt->launch_ns[k] < stagger ) return 0;
+  int f = vt->fill, launched = 0;
+  if( vt_should_launch( vt, f, max_inflight, now, &filling ) ) {
+    vt_fence();
+    if( !fdgpu_ed25519_flush( vt->ctx[f] ) ) {   /* (the launch gathers the batch's frags not yet copied) */
+      vt_launched( vt, f, now, filling );
+      vt->fill = ( f + 1 ) % vt->nctx;
+      vt->copy_t0 = 0UL;
+      launched = 1;
+    }
+  } else if( vt->zc && vt->copy_t0 && !fdgpu_ed25519_faulted( vt->ctx[f] ) &&
+             ( now - vt->copy_t0 >= vt->opt.copy_wait_ns ||
+               vt->sub_cnt[f] - fdgpu_ed25519_gather_launched( vt->ctx[f] ) >= vt->opt.copy_min ) ) {
+    /* the batch waits for the GPU: copy the frags taken since the last copy now, once the oldest has
+       waited copy_wait_ns or copy_min are waiting -- what bounds a frag's exposure to a lapping
+       producer (and a reliable link's credit) to about copy_wait_ns plus one gather, whatever the
+       batch size and however long it queues */
+    if( fdgpu_ed25519_gather( vt->ctx[f] ) > 0 ) vt_copy_launched( vt, f );
+    vt->copy_t0 = 0UL;
   }
+  vt_copy_poll( vt );
+  return launched;
+}
+
+/* room for one more frag, and a healthy context to fill: 0, -2 (ring full: drain and retry), -3 */
+static int
+vt_room( fdgpu_vtile_t * vt ) {
   vt_fence();
-  if( fdgpu_ed25519_flush( vt->ctx[f] ) ) return 0;
-  vt_launched( vt, f, now, filling );
-  vt->fill = ( f + 1 ) % vt->nctx;
-  return 1;
+  if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_vtile_flush( vt ); return -2; }
+  /* a faulted context takes no more frags: fill the next healthy one (none: -3) */
+  for( int i=0; i<vt->nctx && fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ); i++ ) vt->fill = ( vt->fill + 1 ) % vt->nctx;
+  if( fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ) ) return -3;
+  return 0;
+}
+
+/* the frag whose record is (or will be, gathered) at the out dcache's out_chunk was submitted */
+static void
+vt_taken( fdgpu_vtile_t * vt, ulong seq, ulong tsorig, ulong bundle_id, unsigned short payload_sz ) {
+  vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
+  p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill; p->ovr = 0;
+  if( vt->zc ) {
+    p->cidx = vt->sub_cnt[ vt->fill ]++;
+    vt->uncopied[ FDGPU_VTILE_SEQ_LINK( seq ) ]++;
+    if( !vt->copy_t0 ) vt->copy_t0 = now_ns();
+  }
+  if( vt->min_batch ) {                          /* first frag of the filling batch: its wait starts */
+    ulong f, i; fdgpu_ed25519_pipeline_state( vt->ctx[ vt->fill ], &f, &i );
+    if( f == 1UL ) vt->fill_t0 = now_ns();
+  }
+  p->bundle_id = bundle_id; p->payload_sz = payload_sz;
+  vt->pend_tail++;
+  ulong reserve = ( ( FDGPU_TXNM_HDR_SZ + payload_sz + 1UL ) & ~1UL ) + 852UL;
+  vt->out_chunk = fdgpu_dcache_compact_next( vt->out_chunk, reserve, vt->chunk0, vt->wmark );
+}
+
+/* submit the record the host has just written at dst (the out dcache's out_chunk) */
+static int
+vt_submit_host_record( fdgpu_vtile_t * vt, uchar * dst, unsigned short payload_sz, ulong seq ) {
+  if( vt->zc )   /* keep the batch in gathered mode: the GPU "gathers" the record from where it already is */
+    return fdgpu_ed25519_submit_raw_gather_chk( vt->ctx[ vt->fill ], dst, vt->dcache, dst,
+                                                (unsigned short)( FDGPU_TXNM_HDR_SZ + payload_sz ),
+                                                (unsigned short)FDGPU_TXNM_HDR_SZ, payload_sz, vt->pend_tail, NULL,
+                                                FDGPU_VTILE_SEQ_SEQ( seq ) );
+  return fdgpu_ed25519_submit_raw_ref( vt->ctx[ vt->fill ], vt->dcache, dst + FDGPU_TXNM_HDR_SZ, payload_sz, vt->pend_tail );
 }
 
 int
@@ -658,16 +719,12 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   /* fd_verify_tile.c:78-85: the frag must hold its header + payload and
      the payload must fit the MTU (the reference FD_LOG_ERRs) */
   if( sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U || FDGPU_TXNM_HDR_SZ + in->payload_sz > sz ) return -4;
-  vt_fence();
-  if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_vtile_flush( vt ); return -2; }
-  /* a faulted context takes no more frags: fill the next healthy one (none: -3) */
-  for( int i=0; i<vt->nctx && fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ); i++ ) vt->fill = ( vt->fill + 1 ) % vt->nctx;
-  if( fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ) ) return -3;
-  uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
-  int rc;
   int link = FDGPU_VTILE_SEQ_LINK( seq );
+  if( link >= FDGPU_VTILE_IN_MAX || ( vt->zc && link >= vt->n_in ) ) return -4;   /* a link set_in_links was not told about */
+  int rc = vt_room( vt );
+  if( rc ) return rc;
+  uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
   if( vt->zc ) {   /* the GPU copies the frag into dst itself (no host copy) and re-checks its mcache line */
-    if( link >= vt->n_in ) return -4;                   /* a link set_in_links was not told about */
     fdgpu_mcache_t const * mc = vt->in_mcs[ link ];
     ulong const * seq_addr = mc ? (ulong const *)&mc->line[ FDGPU_VTILE_SEQ_SEQ( seq ) & ( mc->depth - 1UL ) ].seq : NULL;
     rc = fdgpu_ed25519_submit_raw_gather_chk( vt->ctx[ vt->fill ], (uchar const *)frag, vt->dcache, dst,
@@ -676,24 +733,76 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
                                               seq_addr, FDGPU_VTILE_SEQ_SEQ( seq ) );
   } else {
     vt_copy( dst, (uchar const *)frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
-    rc = fdgpu_ed25519_submit_raw_ref( vt->ctx[ vt->fill ], vt->dcache, dst + FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail );
+    rc = vt_submit_host_record( vt, dst, in->payload_sz, seq );
   }
   if( rc ) return rc;
-  vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
-  p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill;
-  if( vt->zc ) {
-    p->cidx = vt->sub_cnt[ vt->fill ]++;
-    vt->uncopied[ link ]++;
-    if( !vt->copy_t0 ) vt->copy_t0 = now_ns();
+  vt_taken( vt, seq, tsorig, in->bundle_id, in->payload_sz );
+  return 0;
+}
+
+/* The reference's other in kinds (fd_verify_tile.c:7-10).  before_frag
+   (:36-59): a QUIC frag, or a bundle-tile "packet" (sig 0), goes to the
+   tile with seq % round_robin_cnt == its index; a bundle (sig != 0) only
+   to verify:0, so a bundle's transactions are never interleaved across
+   tiles; a gossip update only if it is a vote (sig ==
+   FD_GOSSIP_UPDATE_TAG_VOTE) and round robin; a send-tile frag always. */
+void
+fdgpu_vtile_set_round_robin( fdgpu_vtile_t * vt, ulong idx, ulong cnt ) {
+  vt->rr_cnt = cnt ? cnt : 1UL; vt->rr_idx = idx < vt->rr_cnt ? idx : 0UL;
+}
+
+int
+fdgpu_vtile_before_frag( fdgpu_vtile_t const * vt, int in_kind, ulong seq, ulong sig ) {
+  ulong cnt = vt->rr_cnt ? vt->rr_cnt : 1UL;
+  seq = FDGPU_VTILE_SEQ_SEQ( seq );
+  int is_bundle_packet = in_kind==FDGPU_VTILE_IN_KIND_BUNDLE && !sig;
+  if( is_bundle_packet || in_kind==FDGPU_VTILE_IN_KIND_QUIC ) return ( seq % cnt ) != vt->rr_idx;
+  if( in_kind==FDGPU_VTILE_IN_KIND_BUNDLE ) return vt->rr_idx != 0UL;
+  if( in_kind==FDGPU_VTILE_IN_KIND_GOSSIP ) return ( seq % cnt ) != vt->rr_idx || sig != FDGPU_GOSSIP_UPDATE_TAG_VOTE;
+  return 0;
+}
+
+/* during_frag of every in kind (:65-101).  QUIC, bundle and send frags are
+   fd_txn_m_t records (fdgpu_vtile_during_frag).  A gossip frag is an
+   fd_gossip_update_message_t: its vote transaction becomes a fresh
+   record in the out dcache -- payload_sz, bundle_id 0, the payload -- as
+   the reference copies it; the GPU takes it from there (the gossip link
+   is reliable in the reference topology, topology.c:591, so there is no
+   overrun to check).  The reference leaves the record's other header
+   fields as the chunk's previous frag left them; here they are zero. */
+int
+fdgpu_vtile_during_frag_kind( fdgpu_vtile_t * vt, int in_kind, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
+  if( in_kind != FDGPU_VTILE_IN_KIND_GOSSIP ) {
+    if( sz > FDGPU_TPU_RAW_MTU ) return -4;                      /* fd_verify_tile.c:75-76 */
+    return fdgpu_vtile_during_frag( vt, frag, sz, seq, tsorig );
   }
-  if( vt->min_batch ) {                          /* first frag of the filling batch: its wait starts */
-    ulong f, i; fdgpu_ed25519_pipeline_state( vt->ctx[ vt->fill ], &f, &i );
-    if( f == 1UL ) vt->fill_t0 = now_ns();
-  }
-  p->bundle_id = in->bundle_id; p->payload_sz = in->payload_sz;
-  vt->pend_tail++;
-  ulong reserve = ( ( FDGPU_TXNM_HDR_SZ + in->payload_sz + 1UL ) & ~1UL ) + 852UL;
-  vt->out_chunk = fdgpu_dcache_compact_next( vt->out_chunk, reserve, vt->chunk0, vt->wmark );
+  if( sz > FDGPU_GOSSIP_MSG_MAX || sz < FDGPU_GOSSIP_VOTE_TXN_OFF ) return -4;   /* :89-90 */
+  uchar const * msg = (uchar const *)frag;
+  ulong txn_sz; memcpy( &txn_sz, msg + FDGPU_GOSSIP_VOTE_TXN_SZ_OFF, sizeof(ulong) );
+  /* the reference copies vote.txn_sz bytes out of the 1232-byte vote.txn array unchecked; past the array
+     (or past the frag) there is nothing defined to copy: refused as corrupt */
+  if( txn_sz > 1232UL || FDGPU_GOSSIP_VOTE_TXN_OFF + txn_sz > sz ) return -4;
+  int link = FDGPU_VTILE_SEQ_LINK( seq );
+  if( link >= FDGPU_VTILE_IN_MAX ) return -4;
+  int rc = vt_room( vt );
+  if( rc ) return rc;
+  uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
+  fdgpu_txnm_t * t = (fdgpu_txnm_t *)dst;
+  memset( t, 0, FDGPU_TXNM_HDR_SZ );
+  t->payload_sz = (unsigned short)txn_sz;
+  t->bundle_id = 0UL;
+  memcpy( dst + FDGPU_TXNM_HDR_SZ, msg + FDGPU_GOSSIP_VOTE_TXN_OFF, txn_sz );
+  vt_fence();
+  rc = vt_submit_host_record( vt, dst, (unsigned short)txn_sz, seq );
+  if( rc ) return rc;
+  vt_taken( vt, seq, tsorig, 0UL, (unsigned short)txn_sz );
+  return 0;
+}
+
+int
+fdgpu_vtile_during_frag_overrun( fdgpu_vtile_t * vt ) {
+  if( vt->pend_tail == vt->pend_head ) return -1;
+  vt->pend[ ( vt->pend_tail - 1UL ) % vt->pend_cap ].ovr = 1;
   return 0;
 }
 
@@ -709,7 +818,7 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
   /* zero-copy: the GPU re-read the frag's mcache line right after copying it and found it reused
      -- the stem's "overrun while reading" (fd_stem.c:667-686), decided at copy time: the frag
      never reaches after_frag in the reference, so no bundle state or metric changes */
-  if( code == FDGPU_ERR_OVERRUN ) { vt->overruns++; return FDGPU_VTILE_OVERRUN; }
+  if( code == FDGPU_ERR_OVERRUN || p->ovr ) { vt->overruns++; return FDGPU_VTILE_OVERRUN; }
   fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( vt->dcache + p->chunk * FDGPU_CHUNK_SZ );
   if( !vt->zc ) txnm->txn_t_sz = (unsigned short)fp;
   int is_bundle = p->bundle_id != 0UL;
@@ -1254,7 +1363,7 @@ static void * link_tile( void * _a ) {
   ulong mult = c->out_mult ? c->out_mult : 6UL;
   fdgpu_vtile_opts_t vo;
   memset( &vo, 0, sizeof(vo) );
-  vo.nctx = c->nctx; vo.copy_wait_ns = c->copy_wait_ns; vo.copy_min = c->copy_min;
+  vo.nctx = c->nctx; vo.copy_wait_ns = c->copy_wait_ns; vo.copy_min = c->copy_min; vo.gather_cus = c->gather_cus;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                              ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
@@ -1477,6 +1586,10 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     st->launch_ns += r->gm.launch_ns;
     st->copies += r->gm.copies; st->copy_lat_n += r->gm.copy_lat_n; st->copy_lat_ns_sum += r->gm.copy_lat_ns_sum;
     if( r->gm.copy_lat_ns_max > st->copy_lat_ns_max ) st->copy_lat_ns_max = r->gm.copy_lat_ns_max;
+    for( int k=0; k<5; k++ ) {
+      if( k == 2 || k == 4 ) { if( r->gm.gather_gpu[k] > st->gather_gpu[k] ) st->gather_gpu[k] = r->gm.gather_gpu[k]; }
+      else st->gather_gpu[k] += r->gm.gather_gpu[k];
+    }
     st->tile_idle_ns += r->ns_idle;
     for( int k=0; k<8; k++ ) st->prof_ns[k] += r->prof[k];
     if( r->t_last > t_end ) t_end = r->t_last;

@@ -15,6 +15,14 @@ LIB_PATH = os.environ.get("FDGPU_VTILE_LIB") or os.path.join(PKG_DIR, "libfdgpu_
 TXNM_HDR_SZ = 80
 CHUNK_SZ = 64
 PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL, OVERRUN, GPU_FAULT = range(7)
+IN_QUIC, IN_BUNDLE, IN_GOSSIP, IN_SEND = range(4)        # fd_verify_tile.c:7-10
+
+
+def FDGPU_VTILE_SEQ(link: int, seq: int) -> int:
+    """include/fd_verify_gpu.h FDGPU_VTILE_SEQ: a frag's seq with its in link in bits 56..63"""
+    return (link << 56) | seq
+GOSSIP_TAG_VOTE = 3                                      # fd_gossip_types.h:26
+GOSSIP_VOTE_TXN_SZ_OFF, GOSSIP_VOTE_TXN_OFF, GOSSIP_MSG_SZ = 64, 72, 1304   # fd_gossip_update_message_t, x86-64
 LAT_BUCKETS = 40
 
 EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
@@ -23,7 +31,8 @@ EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_
            "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_housekeep", "fdgpu_vtile_pipeline_state", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
            "fdgpu_vtile_metrics", "fdgpu_vtile_set_in_link", "fdgpu_vtile_set_in_links", "fdgpu_vtile_oldest_pending_seq", "fdgpu_vtile_overruns",
            "fdgpu_vtile_faulted", "fdgpu_vtile_recover", "fdgpu_vtile_debug_fault", "fdgpu_vtile_gpu_metrics",
-           "fdgpu_vtile_new_opts", "fdgpu_vtile_copy", "fdgpu_vtile_copy_state",
+           "fdgpu_vtile_new_opts", "fdgpu_vtile_copy", "fdgpu_vtile_copy_state", "fdgpu_vtile_during_frag_overrun",
+           "fdgpu_vtile_set_round_robin", "fdgpu_vtile_before_frag", "fdgpu_vtile_during_frag_kind",
            "fdgpu_link_new", "fdgpu_link_join", "fdgpu_link_delete", "fdgpu_link_joined", "fdgpu_link_cfg",
            "fdgpu_link_run", "fdgpu_link_tiles_of", "fdgpu_link_mcache", "fdgpu_link_dcache", "fdgpu_link_result",
            "fdgpu_stream_run", "fdgpu_stream_bench")
@@ -51,17 +60,19 @@ class GpuMetrics(ctypes.Structure):
                 ("lat_hist", ctypes.c_ulong * LAT_BUCKETS), ("wait_ns", ctypes.c_ulong),
                 ("poll_ns", ctypes.c_ulong), ("after_ns", ctypes.c_ulong),
                 ("launch_ns", ctypes.c_ulong), ("copies", ctypes.c_ulong), ("copy_lat_n", ctypes.c_ulong),
-                ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong)]
+                ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong),
+                ("gather_gpu", ctypes.c_ulong * 5)]
 
     def as_dict(self) -> dict:
-        return {k: (list(getattr(self, k)) if k == "lat_hist" else int(getattr(self, k))) for k, _ in self._fields_}
+        return {k: (list(getattr(self, k)) if k in ("lat_hist", "gather_gpu") else int(getattr(self, k)))
+                for k, _ in self._fields_}
 
 
 class VTileOpts(ctypes.Structure):
     """fdgpu_vtile_opts_t (0 = default everywhere)."""
     _fields_ = [("nctx", ctypes.c_int), ("host_dedup_tag", ctypes.c_int), ("small_max", ctypes.c_ulong),
                 ("min_batch", ctypes.c_ulong), ("max_wait_ns", ctypes.c_ulong), ("copy_wait_ns", ctypes.c_ulong),
-                ("copy_min", ctypes.c_ulong)]
+                ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint)]
 
 
 class StreamCfg(ctypes.Structure):
@@ -69,7 +80,7 @@ class StreamCfg(ctypes.Structure):
                 ("rate_fps", ctypes.c_double), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int),
                 ("zero_copy", ctypes.c_int), ("reliable", ctypes.c_int), ("producers", ctypes.c_int),
                 ("nctx", ctypes.c_int), ("prof", ctypes.c_int), ("out_mult", ctypes.c_ulong),
-                ("copy_wait_ns", ctypes.c_ulong), ("copy_min", ctypes.c_ulong)]
+                ("copy_wait_ns", ctypes.c_ulong), ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint)]
 
 
 class StreamStats(ctypes.Structure):
@@ -83,13 +94,14 @@ class StreamStats(ctypes.Structure):
                 ("gpu_wait_ns", ctypes.c_ulong), ("poll_ns", ctypes.c_ulong), ("after_ns", ctypes.c_ulong),
                 ("launch_ns", ctypes.c_ulong), ("tile_idle_ns", ctypes.c_ulong), ("prod_seconds", ctypes.c_double),
                 ("prod_wait_ns", ctypes.c_ulong), ("prof_ns", ctypes.c_ulong * 8), ("copies", ctypes.c_ulong),
-                ("copy_lat_n", ctypes.c_ulong), ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong)]
+                ("copy_lat_n", ctypes.c_ulong), ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong),
+                ("gather_gpu", ctypes.c_ulong * 5)]
 
     def as_dict(self) -> dict:
         out = {}
         for k, _ in self._fields_:
             v = getattr(self, k)
-            out[k] = list(v) if k in ("metrics", "tile_ns", "gpu_lat_hist", "prof_ns") else v
+            out[k] = list(v) if k in ("metrics", "tile_ns", "gpu_lat_hist", "prof_ns", "gather_gpu") else v
         return out
 
 
@@ -126,6 +138,10 @@ def load():
         L.fdgpu_vtile_copy.argtypes = [vp, ctypes.c_int]
         L.fdgpu_vtile_copy_state.restype = ul
         L.fdgpu_vtile_copy_state.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_ulong)]
+        L.fdgpu_vtile_during_frag_overrun.argtypes = [vp]
+        L.fdgpu_vtile_set_round_robin.argtypes = [vp, ul, ul]
+        L.fdgpu_vtile_before_frag.argtypes = [vp, ctypes.c_int, ul, ul]
+        L.fdgpu_vtile_during_frag_kind.argtypes = [vp, ctypes.c_int, vp, ul, ul, ul]
         L.fdgpu_vtile_delete.argtypes = [vp]
         L.fdgpu_vtile_out_dcache.restype = vp
         L.fdgpu_vtile_out_dcache.argtypes = [vp]
@@ -193,6 +209,17 @@ class TCache:
             self.p = None
 
 
+def gossip_vote_msg(txn: bytes, tag: int = GOSSIP_TAG_VOTE, origin: bytes = bytes(32)) -> bytes:
+    """An fd_gossip_update_message_t (src/flamenco/gossip/fd_gossip_types.h:182-205, x86-64 layout) carrying
+    txn as its vote (tag VOTE) -- or, for another tag, whatever the union holds."""
+    b = bytearray(GOSSIP_MSG_SZ)
+    b[0] = tag
+    b[1:33] = origin[:32].ljust(32, b"\0")
+    b[GOSSIP_VOTE_TXN_SZ_OFF:GOSSIP_VOTE_TXN_SZ_OFF + 8] = len(txn).to_bytes(8, "little")
+    b[GOSSIP_VOTE_TXN_OFF:GOSSIP_VOTE_TXN_OFF + len(txn)] = txn
+    return bytes(b)
+
+
 def frag_bytes(payload: bytes, bundle_id: int = 0) -> bytes:
     h = np.zeros(1, TXNM_DTYPE)
     h["payload_sz"] = len(payload)
@@ -224,6 +251,29 @@ class VTile:
     def during_frag_at(self, addr: int, sz: int, seq: int, tsorig: int = 0) -> int:
         """during_frag on a frag already in memory at addr (zero-copy intake: inside a registered in dcache)."""
         return self.L.fdgpu_vtile_during_frag(self.p, addr, sz, seq, tsorig)
+
+    def set_round_robin(self, idx: int, cnt: int):
+        self.L.fdgpu_vtile_set_round_robin(self.p, idx, cnt)
+
+    def before_frag(self, in_kind: int, seq: int, sig: int) -> bool:
+        """fdgpu_vtile_before_frag: True = this tile skips the frag (fd_verify_tile.c:36-59)."""
+        return bool(self.L.fdgpu_vtile_before_frag(self.p, in_kind, seq, sig))
+
+    def during_frag_kind(self, in_kind: int, frag: bytes | None, seq: int, tsorig: int = 0, addr: int | None = None,
+                         sz: int | None = None) -> int:
+        """fdgpu_vtile_during_frag_kind; addr/sz: a frag already in memory (zero-copy intake)."""
+        if addr is None:
+            b = np.frombuffer(frag, np.uint8)
+            return self.L.fdgpu_vtile_during_frag_kind(self.p, in_kind, b.ctypes.data, len(frag), seq, tsorig)
+        return self.L.fdgpu_vtile_during_frag_kind(self.p, in_kind, addr, sz, seq, tsorig)
+
+    def during_frag_overrun(self) -> int:
+        return int(self.L.fdgpu_vtile_during_frag_overrun(self.p))
+
+    def set_in_links(self, mcaches) -> int:
+        """fdgpu_vtile_set_in_links: zero-copy intake from len(mcaches) links (entries may be None)."""
+        arr = (ctypes.c_void_p * len(mcaches))(*[m or None for m in mcaches])
+        return int(self.L.fdgpu_vtile_set_in_links(self.p, arr, len(mcaches)))
 
     def set_in_link(self, mcache=None) -> int:
         """Switch to zero-copy intake (fdgpu_vtile_set_in_link); mcache: an in-link mcache handle or None."""
@@ -314,10 +364,11 @@ def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
 
 
 def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers=1, nctx=0, prof=0,
-         out_mult=0, copy_wait_ns=0, copy_min=0) -> StreamCfg:
+         out_mult=0, copy_wait_ns=0, copy_min=0, gather_cus=0) -> StreamCfg:
     return StreamCfg(n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
                      gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0, producers=producers,
-                     nctx=nctx, prof=prof, out_mult=out_mult, copy_wait_ns=copy_wait_ns, copy_min=copy_min)
+                     nctx=nctx, prof=prof, out_mult=out_mult, copy_wait_ns=copy_wait_ns, copy_min=copy_min,
+                     gather_cus=gather_cus)
 
 
 def stream_run(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,

@@ -491,6 +491,18 @@ fdgpu_ed25519_submit_raw_gather_chk( fdgpu_ed25519_ctx_t * ctx,
 long          fdgpu_ed25519_gather( fdgpu_ed25519_ctx_t * ctx );
 unsigned long fdgpu_ed25519_gathered( fdgpu_ed25519_ctx_t const * ctx );
 unsigned long fdgpu_ed25519_gather_launched( fdgpu_ed25519_ctx_t const * ctx );
+/* Reserve n CUs for ctx's gathers: its verify kernels run on the other
+   CUs (a CU-masked stream) and the gathers on those n only, so a copy
+   starts at once however busy the verify kernels keep the GPU (without
+   a reservation a gather waits for wave slots the verify kernels hold).
+   Only on a fresh context (before any submit).  0, or < 0 (e.g. the
+   runtime refused CU masks: the context is unchanged). */
+int           fdgpu_ed25519_reserve_gather_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n );
+/* gathers timed on the GPU clock (mapped to host time once): out[0] how
+   many, out[1] / out[2] the sum / max of host launch -> first block's
+   start, out[3] / out[4] the sum / max of first block's start -> last
+   block's end, ns */
+void          fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 5 ] );
 /* wait until every launched gather of ctx has completed: 0, or -3 (ctx faulted) */
 int           fdgpu_ed25519_gather_wait( fdgpu_ed25519_ctx_t * ctx );
 

@@ -146,6 +146,9 @@ typedef struct fdgpu_vtile_gpu_metrics {
   unsigned long launch_ns;        /* host time inside batch launches and early copies (in during_frag, housekeep or a drain) */
   unsigned long copies;           /* zero-copy: early GPU copies started (housekeep, fdgpu_vtile_copy) */
   unsigned long copy_lat_n, copy_lat_ns_sum, copy_lat_ns_max;   /* ... of them timed: launch -> completion seen */
+  unsigned long gather_gpu[ 5 ];  /* every GPU copy (early or at a batch launch), on the GPU clock, summed over the
+                                     tile's contexts: fdgpu_ed25519_gather_stats (count, launch -> start sum / max,
+                                     start -> end sum / max, ns) */
 } fdgpu_vtile_gpu_metrics_t;
 
 /* device: HIP device; batch_txn: transactions per GPU batch (staging
@@ -168,6 +171,7 @@ typedef struct fdgpu_vtile_opts {
   unsigned long copy_wait_ns;    /* zero-copy: housekeep starts the GPU copy of the frags taken since the last one
                                     once the oldest has waited this long (0 = FDGPU_VTILE_COPY_WAIT_NS) ... */
   unsigned long copy_min;        /* ... or once this many are waiting (0 = FDGPU_VTILE_COPY_MIN) */
+  unsigned int  gather_cus;      /* CUs of the GPU reserved for the copies (fdgpu_ed25519_reserve_gather_cus; 0 = none) */
 } fdgpu_vtile_opts_t;
 
 fdgpu_vtile_t * fdgpu_vtile_new( int device, unsigned long batch_txn, unsigned long tcache_depth, unsigned long seed,
@@ -226,6 +230,39 @@ int             fdgpu_vtile_copy( fdgpu_vtile_t * vt, int blocking );
 unsigned long   fdgpu_vtile_copy_state( fdgpu_vtile_t const * vt, int link, unsigned long * copied_next );
 /* frags dropped as FDGPU_VTILE_OVERRUN */
 unsigned long   fdgpu_vtile_overruns( fdgpu_vtile_t const * vt );
+/* The stem's seq re-check after during_frag's HOST copy (no zero-copy
+   intake) found the frag overrun: it is abandoned -- completed as
+   FDGPU_VTILE_OVERRUN, never published (fd_stem.c:667-686 skips
+   after_frag).  Call right after the during_frag that took it.  0, or -1
+   if nothing is pending. */
+int             fdgpu_vtile_during_frag_overrun( fdgpu_vtile_t * vt );
+
+/* ---- the reference's in kinds (fd_verify_tile.c:7-10, 36-101) -------- */
+#define FDGPU_VTILE_IN_KIND_QUIC     (0)
+#define FDGPU_VTILE_IN_KIND_BUNDLE   (1)
+#define FDGPU_VTILE_IN_KIND_GOSSIP   (2)
+#define FDGPU_VTILE_IN_KIND_SEND     (3)
+#define FDGPU_TPU_RAW_MTU            (1312UL)  /* FD_TPU_RAW_MTU: fd_txn_m_t header + FD_TPU_MTU, src/disco/fd_txn_m_t.h */
+#define FDGPU_GOSSIP_UPDATE_TAG_VOTE (3UL)     /* src/flamenco/gossip/fd_gossip_types.h:26 */
+/* what the tile reads of an fd_gossip_update_message_t (fd_gossip_types.h:128-205, x86-64 layout):
+   the ulong vote.txn_sz and the vote.txn bytes */
+#define FDGPU_GOSSIP_VOTE_TXN_SZ_OFF (64UL)
+#define FDGPU_GOSSIP_VOTE_TXN_OFF    (72UL)
+#define FDGPU_GOSSIP_MSG_MAX         (2048UL)  /* fd_verify_tile.c:89-90 */
+/* before_frag's round robin: this tile is verify:idx of cnt */
+void            fdgpu_vtile_set_round_robin( fdgpu_vtile_t * vt, unsigned long idx, unsigned long cnt );
+/* before_frag (fd_verify_tile.c:36-59): 1 = this tile skips the frag.  A QUIC frag or a bundle-tile
+   packet (sig 0) round robin; a bundle (sig != 0) only verify:0; a gossip update round robin and only a
+   vote (sig == FDGPU_GOSSIP_UPDATE_TAG_VOTE); a send-tile frag never skipped. */
+int             fdgpu_vtile_before_frag( fdgpu_vtile_t const * vt, int in_kind, unsigned long seq, unsigned long sig );
+/* during_frag of any in kind: QUIC / bundle / send frags are fd_txn_m_t records (fdgpu_vtile_during_frag;
+   sz > FDGPU_TPU_RAW_MTU is -4, the reference's FD_LOG_ERR); a gossip frag is an
+   fd_gossip_update_message_t whose vote transaction becomes a fresh out-dcache record (payload_sz, bundle
+   id 0, payload), copied by the host as the reference does (sz > 2048 or a vote txn_sz past 1232 / the frag:
+   -4).  Returns as fdgpu_vtile_during_frag. */
+int             fdgpu_vtile_during_frag_kind( fdgpu_vtile_t * vt, int in_kind, void const * frag, unsigned long sz,
+                                              unsigned long seq, unsigned long tsorig );
+
 /* launch the partially filled batches (call when the input is idle) */
 int             fdgpu_vtile_flush( fdgpu_vtile_t * vt );
 /* transactions waiting in unlaunched batches, and launched batches not yet
@@ -264,7 +301,7 @@ int             fdgpu_vtile_faulted( fdgpu_vtile_t const * vt );
 int             fdgpu_vtile_recover( fdgpu_vtile_t * vt );
 /* host-side test hook: engine context k of the tile fails (fdgpu_ed25519_debug_fault) */
 void            fdgpu_vtile_debug_fault( fdgpu_vtile_t * vt, int k );
-void            fdgpu_vtile_gpu_metrics( fdgpu_vtile_t const * vt, fdgpu_vtile_gpu_metrics_t * out );
+void            fdgpu_vtile_gpu_metrics( fdgpu_vtile_t * vt, fdgpu_vtile_gpu_metrics_t * out );
 /* metrics: [0] parse_fail [1] verify_fail [2] dedup_fail
    [3] bundle_peer_fail [4] published (fd_verify_tile.c:29-34) */
 void            fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, unsigned long out[ 5 ] );
@@ -290,6 +327,7 @@ typedef struct fdgpu_stream_cfg {
   unsigned long out_mult;        /* out dcache per tile, in batch limits (0 = 6) */
   unsigned long copy_wait_ns;    /* zero-copy: fdgpu_vtile_opts_t.copy_wait_ns (0 = its default) */
   unsigned long copy_min;        /* zero-copy: fdgpu_vtile_opts_t.copy_min (0 = its default) */
+  unsigned int  gather_cus;      /* fdgpu_vtile_opts_t.gather_cus */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
@@ -317,6 +355,7 @@ typedef struct fdgpu_stream_stats {
                                     after_frags, housekeep (launch decisions) */
   unsigned long copies, copy_lat_n, copy_lat_ns_sum, copy_lat_ns_max;   /* zero-copy: early GPU copies (summed over
                                     tiles; max over tiles), as fdgpu_vtile_gpu_metrics_t */
+  unsigned long gather_gpu[ 5 ];  /* fdgpu_vtile_gpu_metrics_t.gather_gpu, summed (maxima: max) over tiles */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per

@@ -200,6 +200,45 @@ class RefTile:
         return [int(x) for x in res], [int(x) for x in metrics], recs, [int(x) for x in tag]
 
 
+    def run_kinds(self, frags, rr_idx: int, rr_cnt: int, depth: int, seed: int):
+        """The full frag path of verify:rr_idx of rr_cnt (before_frag, during_frag, after_frag) over a mixed
+        stream: frags = [(in_kind, sig, seq, frag bytes)] -- an fd_txn_m_t record for QUIC / bundle / send
+        frags, an fd_gossip_update_message_t for gossip frags.  Returns (results with -2 = skipped by
+        before_frag, metrics[5], {i: record bytes}, tags)."""
+        n = len(frags)
+        L = self.lib
+        if not hasattr(self, "_kinds"):
+            L.ref_tile_run_kinds.restype = ctypes.c_int
+            L.ref_tile_run_kinds.argtypes = [ctypes.c_void_p] * 6 + [ctypes.c_ulong] * 5 + [ctypes.c_void_p] * 3 + \
+                [ctypes.c_ulong, ctypes.c_void_p, ctypes.c_void_p]
+            self._kinds = True
+        sz = np.array([len(f) for _, _, _, f in frags], np.uint16)
+        off = np.zeros(n, np.uint32)
+        pos, parts = 0, []
+        for i, (_, _, _, f) in enumerate(frags):          # 64-B aligned, as chunks of a dcache
+            off[i] = pos
+            pad = (-len(f)) % 64
+            parts.append(bytes(f) + bytes(pad))
+            pos += len(f) + pad
+        arena = np.frombuffer(b"".join(parts) + bytes(64), np.uint8).copy()
+        kind = np.array([k for k, _, _, _ in frags], np.uint64)
+        sig = np.array([g for _, g, _, _ in frags], np.uint64)
+        seq = np.array([q for _, _, q, _ in frags], np.uint64)
+        res = np.zeros(n, np.int32)
+        rec_sz = np.zeros(n, np.uint64)
+        rec = np.zeros((n, self.REC_STRIDE), np.uint8)
+        tag = np.zeros(n, np.uint64)
+        metrics = np.zeros(5, np.uint64)
+        rc = L.ref_tile_run_kinds(arena.ctypes.data, off.ctypes.data, sz.ctypes.data, kind.ctypes.data,
+                                  seq.ctypes.data, sig.ctypes.data, n, rr_idx, rr_cnt, depth, seed, res.ctypes.data,
+                                  rec_sz.ctypes.data, rec.ctypes.data, self.REC_STRIDE, tag.ctypes.data,
+                                  metrics.ctypes.data)
+        if rc:
+            raise RuntimeError(f"ref_tile_run_kinds: {rc}")
+        recs = {i: rec[i, : int(rec_sz[i])].tobytes() for i in range(n) if res[i] == 0}
+        return [int(x) for x in res], [int(x) for x in metrics], recs, [int(x) for x in tag]
+
+
 def cpu_has_avx512_ifma() -> bool:
     try:
         with open("/proc/cpuinfo") as f:

@@ -393,3 +393,76 @@ def test_stream_run_link(tiles, reliable, zero_copy, producers):
         assert m[0] == 0 and m[1] == 0 and sum(m) == n          # no parse / verify failures in valid txns
     else:
         assert st["verdicts"] > 0
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
+@pytest.mark.parametrize("rr_idx", [0, 1])
+def test_vtile_in_kinds_vs_reference(oracle, rr_idx, zero_copy):
+    """The reference tile's four in kinds (fd_verify_tile.c:7-10) through the GPU tile, verify:rr_idx of 2:
+    QUIC frags and bundle-tile packets round robin, bundles (sig != 0) only on verify:0, gossip updates
+    round robin and only votes (whose txn becomes a fresh record, fd_verify_tile.c:85-95), send frags
+    always -- interleaved in stem order.  Which frags the tile keeps (before_frag), each kept frag's
+    outcome, the metrics, the published records and the HA dedup tags equal the reference tile's
+    (oracle/_ref/libfdref_tile.so, ref_tile_run_kinds).  zero_copy: QUIC / bundle / send records stay in
+    a registered in dcache (one link per kind); gossip votes are host-built records either way."""
+    pytest.importorskip("xxhash")
+    from firedancer_amd import engine, vtile
+    from oracle.oracle import RefTile
+    from kind_stream import make_kind_stream
+    try:
+        ref = RefTile()
+    except (FileNotFoundError, RuntimeError) as e:
+        pytest.skip(f"reference tile build unavailable: {e}")
+    frags = make_kind_stream(31)
+    depth, seed = 1 << 12, 0x77aa
+    want_res, want_m, want_recs, want_tags = ref.run_kinds([(k, g, q, fb) for k, g, q, fb, _, _ in frags], rr_idx, 2,
+                                                           depth, seed)
+    vt = vtile.VTile(device=0, batch_txn=64, tcache_depth=depth, seed=seed)
+    vt.set_round_robin(rr_idx, 2)
+    if zero_copy:
+        recs = [fb if k != vtile.IN_GOSSIP else b"" for k, _, _, fb, _, _ in frags]
+        buf, offs = in_dcache([r if r else bytes(64) for r in recs])
+        engine.host_register(buf)
+        assert vt.set_in_links([None] * 4) == 0
+    got, kept = [], []
+    for i, (k, g, q, fb, _, _) in enumerate(frags):
+        if vt.before_frag(k, q, g):
+            continue
+        kept.append(i)
+        s = vtile.FDGPU_VTILE_SEQ(k, q)
+        while True:
+            if zero_copy and k != vtile.IN_GOSSIP:
+                rc = vt.during_frag_kind(k, None, s, addr=buf.ctypes.data + offs[i], sz=len(fb))
+            else:
+                rc = vt.during_frag_kind(k, fb, s)
+            if rc != -2:
+                break
+            got += vt.after_frags(blocking=True)
+        assert rc == 0, rc
+        if i % 29 == 0:
+            got += vt.after_frags(blocking=False)
+    vt.flush()
+    while vt.pending():
+        got += vt.after_frags(blocking=True)
+    assert kept == [i for i, r in enumerate(want_res) if r != -2]
+    assert [g[0] & ((1 << 56) - 1) for g in got] == [frags[i][2] for i in kept]
+    assert [g[1] for g in got] == [want_res[i] for i in kept]
+    assert vt.metrics() == want_m
+    bad = []
+    for (seqv, r, chunk, sz, tag), i in zip(got, kept):
+        if r != vtile.PUBLISH:
+            continue
+        rec, want = vt.record(chunk, sz), want_recs[i]
+        hl = 80 + len(frags[i][4])
+        same = len(rec) == len(want) and rec[(hl + 1) & ~1:] == want[(hl + 1) & ~1:] and rec[80:hl] == want[80:hl]
+        if frags[i][0] == vtile.IN_GOSSIP:     # a vote record: payload_sz, txn_t_sz, bundle id (the rest is stale there)
+            same = same and rec[8:12] == want[8:12] and rec[24:32] == want[24:32]
+        else:
+            same = same and rec[:80] == want[:80]
+        if not same or tag != want_tags[i]:
+            bad.append(i)
+    assert bad == []
+    assert sum(1 for i in kept if frags[i][0] == vtile.IN_GOSSIP and want_res[i] == vtile.PUBLISH) > 5
+    vt.close()
+    if zero_copy:
+        engine.host_unregister(buf)

@@ -55,3 +55,36 @@ def test_reference_tile_scenarios(ref_tile):
     assert run([(V1, 0), (I1, 0)]) == [P, D]
     assert run([(V1, 2), (I1, 3), (I1, 0), (I1, 0)]) == [P, F, F, F]
     assert run([(V1, 0), (I64, 0)]) == [P, F]
+
+
+def _before_frag_model(rr_idx, rr_cnt, kind, seq, sig):
+    """fd_verify_tile.c:36-59, as the harness and the GPU tile restate it"""
+    if (kind == 1 and not sig) or kind == 0:
+        return seq % rr_cnt != rr_idx
+    if kind == 1:
+        return rr_idx != 0
+    if kind == 2:
+        return seq % rr_cnt != rr_idx or sig != 3
+    return False
+
+
+@pytest.mark.parametrize("rr_idx", [0, 1])
+def test_reference_tile_in_kinds(ref_tile, oracle, rr_idx):
+    """The harness's in-kind dispatch (before_frag + during_frag, fd_verify_tile.c:36-101, restated in
+    ref_tile_harness.c over the reference's own fd_gossip_update_message_t) against a model: the frags
+    this tile keeps are exactly the model's, and their outcomes are the reference tile's after_frag
+    outcomes of the records the model's during_frag builds (gossip votes -> a fresh record of the vote
+    txn with bundle id 0)."""
+    pytest.importorskip("xxhash")
+    from kind_stream import make_kind_stream
+    frags = make_kind_stream(31)
+    depth, seed = 1 << 12, 0x77aa
+    res, m, recs, tags = ref_tile.run_kinds([(k, g, q, fb) for k, g, q, fb, _, _ in frags], rr_idx, 2, depth, seed)
+    keep = [i for i, (k, g, q, _, _, _) in enumerate(frags) if not _before_frag_model(rr_idx, 2, k, q, g)]
+    assert [i for i, r in enumerate(res) if r != -2] == keep
+    kinds = {k for i in keep for k in [frags[i][0]]}
+    assert kinds == {0, 1, 2, 3}
+    # the kept frags as plain (payload, bundle id) records through the single-kind reference run
+    want_res, want_m, _, _ = ref_tile.run([(frags[i][4], frags[i][5]) for i in keep], depth, seed)
+    assert [res[i] for i in keep] == want_res and m == want_m
+    assert sum(m[:4]) > 20
