@@ -2,9 +2,16 @@
 
 Verdicts are per signature, so each rank verifies its own
 shard; the only collectives are the measurement ones (MAX of the timed
-interval, MIN of the correctness flag).  Mirrors the verify tiles'
-round-robin sharding (src/disco/verify/fd_verify_tile.c:47-48): rank r
-owns the transactions whose sequence number is r mod world.
+interval, MIN of the correctness flag).
+
+Two sharding rules are used, one per bench line:
+- the headline (configs[1]) gives every rank its own synthetic batch,
+  generated from a distinct seed (`shard_seed`) and resident in that rank's
+  HBM; no rank sees another's transactions;
+- the configs[4] stream keeps the reference's verify-tile rule
+  (src/disco/verify/fd_verify_tile.c:47-48): tile i of T keeps the frags
+  with seq % T == i, and tile i runs on GPU i % G (fd_verify_gpu.c, the
+  link).  That rule lives in the tile, not here.
 """
 from __future__ import annotations
 
