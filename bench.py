@@ -179,7 +179,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 # link carries 1/G of the frags but is read by all 2G tiles -> twice the single-GPU depth
                 mcache_depth=args.stream_depth * min(procs, 2) if not paced else 1 << 18,
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
-                copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus)
+                copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus,
+                max_uncopied=args.stream_max_uncopied)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -192,6 +193,14 @@ def _leg_cfg(args, leg, procs, cal_fps):
     # unreliable, producer unthrottled: tiles that fall a lap behind are overrun and skip frags
     n = args.stream_frags if args.stream_frags > 0 else int(cal_fps * args.stream_unrel_seconds)
     return dict(base, tiles=T, n_frags=n, rate_fps=0.0, reliable=False)
+
+
+def _phases(ph) -> dict:
+    n, ng = max(ph[0], 1), max(ph[8], 1)
+    return {"batches": ph[0], "launch_to_kernels_mean": ph[1] / n * 1e-3, "launch_to_kernels_max": ph[2] * 1e-3,
+            "kernels_mean": ph[3] / n * 1e-3, "kernels_max": ph[4] * 1e-3,
+            "end_to_seen_mean": ph[5] / n * 1e-3, "end_to_seen_max": ph[6] * 1e-3,
+            "launch_to_last_gather_end_mean": ph[7] / ng * 1e-3 if ph[8] else None}
 
 
 def _leg_summary(st: dict, cfg: dict) -> dict:
@@ -228,6 +237,10 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
                            "launch_to_start_max_us": st["gather_gpu"][2] * 1e-3,
                            "run_mean_us": st["gather_gpu"][3] / max(st["gather_gpu"][0], 1) * 1e-3,
                            "run_max_us": st["gather_gpu"][4] * 1e-3},
+            # each batch's GPU time split (fdgpu_ed25519_phase_stats): launch -> its verify kernels start (its
+            # gathers and the stream's earlier batch), kernels, end -> the tile saw it; launch -> last gather end
+            "batch_phases_us": _phases(st["phase"]),
+            "copy_backlog_refusals": st["copy_backlog"],
             "inflight_max": st["inflight_max"], "gpu_batch_lat_p50_us_le": hq(0.5),
             "gpu_batch_lat_p99_us_le": hq(0.99)}
 
@@ -238,6 +251,9 @@ def stream_child_main(args) -> None:
     from firedancer_amd import vtile
     proc, procs, dev = args.stream_proc, args.stream_procs, args.stream_device
     out, cal_fps = {}, 0.0
+    if args.stream_diag_no_writeback:
+        from firedancer_amd import engine
+        engine.debug_set_opts(gather_no_writeback=1)
     payload = desc = None
     if proc == 0:
         from firedancer_amd import synth
@@ -290,7 +306,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-lat-inflight", str(args.stream_lat_inflight), "--stream-producers", str(args.stream_producers),
            "--stream-ctx", str(args.stream_ctx), "--stream-lat-ctx", str(args.stream_lat_ctx),
            "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
-           "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus)]
+           "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus),
+           "--stream-max-uncopied", str(args.stream_max_uncopied)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -350,6 +367,12 @@ def main():
     ap.add_argument("--stream-paced-seconds", type=float, default=3.0, help="length of each paced leg")
     ap.add_argument("--stream-gather-cus", type=int, default=0,
                     help="zero-copy intake: CUs each tile's engine contexts reserve for the copies (fdgpu_vtile_opts_t)")
+    ap.add_argument("--stream-max-uncopied", type=int, default=0,
+                    help="zero-copy intake: frags a tile may hold whose GPU copy has not completed (fdgpu_vtile_opts_t."
+                         "max_uncopied; 0 = its default)")
+    ap.add_argument("--stream-diag-no-writeback", action="store_true",
+                    help="DIAGNOSTIC (stream child only): gathers skip the record write-back into the out dcache, so "
+                         "published records lack their payload -- what the write-back costs; never a result")
     ap.add_argument("--stream-copy-wait-us", type=float, default=0.0,
                     help="zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
                          "waited this long (0 = fdgpu_vtile default, FDGPU_VTILE_COPY_WAIT_NS)")

@@ -1792,8 +1792,16 @@ __global__ void __launch_bounds__( 256 ) fd_btab_kernel( uint4 * out, int dbl ) 
    every earlier command of the stream -- copies included -- completed.
    The tile polls that word with a plain load instead of a HIP call per
    poll (hipEventQuery takes runtime locks every tile thread shares). */
-__global__ void fd_done_kernel( unsigned long * flag, unsigned long token ) {
+__global__ void fd_done_kernel( unsigned long * flag, unsigned long token, unsigned long * stamp ) {
+  /* stamp (pinned, may be NULL): the 100-MHz GPU clock at the batch's end (fdgpu_ed25519_phase_stats) */
+  if( stamp ) __hip_atomic_store( stamp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
   __hip_atomic_store( flag, token, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM );
+}
+
+/* the 100-MHz GPU clock when a batch's verify kernels may start (its gathers done, the stream's
+   earlier batch finished): fdgpu_ed25519_phase_stats */
+__global__ void fd_stamp_kernel( unsigned long * stamp ) {
+  __hip_atomic_store( stamp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 }
 
 struct fd_gather {             /* mode 3: copy sz bytes from src (host, device view) to arena / region offset dst */
@@ -1848,10 +1856,10 @@ fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__
       unsigned long s = __hip_atomic_load( (unsigned long *)r.seq_addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
       bad = s != r.seq;
     }
-    if( i < n16 ) { a[i] = v0; o[i] = v0; }
-    if( i + 64u < n16 ) { a[i + 64u] = v1; o[i + 64u] = v1; }
+    if( i < n16 ) { a[i] = v0; if( out ) o[i] = v0; }
+    if( i + 64u < n16 ) { a[i + 64u] = v1; if( out ) o[i + 64u] = v1; }
   } else {
-    for( ; i<n16; i+=64u ) { uint4 v = src[i]; a[i] = v; o[i] = v; }
+    for( ; i<n16; i+=64u ) { uint4 v = src[i]; a[i] = v; if( out ) o[i] = v; }
     if( r.seq_addr ) {
       asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
       unsigned long s = __hip_atomic_load( (unsigned long *)r.seq_addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
@@ -1935,6 +1943,8 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   struct fd_gather * g_dev;    /*         its device view */
   unsigned char *    d_ovr;    /*         per transaction: 1 = overrun while gathered */
   unsigned long      gathered; /*         records whose gather has been launched (fdgpu_ed25519_gather) */
+  long               gt_idx;   /*         the gt[] entry timing the batch's last gather (-1: untimed) */
+  unsigned long      gt_target;/*         ... and the gathered count it ends at (the entry may be reused) */
 };
 
 struct fdgpu_ed25519_ctx {
@@ -1955,7 +1965,8 @@ struct fdgpu_ed25519_ctx {
   uint4 * d_btab;
   fdgpu_txn_desc_t * d_rdesc;    /* raw path: descriptors derived by fd_parse_kernel */
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
-  int dsm_lanes;                 /* latency path: lanes per signature in the DSM, 0 = by batch size (env FDGPU_DSM_LANES) */
+  int dsm_lanes;                 /* latency path: lanes per signature in the DSM, 0 = by batch size (fdgpu_debug_opts_t) */
+  int gather_nowb;               /* fdgpu_debug_opts_t.gather_no_writeback (diagnostic) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
   unsigned long nofold_max;      /* fd_dsm_kernel<0> (no carry fold) for batches of at most this many signatures */
   u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
@@ -1995,6 +2006,11 @@ struct fdgpu_ed25519_ctx {
   double          gclk_off_ns;   /*   GPU clock ns - host CLOCK_MONOTONIC ns (calibrated once) */
   int             gclk_ok;
   unsigned long   gs_n, gs_start_sum, gs_start_max, gs_run_sum, gs_run_max;   /* fdgpu_ed25519_gather_stats */
+  long            last_gt;       /*   gt[] entry of the last gather launched (-1: untimed) */
+  unsigned long * h_stamp;       /*   pinned [NSLOT][2] + 1: per slot the GPU clock when its verify kernels start
+                                      (fd_stamp_kernel) and end (fd_done_kernel); [2 NSLOT]: clock calibration */
+  unsigned long * d_stamp;
+  unsigned long   ph[ 9 ];       /*   fdgpu_ed25519_phase_stats */
   unsigned long n_batches, n_txns;                /* async batches launched, transactions in them */
   unsigned long launch_ns;                        /* host time inside slot_launch */
   unsigned long volatile * h_flag;                /* per slot: completion token written by fd_done_kernel (pinned);
@@ -2019,7 +2035,7 @@ struct fdgpu_ed25519_ctx {
 static int stream_wait( fdgpu_ed25519_ctx_t * ctx, hipStream_t st, int pageable ) {
   if( !pageable ) {
     unsigned long tok = ++ctx->sync_token;
-    hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT, tok );
+    hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT, tok, (unsigned long *)NULL );
     if( hipGetLastError() == hipSuccess ) {
       unsigned long t0 = fd_now_ns();
       while( fd_now_ns() - t0 < FD_SYNC_SPIN_NS ) {
@@ -2199,14 +2215,14 @@ extern "C" void fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx );
 /* Test / A/B options of contexts created from now on (fdgpu_debug_set_opts).
    Process-wide, behind a mutex; the defaults are the product's choices. */
 static std::mutex g_dbg_mu;
-static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L };
+static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L, 0 };
 static void debug_opts_get( fdgpu_debug_opts_t * o ) { std::lock_guard<std::mutex> lk( g_dbg_mu ); *o = g_dbg; }
 
 extern "C" void
 fdgpu_debug_set_opts( fdgpu_debug_opts_t const * opts ) {
   std::lock_guard<std::mutex> lk( g_dbg_mu );
   if( opts ) g_dbg = *opts;
-  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L };
+  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L, 0 };
 }
 
 /* staging + device buffers of async slot i (once) */
@@ -2229,6 +2245,26 @@ slot_bufs( fdgpu_ed25519_ctx_t * ctx, int i ) {
 
 /* allocations of a new context; on failure the caller deletes the
    partially built context (every handle starts NULL) */
+__global__ void fd_clock_kernel( unsigned long * out ) {
+  __hip_atomic_store( out, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+}
+
+/* GPU clock -> host clock offset, from the shortest of three probe launches on the context's idle
+   stream at creation (error <= half that round trip, ~10 us) */
+static void gclk_calibrate( fdgpu_ed25519_ctx_t * ctx ) {
+  unsigned long volatile * w = (unsigned long volatile *)( ctx->h_stamp + 2*fdgpu_ed25519_ctx_t::NSLOT );
+  double best = 1e30;
+  for( int k=0; k<3; k++ ) {
+    w[0] = 0UL;
+    unsigned long t0 = fd_now_ns();
+    hipLaunchKernelGGL( fd_clock_kernel, dim3(1), dim3(1), 0, ctx->stream, ctx->d_stamp + 2*fdgpu_ed25519_ctx_t::NSLOT );
+    if( hipStreamSynchronize( ctx->stream ) != hipSuccess || !w[0] ) return;
+    unsigned long t1 = fd_now_ns();
+    if( (double)( t1 - t0 ) < best ) { best = (double)( t1 - t0 ); ctx->gclk_off_ns = (double)w[0] * 10.0 - 0.5 * ( (double)t0 + (double)t1 ); }
+  }
+  ctx->gclk_ok = 1;
+}
+
 static int
 ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned long max_sig,
           unsigned long max_payload_bytes, int semantics ) {
@@ -2264,6 +2300,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->small_max  = dbg.small_batch_max >= 0 ? (unsigned long)dbg.small_batch_max : FD_SMALL_BATCH_MAX;
   ctx->dsm_lanes  = dbg.dsm_lanes;
   ctx->nofold_max = dbg.nofold_max >= 0 ? (unsigned long)dbg.nofold_max : FD_NOFOLD_MAX;
+  ctx->gather_nowb = dbg.gather_no_writeback;
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
@@ -2277,11 +2314,16 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   HIPCHK( hipMalloc( &ctx->d_gcnt, sizeof(unsigned long) ), -1 );
   HIPCHK( hipMemsetAsync( ctx->d_gcnt, 0, sizeof(unsigned long), ctx->stream ), -1 );
   HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_flag, (void *)ctx->h_flag, 0 ), -1 );
+  HIPCHK( hipHostMalloc( (void **)&ctx->h_stamp, ( 2*fdgpu_ed25519_ctx_t::NSLOT + 1 ) * sizeof(unsigned long), hipHostMallocDefault ), -1 );
+  memset( ctx->h_stamp, 0, ( 2*fdgpu_ed25519_ctx_t::NSLOT + 1 ) * sizeof(unsigned long) );
+  HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_stamp, (void *)ctx->h_stamp, 0 ), -1 );
+  ctx->last_gt = -1;
   /* slot 0 now (the synchronous host calls stage through it); the async
      pipeline's other slots on first use (slot_bufs) */
   if( max_payload_bytes && slot_bufs( ctx, 0 ) ) return -1;
   ctx->cur = 0; ctx->rec_fp_off = -1;
   HIPCHK( hipStreamSynchronize( ctx->stream ), -1 );
+  gclk_calibrate( ctx );
   return 0;
 }
 
@@ -2334,6 +2376,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   if( ctx->h_gtime ) (void)hipHostFree( ctx->h_gtime );
   (void)hipFree( ctx->d_gcnt );
   if( ctx->h_flag ) (void)hipHostFree( (void *)ctx->h_flag );
+  if( ctx->h_stamp ) (void)hipHostFree( (void *)ctx->h_stamp );
   for( unsigned long i=0; i<FD_PIPE_MAX; i++ ) if( ctx->pipe_ev[i] ) (void)hipEventDestroy( ctx->pipe_ev[i] );
   if( ctx->stream ) (void)hipStreamDestroy( ctx->stream );
   delete ctx;
@@ -2771,22 +2814,6 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
    contexts, one per verify tile.) */
 /* launch the gather of slot sl's records not yet gathered (mode 3) on the
    context's gather stream; returns how many, or < 0 */
-__global__ void fd_clock_kernel( unsigned long * out ) {
-  __hip_atomic_store( out, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
-}
-
-/* GPU clock -> host clock offset, from one probe launch (error <= half its round trip, ~10 us) */
-static void gclk_calibrate( fdgpu_ed25519_ctx_t * ctx ) {
-  unsigned long volatile * w = (unsigned long volatile *)ctx->h_gtime;
-  w[0] = 0UL;
-  unsigned long t0 = fd_now_ns();
-  hipLaunchKernelGGL( fd_clock_kernel, dim3(1), dim3(1), 0, ctx->gstream, ctx->d_gtime );
-  if( hipStreamSynchronize( ctx->gstream ) != hipSuccess || !w[0] ) return;
-  unsigned long t1 = fd_now_ns();
-  ctx->gclk_off_ns = (double)w[0] * 10.0 - 0.5 * ( (double)t0 + (double)t1 );
-  ctx->gclk_ok = 1;
-}
-
 /* account the timed gathers whose count has been reached */
 static void gather_times( fdgpu_ed25519_ctx_t * ctx, unsigned long gathered ) {
   while( ctx->gt_head < ctx->gt_tail && ctx->gt[ ctx->gt_head % fdgpu_ed25519_ctx_t::NGT ].target <= gathered ) {
@@ -2818,7 +2845,6 @@ static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
     HIPCHK( hipStreamCreateWithPriority( &ctx->gstream, hipStreamNonBlocking, hi ), -2 );
     HIPCHK( hipEventCreateWithFlags( &ctx->gev, hipEventDisableTiming ), -2 );
   }
-  if( !ctx->gclk_ok && !ctx->g_launched ) gclk_calibrate( ctx );
   unsigned long target = ctx->g_launched + n;
   /* time this gather if a ring entry is free (the ring is drained as gathers complete) */
   unsigned long * gt = NULL;
@@ -2829,9 +2855,10 @@ static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
     ctx->gt[i].target = target; ctx->gt[i].t_launch = fd_now_ns();
     ctx->gt_tail++;
     gt = ctx->d_gtime + 2*i;
-  } else gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT;   /* untimed: a scratch entry */
+    ctx->last_gt = (long)i;
+  } else { gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT; ctx->last_gt = -1; }   /* untimed: a scratch entry */
   hipLaunchKernelGGL( fd_gather_kernel, dim3( (unsigned)n ), dim3( 64 ), 0, ctx->gstream, sl.g_dev + sl.gathered,
-                      sl.d_payload, sl.ref_dev + sl.ref_lo, sl.d_ovr + sl.gathered, ctx->d_gcnt,
+                      sl.d_payload, ctx->gather_nowb ? (unsigned char *)NULL : sl.ref_dev + sl.ref_lo, sl.d_ovr + sl.gathered, ctx->d_gcnt,
                       (unsigned long *)( ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT + 1 ), target, gt );
   HIPCHK( hipGetLastError(), -2 );
   ctx->g_launched = target; sl.gathered = sl.txn_cnt;
@@ -2853,6 +2880,8 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
   } else if( sl.mode==3 ) {   /* gathered: the rest of the records, then this stream waits for every gather */
     int g = gather_launch( ctx, sl );
     if( g < 0 ) return g;
+    /* the batch's last gather (this one, or the last early copy): phase timing */
+    sl.gt_idx = ctx->last_gt; sl.gt_target = ctx->g_launched;
     HIPCHK( hipEventRecord( ctx->gev, ctx->gstream ), -2 );
     HIPCHK( hipStreamWaitEvent( st, ctx->gev, 0 ), -2 );
   } else {
@@ -2860,6 +2889,9 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
     HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
   }
   HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
+  ctx->h_stamp[ 2*i ] = 0UL; ctx->h_stamp[ 2*i + 1 ] = 0UL;
+  if( sl.mode != 3 ) sl.gt_idx = -1;
+  hipLaunchKernelGGL( fd_stamp_kernel, dim3(1), dim3(1), 0, st, ctx->d_stamp + 2*i );
   int rc = sl.mode
          ? launch_raw( ctx, sl.d_payload, (fdgpu_txn_raw_t const *)sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out,
                        sl.d_img, FDGPU_TXN_IMG_STRIDE, sl.d_fp, st, ctx->dedup ? (u64 *)sl.d_dtag : (u64 *)NULL,
@@ -2880,7 +2912,7 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
   if( sl.mode && ctx->dedup )
     HIPCHK( hipMemcpyAsync( sl.h_dtag, sl.d_dtag, sl.txn_cnt * sizeof(unsigned long), hipMemcpyDeviceToHost, st ), -2 );
   sl.token++;
-  hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + i, sl.token );
+  hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + i, sl.token, ctx->d_stamp + 2*i + 1 );
   HIPCHK( hipGetLastError(), -2 );
   HIPCHK( hipEventRecord( sl.done, st ), -2 );
   sl.state = 1; sl.cursor = 0;
@@ -3235,6 +3267,34 @@ fdgpu_ed25519_gather_wait( fdgpu_ed25519_ctx_t * ctx ) {
 extern "C" void *
 fdgpu_host_dev_ptr( void const * p, unsigned long sz ) { return region_dev( p, sz ); }
 
+/* Phases of a completed batch (fdgpu_ed25519_phase_stats), from the GPU clock stamps converted to host
+   time: launch -> its verify kernels start (its gathers, the stream's previous batch), start -> end,
+   end -> the host sees it, and launch -> its last gather ends (gathered batches). */
+static void phase_max( unsigned long * m, double v ) { if( v > (double)*m ) *m = (unsigned long)v; }
+static void phase_account( fdgpu_ed25519_ctx_t * ctx, int i, unsigned long now ) {
+  fd_slot const & sl = ctx->slot[i];
+  unsigned long s0 = ctx->h_stamp[ 2*i ], s1 = ctx->h_stamp[ 2*i + 1 ];
+  if( !ctx->gclk_ok || !s0 || s1 < s0 ) return;
+  double l = (double)sl.launch_ns, t0 = (double)s0 * 10.0 - ctx->gclk_off_ns, t1 = (double)s1 * 10.0 - ctx->gclk_off_ns;
+  double a = t0 > l ? t0 - l : 0., c = t1 - t0, r = (double)now > t1 ? (double)now - t1 : 0.;
+  unsigned long * ph = ctx->ph;
+  ph[0]++; ph[1] += (unsigned long)a; phase_max( &ph[2], a );
+  ph[3] += (unsigned long)c; phase_max( &ph[4], c );
+  ph[5] += (unsigned long)r; phase_max( &ph[6], r );
+  if( sl.mode == 3 && sl.gt_idx >= 0 && ctx->gt[ sl.gt_idx ].target == sl.gt_target ) {
+    unsigned long ge = ctx->h_gtime[ 2*sl.gt_idx + 1 ];
+    if( ge ) {
+      double g = (double)ge * 10.0 - ctx->gclk_off_ns - l;
+      ph[7] += g > 0. ? (unsigned long)g : 0UL; ph[8]++;
+    }
+  }
+}
+
+extern "C" void
+fdgpu_ed25519_phase_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long out[ 9 ] ) {
+  memcpy( out, ctx->ph, sizeof(ctx->ph) );
+}
+
 /* Drain completed slots in submission order, at most max results. */
 static unsigned long
 poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes, unsigned char * out_img,
@@ -3265,7 +3325,9 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
       if( ctx->fault ) break;
       if( !ready ) break;
       std::atomic_thread_fence( std::memory_order_acquire );
-      ctx->lat_hist[ fdgpu_lat_bucket( fd_now_ns() - sl.launch_ns ) ]++;
+      unsigned long now = fd_now_ns();
+      ctx->lat_hist[ fdgpu_lat_bucket( now - sl.launch_ns ) ]++;
+      phase_account( ctx, i, now );
     }
     unsigned long k = sl.txn_cnt - sl.cursor;
     if( k > max - n ) k = max - n;

@@ -314,6 +314,7 @@ struct fdgpu_vtile {
   ulong                 copy_cursor;     /* pending-ring counter: frags below it are known to be copied */
   ulong                 copy_t0;         /* host time the oldest frag not yet given to a gather was taken (0: none) */
   ulong                 uncopied[ FDGPU_VTILE_IN_MAX ];    /* per in link: frags taken and not yet known copied */
+  ulong                 uncopied_tot;                      /* ... over all links (bounded by opt.max_uncopied) */
   ulong                 copied_next[ FDGPU_VTILE_IN_MAX ]; /* per in link: 1 + seq of the last frag known copied */
   struct { ulong target, t; } cq[ VT_NCTX_MAX ][ 8 ];     /* early copies in flight: gathered count they complete at */
   ulong                 cq_head[ VT_NCTX_MAX ], cq_tail[ VT_NCTX_MAX ];
@@ -386,6 +387,7 @@ fdgpu_vtile_new_opts( int device, ulong batch_txn, ulong tcache_depth, ulong see
   if( !vt->opt.max_wait_ns )  vt->opt.max_wait_ns = 2000000UL;
   if( !vt->opt.copy_wait_ns ) vt->opt.copy_wait_ns = FDGPU_VTILE_COPY_WAIT_NS;
   if( !vt->opt.copy_min )     vt->opt.copy_min = FDGPU_VTILE_COPY_MIN;
+  if( !vt->opt.max_uncopied ) vt->opt.max_uncopied = FDGPU_VTILE_MAX_UNCOPIED;
   /* staging arena of a batch = its range of the out dcache (in-place submits): up to
      batch_txn records of at most VT_RESERVE_MAX bytes (rounded to chunk pairs) */
   vt->nctx = vt->opt.nctx;
@@ -504,6 +506,7 @@ fdgpu_vtile_gpu_metrics( fdgpu_vtile_t * vt, fdgpu_vtile_gpu_metrics_t * out ) {
   memset( out->lat_hist, 0, sizeof(out->lat_hist) );
   out->batches = out->batch_txns = out->launch_ns = 0UL;
   memset( out->gather_gpu, 0, sizeof(out->gather_gpu) );
+  memset( out->phase, 0, sizeof(out->phase) );
   for( int k=0; k<vt->nctx; k++ ) {
     fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i ); infl += i;
     /* the engine counts every launch (a full slot launches inside submit) and times each batch */
@@ -514,6 +517,11 @@ fdgpu_vtile_gpu_metrics( fdgpu_vtile_t * vt, fdgpu_vtile_gpu_metrics_t * out ) {
     out->gather_gpu[0] += gs[0]; out->gather_gpu[1] += gs[1]; out->gather_gpu[3] += gs[3];
     if( gs[2] > out->gather_gpu[2] ) out->gather_gpu[2] = gs[2];
     if( gs[4] > out->gather_gpu[4] ) out->gather_gpu[4] = gs[4];
+    ulong ph[9]; fdgpu_ed25519_phase_stats( vt->ctx[k], ph );
+    for( int j=0; j<9; j++ ) {
+      if( j == 2 || j == 4 || j == 6 ) { if( ph[j] > out->phase[j] ) out->phase[j] = ph[j]; }
+      else out->phase[j] += ph[j];
+    }
     out->batches += b; out->batch_txns += t;
     for( int j=0; j<FDGPU_LAT_BUCKETS; j++ ) out->lat_hist[j] += h[j];
   }
@@ -541,6 +549,7 @@ fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_
   vt->zc = 1; vt->n_in = n;
   for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) vt->in_mcs[i] = i < n ? in_mc[i] : NULL;
   for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) { vt->uncopied[i] = 0UL; vt->copied_next[i] = 0UL; }
+  vt->uncopied_tot = 0UL;
   vt->copy_cursor = vt->pend_tail; vt->copy_t0 = 0UL;
   return 0;
 }
@@ -548,7 +557,7 @@ fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_
 /* a frag's copy has completed (or it left the pipeline without one) */
 static inline void vt_copied( fdgpu_vtile_t * vt, vt_pend_t const * p ) {
   int l = FDGPU_VTILE_SEQ_LINK( p->seq );
-  vt->uncopied[l]--; vt->copied_next[l] = FDGPU_VTILE_SEQ_SEQ( p->seq ) + 1UL;
+  vt->uncopied[l]--; vt->uncopied_tot--; vt->copied_next[l] = FDGPU_VTILE_SEQ_SEQ( p->seq ) + 1UL;
 }
 
 /* an early copy of context k was launched (for its latency metric) */
@@ -689,7 +698,7 @@ vt_taken( fdgpu_vtile_t * vt, ulong seq, ulong tsorig, ulong bundle_id, unsigned
   p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill; p->ovr = 0;
   if( vt->zc ) {
     p->cidx = vt->sub_cnt[ vt->fill ]++;
-    vt->uncopied[ FDGPU_VTILE_SEQ_LINK( seq ) ]++;
+    vt->uncopied[ FDGPU_VTILE_SEQ_LINK( seq ) ]++; vt->uncopied_tot++;
     if( !vt->copy_t0 ) vt->copy_t0 = now_ns();
   }
   if( vt->min_batch ) {                          /* first frag of the filling batch: its wait starts */
@@ -723,6 +732,16 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   if( link >= FDGPU_VTILE_IN_MAX || ( vt->zc && link >= vt->n_in ) ) return -4;   /* a link set_in_links was not told about */
   int rc = vt_room( vt );
   if( rc ) return rc;
+  if( vt->zc && vt->uncopied_tot >= vt->opt.max_uncopied ) {   /* copy backlog: start the copies, take nothing */
+    vt_copy_poll( vt );
+    if( vt->uncopied_tot >= vt->opt.max_uncopied ) {
+      for( int k=0; k<vt->nctx; k++ )
+        if( !fdgpu_ed25519_faulted( vt->ctx[k] ) && fdgpu_ed25519_gather( vt->ctx[k] ) > 0 ) vt_copy_launched( vt, k );
+      vt->copy_t0 = 0UL;
+      vt->gm.copy_backlog++;
+      return FDGPU_VTILE_COPY_BACKLOG;
+    }
+  }
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
   if( vt->zc ) {   /* the GPU copies the frag into dst itself (no host copy) and re-checks its mcache line */
     fdgpu_mcache_t const * mc = vt->in_mcs[ link ];
@@ -1364,6 +1383,7 @@ static void * link_tile( void * _a ) {
   fdgpu_vtile_opts_t vo;
   memset( &vo, 0, sizeof(vo) );
   vo.nctx = c->nctx; vo.copy_wait_ns = c->copy_wait_ns; vo.copy_min = c->copy_min; vo.gather_cus = c->gather_cus;
+  vo.max_uncopied = c->max_uncopied;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                              ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
@@ -1420,9 +1440,9 @@ static void * link_tile( void * _a ) {
        line of seq implies every earlier seq is published, so the tile reads
        only its own lines (the same frags, without T-1 cross-core line
        transfers per own frag) */
-    int drain = 0, all_done = 1;
+    int drain = 0, all_done = 1, backlog = 0;
     ulong took = 0UL;
-    for( ulong qi=0; qi<Q && !drain; qi++ ) {
+    for( ulong qi=0; qi<Q && !drain && !backlog; qi++ ) {
       ulong q = ( q0 + qi ) % Q;
       link_in_t * li = &in[q];
       mc_line_t const * line = l->line[q];
@@ -1445,6 +1465,7 @@ static void * link_tile( void * _a ) {
                                           ts_decomp( m.tsorig, t0 ) );   /* the pass's start is "now" to 2^31 ns */
         PROF_ADD( 1 );
         if( rc == -2 ) { drain = 1; li->seq = own; break; }         /* staging full: drain, retry this seq */
+        if( rc == FDGPU_VTILE_COPY_BACKLOG ) { backlog = 1; li->seq = own; break; }   /* copies behind: poll them, retry */
         if( rc ) { fprintf( stderr, "fdgpu_link: tile %d during_frag %d\n", idx, rc ); atomic_store( &h->fail, 2 ); drain = 1; break; }
         li->app++; took++;
         /* this tile's next frag of the link is usually published already: start its cold lines */
@@ -1471,6 +1492,7 @@ static void * link_tile( void * _a ) {
     if( !took && !drain ) ns_idle += t1 - t0;
     if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
     if( drain || ( all_done && fdgpu_vtile_pending( vt ) ) ) {
+      fdgpu_vtile_copy( vt, 0 );                                     /* the frags taken are copied while it waits */
       PROF_T0();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
       PROF_ADD( 3 );
@@ -1483,7 +1505,7 @@ static void * link_tile( void * _a ) {
     }
     /* housekeeping: launch / drain at most every 10 us while frags flow
        (the HIP runtime calls behind them take locks shared by all tiles) */
-    if( t1 - t_hk >= 10000UL ) {
+    if( backlog || t1 - t_hk >= 10000UL ) {
       t_hk = t1;
       PROF_T0();
       fdgpu_vtile_housekeep( vt, c->max_inflight );                 /* adaptive batching */
@@ -1590,6 +1612,11 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
       if( k == 2 || k == 4 ) { if( r->gm.gather_gpu[k] > st->gather_gpu[k] ) st->gather_gpu[k] = r->gm.gather_gpu[k]; }
       else st->gather_gpu[k] += r->gm.gather_gpu[k];
     }
+    for( int k=0; k<9; k++ ) {
+      if( k == 2 || k == 4 || k == 6 ) { if( r->gm.phase[k] > st->phase[k] ) st->phase[k] = r->gm.phase[k]; }
+      else st->phase[k] += r->gm.phase[k];
+    }
+    st->copy_backlog += r->gm.copy_backlog;
     st->tile_idle_ns += r->ns_idle;
     for( int k=0; k<8; k++ ) st->prof_ns[k] += r->prof[k];
     if( r->t_last > t_end ) t_end = r->t_last;

@@ -61,10 +61,10 @@ class GpuMetrics(ctypes.Structure):
                 ("poll_ns", ctypes.c_ulong), ("after_ns", ctypes.c_ulong),
                 ("launch_ns", ctypes.c_ulong), ("copies", ctypes.c_ulong), ("copy_lat_n", ctypes.c_ulong),
                 ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong),
-                ("gather_gpu", ctypes.c_ulong * 5)]
+                ("gather_gpu", ctypes.c_ulong * 5), ("phase", ctypes.c_ulong * 9), ("copy_backlog", ctypes.c_ulong)]
 
     def as_dict(self) -> dict:
-        return {k: (list(getattr(self, k)) if k in ("lat_hist", "gather_gpu") else int(getattr(self, k)))
+        return {k: (list(getattr(self, k)) if k in ("lat_hist", "gather_gpu", "phase") else int(getattr(self, k)))
                 for k, _ in self._fields_}
 
 
@@ -72,7 +72,7 @@ class VTileOpts(ctypes.Structure):
     """fdgpu_vtile_opts_t (0 = default everywhere)."""
     _fields_ = [("nctx", ctypes.c_int), ("host_dedup_tag", ctypes.c_int), ("small_max", ctypes.c_ulong),
                 ("min_batch", ctypes.c_ulong), ("max_wait_ns", ctypes.c_ulong), ("copy_wait_ns", ctypes.c_ulong),
-                ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint)]
+                ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint), ("max_uncopied", ctypes.c_ulong)]
 
 
 class StreamCfg(ctypes.Structure):
@@ -80,7 +80,8 @@ class StreamCfg(ctypes.Structure):
                 ("rate_fps", ctypes.c_double), ("tiles", ctypes.c_int), ("gpus", ctypes.c_int),
                 ("zero_copy", ctypes.c_int), ("reliable", ctypes.c_int), ("producers", ctypes.c_int),
                 ("nctx", ctypes.c_int), ("prof", ctypes.c_int), ("out_mult", ctypes.c_ulong),
-                ("copy_wait_ns", ctypes.c_ulong), ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint)]
+                ("copy_wait_ns", ctypes.c_ulong), ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint),
+                ("max_uncopied", ctypes.c_ulong)]
 
 
 class StreamStats(ctypes.Structure):
@@ -95,13 +96,13 @@ class StreamStats(ctypes.Structure):
                 ("launch_ns", ctypes.c_ulong), ("tile_idle_ns", ctypes.c_ulong), ("prod_seconds", ctypes.c_double),
                 ("prod_wait_ns", ctypes.c_ulong), ("prof_ns", ctypes.c_ulong * 8), ("copies", ctypes.c_ulong),
                 ("copy_lat_n", ctypes.c_ulong), ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong),
-                ("gather_gpu", ctypes.c_ulong * 5)]
+                ("gather_gpu", ctypes.c_ulong * 5), ("phase", ctypes.c_ulong * 9), ("copy_backlog", ctypes.c_ulong)]
 
     def as_dict(self) -> dict:
         out = {}
         for k, _ in self._fields_:
             v = getattr(self, k)
-            out[k] = list(v) if k in ("metrics", "tile_ns", "gpu_lat_hist", "prof_ns", "gather_gpu") else v
+            out[k] = list(v) if k in ("metrics", "tile_ns", "gpu_lat_hist", "prof_ns", "gather_gpu", "phase") else v
         return out
 
 
@@ -364,11 +365,11 @@ def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
 
 
 def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers=1, nctx=0, prof=0,
-         out_mult=0, copy_wait_ns=0, copy_min=0, gather_cus=0) -> StreamCfg:
+         out_mult=0, copy_wait_ns=0, copy_min=0, gather_cus=0, max_uncopied=0) -> StreamCfg:
     return StreamCfg(n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
                      gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0, producers=producers,
                      nctx=nctx, prof=prof, out_mult=out_mult, copy_wait_ns=copy_wait_ns, copy_min=copy_min,
-                     gather_cus=gather_cus)
+                     gather_cus=gather_cus, max_uncopied=max_uncopied)
 
 
 def stream_run(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,

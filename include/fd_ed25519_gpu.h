@@ -503,6 +503,14 @@ int           fdgpu_ed25519_reserve_gather_cus( fdgpu_ed25519_ctx_t * ctx, unsig
    start, out[3] / out[4] the sum / max of first block's start -> last
    block's end, ns */
 void          fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 5 ] );
+/* where the async batches' time goes, from GPU clock stamps at each batch's
+   verify kernels' start and end (mapped to host time once, at context
+   creation): out[0] batches timed; out[1] / out[2] sum / max of host launch
+   -> its verify kernels start (waiting for its gathers and for the stream's
+   earlier batch); out[3] / out[4] sum / max of kernels start -> end;
+   out[5] / out[6] sum / max of end -> poll saw it; out[7] / out[8] sum and
+   count of launch -> its last gather ended (gathered batches), ns */
+void          fdgpu_ed25519_phase_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long out[ 9 ] );
 /* wait until every launched gather of ctx has completed: 0, or -3 (ctx faulted) */
 int           fdgpu_ed25519_gather_wait( fdgpu_ed25519_ctx_t * ctx );
 
@@ -587,6 +595,9 @@ typedef struct fdgpu_debug_opts {
   long          small_batch_max;  /* -1: default; else the initial fdgpu_ed25519_set_small_batch_max */
   int           dsm_lanes;        /* latency path: lanes per signature in the DSM (1, 2, 4, 8); 0 = by batch size */
   long          nofold_max;       /* -1: default; batches of at most this many signatures use the unfolded DSM */
+  int           gather_no_writeback; /* DIAGNOSTIC: gathered records are copied into the device arena only, not back
+                                        into the caller's out region (published records then lack their payload:
+                                        measures what the write-back costs, never for parity) */
 } fdgpu_debug_opts_t;
 
 void

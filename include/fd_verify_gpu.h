@@ -149,6 +149,8 @@ typedef struct fdgpu_vtile_gpu_metrics {
   unsigned long gather_gpu[ 5 ];  /* every GPU copy (early or at a batch launch), on the GPU clock, summed over the
                                      tile's contexts: fdgpu_ed25519_gather_stats (count, launch -> start sum / max,
                                      start -> end sum / max, ns) */
+  unsigned long phase[ 9 ];       /* fdgpu_ed25519_phase_stats summed over the tile's contexts (maxima: max) */
+  unsigned long copy_backlog;     /* during_frag calls refused with FDGPU_VTILE_COPY_BACKLOG */
 } fdgpu_vtile_gpu_metrics_t;
 
 /* device: HIP device; batch_txn: transactions per GPU batch (staging
@@ -160,6 +162,13 @@ typedef struct fdgpu_vtile_gpu_metrics {
    default); nothing is read from the environment. */
 #define FDGPU_VTILE_COPY_WAIT_NS (50000UL)   /* default copy_wait_ns */
 #define FDGPU_VTILE_COPY_MIN     (4096UL)    /* default copy_min */
+#define FDGPU_VTILE_MAX_UNCOPIED (16384UL)   /* default max_uncopied */
+/* during_frag's answer when max_uncopied frags await their GPU copy: the frag was not taken.  The copies
+   of the frags taken have been started; poll them (fdgpu_vtile_housekeep or fdgpu_vtile_copy) and retry
+   later.  A tile that takes frags faster than the GPU copies them thus falls behind in the link, where
+   a lapping producer overruns it at the mcache poll (frags lost, as for a slow reference tile), instead
+   of taking frags whose copy would start after the producer reused their line (overrun at copy time). */
+#define FDGPU_VTILE_COPY_BACKLOG (-5)
 typedef struct fdgpu_vtile_opts {
   int           nctx;            /* engine contexts per tile, 1..3 (0 = 2): batches of consecutive frags go to them in
                                     turn, launched staggered, so a frag does not wait for a whole running batch */
@@ -172,6 +181,8 @@ typedef struct fdgpu_vtile_opts {
                                     once the oldest has waited this long (0 = FDGPU_VTILE_COPY_WAIT_NS) ... */
   unsigned long copy_min;        /* ... or once this many are waiting (0 = FDGPU_VTILE_COPY_MIN) */
   unsigned int  gather_cus;      /* CUs of the GPU reserved for the copies (fdgpu_ed25519_reserve_gather_cus; 0 = none) */
+  unsigned long max_uncopied;    /* zero-copy: frags taken whose copy has not completed, at most (0 =
+                                    FDGPU_VTILE_MAX_UNCOPIED); at the bound during_frag returns FDGPU_VTILE_COPY_BACKLOG */
 } fdgpu_vtile_opts_t;
 
 fdgpu_vtile_t * fdgpu_vtile_new( int device, unsigned long batch_txn, unsigned long tcache_depth, unsigned long seed,
@@ -328,6 +339,7 @@ typedef struct fdgpu_stream_cfg {
   unsigned long copy_wait_ns;    /* zero-copy: fdgpu_vtile_opts_t.copy_wait_ns (0 = its default) */
   unsigned long copy_min;        /* zero-copy: fdgpu_vtile_opts_t.copy_min (0 = its default) */
   unsigned int  gather_cus;      /* fdgpu_vtile_opts_t.gather_cus */
+  unsigned long max_uncopied;    /* fdgpu_vtile_opts_t.max_uncopied (0 = its default) */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
@@ -356,6 +368,8 @@ typedef struct fdgpu_stream_stats {
   unsigned long copies, copy_lat_n, copy_lat_ns_sum, copy_lat_ns_max;   /* zero-copy: early GPU copies (summed over
                                     tiles; max over tiles), as fdgpu_vtile_gpu_metrics_t */
   unsigned long gather_gpu[ 5 ];  /* fdgpu_vtile_gpu_metrics_t.gather_gpu, summed (maxima: max) over tiles */
+  unsigned long phase[ 9 ];       /* fdgpu_vtile_gpu_metrics_t.phase, summed (maxima: max) over tiles */
+  unsigned long copy_backlog;     /* fdgpu_vtile_gpu_metrics_t.copy_backlog, summed over tiles */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per
