@@ -48,6 +48,10 @@ WALK_MAC = HS_MAC if HALF else DSM_MAC
 # MI355X_MICROARCH.md: 157.3 TF FP32 vector FMA = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz x 2 flops, i.e. a
 # wave64 VALU instruction issues in 2 cycles per SIMD: 78.6 T lane-instructions/s for the whole chip
 GUIDE_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
+# v_mad_u64_u32 is a half-rate instruction: 4.32 cycles per wave64 instruction per SIMD against 2.22 for
+# v_fma_f32 / v_add_u32 (the guide's 2-cycle row) in the same probe (profiles/r03/ROOFLINE.md), so the
+# guide's issue rate gives the MAC half the full-rate peak
+GUIDE_MAD_PEAK = GUIDE_VALU_LANE_OPS / 2
 PREP_MAC = PREP_MUL * MAC_PER_MUL + PREP_SQR * MAC_PER_SQR
 
 
@@ -634,7 +638,7 @@ def main():
     rows = shard.gather_rows(dd, [rank, ms_dsm, ms_prep, my_ach, my_peak, dt], "cpu")
     per_gpu = [{"rank": int(r[0]), "dsm_ms": r[1], "prep_ms": r[2], "achieved_gmac_s": r[3] / 1e9,
                 "peak_gmac_s": r[4] / 1e9, "frac": r[3] / r[4] if r[4] > 0 else None,
-                "frac_guide": r[3] / GUIDE_VALU_LANE_OPS if r[3] > 0 else None,
+                "frac_guide": r[3] / GUIDE_MAD_PEAK if r[3] > 0 else None,
                 "sigs_per_s": nsig * args.steps / r[5]} for r in rows]
 
     if rank == 0:
@@ -688,17 +692,22 @@ def main():
                          # this walk is worth in the reference algorithm's terms (not a hardware efficiency)
                          "achieved_ref_equiv": ref_equiv / 1e9,
                          "frac_ref_equiv": ref_equiv / peak if peak > 0 else None,
-                         "peak_source": "fdgpu_mad_peak_per_s: measured v_mad_u64_u32 throughput, this device (max of 3)",
-                         # the same achieved rate against MI355X_MICROARCH.md's VALU issue rate (157.3 TF FP32
-                         # vector = 78.6 T wave64 lane-instructions/s), one MAC priced as one lane-instruction
-                         "peak_guide": GUIDE_VALU_LANE_OPS / 1e9,
-                         "frac_guide": achieved / GUIDE_VALU_LANE_OPS,
+                         "peak_source": "fdgpu_mad_peak_per_s: measured v_mad_u64_u32 throughput of this device at "
+                                        "its sustained clock (8 waves/SIMD, 16 chains; max of 3)",
+                         # the same achieved rate against MI355X_MICROARCH.md's VALU issue rate: 2 cycles per
+                         # full-rate wave64 instruction (78.6 T lane-ops/s at 2.4 GHz), and v_mad_u64_u32 measured
+                         # at twice that cost -> 39.3 T MAC/s
+                         "peak_guide": GUIDE_MAD_PEAK / 1e9,
+                         "frac_guide": achieved / GUIDE_MAD_PEAK,
                          "peak_guide_source": "MI355X_MICROARCH.md: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6 T "
-                                              "lane-ops/s (157.3 TF FP32 FMA / 2); profiles/r02/ROOFLINE.md",
+                                              "full-rate lane-ops/s; v_mad_u64_u32 is half rate (4.32 vs 2.22 cycles per "
+                                              "wave-instruction, tools/instprobe/instprobe2 + PMC clock) -> 39.3 T MAC/s; "
+                                              "profiles/r03/ROOFLINE.md",
+                         "frac_guide_fullrate": achieved / GUIDE_VALU_LANE_OPS,
                          "valu_busy": valu_busy,
                          "valu_busy_source": "profiles/dsm_pmc.json: issue cycles of the walk kernel's ISA priced at "
                                              "the measured per-instruction costs (tools/dsm_issue_model.py, "
-                                             "profiles/r02/roofline/issue_model_dsmh.json) / measured kernel cycles",
+                                             "profiles/r03/roofline/issue_model_dsmh.json) / measured kernel cycles",
                          # the same kernel against the HBM roofline: PMC bytes per launch / this run's launch time
                          "hbm": ({"achieved": traffic * nsig / (1 << 20) / (dom_ms * 1e-3) / 1e9, "peak": 8000.0,
                                   "unit": "GB/s",

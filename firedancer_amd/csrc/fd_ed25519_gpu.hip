@@ -2830,9 +2830,8 @@ static void gather_times( fdgpu_ed25519_ctx_t * ctx, unsigned long gathered ) {
   }
 }
 
-static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
-  unsigned long n = sl.txn_cnt - sl.gathered;
-  if( !n ) return 0;
+/* the gather stream and its timing ring (on first use, or by fdgpu_ed25519_prepare) */
+static int gather_init( fdgpu_ed25519_ctx_t * ctx ) {
   if( !ctx->h_gtime ) {
     HIPCHK( hipHostMalloc( (void **)&ctx->h_gtime, ( fdgpu_ed25519_ctx_t::NGT + 1 ) * 2 * sizeof(unsigned long), hipHostMallocDefault ), -2 );
     HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_gtime, (void *)ctx->h_gtime, 0 ), -2 );
@@ -2845,6 +2844,13 @@ static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
     HIPCHK( hipStreamCreateWithPriority( &ctx->gstream, hipStreamNonBlocking, hi ), -2 );
     HIPCHK( hipEventCreateWithFlags( &ctx->gev, hipEventDisableTiming ), -2 );
   }
+  return 0;
+}
+
+static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
+  unsigned long n = sl.txn_cnt - sl.gathered;
+  if( !n ) return 0;
+  if( gather_init( ctx ) ) return -2;
   unsigned long target = ctx->g_launched + n;
   /* time this gather if a ring entry is free (the ring is drained as gathers complete) */
   unsigned long * gt = NULL;
@@ -2997,6 +3003,19 @@ static int slot_raw_bufs( fdgpu_ed25519_ctx_t * ctx, fd_slot * sl ) {
   HIPCHK( hipHostMalloc( (void **)&sl->h_gat, ctx->max_txn * sizeof(fd_gather), hipHostMallocDefault ), -3 );
   HIPCHK( hipHostGetDevicePointer( (void **)&sl->g_dev, (void *)sl->h_gat, 0 ), -3 );
   HIPCHK( hipMalloc( (void **)&sl->d_ovr, ctx->max_txn ), -3 );
+  return 0;
+}
+
+/* every allocation the async pipeline would make on first use, now (a tile's privileged init: after
+   it, batches make no allocation syscalls -- tools/sandbox/vtile_sandbox.c) */
+extern "C" int
+fdgpu_ed25519_prepare( fdgpu_ed25519_ctx_t * ctx, int raw ) {
+  if( !ctx ) return -1;
+  for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
+    if( slot_bufs( ctx, i ) ) return -3;
+    if( raw && slot_raw_bufs( ctx, &ctx->slot[i] ) ) return -3;
+  }
+  if( raw && gather_init( ctx ) ) return -3;
   return 0;
 }
 

@@ -63,6 +63,25 @@ xxh64_64( ulong seed, uchar const * p ) {
 
 ulong fdgpu_dedup_tag( ulong seed, uchar const sig[ 64 ] ) { return xxh64_64( seed, sig ); }
 
+/* XXH64 of any length (the published algorithm): the link's verdict trace hashes published records */
+ulong
+fdgpu_xxh64( ulong seed, uchar const * p, ulong n ) {
+  uchar const * e = p + n;
+  ulong h;
+  if( n >= 32UL ) {
+    ulong v[4] = { seed + P1 + P2, seed + P2, seed, seed - P1 };
+    for( ; p + 32 <= e; p += 32 ) for( int i=0; i<4; i++ ) v[i] = xxh_round( v[i], ld64( p + 8*i ) );
+    h = rotl64( v[0], 1 ) + rotl64( v[1], 7 ) + rotl64( v[2], 12 ) + rotl64( v[3], 18 );
+    for( int i=0; i<4; i++ ) { h ^= xxh_round( 0UL, v[i] ); h = h * P1 + P4; }
+  } else h = seed + P5;
+  h += n;
+  for( ; p + 8 <= e; p += 8 ) { h ^= xxh_round( 0UL, ld64( p ) ); h = rotl64( h, 27 ) * P1 + P4; }
+  if( p + 4 <= e ) { unsigned w; memcpy( &w, p, 4 ); h ^= (ulong)w * P1; h = rotl64( h, 23 ) * P2 + P3; p += 4; }
+  for( ; p < e; p++ ) { h ^= (ulong)*p * P5; h = rotl64( h, 11 ) * P1; }
+  h ^= h >> 33; h *= P2; h ^= h >> 29; h *= P3; h ^= h >> 32;
+  return h;
+}
+
 /* ---- tcache ----------------------------------------------------------
    Semantics of FD_TCACHE_QUERY / FD_TCACHE_INSERT (src/tango/tcache/
    fd_tcache.h:281-404): a ring of the last depth unique tags plus an
@@ -367,6 +386,9 @@ vt_ctx_new( fdgpu_vtile_t const * vt ) {
       fdgpu_ed25519_ctx_delete( c ); return NULL;
     }
     fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
+    /* every staging buffer and the gather stream now: batches then allocate nothing (the tile's sandbox
+       allows no allocation it does not need, fd_verify_gpu_tile.seccomppolicy) */
+    if( fdgpu_ed25519_prepare( c, 1 ) ) { fdgpu_ed25519_ctx_delete( c ); return NULL; }
   }
   return c;
 }
@@ -1032,6 +1054,8 @@ struct fdgpu_link {
   link_res_t *     res;
   ulong *          hist;
   fdgpu_mcache_t   mc[ LINK_PROD_MAX ];   /* local views of the shared lines (the tiles' in links) */
+  fdgpu_link_trace_t * trace[ LINK_TILE_MAX ];   /* fdgpu_link_set_trace: this process's tiles' verdicts, in order */
+  ulong            trace_cap, trace_cnt[ LINK_TILE_MAX ];
 };
 
 static ulong al64( ulong x ) { return ( x + 63UL ) & ~63UL; }
@@ -1162,7 +1186,49 @@ fdgpu_link_delete( fdgpu_link_t * l ) {
     for( int q=0; q<l->h->cfg.producers; q++ ) fdgpu_host_unregister( l->line[q] );
   }
   munmap( l->base, l->sz );
+  for( int i=0; i<LINK_TILE_MAX; i++ ) free( l->trace[i] );
   free( l );
+}
+
+int
+fdgpu_link_set_trace( fdgpu_link_t * l, ulong cap ) {
+  for( int i=0; i<LINK_TILE_MAX; i++ ) { free( l->trace[i] ); l->trace[i] = NULL; l->trace_cnt[i] = 0UL; }
+  l->trace_cap = 0UL;
+  if( !cap ) return 0;
+  for( int i=0; i<l->h->cfg.tiles && i<LINK_TILE_MAX; i++ )
+    if( !( l->trace[i] = (fdgpu_link_trace_t *)calloc( cap, sizeof(fdgpu_link_trace_t) ) ) ) return -1;
+  l->trace_cap = cap;
+  return 0;
+}
+
+ulong
+fdgpu_link_trace( fdgpu_link_t const * l, int tile, fdgpu_link_trace_t * out, ulong max ) {
+  if( tile < 0 || tile >= LINK_TILE_MAX || !l->trace[tile] ) return 0UL;
+  ulong n = l->trace_cnt[tile] < max ? l->trace_cnt[tile] : max;
+  memcpy( out, l->trace[tile], n * sizeof(fdgpu_link_trace_t) );
+  return n;
+}
+
+/* the verdicts a tile just returned, in order (fdgpu_link_set_trace): a published frag's record is
+   hashed where the tile published it, in its out dcache, with the alignment byte between an odd-sized
+   payload and the fd_txn_t taken as 0 (the reference leaves whatever the chunk held there) */
+static void
+link_trace( fdgpu_link_t * l, int idx, fdgpu_vtile_t * vt, fdgpu_vtile_done_t const * d, ulong n ) {
+  fdgpu_link_trace_t * t = l->trace[idx];
+  if( !t ) return;
+  uchar const * out = fdgpu_vtile_out_dcache( vt );
+  for( ulong i=0; i<n && l->trace_cnt[idx] < l->trace_cap; i++ ) {
+    fdgpu_link_trace_t * e = &t[ l->trace_cnt[idx]++ ];
+    e->seq = d[i].seq; e->tag = d[i].tag; e->result = d[i].result; e->rec_sz = (unsigned)d[i].sz;
+    e->rec_hash = 0UL;
+    if( d[i].result == FDGPU_VTILE_PUBLISH && d[i].sz <= VT_RESERVE_MAX ) {
+      uchar rec[ VT_RESERVE_MAX ];
+      memcpy( rec, out + d[i].chunk * FDGPU_CHUNK_SZ, d[i].sz );
+      ulong pe = FDGPU_TXNM_HDR_SZ + ((fdgpu_txnm_t const *)rec)->payload_sz;
+      if( ( pe & 1UL ) && pe < d[i].sz ) rec[ pe ] = 0;
+      e->rec_hash = fdgpu_xxh64( 0UL, rec, d[i].sz );
+    }
+  }
 }
 
 ulong fdgpu_link_joined( fdgpu_link_t const * l ) { return atomic_load( &l->h->joined ); }
@@ -1496,6 +1562,7 @@ static void * link_tile( void * _a ) {
       PROF_T0();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
       PROF_ADD( 3 );
+      link_trace( l, idx, vt, done, n );
       link_account( l, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
       PROF_ADD( 5 );
       if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );
@@ -1514,6 +1581,7 @@ static void * link_tile( void * _a ) {
       PROF_T0();
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
       PROF_ADD( 4 );
+      link_trace( l, idx, vt, done, n );
       link_account( l, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
       PROF_ADD( 5 );
       if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );

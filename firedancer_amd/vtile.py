@@ -25,7 +25,7 @@ GOSSIP_TAG_VOTE = 3                                      # fd_gossip_types.h:26
 GOSSIP_VOTE_TXN_SZ_OFF, GOSSIP_VOTE_TXN_OFF, GOSSIP_MSG_SZ = 64, 72, 1304   # fd_gossip_update_message_t, x86-64
 LAT_BUCKETS = 40
 
-EXPORTS = ("fdgpu_dedup_tag", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
+EXPORTS = ("fdgpu_dedup_tag", "fdgpu_xxh64", "fdgpu_link_set_trace", "fdgpu_link_trace", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
            "fdgpu_mcache_new", "fdgpu_mcache_delete", "fdgpu_mcache_publish", "fdgpu_mcache_poll",
            "fdgpu_dcache_compact_next", "fdgpu_vtile_new", "fdgpu_vtile_delete", "fdgpu_vtile_out_dcache",
            "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_housekeep", "fdgpu_vtile_pipeline_state", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
@@ -180,12 +180,26 @@ def load():
         L.fdgpu_link_dcache.restype = vp
         L.fdgpu_link_dcache.argtypes = [vp]
         L.fdgpu_link_result.argtypes = [vp, ctypes.c_double, ctypes.POINTER(StreamStats)]
+        L.fdgpu_xxh64.restype = ul
+        L.fdgpu_xxh64.argtypes = [ul, vp, ul]
+        L.fdgpu_link_set_trace.restype = ctypes.c_int
+        L.fdgpu_link_set_trace.argtypes = [vp, ul]
+        L.fdgpu_link_trace.restype = ul
+        L.fdgpu_link_trace.argtypes = [vp, ctypes.c_int, vp, ul]
         L.fdgpu_stream_run.argtypes = [ctypes.c_int, ctypes.POINTER(StreamCfg), vp, vp, vp, ul, ul,
                                        ctypes.POINTER(StreamStats)]
         L.fdgpu_stream_bench.argtypes = [ctypes.c_int, vp, vp, vp, ul, ul, ctypes.c_int, ul, ul, ul, ctypes.c_double,
                                          ctypes.c_int, ctypes.POINTER(StreamStats)]
         _lib = L
     return _lib
+
+
+TRACE_DTYPE = np.dtype([("seq", "<u8"), ("tag", "<u8"), ("rec_hash", "<u8"), ("result", "<i4"), ("rec_sz", "<u4")])
+
+
+def xxh64(seed: int, data: bytes) -> int:
+    b = np.frombuffer(bytes(data) + b"\0", np.uint8)
+    return int(load().fdgpu_xxh64(seed, b.ctypes.data, len(data)))
 
 
 def dedup_tag(seed: int, sig: bytes) -> int:
@@ -427,6 +441,16 @@ class Link:
 
     def run(self, proc: int, device: int, run_producer: bool) -> int:
         return int(self.L.fdgpu_link_run(self.p, proc, device, 1 if run_producer else 0))
+
+    def set_trace(self, cap: int) -> None:
+        """fdgpu_link_set_trace: record up to cap verdicts of each of this process's tiles (before run)."""
+        if self.L.fdgpu_link_set_trace(self.p, cap):
+            raise RuntimeError("fdgpu_link_set_trace failed")
+
+    def trace(self, tile: int, cap: int) -> np.ndarray:
+        out = np.zeros(cap, TRACE_DTYPE)
+        n = int(self.L.fdgpu_link_trace(self.p, tile, out.ctypes.data, cap))
+        return out[:n]
 
     def result(self, timeout_s: float = 120.0) -> dict:
         st = StreamStats()

@@ -511,6 +511,10 @@ void          fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned lo
    out[5] / out[6] sum / max of end -> poll saw it; out[7] / out[8] sum and
    count of launch -> its last gather ended (gathered batches), ns */
 void          fdgpu_ed25519_phase_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long out[ 9 ] );
+/* make now every allocation the async pipeline otherwise makes on first use (all staging slots; raw:
+   the raw-payload buffers and the gather stream too), so that batches later make no allocation
+   syscalls -- a tile calls it in privileged init, before its sandbox.  0, or < 0 */
+int           fdgpu_ed25519_prepare( fdgpu_ed25519_ctx_t * ctx, int raw );
 /* wait until every launched gather of ctx has completed: 0, or -3 (ctx faulted) */
 int           fdgpu_ed25519_gather_wait( fdgpu_ed25519_ctx_t * ctx );
 

@@ -61,6 +61,8 @@ typedef struct fdgpu_txnm {
 /* fd_hash( seed, sig0, 64 ) of fd_txn_verify (fd_verify_tile.h:79):
    XXH64 of the transaction's first signature */
 unsigned long fdgpu_dedup_tag( unsigned long seed, unsigned char const sig[ 64 ] );
+/* XXH64 of n bytes (the link's verdict trace hashes published records with it) */
+unsigned long fdgpu_xxh64( unsigned long seed, unsigned char const * p, unsigned long n );
 
 /* ---- tcache: HA dedup of the last `depth` unique tags -------------- */
 
@@ -398,6 +400,18 @@ int             fdgpu_link_tiles_of( int tiles, int gpus, int proc, int * out );
 fdgpu_mcache_t * fdgpu_link_mcache( fdgpu_link_t * link );
 unsigned char *  fdgpu_link_dcache( fdgpu_link_t * link );
 int             fdgpu_link_result( fdgpu_link_t * link, double timeout_s, fdgpu_stream_stats_t * st );
+/* Verdict trace (parity at scale, tests/test_gpu_stream_parity.py): with cap > 0 every tile this
+   process runs records up to cap of its verdicts in after_frags order -- the seq handed to during_frag
+   (link in bits 56-63), FDGPU_VTILE_* result, HA dedup tag, and for a published frag the XXH64 (seed 0)
+   and size of its fd_txn_m_t record as published in the tile's out dcache.  Set before fdgpu_link_run;
+   0 on success.  fdgpu_link_trace copies tile's entries out and returns their count. */
+typedef struct fdgpu_link_trace {
+  unsigned long seq, tag, rec_hash;
+  int           result;
+  unsigned int  rec_sz;
+} fdgpu_link_trace_t;
+int             fdgpu_link_set_trace( fdgpu_link_t * link, unsigned long cap );
+unsigned long   fdgpu_link_trace( fdgpu_link_t const * link, int tile, fdgpu_link_trace_t * out, unsigned long max );
 
 /* one process, private link, every tile on `device` (G = 1) */
 int             fdgpu_stream_run( int device, fdgpu_stream_cfg_t const * cfg, unsigned char const * payload,

@@ -233,6 +233,7 @@ run_batch( fdgpu_vtile_t * vt, fdgpu_mcache_t * mc, uchar * dcache, uchar const 
       for( ulong j=0; j<k; j++ ) *published += d[j].result == FDGPU_VTILE_PUBLISH;
     }
     if( rc ) return rc;
+    if( ( i & 511UL ) == 511UL ) fdgpu_vtile_housekeep( vt, 1 );   /* early GPU copies and partial launches too */
   }
   if( fdgpu_vtile_flush( vt ) ) return -10;
   static fdgpu_vtile_done_t d[ N_FRAG ];
