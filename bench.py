@@ -184,7 +184,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 mcache_depth=args.stream_depth * min(procs, 2) if not paced else 1 << 18,
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
                 copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus,
-                max_uncopied=args.stream_max_uncopied)
+                max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -245,6 +245,11 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
             # gathers and the stream's earlier batch), kernels, end -> the tile saw it; launch -> last gather end
             "batch_phases_us": _phases(st["phase"]),
             "copy_backlog_refusals": st["copy_backlog"],
+            # --stream-prof: rdtsc sections of the tile loop, ns per own frag (fdgpu_stream_stats_t.prof_ns)
+            "tile_prof_ns_per_frag": (dict(zip(("mcache_poll", "during_frag", "prefetch_credit", "drain_after_frags",
+                                                "hk_after_frags", "account", "credit", "housekeep"),
+                                               [round(x / n, 1) for x in st["prof_ns"]]))
+                                      if any(st["prof_ns"]) else None),
             "inflight_max": st["inflight_max"], "gpu_batch_lat_p50_us_le": hq(0.5),
             "gpu_batch_lat_p99_us_le": hq(0.99)}
 
@@ -311,7 +316,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-ctx", str(args.stream_ctx), "--stream-lat-ctx", str(args.stream_lat_ctx),
            "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
            "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus),
-           "--stream-max-uncopied", str(args.stream_max_uncopied)]
+           "--stream-max-uncopied", str(args.stream_max_uncopied)] + (["--stream-prof"] if args.stream_prof else [])
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -373,6 +378,8 @@ def main():
                     help="zero-copy intake: CUs each tile's engine contexts reserve for the copies (fdgpu_vtile_opts_t; "
                          "16 vs 0 on 2 tiles: max 21.6M vs 18.7M sigs/s, paced 10M/s p99 2.0 vs 4.6 ms, "
                          "profiles/r03/stream_tiles)")
+    ap.add_argument("--stream-prof", action="store_true",
+                    help="rdtsc section profile of the tile loop (fdgpu_stream_cfg_t.prof), in each leg's summary")
     ap.add_argument("--stream-max-uncopied", type=int, default=0,
                     help="zero-copy intake: frags a tile may hold whose GPU copy has not completed (fdgpu_vtile_opts_t."
                          "max_uncopied; 0 = its default)")

@@ -1641,28 +1641,77 @@ fd_rslow_kernel( u32 nsig, int semantics, i8 * __restrict__ code, uint4 const * 
   code[s] = (i8)r;
 }
 
+/* a transaction's code from its signatures' codes: fd_ed25519_verify_batch_single_msg's order */
+FD_DEV int txn_code( fdgpu_txn_desc_t const & d, u32 t, u32 nsig, i8 const * __restrict__ code,
+                     unsigned char const * __restrict__ pflag ) {
+  u32 cnt = d.sig_cnt;
+  if( pflag && pflag[t] ) return pflag[t]==2u ? FDGPU_ERR_OVERRUN : FDGPU_ERR_PARSE;   /* fd_verify_tile.c:127-131 */
+  if( cnt==0u || cnt>16u ) return FD_ED25519_ERR_SIG;         /* fd_ed25519_user.c:238-241 */
+  int first = 0, any_msg = 0;
+  for( u32 j=0; j<cnt; j++ ) {
+    u32 s = d.sig_base + j;
+    int c = s < nsig ? (int)code[s] : FD_ED25519_ERR_SIG;
+    if( c==FD_ED25519_ERR_MSG ) any_msg = 1;
+    else if( c && !first ) first = c;                         /* pass-1 order, :264-294 */
+  }
+  return first ? first : ( any_msg ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS );   /* pass 2, :297-306 */
+}
+
 __global__ void __launch_bounds__( FD_WG )
 fd_reduce_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 nsig,
                   i8 const * __restrict__ code, unsigned char const * __restrict__ pflag,
                   i8 * __restrict__ txn_out ) {
   u32 t = blockIdx.x * FD_WG + threadIdx.x;
   if( t >= txn_cnt ) return;
-  fdgpu_txn_desc_t d = desc[t];
-  u32 cnt = d.sig_cnt;
-  int r;
-  if( pflag && pflag[t] ) r = pflag[t]==2u ? FDGPU_ERR_OVERRUN : FDGPU_ERR_PARSE;   /* fd_verify_tile.c:127-131 */
-  else if( cnt==0u || cnt>16u ) r = FD_ED25519_ERR_SIG;      /* fd_ed25519_user.c:238-241 */
-  else {
-    int first = 0, any_msg = 0;
-    for( u32 j=0; j<cnt; j++ ) {
-      u32 s = d.sig_base + j;
-      int c = s < nsig ? (int)code[s] : FD_ED25519_ERR_SIG;
-      if( c==FD_ED25519_ERR_MSG ) any_msg = 1;
-      else if( c && !first ) first = c;                       /* pass-1 order, :264-294 */
+  txn_out[t] = (i8)txn_code( desc[t], t, nsig, code, pflag );
+}
+
+/* The async raw batches' last work kernel (fdgpu_ed25519_submit_raw*): the reduce, then every result
+   straight into the slot's pinned host arrays (device views), so no copy commands follow the batch:
+   each thread one transaction's code, footprint and dedup tag (consecutive lanes, consecutive host
+   addresses), then the block's 256 fd_txn_t images one after another, each copied by all 256 lanes
+   in 2-byte stores -- into the caller's out region behind the payload with txn_t_sz in the record
+   header (gathered batches, as fd_img_scatter_kernel), or into the slot's image array (the others). */
+__global__ void __launch_bounds__( FD_WG )
+fd_finish_kernel( fdgpu_txn_desc_t const * __restrict__ desc, fdgpu_txn_raw_t const * __restrict__ raw, u32 txn_cnt,
+                  u32 nsig, i8 const * __restrict__ code, unsigned char const * __restrict__ pflag,
+                  unsigned short const * __restrict__ fp, u64 const * __restrict__ dtag,
+                  unsigned char const * __restrict__ img, u32 stride,
+                  i8 * __restrict__ h_out, unsigned short * __restrict__ h_fp, u64 * __restrict__ h_dtag,
+                  unsigned char * __restrict__ out_region, int rec_fp_off, unsigned char * __restrict__ h_img ) {
+  /* the descriptors live in pinned host memory: each lane reads its own once (in parallel), the image
+     loop below takes the offsets from LDS */
+  __shared__ u32 s_img_off[ FD_WG ], s_hdr_off[ FD_WG ];
+  __shared__ unsigned short s_n[ FD_WG ];
+  u32 t0 = blockIdx.x * FD_WG, t = t0 + threadIdx.x;
+  if( t < txn_cnt ) {
+    unsigned short n = fp[t];
+    h_out[t] = (i8)txn_code( desc[t], t, nsig, code, pflag );
+    h_fp[t] = n;
+    if( h_dtag ) h_dtag[t] = dtag[t];
+    s_n[ threadIdx.x ] = n;
+    if( out_region && n ) {
+      fdgpu_txn_raw_t r = raw[t];
+      s_img_off[ threadIdx.x ] = ( r.payload_off + (u32)r.payload_sz + 1u ) & ~1u;
+      s_hdr_off[ threadIdx.x ] = r.payload_off - (u32)r._pad[0];
     }
-    r = first ? first : ( any_msg ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS );  /* pass 2, :297-306 */
   }
-  txn_out[t] = (i8)r;
+  __syncthreads();
+  u32 nt = txn_cnt - t0 < (u32)FD_WG ? txn_cnt - t0 : (u32)FD_WG;
+  for( u32 k=0; k<nt; k++ ) {
+    u32 u = t0 + k;
+    u32 n = s_n[k];
+    if( !n ) continue;
+    unsigned short const * s16 = (unsigned short const *)( img + (size_t)u*stride );
+    unsigned char * dst;
+    if( out_region ) {
+      dst = out_region + s_img_off[k];
+      if( rec_fp_off >= 0 && threadIdx.x==0u )
+        *(unsigned short *)( out_region + s_hdr_off[k] + (u32)rec_fp_off ) = (unsigned short)n;
+    } else dst = h_img + (size_t)u*stride;
+    for( u32 i=threadIdx.x; i<(n >> 1); i+=FD_WG ) ((unsigned short *)dst)[i] = s16[i];
+    if( ( n & 1u ) && threadIdx.x==0u ) dst[n-1u] = img[(size_t)u*stride + n - 1u];
+  }
 }
 
 /* Raw-payload batches: fd_txn_parse per transaction (fd_gpu_txn.h), then
@@ -1708,8 +1757,16 @@ fd_parse_kernel( unsigned char const *    __restrict__ payload,
                  unsigned short *         __restrict__ fp_out,
                  u64                                    dedup_seed,
                  u64 *                    __restrict__ dtag_out,
-                 unsigned char const *    __restrict__ ovr ) {
+                 unsigned char const *    __restrict__ ovr,
+                 u32 *                    __restrict__ map,       /* fused fd_expand_kernel (async batches), or NULL */
+                 u32                                    nsig,
+                 u32 *                    __restrict__ zero_word,
+                 unsigned long *          __restrict__ stamp ) {  /* fd_stamp_kernel's GPU clock, or NULL */
   u32 t = blockIdx.x * FD_WG + threadIdx.x;
+  if( t == 0u ) {
+    if( stamp ) __hip_atomic_store( stamp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+    if( zero_word ) *zero_word = 0u;                 /* the batch's slow-list count (half-size path) */
+  }
   if( t >= txn_cnt ) return;
   fdgpu_txn_raw_t r = raw[t];
   if( ovr && ovr[t] ) {        /* overrun while gathered (fd_gather_kernel): never parsed, never verified */
@@ -1721,6 +1778,7 @@ fd_parse_kernel( unsigned char const *    __restrict__ payload,
     d.signature_off = 0; d.sig_cnt = r.sig_lanes;
     desc_out[t] = d;
     pflag[t] = 2u;
+    if( map ) for( u32 j=0; j<d.sig_cnt; j++ ) { u32 s = d.sig_base + j; if( s < nsig ) map[s] = t | (j << 24); }
     return;
   }
   fd_txn_hdr h;
@@ -1743,6 +1801,7 @@ fd_parse_kernel( unsigned char const *    __restrict__ payload,
   }
   desc_out[t] = d;
   pflag[t] = ok ? 0u : 1u;
+  if( map ) for( u32 j=0; j<d.sig_cnt; j++ ) { u32 s = d.sig_base + j; if( s < nsig ) map[s] = t | (j << 24); }
 }
 
 /* Batch SHA-512 (the fd_sha512_batch_* API, src/ballet/sha512/
@@ -1944,6 +2003,13 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   unsigned char *    d_ovr;    /*         per transaction: 1 = overrun while gathered */
   unsigned long      gathered; /*         records whose gather has been launched (fdgpu_ed25519_gather) */
   long               gt_idx;   /*         the gt[] entry timing the batch's last gather (-1: untimed) */
+  /* device views of the pinned host arrays: raw batches' descriptors are read, and their results written,
+     by the kernels themselves (fd_parse_kernel, fd_finish_kernel), with no copy command around the batch */
+  fdgpu_txn_desc_t * hd_desc;
+  i8 *               hd_txn_out;
+  unsigned short *   hd_fp;
+  unsigned long *    hd_dtag;
+  unsigned char *    hd_img;
   unsigned long      gt_target;/*         ... and the gathered count it ends at (the entry may be reused) */
 };
 
@@ -2074,9 +2140,10 @@ static int async_busy( fdgpu_ed25519_ctx_t const * ctx ) {
   return 0;
 }
 
+/* flags: 1 = the map is written already (fused into fd_parse_kernel), 2 = no reduce (fd_finish_kernel does it) */
 static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_desc_t const * d_desc,
                          unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, i8 * d_sig_out, hipStream_t st,
-                         unsigned char const * d_pflag = NULL ) {
+                         unsigned char const * d_pflag = NULL, int flags = 0 ) {
   if( !txn_cnt ) return 0;
   i8 * code = d_sig_out ? d_sig_out : ctx->d_code;
   hipEvent_t * ev = ctx->ev;
@@ -2085,8 +2152,9 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
   unsigned tg = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   unsigned sg = (unsigned)( (sig_cnt + FD_WG - 1) / FD_WG );
   if( nsig ) {
-    hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig,
-                        ctx->d_slow + ctx->max_sig );
+    if( !( flags & 1 ) )
+      hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig,
+                          ctx->d_slow + ctx->max_sig );
     if( ctx->timing ) hipEventRecord( ev[0], st );
     /* small batch: cannot fill the GPU, so latency is the sum of the kernels' per-wave
        instruction streams -- decode A, decode R and hash side by side in one launch,
@@ -2204,7 +2272,8 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
                           ctx->d_slow, slow_cnt );
     }
   }
-  hipLaunchKernelGGL( fd_reduce_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, nsig, code, d_pflag, d_txn_out );
+  if( !( flags & 2 ) )
+    hipLaunchKernelGGL( fd_reduce_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, nsig, code, d_pflag, d_txn_out );
   if( ctx->timing ) hipEventRecord( ev[3], st );
   HIPCHK( hipGetLastError(), -3 );
   return 0;
@@ -2239,6 +2308,8 @@ slot_bufs( fdgpu_ed25519_ctx_t * ctx, int i ) {
   HIPCHK( hipMalloc( &sl.d_payload, mp + FD_ARENA_SLACK + FD_IMG_TAIL ), -1 );   /* + the last gathered record's image */
   HIPCHK( hipMalloc( &sl.d_desc, mt * sizeof(fdgpu_txn_desc_t) ), -1 );
   HIPCHK( hipMalloc( &sl.d_txn_out, mt ), -1 );
+  HIPCHK( hipHostGetDevicePointer( (void **)&sl.hd_desc, (void *)sl.h_desc, 0 ), -1 );
+  HIPCHK( hipHostGetDevicePointer( (void **)&sl.hd_txn_out, (void *)sl.h_txn_out, 0 ), -1 );
   memset( sl.h_payload, 0, FD_ARENA_SLACK );
   return 0;
 }
@@ -2725,21 +2796,26 @@ fdgpu_txn_parse_device( unsigned char const * d_payload, fdgpu_txn_raw_t const *
   unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, (hipStream_t)stream, d_payload, d_raw, (u32)txn_cnt,
                       (fdgpu_txn_desc_t *)NULL, (unsigned char *)NULL, d_img, (u32)img_stride, d_fp, 0UL, (u64 *)NULL,
-                      (unsigned char const *)NULL );
+                      (unsigned char const *)NULL , (u32 *)NULL, 0u, (u32 *)NULL, (unsigned long *)NULL);
   HIPCHK( hipGetLastError(), -3 );
   return 0;
 }
 
+/* fused = 1 (the async pipeline): the parse kernel also writes the signature map (no fd_expand_kernel)
+   and the batch's start stamp, and the reduce is left to the caller's fd_finish_kernel */
 static int launch_raw( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_raw_t const * d_raw,
                        unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, unsigned char * d_img,
                        unsigned long img_stride, unsigned short * d_fp, hipStream_t st, u64 * d_dtag = NULL,
-                       unsigned char const * d_ovr = NULL ) {
+                       unsigned char const * d_ovr = NULL, int fused = 0, unsigned long * stamp = NULL ) {
   if( !txn_cnt ) return 0;
   unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, st, d_payload, d_raw, (u32)txn_cnt,
-                      ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp, (u64)ctx->dedup_seed, d_dtag, d_ovr );
+                      ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp, (u64)ctx->dedup_seed, d_dtag, d_ovr,
+                      fused ? ctx->d_map : (u32 *)NULL, (u32)sig_cnt, fused ? ctx->d_slow + ctx->max_sig : (u32 *)NULL,
+                      stamp );
   HIPCHK( hipGetLastError(), -3 );
-  return launch_batch( ctx, d_payload, ctx->d_rdesc, txn_cnt, sig_cnt, d_txn_out, NULL, st, ctx->d_pflag );
+  return launch_batch( ctx, d_payload, ctx->d_rdesc, txn_cnt, sig_cnt, d_txn_out, NULL, st, ctx->d_pflag,
+                       fused ? 3 : 0 );
 }
 
 extern "C" int
@@ -2894,29 +2970,31 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
     memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
     HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
   }
-  HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
   ctx->h_stamp[ 2*i ] = 0UL; ctx->h_stamp[ 2*i + 1 ] = 0UL;
   if( sl.mode != 3 ) sl.gt_idx = -1;
-  hipLaunchKernelGGL( fd_stamp_kernel, dim3(1), dim3(1), 0, st, ctx->d_stamp + 2*i );
-  int rc = sl.mode
-         ? launch_raw( ctx, sl.d_payload, (fdgpu_txn_raw_t const *)sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out,
-                       sl.d_img, FDGPU_TXN_IMG_STRIDE, sl.d_fp, st, ctx->dedup ? (u64 *)sl.d_dtag : (u64 *)NULL,
-                       sl.mode==3 ? sl.d_ovr : (unsigned char const *)NULL )
-         : launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
-  if( rc ) return rc;
-  HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
-  if( sl.mode==3 ) {   /* gathered: the images go into the out region, only the footprints come back */
-    hipLaunchKernelGGL( fd_img_scatter_kernel, dim3( (unsigned)sl.txn_cnt ), dim3( 64 ), 0, st,
-                        (fdgpu_txn_raw_t const *)sl.d_desc, sl.d_img, (u32)FDGPU_TXN_IMG_STRIDE, sl.d_fp,
-                        sl.ref_dev + sl.ref_lo, ctx->rec_fp_off );
+  if( sl.mode ) {
+    /* raw batches: the parse kernel reads the descriptors from pinned host memory and stamps the start,
+       fd_finish_kernel writes every result into pinned host memory -- four kernels fewer on the batch's
+       chain than with the upload, stamp, expand and the result copies */
+    int rc = launch_raw( ctx, sl.d_payload, (fdgpu_txn_raw_t const *)sl.hd_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out,
+                         sl.d_img, FDGPU_TXN_IMG_STRIDE, sl.d_fp, st, ctx->dedup ? (u64 *)sl.d_dtag : (u64 *)NULL,
+                         sl.mode==3 ? sl.d_ovr : (unsigned char const *)NULL, 1, ctx->d_stamp + 2*i );
+    if( rc ) return rc;
+    unsigned tg = (unsigned)( ( sl.txn_cnt + FD_WG - 1 ) / FD_WG );
+    hipLaunchKernelGGL( fd_finish_kernel, dim3(tg), dim3(FD_WG), 0, st, ctx->d_rdesc, (fdgpu_txn_raw_t const *)sl.hd_desc,
+                        (u32)sl.txn_cnt, (u32)sl.sig_cnt, ctx->d_code, ctx->d_pflag, sl.d_fp,
+                        ctx->dedup ? (u64 const *)sl.d_dtag : (u64 const *)NULL, sl.d_img, (u32)FDGPU_TXN_IMG_STRIDE,
+                        sl.hd_txn_out, sl.hd_fp, ctx->dedup ? (u64 *)sl.hd_dtag : (u64 *)NULL,
+                        sl.mode==3 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, ctx->rec_fp_off,
+                        sl.mode==3 ? (unsigned char *)NULL : sl.hd_img );
     HIPCHK( hipGetLastError(), -2 );
-    HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
-  } else if( sl.mode ) {   /* raw and in-place raw */
-    HIPCHK( hipMemcpyAsync( sl.h_fp, sl.d_fp, sl.txn_cnt * sizeof(unsigned short), hipMemcpyDeviceToHost, st ), -2 );
-    HIPCHK( hipMemcpyAsync( sl.h_img, sl.d_img, sl.txn_cnt * FDGPU_TXN_IMG_STRIDE, hipMemcpyDeviceToHost, st ), -2 );
+  } else {
+    HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
+    hipLaunchKernelGGL( fd_stamp_kernel, dim3(1), dim3(1), 0, st, ctx->d_stamp + 2*i );
+    int rc = launch_batch( ctx, sl.d_payload, sl.d_desc, sl.txn_cnt, sl.sig_cnt, sl.d_txn_out, NULL, st );
+    if( rc ) return rc;
+    HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
   }
-  if( sl.mode && ctx->dedup )
-    HIPCHK( hipMemcpyAsync( sl.h_dtag, sl.d_dtag, sl.txn_cnt * sizeof(unsigned long), hipMemcpyDeviceToHost, st ), -2 );
   sl.token++;
   hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + i, sl.token, ctx->d_stamp + 2*i + 1 );
   HIPCHK( hipGetLastError(), -2 );
@@ -3003,6 +3081,9 @@ static int slot_raw_bufs( fdgpu_ed25519_ctx_t * ctx, fd_slot * sl ) {
   HIPCHK( hipHostMalloc( (void **)&sl->h_gat, ctx->max_txn * sizeof(fd_gather), hipHostMallocDefault ), -3 );
   HIPCHK( hipHostGetDevicePointer( (void **)&sl->g_dev, (void *)sl->h_gat, 0 ), -3 );
   HIPCHK( hipMalloc( (void **)&sl->d_ovr, ctx->max_txn ), -3 );
+  HIPCHK( hipHostGetDevicePointer( (void **)&sl->hd_fp, (void *)sl->h_fp, 0 ), -3 );
+  HIPCHK( hipHostGetDevicePointer( (void **)&sl->hd_dtag, (void *)sl->h_dtag, 0 ), -3 );
+  HIPCHK( hipHostGetDevicePointer( (void **)&sl->hd_img, (void *)sl->h_img, 0 ), -3 );
   return 0;
 }
 

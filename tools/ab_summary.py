@@ -14,6 +14,8 @@ for f in sys.argv[1:]:
               f"wait {v['tile_after_split_ns_per_frag']['gpu_wait_ns']} | copy lat {v['copy_lat_mean_us']:.0f}/"
               f"{v['copy_lat_max_us']:.0f} us, gather start {g.get('launch_to_start_mean_us', 0):.0f}/"
               f"{g.get('launch_to_start_max_us', 0):.0f} us, batch {v['mean_batch_txns']:.0f}")
+        if v.get("tile_prof_ns_per_frag"):
+            print("      prof ns/frag: " + ", ".join(f"{k} {x}" for k, x in v["tile_prof_ns_per_frag"].items()))
         ph = v.get("batch_phases_us")
         if ph:
             print("      phases us: " + ", ".join(f"{k} {x:.0f}" for k, x in ph.items() if x is not None))
