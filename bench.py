@@ -389,9 +389,10 @@ def main():
     ap.add_argument("--stream-copy-wait-us", type=float, default=0.0,
                     help="zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
                          "waited this long (0 = fdgpu_vtile default, FDGPU_VTILE_COPY_WAIT_NS)")
-    ap.add_argument("--stream-lat-tiles", type=int, default=2,
-                    help="verify tiles per GPU of the paced leg (fewer tiles = fewer HIP streams sharing the "
-                         "device's hardware queues; 2 tiles carry 2M frags/s)")
+    ap.add_argument("--stream-lat-tiles", type=int, default=1,
+                    help="verify tiles per GPU of the paced legs (fewer tiles = fewer HIP streams sharing the "
+                         "device: 1 tile x 2 contexts p99 0.81 / 0.99 / 1.37 ms at 2 / 5 / 10M frags/s against "
+                         "1.09 / 1.16 / 1.61 with 2 tiles, profiles/r03/stream_fused)")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="skip the BASELINE configs[0,2,3] side measurements (small / adversarial / multi-sig)")
     ap.add_argument("--stream-child", action="store_true", help=argparse.SUPPRESS)
