@@ -3197,6 +3197,19 @@ static unsigned char * region_dev( void const * p, unsigned long sz ) {
   return NULL;
 }
 
+/* the registered region holding p: its host base, size and device base (0), or -1 */
+extern "C" int
+fdgpu_host_region( void const * p, void ** base, unsigned long * sz, void ** dev_base ) {
+  unsigned char const * q = (unsigned char const *)p;
+  int n = g_region_cnt.load( std::memory_order_acquire );
+  for( int i=0; i<n; i++ ) {
+    unsigned long rs = g_regions[i].sz.load( std::memory_order_acquire );
+    unsigned char const * h = g_regions[i].h;
+    if( rs && q >= h && q < h + rs ) { *base = (void *)h; *sz = rs; *dev_base = g_regions[i].d; return 0; }
+  }
+  return -1;
+}
+
 extern "C" void *
 fdgpu_host_alloc( unsigned long sz ) {
   void * p = NULL;
@@ -3243,6 +3256,10 @@ fdgpu_device_numa_node( int device ) {
    device arena and into dst, the record's place in the caller's pinned
    out region dst_base.  Records of one batch lie at increasing dst
    addresses (a lower one starts a new batch), chunk aligned. */
+static int submit_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char const * dsrc,
+                          unsigned char * dst_base, unsigned char * dst, unsigned long csz, unsigned short payload_off,
+                          unsigned short payload_sz, unsigned long tag, unsigned char const * dseq, unsigned long seq );
+
 extern "C" int
 fdgpu_ed25519_submit_raw_gather_chk( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char * dst_base,
                                      unsigned char * dst, unsigned short copy_sz, unsigned short payload_off,
@@ -3260,6 +3277,29 @@ fdgpu_ed25519_submit_raw_gather_chk( fdgpu_ed25519_ctx_t * ctx, unsigned char co
   if( seq_addr && !( dseq = region_dev( seq_addr, sizeof(unsigned long) ) ) ) {
     fd_err = "fdgpu_ed25519_submit_raw_gather: seq_addr not in a registered region"; return -3;
   }
+  return submit_gather( ctx, src, dsrc, dst_base, dst, csz, payload_off, payload_sz, tag, dseq, seq );
+}
+
+/* the same with the device addresses of src and seq_addr already known to the caller (a tile that
+   translated its in link's regions once, fdgpu_host_dev_ptr): no region lookup per frag */
+extern "C" int
+fdgpu_ed25519_submit_raw_gather_dev( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char const * src_dev,
+                                     unsigned char * dst_base, unsigned char * dst, unsigned short copy_sz,
+                                     unsigned short payload_off, unsigned short payload_sz, unsigned long tag,
+                                     unsigned long const * seq_dev, unsigned long seq ) {
+  if( (unsigned)payload_off + payload_sz > copy_sz || ( (uintptr_t)src & 15 ) || ( (uintptr_t)src_dev & 15 ) ||
+      ( (uintptr_t)( dst - dst_base ) & 15 ) ||
+      ( ctx->rec_fp_off >= 0 && ( payload_off > 255u || (unsigned)ctx->rec_fp_off + 2u > payload_off ) ) ||
+      ( (uintptr_t)seq_dev & 7 ) ) {
+    fd_err = "fdgpu_ed25519_submit_raw_gather: bad record"; return -1;
+  }
+  return submit_gather( ctx, src, src_dev, dst_base, dst, ( (unsigned long)copy_sz + 15UL ) & ~15UL, payload_off,
+                        payload_sz, tag, (unsigned char const *)seq_dev, seq );
+}
+
+static int submit_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char const * dsrc,
+                          unsigned char * dst_base, unsigned char * dst, unsigned long csz, unsigned short payload_off,
+                          unsigned short payload_sz, unsigned long tag, unsigned char const * dseq, unsigned long seq ) {
   unsigned b0 = payload_sz ? src[ payload_off ] : 0u;
   unsigned lanes = ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u;
   size_t off = (size_t)( dst - dst_base );

@@ -356,6 +356,8 @@ struct fdgpu_vtile {
      dcache, the GPU gathers them; in_mc (optional) for the overrun check */
   int                   zc;
   fdgpu_mcache_t const * in_mcs[ FDGPU_VTILE_IN_MAX ];
+  uchar const *         in_mc_dev[ FDGPU_VTILE_IN_MAX ];   /* device view of each in link's mcache lines (or NULL) */
+  uchar const *         src_lo, * src_hi, * src_dev;       /* the registered region the last frag came from */
   int                   n_in;
   ulong                 overruns;
   /* poll scratch */
@@ -569,7 +571,11 @@ fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_
     mc->reg = 1;
   }
   vt->zc = 1; vt->n_in = n;
-  for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) vt->in_mcs[i] = i < n ? in_mc[i] : NULL;
+  for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) {
+    vt->in_mcs[i] = i < n ? in_mc[i] : NULL;
+    vt->in_mc_dev[i] = vt->in_mcs[i] ? (uchar const *)fdgpu_host_dev_ptr( vt->in_mcs[i]->line, 8UL ) : NULL;
+  }
+  vt->src_lo = vt->src_hi = vt->src_dev = NULL;
   for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) { vt->uncopied[i] = 0UL; vt->copied_next[i] = 0UL; }
   vt->uncopied_tot = 0UL;
   vt->copy_cursor = vt->pend_tail; vt->copy_t0 = 0UL;
@@ -705,7 +711,7 @@ fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
 /* room for one more frag, and a healthy context to fill: 0, -2 (ring full: drain and retry), -3 */
 static int
 vt_room( fdgpu_vtile_t * vt ) {
-  vt_fence();
+  if( !vt->zc ) vt_fence();                      /* (zero-copy intake makes no streaming stores) */
   if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_vtile_flush( vt ); return -2; }
   /* a faulted context takes no more frags: fill the next healthy one (none: -3) */
   for( int i=0; i<vt->nctx && fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ); i++ ) vt->fill = ( vt->fill + 1 ) % vt->nctx;
@@ -767,11 +773,25 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
   if( vt->zc ) {   /* the GPU copies the frag into dst itself (no host copy) and re-checks its mcache line */
     fdgpu_mcache_t const * mc = vt->in_mcs[ link ];
-    ulong const * seq_addr = mc ? (ulong const *)&mc->line[ FDGPU_VTILE_SEQ_SEQ( seq ) & ( mc->depth - 1UL ) ].seq : NULL;
-    rc = fdgpu_ed25519_submit_raw_gather_chk( vt->ctx[ vt->fill ], (uchar const *)frag, vt->dcache, dst,
+    /* device views: the mcache lines' translated once (set_in_links), the frag's region cached */
+    ulong const * seq_dev = NULL;
+    if( mc ) {
+      if( !vt->in_mc_dev[ link ] ) return -3;
+      ulong li = FDGPU_VTILE_SEQ_SEQ( seq ) & ( mc->depth - 1UL );
+      seq_dev = (ulong const *)( vt->in_mc_dev[ link ] + ( (uchar const *)&mc->line[ li ].seq - (uchar const *)mc->line ) );
+    }
+    uchar const * src = (uchar const *)frag;
+    ulong csz = ( FDGPU_TXNM_HDR_SZ + in->payload_sz + 15UL ) & ~15UL;
+    if( src < vt->src_lo || src + csz > vt->src_hi ) {
+      void * b, * d; ulong rs;
+      if( fdgpu_host_region( src, &b, &rs, &d ) ) return -3;   /* not in a registered region */
+      vt->src_lo = (uchar const *)b; vt->src_hi = (uchar const *)b + rs; vt->src_dev = (uchar const *)d;
+      if( src + csz > vt->src_hi ) return -3;
+    }
+    rc = fdgpu_ed25519_submit_raw_gather_dev( vt->ctx[ vt->fill ], src, vt->src_dev + ( src - vt->src_lo ), vt->dcache, dst,
                                               (unsigned short)( FDGPU_TXNM_HDR_SZ + in->payload_sz ),
                                               (unsigned short)FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail,
-                                              seq_addr, FDGPU_VTILE_SEQ_SEQ( seq ) );
+                                              seq_dev, FDGPU_VTILE_SEQ_SEQ( seq ) );
   } else {
     vt_copy( dst, (uchar const *)frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
     rc = vt_submit_host_record( vt, dst, in->payload_sz, seq );

@@ -515,6 +515,17 @@ void          fdgpu_ed25519_phase_stats( fdgpu_ed25519_ctx_t const * ctx, unsign
    the raw-payload buffers and the gather stream too), so that batches later make no allocation
    syscalls -- a tile calls it in privileged init, before its sandbox.  0, or < 0 */
 int           fdgpu_ed25519_prepare( fdgpu_ed25519_ctx_t * ctx, int raw );
+/* fdgpu_ed25519_submit_raw_gather_chk with the device views of src and of the seq word given by the
+   caller (translated once per registered region, fdgpu_host_region), so the per-frag call does no
+   region lookup.  Same checks and results. */
+int           fdgpu_ed25519_submit_raw_gather_dev( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src,
+                                                   unsigned char const * src_dev, unsigned char * dst_base,
+                                                   unsigned char * dst, unsigned short copy_sz, unsigned short payload_off,
+                                                   unsigned short payload_sz, unsigned long tag,
+                                                   unsigned long const * seq_dev, unsigned long seq );
+/* the region registered with fdgpu_host_register / fdgpu_host_alloc that holds p: its host base, size and
+   device base; 0, or -1 if p is in none */
+int           fdgpu_host_region( void const * p, void ** base, unsigned long * sz, void ** dev_base );
 /* wait until every launched gather of ctx has completed: 0, or -3 (ctx faulted) */
 int           fdgpu_ed25519_gather_wait( fdgpu_ed25519_ctx_t * ctx );
 
