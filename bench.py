@@ -52,6 +52,8 @@ GUIDE_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
 # v_fma_f32 / v_add_u32 (the guide's 2-cycle row) in the same probe (profiles/r03/ROOFLINE.md), so the
 # guide's issue rate gives the MAC half the full-rate peak
 GUIDE_MAD_PEAK = GUIDE_VALU_LANE_OPS / 2
+PCIE_GBS = 63.0        # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s per direction (spec)
+PCIE_DMA_GBS = 55.2    # hipMemcpyAsync H2D, measured (tools/gatherprobe, profiles/r02/stream/gather_probe.log)
 PREP_MAC = PREP_MUL * MAC_PER_MUL + PREP_SQR * MAC_PER_SQR
 
 
@@ -245,6 +247,11 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
             # gathers and the stream's earlier batch), kernels, end -> the tile saw it; launch -> last gather end
             "batch_phases_us": _phases(st["phase"]),
             "copy_backlog_refusals": st["copy_backlog"],
+            # the host link at this leg's rate: each verdict's fd_txn_m_t record (80 + 1232 B) is read over PCIe
+            # by the GPU copy and written back into the out dcache (plus its fd_txn_t image)
+            "pcie": {"record_bytes": 1312, "in_gbs": st["frags_per_s"] * 1312 / 1e9,
+                     "out_gbs_at_least": st["frags_per_s"] * 1312 / 1e9, "peak_gbs_each_way": PCIE_GBS,
+                     "frac_each_way": st["frags_per_s"] * 1312 / 1e9 / PCIE_GBS} if cfg.get("zero_copy") else None,
             # --stream-prof: rdtsc sections of the tile loop, ns per own frag (fdgpu_stream_stats_t.prof_ns)
             "tile_prof_ns_per_frag": (dict(zip(("mcache_poll", "during_frag", "prefetch_credit", "drain_after_frags",
                                                 "hk_after_frags", "account", "credit", "housekeep"),
@@ -557,8 +564,16 @@ def main():
         finally:
             _engine.host_unregister(hpay)
         heng.close()
+        hgbs = payload.nbytes / float(np.median(hts)) / 1e9
         host_staged = {"sigs_per_s": nsig / float(np.median(hts)), "ms_per_batch": 1e3 * float(np.median(hts)),
                        "batch_txns": n, "bytes_per_batch": int(payload.nbytes), "results_ok": hok,
+                       # the host -> device link: the batch's payload bytes over the step's wall time
+                       "roofline": {"bound": "pcie", "achieved": hgbs, "peak": PCIE_GBS, "unit": "GB/s",
+                                    "frac": hgbs / PCIE_GBS, "dma_measured_peak": PCIE_DMA_GBS,
+                                    "frac_of_dma_peak": hgbs / PCIE_DMA_GBS,
+                                    "peak_source": "MI355X_MICROARCH.md host link: PCIe Gen5 x16, 63 GB/s (spec); "
+                                                   "dma_measured_peak: hipMemcpyAsync H2D of 32K records, "
+                                                   "profiles/r02/stream/gather_probe.log"},
                        "path": "payload in a registered (pinned) host buffer -> H2D in 1-MB chunks on a copy stream, "
                                "kernels on the compute stream, verdicts D2H; synchronous per batch"}
 
