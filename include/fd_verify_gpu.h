@@ -13,15 +13,19 @@
                    + fd_ed25519_verify_batch_single_msg, publish)
 
    The reference does all of after_frag synchronously per frag.  Here
-   during_frag copies the frag into the out dcache exactly as before and
-   hands its payload to the GPU (fdgpu_ed25519_submit_raw: parse and
-   verify happen on the device); after_frags drains verdicts in frag
-   order and applies the parts of after_frag that depend on order --
-   bundle state, the tcache HA dedup query / insert, metrics, the
-   fd_txn_t write-back behind the payload and the publish decision --
-   with the reference's decision order, so the published stream and the
-   four metrics equal the reference tile's for the same input stream
-   (tests/test_gpu_vtile.py checks this against a sequential model).
+   during_frag hands the frag to the GPU: either it copies the frag into
+   the out dcache as the reference does and the batch uploads it, or
+   (zero-copy intake, fdgpu_vtile_set_in_links) the GPU itself copies it
+   from the in dcache into the device and into the out-dcache record,
+   re-checking the frag's in-mcache line after the copy as the stem does.
+   Parse and verify happen on the device; after_frags drains verdicts in
+   frag order and applies the parts of after_frag that depend on order --
+   bundle state, the tcache HA dedup query / insert, metrics and the
+   publish decision -- with the reference's decision order, so the
+   published stream and the four metrics equal the reference tile's for
+   the same input stream (tests/test_gpu_vtile.py, and at 200K frags per
+   leg tests/test_gpu_stream_parity.py, against the reference tile
+   compiled in place).
 
    Also here: a minimal tango (mcache / dcache rings with the frag
    metadata and chunk addressing of src/tango/mcache/fd_mcache.h and
