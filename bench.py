@@ -379,7 +379,7 @@ def main():
                     help="mcache lines of the max-rate legs' link: a reliable producer runs depth/2 ahead of the "
                          "oldest frag a tile still holds, so the depth bounds the frags in flight (2^18: 13.8M, "
                          "2^20: 16-17.6M sigs/s on 2 tiles, profiles/r02/stream/sweep_depth.log)")
-    ap.add_argument("--stream-rates", default="2e6,5e6,10e6,15e6",
+    ap.add_argument("--stream-rates", default="2e6,5e6,7.5e6,10e6,15e6",
                     help="paced legs (the latency-under-load curve): offered frags/s per GPU, comma separated; "
                          "stream.knee = the highest whose p99 is <= 1 ms with no frag lost")
     ap.add_argument("--stream-paced-seconds", type=float, default=3.0, help="length of each paced leg")

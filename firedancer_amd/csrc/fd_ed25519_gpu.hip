@@ -1667,51 +1667,48 @@ fd_reduce_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 n
 }
 
 /* The async raw batches' last work kernel (fdgpu_ed25519_submit_raw*): the reduce, then every result
-   straight into the slot's pinned host arrays (device views), so no copy commands follow the batch:
-   each thread one transaction's code, footprint and dedup tag (consecutive lanes, consecutive host
-   addresses), then the block's 256 fd_txn_t images one after another, each copied by all 256 lanes
-   in 2-byte stores -- into the caller's out region behind the payload with txn_t_sz in the record
-   header (gathered batches, as fd_img_scatter_kernel), or into the slot's image array (the others). */
+   straight into the slot's pinned host arrays (device views), so no copy commands follow the batch.
+   Blocks [0, tg): one thread per transaction writes its code, footprint and dedup tag (consecutive
+   lanes, consecutive host addresses).  Blocks [tg, tg + ceil(n/4)): one wave per transaction copies its
+   fd_txn_t image in 2-byte stores -- into the caller's out region behind the payload, with txn_t_sz in
+   the record header (gathered batches), or into the slot's image array (the others).  One wave per
+   image keeps every image's loads in flight at once (a block looping over its transactions' images
+   waited one load latency per transaction: 80 us for a 1,536-transaction batch). */
 __global__ void __launch_bounds__( FD_WG )
 fd_finish_kernel( fdgpu_txn_desc_t const * __restrict__ desc, fdgpu_txn_raw_t const * __restrict__ raw, u32 txn_cnt,
                   u32 nsig, i8 const * __restrict__ code, unsigned char const * __restrict__ pflag,
                   unsigned short const * __restrict__ fp, u64 const * __restrict__ dtag,
                   unsigned char const * __restrict__ img, u32 stride,
                   i8 * __restrict__ h_out, unsigned short * __restrict__ h_fp, u64 * __restrict__ h_dtag,
-                  unsigned char * __restrict__ out_region, int rec_fp_off, unsigned char * __restrict__ h_img ) {
-  /* the descriptors live in pinned host memory: each lane reads its own once (in parallel), the image
-     loop below takes the offsets from LDS */
-  __shared__ u32 s_img_off[ FD_WG ], s_hdr_off[ FD_WG ];
-  __shared__ unsigned short s_n[ FD_WG ];
-  u32 t0 = blockIdx.x * FD_WG, t = t0 + threadIdx.x;
-  if( t < txn_cnt ) {
-    unsigned short n = fp[t];
+                  unsigned char * __restrict__ out_region, int rec_fp_off, unsigned char * __restrict__ h_img,
+                  u32 tg ) {
+  if( blockIdx.x < tg ) {
+    u32 t = blockIdx.x * FD_WG + threadIdx.x;
+    if( t >= txn_cnt ) return;
     h_out[t] = (i8)txn_code( desc[t], t, nsig, code, pflag );
-    h_fp[t] = n;
+    h_fp[t] = fp[t];
     if( h_dtag ) h_dtag[t] = dtag[t];
-    s_n[ threadIdx.x ] = n;
-    if( out_region && n ) {
-      fdgpu_txn_raw_t r = raw[t];
-      s_img_off[ threadIdx.x ] = ( r.payload_off + (u32)r.payload_sz + 1u ) & ~1u;
-      s_hdr_off[ threadIdx.x ] = r.payload_off - (u32)r._pad[0];
-    }
+    return;
   }
-  __syncthreads();
-  u32 nt = txn_cnt - t0 < (u32)FD_WG ? txn_cnt - t0 : (u32)FD_WG;
-  for( u32 k=0; k<nt; k++ ) {
-    u32 u = t0 + k;
-    u32 n = s_n[k];
-    if( !n ) continue;
-    unsigned short const * s16 = (unsigned short const *)( img + (size_t)u*stride );
-    unsigned char * dst;
-    if( out_region ) {
-      dst = out_region + s_img_off[k];
-      if( rec_fp_off >= 0 && threadIdx.x==0u )
-        *(unsigned short *)( out_region + s_hdr_off[k] + (u32)rec_fp_off ) = (unsigned short)n;
-    } else dst = h_img + (size_t)u*stride;
-    for( u32 i=threadIdx.x; i<(n >> 1); i+=FD_WG ) ((unsigned short *)dst)[i] = s16[i];
-    if( ( n & 1u ) && threadIdx.x==0u ) dst[n-1u] = img[(size_t)u*stride + n - 1u];
-  }
+  u32 lane = threadIdx.x & 63u;
+  u32 u = ( blockIdx.x - tg ) * ( FD_WG / 64u ) + ( threadIdx.x >> 6 );
+  if( u >= txn_cnt ) return;
+  u32 n = fp[u];
+  if( !n ) return;
+  unsigned char * dst;
+  if( out_region ) {
+    fdgpu_txn_raw_t r = raw[u];
+    dst = out_region + ( ( r.payload_off + (u32)r.payload_sz + 1u ) & ~1u );
+    if( rec_fp_off >= 0 && lane==0u )
+      *(unsigned short *)( out_region + r.payload_off - (u32)r._pad[0] + (u32)rec_fp_off ) = (unsigned short)n;
+  } else dst = h_img + (size_t)u*stride;
+  unsigned short const * s16 = (unsigned short const *)( img + (size_t)u*stride );
+  unsigned short v[ 7 ];                          /* up to 852 B: 426 shorts, 7 per lane, all loads first */
+#pragma unroll
+  for( int k=0; k<7; k++ ) { u32 i = lane + 64u*(u32)k; v[k] = i < (n >> 1) ? s16[i] : (unsigned short)0; }
+#pragma unroll
+  for( int k=0; k<7; k++ ) { u32 i = lane + 64u*(u32)k; if( i < (n >> 1) ) ((unsigned short *)dst)[i] = v[k]; }
+  if( ( n & 1u ) && lane==0u ) dst[n-1u] = img[(size_t)u*stride + n - 1u];
 }
 
 /* Raw-payload batches: fd_txn_parse per transaction (fd_gpu_txn.h), then
@@ -2981,12 +2978,13 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
                          sl.mode==3 ? sl.d_ovr : (unsigned char const *)NULL, 1, ctx->d_stamp + 2*i );
     if( rc ) return rc;
     unsigned tg = (unsigned)( ( sl.txn_cnt + FD_WG - 1 ) / FD_WG );
-    hipLaunchKernelGGL( fd_finish_kernel, dim3(tg), dim3(FD_WG), 0, st, ctx->d_rdesc, (fdgpu_txn_raw_t const *)sl.hd_desc,
+    unsigned ig = (unsigned)( ( sl.txn_cnt + FD_WG/64 - 1 ) / ( FD_WG/64 ) );
+    hipLaunchKernelGGL( fd_finish_kernel, dim3(tg + ig), dim3(FD_WG), 0, st, ctx->d_rdesc, (fdgpu_txn_raw_t const *)sl.hd_desc,
                         (u32)sl.txn_cnt, (u32)sl.sig_cnt, ctx->d_code, ctx->d_pflag, sl.d_fp,
                         ctx->dedup ? (u64 const *)sl.d_dtag : (u64 const *)NULL, sl.d_img, (u32)FDGPU_TXN_IMG_STRIDE,
                         sl.hd_txn_out, sl.hd_fp, ctx->dedup ? (u64 *)sl.hd_dtag : (u64 *)NULL,
                         sl.mode==3 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, ctx->rec_fp_off,
-                        sl.mode==3 ? (unsigned char *)NULL : sl.hd_img );
+                        sl.mode==3 ? (unsigned char *)NULL : sl.hd_img, tg );
     HIPCHK( hipGetLastError(), -2 );
   } else {
     HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
