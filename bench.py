@@ -267,9 +267,10 @@ def stream_child_main(args) -> None:
     from firedancer_amd import vtile
     proc, procs, dev = args.stream_proc, args.stream_procs, args.stream_device
     out, cal_fps = {}, 0.0
-    if args.stream_diag_no_writeback:
+    wb = {"gather": 0, "none": 1, "finish": 2}[args.stream_writeback]
+    if wb:
         from firedancer_amd import engine
-        engine.debug_set_opts(gather_no_writeback=1)
+        engine.debug_set_opts(gather_no_writeback=wb)
     payload = desc = None
     if proc == 0:
         from firedancer_amd import synth
@@ -392,9 +393,10 @@ def main():
     ap.add_argument("--stream-max-uncopied", type=int, default=0,
                     help="zero-copy intake: frags a tile may hold whose GPU copy has not completed (fdgpu_vtile_opts_t."
                          "max_uncopied; 0 = its default)")
-    ap.add_argument("--stream-diag-no-writeback", action="store_true",
-                    help="DIAGNOSTIC (stream child only): gathers skip the record write-back into the out dcache, so "
-                         "published records lack their payload -- what the write-back costs; never a result")
+    ap.add_argument("--stream-writeback", choices=("gather", "finish", "none"), default="gather",
+                    help="(stream child only) who writes a gathered record into the out dcache: the gather kernel as it "
+                         "copies (default), the batch's finish kernel (A/B), or nobody (DIAGNOSTIC: published records lack "
+                         "their payload -- what the write-back costs; never a result)")
     ap.add_argument("--stream-copy-wait-us", type=float, default=0.0,
                     help="zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
                          "waited this long (0 = fdgpu_vtile default, FDGPU_VTILE_COPY_WAIT_NS)")

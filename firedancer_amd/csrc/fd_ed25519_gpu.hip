@@ -1681,7 +1681,7 @@ fd_finish_kernel( fdgpu_txn_desc_t const * __restrict__ desc, fdgpu_txn_raw_t co
                   unsigned char const * __restrict__ img, u32 stride,
                   i8 * __restrict__ h_out, unsigned short * __restrict__ h_fp, u64 * __restrict__ h_dtag,
                   unsigned char * __restrict__ out_region, int rec_fp_off, unsigned char * __restrict__ h_img,
-                  u32 tg ) {
+                  u32 tg, unsigned char const * __restrict__ arena ) {
   if( blockIdx.x < tg ) {
     u32 t = blockIdx.x * FD_WG + threadIdx.x;
     if( t >= txn_cnt ) return;
@@ -1698,9 +1698,30 @@ fd_finish_kernel( fdgpu_txn_desc_t const * __restrict__ desc, fdgpu_txn_raw_t co
   unsigned char * dst;
   if( out_region ) {
     fdgpu_txn_raw_t r = raw[u];
+    u32 rec = r.payload_off - (u32)r._pad[0];        /* the record's offset in the arena and in the out region */
     dst = out_region + ( ( r.payload_off + (u32)r.payload_sz + 1u ) & ~1u );
-    if( rec_fp_off >= 0 && lane==0u )
-      *(unsigned short *)( out_region + r.payload_off - (u32)r._pad[0] + (u32)rec_fp_off ) = (unsigned short)n;
+    if( arena ) {
+      /* the record's write-back into the out region, deferred from its gather to here (the gather then
+         only reads over PCIe): header + payload exactly as copied at gather time -- whole 16-B pieces,
+         then the tail bytes, so nothing lands where the fd_txn_t goes -- with txn_t_sz set */
+      u32 end = r.payload_off + (u32)r.payload_sz - rec, n16 = end >> 4;
+      uint4 const * a = (uint4 const *)( arena + rec );
+      uint4 * o = (uint4 *)( out_region + rec );
+      uint4 w0 = make_uint4( 0u, 0u, 0u, 0u ), w1 = w0;
+      if( lane < n16 ) w0 = a[lane];
+      if( lane + 64u < n16 ) w1 = a[lane + 64u];
+      int fix = rec_fp_off >= 0 && !( rec_fp_off & 1 ) && rec_fp_off + 2 <= 16 && n16 > 0u;
+      if( fix && lane == 0u ) ((unsigned short *)&w0)[ rec_fp_off >> 1 ] = (unsigned short)n;   /* txn_t_sz */
+      if( lane < n16 ) o[lane] = w0;
+      if( lane + 64u < n16 ) o[lane + 64u] = w1;
+      for( u32 i=lane+128u; i<n16; i+=64u ) o[i] = a[i];      /* (records past 2 KB: none from a tile) */
+      for( u32 b=( n16 << 4 ) + lane; b<end; b+=64u ) out_region[ rec + b ] = arena[ rec + b ];
+      if( !fix && rec_fp_off >= 0 && lane==0u ) {
+        __builtin_amdgcn_s_waitcnt( 0 );                     /* (after this lane's own copy stores) */
+        *(unsigned short *)( out_region + rec + (u32)rec_fp_off ) = (unsigned short)n;
+      }
+    } else if( rec_fp_off >= 0 && lane==0u )
+      *(unsigned short *)( out_region + rec + (u32)rec_fp_off ) = (unsigned short)n;
   } else dst = h_img + (size_t)u*stride;
   unsigned short const * s16 = (unsigned short const *)( img + (size_t)u*stride );
   unsigned short v[ 7 ];                          /* up to 852 B: 426 shorts, 7 per lane, all loads first */
@@ -2029,7 +2050,8 @@ struct fdgpu_ed25519_ctx {
   fdgpu_txn_desc_t * d_rdesc;    /* raw path: descriptors derived by fd_parse_kernel */
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
   int dsm_lanes;                 /* latency path: lanes per signature in the DSM, 0 = by batch size (fdgpu_debug_opts_t) */
-  int gather_nowb;               /* fdgpu_debug_opts_t.gather_no_writeback (diagnostic) */
+  int gather_nowb;               /* fdgpu_debug_opts_t.gather_no_writeback: 0 = the records' write-back in
+                                    the gather kernel, 1 = none (diagnostic), 2 = in fd_finish_kernel (A/B) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
   unsigned long nofold_max;      /* fd_dsm_kernel<0> (no carry fold) for batches of at most this many signatures */
   u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
@@ -2937,7 +2959,7 @@ static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
     ctx->last_gt = (long)i;
   } else { gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT; ctx->last_gt = -1; }   /* untimed: a scratch entry */
   hipLaunchKernelGGL( fd_gather_kernel, dim3( (unsigned)n ), dim3( 64 ), 0, ctx->gstream, sl.g_dev + sl.gathered,
-                      sl.d_payload, ctx->gather_nowb ? (unsigned char *)NULL : sl.ref_dev + sl.ref_lo, sl.d_ovr + sl.gathered, ctx->d_gcnt,
+                      sl.d_payload, ctx->gather_nowb == 0 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, sl.d_ovr + sl.gathered, ctx->d_gcnt,
                       (unsigned long *)( ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT + 1 ), target, gt );
   HIPCHK( hipGetLastError(), -2 );
   ctx->g_launched = target; sl.gathered = sl.txn_cnt;
@@ -2984,7 +3006,8 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
                         ctx->dedup ? (u64 const *)sl.d_dtag : (u64 const *)NULL, sl.d_img, (u32)FDGPU_TXN_IMG_STRIDE,
                         sl.hd_txn_out, sl.hd_fp, ctx->dedup ? (u64 *)sl.hd_dtag : (u64 *)NULL,
                         sl.mode==3 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, ctx->rec_fp_off,
-                        sl.mode==3 ? (unsigned char *)NULL : sl.hd_img, tg );
+                        sl.mode==3 ? (unsigned char *)NULL : sl.hd_img, tg,
+                        sl.mode==3 && ctx->gather_nowb == 2 ? (unsigned char const *)sl.d_payload : (unsigned char const *)NULL );
     HIPCHK( hipGetLastError(), -2 );
   } else {
     HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );

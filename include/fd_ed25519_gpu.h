@@ -610,9 +610,10 @@ typedef struct fdgpu_debug_opts {
   long          small_batch_max;  /* -1: default; else the initial fdgpu_ed25519_set_small_batch_max */
   int           dsm_lanes;        /* latency path: lanes per signature in the DSM (1, 2, 4, 8); 0 = by batch size */
   long          nofold_max;       /* -1: default; batches of at most this many signatures use the unfolded DSM */
-  int           gather_no_writeback; /* DIAGNOSTIC: gathered records are copied into the device arena only, not back
-                                        into the caller's out region (published records then lack their payload:
-                                        measures what the write-back costs, never for parity) */
+  int           gather_no_writeback; /* gathered records' write-back into the caller's out region: 0 = by the
+                                        gather kernel as it copies (default); 2 = by the batch's fd_finish_kernel
+                                        from the device arena (A/B: measured slower, profiles/r03/stream_defer);
+                                        1 = DIAGNOSTIC, none (published records lack their payload) */
 } fdgpu_debug_opts_t;
 
 void
