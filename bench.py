@@ -186,7 +186,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 mcache_depth=args.stream_depth * min(procs, 2) if not paced else 1 << 18,
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
                 copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus,
-                max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0)
+                max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -324,7 +324,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-ctx", str(args.stream_ctx), "--stream-lat-ctx", str(args.stream_lat_ctx),
            "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
            "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus),
-           "--stream-max-uncopied", str(args.stream_max_uncopied)] + (["--stream-prof"] if args.stream_prof else [])
+           "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
+        (["--stream-prof"] if args.stream_prof else [])
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -393,6 +394,8 @@ def main():
     ap.add_argument("--stream-max-uncopied", type=int, default=0,
                     help="zero-copy intake: frags a tile may hold whose GPU copy has not completed (fdgpu_vtile_opts_t."
                          "max_uncopied; 0 = its default)")
+    ap.add_argument("--stream-pf-dist", type=int, default=0,
+                    help="tile loop prefetch distance in own frags (fdgpu_stream_cfg_t.pf_dist; 0 = its default)")
     ap.add_argument("--stream-writeback", choices=("gather", "finish", "none"), default="gather",
                     help="(stream child only) who writes a gathered record into the out dcache: the gather kernel as it "
                          "copies (default), the batch's finish kernel (A/B), or nobody (DIAGNOSTIC: published records lack "

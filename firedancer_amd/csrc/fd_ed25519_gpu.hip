@@ -267,7 +267,15 @@ FD_DEV void decode_one( unsigned char const * __restrict__ payload, fdgpu_txn_de
 
 /* Large batches (deferred R): one lane per signature, A only.  With
    both = 1 (FD_DEFER_R=0 builds): lane 2s decodes A, lane 2s+1 R. */
+/* FD_DECODE_MINW: minimum waves per SIMD asked of the compiler (A/B; 0 = none: 127 VGPRs, 4 waves) */
+#ifndef FD_DECODE_MINW
+#define FD_DECODE_MINW 0
+#endif
+#if FD_DECODE_MINW
+__global__ void __launch_bounds__( FD_WG, FD_DECODE_MINW )
+#else
 __global__ void __launch_bounds__( FD_WG )
+#endif
 fd_decode_kernel( unsigned char const *    __restrict__ payload,
                   fdgpu_txn_desc_t const * __restrict__ desc,
                   u32 const *              __restrict__ map,
@@ -549,7 +557,15 @@ FD_DEV void hashh_one( unsigned char const * __restrict__ payload, fdgpu_txn_des
   }
 }
 
+/* FD_HASHH_MINW: as FD_DECODE_MINW for fd_hashh_kernel (0: 159 VGPRs, 3 waves) */
+#ifndef FD_HASHH_MINW
+#define FD_HASHH_MINW 0
+#endif
+#if FD_HASHH_MINW
+__global__ void __launch_bounds__( FD_WG, FD_HASHH_MINW )
+#else
 __global__ void __launch_bounds__( FD_WG )
+#endif
 fd_hashh_kernel( unsigned char const *    __restrict__ payload,
                  fdgpu_txn_desc_t const * __restrict__ desc,
                  u32 const *              __restrict__ map,
@@ -569,6 +585,37 @@ fd_hashh_kernel( unsigned char const *    __restrict__ payload,
   if( s >= nsig ) return;
   hashh_one( payload, desc, map, s, nsig, semantics, 1, pstat, code_out, digA, digR, digB, slow, slow_cnt, khash,
              force_slow, htop );
+}
+
+/* FD_SHA_SPLIT (A/B): the half-size throughput path hashes in a kernel of its own, at the occupancy the
+   SHA-512 registers allow, instead of inside fd_hashh_kernel, whose lattice reduction sets 159 VGPRs (3
+   waves per SIMD) for the whole hash; fd_hashh_kernel then reads the digests (its khash input) */
+#ifndef FD_SHA_SPLIT
+#define FD_SHA_SPLIT 0
+#endif
+#ifndef FD_SHA_MINW
+#define FD_SHA_MINW 4
+#endif
+__global__ void __launch_bounds__( FD_WG, FD_SHA_MINW )
+fd_sha_kernel( unsigned char const *    __restrict__ payload,
+               fdgpu_txn_desc_t const * __restrict__ desc,
+               u32 const *              __restrict__ map,
+               u32                                   nsig,
+               uint4 *                  __restrict__ dig ) {
+  u32 s = blockIdx.x * FD_WG + threadIdx.x;
+  if( s >= nsig ) return;
+  u32 m = map[s];
+  u32 t = m & 0xffffffu, j = m >> 24;
+  fdgpu_txn_desc_t d = desc[t];
+  if( !txn_desc_ok( d ) ) return;
+  unsigned char const * base = payload + d.payload_off;
+  u32 Rw[8], Aw[8], h[16];
+  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
+  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
+  fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
+  uint4 * o = dig + 4*(size_t)s;
+#pragma unroll
+  for( int i=0; i<4; i++ ) o[i] = make_uint4( h[4*i], h[4*i+1], h[4*i+2], h[4*i+3] );
 }
 
 /* Small batches (latency): the three independent parts of the prep in
@@ -2066,6 +2113,7 @@ struct fdgpu_ed25519_ctx {
   unsigned char * d_htop;        /*                 highest nonzero window of c0 / c1, [max_sig] */
   uint4 * d_btab2;               /*                 [0..32768](2^120 B) */
   uint4 * d_khash;               /* NULL, or (drop-in, long messages) SHA-512(R||A||M) per signature, computed beforehand */
+  uint4 * d_kdig;                /* FD_SHA_SPLIT: fd_sha_kernel's digests, [max_sig][4] */
   hipEvent_t ev[4];
   enum { NRING = 64 };
   hipEvent_t ring[ NRING ][ 4 ];  /* per-batch kernel boundaries while timing is on */
@@ -2214,10 +2262,14 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, 1,
                           ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, (uint4 *)NULL, (uint4 *)NULL );
 #endif
+      uint4 const * kh = (uint4 const *)ctx->d_khash;
+      if( FD_SHA_SPLIT && !kh ) {
+        hipLaunchKernelGGL( fd_sha_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, ctx->d_kdig );
+        kh = ctx->d_kdig;
+      }
       hipLaunchKernelGGL( fd_hashh_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
                           ctx->semantics, ctx->d_pstat, code, ctx->d_digA, ctx->d_digR, ctx->d_digB, ctx->d_slow,
-                          ctx->d_slow + ctx->max_sig, (uint4 const *)ctx->d_khash, ctx->half_force_slow,
-                          ctx->d_htop );
+                          ctx->d_slow + ctx->max_sig, kh, ctx->half_force_slow, ctx->d_htop );
 #if !FD_HALF_FUSED_TABLE
       hipLaunchKernelGGL( fd_tableh_kernel, dim3(2*sg), dim3(FD_WG), 0, st, nsig, (u32)sg, code, ctx->d_Axy, ctx->d_Rxy,
                           ctx->d_tab, ctx->d_tabR );
@@ -2385,6 +2437,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
     HIPCHK( hipMalloc( &ctx->d_tabR, ns * FD_ATAB_STORED * 8 * sizeof(uint4) ), -1 );
     HIPCHK( hipMalloc( &ctx->d_digR, ns * FD_HDIG ), -1 );
     HIPCHK( hipMalloc( &ctx->d_htop, ns ), -1 );
+    if( FD_SHA_SPLIT ) HIPCHK( hipMalloc( &ctx->d_kdig, ns * 4 * sizeof(uint4) ), -1 );
     HIPCHK( hipMalloc( &ctx->d_btab2, FD_BTAB_ENTRIES * 6 * sizeof(uint4) ), -1 );
   }
   ctx->small_max  = dbg.small_batch_max >= 0 ? (unsigned long)dbg.small_batch_max : FD_SMALL_BATCH_MAX;
@@ -2442,6 +2495,7 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   (void)hipFree( ctx->d_Rxy ); (void)hipFree( ctx->d_Axy ); (void)hipFree( ctx->d_digA ); (void)hipFree( ctx->d_digB );
   (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_rdesc ); (void)hipFree( ctx->d_pflag );
   (void)hipFree( ctx->d_tabR ); (void)hipFree( ctx->d_digR ); (void)hipFree( ctx->d_htop ); (void)hipFree( ctx->d_btab2 );
+  (void)hipFree( ctx->d_kdig );
   (void)hipFree( ctx->d_P ); (void)hipFree( ctx->d_O ); (void)hipFree( ctx->d_blk ); (void)hipFree( ctx->d_slow );
   for( int i=0; i<4; i++ ) if( ctx->ev[i] ) (void)hipEventDestroy( ctx->ev[i] );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) if( ctx->ring[r][i] ) (void)hipEventDestroy( ctx->ring[r][i] );

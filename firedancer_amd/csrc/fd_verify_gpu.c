@@ -1500,6 +1500,7 @@ static void * link_tile( void * _a ) {
   for( ulong q=0; q<Q; q++ ) { in[q].n = prod_frags( c->n_frags, Q, q ); mine += own_in( 0UL, in[q].n, T, (ulong)idx ); }
   ulong last_prog = ~0UL, t_prog = now_ns(), q0 = 0UL;
   ulong per_link = Q > 1UL ? ( 64UL / Q > 8UL ? 64UL / Q : 8UL ) : 64UL;   /* own frags per link per pass */
+  ulong pfl = c->pf_dist > 0 ? (ulong)c->pf_dist : 1UL, pfh = pfl > 1UL ? pfl / 2UL : 1UL;   /* prefetch distances */
   ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, ns_idle = 0UL, t_begin = now_ns();
   /* FDGPU_LINK_PROF=1: rdtsc section profile (mcache poll, during_frag, prefetch + credit, drain
      after_frags, housekeep after_frags, link_account, credit after a drain, housekeep) */
@@ -1554,11 +1555,14 @@ static void * link_tile( void * _a ) {
         if( rc == FDGPU_VTILE_COPY_BACKLOG ) { backlog = 1; li->seq = own; break; }   /* copies behind: poll them, retry */
         if( rc ) { fprintf( stderr, "fdgpu_link: tile %d during_frag %d\n", idx, rc ); atomic_store( &h->fail, 2 ); drain = 1; break; }
         li->app++; took++;
-        /* this tile's next frag of the link is usually published already: start its cold lines */
-        if( own + T < li->n ) {
-          mc_line_t const * nl = &line[ ( own + T ) & mask ];
-          __builtin_prefetch( nl );
-          if( atomic_load_explicit( (_Atomic ulong *)&nl->seq, memory_order_relaxed ) == own + T ) {
+        /* this tile's next frags of the link are usually published already: start their cold lines,
+           software-pipelined -- the mcache line pf_dist own frags ahead, and the record header of the
+           frag pf_dist/2 ahead, whose line the prefetch pf_dist/2 iterations ago brought in */
+        if( own + pfl*T < li->n ) __builtin_prefetch( &line[ ( own + pfl*T ) & mask ] );
+        if( own + pfh*T < li->n ) {
+          mc_line_t const * nl = &line[ ( own + pfh*T ) & mask ];
+          if( pfh == pfl ) __builtin_prefetch( nl );
+          if( atomic_load_explicit( (_Atomic ulong *)&nl->seq, memory_order_relaxed ) == own + pfh*T ) {
             uchar const * pf = l->dcache + (ulong)nl->chunk * FDGPU_CHUNK_SZ;
             __builtin_prefetch( pf ); __builtin_prefetch( pf + 64 );
           }

@@ -346,6 +346,9 @@ typedef struct fdgpu_stream_cfg {
   unsigned long copy_min;        /* zero-copy: fdgpu_vtile_opts_t.copy_min (0 = its default) */
   unsigned int  gather_cus;      /* fdgpu_vtile_opts_t.gather_cus */
   unsigned long max_uncopied;    /* fdgpu_vtile_opts_t.max_uncopied (0 = its default) */
+  int           pf_dist;         /* tile loop prefetch distance, in own frags: the mcache line pf_dist ahead and
+                                    the record header of the frag pf_dist/2 ahead (0 = 1: the next own frag's
+                                    line and header; 4 and 8 measured the same, profiles/r03/prep_pf_ab) */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
