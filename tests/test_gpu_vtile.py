@@ -120,13 +120,18 @@ def in_dcache(frag_list):
     return buf, [base + o for o in offs]
 
 
-@pytest.mark.parametrize("zero_copy", [False, True])
+@pytest.mark.parametrize("zero_copy", [False, True, "finish"])
 @pytest.mark.parametrize("batch,depth", [(64, 32), (512, 1 << 12)])
-def test_vtile_vs_model(oracle, batch, depth, zero_copy):
+def test_vtile_vs_model(oracle, batch, depth, zero_copy, engine_path):
     """zero_copy: the frags stay in a registered in dcache and the GPU gathers them into the out
-    dcache records (fdgpu_vtile_set_in_link); outcomes and published records must not change."""
+    dcache records (fdgpu_vtile_set_in_link); outcomes and published records must not change.
+    "finish": the same, with the records written into the out dcache by each batch's fd_finish_kernel
+    from the device arena instead of by the gather kernel (fdgpu_debug_opts_t.gather_no_writeback = 2)."""
     pytest.importorskip("xxhash")
     from firedancer_amd import engine, vtile
+    if zero_copy == "finish":
+        from conftest import engine_opts
+        engine.debug_set_opts(**engine_opts(engine_path, gather_no_writeback=2))
     frags = make_stream()
     seed = 0x1234abcd
     want_res, want_m, want_recs, want_tags = expectation(oracle, frags, seed, depth)
