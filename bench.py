@@ -268,9 +268,9 @@ def stream_child_main(args) -> None:
     proc, procs, dev = args.stream_proc, args.stream_procs, args.stream_device
     out, cal_fps = {}, 0.0
     wb = {"gather": 0, "none": 1, "finish": 2}[args.stream_writeback]
-    if wb:
+    if wb or args.stream_poll_prefetch:
         from firedancer_amd import engine
-        engine.debug_set_opts(gather_no_writeback=wb)
+        engine.debug_set_opts(gather_no_writeback=wb, poll_prefetch=args.stream_poll_prefetch)
     payload = desc = None
     if proc == 0:
         from firedancer_amd import synth
@@ -394,6 +394,9 @@ def main():
     ap.add_argument("--stream-max-uncopied", type=int, default=0,
                     help="zero-copy intake: frags a tile may hold whose GPU copy has not completed (fdgpu_vtile_opts_t."
                          "max_uncopied; 0 = its default)")
+    ap.add_argument("--stream-poll-prefetch", type=int, default=0,
+                    help="(stream child only, A/B) software prefetch distance of the tiles' completion polls "
+                         "(fdgpu_debug_opts_t.poll_prefetch; 0 = none)")
     ap.add_argument("--stream-pf-dist", type=int, default=0,
                     help="tile loop prefetch distance in own frags (fdgpu_stream_cfg_t.pf_dist; 0 = its default)")
     ap.add_argument("--stream-writeback", choices=("gather", "finish", "none"), default="gather",

@@ -2097,6 +2097,7 @@ struct fdgpu_ed25519_ctx {
   fdgpu_txn_desc_t * d_rdesc;    /* raw path: descriptors derived by fd_parse_kernel */
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
   int dsm_lanes;                 /* latency path: lanes per signature in the DSM, 0 = by batch size (fdgpu_debug_opts_t) */
+  int poll_pf;                   /* fdgpu_debug_opts_t.poll_prefetch */
   int gather_nowb;               /* fdgpu_debug_opts_t.gather_no_writeback: 0 = the records' write-back in
                                     the gather kernel, 1 = none (diagnostic), 2 = in fd_finish_kernel (A/B) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
@@ -2444,6 +2445,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->dsm_lanes  = dbg.dsm_lanes;
   ctx->nofold_max = dbg.nofold_max >= 0 ? (unsigned long)dbg.nofold_max : FD_NOFOLD_MAX;
   ctx->gather_nowb = dbg.gather_no_writeback;
+  ctx->poll_pf = dbg.poll_prefetch > 0 ? dbg.poll_prefetch : 0;
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
@@ -3546,8 +3548,15 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
     }
     unsigned long k = sl.txn_cnt - sl.cursor;
     if( k > max - n ) k = max - n;
+    unsigned long pf = (unsigned long)ctx->poll_pf;
     for( unsigned long t=0; t<k; t++ ) {
       unsigned long u = sl.cursor + t;
+      /* the result arrays were written by the GPU over PCIe: their lines are not in the CPU's caches */
+      if( pf && !( u & 7UL ) && u + pf < sl.txn_cnt ) {
+        __builtin_prefetch( sl.h_tags + u + pf );
+        if( sl.mode ) { __builtin_prefetch( sl.h_dtag + u + pf ); __builtin_prefetch( sl.h_fp + u + 4*pf ); }
+        __builtin_prefetch( sl.h_txn_out + u + 8*pf );
+      }
       out_tags[n+t]  = sl.h_tags[u];
       out_codes[n+t] = sl.h_txn_out[u];
       if( out_fp )  out_fp[n+t] = sl.mode ? sl.h_fp[u] : 0;

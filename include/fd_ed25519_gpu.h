@@ -614,6 +614,8 @@ typedef struct fdgpu_debug_opts {
                                         gather kernel as it copies (default); 2 = by the batch's fd_finish_kernel
                                         from the device arena (A/B: measured slower, profiles/r03/stream_defer);
                                         1 = DIAGNOSTIC, none (published records lack their payload) */
+  int           poll_prefetch;       /* completions polled: software prefetch this many entries ahead in the
+                                        GPU-written result arrays (0: none, A/B) */
 } fdgpu_debug_opts_t;
 
 void
