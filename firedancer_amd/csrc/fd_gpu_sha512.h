@@ -156,18 +156,22 @@ FD_DEV void fd_sha512_RAM( u32 out[ 16 ], u32 const R[ 8 ], u32 const A[ 8 ],
       fd_load_words<32>( lw, msg + (128u*b - 64u) );
     }
 #pragma unroll
-    for( int i=0; i<16; i++ ) {
-      u64 x = ((u64)fd_bswap32( lw[2*i] ) << 32) | (u64)fd_bswap32( lw[2*i+1] );
-      /* mask bytes past the end, insert 0x80, insert the bit length */
-      int pos = (int)(128u*b) + 8*i;
-      int nv  = (int)L - pos;                     /* valid bytes in this word */
-      if( b==0 && i<8 ) nv = 8;                   /* R||A always present */
-      u64 m = nv>=8 ? ~0UL : ( nv<=0 ? 0UL : ( ~0UL << (8*(8-nv)) ) );
-      x &= m;
-      if( nv>=0 && nv<8 ) x |= 0x80UL << (8*(7-nv));
-      if( b==nb-1u && i==15 ) x = (u64)L << 3;
-      if( b==nb-1u && i==14 ) x = 0UL;
-      w[i] = x;
+    for( int i=0; i<16; i++ ) w[i] = ((u64)fd_bswap32( lw[2*i] ) << 32) | (u64)fd_bswap32( lw[2*i+1] );
+    if( 128u*(b+1u) > L ) {                       /* the message ends in this block: mask, pad, length */
+#pragma unroll
+      for( int i=0; i<16; i++ ) {
+        /* mask bytes past the end, insert 0x80, insert the bit length */
+        u64 x = w[i];
+        int pos = (int)(128u*b) + 8*i;
+        int nv  = (int)L - pos;                   /* valid bytes in this word */
+        if( b==0 && i<8 ) nv = 8;                 /* R||A always present */
+        u64 m = nv>=8 ? ~0UL : ( nv<=0 ? 0UL : ( ~0UL << (8*(8-nv)) ) );
+        x &= m;
+        if( nv>=0 && nv<8 ) x |= 0x80UL << (8*(7-nv));
+        if( b==nb-1u && i==15 ) x = (u64)L << 3;
+        if( b==nb-1u && i==14 ) x = 0UL;
+        w[i] = x;
+      }
     }
     fd_sha512_block( h, w );
   }
