@@ -468,13 +468,13 @@ FD_DEV void fe_pack( u32 w[ 8 ], fe const & a ) {
   u32 h[10];
 #pragma unroll
   for( int i=0; i<10; i++ ) h[i] = a.v[i];
+  /* one carry pass: limbs 1-9 exact, h0 < 2^26 + 19 * 65, so h < 2^255 + 2^11 < 2p and the
+     quotient ripple below sees carries of 0 or 1 (a second pass here changed nothing: checked on
+     limbs up to 2^31 - 1 and on values around p, 2p and 2^255, against the value mod p) */
 #pragma unroll
-  for( int pass=0; pass<2; pass++ ) {
-#pragma unroll
-    for( int i=0; i<9; i++ ) { h[i+1] += h[i] >> FE_W(i); h[i] &= FE_M(i); }
-    h[0] += 19u * (h[9] >> 25); h[9] &= 0x1ffffffu;
-  }
-  /* now h < 2^255 + 2^26: subtract p iff h + 19 >= 2^255 */
+  for( int i=0; i<9; i++ ) { h[i+1] += h[i] >> FE_W(i); h[i] &= FE_M(i); }
+  h[0] += 19u * (h[9] >> 25); h[9] &= 0x1ffffffu;
+  /* subtract p iff h + 19 >= 2^255 */
   u32 q = (h[0] + 19u) >> 26;
 #pragma unroll
   for( int i=1; i<10; i++ ) q = (h[i] + q) >> FE_W(i);
