@@ -1,12 +1,14 @@
 #!/bin/bash
 # Interleaved A/B of engine builds on the headline bench (HBM-resident configs[1]):
 # tools/ab_bench.sh <reps> <name=lib-or-env>...   e.g. base= v1=build/ab/v1.so full=FDGPU_HALF=0
-# Each run prints one line: name value dsm prep.
+# Each run prints one line: name value dsm prep.  Reps alternate the order (ABBA).
 reps="$1"; shift
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 B="python3 bench.py --steps 10 --warmup 3 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
 for r in $(seq "$reps"); do
-  for spec in "$@"; do
+  # odd reps run the list forward, even reps backward (ABBA): an order effect cancels over pairs
+  if (( r % 2 )); then order=("$@"); else order=(); for (( i=$#; i>=1; i-- )); do order+=("${!i}"); done; fi
+  for spec in "${order[@]}"; do
     name="${spec%%=*}"; val="${spec#*=}"
     if [[ "$val" == *.so ]]; then envs="FDGPU_LIB=$val"; else envs="$val"; fi
     out=$(env $envs timeout -k 10 120 $B 2>/dev/null | tail -1)
