@@ -155,3 +155,26 @@ def test_half_size_no_silent_fallback(fa, path):
     assert eng.slow_count() == (nsig + 6) // 7
     eng.close()
     np.testing.assert_array_equal(t, expect)
+
+
+def test_message_lengths_at_sha512_block_edges(fa, oracle, engine_path):
+    """k = SHA-512(R || A || M) for inputs that end exactly at, just before and just after a 128-byte block
+    boundary, and where the 0x80 byte and the 16-byte length do or do not fit the last data block
+    (64 + msg_sz mod 128 around 0, 111 and 112): the full-block fast path of fd_sha512_RAM must give the
+    same codes as the oracle -- valid signatures verify, a flipped message bit gives ERR_MSG."""
+    sizes = sorted({max(0, L - 64) for b in range(0, 11) for d in (-1, 0, 1, 111, 112, 113)
+                    for L in (128 * b + d,) if L >= 64} | {0, 1, 2})
+    keys = _keys(oracle, len(sizes), seed=11)
+    rng = np.random.default_rng(12)
+    msgs, sigs, pubs, want = [], [], [], []
+    for (prv, pub), n in zip(keys, sizes):
+        m = rng.bytes(n)
+        sig = oracle.sign(m, pub, prv)
+        msgs.append(m); sigs.append(sig); pubs.append(pub); want.append(0)
+        if n:
+            f = bytearray(m); f[n // 2] ^= 1
+            msgs.append(bytes(f)); sigs.append(sig); pubs.append(pub); want.append(-3)
+    eng = fa.Engine(device=0, max_txn=len(msgs), max_sig=len(msgs), max_payload=len(msgs) * 1600 + 4096)
+    got = eng.verify_many(msgs, sigs, pubs)
+    eng.close()
+    np.testing.assert_array_equal(np.asarray(got), np.asarray(want))
