@@ -50,7 +50,8 @@ ROW = {"v_mad_u64_u32": "v_mad_u64_u32", "v_and_b32": "v_and_b32", "v_lshrrev_b6
        "v_readfirstlane_b32": "v_mov_b32", "v_lshl_or_b32": "v_lshl_add_u32", "v_and_or_b32": "v_lshl_add_u32",
        "v_add3_u32": "v_lshl_add_u32", "v_or3_b32": "v_lshl_add_u32", "v_max_i32": "v_add_u32",
        "v_sub_co_u32": "v_add_u32", "v_subb_co_u32": "v_add_u32", "v_ashrrev_i64": "v_lshrrev_b64",
-       "v_lshlrev_b64": "v_lshrrev_b64", "v_mul_hi_u32": "v_mul_lo_u32"}
+       "v_lshlrev_b64": "v_lshrrev_b64", "v_mul_hi_u32": "v_mul_lo_u32", "v_bfi_b32": "v_bfi_b32",
+       "v_perm_b32": "v_perm_b32", "v_alignbyte_b32": "v_alignbit_b32"}
 
 
 def parse_probe(path):

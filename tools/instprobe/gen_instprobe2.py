@@ -45,7 +45,7 @@ def body(kind):
     lines = []
     used = set()
     for c in range(CH):
-        if kind.startswith(("mad64", "lshladd64", "pkfma")):
+        if kind.startswith(("mad64", "lshladd64", "pkfma", "lshr64")):
             C = CHAIN0 + 2 * c                                  # pairs in banks {0,1} / {2,3} alternately
             cb = C % 4
             if kind.endswith("_same"):                          # sources in the accumulator's banks
@@ -56,6 +56,8 @@ def body(kind):
             if kind.startswith("mad64"):
                 sd = "vcc" if kind.startswith("mad64v") else f"s[{40 + 2 * (c % 8)}:{41 + 2 * (c % 8)}]"
                 lines.append(f"v_mad_u64_u32 {pair(C)}, {sd}, {reg(A)}, {reg(B)}, {pair(C)}")
+            elif kind.startswith("lshr64"):                     # the field carries (64-bit shift)
+                lines.append(f"v_lshrrev_b64 {pair(C)}, 26, {pair(C)}")
             elif kind.startswith("lshladd64"):
                 lines.append(f"v_lshl_add_u64 {pair(C)}, {pair(C)}, 1, {pair(min(A, B))}")
             else:                                               # packed f32 FMA on pairs
@@ -91,6 +93,13 @@ def body(kind):
             lines.append(f"v_bitop3_b32 {reg(C)}, {reg(C)}, {reg(A)}, {reg(B)} bitop3:0x96"); used |= {C, A, B}
         elif op == "mov":
             lines.append(f"v_mov_b32 {reg(C)}, {reg(A)}"); used |= {C, A}
+        elif op == "alignbit":                                  # SHA-512's 64-bit rotations (one half each)
+            lines.append(f"v_alignbit_b32 {reg(C)}, {reg(C)}, {reg(A)}, 13"); used |= {C, A}
+        elif op == "bfi":                                       # SHA-512's Ch
+            lines.append(f"v_bfi_b32 {reg(C)}, {reg(A)}, {reg(C)}, {reg(B)}"); used |= {C, A, B}
+        elif op == "perm":                                      # byte swaps of the message words
+            lines.append(f"v_perm_b32 {reg(C)}, {reg(C)}, {reg(A)}, {reg(B)}"); used |= {C, A, B}
+
         else:
             raise ValueError(kind)
     return lines, used
@@ -98,7 +107,8 @@ def body(kind):
 
 KINDS = ["fma_dist", "fma_same", "fma_dup", "fma_const", "addf_dist", "addf_same", "addf_const",
          "add_dist", "add_same", "add_const", "mullo_dist", "bitop3_dist", "bitop3_same", "mov_dist",
-         "pkfma_dist", "pkfma_same", "mad64s_dist", "mad64s_same", "mad64v_dist", "lshladd64_dist"]
+         "pkfma_dist", "pkfma_same", "mad64s_dist", "mad64s_same", "mad64v_dist", "lshladd64_dist",
+         "alignbit_dist", "bfi_dist", "perm_dist", "lshr64_dist"]
 
 
 def kernel(kind):
