@@ -6,8 +6,8 @@
    fd_sha512.c:265-398) over the AVX2 block core fd_sha512_core_avx2.S and
    the 4/8-lane AVX batch API (fd_sha512_batch_avx512.c).  Here every
    lane of a wave hashes its own signature's R||A||M: the 64-bit state
-   words are VGPR pairs, rotations are v_alignbit_b32 pairs, Ch is v_bfi_b32,
-   the 3-way xors and Maj are v_bitop3_b32.  The message is read straight from the transaction payload
+   words are VGPR pairs, rotations are v_alignbit_b32 pairs, Ch, Maj and
+   the 3-way xors are v_bitop3_b32.  The message is read straight from the transaction payload
    (arbitrary byte alignment) with dword loads + v_alignbyte_b32; padding
    and the length block are synthesised in registers. */
 
@@ -59,6 +59,13 @@ FD_DEV u64 fd_xor3_64( u64 x, u64 y, u64 z ) {
   return fd_mk64( __builtin_amdgcn_bitop3_b32( (u32)x, (u32)y, (u32)z, 0x96 ),
                   __builtin_amdgcn_bitop3_b32( (u32)(x>>32), (u32)(y>>32), (u32)(z>>32), 0x96 ) );
 }
+/* Ch(x, y, z) = x ? y : z as v_bitop3_b32 (truth table 0xca): the compiler's form is v_bfi_b32, which
+   issues at half rate on gfx950 (4.25 cycles per wave64 instruction against 2.22 for v_bitop3_b32,
+   profiles/r03/roofline/probe_r03b.txt) */
+FD_DEV u64 fd_ch64( u64 x, u64 y, u64 z ) {
+  return fd_mk64( __builtin_amdgcn_bitop3_b32( (u32)x, (u32)y, (u32)z, 0xca ),
+                  __builtin_amdgcn_bitop3_b32( (u32)(x>>32), (u32)(y>>32), (u32)(z>>32), 0xca ) );
+}
 FD_DEV u64 fd_maj64( u64 x, u64 y, u64 z ) {
   return fd_mk64( __builtin_amdgcn_bitop3_b32( (u32)x, (u32)y, (u32)z, 0xe8 ),
                   __builtin_amdgcn_bitop3_b32( (u32)(x>>32), (u32)(y>>32), (u32)(z>>32), 0xe8 ) );
@@ -105,7 +112,7 @@ FD_DEV void fd_load_words( u32 w[ N32 ], unsigned char const * p ) {
    at once (a fully unrolled block needed ~200 VGPRs). */
 #define FD_SHA512_ROUND( kt, wt ) do {                                              \
     u64 S1 = fd_xor3_64( fd_rotr64( e,14 ), fd_rotr64( e,18 ), fd_rotr64( e,41 ) ); \
-    u64 ch = g ^ ( e & ( f ^ g ) );                                                 \
+    u64 ch = fd_ch64( e, f, g );                                                    \
     u64 t1 = hh + S1 + ch + (kt) + (wt);                                            \
     u64 S0 = fd_xor3_64( fd_rotr64( a,28 ), fd_rotr64( a,34 ), fd_rotr64( a,39 ) ); \
     u64 mj = fd_maj64( a, b, c );                                                   \
