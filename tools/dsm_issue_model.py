@@ -44,12 +44,12 @@ ROW = {"v_mad_u64_u32": "v_mad_u64_u32", "v_and_b32": "v_and_b32", "v_lshrrev_b6
        "v_mov_b32": "v_mov_b32", "v_mad_u32_u24": "v_mad_u32_u24", "v_lshrrev_b32": "v_lshrrev_b32",
        "v_cndmask_b32": "v_cmp+v_cndmask", "v_lshl_add_u32": "v_lshl_add_u32", "v_bitop3_b32": "v_bitop3_b32",
        "v_mul_u32_u24": "v_mul_u32_u24", "v_or_b32": "v_and_b32", "v_xor_b32": "v_and_b32",
-       "v_subrev_u32": "v_sub_u32", "v_add_co_u32": "v_add_u32", "v_addc_co_u32": "v_add_u32",
+       "v_subrev_u32": "v_sub_u32", "v_add_co_u32": "v_add_co_u32", "v_addc_co_u32": "v_add_co_u32",
        "v_cmp_gt_i32": "v_add_u32", "v_cmp_lt_i32": "v_add_u32", "v_cmp_eq_u32": "v_add_u32",
        "v_cmp_ne_u32": "v_add_u32", "v_ashrrev_i32": "v_lshrrev_b32", "v_bfe_u32": "v_alignbit_b32",
-       "v_readfirstlane_b32": "v_mov_b32", "v_lshl_or_b32": "v_lshl_add_u32", "v_and_or_b32": "v_lshl_add_u32",
-       "v_add3_u32": "v_lshl_add_u32", "v_or3_b32": "v_lshl_add_u32", "v_max_i32": "v_add_u32",
-       "v_sub_co_u32": "v_add_u32", "v_subb_co_u32": "v_add_u32", "v_ashrrev_i64": "v_lshrrev_b64",
+       "v_readfirstlane_b32": "v_mov_b32", "v_lshl_or_b32": "v_lshl_or_b32", "v_and_or_b32": "v_add3_u32",
+       "v_add3_u32": "v_add3_u32", "v_or3_b32": "v_add3_u32", "v_max_i32": "v_add_u32",
+       "v_sub_co_u32": "v_add_co_u32", "v_subb_co_u32": "v_add_co_u32", "v_ashrrev_i64": "v_lshrrev_b64",
        "v_lshlrev_b64": "v_lshrrev_b64", "v_mul_hi_u32": "v_mul_lo_u32", "v_bfi_b32": "v_bfi_b32",
        "v_perm_b32": "v_perm_b32", "v_alignbyte_b32": "v_alignbit_b32"}
 

@@ -93,6 +93,16 @@ def body(kind):
             lines.append(f"v_bitop3_b32 {reg(C)}, {reg(C)}, {reg(A)}, {reg(B)} bitop3:0x96"); used |= {C, A, B}
         elif op == "mov":
             lines.append(f"v_mov_b32 {reg(C)}, {reg(A)}"); used |= {C, A}
+        elif op == "lshr32":
+            lines.append(f"v_lshrrev_b32 {reg(C)}, 13, {reg(C)}"); used |= {C}
+        elif op == "lshlor":
+            lines.append(f"v_lshl_or_b32 {reg(C)}, {reg(C)}, 3, {reg(A)}"); used |= {C, A}
+        elif op == "lshladd32":
+            lines.append(f"v_lshl_add_u32 {reg(C)}, {reg(C)}, 3, {reg(A)}"); used |= {C, A}
+        elif op == "cndmask":
+            lines.append(f"v_cndmask_b32 {reg(C)}, {reg(C)}, {reg(A)}, vcc"); used |= {C, A}
+        elif op == "addco":
+            lines.append(f"v_add_co_u32 {reg(C)}, vcc, {reg(A)}, {reg(C)}"); used |= {C, A}
         elif op == "alignbit":                                  # SHA-512's 64-bit rotations (one half each)
             lines.append(f"v_alignbit_b32 {reg(C)}, {reg(C)}, {reg(A)}, 13"); used |= {C, A}
         elif op == "bfi":                                       # SHA-512's Ch
@@ -108,7 +118,8 @@ def body(kind):
 KINDS = ["fma_dist", "fma_same", "fma_dup", "fma_const", "addf_dist", "addf_same", "addf_const",
          "add_dist", "add_same", "add_const", "mullo_dist", "bitop3_dist", "bitop3_same", "mov_dist",
          "pkfma_dist", "pkfma_same", "mad64s_dist", "mad64s_same", "mad64v_dist", "lshladd64_dist",
-         "alignbit_dist", "bfi_dist", "perm_dist", "lshr64_dist"]
+         "alignbit_dist", "bfi_dist", "perm_dist", "lshr64_dist", "lshr32_dist", "lshlor_dist", "lshladd32_dist",
+         "cndmask_dist", "addco_dist"]
 
 
 def kernel(kind):
