@@ -775,7 +775,7 @@ def main():
                          "valu_busy": valu_busy,
                          "valu_busy_source": "profiles/dsm_pmc.json: issue cycles of the walk kernel's ISA priced at "
                                              "the measured per-instruction costs (tools/dsm_issue_model.py, "
-                                             "profiles/r03/roofline/issue_model_dsmh.json) / measured kernel cycles",
+                                             "profiles/r03/roofline/issue_model_dsmh_r03c.json, every row measured) / measured kernel cycles",
                          # the same kernel against the HBM roofline: PMC bytes per launch / this run's launch time
                          "hbm": ({"achieved": traffic * nsig / (1 << 20) / (dom_ms * 1e-3) / 1e9, "peak": 8000.0,
                                   "unit": "GB/s",

@@ -78,8 +78,10 @@ if os.path.exists(blog):
 dk = next((k for k in DSM if k in out), None)
 d = out.get(dk)
 if d and "hbm_read_bytes" in d:
-    im = os.path.join(os.path.dirname(dst.rstrip("/")), "roofline",
-                      "issue_model_dsmh.json" if dk.startswith("fd_dsmh") else "issue_model.json")
+    rd = os.path.join(os.path.dirname(dst.rstrip("/")), "roofline")
+    im = os.path.join(rd, "issue_model_dsmh_r03c.json")      # the model priced with every measured row
+    if not dk.startswith("fd_dsmh") or not os.path.exists(im):
+        im = os.path.join(rd, "issue_model_dsmh.json" if dk.startswith("fd_dsmh") else "issue_model.json")
     busy = json.load(open(im))["valu_busy_model"] if os.path.exists(im) else None
     json.dump({"kernel": dk, "source": dst,
                "hbm_bytes_per_launch": d["hbm_read_bytes"] + d.get("hbm_write_bytes", 0),
