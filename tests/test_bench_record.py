@@ -1,0 +1,120 @@
+"""CPU: bench.py's driver contract -- the compact headline line (<= 4 KB, last on stdout, the keys the
+driver reads) built from a canned full record of the size round 3's grew to, and `--gpus N` starting N
+ranks itself (gloo on CPU, GPU legs stubbed by --dry-run)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def _leg(rate):
+    return {"tiles": 2, "gpus": 8, "reliable": False, "rate_fps": rate, "frags": 10 ** 8, "verdicts": 10 ** 8, "lost": 0,
+            "overruns_at_verdict": 0, "p50_us": 512.123456, "p99_us": 812.987654, "max_us": 1999.1,
+            "published": 10 ** 8, "metrics": [0, 0, 0, 0, 10 ** 8], "tile_host_ns_per_frag": [30.8, 46.7, 10.9, 92.3],
+            "sigs_per_s": rate, "frags_per_s": rate, "batch_limit": 8192, "offered_frags_per_s_per_gpu": rate,
+            "padding": "x" * 1500}
+
+
+def canned_full(n_gpus=8):
+    curve = [_leg(r) for r in (2e6, 5e6, 7.5e6, 10e6, 15e6)]
+    return {
+        "metric": "ed25519 verified sigs/sec at 1/8 MI355X vs host AVX-512; p99 batch latency",
+        "value": 8.3e8, "unit": "sigs/s", "n_gpus": n_gpus, "steps": 20, "warmup": 5, "ms_per_step": 10.1,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (fd_benchg large_noop layout, seeded ed25519 keys/signatures)",
+        "config": {"workload": "BASELINE configs[1]: 1M single-sig 1232-byte synthetic Solana txns, all valid",
+                   "txns_per_gpu": 1 << 20, "sigs_per_gpu": 1 << 20, "signed_msg_bytes": 1167,
+                   "parallelism": "independent per-GPU shards x8", "semantics": "avx512", "contexts_per_gpu": 1},
+        "results_ok": True, "kernel_ms": {"prep": 3.9123456, "dsm": 6.7298765, "reduce": 0.05},
+        "roofline": {"bound": "valu", "achieved": 15000.123, "peak": 31400.0, "unit": "GMAC/s", "frac": 0.4777,
+                     "traffic": 10.1e9, "kernel": "fd_dsmh_kernel<1>", "mac_per_sig": 96256,
+                     "frac_ref_equiv": 0.56, "peak_guide": 39321.6, "frac_guide": 0.3815,
+                     "frac_guide_fullrate": 0.19, "valu_busy": 0.99, "work_per_sig": "y" * 300,
+                     "hbm": {"frac": 0.2}},
+        "cpu_baseline": {"value": 900457.2, "unit": "sigs/s", "cores": 16, "kind": "reference",
+                         "sample": "first 1048576 txns (1048576 sigs) of the same 1232-byte workload, 16 threads, "
+                                   "1.16 s wall; host CPU: AMD EPYC 9575F 64-Core Processor",
+                         "sweep_configs0": {"points": [{"threads": t, "sigs_per_s": 59000.0 * t, "sigs": 65536}
+                                                       for t in (1, 2, 4, 8, 16)]}},
+        "per_gpu": [{"rank": r, "dsm_ms": 6.7, "prep_ms": 3.9, "achieved_gmac_s": 15000.0, "peak_gmac_s": 31400.0,
+                     "frac": 0.4777123, "frac_guide": 0.3815123, "sigs_per_s": 1.04e8} for r in range(n_gpus)],
+        "latency": {"batch_txns": 8192, "p50_ms": 0.64, "p99_ms": 0.66, "device_p99_ms": 0.33, "pinned_p99_ms": 0.55,
+                    "dropin_call_p99_us": 379.5, "path": "z" * 500},
+        "host_staged": {"sigs_per_s": 3.97e7, "roofline": {"x": "w" * 400}},
+        "stream": {"sigs_per_s": 1.7e8, "n_gpus": n_gpus, "tiles_per_gpu": 2, "max_rate": curve[0], "paced": curve[0],
+                   "latency_curve": curve, "knee": {"frags_per_s_per_gpu": 7.5e6}, "unreliable_max": curve[0],
+                   "unreliable_goodput_vs_max": 0.86, "all_published": True},
+        "extra_configs": {"configs0_small_msg_200B": {"sigs_per_s": 9.5e7, "results_ok": True},
+                          "configs2_adversarial_10pct": {"sigs_per_s": 1.06e8, "results_ok": True},
+                          "configs3_multisig_1to12": {"sigs_per_s": 9.9e7, "results_ok": True}},
+        "headline_two_contexts": {"sigs_per_s": 1.07e8},
+    }
+
+
+def test_compact_line_fits_and_carries_the_contract(tmp_path):
+    full = canned_full()
+    assert len(json.dumps(full)) > 15000            # the round-3 size that the driver could not parse
+    detail = str(tmp_path / "d" / "bench_detail.json")
+    line = bench.emit_record(full, detail)
+    assert len(line) <= bench.HEADLINE_MAX_BYTES and "\n" not in line
+    rec = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "results_ok", "kernel_ms", "roofline", "cpu_baseline"):
+        assert k in rec, k
+    assert rec["value"] == full["value"] and rec["n_gpus"] == 8
+    rf = rec["roofline"]
+    assert rf["frac"] == pytest.approx(0.3815, rel=1e-3) and rf["frac_live"] == pytest.approx(0.4777, rel=1e-3)
+    assert rf["peak"] == pytest.approx(39321.6, rel=1e-3) and rf["traffic"] == 10.1e9
+    assert rec["cpu_baseline"]["cores"] == 16 and rec["cpu_baseline"]["kind"] == "reference"
+    assert len(rec["per_gpu"]) == 8
+    assert rec["stream"]["knee"] == 7.5e6 and len(rec["stream"]["paced_fps_p50_p99_us"]) == 5
+    assert json.load(open(detail)) == full          # the detail file keeps everything
+
+
+def test_oversized_summaries_are_dropped_not_the_headline(tmp_path):
+    full = canned_full(n_gpus=8)
+    full["stream"] = {"error": "e" * 10000}
+    full["per_gpu"] = full["per_gpu"] * 40            # absurdly many rows
+    line = bench.emit_record(full, None)
+    rec = json.loads(line)
+    assert len(line) <= bench.HEADLINE_MAX_BYTES
+    assert rec["roofline"]["frac"] and rec["cpu_baseline"]["value"]
+
+
+@pytest.mark.parametrize("n", [2])
+def test_gpus_n_starts_n_ranks(tmp_path, n):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    detail = str(tmp_path / "detail.json")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(n), "--steps", "3", "--warmup",
+                        "1", "--txns", "1000", "--dry-run", "--detail-out", detail],
+                       capture_output=True, text=True, timeout=180, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    rec = json.loads(lines[-1])
+    assert rec["n_gpus"] == n and [row[0] for row in rec["per_gpu"]] == list(range(n))
+    # rank 1 sleeps 4 ms per step: the value is all ranks' units over the slowest rank's time
+    assert rec["ms_per_step"] >= 4.0
+    assert rec["value"] == pytest.approx(n * 1000 * 1e3 / rec["ms_per_step"], rel=1e-6)
+
+
+def test_gpus_mismatch_refused():
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_failed_rank_takes_the_others_down(tmp_path):
+    stub = tmp_path / "stub.py"
+    stub.write_text("import os, sys, time\n"
+                    "sys.exit(3) if os.environ['RANK'] == '1' else time.sleep(600)\n")
+    import time
+    t0 = time.time()
+    rc = bench.launch_ranks(2, [], script=str(stub), timeout_s=120)
+    assert rc == 3 and time.time() - t0 < 60

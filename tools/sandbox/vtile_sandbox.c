@@ -227,7 +227,7 @@ run_batch( fdgpu_vtile_t * vt, fdgpu_mcache_t * mc, uchar * dcache, uchar const 
     ulong ts = now_ns();
     fdgpu_mcache_publish( mc, seq0 + i, 0UL, (unsigned)chunk, (unsigned)sz, ts, ts );
     int rc;
-    while( ( rc = fdgpu_vtile_during_frag( vt, rec, sz, seq0 + i, ts ) ) == -2 ) {
+    while( ( rc = fdgpu_vtile_during_frag( vt, 0UL, rec, sz, seq0 + i, ts ) ) == -2 ) {
       fdgpu_vtile_done_t d[ 64 ];
       ulong k = fdgpu_vtile_after_frags( vt, d, 64, 1 );
       for( ulong j=0; j<k; j++ ) *published += d[j].result == FDGPU_VTILE_PUBLISH;
