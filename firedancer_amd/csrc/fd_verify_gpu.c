@@ -191,8 +191,9 @@ typedef struct {
 struct fdgpu_mcache {
   ulong       depth;
   mc_line_t * line;
-  int         own;          /* line[] allocated here (else it lives in a shared link) */
-  int         reg;          /* line[] registered with the GPU here (fdgpu_vtile_set_in_links) */
+  int         own;          /* line[] allocated here (else it lives in a shared link or the caller's mcache) */
+  int         reg;          /* registered with the GPU here (fdgpu_vtile_set_in_links), from reg_base */
+  void *      reg_base;
 };
 
 /* bytes of an mcache's lines, whole pages (page-aligned line arrays can be
@@ -217,9 +218,24 @@ fdgpu_mcache_new( ulong depth, ulong seq0 ) {
   return mc;
 }
 
+/* an existing fd_frag_meta_t ring (fd_mcache_join's return, src/tango/mcache/fd_mcache.h:113,137; line
+   layout src/tango/fd_tango_base.h:146-203, the same 32 bytes as mc_line_t): no copy, nothing written.
+   Line of seq = seq & (depth-1), FD_MCACHE_LG_INTERLEAVE 0 (fd_mcache.h:265-272) */
+fdgpu_mcache_t *
+fdgpu_mcache_wrap( void * lines, ulong depth ) {
+  if( !lines || !depth || (depth & (depth - 1UL)) || ( (ulong)lines & 31UL ) ) return NULL;
+  fdgpu_mcache_t * mc = (fdgpu_mcache_t *)calloc( 1, sizeof(fdgpu_mcache_t) );
+  if( !mc ) return NULL;
+  mc->depth = depth; mc->line = (mc_line_t *)lines; mc->own = 0;
+  return mc;
+}
+
+ulong fdgpu_mcache_depth( fdgpu_mcache_t const * mc ) { return mc->depth; }
+void * fdgpu_mcache_lines( fdgpu_mcache_t * mc ) { return (void *)mc->line; }
+
 void fdgpu_mcache_delete( fdgpu_mcache_t * mc ) {
   if( !mc ) return;
-  if( mc->reg ) fdgpu_host_unregister( mc->line );
+  if( mc->reg ) fdgpu_host_unregister( mc->reg_base );
   if( mc->own ) free( mc->line );
   free( mc );
 }
@@ -256,6 +272,14 @@ int
 fdgpu_mcache_poll( fdgpu_mcache_t const * mc, ulong seq, fdgpu_frag_meta_t * out ) {
   ulong found;
   return mc_poll( &mc->line[ seq & (mc->depth - 1UL) ], seq, out, &found );
+}
+
+int
+fdgpu_mcache_query( fdgpu_mcache_t const * mc, ulong seq, fdgpu_frag_meta_t * out, ulong * seq_found ) {
+  ulong found;
+  int r = mc_poll( &mc->line[ seq & (mc->depth - 1UL) ], seq, out, &found );
+  if( seq_found ) *seq_found = found;
+  return r;
 }
 
 /* fd_frag_meta_ts_decomp: the full timestamp nearest to now whose low 32
@@ -303,12 +327,13 @@ vt_fence( void ) {
 #define VT_RESERVE_MAX ( FDGPU_TXNM_HDR_SZ + 1232UL + 2UL + 852UL )   /* header + MTU payload + fd_txn_t */
 
 typedef struct {
-  ulong seq, tsorig, chunk;
+  ulong seq, tsorig, chunk;              /* seq: the frag's full 64-bit seq on its in link */
   ulong bundle_id;                       /* from the frag header, read in during_frag */
   ulong cidx;                            /* zero-copy: the frag's index among context k's gathered submissions */
   unsigned short payload_sz;
   int   k;                               /* engine context the frag's batch went to */
   int   ovr;                             /* the caller's seq re-check failed after during_frag's host copy */
+  int   in_idx;                          /* the in link it came from (the stem's in_idx) */
 } vt_pend_t;
 
 /* Engine contexts per tile (fdgpu_vtile_opts_t.nctx, 1..VT_NCTX_MAX, default 2).
@@ -359,6 +384,10 @@ struct fdgpu_vtile {
   uchar const *         in_mc_dev[ FDGPU_VTILE_IN_MAX ];   /* device view of each in link's mcache lines (or NULL) */
   uchar const *         src_lo, * src_hi, * src_dev;       /* the registered region the last frag came from */
   int                   n_in;
+  /* the tile's in links as the stem numbers them (fdgpu_vtile_set_in): kind and data region */
+  int                   in_kind[ FDGPU_VTILE_IN_MAX ];
+  uchar const *         in_mem[ FDGPU_VTILE_IN_MAX ];
+  ulong                 in_chunk0[ FDGPU_VTILE_IN_MAX ], in_wmark[ FDGPU_VTILE_IN_MAX ];
   ulong                 overruns;
   /* poll scratch */
   ulong                 batch;
@@ -567,8 +596,10 @@ fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_
   for( int i=0; i<n; i++ ) {
     fdgpu_mcache_t * mc = (fdgpu_mcache_t *)in_mc[i];
     if( !mc || fdgpu_host_dev_ptr( mc->line, mc->depth * sizeof(mc_line_t) ) ) continue;
-    if( fdgpu_host_register( mc->line, mc_bytes( mc->depth ) ) ) return -2;
-    mc->reg = 1;
+    /* the lines' whole pages (an fd_mcache's lines start 256 bytes into its region, not on a page) */
+    ulong lo = (ulong)mc->line & ~4095UL, hi = ( (ulong)mc->line + mc->depth * sizeof(mc_line_t) + 4095UL ) & ~4095UL;
+    if( fdgpu_host_register( (void *)lo, hi - lo ) ) return -2;
+    mc->reg = 1; mc->reg_base = (void *)lo;
   }
   vt->zc = 1; vt->n_in = n;
   for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) {
@@ -584,8 +615,8 @@ fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_
 
 /* a frag's copy has completed (or it left the pipeline without one) */
 static inline void vt_copied( fdgpu_vtile_t * vt, vt_pend_t const * p ) {
-  int l = FDGPU_VTILE_SEQ_LINK( p->seq );
-  vt->uncopied[l]--; vt->uncopied_tot--; vt->copied_next[l] = FDGPU_VTILE_SEQ_SEQ( p->seq ) + 1UL;
+  int l = p->in_idx;
+  vt->uncopied[l]--; vt->uncopied_tot--; vt->copied_next[l] = p->seq + 1UL;
 }
 
 /* an early copy of context k was launched (for its latency metric) */
@@ -644,8 +675,11 @@ fdgpu_vtile_copy_state( fdgpu_vtile_t const * vt, int link, ulong * copied_next 
 }
 
 ulong
-fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt ) {
-  return vt->pend_head < vt->pend_tail ? vt->pend[ vt->pend_head % vt->pend_cap ].seq : ~0UL;
+fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt, ulong * in_idx ) {
+  if( vt->pend_head >= vt->pend_tail ) { if( in_idx ) *in_idx = ~0UL; return ~0UL; }
+  vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
+  if( in_idx ) *in_idx = (ulong)p->in_idx;
+  return p->seq;
 }
 
 /* launch decision of housekeep: 1 if context f's filling batch should go now */
@@ -721,12 +755,12 @@ vt_room( fdgpu_vtile_t * vt ) {
 
 /* the frag whose record is (or will be, gathered) at the out dcache's out_chunk was submitted */
 static void
-vt_taken( fdgpu_vtile_t * vt, ulong seq, ulong tsorig, ulong bundle_id, unsigned short payload_sz ) {
+vt_taken( fdgpu_vtile_t * vt, int in_idx, ulong seq, ulong tsorig, ulong bundle_id, unsigned short payload_sz ) {
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
-  p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill; p->ovr = 0;
+  p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill; p->ovr = 0; p->in_idx = in_idx;
   if( vt->zc ) {
     p->cidx = vt->sub_cnt[ vt->fill ]++;
-    vt->uncopied[ FDGPU_VTILE_SEQ_LINK( seq ) ]++; vt->uncopied_tot++;
+    vt->uncopied[ in_idx ]++; vt->uncopied_tot++;
     if( !vt->copy_t0 ) vt->copy_t0 = now_ns();
   }
   if( vt->min_batch ) {                          /* first frag of the filling batch: its wait starts */
@@ -746,18 +780,21 @@ vt_submit_host_record( fdgpu_vtile_t * vt, uchar * dst, unsigned short payload_s
     return fdgpu_ed25519_submit_raw_gather_chk( vt->ctx[ vt->fill ], dst, vt->dcache, dst,
                                                 (unsigned short)( FDGPU_TXNM_HDR_SZ + payload_sz ),
                                                 (unsigned short)FDGPU_TXNM_HDR_SZ, payload_sz, vt->pend_tail, NULL,
-                                                FDGPU_VTILE_SEQ_SEQ( seq ) );
+                                                seq );
   return fdgpu_ed25519_submit_raw_ref( vt->ctx[ vt->fill ], vt->dcache, dst + FDGPU_TXNM_HDR_SZ, payload_sz, vt->pend_tail );
 }
 
-int
-fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
+static int vt_during_gossip( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong seq, ulong tsorig );
+
+/* during_frag of an fd_txn_m_t record (QUIC, bundle and send in links) */
+static int
+vt_during_txnm( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
   fdgpu_txnm_t const * in = (fdgpu_txnm_t const *)frag;
-  /* fd_verify_tile.c:78-85: the frag must hold its header + payload and
-     the payload must fit the MTU (the reference FD_LOG_ERRs) */
-  if( sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U || FDGPU_TXNM_HDR_SZ + in->payload_sz > sz ) return -4;
-  int link = FDGPU_VTILE_SEQ_LINK( seq );
-  if( link >= FDGPU_VTILE_IN_MAX || ( vt->zc && link >= vt->n_in ) ) return -4;   /* a link set_in_links was not told about */
+  /* fd_verify_tile.c:75-85: the frag fits FD_TPU_RAW_MTU, holds its header + payload and the payload fits
+     the MTU (the reference FD_LOG_ERRs) */
+  if( sz > FDGPU_TPU_RAW_MTU || sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U || FDGPU_TXNM_HDR_SZ + in->payload_sz > sz )
+    return -4;
+  if( vt->zc && link >= vt->n_in ) return -4;            /* a link the zero-copy intake was not told about */
   int rc = vt_room( vt );
   if( rc ) return rc;
   if( vt->zc && vt->uncopied_tot >= vt->opt.max_uncopied ) {   /* copy backlog: start the copies, take nothing */
@@ -777,7 +814,7 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
     ulong const * seq_dev = NULL;
     if( mc ) {
       if( !vt->in_mc_dev[ link ] ) return -3;
-      ulong li = FDGPU_VTILE_SEQ_SEQ( seq ) & ( mc->depth - 1UL );
+      ulong li = seq & ( mc->depth - 1UL );
       seq_dev = (ulong const *)( vt->in_mc_dev[ link ] + ( (uchar const *)&mc->line[ li ].seq - (uchar const *)mc->line ) );
     }
     uchar const * src = (uchar const *)frag;
@@ -791,13 +828,39 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, ulong sz, ulong 
     rc = fdgpu_ed25519_submit_raw_gather_dev( vt->ctx[ vt->fill ], src, vt->src_dev + ( src - vt->src_lo ), vt->dcache, dst,
                                               (unsigned short)( FDGPU_TXNM_HDR_SZ + in->payload_sz ),
                                               (unsigned short)FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail,
-                                              seq_dev, FDGPU_VTILE_SEQ_SEQ( seq ) );
+                                              seq_dev, seq );
   } else {
     vt_copy( dst, (uchar const *)frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
     rc = vt_submit_host_record( vt, dst, in->payload_sz, seq );
   }
   if( rc ) return rc;
-  vt_taken( vt, seq, tsorig, in->bundle_id, in->payload_sz );
+  vt_taken( vt, link, seq, tsorig, in->bundle_id, in->payload_sz );
+  return 0;
+}
+
+int
+fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, ulong in_idx, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
+  if( in_idx >= FDGPU_VTILE_IN_MAX ) return -4;
+  if( vt->in_kind[ in_idx ] == FDGPU_VTILE_IN_KIND_GOSSIP ) return vt_during_gossip( vt, (int)in_idx, frag, sz, seq, tsorig );
+  return vt_during_txnm( vt, (int)in_idx, frag, sz, seq, tsorig );
+}
+
+int
+fdgpu_vtile_during_frag_chunk( fdgpu_vtile_t * vt, ulong in_idx, ulong seq, ulong sig, ulong chunk, ulong sz, ulong ctl,
+                               ulong tsorig ) {
+  (void)sig; (void)ctl;
+  if( in_idx >= FDGPU_VTILE_IN_MAX || !vt->in_mem[ in_idx ] ) return -4;
+  /* fd_verify_tile.c:75-76,89-90: a chunk outside the link's [chunk0, wmark] is corrupt (FD_LOG_ERR) */
+  if( chunk < vt->in_chunk0[ in_idx ] || chunk > vt->in_wmark[ in_idx ] ) return -4;
+  return fdgpu_vtile_during_frag( vt, in_idx, vt->in_mem[ in_idx ] + chunk * FDGPU_CHUNK_SZ, sz, seq, tsorig );
+}
+
+int
+fdgpu_vtile_set_in( fdgpu_vtile_t * vt, ulong in_idx, int in_kind, void const * mem, ulong chunk0, ulong wmark ) {
+  if( in_idx >= FDGPU_VTILE_IN_MAX || in_kind < FDGPU_VTILE_IN_KIND_QUIC || in_kind > FDGPU_VTILE_IN_KIND_SEND ) return -1;
+  if( vt->pend_tail != vt->pend_head ) return -1;       /* only while idle */
+  vt->in_kind[ in_idx ] = in_kind;
+  vt->in_mem[ in_idx ] = (uchar const *)mem; vt->in_chunk0[ in_idx ] = chunk0; vt->in_wmark[ in_idx ] = wmark;
   return 0;
 }
 
@@ -813,9 +876,10 @@ fdgpu_vtile_set_round_robin( fdgpu_vtile_t * vt, ulong idx, ulong cnt ) {
 }
 
 int
-fdgpu_vtile_before_frag( fdgpu_vtile_t const * vt, int in_kind, ulong seq, ulong sig ) {
+fdgpu_vtile_before_frag( fdgpu_vtile_t const * vt, ulong in_idx, ulong seq, ulong sig ) {
+  if( in_idx >= FDGPU_VTILE_IN_MAX ) return 1;
+  int in_kind = vt->in_kind[ in_idx ];
   ulong cnt = vt->rr_cnt ? vt->rr_cnt : 1UL;
-  seq = FDGPU_VTILE_SEQ_SEQ( seq );
   int is_bundle_packet = in_kind==FDGPU_VTILE_IN_KIND_BUNDLE && !sig;
   if( is_bundle_packet || in_kind==FDGPU_VTILE_IN_KIND_QUIC ) return ( seq % cnt ) != vt->rr_idx;
   if( in_kind==FDGPU_VTILE_IN_KIND_BUNDLE ) return vt->rr_idx != 0UL;
@@ -831,20 +895,14 @@ fdgpu_vtile_before_frag( fdgpu_vtile_t const * vt, int in_kind, ulong seq, ulong
    is reliable in the reference topology, topology.c:591, so there is no
    overrun to check).  The reference leaves the record's other header
    fields as the chunk's previous frag left them; here they are zero. */
-int
-fdgpu_vtile_during_frag_kind( fdgpu_vtile_t * vt, int in_kind, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
-  if( in_kind != FDGPU_VTILE_IN_KIND_GOSSIP ) {
-    if( sz > FDGPU_TPU_RAW_MTU ) return -4;                      /* fd_verify_tile.c:75-76 */
-    return fdgpu_vtile_during_frag( vt, frag, sz, seq, tsorig );
-  }
+static int
+vt_during_gossip( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
   if( sz > FDGPU_GOSSIP_MSG_MAX || sz < FDGPU_GOSSIP_VOTE_TXN_OFF ) return -4;   /* :89-90 */
   uchar const * msg = (uchar const *)frag;
   ulong txn_sz; memcpy( &txn_sz, msg + FDGPU_GOSSIP_VOTE_TXN_SZ_OFF, sizeof(ulong) );
   /* the reference copies vote.txn_sz bytes out of the 1232-byte vote.txn array unchecked; past the array
      (or past the frag) there is nothing defined to copy: refused as corrupt */
   if( txn_sz > 1232UL || FDGPU_GOSSIP_VOTE_TXN_OFF + txn_sz > sz ) return -4;
-  int link = FDGPU_VTILE_SEQ_LINK( seq );
-  if( link >= FDGPU_VTILE_IN_MAX ) return -4;
   int rc = vt_room( vt );
   if( rc ) return rc;
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
@@ -856,7 +914,7 @@ fdgpu_vtile_during_frag_kind( fdgpu_vtile_t * vt, int in_kind, void const * frag
   vt_fence();
   rc = vt_submit_host_record( vt, dst, (unsigned short)txn_sz, seq );
   if( rc ) return rc;
-  vt_taken( vt, seq, tsorig, 0UL, (unsigned short)txn_sz );
+  vt_taken( vt, link, seq, tsorig, 0UL, (unsigned short)txn_sz );
   return 0;
 }
 
@@ -875,7 +933,7 @@ fdgpu_vtile_during_frag_overrun( fdgpu_vtile_t * vt ) {
 static int
 vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, unsigned fp, ulong tag,
           fdgpu_vtile_done_t * d ) {
-  d->seq = p->seq; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
+  d->seq = p->seq; d->in_idx = (ulong)p->in_idx; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
   /* zero-copy: the GPU re-read the frag's mcache line right after copying it and found it reused
      -- the stem's "overrun while reading" (fd_stem.c:667-686), decided at copy time: the frag
      never reaches after_frag in the reference, so no bundle state or metric changes */
@@ -943,7 +1001,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
       for( ulong i=0; i<want; i++ ) {
         vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
         fdgpu_vtile_done_t * d = &out[n];
-        d->seq = p->seq; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
+        d->seq = p->seq; d->in_idx = (ulong)p->in_idx; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
         d->result = FDGPU_VTILE_GPU_FAULT;
         vt->gm.gpu_fault_frags++;
         vt_pop( vt, p ); n++;
@@ -1007,7 +1065,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
    on its link) lose nothing; unreliable ones never wait and a tile that
    falls a lap behind on a link is overrun: it resumes at the seq it found
    (fd_stem.c:590-596, 676-688) and the frags it skipped are counted.  A
-   frag's seq as the tile hands it on carries its link (FDGPU_VTILE_SEQ). */
+   frag goes to during_frag with its link as in_idx and its own seq. */
 
 #define LINK_MAGIC    0xfd6e11c0ffee0004UL
 #define LINK_TILE_MAX 64
@@ -1239,7 +1297,7 @@ link_trace( fdgpu_link_t * l, int idx, fdgpu_vtile_t * vt, fdgpu_vtile_done_t co
   uchar const * out = fdgpu_vtile_out_dcache( vt );
   for( ulong i=0; i<n && l->trace_cnt[idx] < l->trace_cap; i++ ) {
     fdgpu_link_trace_t * e = &t[ l->trace_cnt[idx]++ ];
-    e->seq = d[i].seq; e->tag = d[i].tag; e->result = d[i].result; e->rec_sz = (unsigned)d[i].sz;
+    e->seq = d[i].seq; e->in_idx = d[i].in_idx; e->tag = d[i].tag; e->result = d[i].result; e->rec_sz = (unsigned)d[i].sz;
     e->rec_hash = 0UL;
     if( d[i].result == FDGPU_VTILE_PUBLISH && d[i].sz <= VT_RESERVE_MAX ) {
       uchar rec[ VT_RESERVE_MAX ];
@@ -1445,8 +1503,8 @@ link_account( fdgpu_link_t * l, fdgpu_vtile_done_t const * d, ulong n, ulong * s
     ulong lat = t - d[i].tsorig;
     lh[ lh_idx( lat ) ]++;
     if( lat > *lmax ) *lmax = lat;
-    int q = FDGPU_VTILE_SEQ_LINK( d[i].seq );        /* < Q: the tile handed it over with its link */
-    ulong s = FDGPU_VTILE_SEQ_SEQ( d[i].seq );
+    int q = (int)d[i].in_idx;                      /* < Q: the tile handed it over with its link */
+    ulong s = d[i].seq;
     in[q].fin++;
     if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL )
       *sigs += l->psig[ ( s * Q + (ulong)q ) % np ];
@@ -1548,7 +1606,7 @@ static void * link_tile( void * _a ) {
           li->seq = found < li->n ? found : li->n;
           continue;
         }
-        int rc = fdgpu_vtile_during_frag( vt, l->dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, FDGPU_VTILE_SEQ( q, own ),
+        int rc = fdgpu_vtile_during_frag( vt, q, l->dcache + (ulong)m.chunk * FDGPU_CHUNK_SZ, m.sz, own,
                                           ts_decomp( m.tsorig, t0 ) );   /* the pass's start is "now" to 2^31 ns */
         PROF_ADD( 1 );
         if( rc == -2 ) { drain = 1; li->seq = own; break; }         /* staging full: drain, retry this seq */

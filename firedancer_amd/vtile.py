@@ -17,22 +17,20 @@ CHUNK_SZ = 64
 PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL, OVERRUN, GPU_FAULT = range(7)
 IN_QUIC, IN_BUNDLE, IN_GOSSIP, IN_SEND = range(4)        # fd_verify_tile.c:7-10
 
-
-def FDGPU_VTILE_SEQ(link: int, seq: int) -> int:
-    """include/fd_verify_gpu.h FDGPU_VTILE_SEQ: a frag's seq with its in link in bits 56..63"""
-    return (link << 56) | seq
 GOSSIP_TAG_VOTE = 3                                      # fd_gossip_types.h:26
 GOSSIP_VOTE_TXN_SZ_OFF, GOSSIP_VOTE_TXN_OFF, GOSSIP_MSG_SZ = 64, 72, 1304   # fd_gossip_update_message_t, x86-64
 LAT_BUCKETS = 40
 
 EXPORTS = ("fdgpu_dedup_tag", "fdgpu_xxh64", "fdgpu_link_set_trace", "fdgpu_link_trace", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
            "fdgpu_mcache_new", "fdgpu_mcache_delete", "fdgpu_mcache_publish", "fdgpu_mcache_poll",
+           "fdgpu_mcache_query", "fdgpu_mcache_wrap", "fdgpu_mcache_depth", "fdgpu_mcache_lines",
            "fdgpu_dcache_compact_next", "fdgpu_vtile_new", "fdgpu_vtile_delete", "fdgpu_vtile_out_dcache",
            "fdgpu_vtile_during_frag", "fdgpu_vtile_flush", "fdgpu_vtile_housekeep", "fdgpu_vtile_pipeline_state", "fdgpu_vtile_after_frags", "fdgpu_vtile_pending",
            "fdgpu_vtile_metrics", "fdgpu_vtile_set_in_link", "fdgpu_vtile_set_in_links", "fdgpu_vtile_oldest_pending_seq", "fdgpu_vtile_overruns",
            "fdgpu_vtile_faulted", "fdgpu_vtile_recover", "fdgpu_vtile_debug_fault", "fdgpu_vtile_gpu_metrics",
            "fdgpu_vtile_new_opts", "fdgpu_vtile_copy", "fdgpu_vtile_copy_state", "fdgpu_vtile_during_frag_overrun",
-           "fdgpu_vtile_set_round_robin", "fdgpu_vtile_before_frag", "fdgpu_vtile_during_frag_kind",
+           "fdgpu_vtile_set_round_robin", "fdgpu_vtile_before_frag", "fdgpu_vtile_set_in",
+           "fdgpu_vtile_during_frag_chunk",
            "fdgpu_link_new", "fdgpu_link_join", "fdgpu_link_delete", "fdgpu_link_joined", "fdgpu_link_cfg",
            "fdgpu_link_run", "fdgpu_link_tiles_of", "fdgpu_link_mcache", "fdgpu_link_dcache", "fdgpu_link_result",
            "fdgpu_stream_run", "fdgpu_stream_bench")
@@ -50,7 +48,7 @@ class FragMeta(ctypes.Structure):
 
 class Done(ctypes.Structure):
     _fields_ = [("seq", ctypes.c_ulong), ("tsorig", ctypes.c_ulong), ("chunk", ctypes.c_ulong), ("sz", ctypes.c_ulong),
-                ("tag", ctypes.c_ulong), ("result", ctypes.c_int)]
+                ("tag", ctypes.c_ulong), ("result", ctypes.c_int), ("in_idx", ctypes.c_ulong)]
 
 
 class GpuMetrics(ctypes.Structure):
@@ -129,6 +127,13 @@ def load():
         L.fdgpu_mcache_delete.argtypes = [vp]
         L.fdgpu_mcache_publish.argtypes = [vp, ul, ul, ctypes.c_uint, ctypes.c_uint, ul, ul]
         L.fdgpu_mcache_poll.argtypes = [vp, ul, ctypes.POINTER(FragMeta)]
+        L.fdgpu_mcache_query.argtypes = [vp, ul, ctypes.POINTER(FragMeta), ctypes.POINTER(ctypes.c_ulong)]
+        L.fdgpu_mcache_wrap.restype = vp
+        L.fdgpu_mcache_wrap.argtypes = [vp, ul]
+        L.fdgpu_mcache_depth.restype = ul
+        L.fdgpu_mcache_depth.argtypes = [vp]
+        L.fdgpu_mcache_lines.restype = vp
+        L.fdgpu_mcache_lines.argtypes = [vp]
         L.fdgpu_dcache_compact_next.restype = ul
         L.fdgpu_dcache_compact_next.argtypes = [ul, ul, ul, ul]
         L.fdgpu_vtile_new.restype = vp
@@ -141,12 +146,13 @@ def load():
         L.fdgpu_vtile_copy_state.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_ulong)]
         L.fdgpu_vtile_during_frag_overrun.argtypes = [vp]
         L.fdgpu_vtile_set_round_robin.argtypes = [vp, ul, ul]
-        L.fdgpu_vtile_before_frag.argtypes = [vp, ctypes.c_int, ul, ul]
-        L.fdgpu_vtile_during_frag_kind.argtypes = [vp, ctypes.c_int, vp, ul, ul, ul]
+        L.fdgpu_vtile_before_frag.argtypes = [vp, ul, ul, ul]
+        L.fdgpu_vtile_set_in.argtypes = [vp, ul, ctypes.c_int, vp, ul, ul]
+        L.fdgpu_vtile_during_frag_chunk.argtypes = [vp, ul, ul, ul, ul, ul, ul, ul]
         L.fdgpu_vtile_delete.argtypes = [vp]
         L.fdgpu_vtile_out_dcache.restype = vp
         L.fdgpu_vtile_out_dcache.argtypes = [vp]
-        L.fdgpu_vtile_during_frag.argtypes = [vp, vp, ul, ul, ul]
+        L.fdgpu_vtile_during_frag.argtypes = [vp, ul, vp, ul, ul, ul]
         L.fdgpu_vtile_flush.argtypes = [vp]
         L.fdgpu_vtile_housekeep.argtypes = [vp, ul]
         L.fdgpu_vtile_housekeep.restype = ctypes.c_int
@@ -158,7 +164,7 @@ def load():
         L.fdgpu_vtile_set_in_link.argtypes = [vp, vp]
         L.fdgpu_vtile_set_in_links.argtypes = [vp, vp, ctypes.c_int]
         L.fdgpu_vtile_oldest_pending_seq.restype = ul
-        L.fdgpu_vtile_oldest_pending_seq.argtypes = [vp]
+        L.fdgpu_vtile_oldest_pending_seq.argtypes = [vp, ctypes.POINTER(ctypes.c_ulong)]
         L.fdgpu_vtile_overruns.restype = ul
         L.fdgpu_vtile_overruns.argtypes = [vp]
         L.fdgpu_vtile_faulted.argtypes = [vp]
@@ -194,7 +200,8 @@ def load():
     return _lib
 
 
-TRACE_DTYPE = np.dtype([("seq", "<u8"), ("tag", "<u8"), ("rec_hash", "<u8"), ("result", "<i4"), ("rec_sz", "<u4")])
+TRACE_DTYPE = np.dtype([("seq", "<u8"), ("tag", "<u8"), ("rec_hash", "<u8"), ("result", "<i4"), ("rec_sz", "<u4"),
+                        ("in_idx", "<u8")])
 
 
 def xxh64(seed: int, data: bytes) -> int:
@@ -259,28 +266,36 @@ class VTile:
         self.seed = seed
         self.dcache = self.L.fdgpu_vtile_out_dcache(self.p)
 
-    def during_frag(self, frag: bytes, seq: int, tsorig: int = 0) -> int:
+    def during_frag(self, frag: bytes, seq: int, tsorig: int = 0, in_idx: int = 0) -> int:
+        """fdgpu_vtile_during_frag of a frag from in link in_idx (its kind: set_in)."""
         b = np.frombuffer(frag, np.uint8)
-        return self.L.fdgpu_vtile_during_frag(self.p, b.ctypes.data, len(frag), seq, tsorig)
+        return self.L.fdgpu_vtile_during_frag(self.p, in_idx, b.ctypes.data, len(frag), seq, tsorig)
 
-    def during_frag_at(self, addr: int, sz: int, seq: int, tsorig: int = 0) -> int:
+    def during_frag_at(self, addr: int, sz: int, seq: int, tsorig: int = 0, in_idx: int = 0) -> int:
         """during_frag on a frag already in memory at addr (zero-copy intake: inside a registered in dcache)."""
-        return self.L.fdgpu_vtile_during_frag(self.p, addr, sz, seq, tsorig)
+        return self.L.fdgpu_vtile_during_frag(self.p, in_idx, addr, sz, seq, tsorig)
+
+    def during_frag_chunk(self, in_idx: int, seq: int, sig: int, chunk: int, sz: int, ctl: int = 0,
+                          tsorig: int = 0) -> int:
+        """fdgpu_vtile_during_frag_chunk: the stem's during_frag (in_idx, seq, sig, chunk, sz, ctl)."""
+        return self.L.fdgpu_vtile_during_frag_chunk(self.p, in_idx, seq, sig, chunk, sz, ctl, tsorig)
+
+    def set_in(self, in_idx: int, in_kind: int, mem: int = 0, chunk0: int = 0, wmark: int = 0) -> int:
+        """fdgpu_vtile_set_in: in link in_idx's kind and data region (chunk c at mem + 64 c)."""
+        return int(self.L.fdgpu_vtile_set_in(self.p, in_idx, in_kind, mem or None, chunk0, wmark))
 
     def set_round_robin(self, idx: int, cnt: int):
         self.L.fdgpu_vtile_set_round_robin(self.p, idx, cnt)
 
-    def before_frag(self, in_kind: int, seq: int, sig: int) -> bool:
+    def before_frag(self, in_idx: int, seq: int, sig: int) -> bool:
         """fdgpu_vtile_before_frag: True = this tile skips the frag (fd_verify_tile.c:36-59)."""
-        return bool(self.L.fdgpu_vtile_before_frag(self.p, in_kind, seq, sig))
+        return bool(self.L.fdgpu_vtile_before_frag(self.p, in_idx, seq, sig))
 
-    def during_frag_kind(self, in_kind: int, frag: bytes | None, seq: int, tsorig: int = 0, addr: int | None = None,
-                         sz: int | None = None) -> int:
-        """fdgpu_vtile_during_frag_kind; addr/sz: a frag already in memory (zero-copy intake)."""
-        if addr is None:
-            b = np.frombuffer(frag, np.uint8)
-            return self.L.fdgpu_vtile_during_frag_kind(self.p, in_kind, b.ctypes.data, len(frag), seq, tsorig)
-        return self.L.fdgpu_vtile_during_frag_kind(self.p, in_kind, addr, sz, seq, tsorig)
+    def oldest_pending(self) -> tuple[int, int]:
+        """(seq, in_idx) of the oldest frag not yet returned by after_frags (~0 both: none)."""
+        li = ctypes.c_ulong(0)
+        s = self.L.fdgpu_vtile_oldest_pending_seq(self.p, ctypes.byref(li))
+        return int(s), int(li.value)
 
     def during_frag_overrun(self) -> int:
         return int(self.L.fdgpu_vtile_during_frag_overrun(self.p))
@@ -317,7 +332,7 @@ class VTile:
     def after_frags(self, max_n: int = 4096, blocking: bool = False):
         out = (Done * max_n)()
         n = self.L.fdgpu_vtile_after_frags(self.p, out, max_n, 1 if blocking else 0)
-        return [(d.seq, d.result, d.chunk, d.sz, d.tag) for d in out[:n]]
+        return [(d.seq, d.result, d.chunk, d.sz, d.tag, d.in_idx) for d in out[:n]]
 
     def pending(self) -> int:
         return int(self.L.fdgpu_vtile_pending(self.p))

@@ -103,6 +103,19 @@ void             fdgpu_mcache_publish( fdgpu_mcache_t * mc, unsigned long seq, u
    tsorig / tspub are the compressed low 32 bits of the timestamps given to
    publish (fd_frag_meta_ts_comp). */
 int              fdgpu_mcache_poll   ( fdgpu_mcache_t const * mc, unsigned long seq, fdgpu_frag_meta_t * out );
+/* the same, plus the seq the line held (*seq_found): where an overrun consumer resumes (the stem's
+   FD_MCACHE_WAIT seq_found, src/tango/mcache/fd_mcache.h:451-520; src/disco/stem/fd_stem.c:590-596) */
+int              fdgpu_mcache_query  ( fdgpu_mcache_t const * mc, unsigned long seq, fdgpu_frag_meta_t * out,
+                                       unsigned long * seq_found );
+/* A handle on the reference's own mcache: `lines` is what fd_mcache_join returns (an fd_frag_meta_t
+   array of depth lines, src/tango/mcache/fd_mcache.h:113,137; 32-byte lines laid out as
+   src/tango/fd_tango_base.h:146-203; line of seq = seq & (depth-1), FD_MCACHE_LG_INTERLEAVE 0).  Nothing
+   is copied or written; the producer keeps publishing with fd_mcache_publish.  fdgpu_mcache_delete
+   frees only the handle (and unregisters the lines' pages if fdgpu_vtile_set_in_links registered them).
+   NULL if depth is not a power of 2 or lines is not 32-byte aligned. */
+fdgpu_mcache_t * fdgpu_mcache_wrap   ( void * lines, unsigned long depth );
+unsigned long    fdgpu_mcache_depth  ( fdgpu_mcache_t const * mc );
+void *           fdgpu_mcache_lines  ( fdgpu_mcache_t * mc );
 
 /* next chunk after a frag of sz bytes at chunk, wrapping to chunk0 past
    wmark (fd_dcache_compact_next, src/tango/dcache/fd_dcache.h) */
@@ -121,12 +134,13 @@ unsigned long    fdgpu_dcache_compact_next( unsigned long chunk, unsigned long s
                                               reference tile would FD_LOG_ERR, fd_verify_tile.c:74-84) */
 
 typedef struct fdgpu_vtile_done {
-  unsigned long seq;      /* as given to during_frag */
+  unsigned long seq;      /* the frag's seq on its in link, as given to during_frag (full 64 bits) */
   unsigned long tsorig;
   unsigned long chunk;    /* out dcache chunk of the fd_txn_m_t record */
   unsigned long sz;       /* realized footprint (fd_txn_m_realized_footprint) when published */
   unsigned long tag;      /* HA dedup tag (0 for bundles) */
   int           result;   /* FDGPU_VTILE_* */
+  unsigned long in_idx;   /* the in link, as given to during_frag (the stem's in_idx) */
 } fdgpu_vtile_done_t;
 
 typedef struct fdgpu_vtile fdgpu_vtile_t;
@@ -199,12 +213,30 @@ fdgpu_vtile_t * fdgpu_vtile_new_opts( int device, unsigned long batch_txn, unsig
 void            fdgpu_vtile_delete( fdgpu_vtile_t * vt );
 unsigned char * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt );   /* chunk c is at base + 64 c */
 
-/* during_frag: copy the frag (fd_txn_m_t header + payload, sz bytes)
-   into the out dcache and submit its payload.  Returns 0, or -2 when the
-   out dcache or the GPU staging is full (call fdgpu_vtile_after_frags
-   and retry), <= -3 on error. */
-int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, unsigned long sz, unsigned long seq,
-                                         unsigned long tsorig );
+/* The stem's callbacks (src/disco/stem/fd_stem.c:627,668,700) take the in link as in_idx and the frag's
+   full 64-bit seq on that link; so do these.  fdgpu_vtile_set_in records what the reference tile keeps
+   per in link (ctx->in_kind[ in_idx ], ctx->in[ in_idx ].mem / chunk0 / wmark, fd_verify_tile.c:181-
+   230): its kind (FDGPU_VTILE_IN_KIND_*; a link never set is QUIC) and its data region -- chunk c of
+   the link is at mem + 64 c (fd_chunk_to_laddr), valid for chunk0 <= c <= wmark.  Call while no frag
+   is pending; 0, or -1 for a bad in_idx / kind. */
+int             fdgpu_vtile_set_in( fdgpu_vtile_t * vt, unsigned long in_idx, int in_kind, void const * mem,
+                                    unsigned long chunk0, unsigned long wmark );
+/* STEM_CALLBACK_DURING_FRAG( ctx, in_idx, seq, sig, chunk, sz, ctl ) (fd_verify_tile.c:65-101), plus the
+   frag's tsorig (the stem hands it to after_frag; here after_frags returns it): the frag at chunk of
+   in link in_idx.  A chunk outside [chunk0, wmark] is -4 (the reference's FD_LOG_ERR).  Otherwise as
+   fdgpu_vtile_during_frag. */
+int             fdgpu_vtile_during_frag_chunk( fdgpu_vtile_t * vt, unsigned long in_idx, unsigned long seq,
+                                               unsigned long sig, unsigned long chunk, unsigned long sz,
+                                               unsigned long ctl, unsigned long tsorig );
+/* during_frag of the frag at `frag` (sz bytes) from in link in_idx.  QUIC / bundle / send links carry
+   fd_txn_m_t records: the record is copied into the out dcache (or, zero-copy intake, the GPU copies
+   it) and its payload submitted; sz > FDGPU_TPU_RAW_MTU or a payload past the frag or past 1232 bytes is
+   -4 (the reference's FD_LOG_ERR).  A gossip link's frag is an fd_gossip_update_message_t whose vote
+   transaction becomes a fresh out-dcache record (payload_sz, bundle id 0, payload), copied by the host
+   as the reference does (sz > 2048, or a vote txn_sz past 1232 / the frag: -4).  Returns 0, or -2 when
+   the out dcache or the GPU staging is full (call fdgpu_vtile_after_frags and retry), <= -3 on error. */
+int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, unsigned long in_idx, void const * frag, unsigned long sz,
+                                         unsigned long seq, unsigned long tsorig );
 /* Zero-copy intake: from now on during_frag leaves the frag where it
    is -- frag must then lie in a range registered with
    fdgpu_host_register (the in dcache), 16-B aligned -- and the GPU
@@ -223,18 +255,15 @@ int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, void const * frag, 
    frag is pending; 0 on success. */
 int             fdgpu_vtile_set_in_link( fdgpu_vtile_t * vt, fdgpu_mcache_t const * in_mc );
 /* The same for a tile that reads n in links (the reference's verify tile
-   reads every QUIC tile's link, topology.c:167-169): the seq a frag is
-   handed to during_frag with carries its link in bits 56..63
-   (FDGPU_VTILE_SEQ( link, seq )), and after_frag checks the frag against
-   in_mc[ link ] (entries may be NULL).  n <= FDGPU_VTILE_IN_MAX. */
+   reads every QUIC tile's link, topology.c:167-169): a frag handed to
+   during_frag from in link in_idx is checked against in_mc[ in_idx ]
+   (entries may be NULL; fdgpu_mcache_wrap makes one of the reference's
+   own mcache).  n <= FDGPU_VTILE_IN_MAX. */
 #define FDGPU_VTILE_IN_MAX   16
-#define FDGPU_VTILE_SEQ( link, seq )  ( ( (unsigned long)(link) << 56 ) | (unsigned long)(seq) )
-#define FDGPU_VTILE_SEQ_LINK( s )     ( (int)( (s) >> 56 ) )
-#define FDGPU_VTILE_SEQ_SEQ( s )      ( (s) & ( ( 1UL << 56 ) - 1UL ) )
 int             fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_mc, int n );
 /* seq of the oldest frag not yet returned by after_frags, as handed to
-   during_frag (link bits included, FDGPU_VTILE_SEQ); ~0UL if none */
-unsigned long   fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt );
+   during_frag, and (in_idx, may be NULL) its in link; ~0UL (both) if none */
+unsigned long   fdgpu_vtile_oldest_pending_seq( fdgpu_vtile_t const * vt, unsigned long * in_idx );
 /* Zero-copy intake: start the GPU copy of every frag taken and not yet
    copied; blocking: wait until every copy has completed.  0, or < 0 if a
    context failed (its frags come back as FDGPU_VTILE_GPU_FAULT). */
@@ -268,17 +297,12 @@ int             fdgpu_vtile_during_frag_overrun( fdgpu_vtile_t * vt );
 #define FDGPU_GOSSIP_MSG_MAX         (2048UL)  /* fd_verify_tile.c:89-90 */
 /* before_frag's round robin: this tile is verify:idx of cnt */
 void            fdgpu_vtile_set_round_robin( fdgpu_vtile_t * vt, unsigned long idx, unsigned long cnt );
-/* before_frag (fd_verify_tile.c:36-59): 1 = this tile skips the frag.  A QUIC frag or a bundle-tile
-   packet (sig 0) round robin; a bundle (sig != 0) only verify:0; a gossip update round robin and only a
-   vote (sig == FDGPU_GOSSIP_UPDATE_TAG_VOTE); a send-tile frag never skipped. */
-int             fdgpu_vtile_before_frag( fdgpu_vtile_t const * vt, int in_kind, unsigned long seq, unsigned long sig );
-/* during_frag of any in kind: QUIC / bundle / send frags are fd_txn_m_t records (fdgpu_vtile_during_frag;
-   sz > FDGPU_TPU_RAW_MTU is -4, the reference's FD_LOG_ERR); a gossip frag is an
-   fd_gossip_update_message_t whose vote transaction becomes a fresh out-dcache record (payload_sz, bundle
-   id 0, payload), copied by the host as the reference does (sz > 2048 or a vote txn_sz past 1232 / the frag:
-   -4).  Returns as fdgpu_vtile_during_frag. */
-int             fdgpu_vtile_during_frag_kind( fdgpu_vtile_t * vt, int in_kind, void const * frag, unsigned long sz,
-                                              unsigned long seq, unsigned long tsorig );
+/* STEM_CALLBACK_BEFORE_FRAG( ctx, in_idx, seq, sig ) (fd_verify_tile.c:36-59): 1 = this tile skips the
+   frag.  By in_idx's kind (fdgpu_vtile_set_in): a QUIC frag or a bundle-tile packet (sig 0) round robin
+   on the full seq; a bundle (sig != 0) only verify:0; a gossip update round robin and only a vote (sig ==
+   FDGPU_GOSSIP_UPDATE_TAG_VOTE); a send-tile frag never skipped.  in_idx >= FDGPU_VTILE_IN_MAX: 1. */
+int             fdgpu_vtile_before_frag( fdgpu_vtile_t const * vt, unsigned long in_idx, unsigned long seq,
+                                         unsigned long sig );
 
 /* launch the partially filled batches (call when the input is idle) */
 int             fdgpu_vtile_flush( fdgpu_vtile_t * vt );
@@ -408,14 +432,15 @@ fdgpu_mcache_t * fdgpu_link_mcache( fdgpu_link_t * link );
 unsigned char *  fdgpu_link_dcache( fdgpu_link_t * link );
 int             fdgpu_link_result( fdgpu_link_t * link, double timeout_s, fdgpu_stream_stats_t * st );
 /* Verdict trace (parity at scale, tests/test_gpu_stream_parity.py): with cap > 0 every tile this
-   process runs records up to cap of its verdicts in after_frags order -- the seq handed to during_frag
-   (link in bits 56-63), FDGPU_VTILE_* result, HA dedup tag, and for a published frag the XXH64 (seed 0)
+   process runs records up to cap of its verdicts in after_frags order -- the seq and in link handed to
+   during_frag, FDGPU_VTILE_* result, HA dedup tag, and for a published frag the XXH64 (seed 0)
    and size of its fd_txn_m_t record as published in the tile's out dcache.  Set before fdgpu_link_run;
    0 on success.  fdgpu_link_trace copies tile's entries out and returns their count. */
 typedef struct fdgpu_link_trace {
   unsigned long seq, tag, rec_hash;
   int           result;
   unsigned int  rec_sz;
+  unsigned long in_idx;
 } fdgpu_link_trace_t;
 int             fdgpu_link_set_trace( fdgpu_link_t * link, unsigned long cap );
 unsigned long   fdgpu_link_trace( fdgpu_link_t const * link, int tile, fdgpu_link_trace_t * out, unsigned long max );

@@ -239,6 +239,54 @@ class RefTile:
         return [int(x) for x in res], [int(x) for x in metrics], recs, [int(x) for x in tag]
 
 
+class RefMcache:
+    """A tango mcache written and read by the reference's own inline code (oracle/_ref/libfdref_mcache.so:
+    fd_mcache_publish / fd_mcache_publish_avx / FD_MCACHE_WAIT compiled in place; fd_mcache_new's line
+    initialisation restated).  The ring is an FD_MCACHE_ALIGN-aligned fd_frag_meta_t array inside a
+    page-aligned numpy buffer (at byte offset `off`, like the lines of an fd_mcache region, which start
+    past its header), so tests can hand `lines_addr` to fdgpu_mcache_wrap."""
+
+    META_DTYPE = np.dtype([("seq", "<u8"), ("sig", "<u8"), ("chunk", "<u4"), ("sz", "<u2"), ("ctl", "<u2"),
+                           ("tsorig", "<u4"), ("tspub", "<u4")])
+
+    def __init__(self, depth: int, seq0: int = 0, off: int = 256):
+        path = os.path.join(HERE, "_ref", "libfdref_mcache.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.lib = L = ctypes.CDLL(path)
+        ul, vp = ctypes.c_ulong, ctypes.c_void_p
+        for n in ("ref_frag_meta_sz", "ref_mcache_align"):
+            getattr(L, n).restype = ul
+        L.ref_mcache_line_idx.restype = ul
+        L.ref_mcache_line_idx.argtypes = [ul, ul]
+        L.ref_mcache_init_lines.argtypes = [vp, ul, ul]
+        L.ref_mcache_publish.argtypes = [vp] + [ul] * 8 + [ctypes.c_int]
+        L.ref_mcache_wait.argtypes = [vp, ul, ul, vp, ctypes.POINTER(ul)]
+        assert L.ref_frag_meta_sz() == self.META_DTYPE.itemsize == 32
+        assert off % L.ref_mcache_align() == 0
+        self.depth = depth
+        nbytes = off + depth * 32
+        self._raw = np.zeros(nbytes + 8192, np.uint8)
+        base = (-self._raw.ctypes.data) % 4096
+        self.buf = self._raw[base: base + ((nbytes + 4095) // 4096) * 4096]
+        self.lines_addr = self.buf.ctypes.data + off
+        self.lines = self.buf[off: off + depth * 32].view(self.META_DTYPE)
+        L.ref_mcache_init_lines(self.lines_addr, depth, seq0)
+
+    def line_idx(self, seq: int) -> int:
+        return int(self.lib.ref_mcache_line_idx(seq, self.depth))
+
+    def publish(self, seq, sig, chunk, sz, ctl=0, tsorig=0, tspub=0, avx=False):
+        self.lib.ref_mcache_publish(self.lines_addr, self.depth, seq, sig, chunk, sz, ctl, tsorig, tspub, 1 if avx else 0)
+
+    def wait(self, seq):
+        """FD_MCACHE_WAIT once: (rc, meta record or None, seq_found); rc 0 ready, 1 not yet, -1 overrun."""
+        out = np.zeros(1, self.META_DTYPE)
+        found = ctypes.c_ulong(0)
+        rc = self.lib.ref_mcache_wait(self.lines_addr, self.depth, seq, out.ctypes.data, ctypes.byref(found))
+        return rc, (out[0] if rc == 0 else None), int(found.value)
+
+
 def cpu_has_avx512_ifma() -> bool:
     try:
         with open("/proc/cpuinfo") as f:

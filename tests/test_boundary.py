@@ -9,8 +9,10 @@ from firedancer_amd import engine
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _header_functions():
-    txt = open(os.path.join(ROOT, "include", "fd_ed25519_gpu.h")).read()
+def _header_functions(name="fd_ed25519_gpu.h"):
+    txt = open(os.path.join(ROOT, "include", name)).read()
+    if name != "fd_ed25519_gpu.h":
+        txt = txt.split('#include "fd_ed25519_gpu.h"', 1)[1]
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     txt = re.sub(r"static inline[^{]*\{.*?\n\}", "", txt, flags=re.S)    # header-only helpers, not exports
     return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", txt)) - {"sizeof"})
@@ -18,6 +20,18 @@ def _header_functions():
 
 def test_header_matches_exports_list():
     assert sorted(engine.EXPORTS) == _header_functions()
+
+
+def test_vtile_header_matches_exports_list():
+    from firedancer_amd import vtile
+    assert sorted(vtile.EXPORTS) == _header_functions("fd_verify_gpu.h")
+
+
+def test_vtile_library_exports():
+    from firedancer_amd import vtile
+    out = subprocess.run(["nm", "-D", "--defined-only", vtile.LIB_PATH], capture_output=True, text=True).stdout
+    syms = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert [n for n in vtile.EXPORTS if n not in syms] == []
 
 
 def test_library_loads_and_exports():

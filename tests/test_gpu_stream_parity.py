@@ -80,7 +80,8 @@ def check_tiles(pays, traces):
     n = len(pays)
     for i, tr in enumerate(traces):
         keep = tr[tr["result"] != vtile.OVERRUN]
-        seqs = keep["seq"] & np.uint64((1 << 56) - 1)
+        seqs = keep["seq"]
+        assert np.all(keep["in_idx"] == 0), "one producer link: every frag on in link 0"
         assert np.all(seqs % TILES == i), "a tile took a frag of another tile's round-robin share"
         assert np.all(np.diff(seqs.astype(np.int64)) > 0), "verdicts out of frag order"
         frags = [(pays[int(s) % n], 0) for s in seqs]

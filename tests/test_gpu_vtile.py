@@ -146,7 +146,7 @@ def test_vtile_vs_model(oracle, batch, depth, zero_copy, engine_path):
     def drain(blocking):
         # downstream reads each published record as it is published (the out dcache is a ring)
         out = vt.after_frags(blocking=blocking)
-        for seq, r, chunk, sz, tag in out:
+        for seq, r, chunk, sz, tag, _ in out:
             if r == vtile.PUBLISH:
                 head, timg = want_recs.get(seq, (b"", b""))
                 rec = vt.record(chunk, sz)
@@ -200,7 +200,7 @@ def test_vtile_multictx_vs_model(oracle, nctx, zero_copy):
 
     def drain(blocking):
         out = vt.after_frags(blocking=blocking)
-        for seq, r, chunk, sz, tag in out:
+        for seq, r, chunk, sz, tag, _ in out:
             if r == vtile.PUBLISH:
                 head, timg = want_recs.get(seq, (b"", b""))
                 rec = vt.record(chunk, sz)
@@ -311,12 +311,87 @@ def test_vtile_zero_copy_lap_after_copy():
     want = [vtile.PUBLISH] * 32 + [vtile.OVERRUN] * 8 + [vtile.PUBLISH] * (n - 40)
     assert [g[1] for g in got] == want
     assert vt.overruns() == 8 and vt.metrics() == [0, 0, 0, 0, n - 8]
-    for seq, r, chunk, sz, tag in got[:8]:             # published records hold the bytes copied before the rewrite
+    for seq, r, chunk, sz, tag, _ in got[:8]:             # published records hold the bytes copied before the rewrite
         rec = vt.record(chunk, sz)
         assert rec[:len(fbs[seq])][80:] == fbs[seq][80:]
     vt.close()
     L.fdgpu_mcache_delete(mc)
     engine.host_unregister(buf)
+
+
+@pytest.mark.parametrize("lap", [0, 24])
+@pytest.mark.parametrize("rr_idx", [0, 1])
+def test_vtile_on_reference_mcache(rr_idx, lap):
+    """The tile bound to the reference's own tango shapes.  The in link's ring is an fd_frag_meta_t array
+    written by the reference's fd_mcache_publish (oracle/_ref/libfdref_mcache.so, compiled in place) with
+    seqs that cross 2^64, wrapped with fdgpu_mcache_wrap; the tile is driven as the stem drives it
+    (fd_stem.c:627,668,700): before_frag( in_idx, seq, sig ) and during_frag_chunk( in_idx, seq, sig,
+    chunk, sz, ctl ) on the line's fields, zero-copy intake from the registered in dcache with the GPU's
+    line re-check.  Verify:rr_idx of 2 keeps every other frag (round robin on the full 64-bit seq); the
+    kept frags' outcomes, records and HA tags equal the reference tile's, and each verdict carries its
+    in_idx and full seq.  lap: the producer reuses the lines of the first `lap` seqs after the tile took
+    them and before the GPU copied them -- those frags are OVERRUN and never reach after_frag, as in
+    the reference."""
+    pytest.importorskip("xxhash")
+    from firedancer_amd import engine, vtile
+    from oracle.oracle import RefMcache, RefTile
+    try:
+        ring, ref = RefMcache(256, (1 << 64) - 100), RefTile()
+    except (FileNotFoundError, RuntimeError) as e:
+        pytest.skip(f"reference build unavailable: {e}")
+    M = (1 << 64) - 1
+    seq0 = (1 << 64) - 100
+    frags = make_stream(5)[:200]
+    fbs = [vtile.frag_bytes(p, b) for p, b in frags]
+    buf, offs = in_dcache(fbs)
+    mem = buf.ctypes.data + offs[0]                     # chunk 0 of the link (64-B aligned)
+    chunks = [(buf.ctypes.data + o - mem) // 64 for o in offs]
+    engine.host_register(buf)
+    L = vtile.load()
+    mc = L.fdgpu_mcache_wrap(ring.lines_addr, ring.depth)
+    depth, seed = 1 << 12, 0x5eed
+    vt = vtile.VTile(device=0, batch_txn=256, tcache_depth=depth, seed=seed)
+    vt.set_round_robin(rr_idx, 2)
+    assert vt.set_in(0, vtile.IN_QUIC, mem, 0, max(chunks)) == 0
+    assert vt.set_in_links([mc]) == 0
+    assert vt.during_frag_chunk(0, seq0, 0, max(chunks) + 1, 100) == -4   # outside [chunk0, wmark]: corrupt
+    for i, fb in enumerate(fbs):                        # the producer (the reference's publish)
+        ring.publish((seq0 + i) & M, sig=0, chunk=chunks[i], sz=len(fb), ctl=0, tsorig=i, tspub=i)
+    kept = []
+    for i in range(len(fbs)):                           # the stem: poll the line, before_frag, during_frag
+        s = (seq0 + i) & M
+        m = vtile.FragMeta()
+        assert L.fdgpu_mcache_poll(mc, s, m) == 0 and m.seq == s
+        if vt.before_frag(0, s, m.sig):
+            continue
+        assert vt.during_frag_chunk(0, s, m.sig, m.chunk, m.sz, 0, m.tsorig) == 0
+        kept.append(i)
+    assert kept == [i for i in range(len(fbs)) if ((seq0 + i) & M) % 2 == rr_idx]
+    for j in range(lap):                                # laps the lines of seqs seq0 .. seq0+lap-1
+        ring.publish((seq0 + ring.depth + j) & M, sig=0, chunk=0, sz=0)
+    got = _drain_all(vt)
+    assert [g[0] for g in got] == [(seq0 + i) & M for i in kept] and all(g[5] == 0 for g in got)
+    ovr = [i for i in kept if i < lap]
+    assert [g[1] == vtile.OVERRUN for g in got] == [i in ovr for i in kept]
+    rest = [i for i in kept if i >= lap]
+    want_res, want_m, want_recs, want_tags = ref.run([frags[i] for i in rest], depth, seed)
+    gr = [g for g in got if g[1] != vtile.OVERRUN]
+    assert [g[1] for g in gr] == want_res
+    assert vt.metrics() == want_m and vt.overruns() == len(ovr)
+    for k, (seqv, r, chunk, sz, tag, _) in enumerate(gr):
+        if r == vtile.PUBLISH:
+            assert _same_record(vt.record(chunk, sz), want_recs[k], len(frags[rest[k]][0])), k
+            assert tag == want_tags[k]
+    assert sum(1 for r in want_res if r == vtile.PUBLISH) > 20
+    vt.close()
+    L.fdgpu_mcache_delete(mc)
+    engine.host_unregister(buf)
+
+
+def _same_record(rec, want, payload_sz):
+    """published records agree but for the alignment pad byte between payload and fd_txn_t"""
+    hl = 80 + payload_sz
+    return len(rec) == len(want) and rec[:hl] == want[:hl] and rec[(hl + 1) & ~1:] == want[(hl + 1) & ~1:]
 
 
 def _run_frags(vt, frags, seq0=0):
@@ -328,7 +403,7 @@ def _run_frags(vt, frags, seq0=0):
     vt.flush()
     while vt.pending():
         out += vt.after_frags(blocking=True)
-    return [r for _, r, _, _, _ in out]
+    return [r for _, r, _, _, _, _ in out]
 
 
 def test_reference_tile_scenarios():
@@ -429,17 +504,18 @@ def test_vtile_in_kinds_vs_reference(oracle, rr_idx, zero_copy):
         buf, offs = in_dcache([r if r else bytes(64) for r in recs])
         engine.host_register(buf)
         assert vt.set_in_links([None] * 4) == 0
+    for k in range(4):                    # in link k carries kind k (the stem's in_idx, the tile's in_kind[ in_idx ])
+        assert vt.set_in(k, k) == 0
     got, kept = [], []
     for i, (k, g, q, fb, _, _) in enumerate(frags):
         if vt.before_frag(k, q, g):
             continue
         kept.append(i)
-        s = vtile.FDGPU_VTILE_SEQ(k, q)
         while True:
             if zero_copy and k != vtile.IN_GOSSIP:
-                rc = vt.during_frag_kind(k, None, s, addr=buf.ctypes.data + offs[i], sz=len(fb))
+                rc = vt.during_frag_at(buf.ctypes.data + offs[i], len(fb), q, in_idx=k)
             else:
-                rc = vt.during_frag_kind(k, fb, s)
+                rc = vt.during_frag(fb, q, in_idx=k)
             if rc != -2:
                 break
             got += vt.after_frags(blocking=True)
@@ -450,11 +526,12 @@ def test_vtile_in_kinds_vs_reference(oracle, rr_idx, zero_copy):
     while vt.pending():
         got += vt.after_frags(blocking=True)
     assert kept == [i for i, r in enumerate(want_res) if r != -2]
-    assert [g[0] & ((1 << 56) - 1) for g in got] == [frags[i][2] for i in kept]
+    assert [g[0] for g in got] == [frags[i][2] for i in kept]
+    assert [g[5] for g in got] == [frags[i][0] for i in kept]
     assert [g[1] for g in got] == [want_res[i] for i in kept]
     assert vt.metrics() == want_m
     bad = []
-    for (seqv, r, chunk, sz, tag), i in zip(got, kept):
+    for (seqv, r, chunk, sz, tag, _), i in zip(got, kept):
         if r != vtile.PUBLISH:
             continue
         rec, want = vt.record(chunk, sz), want_recs[i]
