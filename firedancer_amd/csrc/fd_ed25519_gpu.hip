@@ -3458,6 +3458,10 @@ fdgpu_ed25519_reserve_gather_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n ) {
   if( e != hipSuccess ) { (void)hipStreamDestroy( s ); set_err( "hipExtStreamCreateWithCUMask", e ); return -2; }
   e = hipEventCreateWithFlags( &ctx->gev, hipEventDisableTiming );
   if( e != hipSuccess ) { (void)hipStreamDestroy( s ); (void)hipStreamDestroy( g ); set_err( "hipEventCreate", e ); return -2; }
+  /* HIP has no CU-masked stream with flags or a priority: both streams are blocking (they order with
+     the null stream, which the tile never uses) and of default priority -- the copies' precedence over
+     queued verify work comes from their reserved CUs, not from a stream priority (gather_init's
+     highest-priority stream is only made when no CUs are reserved) */
   (void)hipStreamSynchronize( ctx->stream );
   (void)hipStreamDestroy( ctx->stream );
   ctx->stream = s; ctx->gstream = g; ctx->gather_cus = n;

@@ -900,9 +900,11 @@ vt_during_gossip( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulo
   if( sz > FDGPU_GOSSIP_MSG_MAX || sz < FDGPU_GOSSIP_VOTE_TXN_OFF ) return -4;   /* :89-90 */
   uchar const * msg = (uchar const *)frag;
   ulong txn_sz; memcpy( &txn_sz, msg + FDGPU_GOSSIP_VOTE_TXN_SZ_OFF, sizeof(ulong) );
-  /* the reference copies vote.txn_sz bytes out of the 1232-byte vote.txn array unchecked; past the array
-     (or past the frag) there is nothing defined to copy: refused as corrupt */
-  if( txn_sz > 1232UL || FDGPU_GOSSIP_VOTE_TXN_OFF + txn_sz > sz ) return -4;
+  /* the reference copies vote.txn_sz bytes out of the 1232-byte vote.txn array unchecked
+     (fd_verify_tile.c:91-95), also past the frame the gossip tile publishes (FD_GOSSIP_UPDATE_SZ_VOTE
+     = 1297 bytes ends 1225 bytes into vote.txn, fd_gossip_private.h:80): so does this.  Past the array
+     there is nothing defined to copy: refused as corrupt */
+  if( txn_sz > 1232UL ) return -4;
   int rc = vt_room( vt );
   if( rc ) return rc;
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
@@ -1700,7 +1702,12 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   if( c->zero_copy && !l->registered ) {
     if( fdgpu_host_register( l->dcache, h->in_bytes + 4096UL ) ) { atomic_store( &h->fail, 7 ); return -3; }
     for( int q=0; q<c->producers; q++ )          /* the gather re-reads each frag's line after its copy */
-      if( fdgpu_host_register( l->line[q], mc_bytes( h->depth ) ) ) { atomic_store( &h->fail, 7 ); return -3; }
+      if( fdgpu_host_register( l->line[q], mc_bytes( h->depth ) ) ) {
+        /* undo what was registered: fdgpu_link_delete unregisters only a complete registration */
+        while( q-- > 0 ) fdgpu_host_unregister( l->line[q] );
+        fdgpu_host_unregister( l->dcache );
+        atomic_store( &h->fail, 7 ); return -3;
+      }
     l->registered = 1;
   }
   pthread_t prod[ LINK_PROD_MAX ], th[ LINK_TILE_MAX ];

@@ -18,7 +18,9 @@ PUBLISH, PARSE_FAIL, VERIFY_FAIL, DEDUP_FAIL, BUNDLE_PEER_FAIL, OVERRUN, GPU_FAU
 IN_QUIC, IN_BUNDLE, IN_GOSSIP, IN_SEND = range(4)        # fd_verify_tile.c:7-10
 
 GOSSIP_TAG_VOTE = 3                                      # fd_gossip_types.h:26
-GOSSIP_VOTE_TXN_SZ_OFF, GOSSIP_VOTE_TXN_OFF, GOSSIP_MSG_SZ = 64, 72, 1304   # fd_gossip_update_message_t, x86-64
+GOSSIP_VOTE_TXN_SZ_OFF, GOSSIP_VOTE_TXN_OFF = 64, 72   # fd_gossip_update_message_t vote.txn_sz / vote.txn, x86-64
+GOSSIP_MSG_SZ = 1297     # FD_GOSSIP_UPDATE_SZ_VOTE = 49 + sizeof(fd_gossip_vote_t), the frame the gossip tile publishes
+                         # (src/flamenco/gossip/fd_gossip_private.h:80, crds/fd_crds.c:938)
 LAT_BUCKETS = 40
 
 EXPORTS = ("fdgpu_dedup_tag", "fdgpu_xxh64", "fdgpu_link_set_trace", "fdgpu_link_trace", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
@@ -234,7 +236,7 @@ class TCache:
 def gossip_vote_msg(txn: bytes, tag: int = GOSSIP_TAG_VOTE, origin: bytes = bytes(32)) -> bytes:
     """An fd_gossip_update_message_t (src/flamenco/gossip/fd_gossip_types.h:182-205, x86-64 layout) carrying
     txn as its vote (tag VOTE) -- or, for another tag, whatever the union holds."""
-    b = bytearray(GOSSIP_MSG_SZ)
+    b = bytearray(max(GOSSIP_MSG_SZ, GOSSIP_VOTE_TXN_OFF + len(txn)))   # a vote txn past 1225 bytes runs past the frame
     b[0] = tag
     b[1:33] = origin[:32].ljust(32, b"\0")
     b[GOSSIP_VOTE_TXN_SZ_OFF:GOSSIP_VOTE_TXN_SZ_OFF + 8] = len(txn).to_bytes(8, "little")

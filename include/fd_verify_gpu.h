@@ -233,7 +233,8 @@ int             fdgpu_vtile_during_frag_chunk( fdgpu_vtile_t * vt, unsigned long
    it) and its payload submitted; sz > FDGPU_TPU_RAW_MTU or a payload past the frag or past 1232 bytes is
    -4 (the reference's FD_LOG_ERR).  A gossip link's frag is an fd_gossip_update_message_t whose vote
    transaction becomes a fresh out-dcache record (payload_sz, bundle id 0, payload), copied by the host
-   as the reference does (sz > 2048, or a vote txn_sz past 1232 / the frag: -4).  Returns 0, or -2 when
+   as the reference does (sz > 2048 or a vote txn_sz past 1232: -4; as the reference, txn_sz bytes are read from vote.txn even past
+   the frame: the 1297-byte FD_GOSSIP_UPDATE_SZ_VOTE frame holds 1225 of them).  Returns 0, or -2 when
    the out dcache or the GPU staging is full (call fdgpu_vtile_after_frags and retry), <= -3 on error. */
 int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, unsigned long in_idx, void const * frag, unsigned long sz,
                                          unsigned long seq, unsigned long tsorig );

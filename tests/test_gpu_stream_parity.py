@@ -116,6 +116,11 @@ def test_stream_parity_unreliable_laps():
     pays = payload_set()
     st, traces = run_leg(pays, reliable=False, depth=1 << 12)
     assert st["verdicts"] + st["lost"] == N_FRAGS
+    # the leg must exercise what it is for: tiles lapped at the poll (lost frags), and the verdicts of
+    # frags overrun while the GPU copied them recorded as such (the gather-time line re-check)
+    assert st["lost"] > 0, "the 4096-line link was never lapped"
+    n_ovr = sum(int((t["result"] == 5).sum()) for t in traces)      # FDGPU_VTILE_OVERRUN
+    assert n_ovr == st["overruns"]
     assert sum(len(t) for t in traces) == st["verdicts"]
     seen = list(check_tiles(pays, traces))
     assert sum(k for _, k, _ in seen) == st["verdicts"] - st["overruns"]

@@ -388,6 +388,37 @@ def test_vtile_on_reference_mcache(rr_idx, lap):
     engine.host_unregister(buf)
 
 
+def test_vtile_gossip_vote_past_frame():
+    """The gossip tile publishes every vote update as a 1297-byte frame (FD_GOSSIP_UPDATE_SZ_VOTE,
+    fd_gossip_private.h:80), which holds 1225 bytes of vote.txn; the reference tile copies vote.txn_sz
+    bytes regardless (fd_verify_tile.c:91-95).  A 1232-byte vote transaction in such a frame -- its last
+    7 bytes past the frame, where the update message's vote.txn array continues -- verifies and
+    publishes whole, as in the reference; a txn_sz past the 1232-byte array is corrupt (-4)."""
+    from firedancer_amd import synth, vtile
+    payload, desc, _, _ = synth.make_batch(4, synth.LARGE_NOOP, seed=9)
+    txns = [payload[d["payload_off"]: d["payload_off"] + d["payload_sz"]].tobytes() for d in desc]
+    assert all(len(t) == 1232 for t in txns)
+    vt = vtile.VTile(device=0, batch_txn=64, tcache_depth=1024)
+    assert vt.set_in(2, vtile.IN_GOSSIP) == 0
+    bufs = []
+    for i, t in enumerate(txns):
+        msg = np.frombuffer(vtile.gossip_vote_msg(t), np.uint8)      # 72 + 1232 = 1304 bytes of message
+        assert len(msg) == 1304
+        buf = np.zeros(2048, np.uint8)
+        buf[:1304] = msg
+        bufs.append(buf)
+        assert vt.during_frag_at(buf.ctypes.data, vtile.GOSSIP_MSG_SZ, i, in_idx=2) == 0
+    bad = bufs[0].copy()
+    bad[64:72] = np.frombuffer(np.uint64(1233).tobytes(), np.uint8)
+    assert vt.during_frag_at(bad.ctypes.data, vtile.GOSSIP_MSG_SZ, 9, in_idx=2) == -4
+    got = _drain_all(vt)
+    assert [g[1] for g in got] == [vtile.PUBLISH] * 4 and [g[5] for g in got] == [2] * 4
+    for (seq, r, chunk, sz, tag, _), t in zip(got, txns):
+        rec = vt.record(chunk, sz)
+        assert rec[80:80 + 1232] == t and rec[8:10] == (1232).to_bytes(2, "little")
+    vt.close()
+
+
 def _same_record(rec, want, payload_sz):
     """published records agree but for the alignment pad byte between payload and fd_txn_t"""
     hl = 80 + payload_sz
