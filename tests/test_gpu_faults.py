@@ -141,12 +141,12 @@ def test_vtile_all_contexts_faulted_refuses_intake():
         vt.debug_fault(k)
     assert vt.during_frag(frags[1], 1) == -3
     out = vt.after_frags(blocking=True)
-    assert [(s, r) for s, r, _, _, _ in out] == [(0, vtile.GPU_FAULT)]
+    assert [(s, r) for s, r, _, _, _, _ in out] == [(0, vtile.GPU_FAULT)]
     assert vt.recover() == 0
     assert vt.during_frag(frags[1], 1) == 0
     vt.flush()
     out = []
     while vt.pending():
         out += vt.after_frags(blocking=True)
-    assert [(s, r) for s, r, _, _, _ in out] == [(1, vtile.PUBLISH)]
+    assert [(s, r) for s, r, _, _, _, _ in out] == [(1, vtile.PUBLISH)]
     vt.close()
