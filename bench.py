@@ -266,7 +266,17 @@ def stream_child_main(args) -> None:
     regenerates the payloads (same seed), creates each leg's link and runs the producer; the others join."""
     from firedancer_amd import vtile
     proc, procs, dev = args.stream_proc, args.stream_procs, args.stream_device
-    out, cal_fps = {}, 0.0
+    out, cal_fps, anom = {}, 0.0, {}
+
+    def anomalies(link, leg):
+        # verdicts neither published nor overrun: in these all-valid streams every one is an anomaly
+        n, first = 0, []
+        for t in vtile.tiles_of(int(link.cfg()["tiles"]), procs, proc):
+            c, f = link.anomalies(t)
+            n += c
+            first += [dict(e, tile=t) for e in f]
+        if n:
+            anom[leg] = {"count": n, "first": first[:8]}
     wb = {"gather": 0, "none": 1, "finish": 2}[args.stream_writeback]
     if wb or args.stream_poll_prefetch:
         from firedancer_amd import engine
@@ -291,6 +301,7 @@ def stream_child_main(args) -> None:
                 if rc:
                     raise RuntimeError(f"leg {leg}: fdgpu_link_run {rc}")
                 st = link.result(timeout_s=120.0)
+                anomalies(link, leg)
             finally:
                 link.close()
                 if path and os.path.exists(path):
@@ -303,11 +314,12 @@ def stream_child_main(args) -> None:
             link = vtile.Link(path, create=False, timeout_s=180.0 if leg == "cal" else 120.0)   # bounded if process 0 failed
             try:
                 rc = link.run(proc, dev, True)          # its producers: q % G == proc
+                anomalies(link, leg)
             finally:
                 link.close()
             if rc:
                 raise RuntimeError(f"leg {leg}: fdgpu_link_run {rc} (process {proc})")
-    print(json.dumps({"legs": out, "cal_frags_per_s": cal_fps}), flush=True)
+    print(json.dumps({"legs": out, "cal_frags_per_s": cal_fps, "anomalies": anom}), flush=True)
 
 
 def run_stream_child(args, dev, proc, procs, token) -> dict:
@@ -335,6 +347,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
     return json.loads(lines[-1])
 
 
+ROOF_STEPS = 3                 # steps of the roofline pass (per-kernel timing, one launch per kernel)
 HEADLINE_MAX_BYTES = 4096      # the driver keeps the last ~8 KB of stdout: the headline line stays well inside
 
 
@@ -410,7 +423,8 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 "p99_us": _r(curve[0]["p99_us"]) if curve else None,
                 "unreliable_vs_max": _r(st.get("unreliable_goodput_vs_max"), 3),
                 "tile_host_ns_per_frag": (st.get("max_rate") or {}).get("tile_host_ns_per_frag"),
-                "all_published": st.get("all_published")}
+                "all_published": st.get("all_published"),
+                "anomalies": sum(v["count"] for v in (st.get("anomalies") or {}).values())}
     rec["detail"] = detail_path
     return rec
 
@@ -661,12 +675,20 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    eng.set_timing(True)
     dt = shard.timed_steps(step, args.steps, 0, torch.cuda.synchronize, barrier)
+    ok = all(bool(np.array_equal(o.cpu().numpy(), expect)) for _, _, o in pipe)
+
+    # the roofline pass: a few more steps of the same batch with per-kernel HIP events on the launch stream
+    # (the headline steps above run without event records between their kernels)
+    eng.verify_txns_device(pay_d.data_ptr(), desc_d.data_ptr(), n, nsig, out_d.data_ptr(), None, st)
+    torch.cuda.synchronize()
+    eng.set_timing(True)
+    for _ in range(ROOF_STEPS):
+        eng.verify_txns_device(pay_d.data_ptr(), desc_d.data_ptr(), n, nsig, out_d.data_ptr(), None, st)
+    torch.cuda.synchronize()
     ms_prep, ms_dsm, ms_red = eng.kernel_ms(0), eng.kernel_ms(1), eng.kernel_ms(2)
     eng.set_timing(False)
-
-    ok = all(bool(np.array_equal(o.cpu().numpy(), expect)) for _, _, o in pipe)
+    ok = ok and bool(np.array_equal(out_d.cpu().numpy(), expect))
     # the same steps alternating over two contexts / streams (one batch's prep overlaps the other's walk
     # tail): the engine's best whole-job rate on this workload.  Reported beside `value`, which stays the
     # one-context rate so that the roofline's per-launch kernel times are not stretched by the overlap
@@ -825,8 +847,19 @@ def main():
             res = run_stream_child(args, dev, rank, world, token)
         except Exception as e:      # keep the headline line even if the stream leg fails
             err = str(e)[-2000:]
-        # every rank takes part in the same collective, whatever happened locally
+        # every rank takes part in the same collectives, whatever happened locally
         _, stream_ok = shard.reduce_max_min(dd, 0.0, err is None, "cpu")
+        mine = (res or {}).get("anomalies", {})
+        all_anom = [mine]
+        if world > 1:
+            all_anom = [None] * world
+            dist.all_gather_object(all_anom, mine)
+        anomalies = {}
+        for r, a in enumerate(all_anom):
+            for leg, v in (a or {}).items():
+                m = anomalies.setdefault(leg, {"count": 0, "first": []})
+                m["count"] += v["count"]
+                m["first"] = (m["first"] + [dict(e, rank=r) for e in v["first"]])[:8]
         if rank == 0:
             if res is not None and stream_ok:
                 legs = res["legs"]
@@ -860,6 +893,8 @@ def main():
                           # goodput of the reference's own link mode under overload, against the reliable max rate
                           "unreliable_goodput_vs_max": ur["sigs_per_s"] / mx["sigs_per_s"] if mx["sigs_per_s"] else None,
                           "all_published": bool(ok_s),
+                          # verdicts neither published nor overrun, per leg (fdgpu_link_anomalies): none expected
+                          "anomalies": anomalies,
                           "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
             else:
                 stream = {"error": err or "a stream child failed on another rank"}
@@ -935,7 +970,8 @@ def main():
                        "parallelism": f"independent per-GPU shards x{world}", "semantics": "avx512",
                        "contexts_per_gpu": args.pipe},
             "results_ok": all_ok,
-            "kernel_ms": {"prep": ms_prep, "dsm": ms_dsm, "reduce": ms_red},
+            "kernel_ms": {"prep": ms_prep, "dsm": ms_dsm, "reduce": ms_red,
+                          "source": f"roofline pass: {ROOF_STEPS} more steps of the same batch, HIP events"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GMAC/s",
                          "frac": achieved / peak if peak > 0 else None, "traffic": traffic,
                          # rocprof name of the 1M launch (carry-fold instantiation)

@@ -1071,6 +1071,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
 
 #define LINK_MAGIC    0xfd6e11c0ffee0004UL
 #define LINK_TILE_MAX 64
+#define LINK_ANOM_MAX 8
 
 /* Latency histogram (per tile, merged at the end): log-linear buckets,
    64 per octave (< 1.6 % wide), exact below 64 ns. */
@@ -1136,6 +1137,10 @@ struct fdgpu_link {
   fdgpu_mcache_t   mc[ LINK_PROD_MAX ];   /* local views of the shared lines (the tiles' in links) */
   fdgpu_link_trace_t * trace[ LINK_TILE_MAX ];   /* fdgpu_link_set_trace: this process's tiles' verdicts, in order */
   ulong            trace_cap, trace_cnt[ LINK_TILE_MAX ];
+  /* fdgpu_link_anomalies: per tile of this process, the first LINK_ANOM_MAX verdicts that are neither
+     published nor overrun (parse / verify / dedup / bundle failures), and how many there were */
+  fdgpu_link_trace_t anom[ LINK_TILE_MAX ][ LINK_ANOM_MAX ];
+  ulong            anom_cnt[ LINK_TILE_MAX ];
 };
 
 static ulong al64( ulong x ) { return ( x + 63UL ) & ~63UL; }
@@ -1495,8 +1500,17 @@ static ulong own_in( ulong a, ulong b, ulong T, ulong idx ) {
   return cb - ca;
 }
 
+ulong
+fdgpu_link_anomalies( fdgpu_link_t const * l, int tile, fdgpu_link_trace_t * out, ulong max ) {
+  if( tile < 0 || tile >= LINK_TILE_MAX ) return 0UL;
+  ulong n = l->anom_cnt[tile] < LINK_ANOM_MAX ? l->anom_cnt[tile] : LINK_ANOM_MAX;
+  if( n > max ) n = max;
+  memcpy( out, l->anom[tile], n * sizeof(fdgpu_link_trace_t) );
+  return l->anom_cnt[tile];
+}
+
 static void
-link_account( fdgpu_link_t * l, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs, ulong * lh, ulong * lmax,
+link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs, ulong * lh, ulong * lmax,
               ulong * t_last, link_in_t * in ) {
   /* bench accounting only (not after_frag): the signature count comes from
      the link's per-payload table, not from the (cold) record in the out dcache */
@@ -1510,6 +1524,14 @@ link_account( fdgpu_link_t * l, fdgpu_vtile_done_t const * d, ulong n, ulong * s
     in[q].fin++;
     if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL )
       *sigs += l->psig[ ( s * Q + (ulong)q ) % np ];
+    if( __builtin_expect( d[i].result != FDGPU_VTILE_PUBLISH && d[i].result != FDGPU_VTILE_OVERRUN, 0 ) ) {
+      ulong k = l->anom_cnt[idx]++;
+      if( k < LINK_ANOM_MAX ) {                  /* rec_hash: the frag's payload index (the link's layout) */
+        fdgpu_link_trace_t * e = &l->anom[idx][k];
+        e->seq = s; e->in_idx = d[i].in_idx; e->tag = d[i].tag; e->result = d[i].result;
+        e->rec_sz = (unsigned)d[i].sz; e->rec_hash = ( s * Q + (ulong)q ) % np;
+      }
+    }
   }
   if( n ) *t_last = t;
 }
@@ -1647,7 +1669,7 @@ static void * link_tile( void * _a ) {
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
       PROF_ADD( 3 );
       link_trace( l, idx, vt, done, n );
-      link_account( l, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
+      link_account( l, idx, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
       PROF_ADD( 5 );
       if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );
       PROF_ADD( 6 );
@@ -1666,7 +1688,7 @@ static void * link_tile( void * _a ) {
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
       PROF_ADD( 4 );
       link_trace( l, idx, vt, done, n );
-      link_account( l, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
+      link_account( l, idx, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
       PROF_ADD( 5 );
       if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );
       PROF_ADD( 6 );

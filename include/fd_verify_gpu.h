@@ -445,6 +445,10 @@ typedef struct fdgpu_link_trace {
 } fdgpu_link_trace_t;
 int             fdgpu_link_set_trace( fdgpu_link_t * link, unsigned long cap );
 unsigned long   fdgpu_link_trace( fdgpu_link_t const * link, int tile, fdgpu_link_trace_t * out, unsigned long max );
+/* Always on, per tile this process runs: the first 8 verdicts that were neither published nor overrun
+   (parse / verify / dedup / bundle failures; in the bench's all-valid streams each one is an anomaly),
+   with rec_hash holding the frag's payload index in the link; returns how many such verdicts there were. */
+unsigned long   fdgpu_link_anomalies( fdgpu_link_t const * link, int tile, fdgpu_link_trace_t * out, unsigned long max );
 
 /* one process, private link, every tile on `device` (G = 1) */
 int             fdgpu_stream_run( int device, fdgpu_stream_cfg_t const * cfg, unsigned char const * payload,
