@@ -10,8 +10,8 @@ d="gpurun_out/prof_${tag}"
 bash "$(dirname "$0")/gpu_job.sh" \
   "tests:1100:python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread" \
   "smoke:300:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
-  "bench:480:python bench.py --steps 20 --warmup 5 > gpurun_out/bench_${tag}.json" \
-  "stats:180:mkdir -p $d && rocprofv3 --kernel-trace --stats -f csv -d $d/stats -o run -- $B > $d/bench_under_rocprof.json" \
+  "bench:480:mkdir -p $d && python bench.py --steps 20 --warmup 5 --detail-out $d/bench_detail.json > gpurun_out/bench_${tag}.json" \
+  "stats:180:rocprofv3 --kernel-trace --stats -f csv -d $d/stats -o run -- $B > $d/bench_under_rocprof.json" \
   "pmc_fetch:150:$P --pmc FETCH_SIZE -d $d/fetch -o run -- $B" \
   "pmc_write:150:$P --pmc WRITE_SIZE -d $d/write -o run -- $B" \
   "pmc_sq:150:$P --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE -d $d/sq -o run -- $B"
