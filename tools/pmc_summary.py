@@ -80,12 +80,24 @@ d = out.get(dk)
 if d and "hbm_read_bytes" in d:
     rd = os.path.join(os.path.dirname(dst.rstrip("/")), "roofline")
     im = os.path.join(rd, "issue_model_dsmh_r03c.json")      # the model priced with every measured row
+    if dk.startswith("fd_dsmh") and not os.path.exists(im):  # a later round without its own model: the last one
+        im = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "profiles", "r03", "roofline",
+                          "issue_model_dsmh_r03c.json")
     if not dk.startswith("fd_dsmh") or not os.path.exists(im):
         im = os.path.join(rd, "issue_model_dsmh.json" if dk.startswith("fd_dsmh") else "issue_model.json")
-    busy = json.load(open(im))["valu_busy_model"] if os.path.exists(im) else None
+    busy = None
+    if os.path.exists(im):
+        mj = json.load(open(im))
+        busy = mj["valu_busy_model"]
+        # the model's issue time (at its clock) over THIS run's measured launch time, when rocprof has it
+        for r in (csv.DictReader(open(stats)) if os.path.exists(stats) else []):
+            if norm(r["Name"]) == dk and mj.get("predicted_ms"):
+                busy = mj["predicted_ms"] / (float(r["AverageNs"]) / 1e6)
     json.dump({"kernel": dk, "source": dst,
                "hbm_bytes_per_launch": d["hbm_read_bytes"] + d.get("hbm_write_bytes", 0),
-               "valu_busy": busy, "valu_busy_source": im if busy is not None else None,
+               "valu_busy": busy,
+               "valu_busy_source": os.path.relpath(os.path.abspath(im), os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+                                   + " (predicted issue time / this run's rocprof launch time)" if busy is not None else None,
                "valu_busy_flat4": d.get("valu_busy_flat4"), "valu_insts_per_wave": d.get("valu_insts_per_wave")},
               open(os.path.join(os.path.dirname(dst.rstrip("/")), "..", "dsm_pmc.json"), "w"), indent=1)
 for k, e in sorted(out.items()):
