@@ -186,7 +186,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 mcache_depth=args.stream_depth * min(procs, 2) if not paced else 1 << 18,
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
                 copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus,
-                max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist)
+                max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
+                no_huge_pages=1 if args.stream_no_huge else 0)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -261,6 +262,17 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
             "gpu_batch_lat_p99_us_le": hq(0.99)}
 
 
+def _anon_huge_mb() -> float | None:
+    """This process's memory in transparent huge pages (the link region's backing, when the kernel allows)."""
+    try:
+        for line in open("/proc/self/smaps_rollup"):
+            if line.startswith("AnonHugePages:"):
+                return int(line.split()[1]) / 1024.0
+    except OSError:
+        pass
+    return None
+
+
 def stream_child_main(args) -> None:
     """--stream-child: the configs[4] legs for one process (one GPU); no torch GPU context here.  Process 0
     regenerates the payloads (same seed), creates each leg's link and runs the producer; the others join."""
@@ -296,6 +308,7 @@ def stream_child_main(args) -> None:
         if proc == 0:
             cfg = _leg_cfg(args, leg, procs, cal_fps)
             link = vtile.Link(path, create=True, payload=payload, off=desc["payload_off"], sz=desc["payload_sz"], **cfg)
+            huge_mb = _anon_huge_mb()
             try:
                 rc = link.run(0, dev, True)
                 if rc:
@@ -309,7 +322,7 @@ def stream_child_main(args) -> None:
             if leg == "cal":
                 cal_fps = st["frags_per_s"]
             else:
-                out[leg] = _leg_summary(st, cfg)
+                out[leg] = dict(_leg_summary(st, cfg), anon_huge_mb=huge_mb)
         else:
             link = vtile.Link(path, create=False, timeout_s=180.0 if leg == "cal" else 120.0)   # bounded if process 0 failed
             try:
@@ -337,7 +350,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
            "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus),
            "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
-        (["--stream-prof"] if args.stream_prof else [])
+        (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else [])
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -471,7 +484,8 @@ def launch_ranks(n: int, argv: list[str], script: str | None = None, timeout_s: 
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, script] + argv, env=env))
+        # only rank 0's stdout is the bench's: the other ranks' (gloo's connection notes, ...) go to stderr
+        procs.append(subprocess.Popen([sys.executable, script] + argv, env=env, stdout=None if r == 0 else sys.stderr))
     t0, rc = time.time(), 0
     while True:
         codes = [p.poll() for p in procs]
@@ -587,6 +601,10 @@ def main():
                     help="zero-copy intake: CUs each tile's engine contexts reserve for the copies (fdgpu_vtile_opts_t; "
                          "16 vs 0 on 2 tiles: max 21.6M vs 18.7M sigs/s, paced 10M/s p99 2.0 vs 4.6 ms, "
                          "profiles/r03/stream_tiles)")
+    ap.add_argument("--stream-first", action="store_true",
+                    help="run the configs[4] stream legs before the headline, before this process initialises the GPU")
+    ap.add_argument("--stream-no-huge", action="store_true",
+                    help="(A/B) the link region in 4 KiB pages instead of transparent huge pages")
     ap.add_argument("--stream-prof", action="store_true",
                     help="rdtsc section profile of the tile loop (fdgpu_stream_cfg_t.prof), in each leg's summary")
     ap.add_argument("--stream-max-uncopied", type=int, default=0,
@@ -633,7 +651,6 @@ def main():
     rank, world, local_rank = rank_env(args.gpus)
     # rehearsal knob for the N>1 flow on a one-GPU box: FDGPU_BENCH_ONE_DEVICE=1 puts every rank on GPU 0
     dev = 0 if os.environ.get("FDGPU_BENCH_ONE_DEVICE") == "1" else local_rank
-    torch.cuda.set_device(dev)
     # The data path has no collective (independent shards); the measurement reductions (MAX of time, MIN of
     # the results flag, SUM of signatures) are a few scalars, so they go over gloo on CPU tensors: no RCCL.
     if world > 1:
@@ -643,6 +660,80 @@ def main():
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def stream_section():
+        """BASELINE configs[4] on every rank (its tile process), merged on rank 0; None elsewhere."""
+        stream = None
+        barrier()
+        token = f"{os.getpid()}_{int(time.time())}" if rank == 0 else ""
+        if world > 1:
+            obj = [token]
+            dist.broadcast_object_list(obj, src=0)
+            token = obj[0]
+        res, err = None, None
+        try:
+            res = run_stream_child(args, dev, rank, world, token)
+        except Exception as e:      # keep the headline line even if the stream leg fails
+            err = str(e)[-2000:]
+        # every rank takes part in the same collectives, whatever happened locally
+        _, stream_ok = shard.reduce_max_min(dd, 0.0, err is None, "cpu")
+        mine = (res or {}).get("anomalies", {})
+        all_anom = [mine]
+        if world > 1:
+            all_anom = [None] * world
+            dist.all_gather_object(all_anom, mine)
+        anomalies = {}
+        for r, a in enumerate(all_anom):
+            for leg, v in (a or {}).items():
+                m = anomalies.setdefault(leg, {"count": 0, "first": []})
+                m["count"] += v["count"]
+                m["first"] = (m["first"] + [dict(e, rank=r) for e in v["first"]])[:8]
+        if rank == 0:
+            if res is not None and stream_ok:
+                legs = res["legs"]
+                mx, ur = legs["max"], legs["unrel"]
+                curve = [dict(legs[f"paced@{r}"], offered_frags_per_s_per_gpu=r) for r in _rates(args)]
+                pc = curve[0]
+                ok_s = (mx["metrics"][:4] == [0, 0, 0, 0] and mx["published"] == mx["frags"] and mx["lost"] == 0
+                        and all(c["metrics"][:4] == [0, 0, 0, 0] for c in curve))
+                # the knee: the highest offered rate whose p99 (tsorig -> verdict) stays within 1 ms with
+                # every frag verified (none lost to overruns, none overrun while copied)
+                within = [c["offered_frags_per_s_per_gpu"] for c in curve
+                          if c["p99_us"] <= 1000.0 and c["lost"] == 0 and c["overruns_at_verdict"] == 0]
+                knee = {"frags_per_s_per_gpu": max(within) if within else None, "p99_bound_us": 1000.0,
+                        "rates_tried": _rates(args)}
+                stream = {"workload": "BASELINE configs[4]: 1232-byte txns, Q producer mcache links over one in dcache "
+                                      "-> T verify tiles reading every link (seq % T round robin per link, tile i -> "
+                                      "GPU i % G; device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> "
+                                      "out dcache",
+                          "sigs_per_s": mx["sigs_per_s"], "per_gpu_sigs_per_s": mx["sigs_per_s"] / world,
+                          "n_gpus": world, "tiles_per_gpu": mx["tiles"] // world, "batch_max": args.stream_max_batch,
+                          "batch_paced": pc["batch_limit"],
+                          "max_inflight": args.stream_inflight, "max_inflight_paced": args.stream_lat_inflight,
+                          "link_depth": args.stream_depth * min(world, 2),
+                          "producers": args.stream_producers * world,
+                          "engine_contexts_per_tile": args.stream_ctx, "engine_contexts_per_tile_paced": args.stream_lat_ctx,
+                          "process": "one tile process per GPU without a torch GPU context (as a C verify tile); "
+                                     "link in /dev/shm when G > 1",
+                          "intake": "zero-copy (GPU gathers frags from the registered in dcache)"
+                                    if not args.stream_copy else "host copy into the out dcache (reference during_frag)",
+                          "max_rate": mx, "paced": pc, "latency_curve": curve, "knee": knee, "unreliable_max": ur,
+                          # goodput of the reference's own link mode under overload, against the reliable max rate
+                          "unreliable_goodput_vs_max": ur["sigs_per_s"] / mx["sigs_per_s"] if mx["sigs_per_s"] else None,
+                          "all_published": bool(ok_s),
+                          # verdicts neither published nor overrun, per leg (fdgpu_link_anomalies): none expected
+                          "anomalies": anomalies,
+                          "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
+            else:
+                stream = {"error": err or "a stream child failed on another rank"}
+
+        return stream
+
+
+    # --stream-first: the configs[4] legs before this process touches the GPU (its HIP context, queues and
+    # torch's allocations then do not exist yet while the tile processes run)
+    stream = stream_section() if args.stream_frags != 0 and args.stream_first else None
+    torch.cuda.set_device(dev)
 
     n = args.txns
     gen_threads = min(16, os.cpu_count() or 1)
@@ -834,71 +925,7 @@ def main():
     # (one producer link, T = tiles x G verify tiles, tile i -> GPU i % G), in a child process per GPU that
     # never initialises torch's GPU context: a verify tile is a plain C process, and torch's context in this
     # one measurably inflates the tiles' tail latency (tools/stream_seq.py, TORCH=1: paced p99 1.2 -> 2.2 ms).
-    stream = None
-    if args.stream_frags != 0:
-        barrier()
-        token = f"{os.getpid()}_{int(time.time())}" if rank == 0 else ""
-        if world > 1:
-            obj = [token]
-            dist.broadcast_object_list(obj, src=0)
-            token = obj[0]
-        res, err = None, None
-        try:
-            res = run_stream_child(args, dev, rank, world, token)
-        except Exception as e:      # keep the headline line even if the stream leg fails
-            err = str(e)[-2000:]
-        # every rank takes part in the same collectives, whatever happened locally
-        _, stream_ok = shard.reduce_max_min(dd, 0.0, err is None, "cpu")
-        mine = (res or {}).get("anomalies", {})
-        all_anom = [mine]
-        if world > 1:
-            all_anom = [None] * world
-            dist.all_gather_object(all_anom, mine)
-        anomalies = {}
-        for r, a in enumerate(all_anom):
-            for leg, v in (a or {}).items():
-                m = anomalies.setdefault(leg, {"count": 0, "first": []})
-                m["count"] += v["count"]
-                m["first"] = (m["first"] + [dict(e, rank=r) for e in v["first"]])[:8]
-        if rank == 0:
-            if res is not None and stream_ok:
-                legs = res["legs"]
-                mx, ur = legs["max"], legs["unrel"]
-                curve = [dict(legs[f"paced@{r}"], offered_frags_per_s_per_gpu=r) for r in _rates(args)]
-                pc = curve[0]
-                ok_s = (mx["metrics"][:4] == [0, 0, 0, 0] and mx["published"] == mx["frags"] and mx["lost"] == 0
-                        and all(c["metrics"][:4] == [0, 0, 0, 0] for c in curve))
-                # the knee: the highest offered rate whose p99 (tsorig -> verdict) stays within 1 ms with
-                # every frag verified (none lost to overruns, none overrun while copied)
-                within = [c["offered_frags_per_s_per_gpu"] for c in curve
-                          if c["p99_us"] <= 1000.0 and c["lost"] == 0 and c["overruns_at_verdict"] == 0]
-                knee = {"frags_per_s_per_gpu": max(within) if within else None, "p99_bound_us": 1000.0,
-                        "rates_tried": _rates(args)}
-                stream = {"workload": "BASELINE configs[4]: 1232-byte txns, Q producer mcache links over one in dcache "
-                                      "-> T verify tiles reading every link (seq % T round robin per link, tile i -> "
-                                      "GPU i % G; device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> "
-                                      "out dcache",
-                          "sigs_per_s": mx["sigs_per_s"], "per_gpu_sigs_per_s": mx["sigs_per_s"] / world,
-                          "n_gpus": world, "tiles_per_gpu": mx["tiles"] // world, "batch_max": args.stream_max_batch,
-                          "batch_paced": pc["batch_limit"],
-                          "max_inflight": args.stream_inflight, "max_inflight_paced": args.stream_lat_inflight,
-                          "link_depth": args.stream_depth * min(world, 2),
-                          "producers": args.stream_producers * world,
-                          "engine_contexts_per_tile": args.stream_ctx, "engine_contexts_per_tile_paced": args.stream_lat_ctx,
-                          "process": "one tile process per GPU without a torch GPU context (as a C verify tile); "
-                                     "link in /dev/shm when G > 1",
-                          "intake": "zero-copy (GPU gathers frags from the registered in dcache)"
-                                    if not args.stream_copy else "host copy into the out dcache (reference during_frag)",
-                          "max_rate": mx, "paced": pc, "latency_curve": curve, "knee": knee, "unreliable_max": ur,
-                          # goodput of the reference's own link mode under overload, against the reliable max rate
-                          "unreliable_goodput_vs_max": ur["sigs_per_s"] / mx["sigs_per_s"] if mx["sigs_per_s"] else None,
-                          "all_published": bool(ok_s),
-                          # verdicts neither published nor overrun, per leg (fdgpu_link_anomalies): none expected
-                          "anomalies": anomalies,
-                          "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
-            else:
-                stream = {"error": err or "a stream child failed on another rank"}
-
+    stream = stream_section() if args.stream_frags != 0 and not args.stream_first else stream
     if lat is not None:
         # after the stream leg: the drop-in's process-wide context (and its stream) lives until exit
         # the link-level drop-in: one synchronous fd_ed25519_verify call (one signature, one GPU round trip)

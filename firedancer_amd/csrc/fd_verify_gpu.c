@@ -1126,6 +1126,8 @@ struct fdgpu_link {
   link_hdr_t *     h;
   uchar *          base;
   ulong            sz;
+  uchar *          map;          /* the mapping base is inside (private links: 2 MiB aligned within it) */
+  ulong            map_sz;
   int              shared, registered;
   mc_line_t *      line[ LINK_PROD_MAX ];
   uchar *          dcache;
@@ -1197,13 +1199,28 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
     base = (uchar *)mmap( NULL, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0 );
     close( fd );
     if( base == MAP_FAILED ) { unlink( path ); return NULL; }
-  } else {
-    base = (uchar *)mmap( NULL, total, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0 );
-    if( base == MAP_FAILED ) return NULL;
+  }
+  uchar * map = base; ulong map_sz = total;
+  if( !shared ) {
+    /* The reference's links live in workspaces of huge (2 MiB) or gigantic pages (fd_wksp); the GPU reads
+       this region frag by frag over PCIe (zero-copy intake), and with 4 KiB pages every frag is a GPU TLB
+       miss in a 1+ GB region.  Transparent huge pages where the kernel allows them (madvise mode), unless
+       cfg.no_huge_pages (A/B): a 2 MiB aligned region, advised before first touch. */
+    ulong const huge = 2UL << 20;
+    map_sz = total + ( cfg->no_huge_pages ? 0UL : huge );
+    map = (uchar *)mmap( NULL, map_sz, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0 );
+    if( map == MAP_FAILED ) return NULL;
+    base = map;
+    if( !cfg->no_huge_pages ) {
+      base = (uchar *)( ( (ulong)map + huge - 1UL ) & ~( huge - 1UL ) );
+      (void)madvise( base, total, MADV_HUGEPAGE );   /* whole 2 MiB extents in it become huge pages */
+    }
+  } else if( !cfg->no_huge_pages ) {
+    (void)madvise( base, total, MADV_HUGEPAGE );    /* shmem: honoured only where shmem_enabled allows it */
   }
   fdgpu_link_t * l = (fdgpu_link_t *)calloc( 1, sizeof(fdgpu_link_t) );
-  if( !l ) { munmap( base, total ); return NULL; }
-  l->base = base; l->sz = total; l->shared = shared; l->h = (link_hdr_t *)base;
+  if( !l ) { munmap( map, map_sz ); return NULL; }
+  l->base = base; l->sz = total; l->map = map; l->map_sz = map_sz; l->shared = shared; l->h = (link_hdr_t *)base;
   link_hdr_t * h = l->h;
   memset( (void *)h, 0, sizeof(link_hdr_t) );
   h->total_sz = total; h->cfg = *cfg; h->cfg.producers = (int)Q;
@@ -1249,7 +1266,7 @@ fdgpu_link_join( char const * path, double timeout_s ) {
             if( base == MAP_FAILED ) return NULL;
             fdgpu_link_t * l = (fdgpu_link_t *)calloc( 1, sizeof(fdgpu_link_t) );
             if( !l ) { munmap( base, total ); return NULL; }
-            l->base = base; l->sz = total; l->shared = 1; l->h = (link_hdr_t *)base;
+            l->base = base; l->sz = total; l->map = base; l->map_sz = total; l->shared = 1; l->h = (link_hdr_t *)base;
             link_view( l );
             atomic_fetch_add( &l->h->joined, 1UL );
             return l;
@@ -1270,7 +1287,7 @@ fdgpu_link_delete( fdgpu_link_t * l ) {
     fdgpu_host_unregister( l->dcache );
     for( int q=0; q<l->h->cfg.producers; q++ ) fdgpu_host_unregister( l->line[q] );
   }
-  munmap( l->base, l->sz );
+  munmap( l->map, l->map_sz );
   for( int i=0; i<LINK_TILE_MAX; i++ ) free( l->trace[i] );
   free( l );
 }
