@@ -290,9 +290,10 @@ def stream_child_main(args) -> None:
         if n:
             anom[leg] = {"count": n, "first": first[:8]}
     wb = {"gather": 0, "none": 1, "finish": 2}[args.stream_writeback]
-    if wb or args.stream_poll_prefetch:
+    if wb or args.stream_poll_prefetch or args.stream_gather_rpb:
         from firedancer_amd import engine
-        engine.debug_set_opts(gather_no_writeback=wb, poll_prefetch=args.stream_poll_prefetch)
+        engine.debug_set_opts(gather_no_writeback=wb, poll_prefetch=args.stream_poll_prefetch,
+                              gather_rpb=args.stream_gather_rpb)
     payload = desc = None
     if proc == 0:
         from firedancer_amd import synth
@@ -350,7 +351,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
            "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus),
            "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
-        (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else [])
+        (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else []) + \
+        (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else [])
     if args.stream_copy:
         cmd.append("--stream-copy")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -603,6 +605,8 @@ def main():
                          "profiles/r03/stream_tiles)")
     ap.add_argument("--stream-first", action="store_true",
                     help="run the configs[4] stream legs before the headline, before this process initialises the GPU")
+    ap.add_argument("--stream-gather-rpb", type=int, default=0,
+                    help="(stream child, A/B) records per gather workgroup (fdgpu_debug_opts_t.gather_rpb; 0 = default 4)")
     ap.add_argument("--stream-no-huge", action="store_true",
                     help="(A/B) the link region in 4 KiB pages instead of transparent huge pages")
     ap.add_argument("--stream-prof", action="store_true",

@@ -1956,21 +1956,27 @@ struct fd_gather {             /* mode 3: copy sz bytes from src (host, device v
    copies' stores reach the host's out region before the batch's verdicts,
    behind its completion token), so no release fence is needed: a
    system-scope release per block wrote back the XCD's whole L2 each time,
-   under the verify kernels running beside it (2x slower stream). */
-__global__ void __launch_bounds__( 64 )
-fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__ arena, unsigned char * __restrict__ out,
+   under the verify kernels running beside it (2x slower stream).
+   FD_GATHER_RPB records per workgroup, one wave each (ctx->gather_rpb: 4 by default; 1 = round 3's
+   one-wave groups, fdgpu_debug_opts_t.gather_rpb): fewer, larger workgroups for the dispatcher and one
+   counter atomic per group instead of per record. */
+template<int FD_GATHER_RPB>
+__global__ void __launch_bounds__( 64 * FD_GATHER_RPB )
+fd_gather_kernel( fd_gather const * __restrict__ g, u32 n, unsigned char * __restrict__ arena, unsigned char * __restrict__ out,
                   unsigned char * __restrict__ ovr, unsigned long * cnt, unsigned long * flag, unsigned long target,
                   unsigned long * gtime ) {
   /* gtime (pinned): the 100-MHz GPU clock when block 0 starts and when the last block ends -- the
      engine's gather latency metric (fdgpu_ed25519_gather_stats) */
   if( blockIdx.x == 0u && threadIdx.x == 0u )
     __hip_atomic_store( gtime, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
-  fd_gather r = g[ blockIdx.x ];
+  u32 rec = blockIdx.x * FD_GATHER_RPB + ( threadIdx.x >> 6 ), i = threadIdx.x & 63u;
+  unsigned char bad = 0;
+  if( rec < n ) {
+  fd_gather r = g[ rec ];
   uint4 const * src = (uint4 const *)r.src;
   uint4 * a = (uint4 *)( arena + r.dst );
   uint4 * o = (uint4 *)( out + r.dst );
-  u32 n16 = r.sz >> 4, i = threadIdx.x;
-  unsigned char bad = 0;
+  u32 n16 = r.sz >> 4;
   if( n16 <= 128u ) {          /* every fd_txn_m_t record (<= 80 + 1232 bytes): all loads, the re-check, then stores */
     uint4 v0 = make_uint4( 0u, 0u, 0u, 0u ), v1 = v0;
     if( i < n16 ) v0 = src[i];
@@ -1983,18 +1989,20 @@ fd_gather_kernel( fd_gather const * __restrict__ g, unsigned char * __restrict__
     if( i < n16 ) { a[i] = v0; if( out ) o[i] = v0; }
     if( i + 64u < n16 ) { a[i + 64u] = v1; if( out ) o[i + 64u] = v1; }
   } else {
-    for( ; i<n16; i+=64u ) { uint4 v = src[i]; a[i] = v; if( out ) o[i] = v; }
+    for( u32 j=i; j<n16; j+=64u ) { uint4 v = src[j]; a[j] = v; if( out ) o[j] = v; }
     if( r.seq_addr ) {
       asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );
       unsigned long s = __hip_atomic_load( (unsigned long *)r.seq_addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
       bad = s != r.seq;
     }
   }
-  if( threadIdx.x == 0u ) ovr[ blockIdx.x ] = bad;
-  __syncthreads();                                          /* (one wave: every lane's loads have returned) */
+  if( i == 0u ) ovr[ rec ] = bad;                        /* (lane 0 of the record's wave) */
+  }
+  __syncthreads();                                          /* every lane of every wave: its loads have returned */
   if( threadIdx.x == 0u ) {
-    unsigned long old = __hip_atomic_fetch_add( cnt, 1UL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
-    if( old + 1UL == target ) {
+    unsigned long k = n - blockIdx.x * FD_GATHER_RPB < FD_GATHER_RPB ? n - blockIdx.x * FD_GATHER_RPB : FD_GATHER_RPB;
+    unsigned long old = __hip_atomic_fetch_add( cnt, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+    if( old + k == target ) {
       __hip_atomic_store( gtime + 1, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
       __hip_atomic_store( flag, target, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
     }
@@ -2098,6 +2106,7 @@ struct fdgpu_ed25519_ctx {
   unsigned char *    d_pflag;    /* raw path: 1 = fd_txn_parse rejected the payload */
   int dsm_lanes;                 /* latency path: lanes per signature in the DSM, 0 = by batch size (fdgpu_debug_opts_t) */
   int poll_pf;                   /* fdgpu_debug_opts_t.poll_prefetch */
+  int gather_rpb;                /* fd_gather_kernel records per workgroup (fdgpu_debug_opts_t.gather_rpb) */
   int gather_nowb;               /* fdgpu_debug_opts_t.gather_no_writeback: 0 = the records' write-back in
                                     the gather kernel, 1 = none (diagnostic), 2 = in fd_finish_kernel (A/B) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
@@ -2356,14 +2365,14 @@ extern "C" void fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx );
 /* Test / A/B options of contexts created from now on (fdgpu_debug_set_opts).
    Process-wide, behind a mutex; the defaults are the product's choices. */
 static std::mutex g_dbg_mu;
-static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L, 0 };
+static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L, 0, 0, 0 };
 static void debug_opts_get( fdgpu_debug_opts_t * o ) { std::lock_guard<std::mutex> lk( g_dbg_mu ); *o = g_dbg; }
 
 extern "C" void
 fdgpu_debug_set_opts( fdgpu_debug_opts_t const * opts ) {
   std::lock_guard<std::mutex> lk( g_dbg_mu );
   if( opts ) g_dbg = *opts;
-  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L, 0 };
+  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L, 0, 0, 0 };
 }
 
 /* staging + device buffers of async slot i (once) */
@@ -2446,6 +2455,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->nofold_max = dbg.nofold_max >= 0 ? (unsigned long)dbg.nofold_max : FD_NOFOLD_MAX;
   ctx->gather_nowb = dbg.gather_no_writeback;
   ctx->poll_pf = dbg.poll_prefetch > 0 ? dbg.poll_prefetch : 0;
+  ctx->gather_rpb = dbg.gather_rpb == 1 ? 1 : 4;
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
@@ -3014,7 +3024,9 @@ static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
     gt = ctx->d_gtime + 2*i;
     ctx->last_gt = (long)i;
   } else { gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT; ctx->last_gt = -1; }   /* untimed: a scratch entry */
-  hipLaunchKernelGGL( fd_gather_kernel, dim3( (unsigned)n ), dim3( 64 ), 0, ctx->gstream, sl.g_dev + sl.gathered,
+  unsigned long rpb = ctx->gather_rpb == 1 ? 1UL : 4UL;
+  hipLaunchKernelGGL( ( rpb == 1UL ? fd_gather_kernel<1> : fd_gather_kernel<4> ), dim3( (unsigned)( ( n + rpb - 1UL ) / rpb ) ),
+                      dim3( 64UL * rpb ), 0, ctx->gstream, sl.g_dev + sl.gathered, (u32)n,
                       sl.d_payload, ctx->gather_nowb == 0 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, sl.d_ovr + sl.gathered, ctx->d_gcnt,
                       (unsigned long *)( ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT + 1 ), target, gt );
   HIPCHK( hipGetLastError(), -2 );
