@@ -187,7 +187,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
                 copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus,
                 max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
-                no_huge_pages=1 if args.stream_no_huge else 0)
+                huge_pages=1 if args.stream_huge else 0)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -351,7 +351,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
            "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus),
            "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
-        (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else []) + \
+        (["--stream-prof"] if args.stream_prof else []) + (["--stream-huge"] if args.stream_huge else []) + \
         (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else [])
     if args.stream_copy:
         cmd.append("--stream-copy")
@@ -606,9 +606,9 @@ def main():
     ap.add_argument("--stream-first", action="store_true",
                     help="run the configs[4] stream legs before the headline, before this process initialises the GPU")
     ap.add_argument("--stream-gather-rpb", type=int, default=0,
-                    help="(stream child, A/B) records per gather workgroup (fdgpu_debug_opts_t.gather_rpb; 0 = default 4)")
-    ap.add_argument("--stream-no-huge", action="store_true",
-                    help="(A/B) the link region in 4 KiB pages instead of transparent huge pages")
+                    help="(stream child, A/B) records per gather workgroup (fdgpu_debug_opts_t.gather_rpb; 0 = default 1)")
+    ap.add_argument("--stream-huge", action="store_true",
+                    help="(A/B) the link region in transparent huge pages instead of 4 KiB pages")
     ap.add_argument("--stream-prof", action="store_true",
                     help="rdtsc section profile of the tile loop (fdgpu_stream_cfg_t.prof), in each leg's summary")
     ap.add_argument("--stream-max-uncopied", type=int, default=0,

@@ -1957,9 +1957,9 @@ struct fd_gather {             /* mode 3: copy sz bytes from src (host, device v
    behind its completion token), so no release fence is needed: a
    system-scope release per block wrote back the XCD's whole L2 each time,
    under the verify kernels running beside it (2x slower stream).
-   FD_GATHER_RPB records per workgroup, one wave each (ctx->gather_rpb: 4 by default; 1 = round 3's
-   one-wave groups, fdgpu_debug_opts_t.gather_rpb): fewer, larger workgroups for the dispatcher and one
-   counter atomic per group instead of per record. */
+   FD_GATHER_RPB records per workgroup, one wave each (ctx->gather_rpb: 1 by default; 4 =
+   fdgpu_debug_opts_t.gather_rpb, A/B: fewer, larger workgroups for the dispatcher and one counter
+   atomic per group instead of per record). */
 template<int FD_GATHER_RPB>
 __global__ void __launch_bounds__( 64 * FD_GATHER_RPB )
 fd_gather_kernel( fd_gather const * __restrict__ g, u32 n, unsigned char * __restrict__ arena, unsigned char * __restrict__ out,
@@ -2455,7 +2455,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->nofold_max = dbg.nofold_max >= 0 ? (unsigned long)dbg.nofold_max : FD_NOFOLD_MAX;
   ctx->gather_nowb = dbg.gather_no_writeback;
   ctx->poll_pf = dbg.poll_prefetch > 0 ? dbg.poll_prefetch : 0;
-  ctx->gather_rpb = dbg.gather_rpb == 1 ? 1 : 4;
+  ctx->gather_rpb = dbg.gather_rpb == 4 ? 4 : 1;
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
@@ -3024,7 +3024,7 @@ static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
     gt = ctx->d_gtime + 2*i;
     ctx->last_gt = (long)i;
   } else { gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT; ctx->last_gt = -1; }   /* untimed: a scratch entry */
-  unsigned long rpb = ctx->gather_rpb == 1 ? 1UL : 4UL;
+  unsigned long rpb = ctx->gather_rpb == 4 ? 4UL : 1UL;
   hipLaunchKernelGGL( ( rpb == 1UL ? fd_gather_kernel<1> : fd_gather_kernel<4> ), dim3( (unsigned)( ( n + rpb - 1UL ) / rpb ) ),
                       dim3( 64UL * rpb ), 0, ctx->gstream, sl.g_dev + sl.gathered, (u32)n,
                       sl.d_payload, ctx->gather_nowb == 0 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, sl.d_ovr + sl.gathered, ctx->d_gcnt,
