@@ -259,7 +259,14 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
                                                [round(x / n, 1) for x in st["prof_ns"]]))
                                       if any(st["prof_ns"]) else None),
             "inflight_max": st["inflight_max"], "gpu_batch_lat_p50_us_le": hq(0.5),
-            "gpu_batch_lat_p99_us_le": hq(0.99)}
+            "gpu_batch_lat_p99_us_le": hq(0.99),
+            # host contention: the spinning threads' CPU time over their wall time (1.0 = kept their cores),
+            # involuntary context switches, and the CPUs the tiles were pinned to
+            "host_cpu": {"tile_share": round(st["tile_cpu_ns"] / max(st["tile_wall_ns"], 1), 4),
+                         "tile_share_min": round(st["tile_cpu_share_min"], 4), "tile_nivcsw": st["tile_nivcsw"],
+                         "producer_share": round(st["prod_cpu_ns"] / max(st["prod_wall_ns"], 1), 4),
+                         "producer_nivcsw": st["prod_nivcsw"],
+                         "tile_cpus": [c for c in st["tile_cpu"][:min(cfg["tiles"], 8)]]}}
 
 
 def _anon_huge_mb() -> float | None:
@@ -355,7 +362,12 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
         (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else [])
     if args.stream_copy:
         cmd.append("--stream-copy")
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+    env = dict(os.environ)
+    if args.stream_hw_queues:
+        # HIP maps a process's streams onto at most GPU_MAX_HW_QUEUES hardware queues (default 4); streams beyond
+        # that share a queue and serialise behind each other's packets (2 tiles x 2 contexts x 2 streams = 8)
+        env["GPU_MAX_HW_QUEUES"] = str(args.stream_hw_queues)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env)
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
     if r.returncode or not lines:
         raise RuntimeError(f"stream child rc={r.returncode}: {r.stderr[-1500:]}")
@@ -630,6 +642,9 @@ def main():
                     help="verify tiles per GPU of the paced legs (fewer tiles = fewer HIP streams sharing the "
                          "device: 1 tile x 2 contexts p99 0.81 / 0.99 / 1.37 ms at 2 / 5 / 10M frags/s against "
                          "1.09 / 1.16 / 1.61 with 2 tiles, profiles/r03/stream_fused)")
+    ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",
+                    help="GPU_MAX_HW_QUEUES of the tile processes (0 = the runtime's default, 4): hardware queues "
+                         "their HIP streams are spread over")
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="skip the BASELINE configs[0,2,3] side measurements (small / adversarial / multi-sig)")
     ap.add_argument("--stream-child", action="store_true", help=argparse.SUPPRESS)
@@ -717,6 +732,7 @@ def main():
                           "link_depth": args.stream_depth * min(world, 2),
                           "producers": args.stream_producers * world,
                           "engine_contexts_per_tile": args.stream_ctx, "engine_contexts_per_tile_paced": args.stream_lat_ctx,
+                          "tiles_per_gpu_paced": args.stream_lat_tiles, "hw_queues": args.stream_hw_queues or 4,
                           "process": "one tile process per GPU without a torch GPU context (as a C verify tile); "
                                      "link in /dev/shm when G > 1",
                           "intake": "zero-copy (GPU gathers frags from the registered in dcache)"

@@ -13,6 +13,7 @@
 #include <x86intrin.h>
 #include <stdio.h>
 #include <sys/mman.h>
+#include <sys/resource.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <stdatomic.h>
@@ -1106,6 +1107,8 @@ typedef struct {                 /* one tile's results, written once when it fin
   ulong prof[ 8 ];               /* FDGPU_LINK_PROF=1: section times, ns (fdgpu_stream_stats_t prof_ns) */
   fdgpu_vtile_gpu_metrics_t gm;
   ulong device;
+  ulong cpu_ns, wall_ns, nivcsw; /* the tile thread's CPU time over its loop's wall time, involuntary switches */
+  long  cpu;                     /* the CPU it was pinned to (-1: none) */
 } link_res_t;
 
 #define LINK_PROD_MAX FDGPU_VTILE_IN_MAX
@@ -1119,6 +1122,7 @@ typedef struct {
   _Atomic ulong joined, tiles_ready, tiles_done, go, fail;
   ulong         t_start;
   ulong         prod_end[ LINK_PROD_MAX ], prod_wait_ns[ LINK_PROD_MAX ];   /* per producer: last publish, credit waits */
+  ulong         prod_cpu_ns[ LINK_PROD_MAX ], prod_wall_ns[ LINK_PROD_MAX ], prod_nivcsw[ LINK_PROD_MAX ];
   struct { _Atomic ulong v; uchar pad[56]; } fseq[ LINK_PROD_MAX ][ LINK_TILE_MAX ];   /* per link: next seq each tile may lose */
 } link_hdr_t;
 
@@ -1351,6 +1355,15 @@ void  fdgpu_link_cfg( fdgpu_link_t const * l, fdgpu_stream_cfg_t * cfg ) { *cfg 
 typedef struct { fdgpu_link_t * l; int q, cpu; } link_prod_arg_t;
 
 static void link_pin( int cpu );
+
+/* The calling thread's CPU time and involuntary context switches: on a shared host a pinned
+   thread that loses its core to another process shows CPU time below its wall time. */
+static void thread_usage( ulong * cpu_ns, ulong * nivcsw ) {
+  struct timespec ts; struct rusage ru;
+  *cpu_ns = clock_gettime( CLOCK_THREAD_CPUTIME_ID, &ts ) ? 0UL : (ulong)ts.tv_sec * 1000000000UL + (ulong)ts.tv_nsec;
+  *nivcsw = getrusage( RUSAGE_THREAD, &ru ) ? 0UL : (ulong)ru.ru_nivcsw;
+}
+
 /* producer q (one of the reference's QUIC tiles): publishes its frags on its
    own mcache, seq 0 .. n_q-1, frag s pointing at payload (s Q + q) % n_payload */
 static void * link_producer( void * _a ) {
@@ -1378,7 +1391,8 @@ static void * link_producer( void * _a ) {
       if( now_ns() - t_wait0 > 180000000000UL ) { atomic_store( &h->fail, 6 ); return NULL; }
     }
   }
-  ulong t0 = now_ns();
+  ulong t0 = now_ns(), cpu0, iv0;
+  thread_usage( &cpu0, &iv0 );
   double rate = c->rate_fps > 0. ? c->rate_fps / (double)Q : 0.;   /* the offered load, split over the producers */
   mc_line_t * line = l->line[q];
   ulong cr_until = 0UL, wait_ns = 0UL;      /* may publish seq < cr_until */
@@ -1408,6 +1422,9 @@ static void * link_producer( void * _a ) {
   }
   h->prod_wait_ns[q] = wait_ns;
   h->prod_end[q] = now_ns();
+  ulong cpu1, iv1;
+  thread_usage( &cpu1, &iv1 );
+  h->prod_cpu_ns[q] = cpu1 - cpu0; h->prod_wall_ns[q] = h->prod_end[q] - t0; h->prod_nivcsw[q] = iv1 - iv0;
   return NULL;
 }
 
@@ -1418,8 +1435,10 @@ static void * link_producer( void * _a ) {
    before the next -- the mcache lines the producer writes and every tile
    polls then move between cores that share an L3.  Process proc starts
    at the L3 group proc % groups, so the processes of a multi-GPU run do
-   not share cores.  Env FDGPU_LINK_PIN: 0 = no pinning, an explicit
-   comma list of CPUs (producer first, then the tiles), else automatic. */
+   not share cores.  Cores another process kept busy over a 30 ms sample
+   are passed over while enough idle ones remain (a shared host).  Env
+   FDGPU_LINK_PIN: 0 = no pinning, "lowest" = no sample, an explicit comma
+   list of CPUs (producer first, then the tiles), else automatic. */
 #define LINK_CPU_MAX 1024
 static int cpulist_read( char const * path, uchar * set ) {
   FILE * f = fopen( path, "r" );
@@ -1443,6 +1462,33 @@ static int cpu_first_of( char const * fmt, int cpu ) {          /* lowest CPU of
   for( int i=0; i<LINK_CPU_MAX; i++ ) if( set[i] ) return i;
   return cpu;
 }
+/* Busy fraction of each CPU over `ms` milliseconds (/proc/stat): the cores another process keeps busy
+   are not worth pinning a spinning tile to.  Returns 0 on success. */
+static int cpu_busy_sample( double * busy, int ms ) {
+  static ulong t0[ LINK_CPU_MAX ], i0[ LINK_CPU_MAX ];
+  for( int pass=0; pass<2; pass++ ) {
+    FILE * f = fopen( "/proc/stat", "r" );
+    if( !f ) return -1;
+    char line[ 512 ];
+    while( fgets( line, sizeof(line), f ) ) {
+      int cpu; ulong v[8] = { 0 };
+      if( strncmp( line, "cpu", 3 ) || line[3] < '0' || line[3] > '9' ) continue;
+      if( sscanf( line + 3, "%d %lu %lu %lu %lu %lu %lu %lu %lu", &cpu, v, v+1, v+2, v+3, v+4, v+5, v+6, v+7 ) < 5 ) continue;
+      if( cpu < 0 || cpu >= LINK_CPU_MAX ) continue;
+      ulong tot = 0UL; for( int k=0; k<8; k++ ) tot += v[k];
+      ulong idle = v[3] + v[4];                                  /* idle + iowait */
+      if( !pass ) { t0[cpu] = tot; i0[cpu] = idle; }
+      else {
+        ulong dt = tot - t0[cpu], di = idle - i0[cpu];
+        busy[cpu] = dt ? 1. - (double)di / (double)dt : 0.;
+      }
+    }
+    fclose( f );
+    if( !pass ) usleep( (useconds_t)ms * 1000U );
+  }
+  return 0;
+}
+
 static int
 link_pick_cpus( int device, int proc, int n, int * out ) {
   char const * env = getenv( "FDGPU_LINK_PIN" );
@@ -1462,21 +1508,40 @@ link_pick_cpus( int device, int proc, int n, int * out ) {
     char path[ 96 ]; snprintf( path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node );
     use_node = !cpulist_read( path, node_set );
   }
+  /* a shared machine: skip cores (either hardware thread) that another process kept busy over a short
+     sample, unless too few idle ones are left (FDGPU_LINK_PIN=lowest: no sample, the lowest cores) */
+  static double busy[ LINK_CPU_MAX ];
+  memset( busy, 0, sizeof(busy) );
+  if( !( env && !strcmp( env, "lowest" ) ) ) cpu_busy_sample( busy, 30 );
   /* candidate cores: one hardware thread (the lowest sibling) of each allowed core */
   int cand[ LINK_CPU_MAX ], grp[ LINK_CPU_MAX ], nc = 0;
+  uchar hot[ LINK_CPU_MAX ];
+  static uchar sib[ LINK_CPU_MAX ];
   for( int pass=0; pass<2 && !nc; pass++ )                       /* pass 1: ignore the node if it has no allowed CPU */
     for( int c=0; c<LINK_CPU_MAX && c<CPU_SETSIZE; c++ ) {
       if( !CPU_ISSET( c, &aff ) || ( pass==0 && use_node && !node_set[c] ) ) continue;
       if( cpu_first_of( "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c ) != c ) continue;
+      char path[ 160 ];
+      snprintf( path, sizeof(path), "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c );
+      memset( sib, 0, sizeof(sib) ); sib[c] = 1;
+      cpulist_read( path, sib );
+      double b = 0.;
+      for( int k=0; k<LINK_CPU_MAX; k++ ) if( sib[k] && busy[k] > b ) b = busy[k];
+      hot[nc] = b > 0.25;
       cand[nc] = c; grp[nc] = cpu_first_of( "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", c ); nc++;
     }
   if( !nc ) return 0;
   int gid[ LINK_CPU_MAX ], ng = 0;                               /* L3 groups in CPU order */
   for( int i=0; i<nc; i++ ) { int k=0; while( k<ng && gid[k] != grp[i] ) k++; if( k==ng ) gid[ng++] = grp[i]; }
-  for( int r=0; r<ng && got<n; r++ ) {
-    int g = gid[ ( proc + r ) % ng ];
-    for( int i=0; i<nc && got<n; i++ ) if( grp[i] == g ) out[got++] = cand[i];
-  }
+  for( int pass=0; pass<2 && got<n; pass++ )                    /* pass 0: idle cores only, then the rest */
+    for( int r=0; r<ng && got<n; r++ ) {
+      int g = gid[ ( proc + r ) % ng ];
+      for( int i=0; i<nc && got<n; i++ ) {
+        if( grp[i] != g || ( pass==0 && hot[i] ) ) continue;
+        int dup = 0; for( int k=0; k<got; k++ ) dup |= out[k] == cand[i];
+        if( !dup ) out[got++] = cand[i];
+      }
+    }
   return got;
 }
 static void link_pin( int cpu ) {
@@ -1600,7 +1665,8 @@ static void * link_tile( void * _a ) {
   ulong last_prog = ~0UL, t_prog = now_ns(), q0 = 0UL;
   ulong per_link = Q > 1UL ? ( 64UL / Q > 8UL ? 64UL / Q : 8UL ) : 64UL;   /* own frags per link per pass */
   ulong pfl = c->pf_dist > 0 ? (ulong)c->pf_dist : 1UL, pfh = pfl > 1UL ? pfl / 2UL : 1UL;   /* prefetch distances */
-  ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, ns_idle = 0UL, t_begin = now_ns();
+  ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, ns_idle = 0UL, t_begin = now_ns(), cpu0, iv0;
+  thread_usage( &cpu0, &iv0 );
   /* FDGPU_LINK_PROF=1: rdtsc section profile (mcache poll, during_frag, prefetch + credit, drain
      after_frags, housekeep after_frags, link_account, credit after a drain, housekeep) */
   int prof = c->prof;
@@ -1724,6 +1790,9 @@ static void * link_tile( void * _a ) {
   r->ns[0] = ns_in; r->ns[1] = ns_after; r->ns[2] = ns_hk; r->ns[3] = t_end - t_begin; r->ns_idle = ns_idle;
   fdgpu_vtile_gpu_metrics( vt, &r->gm );
   r->device = (ulong)a->device;
+  ulong cpu1, iv1;
+  thread_usage( &cpu1, &iv1 );
+  r->cpu_ns = cpu1 - cpu0; r->wall_ns = t_end - t_begin; r->nivcsw = iv1 - iv0; r->cpu = a->cpu;
   memcpy( l->hist + (ulong)idx * LH_N, lh, LH_N * sizeof(ulong) );
   atomic_fetch_add_explicit( &h->tiles_done, 1UL, memory_order_release );
   free( done ); free( lh );
@@ -1814,6 +1883,10 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     }
     st->copy_backlog += r->gm.copy_backlog;
     st->tile_idle_ns += r->ns_idle;
+    st->tile_cpu_ns += r->cpu_ns; st->tile_wall_ns += r->wall_ns; st->tile_nivcsw += r->nivcsw;
+    double share = r->wall_ns ? (double)r->cpu_ns / (double)r->wall_ns : 1.;
+    if( i == 0 || share < st->tile_cpu_share_min ) st->tile_cpu_share_min = share;
+    if( i < 8 ) st->tile_cpu[i] = r->cpu;
     for( int k=0; k<8; k++ ) st->prof_ns[k] += r->prof[k];
     if( r->t_last > t_end ) t_end = r->t_last;
     if( r->lmax > lmax ) lmax = r->lmax;
@@ -1823,6 +1896,7 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
   for( int q=0; q<c->producers; q++ ) {
     if( h->prod_end[q] > prod_end ) prod_end = h->prod_end[q];
     st->prod_wait_ns += h->prod_wait_ns[q];
+    st->prod_cpu_ns += h->prod_cpu_ns[q]; st->prod_wall_ns += h->prod_wall_ns[q]; st->prod_nivcsw += h->prod_nivcsw[q];
   }
   st->seconds = t_end > h->t_start ? (double)( t_end - h->t_start ) * 1e-9 : 0.;
   st->prod_seconds = prod_end > h->t_start ? (double)( prod_end - h->t_start ) * 1e-9 : 0.;

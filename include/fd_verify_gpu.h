@@ -406,6 +406,12 @@ typedef struct fdgpu_stream_stats {
   unsigned long gather_gpu[ 5 ];  /* fdgpu_vtile_gpu_metrics_t.gather_gpu, summed (maxima: max) over tiles */
   unsigned long phase[ 9 ];       /* fdgpu_vtile_gpu_metrics_t.phase, summed (maxima: max) over tiles */
   unsigned long copy_backlog;     /* fdgpu_vtile_gpu_metrics_t.copy_backlog, summed over tiles */
+  /* host contention (a shared machine): the threads' CPU time against their loops' wall time, and the
+     involuntary context switches they took -- a pinned spinning thread that keeps its core shows 1.0 and 0 */
+  unsigned long tile_cpu_ns, tile_wall_ns, tile_nivcsw;   /* summed over tiles */
+  double        tile_cpu_share_min;                       /* the lowest tile's cpu_ns / wall_ns */
+  long          tile_cpu[ 8 ];                            /* the CPUs tiles 0..7 were pinned to (-1: none) */
+  unsigned long prod_cpu_ns, prod_wall_ns, prod_nivcsw;   /* summed over producers */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per
