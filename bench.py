@@ -187,7 +187,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
                 copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus,
                 max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
-                huge_pages=1 if args.stream_huge else 0)
+                no_huge_pages=1 if args.stream_no_huge else 0)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -297,10 +297,10 @@ def stream_child_main(args) -> None:
         if n:
             anom[leg] = {"count": n, "first": first[:8]}
     wb = {"gather": 0, "none": 1, "finish": 2}[args.stream_writeback]
-    if wb or args.stream_poll_prefetch or args.stream_gather_rpb:
+    if wb or args.stream_poll_prefetch or args.stream_gather_rpb or args.stream_gather_cu_spread:
         from firedancer_amd import engine
         engine.debug_set_opts(gather_no_writeback=wb, poll_prefetch=args.stream_poll_prefetch,
-                              gather_rpb=args.stream_gather_rpb)
+                              gather_rpb=args.stream_gather_rpb, gather_cu_spread=args.stream_gather_cu_spread)
     payload = desc = None
     if proc == 0:
         from firedancer_amd import synth
@@ -358,8 +358,9 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
            "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus),
            "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
-        (["--stream-prof"] if args.stream_prof else []) + (["--stream-huge"] if args.stream_huge else []) + \
-        (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else [])
+        (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else []) + \
+        (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else []) + \
+        (["--stream-gather-cu-spread", str(args.stream_gather_cu_spread)] if args.stream_gather_cu_spread else [])
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -618,9 +619,12 @@ def main():
     ap.add_argument("--stream-first", action="store_true",
                     help="run the configs[4] stream legs before the headline, before this process initialises the GPU")
     ap.add_argument("--stream-gather-rpb", type=int, default=0,
-                    help="(stream child, A/B) records per gather workgroup (fdgpu_debug_opts_t.gather_rpb; 0 = default 1)")
-    ap.add_argument("--stream-huge", action="store_true",
-                    help="(A/B) the link region in transparent huge pages instead of 4 KiB pages")
+                    help="(stream child, A/B) records per gather workgroup (fdgpu_debug_opts_t.gather_rpb; 0 = default 4)")
+    ap.add_argument("--stream-no-huge", action="store_true",
+                    help="(A/B) the link region in 4 KiB pages instead of transparent huge pages")
+    ap.add_argument("--stream-gather-cu-spread", type=int, default=0, choices=(0, 1, 2),
+                    help="(stream child, A/B) the CUs each tile context reserves for its gathers: 0 the last n, "
+                         "1 every (CUs/n)-th, 2 the first n (fdgpu_debug_opts_t.gather_cu_spread)")
     ap.add_argument("--stream-prof", action="store_true",
                     help="rdtsc section profile of the tile loop (fdgpu_stream_cfg_t.prof), in each leg's summary")
     ap.add_argument("--stream-max-uncopied", type=int, default=0,

@@ -1957,9 +1957,9 @@ struct fd_gather {             /* mode 3: copy sz bytes from src (host, device v
    behind its completion token), so no release fence is needed: a
    system-scope release per block wrote back the XCD's whole L2 each time,
    under the verify kernels running beside it (2x slower stream).
-   FD_GATHER_RPB records per workgroup, one wave each (ctx->gather_rpb: 1 by default; 4 =
-   fdgpu_debug_opts_t.gather_rpb, A/B: fewer, larger workgroups for the dispatcher and one counter
-   atomic per group instead of per record). */
+   FD_GATHER_RPB records per workgroup, one wave each (ctx->gather_rpb: 4 by default -- fewer, larger
+   workgroups for the dispatcher and one counter atomic per group instead of per record: with the link
+   in huge pages, max rate 21.7M vs 20.1M sigs/s, profiles/r04/i; 1 = fdgpu_debug_opts_t.gather_rpb). */
 template<int FD_GATHER_RPB>
 __global__ void __launch_bounds__( 64 * FD_GATHER_RPB )
 fd_gather_kernel( fd_gather const * __restrict__ g, u32 n, unsigned char * __restrict__ arena, unsigned char * __restrict__ out,
@@ -2107,6 +2107,7 @@ struct fdgpu_ed25519_ctx {
   int dsm_lanes;                 /* latency path: lanes per signature in the DSM, 0 = by batch size (fdgpu_debug_opts_t) */
   int poll_pf;                   /* fdgpu_debug_opts_t.poll_prefetch */
   int gather_rpb;                /* fd_gather_kernel records per workgroup (fdgpu_debug_opts_t.gather_rpb) */
+  int gather_cu_spread;          /* which CUs reserve_gather_cus takes (fdgpu_debug_opts_t.gather_cu_spread) */
   int gather_nowb;               /* fdgpu_debug_opts_t.gather_no_writeback: 0 = the records' write-back in
                                     the gather kernel, 1 = none (diagnostic), 2 = in fd_finish_kernel (A/B) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
@@ -2365,14 +2366,14 @@ extern "C" void fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx );
 /* Test / A/B options of contexts created from now on (fdgpu_debug_set_opts).
    Process-wide, behind a mutex; the defaults are the product's choices. */
 static std::mutex g_dbg_mu;
-static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L, 0, 0, 0 };
+static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L, 0, 0, 0, 0 };
 static void debug_opts_get( fdgpu_debug_opts_t * o ) { std::lock_guard<std::mutex> lk( g_dbg_mu ); *o = g_dbg; }
 
 extern "C" void
 fdgpu_debug_set_opts( fdgpu_debug_opts_t const * opts ) {
   std::lock_guard<std::mutex> lk( g_dbg_mu );
   if( opts ) g_dbg = *opts;
-  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L, 0, 0, 0 };
+  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L, 0, 0, 0, 0 };
 }
 
 /* staging + device buffers of async slot i (once) */
@@ -2455,7 +2456,8 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->nofold_max = dbg.nofold_max >= 0 ? (unsigned long)dbg.nofold_max : FD_NOFOLD_MAX;
   ctx->gather_nowb = dbg.gather_no_writeback;
   ctx->poll_pf = dbg.poll_prefetch > 0 ? dbg.poll_prefetch : 0;
-  ctx->gather_rpb = dbg.gather_rpb == 4 ? 4 : 1;
+  ctx->gather_rpb = dbg.gather_rpb == 1 ? 1 : 4;
+  ctx->gather_cu_spread = dbg.gather_cu_spread;
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
@@ -3024,7 +3026,7 @@ static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
     gt = ctx->d_gtime + 2*i;
     ctx->last_gt = (long)i;
   } else { gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT; ctx->last_gt = -1; }   /* untimed: a scratch entry */
-  unsigned long rpb = ctx->gather_rpb == 4 ? 4UL : 1UL;
+  unsigned long rpb = ctx->gather_rpb == 1 ? 1UL : 4UL;
   hipLaunchKernelGGL( ( rpb == 1UL ? fd_gather_kernel<1> : fd_gather_kernel<4> ), dim3( (unsigned)( ( n + rpb - 1UL ) / rpb ) ),
                       dim3( 64UL * rpb ), 0, ctx->gstream, sl.g_dev + sl.gathered, (u32)n,
                       sl.d_payload, ctx->gather_nowb == 0 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, sl.d_ovr + sl.gathered, ctx->d_gcnt,
@@ -3463,7 +3465,13 @@ fdgpu_ed25519_reserve_gather_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n ) {
   HIPCHK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, ctx->device ), -2 );
   if( (int)n >= ncu ) { fd_err = "fdgpu_ed25519_reserve_gather_cus: n >= CUs"; return -1; }
   std::vector<uint32_t> cm( (size_t)( ncu + 31 ) / 32, 0u ), gm( cm.size(), 0u );
-  for( int c=0; c<ncu; c++ ) ( c >= ncu - (int)n ? gm : cm )[ (size_t)c / 32 ] |= 1u << ( c % 32 );
+  /* the last n CUs (default); gather_cu_spread 1: every (ncu/n)-th CU; 2: the first n (A/B) */
+  int stride = ncu / (int)n;
+  for( int c=0; c<ncu; c++ ) {
+    int mine = ctx->gather_cu_spread == 1 ? ( c % stride == stride - 1 && c / stride < (int)n )
+             : ctx->gather_cu_spread == 2 ? c < (int)n : c >= ncu - (int)n;
+    ( mine ? gm : cm )[ (size_t)c / 32 ] |= 1u << ( c % 32 );
+  }
   hipStream_t s = NULL, g = NULL;
   HIPCHK( hipExtStreamCreateWithCUMask( &s, (uint32_t)cm.size(), cm.data() ), -2 );
   hipError_t e = hipExtStreamCreateWithCUMask( &g, (uint32_t)gm.size(), gm.data() );
@@ -3533,7 +3541,6 @@ static unsigned long
 poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes, unsigned char * out_img,
           unsigned short * out_fp, unsigned long * out_dtag, unsigned long max, int blocking ) {
   if( ctx->fault ) return 0;             /* faulted: nothing more completes (never block on it) */
-  hipSetDevice( ctx->device );
   unsigned long n = 0;
   while( n < max && !ctx->inflight.empty() ) {
     int i = ctx->inflight.front();
@@ -3548,6 +3555,7 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
         unsigned long now = fd_now_ns();
         if( now - sl.launch_ns > 2000000UL && now - sl.last_query > 1000000UL ) {
           sl.last_query = now;
+          (void)hipSetDevice( ctx->device );   /* (only here: the poll itself reads host memory) */
           hipError_t e = hipEventQuery( sl.done );
           if( e != hipSuccess && e != hipErrorNotReady ) { set_err( "fdgpu_ed25519_poll: batch failed", e ); ctx->fault = 1; break; }
           if( e == hipSuccess && ctx->h_flag[i] == sl.token ) { ready = 1; break; }

@@ -1208,18 +1208,18 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   if( !shared ) {
     /* The reference's links live in workspaces of huge (2 MiB) or gigantic pages (fd_wksp); the GPU reads
        this region frag by frag over PCIe (zero-copy intake), and with 4 KiB pages every frag is a GPU TLB
-       miss in a 1+ GB region.  cfg.huge_pages (A/B): transparent huge pages where the kernel allows them
-       (madvise mode), a 2 MiB aligned region advised before first touch. */
+       miss in a 1+ GB region.  Transparent huge pages where the kernel allows them (madvise mode): a 2 MiB
+       aligned region advised before first touch (cfg.no_huge_pages: 4 KiB pages, A/B). */
     ulong const huge = 2UL << 20;
-    map_sz = total + ( cfg->huge_pages ? huge : 0UL );
+    map_sz = total + ( cfg->no_huge_pages ? 0UL : huge );
     map = (uchar *)mmap( NULL, map_sz, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0 );
     if( map == MAP_FAILED ) return NULL;
     base = map;
-    if( cfg->huge_pages ) {
+    if( !cfg->no_huge_pages ) {
       base = (uchar *)( ( (ulong)map + huge - 1UL ) & ~( huge - 1UL ) );
       (void)madvise( base, total, MADV_HUGEPAGE );   /* whole 2 MiB extents in it become huge pages */
     }
-  } else if( cfg->huge_pages ) {
+  } else if( !cfg->no_huge_pages ) {
     (void)madvise( base, total, MADV_HUGEPAGE );    /* shmem: honoured only where shmem_enabled allows it */
   }
   fdgpu_link_t * l = (fdgpu_link_t *)calloc( 1, sizeof(fdgpu_link_t) );

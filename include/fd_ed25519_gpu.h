@@ -616,7 +616,9 @@ typedef struct fdgpu_debug_opts {
                                         1 = DIAGNOSTIC, none (published records lack their payload) */
   int           poll_prefetch;       /* completions polled: software prefetch this many entries ahead in the
                                         GPU-written result arrays (0: none, A/B) */
-  int           gather_rpb;          /* records per workgroup of the gather kernel: 0 = default (1), 4 = four (A/B) */
+  int           gather_rpb;          /* records per workgroup of the gather kernel: 0 = default (4), 1 = one (A/B) */
+  int           gather_cu_spread;    /* the CUs a tile context reserves for its gathers: 0 = the last n (default),
+                                        1 = every (CUs/n)-th, 2 = the first n (A/B) */
 } fdgpu_debug_opts_t;
 
 void

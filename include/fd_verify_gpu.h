@@ -374,8 +374,9 @@ typedef struct fdgpu_stream_cfg {
   int           pf_dist;         /* tile loop prefetch distance, in own frags: the mcache line pf_dist ahead and
                                     the record header of the frag pf_dist/2 ahead (0 = 1: the next own frag's
                                     line and header; 4 and 8 measured the same, profiles/r03/prep_pf_ab) */
-  int           huge_pages;      /* 1: the link region in 2 MiB transparent huge pages where the kernel allows them
-                                    (madvise), as the reference's workspaces use huge pages (A/B); 0: 4 KiB pages */
+  int           no_huge_pages;   /* 1: the link region in 4 KiB pages (A/B); 0: 2 MiB transparent huge pages where the
+                                    kernel allows them (madvise), as the reference's workspaces use huge pages (max rate
+                                    +4 %, profiles/r04/i) */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
