@@ -149,7 +149,10 @@ def cpu_sweep_configs0(impl, kind, max_threads, gen_threads, point_s=0.6):
 # G > 1 the link lives in a /dev/shm file that rank 0's child creates and the other ranks' children join.
 
 def stream_legs(args) -> list[str]:
-    """cal, max, one paced leg per --stream-rates entry (frags/s per GPU), unrel"""
+    """cal, max, one paced leg per --stream-rates entry (frags/s per GPU), unrel (--stream-only-paced: the paced
+    legs alone, e.g. under a kernel trace)"""
+    if getattr(args, "stream_only_paced", False):
+        return [f"paced@{r}" for r in _rates(args)]
     return ["cal", "max"] + [f"paced@{r}" for r in _rates(args)] + ["unrel"]
 
 
@@ -360,7 +363,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
         (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else []) + \
         (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else []) + \
-        (["--stream-gather-cu-spread", str(args.stream_gather_cu_spread)] if args.stream_gather_cu_spread else [])
+        (["--stream-gather-cu-spread", str(args.stream_gather_cu_spread)] if args.stream_gather_cu_spread else []) + \
+        (["--stream-only-paced"] if args.stream_only_paced else [])
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -440,6 +444,8 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
     if st:
         if "error" in st:
             rec["stream"] = {"error": str(st["error"])[-300:]}
+        elif "only_paced" in st:
+            rec["stream"] = {"only_paced": {k: [_r(v["p50_us"]), _r(v["p99_us"])] for k, v in st["only_paced"].items()}}
         else:
             curve = st.get("latency_curve") or []
             rec["stream"] = {
@@ -646,6 +652,8 @@ def main():
                     help="verify tiles per GPU of the paced legs (fewer tiles = fewer HIP streams sharing the "
                          "device: 1 tile x 2 contexts p99 0.81 / 0.99 / 1.37 ms at 2 / 5 / 10M frags/s against "
                          "1.09 / 1.16 / 1.61 with 2 tiles, profiles/r03/stream_fused)")
+    ap.add_argument("--stream-only-paced", action="store_true",
+                    help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",
                     help="GPU_MAX_HW_QUEUES of the tile processes (0 = the runtime's default, 4): hardware queues "
                          "their HIP streams are spread over")
@@ -712,7 +720,9 @@ def main():
                 m["count"] += v["count"]
                 m["first"] = (m["first"] + [dict(e, rank=r) for e in v["first"]])[:8]
         if rank == 0:
-            if res is not None and stream_ok:
+            if res is not None and stream_ok and args.stream_only_paced:
+                rec["stream"] = {"only_paced": {k: v for k, v in res["legs"].items()}, "anomalies": anomalies}
+            elif res is not None and stream_ok:
                 legs = res["legs"]
                 mx, ur = legs["max"], legs["unrel"]
                 curve = [dict(legs[f"paced@{r}"], offered_frags_per_s_per_gpu=r) for r in _rates(args)]
