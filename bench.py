@@ -190,7 +190,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
                 copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus,
                 max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
-                no_huge_pages=1 if args.stream_no_huge else 0)
+                no_huge_pages=1 if args.stream_no_huge else 0,
+                cu_split=(args.stream_lat_cu_split if paced else args.stream_cu_split))
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -364,7 +365,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
         (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else []) + \
         (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else []) + \
         (["--stream-gather-cu-spread", str(args.stream_gather_cu_spread)] if args.stream_gather_cu_spread else []) + \
-        (["--stream-only-paced"] if args.stream_only_paced else [])
+        (["--stream-only-paced"] if args.stream_only_paced else []) + \
+        ["--stream-cu-split", str(args.stream_cu_split), "--stream-lat-cu-split", str(args.stream_lat_cu_split)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -652,6 +654,10 @@ def main():
                     help="verify tiles per GPU of the paced legs (fewer tiles = fewer HIP streams sharing the "
                          "device: 1 tile x 2 contexts p99 0.81 / 0.99 / 1.37 ms at 2 / 5 / 10M frags/s against "
                          "1.09 / 1.16 / 1.61 with 2 tiles, profiles/r03/stream_fused)")
+    ap.add_argument("--stream-cu-split", type=int, default=0, choices=(0, 1),
+                    help="max-rate legs: each tile's engine contexts on disjoint CU shares (fdgpu_vtile_opts_t.cu_split)")
+    ap.add_argument("--stream-lat-cu-split", type=int, default=0, choices=(0, 1),
+                    help="paced legs: each tile's engine contexts on disjoint CU shares (fdgpu_vtile_opts_t.cu_split)")
     ap.add_argument("--stream-only-paced", action="store_true",
                     help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",
@@ -721,7 +727,7 @@ def main():
                 m["first"] = (m["first"] + [dict(e, rank=r) for e in v["first"]])[:8]
         if rank == 0:
             if res is not None and stream_ok and args.stream_only_paced:
-                rec["stream"] = {"only_paced": {k: v for k, v in res["legs"].items()}, "anomalies": anomalies}
+                stream = {"only_paced": dict(res["legs"]), "anomalies": anomalies}
             elif res is not None and stream_ok:
                 legs = res["legs"]
                 mx, ur = legs["max"], legs["unrel"]

@@ -3456,21 +3456,31 @@ fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 5 ] ) 
 
 extern "C" int
 fdgpu_ed25519_reserve_gather_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n ) {
+  return fdgpu_ed25519_reserve_cus( ctx, n, 0u, 1u );
+}
+
+extern "C" int
+fdgpu_ed25519_reserve_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n, unsigned part, unsigned parts ) {
   if( !ctx || ctx->gstream || !ctx->inflight.empty() || ctx->slot[ ctx->cur ].txn_cnt ) {
-    fd_err = "fdgpu_ed25519_reserve_gather_cus: only on a fresh context"; return -1;
+    fd_err = "fdgpu_ed25519_reserve_cus: only on a fresh context"; return -1;
   }
+  if( !parts || part >= parts ) { fd_err = "fdgpu_ed25519_reserve_cus: part >= parts"; return -1; }
   if( !n ) return 0;
   HIPCHK( hipSetDevice( ctx->device ), -2 );
   int ncu = 0;
   HIPCHK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, ctx->device ), -2 );
   if( (int)n >= ncu ) { fd_err = "fdgpu_ed25519_reserve_gather_cus: n >= CUs"; return -1; }
   std::vector<uint32_t> cm( (size_t)( ncu + 31 ) / 32, 0u ), gm( cm.size(), 0u );
-  /* the last n CUs (default); gather_cu_spread 1: every (ncu/n)-th CU; 2: the first n (A/B) */
-  int stride = ncu / (int)n;
+  /* the last n CUs (default); gather_cu_spread 1: every (ncu/n)-th CU; 2: the first n (A/B).  The
+     verify kernels get the rest, or with parts > 1 the part-th of `parts` contiguous shares of the rest */
+  int stride = ncu / (int)n, nrest = ncu - (int)n, i = 0;
+  if( nrest < (int)parts ) { fd_err = "fdgpu_ed25519_reserve_cus: fewer CUs than parts"; return -1; }
   for( int c=0; c<ncu; c++ ) {
     int mine = ctx->gather_cu_spread == 1 ? ( c % stride == stride - 1 && c / stride < (int)n )
              : ctx->gather_cu_spread == 2 ? c < (int)n : c >= ncu - (int)n;
-    ( mine ? gm : cm )[ (size_t)c / 32 ] |= 1u << ( c % 32 );
+    if( mine ) { gm[ (size_t)c / 32 ] |= 1u << ( c % 32 ); continue; }
+    if( (unsigned)( (long)i * (long)parts / (long)nrest ) == part ) cm[ (size_t)c / 32 ] |= 1u << ( c % 32 );
+    i++;
   }
   hipStream_t s = NULL, g = NULL;
   HIPCHK( hipExtStreamCreateWithCUMask( &s, (uint32_t)cm.size(), cm.data() ), -2 );

@@ -404,7 +404,7 @@ struct fdgpu_vtile {
    when frags back up (high load: the throughput path, whose per-signature
    work is 0.5x the 4-lane DSM's). */
 static fdgpu_ed25519_ctx_t *
-vt_ctx_new( fdgpu_vtile_t const * vt ) {
+vt_ctx_new( fdgpu_vtile_t const * vt, int k ) {
   ulong b = vt->batch;
   fdgpu_ed25519_ctx_t * c = fdgpu_ed25519_ctx_new( vt->device, b, 16UL*b, b*2304UL + 1024UL, vt->semantics );
   if( c ) {
@@ -414,7 +414,8 @@ vt_ctx_new( fdgpu_vtile_t const * vt ) {
     /* the GPU computes the HA dedup tags and, for gathered records, stores
        txn_t_sz: after_frag then touches neither payload nor record */
     fdgpu_ed25519_set_dedup( c, vt->gpu_tag, vt->seed );
-    if( vt->opt.gather_cus && fdgpu_ed25519_reserve_gather_cus( c, vt->opt.gather_cus ) ) {
+    unsigned parts = vt->opt.cu_split ? (unsigned)vt->nctx : 1u, part = vt->opt.cu_split ? (unsigned)k : 0u;
+    if( vt->opt.gather_cus && fdgpu_ed25519_reserve_cus( c, vt->opt.gather_cus, part, parts ) ) {
       fdgpu_ed25519_ctx_delete( c ); return NULL;
     }
     fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
@@ -453,7 +454,7 @@ fdgpu_vtile_new_opts( int device, ulong batch_txn, ulong tcache_depth, ulong see
   vt->gpu_tag = !vt->opt.host_dedup_tag;
   vt->min_batch = vt->opt.min_batch; vt->max_wait_ns = vt->opt.max_wait_ns;
   int ctx_ok = 1;
-  for( int k=0; k<vt->nctx; k++ ) if( !( vt->ctx[k] = vt_ctx_new( vt ) ) ) ctx_ok = 0;
+  for( int k=0; k<vt->nctx; k++ ) if( !( vt->ctx[k] = vt_ctx_new( vt, k ) ) ) ctx_ok = 0;
   vt->tcache = fdgpu_tcache_new( tcache_depth );
   ulong nchunk = ( out_dcache_bytes / FDGPU_CHUNK_SZ ) & ~1UL;
   vt->dcache = (uchar *)fdgpu_host_alloc( nchunk * FDGPU_CHUNK_SZ );   /* pinned: batches upload from it in place */
@@ -541,7 +542,7 @@ fdgpu_vtile_recover( fdgpu_vtile_t * vt ) {
     for( ulong q=vt->pend_head; q<vt->pend_tail && !busy; q++ ) busy = vt->pend[ q % vt->pend_cap ].k == k;
     if( busy ) { rc = -1; continue; }
     /* the replacement first: if it cannot be made, the faulted context stays (and stays skipped) */
-    fdgpu_ed25519_ctx_t * c = vt_ctx_new( vt );
+    fdgpu_ed25519_ctx_t * c = vt_ctx_new( vt, k );
     if( !c ) { if( !rc ) rc = -2; continue; }
     fdgpu_ed25519_ctx_delete( vt->ctx[k] );
     vt->ctx[k] = c;
@@ -1633,7 +1634,7 @@ static void * link_tile( void * _a ) {
   fdgpu_vtile_opts_t vo;
   memset( &vo, 0, sizeof(vo) );
   vo.nctx = c->nctx; vo.copy_wait_ns = c->copy_wait_ns; vo.copy_min = c->copy_min; vo.gather_cus = c->gather_cus;
-  vo.max_uncopied = c->max_uncopied;
+  vo.max_uncopied = c->max_uncopied; vo.cu_split = c->cu_split;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                              ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }

@@ -498,6 +498,11 @@ unsigned long fdgpu_ed25519_gather_launched( fdgpu_ed25519_ctx_t const * ctx );
    Only on a fresh context (before any submit).  0, or < 0 (e.g. the
    runtime refused CU masks: the context is unchanged). */
 int           fdgpu_ed25519_reserve_gather_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n );
+/* The same, with the verify kernels confined to the part-th of `parts`
+   equal shares of the CUs the gathers leave (reserve_gather_cus = part 0
+   of 1): the contexts of one tile, given parts 0..parts-1, never place
+   their concurrent batches' waves on the same SIMDs. */
+int           fdgpu_ed25519_reserve_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n, unsigned part, unsigned parts );
 /* gathers timed on the GPU clock (mapped to host time once): out[0] how
    many, out[1] / out[2] the sum / max of host launch -> first block's
    start, out[3] / out[4] the sum / max of first block's start -> last

@@ -203,6 +203,9 @@ typedef struct fdgpu_vtile_opts {
   unsigned int  gather_cus;      /* CUs of the GPU reserved for the copies (fdgpu_ed25519_reserve_gather_cus; 0 = none) */
   unsigned long max_uncopied;    /* zero-copy: frags taken whose copy has not completed, at most (0 =
                                     FDGPU_VTILE_MAX_UNCOPIED); at the bound during_frag returns FDGPU_VTILE_COPY_BACKLOG */
+  int           cu_split;        /* 1 (with gather_cus): context k's verify kernels run on the k-th of nctx disjoint
+                                    shares of the other CUs (fdgpu_ed25519_reserve_cus), so the staggered batches
+                                    of one tile do not share SIMDs; 0: every context on all of them */
 } fdgpu_vtile_opts_t;
 
 fdgpu_vtile_t * fdgpu_vtile_new( int device, unsigned long batch_txn, unsigned long tcache_depth, unsigned long seed,
@@ -374,6 +377,7 @@ typedef struct fdgpu_stream_cfg {
   int           pf_dist;         /* tile loop prefetch distance, in own frags: the mcache line pf_dist ahead and
                                     the record header of the frag pf_dist/2 ahead (0 = 1: the next own frag's
                                     line and header; 4 and 8 measured the same, profiles/r03/prep_pf_ab) */
+  int           cu_split;        /* fdgpu_vtile_opts_t.cu_split of every tile */
   int           no_huge_pages;   /* 1: the link region in 4 KiB pages (A/B); 0: 2 MiB transparent huge pages where the
                                     kernel allows them (madvise), as the reference's workspaces use huge pages (max rate
                                     +4 %, profiles/r04/i) */
