@@ -191,7 +191,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus,
                 max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
                 no_huge_pages=1 if args.stream_no_huge else 0,
-                cu_split=(args.stream_lat_cu_split if paced else args.stream_cu_split))
+                cu_split=(args.stream_lat_cu_split if paced else args.stream_cu_split),
+                cu_exclusive=args.stream_cu_exclusive)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -366,7 +367,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
         (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else []) + \
         (["--stream-gather-cu-spread", str(args.stream_gather_cu_spread)] if args.stream_gather_cu_spread else []) + \
         (["--stream-only-paced"] if args.stream_only_paced else []) + \
-        ["--stream-cu-split", str(args.stream_cu_split), "--stream-lat-cu-split", str(args.stream_lat_cu_split)]
+        ["--stream-cu-split", str(args.stream_cu_split), "--stream-lat-cu-split", str(args.stream_lat_cu_split),
+         "--stream-cu-exclusive", str(args.stream_cu_exclusive)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -658,6 +660,8 @@ def main():
                     help="max-rate legs: each tile's engine contexts on disjoint CU shares (fdgpu_vtile_opts_t.cu_split)")
     ap.add_argument("--stream-lat-cu-split", type=int, default=0, choices=(0, 1),
                     help="paced legs: each tile's engine contexts on disjoint CU shares (fdgpu_vtile_opts_t.cu_split)")
+    ap.add_argument("--stream-cu-exclusive", type=int, default=0, choices=(0, 1),
+                    help="every leg: latency-path workgroups alone on their CU (fdgpu_vtile_opts_t.cu_exclusive)")
     ap.add_argument("--stream-only-paced", action="store_true",
                     help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",

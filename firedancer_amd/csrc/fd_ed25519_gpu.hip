@@ -2111,6 +2111,8 @@ struct fdgpu_ed25519_ctx {
   int gather_nowb;               /* fdgpu_debug_opts_t.gather_no_writeback: 0 = the records' write-back in
                                     the gather kernel, 1 = none (diagnostic), 2 = in fd_finish_kernel (A/B) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
+  unsigned      excl_lds[ 7 ];   /* fdgpu_ed25519_set_cu_exclusive: dynamic LDS per workgroup of the latency path's
+                                    prep<0,1>, prep<0,0>, dsm8, dsm4<0,1>, dsm4<0,0>, dsm2<0,1>, dsm2<0,0> (0 = none) */
   unsigned long nofold_max;      /* fd_dsm_kernel<0> (no carry fold) for batches of at most this many signatures */
   u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
   u32 *   d_O;                   /*             product of the block's other Z, planar [10][max_sig] */
@@ -2208,6 +2210,32 @@ fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long smal
   return old;
 }
 
+/* Latency-path workgroups alone on their CU: each reserves more than half of the CU's 160 KiB LDS (it uses none
+   of the extra), so no second such workgroup -- of this batch or of another context's concurrent one -- shares
+   its SIMDs.  A small batch runs under one wave per SIMD, its time the per-wave chain; a second wave on the
+   SIMD stretches that chain (profiles/r04/n: prep 108 us alone, 206 us beside the other context's walk). */
+#define FD_EXCL_LDS ( 84u * 1024u )
+extern "C" int
+fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on ) {
+  if( !ctx ) return -1;
+  void const * f[ 7 ] = { (void const *)fd_prep_kernel<0,1>, (void const *)fd_prep_kernel<0,0>, (void const *)fd_dsm8_kernel<0>,
+                          (void const *)fd_dsm4_kernel<0,1>, (void const *)fd_dsm4_kernel<0,0>,
+                          (void const *)fd_dsm2_kernel<0,1>, (void const *)fd_dsm2_kernel<0,0> };
+  unsigned v[ 7 ] = { 0u, 0u, 0u, 0u, 0u, 0u, 0u };
+  if( on ) {
+    HIPCHK( hipSetDevice( ctx->device ), -2 );
+    for( int i=0; i<7; i++ ) {
+      hipFuncAttributes a;
+      HIPCHK( hipFuncGetAttributes( &a, f[i] ), -2 );
+      unsigned st = (unsigned)a.sharedSizeBytes;
+      v[i] = st < FD_EXCL_LDS ? FD_EXCL_LDS - st : 0u;
+      if( v[i] ) HIPCHK( hipFuncSetAttribute( f[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)v[i] ), -2 );
+    }
+  }
+  for( int i=0; i<7; i++ ) ctx->excl_lds[i] = v[i];
+  return 0;
+}
+
 extern "C" char const * fdgpu_last_error( void ) { return fd_err.c_str(); }
 
 /* the synchronous host calls stage through slot 0: only when the async
@@ -2250,12 +2278,12 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       if( lanes == 8 && !ctx->half ) lanes = 4;       /* the term split needs the half-size walk */
       int d2 = lanes > 1;
       if( hs )      /* half-size: the A and R lanes build both tables, the hash lane (c0, c1, s') */
-        hipLaunchKernelGGL( (fd_prep_kernel<0,1>), dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+        hipLaunchKernelGGL( (fd_prep_kernel<0,1>), dim3(3*sg), dim3(FD_WG), ctx->excl_lds[0], st, d_payload, d_desc, ctx->d_map, nsig,
                             (u32)sg, ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
                             ctx->d_tab, (uint4 const *)ctx->d_khash, ctx->d_tabR, ctx->d_digR, ctx->d_slow,
                             ctx->d_slow + ctx->max_sig, ctx->half_force_slow, ctx->d_htop );
       else {
-        hipLaunchKernelGGL( (fd_prep_kernel<0,0>), dim3(3*sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig,
+        hipLaunchKernelGGL( (fd_prep_kernel<0,0>), dim3(3*sg), dim3(FD_WG), ctx->excl_lds[1], st, d_payload, d_desc, ctx->d_map, nsig,
                             (u32)sg, ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
                             d2 ? ctx->d_tab : (uint4 *)NULL, (uint4 const *)ctx->d_khash, (uint4 *)NULL, (i8 *)NULL,
                             (u32 *)NULL, (u32 *)NULL, 0u, (unsigned char *)NULL );
@@ -2297,15 +2325,17 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     }
     if( ctx->timing ) hipEventRecord( ev[1], st );
     if( small && lanes==8 )
-      hipLaunchKernelGGL( fd_dsm8_kernel<0>, dim3(8*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
+      hipLaunchKernelGGL( fd_dsm8_kernel<0>, dim3(8*sg), dim3(FD_WG), ctx->excl_lds[2], st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
                           ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->semantics, ctx->d_pstat,
                           ctx->d_htop );
     else if( small && lanes==4 )
-      hipLaunchKernelGGL( (hs ? fd_dsm4_kernel<0,1> : fd_dsm4_kernel<0,0>), dim3(4*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab,
+      hipLaunchKernelGGL( (hs ? fd_dsm4_kernel<0,1> : fd_dsm4_kernel<0,0>), dim3(4*sg), dim3(FD_WG),
+                          ctx->excl_lds[ hs ? 3 : 4 ], st, nsig, ctx->d_tab,
                           ctx->d_Rxy, ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat,
                           ctx->d_tabR, ctx->d_digR, ctx->d_btab2, ctx->d_htop );
     else if( small && lanes==2 )
-      hipLaunchKernelGGL( (hs ? fd_dsm2_kernel<0,1> : fd_dsm2_kernel<0,0>), dim3(2*sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab,
+      hipLaunchKernelGGL( (hs ? fd_dsm2_kernel<0,1> : fd_dsm2_kernel<0,0>), dim3(2*sg), dim3(FD_WG),
+                          ctx->excl_lds[ hs ? 5 : 6 ], st, nsig, ctx->d_tab,
                           ctx->d_Rxy, ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat,
                           ctx->d_tabR, ctx->d_digR, ctx->d_btab2, ctx->d_htop );
     else if( hs )                              /* one lane: the half-size walk, result codes at its start */
@@ -2366,14 +2396,14 @@ extern "C" void fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx );
 /* Test / A/B options of contexts created from now on (fdgpu_debug_set_opts).
    Process-wide, behind a mutex; the defaults are the product's choices. */
 static std::mutex g_dbg_mu;
-static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L, 0, 0, 0, 0 };
+static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L, 0, 0, 0, 0, 0 };
 static void debug_opts_get( fdgpu_debug_opts_t * o ) { std::lock_guard<std::mutex> lk( g_dbg_mu ); *o = g_dbg; }
 
 extern "C" void
 fdgpu_debug_set_opts( fdgpu_debug_opts_t const * opts ) {
   std::lock_guard<std::mutex> lk( g_dbg_mu );
   if( opts ) g_dbg = *opts;
-  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L, 0, 0, 0, 0 };
+  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L, 0, 0, 0, 0, 0 };
 }
 
 /* staging + device buffers of async slot i (once) */
@@ -2475,6 +2505,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   memset( ctx->h_stamp, 0, ( 2*fdgpu_ed25519_ctx_t::NSLOT + 1 ) * sizeof(unsigned long) );
   HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_stamp, (void *)ctx->h_stamp, 0 ), -1 );
   ctx->last_gt = -1;
+  if( dbg.cu_exclusive && fdgpu_ed25519_set_cu_exclusive( ctx, 1 ) ) return -1;
   /* slot 0 now (the synchronous host calls stage through it); the async
      pipeline's other slots on first use (slot_bufs) */
   if( max_payload_bytes && slot_bufs( ctx, 0 ) ) return -1;

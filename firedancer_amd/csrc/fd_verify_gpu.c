@@ -418,6 +418,7 @@ vt_ctx_new( fdgpu_vtile_t const * vt, int k ) {
     if( vt->opt.gather_cus && fdgpu_ed25519_reserve_cus( c, vt->opt.gather_cus, part, parts ) ) {
       fdgpu_ed25519_ctx_delete( c ); return NULL;
     }
+    if( vt->opt.cu_exclusive && fdgpu_ed25519_set_cu_exclusive( c, 1 ) ) { fdgpu_ed25519_ctx_delete( c ); return NULL; }
     fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
     /* every staging buffer and the gather stream now: batches then allocate nothing (the tile's sandbox
        allows no allocation it does not need, fd_verify_gpu_tile.seccomppolicy) */
@@ -1634,7 +1635,7 @@ static void * link_tile( void * _a ) {
   fdgpu_vtile_opts_t vo;
   memset( &vo, 0, sizeof(vo) );
   vo.nctx = c->nctx; vo.copy_wait_ns = c->copy_wait_ns; vo.copy_min = c->copy_min; vo.gather_cus = c->gather_cus;
-  vo.max_uncopied = c->max_uncopied; vo.cu_split = c->cu_split;
+  vo.max_uncopied = c->max_uncopied; vo.cu_split = c->cu_split; vo.cu_exclusive = c->cu_exclusive;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                              ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }

@@ -48,7 +48,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_host_alloc", "fdgpu_host_free", "fdgpu_host_register", "fdgpu_host_unregister", "fdgpu_device_numa_node",
            "fdgpu_ed25519_submit_raw_gather", "fdgpu_ed25519_submit_raw_gather_chk", "fdgpu_ed25519_gather",
            "fdgpu_ed25519_gathered", "fdgpu_ed25519_gather_launched", "fdgpu_ed25519_gather_wait", "fdgpu_host_dev_ptr",
-           "fdgpu_ed25519_reserve_gather_cus", "fdgpu_ed25519_reserve_cus", "fdgpu_ed25519_gather_stats", "fdgpu_ed25519_phase_stats", "fdgpu_ed25519_prepare", "fdgpu_ed25519_submit_raw_gather_dev", "fdgpu_host_region",
+           "fdgpu_ed25519_reserve_gather_cus", "fdgpu_ed25519_reserve_cus", "fdgpu_ed25519_set_cu_exclusive", "fdgpu_ed25519_gather_stats", "fdgpu_ed25519_phase_stats", "fdgpu_ed25519_prepare", "fdgpu_ed25519_submit_raw_gather_dev", "fdgpu_host_region",
            "fdgpu_ed25519_dropin_init", "fdgpu_debug_set_opts",
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_slow_count", "fdgpu_ed25519_set_dedup",
@@ -180,18 +180,19 @@ class DebugOpts(ctypes.Structure):
     """fdgpu_debug_opts_t: test / A/B choices for engine contexts created afterwards."""
     _fields_ = [("half", ctypes.c_int), ("half_force_slow", ctypes.c_uint), ("small_batch_max", ctypes.c_long),
                 ("dsm_lanes", ctypes.c_int), ("nofold_max", ctypes.c_long), ("gather_no_writeback", ctypes.c_int),
-                ("poll_prefetch", ctypes.c_int), ("gather_rpb", ctypes.c_int), ("gather_cu_spread", ctypes.c_int)]
+                ("poll_prefetch", ctypes.c_int), ("gather_rpb", ctypes.c_int), ("gather_cu_spread", ctypes.c_int),
+                ("cu_exclusive", ctypes.c_int)]
 
 
 def debug_set_opts(half: int = -1, half_force_slow: int = 0, small_batch_max: int = -1, dsm_lanes: int = 0,
                    nofold_max: int = -1, gather_no_writeback: int = 0, poll_prefetch: int = 0,
-                   gather_rpb: int = 0, gather_cu_spread: int = 0) -> None:
+                   gather_rpb: int = 0, gather_cu_spread: int = 0, cu_exclusive: int = 0) -> None:
     """fdgpu_debug_set_opts: the engine path of every context created from now on (tests only; the
     defaults restore the product's choices).  small_batch_max >= 2**63 means "always the latency path"."""
     o = DebugOpts(half=half, half_force_slow=half_force_slow,
                   small_batch_max=min(small_batch_max, 2**63 - 1), dsm_lanes=dsm_lanes, nofold_max=nofold_max,
                   gather_no_writeback=gather_no_writeback, poll_prefetch=poll_prefetch, gather_rpb=gather_rpb,
-                  gather_cu_spread=gather_cu_spread)
+                  gather_cu_spread=gather_cu_spread, cu_exclusive=cu_exclusive)
     load_library().fdgpu_debug_set_opts(ctypes.byref(o))
 
 

@@ -577,6 +577,14 @@ fdgpu_ed25519_set_record_fp_off( fdgpu_ed25519_ctx_t * ctx, int off );
 unsigned long
 fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long small_max );
 
+/* 1: every workgroup of the latency path's prep and walk kernels reserves
+   more than half of a CU's LDS (unused), so each runs alone on its CU --
+   two contexts' concurrent small batches then never share a SIMD (a
+   tile's staggered contexts, fdgpu_vtile_opts_t.cu_exclusive).  0: off
+   (default).  The throughput path is never affected.  0 or < 0. */
+int
+fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on );
+
 /* Per-kernel timing, in milliseconds: the mean over the batches launched
    since fdgpu_ed25519_set_timing(ctx,1) (at most the last 64) of HIP
    events recorded on the stream the kernels ran on.  idx: 0 = prep
@@ -624,6 +632,7 @@ typedef struct fdgpu_debug_opts {
   int           gather_rpb;          /* records per workgroup of the gather kernel: 0 = default (4), 1 = one (A/B) */
   int           gather_cu_spread;    /* the CUs a tile context reserves for its gathers: 0 = the last n (default),
                                         1 = every (CUs/n)-th, 2 = the first n (A/B) */
+  int           cu_exclusive;        /* 1: new contexts start with fdgpu_ed25519_set_cu_exclusive( ctx, 1 ) */
 } fdgpu_debug_opts_t;
 
 void

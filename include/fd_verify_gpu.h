@@ -206,6 +206,8 @@ typedef struct fdgpu_vtile_opts {
   int           cu_split;        /* 1 (with gather_cus): context k's verify kernels run on the k-th of nctx disjoint
                                     shares of the other CUs (fdgpu_ed25519_reserve_cus), so the staggered batches
                                     of one tile do not share SIMDs; 0: every context on all of them */
+  int           cu_exclusive;    /* 1: each context's latency-path workgroups run alone on their CU
+                                    (fdgpu_ed25519_set_cu_exclusive); 0: off */
 } fdgpu_vtile_opts_t;
 
 fdgpu_vtile_t * fdgpu_vtile_new( int device, unsigned long batch_txn, unsigned long tcache_depth, unsigned long seed,
@@ -378,6 +380,7 @@ typedef struct fdgpu_stream_cfg {
                                     the record header of the frag pf_dist/2 ahead (0 = 1: the next own frag's
                                     line and header; 4 and 8 measured the same, profiles/r03/prep_pf_ab) */
   int           cu_split;        /* fdgpu_vtile_opts_t.cu_split of every tile */
+  int           cu_exclusive;    /* fdgpu_vtile_opts_t.cu_exclusive of every tile */
   int           no_huge_pages;   /* 1: the link region in 4 KiB pages (A/B); 0: 2 MiB transparent huge pages where the
                                     kernel allows them (madvise), as the reference's workspaces use huge pages (max rate
                                     +4 %, profiles/r04/i) */

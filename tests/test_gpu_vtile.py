@@ -506,15 +506,18 @@ def test_stream_run_link(tiles, reliable, zero_copy, producers):
         assert st["verdicts"] > 0
 
 
-@pytest.mark.parametrize("nctx,reliable,rate", [(2, True, 0.0), (3, True, 0.0), (2, False, 2e6)])
-def test_stream_run_cu_split(nctx, reliable, rate):
+@pytest.mark.parametrize("nctx,reliable,rate,split,excl", [(2, True, 0.0, 1, 0), (3, True, 0.0, 1, 0), (2, False, 2e6, 1, 0),
+                                                       (2, True, 0.0, 0, 1), (2, False, 2e6, 0, 1), (3, False, 2e6, 1, 1)])
+def test_stream_run_cu_split(nctx, reliable, rate, split, excl):
     """Each engine context of a tile on its own share of the CUs the gathers leave (fdgpu_vtile_opts_t.cu_split,
-    fdgpu_ed25519_reserve_cus): every frag still gets one verdict, all published, signatures counted."""
+    fdgpu_ed25519_reserve_cus) and / or its latency-path workgroups alone on their CUs (cu_exclusive,
+    fdgpu_ed25519_set_cu_exclusive): every frag still gets one verdict, all published, signatures counted."""
     from firedancer_amd import synth, vtile
     payload, desc, _, _ = synth.make_batch(3000, synth.MULTI, seed=23)
     n = 30001
     st = vtile.stream_run(payload, desc["payload_off"], desc["payload_sz"], n_frags=n, tiles=1, batch_txn=2048,
-                          mcache_depth=1 << 16, reliable=reliable, rate_fps=rate, nctx=nctx, gather_cus=16, cu_split=1)
+                          mcache_depth=1 << 16, reliable=reliable, rate_fps=rate, nctx=nctx, gather_cus=16, cu_split=split,
+                          cu_exclusive=excl)
     assert st["frags"] == n and st["verdicts"] + st["lost"] == n
     assert st["lost"] == 0 and st["verdicts"] == n and st["overruns"] == 0
     m = st["metrics"]
