@@ -2217,7 +2217,9 @@ fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long smal
 #define FD_EXCL_LDS ( 84u * 1024u )
 extern "C" int
 fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on ) {
-  if( !ctx ) return -1;
+  if( !ctx || on < 0 || on > 4 ) return -1;
+  /* on (A/B): 1 prep and walk alone on their CU; 2 at most two per CU; 3 the walk alone; 4 the prep alone */
+  unsigned want = on == 2 ? 56u * 1024u : FD_EXCL_LDS;
   void const * f[ 7 ] = { (void const *)fd_prep_kernel<0,1>, (void const *)fd_prep_kernel<0,0>, (void const *)fd_dsm8_kernel<0>,
                           (void const *)fd_dsm4_kernel<0,1>, (void const *)fd_dsm4_kernel<0,0>,
                           (void const *)fd_dsm2_kernel<0,1>, (void const *)fd_dsm2_kernel<0,0> };
@@ -2228,7 +2230,9 @@ fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on ) {
       hipFuncAttributes a;
       HIPCHK( hipFuncGetAttributes( &a, f[i] ), -2 );
       unsigned st = (unsigned)a.sharedSizeBytes;
-      v[i] = st < FD_EXCL_LDS ? FD_EXCL_LDS - st : 0u;
+      int walk = i >= 2;
+      if( ( on == 3 && !walk ) || ( on == 4 && walk ) ) continue;
+      v[i] = st < want ? want - st : 0u;
       if( v[i] ) HIPCHK( hipFuncSetAttribute( f[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)v[i] ), -2 );
     }
   }
@@ -2505,7 +2509,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   memset( ctx->h_stamp, 0, ( 2*fdgpu_ed25519_ctx_t::NSLOT + 1 ) * sizeof(unsigned long) );
   HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_stamp, (void *)ctx->h_stamp, 0 ), -1 );
   ctx->last_gt = -1;
-  if( dbg.cu_exclusive && fdgpu_ed25519_set_cu_exclusive( ctx, 1 ) ) return -1;
+  if( dbg.cu_exclusive && fdgpu_ed25519_set_cu_exclusive( ctx, dbg.cu_exclusive ) ) return -1;
   /* slot 0 now (the synchronous host calls stage through it); the async
      pipeline's other slots on first use (slot_bufs) */
   if( max_payload_bytes && slot_bufs( ctx, 0 ) ) return -1;

@@ -581,7 +581,8 @@ fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long smal
    more than half of a CU's LDS (unused), so each runs alone on its CU --
    two contexts' concurrent small batches then never share a SIMD (a
    tile's staggered contexts, fdgpu_vtile_opts_t.cu_exclusive).  0: off
-   (default).  The throughput path is never affected.  0 or < 0. */
+   (default).  A/B variants: 2 = at most two per CU, 3 = the walk only,
+   4 = the prep only.  The throughput path is never affected.  0 or < 0. */
 int
 fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on );
 
