@@ -742,10 +742,14 @@ def main():
                         and all(c["metrics"][:4] == [0, 0, 0, 0] for c in curve))
                 # the knee: the highest offered rate whose p99 (tsorig -> verdict) stays within 1 ms with
                 # every frag verified (none lost to overruns, none overrun while copied)
-                within = [c["offered_frags_per_s_per_gpu"] for c in curve
-                          if c["p99_us"] <= 1000.0 and c["lost"] == 0 and c["overruns_at_verdict"] == 0]
-                knee = {"frags_per_s_per_gpu": max(within) if within else None, "p99_bound_us": 1000.0,
-                        "rates_tried": _rates(args)}
+                # every rate up to the knee must hold the bound (a curve that fails at a lower rate and passes
+                # at a higher one has its knee below the failure)
+                knee_fps = None
+                for c in sorted(curve, key=lambda c: c["offered_frags_per_s_per_gpu"]):
+                    if c["p99_us"] > 1000.0 or c["lost"] != 0 or c["overruns_at_verdict"] != 0:
+                        break
+                    knee_fps = c["offered_frags_per_s_per_gpu"]
+                knee = {"frags_per_s_per_gpu": knee_fps, "p99_bound_us": 1000.0, "rates_tried": _rates(args)}
                 stream = {"workload": "BASELINE configs[4]: 1232-byte txns, Q producer mcache links over one in dcache "
                                       "-> T verify tiles reading every link (seq % T round robin per link, tile i -> "
                                       "GPU i % G; device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> "
