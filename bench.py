@@ -660,9 +660,10 @@ def main():
                     help="max-rate legs: each tile's engine contexts on disjoint CU shares (fdgpu_vtile_opts_t.cu_split)")
     ap.add_argument("--stream-lat-cu-split", type=int, default=0, choices=(0, 1),
                     help="paced legs: each tile's engine contexts on disjoint CU shares (fdgpu_vtile_opts_t.cu_split)")
-    ap.add_argument("--stream-cu-exclusive", type=int, default=0, choices=(0, 1, 2, 3, 4),
+    ap.add_argument("--stream-cu-exclusive", type=int, default=0, choices=(-1, 0, 1, 2, 3, 4),
                     help="every leg: latency-path workgroups alone on their CU (fdgpu_vtile_opts_t.cu_exclusive; "
-                         "A/B: 2 at most two per CU, 3 the walk only, 4 the prep only)")
+                         "0 = the tile's default, on; -1 off; A/B: 2 at most two per CU, 3 the walk only, 4 the prep "
+                         "only; profiles/r04/p, q)")
     ap.add_argument("--stream-only-paced", action="store_true",
                     help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",

@@ -418,7 +418,8 @@ vt_ctx_new( fdgpu_vtile_t const * vt, int k ) {
     if( vt->opt.gather_cus && fdgpu_ed25519_reserve_cus( c, vt->opt.gather_cus, part, parts ) ) {
       fdgpu_ed25519_ctx_delete( c ); return NULL;
     }
-    if( vt->opt.cu_exclusive && fdgpu_ed25519_set_cu_exclusive( c, vt->opt.cu_exclusive ) ) { fdgpu_ed25519_ctx_delete( c ); return NULL; }
+    int excl = vt->opt.cu_exclusive ? vt->opt.cu_exclusive : 1;         /* 0 = default: on */
+    if( excl > 0 && fdgpu_ed25519_set_cu_exclusive( c, excl ) ) { fdgpu_ed25519_ctx_delete( c ); return NULL; }
     fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
     /* every staging buffer and the gather stream now: batches then allocate nothing (the tile's sandbox
        allows no allocation it does not need, fd_verify_gpu_tile.seccomppolicy) */

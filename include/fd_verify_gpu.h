@@ -206,8 +206,9 @@ typedef struct fdgpu_vtile_opts {
   int           cu_split;        /* 1 (with gather_cus): context k's verify kernels run on the k-th of nctx disjoint
                                     shares of the other CUs (fdgpu_ed25519_reserve_cus), so the staggered batches
                                     of one tile do not share SIMDs; 0: every context on all of them */
-  int           cu_exclusive;    /* 1: each context's latency-path workgroups run alone on their CU
-                                    (fdgpu_ed25519_set_cu_exclusive); 0: off */
+  int           cu_exclusive;    /* each context's latency-path workgroups alone on their CU
+                                    (fdgpu_ed25519_set_cu_exclusive): 0 = default (on: paced p99 at 10M frags/s
+                                    0.96 vs 1.06 ms, knee 10M vs 7.5M, profiles/r04/q); -1 = off; 1..4 explicit */
 } fdgpu_vtile_opts_t;
 
 fdgpu_vtile_t * fdgpu_vtile_new( int device, unsigned long batch_txn, unsigned long tcache_depth, unsigned long seed,

@@ -506,8 +506,9 @@ def test_stream_run_link(tiles, reliable, zero_copy, producers):
         assert st["verdicts"] > 0
 
 
-@pytest.mark.parametrize("nctx,reliable,rate,split,excl", [(2, True, 0.0, 1, 0), (3, True, 0.0, 1, 0), (2, False, 2e6, 1, 0),
-                                                       (2, True, 0.0, 0, 1), (2, False, 2e6, 0, 1), (3, False, 2e6, 1, 1)])
+@pytest.mark.parametrize("nctx,reliable,rate,split,excl", [(2, True, 0.0, 1, -1), (3, True, 0.0, 1, -1), (2, False, 2e6, 1, -1),
+                                                       (2, True, 0.0, 0, 1), (2, False, 2e6, 0, 0), (3, False, 2e6, 1, 1),
+                                                       (2, False, 2e6, 0, -1)])
 def test_stream_run_cu_split(nctx, reliable, rate, split, excl):
     """Each engine context of a tile on its own share of the CUs the gathers leave (fdgpu_vtile_opts_t.cu_split,
     fdgpu_ed25519_reserve_cus) and / or its latency-path workgroups alone on their CUs (cu_exclusive,
