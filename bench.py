@@ -188,8 +188,12 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 # link carries 1/G of the frags but is read by all 2G tiles -> twice the single-GPU depth
                 mcache_depth=args.stream_depth * min(procs, 2) if not paced else 1 << 18,
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
-                copy_wait_ns=int(args.stream_copy_wait_us * 1000), gather_cus=args.stream_gather_cus,
-                max_uncopied=args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
+                # the max-rate legs copy in bigger gathers (a gather's PCIe rate grows with its size, tools/
+                # gatherprobe): 200 us / 64K frags, max rate +6 % (profiles/r04/r); the paced legs keep the tile's
+                # latency defaults
+                copy_wait_ns=int((args.stream_copy_wait_us if paced else args.stream_tput_copy_wait_us) * 1000),
+                gather_cus=args.stream_gather_cus,
+                max_uncopied=args.stream_max_uncopied if paced else args.stream_tput_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
                 no_huge_pages=1 if args.stream_no_huge else 0,
                 cu_split=(args.stream_lat_cu_split if paced else args.stream_cu_split),
                 cu_exclusive=args.stream_cu_exclusive)
@@ -362,6 +366,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-ctx", str(args.stream_ctx), "--stream-lat-ctx", str(args.stream_lat_ctx),
            "--stream-rates", str(args.stream_rates), "--stream-paced-seconds", str(args.stream_paced_seconds),
            "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus),
+           "--stream-tput-copy-wait-us", str(args.stream_tput_copy_wait_us),
+           "--stream-tput-max-uncopied", str(args.stream_tput_max_uncopied),
            "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
         (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else []) + \
         (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else []) + \
@@ -638,7 +644,7 @@ def main():
     ap.add_argument("--stream-prof", action="store_true",
                     help="rdtsc section profile of the tile loop (fdgpu_stream_cfg_t.prof), in each leg's summary")
     ap.add_argument("--stream-max-uncopied", type=int, default=0,
-                    help="zero-copy intake: frags a tile may hold whose GPU copy has not completed (fdgpu_vtile_opts_t."
+                    help="paced legs, zero-copy intake: frags a tile may hold whose GPU copy has not completed (fdgpu_vtile_opts_t."
                          "max_uncopied; 0 = its default)")
     ap.add_argument("--stream-poll-prefetch", type=int, default=0,
                     help="(stream child only, A/B) software prefetch distance of the tiles' completion polls "
@@ -650,8 +656,12 @@ def main():
                          "copies (default), the batch's finish kernel (A/B), or nobody (DIAGNOSTIC: published records lack "
                          "their payload -- what the write-back costs; never a result)")
     ap.add_argument("--stream-copy-wait-us", type=float, default=0.0,
-                    help="zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
+                    help="paced legs, zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
                          "waited this long (0 = fdgpu_vtile default, FDGPU_VTILE_COPY_WAIT_NS)")
+    ap.add_argument("--stream-tput-copy-wait-us", type=float, default=200.0,
+                    help="max-rate / unreliable legs: --stream-copy-wait-us of their tiles (bigger gathers)")
+    ap.add_argument("--stream-tput-max-uncopied", type=int, default=65536,
+                    help="max-rate / unreliable legs: --stream-max-uncopied of their tiles")
     ap.add_argument("--stream-lat-tiles", type=int, default=1,
                     help="verify tiles per GPU of the paced legs (fewer tiles = fewer HIP streams sharing the "
                          "device: 1 tile x 2 contexts p99 0.81 / 0.99 / 1.37 ms at 2 / 5 / 10M frags/s against "
