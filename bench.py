@@ -176,6 +176,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
     # the max-rate legs batch for throughput (a GPU batch under one wave per SIMD costs about one wave's
     # DSM chain, ~1 ms, whatever its size), the paced leg for latency
     paced = leg.startswith("paced@")
+    tput = leg in ("cal", "max")
     rate = float(leg.split("@")[1]) if paced else 0.0
     # paced legs: a batch limit of about 4 ms of one tile's share of the offered load (8K..64K), so batches
     # stay small at low load (latency path) and can grow with it; adaptive launch sizes them below that
@@ -188,12 +189,13 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 # link carries 1/G of the frags but is read by all 2G tiles -> twice the single-GPU depth
                 mcache_depth=args.stream_depth * min(procs, 2) if not paced else 1 << 18,
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
-                # the max-rate legs copy in bigger gathers (a gather's PCIe rate grows with its size, tools/
-                # gatherprobe): 200 us / 64K frags, max rate +6 % (profiles/r04/r); the paced legs keep the tile's
-                # latency defaults
-                copy_wait_ns=int((args.stream_copy_wait_us if paced else args.stream_tput_copy_wait_us) * 1000),
+                # the reliable max-rate legs copy in bigger gathers (a gather's PCIe rate grows with its size,
+                # tools/gatherprobe): 200 us / 64K frags, max rate +6-8 % (profiles/r04/r, s); the paced and the
+                # unreliable legs keep the tile's defaults (a later copy leaves a frag exposed to overruns longer:
+                # unreliable goodput 17.0M vs 19.1M, profiles/r04/s)
+                copy_wait_ns=int((args.stream_tput_copy_wait_us if tput else args.stream_copy_wait_us) * 1000),
                 gather_cus=args.stream_gather_cus,
-                max_uncopied=args.stream_max_uncopied if paced else args.stream_tput_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
+                max_uncopied=args.stream_tput_max_uncopied if tput else args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
                 no_huge_pages=1 if args.stream_no_huge else 0,
                 cu_split=(args.stream_lat_cu_split if paced else args.stream_cu_split),
                 cu_exclusive=args.stream_cu_exclusive)
@@ -644,7 +646,7 @@ def main():
     ap.add_argument("--stream-prof", action="store_true",
                     help="rdtsc section profile of the tile loop (fdgpu_stream_cfg_t.prof), in each leg's summary")
     ap.add_argument("--stream-max-uncopied", type=int, default=0,
-                    help="paced legs, zero-copy intake: frags a tile may hold whose GPU copy has not completed (fdgpu_vtile_opts_t."
+                    help="paced / unreliable legs, zero-copy intake: frags a tile may hold whose GPU copy has not completed (fdgpu_vtile_opts_t."
                          "max_uncopied; 0 = its default)")
     ap.add_argument("--stream-poll-prefetch", type=int, default=0,
                     help="(stream child only, A/B) software prefetch distance of the tiles' completion polls "
@@ -656,12 +658,12 @@ def main():
                          "copies (default), the batch's finish kernel (A/B), or nobody (DIAGNOSTIC: published records lack "
                          "their payload -- what the write-back costs; never a result)")
     ap.add_argument("--stream-copy-wait-us", type=float, default=0.0,
-                    help="paced legs, zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
+                    help="paced / unreliable legs, zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
                          "waited this long (0 = fdgpu_vtile default, FDGPU_VTILE_COPY_WAIT_NS)")
     ap.add_argument("--stream-tput-copy-wait-us", type=float, default=200.0,
-                    help="max-rate / unreliable legs: --stream-copy-wait-us of their tiles (bigger gathers)")
+                    help="reliable max-rate legs (cal, max): --stream-copy-wait-us of their tiles (bigger gathers)")
     ap.add_argument("--stream-tput-max-uncopied", type=int, default=65536,
-                    help="max-rate / unreliable legs: --stream-max-uncopied of their tiles")
+                    help="reliable max-rate legs (cal, max): --stream-max-uncopied of their tiles")
     ap.add_argument("--stream-lat-tiles", type=int, default=1,
                     help="verify tiles per GPU of the paced legs (fewer tiles = fewer HIP streams sharing the "
                          "device: 1 tile x 2 contexts p99 0.81 / 0.99 / 1.37 ms at 2 / 5 / 10M frags/s against "
