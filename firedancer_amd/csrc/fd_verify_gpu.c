@@ -1676,12 +1676,9 @@ static void * link_tile( void * _a ) {
   ulong pc[ 8 ] = { 0 }, c_begin = __rdtsc(), cx = 0UL;
 #define PROF_T0()    do { if( prof ) cx = __rdtsc(); } while( 0 )
 #define PROF_ADD(i)  do { if( prof ) { ulong cy_ = __rdtsc(); pc[i] += cy_ - cx; cx = cy_; } } while( 0 )
-  ulong t_prev = now_ns();                       /* the last clock read: a pass starts where the previous ended */
   while( got + lost < mine ) {
     if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
-    /* one clock read per pass (clock_gettime costs ~20 ns; at a paced rate a pass often takes one frag):
-       this pass's start is the previous pass's last read, within its loop test */
-    ulong t0 = t_prev;
+    ulong t0 = now_ns();
     ulong prog = got;
     for( ulong q=0; q<Q; q++ ) prog += in[q].seq;
     if( prog != last_prog ) { last_prog = prog; t_prog = t0; }
@@ -1749,7 +1746,6 @@ static void * link_tile( void * _a ) {
     q0++;
     for( ulong q=0; q<Q; q++ ) if( in[q].seq < in[q].n ) all_done = 0;
     ulong t1 = now_ns();
-    t_prev = t1;
     ns_in += t1 - t0;
     if( !took && !drain ) ns_idle += t1 - t0;
     if( atomic_load_explicit( &h->fail, memory_order_relaxed ) ) break;
@@ -1763,8 +1759,7 @@ static void * link_tile( void * _a ) {
       PROF_ADD( 5 );
       if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );
       PROF_ADD( 6 );
-      t_prev = now_ns();
-      ns_after += t_prev - t1;
+      ns_after += now_ns() - t1;
       continue;
     }
     /* housekeeping: launch / drain at most every 10 us while frags flow
@@ -1783,8 +1778,7 @@ static void * link_tile( void * _a ) {
       PROF_ADD( 5 );
       if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );
       PROF_ADD( 6 );
-      t_prev = now_ns();
-      ns_hk += t2 - t1; ns_after += t_prev - t2;
+      ns_hk += t2 - t1; ns_after += now_ns() - t2;
     }
   }
   ulong t_end = now_ns();
