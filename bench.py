@@ -213,6 +213,20 @@ def _leg_cfg(args, leg, procs, cal_fps):
     return dict(base, tiles=T, n_frags=n, rate_fps=0.0, reliable=False)
 
 
+KNEE_P99_US = 1000.0
+
+
+def knee_of(curve: list) -> float | None:
+    """The highest offered rate (frags/s per GPU) such that it and every lower tried rate kept p99 within
+    KNEE_P99_US with no frag lost and none overrun while copied; None if the lowest rate already fails."""
+    knee = None
+    for c in sorted(curve, key=lambda c: c["offered_frags_per_s_per_gpu"]):
+        if c["p99_us"] > KNEE_P99_US or c["lost"] != 0 or c["overruns_at_verdict"] != 0:
+            break
+        knee = c["offered_frags_per_s_per_gpu"]
+    return knee
+
+
 def _phases(ph) -> dict:
     n, ng = max(ph[0], 1), max(ph[8], 1)
     return {"batches": ph[0], "launch_to_kernels_mean": ph[1] / n * 1e-3, "launch_to_kernels_max": ph[2] * 1e-3,
@@ -576,7 +590,7 @@ def dry_run_main(args) -> None:
         dist.destroy_process_group()
 
 
-def main():
+def parse_args(argv=None) -> argparse.Namespace:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs (one rank each); without torchrun's env, bench.py starts the N ranks itself")
@@ -689,7 +703,11 @@ def main():
     ap.add_argument("--stream-procs", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--stream-token", default="x", help=argparse.SUPPRESS)
     ap.add_argument("--stream-seed", type=int, default=1234, help=argparse.SUPPRESS)
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main():
+    args = parse_args()
     if args.stream_child:
         stream_child_main(args)
         return
@@ -757,12 +775,7 @@ def main():
                 # every frag verified (none lost to overruns, none overrun while copied)
                 # every rate up to the knee must hold the bound (a curve that fails at a lower rate and passes
                 # at a higher one has its knee below the failure)
-                knee_fps = None
-                for c in sorted(curve, key=lambda c: c["offered_frags_per_s_per_gpu"]):
-                    if c["p99_us"] > 1000.0 or c["lost"] != 0 or c["overruns_at_verdict"] != 0:
-                        break
-                    knee_fps = c["offered_frags_per_s_per_gpu"]
-                knee = {"frags_per_s_per_gpu": knee_fps, "p99_bound_us": 1000.0, "rates_tried": _rates(args)}
+                knee = {"frags_per_s_per_gpu": knee_of(curve), "p99_bound_us": KNEE_P99_US, "rates_tried": _rates(args)}
                 stream = {"workload": "BASELINE configs[4]: 1232-byte txns, Q producer mcache links over one in dcache "
                                       "-> T verify tiles reading every link (seq % T round robin per link, tile i -> "
                                       "GPU i % G; device fd_txn_parse + verify, in-order after_frag, dedup tcache) -> "

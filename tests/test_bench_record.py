@@ -118,3 +118,30 @@ def test_failed_rank_takes_the_others_down(tmp_path):
     t0 = time.time()
     rc = bench.launch_ranks(2, [], script=str(stub), timeout_s=120)
     assert rc == 3 and time.time() - t0 < 60
+
+
+def _pt(rate, p99, lost=0, ovr=0):
+    return {"offered_frags_per_s_per_gpu": rate, "p99_us": p99, "lost": lost, "overruns_at_verdict": ovr}
+
+
+def test_knee_is_monotone():
+    """stream.knee: every tried rate up to the knee holds p99 <= 1 ms with nothing lost or overrun."""
+    assert bench.knee_of([_pt(2e6, 600), _pt(5e6, 640), _pt(10e6, 960), _pt(15e6, 1700)]) == 10e6
+    assert bench.knee_of([_pt(15e6, 1700), _pt(2e6, 600), _pt(10e6, 960)]) == 10e6           # order-free
+    assert bench.knee_of([_pt(2e6, 600), _pt(5e6, 1200), _pt(10e6, 960)]) == 2e6             # a lower rate failed
+    assert bench.knee_of([_pt(2e6, 600), _pt(5e6, 700, lost=3), _pt(10e6, 900)]) == 2e6      # frags lost
+    assert bench.knee_of([_pt(2e6, 600, ovr=1)]) is None
+    assert bench.knee_of([_pt(2e6, 1000.0)]) == 2e6                                          # the bound is inclusive
+
+
+def test_leg_copy_settings():
+    """The reliable max-rate legs (cal, max) copy in bigger gathers; paced and unreliable legs keep the tile's
+    defaults (0 = fdgpu_vtile_opts_t default)."""
+    args = bench.parse_args([]) if hasattr(bench, "parse_args") else None
+    if args is None:
+        pytest.skip("bench.parse_args not available")
+    for leg, tput in (("cal", True), ("max", True), ("paced@5000000.0", False), ("unrel", False)):
+        cfg = bench._leg_cfg(args, leg, 1, 20e6)
+        assert cfg["copy_wait_ns"] == (int(args.stream_tput_copy_wait_us * 1000) if tput else 0), leg
+        assert cfg["max_uncopied"] == (args.stream_tput_max_uncopied if tput else 0), leg
+    assert args.stream_tput_copy_wait_us == 200.0 and args.stream_tput_max_uncopied == 65536
