@@ -484,6 +484,7 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 "unreliable_vs_max": _r(st.get("unreliable_goodput_vs_max"), 3),
                 "tile_host_ns_per_frag": (st.get("max_rate") or {}).get("tile_host_ns_per_frag"),
                 "all_published": st.get("all_published"),
+                "host_cpu_share_min": _r(st.get("host_cpu_share_min")),
                 "anomalies": sum(v["count"] for v in (st.get("anomalies") or {}).values())}
     rec["detail"] = detail_path
     return rec
@@ -798,6 +799,10 @@ def main():
                           "all_published": bool(ok_s),
                           # verdicts neither published nor overrun, per leg (fdgpu_link_anomalies): none expected
                           "anomalies": anomalies,
+                          # the lowest share of wall time any leg's tile thread kept its core (a shared host
+                          # that steals it inflates that leg's latency tail; 1.0 = undisturbed)
+                          "host_cpu_share_min": min((l.get("host_cpu") or {}).get("tile_share_min", 1.0)
+                                                    for l in [mx, ur] + curve),
                           "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
             else:
                 stream = {"error": err or "a stream child failed on another rank"}
