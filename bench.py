@@ -195,7 +195,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 # unreliable goodput 17.0M vs 19.1M, profiles/r04/s)
                 copy_wait_ns=int((args.stream_tput_copy_wait_us if tput else args.stream_copy_wait_us) * 1000),
                 gather_cus=args.stream_gather_cus,
-                max_uncopied=args.stream_tput_max_uncopied if tput else args.stream_max_uncopied, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
+                max_uncopied=args.stream_tput_max_uncopied if tput else args.stream_max_uncopied,
+                copy_min=args.stream_tput_copy_min if tput else 0, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
                 no_huge_pages=1 if args.stream_no_huge else 0,
                 cu_split=(args.stream_lat_cu_split if paced else args.stream_cu_split),
                 cu_exclusive=args.stream_cu_exclusive)
@@ -384,6 +385,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-copy-wait-us", str(args.stream_copy_wait_us), "--stream-gather-cus", str(args.stream_gather_cus),
            "--stream-tput-copy-wait-us", str(args.stream_tput_copy_wait_us),
            "--stream-tput-max-uncopied", str(args.stream_tput_max_uncopied),
+           "--stream-tput-copy-min", str(args.stream_tput_copy_min),
            "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
         (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else []) + \
         (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else []) + \
@@ -679,6 +681,9 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="reliable max-rate legs (cal, max): --stream-copy-wait-us of their tiles (bigger gathers)")
     ap.add_argument("--stream-tput-max-uncopied", type=int, default=65536,
                     help="reliable max-rate legs (cal, max): --stream-max-uncopied of their tiles")
+    ap.add_argument("--stream-tput-copy-min", type=int, default=0,
+                    help="reliable max-rate legs (cal, max): a tile starts a copy once this many frags wait "
+                         "(fdgpu_vtile_opts_t.copy_min; 0 = its default, 4,096)")
     ap.add_argument("--stream-lat-tiles", type=int, default=1,
                     help="verify tiles per GPU of the paced legs (fewer tiles = fewer HIP streams sharing the "
                          "device: 1 tile x 2 contexts p99 0.81 / 0.99 / 1.37 ms at 2 / 5 / 10M frags/s against "
