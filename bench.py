@@ -190,9 +190,10 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 mcache_depth=args.stream_depth * min(procs, 2) if not paced else 1 << 18,
                 nctx=args.stream_lat_ctx if paced else args.stream_ctx,
                 # the reliable max-rate legs copy in bigger gathers (a gather's PCIe rate grows with its size,
-                # tools/gatherprobe): 200 us / 64K frags, max rate +6-8 % (profiles/r04/r, s); the paced and the
-                # unreliable legs keep the tile's defaults (a later copy leaves a frag exposed to overruns longer:
-                # unreliable goodput 17.0M vs 19.1M, profiles/r04/s)
+                # tools/gatherprobe): ~20K records per gather (copy after 2 ms or 32K waiting frags, 128K
+                # uncopied at most), max rate 25.7-25.8M vs 23.3-23.5M at ~2.6K (profiles/r04/gs); the paced and
+                # the unreliable legs keep the tile's defaults (a later copy leaves a frag exposed to overruns
+                # longer: unreliable goodput 17.0M vs 19.1M, profiles/r04/s)
                 copy_wait_ns=int((args.stream_tput_copy_wait_us if tput else args.stream_copy_wait_us) * 1000),
                 gather_cus=args.stream_gather_cus,
                 max_uncopied=args.stream_tput_max_uncopied if tput else args.stream_max_uncopied,
@@ -677,13 +678,13 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-copy-wait-us", type=float, default=0.0,
                     help="paced / unreliable legs, zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
                          "waited this long (0 = fdgpu_vtile default, FDGPU_VTILE_COPY_WAIT_NS)")
-    ap.add_argument("--stream-tput-copy-wait-us", type=float, default=200.0,
+    ap.add_argument("--stream-tput-copy-wait-us", type=float, default=2000.0,
                     help="reliable max-rate legs (cal, max): --stream-copy-wait-us of their tiles (bigger gathers)")
-    ap.add_argument("--stream-tput-max-uncopied", type=int, default=65536,
+    ap.add_argument("--stream-tput-max-uncopied", type=int, default=131072,
                     help="reliable max-rate legs (cal, max): --stream-max-uncopied of their tiles")
-    ap.add_argument("--stream-tput-copy-min", type=int, default=0,
+    ap.add_argument("--stream-tput-copy-min", type=int, default=32768,
                     help="reliable max-rate legs (cal, max): a tile starts a copy once this many frags wait "
-                         "(fdgpu_vtile_opts_t.copy_min; 0 = its default, 4,096)")
+                         "(fdgpu_vtile_opts_t.copy_min; 0 = the tile's default, 4,096)")
     ap.add_argument("--stream-lat-tiles", type=int, default=1,
                     help="verify tiles per GPU of the paced legs (fewer tiles = fewer HIP streams sharing the "
                          "device: 1 tile x 2 contexts p99 0.81 / 0.99 / 1.37 ms at 2 / 5 / 10M frags/s against "

@@ -144,4 +144,5 @@ def test_leg_copy_settings():
         cfg = bench._leg_cfg(args, leg, 1, 20e6)
         assert cfg["copy_wait_ns"] == (int(args.stream_tput_copy_wait_us * 1000) if tput else 0), leg
         assert cfg["max_uncopied"] == (args.stream_tput_max_uncopied if tput else 0), leg
-    assert args.stream_tput_copy_wait_us == 200.0 and args.stream_tput_max_uncopied == 65536
+    assert args.stream_tput_copy_wait_us == 2000.0 and args.stream_tput_max_uncopied == 131072
+    assert bench._leg_cfg(args, "max", 1, 20e6)["copy_min"] == 32768 and bench._leg_cfg(args, "unrel", 1, 20e6)["copy_min"] == 0

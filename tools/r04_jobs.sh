@@ -25,6 +25,7 @@
 #   copy_ab      y    host-copy intake vs zero-copy at 2 / 3 / 4 tiles
 #   t3_ab        z    2 vs 3 vs 4 tiles at the final defaults
 #   gsize_ab     gs   max-leg gathers of 4K / 16K / 32K / 64K records (copy_min with copy wait and uncopied bound)
+#   big_ab       gt   with ~20K-record gathers (the new max-leg default): 2 vs 3 tiles, 2 producers
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 
@@ -163,8 +164,11 @@ gsize_ab)
   G16="--stream-tput-copy-wait-us 1000 --stream-tput-copy-min 16384 --stream-tput-max-uncopied 131072"
   G32="--stream-tput-copy-wait-us 2000 --stream-tput-copy-min 32768 --stream-tput-max-uncopied 131072"
   G64="--stream-tput-copy-wait-us 4000 --stream-tput-copy-min 65536 --stream-tput-max-uncopied 262144"
-  run_arms r04gs "$Q --stream-rates 5e6 --stream-paced-seconds 1 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
+  run_arms r04gs "$Q --stream-tput-copy-wait-us 200 --stream-tput-copy-min 0 --stream-tput-max-uncopied 65536 --stream-rates 5e6 --stream-paced-seconds 1 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
     d1= "g16a=$G16" "g32a=$G32" "g64a=$G64" "g64b=$G64" "g32b=$G32" "g16b=$G16" d2= ;;
+big_ab)
+  run_arms r04gt "$Q --stream-rates 5e6 --stream-paced-seconds 1 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
+    t2a= "t3a=--stream-tiles 3" "t2p2a=--stream-producers 2" "t2p2b=--stream-producers 2" "t3b=--stream-tiles 3" t2b= ;;
 *)
-  sed -n '2,27p' "$0"; exit 2 ;;
+  sed -n '2,28p' "$0"; exit 2 ;;
 esac
