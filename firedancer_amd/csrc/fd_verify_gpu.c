@@ -151,17 +151,23 @@ static void tc_map_remove( fdgpu_tcache_t * tc, ulong i ) {
   tc->map[i] = 0UL;
 }
 
-int fdgpu_tcache_insert( fdgpu_tcache_t * tc, ulong tag ) {
+/* FD_TCACHE_QUERY and, when the tag is absent and `ins`, FD_TCACHE_INSERT
+   into the empty slot the query's probe ended at: one probe for both */
+static inline int tc_query_insert( fdgpu_tcache_t * tc, ulong tag, int ins ) {
   if( !tag ) return 1;
   ulong i;
   if( tc_find( tc, tag, &i ) ) return 1;
-  tc->map[i] = tag;
-  ulong old = tc->ring[ tc->oldest ];
-  tc->ring[ tc->oldest ] = tag;
-  tc->oldest = ( tc->oldest + 1UL == tc->depth ) ? 0UL : tc->oldest + 1UL;
-  if( old && tc_find( tc, old, &i ) ) tc_map_remove( tc, i );
+  if( ins ) {
+    tc->map[i] = tag;
+    ulong old = tc->ring[ tc->oldest ];
+    tc->ring[ tc->oldest ] = tag;
+    tc->oldest = ( tc->oldest + 1UL == tc->depth ) ? 0UL : tc->oldest + 1UL;
+    if( old && tc_find( tc, old, &i ) ) tc_map_remove( tc, i );
+  }
   return 0;
 }
+
+int fdgpu_tcache_insert( fdgpu_tcache_t * tc, ulong tag ) { return tc_query_insert( tc, tag, 1 ); }
 
 /* ---- mcache / dcache -------------------------------------------------
    An mcache is a ring of 32-byte frag metadata lines indexed by seq &
@@ -752,8 +758,10 @@ vt_room( fdgpu_vtile_t * vt ) {
   if( !vt->zc ) vt_fence();                      /* (zero-copy intake makes no streaming stores) */
   if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_vtile_flush( vt ); return -2; }
   /* a faulted context takes no more frags: fill the next healthy one (none: -3) */
-  for( int i=0; i<vt->nctx && fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ); i++ ) vt->fill = ( vt->fill + 1 ) % vt->nctx;
-  if( fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ) ) return -3;
+  if( __builtin_expect( fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ), 0 ) ) {
+    for( int i=0; i<vt->nctx && fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ); i++ ) vt->fill = ( vt->fill + 1 ) % vt->nctx;
+    if( fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ) ) return -3;
+  }
   return 0;
 }
 
@@ -961,9 +969,10 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
   }
   /* fd_txn_verify (fd_verify_tile.h:59-108): dedup query, verify, insert */
   int res = 0;   /* 0 success, 1 verify failed, 2 dedup */
-  if( !is_bundle && fdgpu_tcache_query( vt->tcache, tag ) ) res = 2;
-  else if( code != 0 ) res = 1;
-  else if( !is_bundle && fdgpu_tcache_insert( vt->tcache, tag ) ) res = 2;
+  if( !is_bundle ) {             /* query; a verified tag goes in at the slot the query's probe found */
+    if( tc_query_insert( vt->tcache, tag, code == 0 ) ) res = 2;
+    else if( code != 0 ) res = 1;
+  } else if( code != 0 ) res = 1;
   if( res ) {
     if( is_bundle ) vt->bundle_failed = 1;
     if( res==2 ) { vt->metrics[2]++; return FDGPU_VTILE_DEDUP_FAIL; }

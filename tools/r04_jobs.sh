@@ -26,6 +26,8 @@
 #   t3_ab        z    2 vs 3 vs 4 tiles at the final defaults
 #   gsize_ab     gs   max-leg gathers of 4K / 16K / 32K / 64K records (copy_min with copy wait and uncopied bound)
 #   big_ab       gt   with ~20K-record gathers (the new max-leg default): 2 vs 3 tiles, 2 producers
+#   host_ab      ha   tile host trims (one tcache probe per verdict, one fault check per frag) vs the previous
+#                     build (firedancer_amd/ab_vtile_old.so)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 
@@ -169,6 +171,10 @@ gsize_ab)
 big_ab)
   run_arms r04gt "$Q --stream-rates 5e6 --stream-paced-seconds 1 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
     t2a= "t3a=--stream-tiles 3" "t2p2a=--stream-producers 2" "t2p2b=--stream-producers 2" "t3b=--stream-tiles 3" t2b= ;;
+host_ab)
+  run_arms r04ha "$Q --stream-rates 10e6 --stream-paced-seconds 2 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
+    new1= "old1=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_old.so;" "old2=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_old.so;" \
+    new2= new3= "old3=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_old.so;" ;;
 *)
-  sed -n '2,28p' "$0"; exit 2 ;;
+  sed -n '2,30p' "$0"; exit 2 ;;
 esac
