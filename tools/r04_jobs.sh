@@ -28,6 +28,7 @@
 #   big_ab       gt   with ~20K-record gathers (the new max-leg default): 2 vs 3 tiles, 2 producers
 #   host_ab      ha   tile host trims (one tcache probe per verdict, one fault check per frag) vs the previous
 #                     build (firedancer_amd/ab_vtile_old.so)
+#   pf_ab        pf   tile-loop prefetch distance 1 / 2 / 4 / 8 own frags, now that the loop bounds the max rate
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 
@@ -175,6 +176,10 @@ host_ab)
   run_arms r04ha "$Q --stream-rates 10e6 --stream-paced-seconds 2 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
     new1= "old1=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_old.so;" "old2=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_old.so;" \
     new2= new3= "old3=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_old.so;" ;;
+pf_ab)
+  run_arms r04pf "$Q --stream-rates 10e6 --stream-paced-seconds 2 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
+    p1a= "p4a=--stream-pf-dist 4" "p8a=--stream-pf-dist 8" "p2a=--stream-pf-dist 2" \
+    "p2b=--stream-pf-dist 2" "p8b=--stream-pf-dist 8" "p4b=--stream-pf-dist 4" p1b= ;;
 *)
-  sed -n '2,30p' "$0"; exit 2 ;;
+  sed -n '2,31p' "$0"; exit 2 ;;
 esac
