@@ -29,6 +29,7 @@
 #   host_ab      ha   tile host trims (one tcache probe per verdict, one fault check per frag) vs the previous
 #                     build (firedancer_amd/ab_vtile_old.so)
 #   pf_ab        pf   tile-loop prefetch distance 1 / 2 / 4 / 8 own frags, now that the loop bounds the max rate
+#   o3_ab        o3   the tile library at -O3 -march=x86-64-v3 (firedancer_amd/ab_vtile_o3.so) vs -O2
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 
@@ -180,6 +181,10 @@ pf_ab)
   run_arms r04pf "$Q --stream-rates 10e6 --stream-paced-seconds 2 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
     p1a= "p4a=--stream-pf-dist 4" "p8a=--stream-pf-dist 8" "p2a=--stream-pf-dist 2" \
     "p2b=--stream-pf-dist 2" "p8b=--stream-pf-dist 8" "p4b=--stream-pf-dist 4" p1b= ;;
+o3_ab)
+  run_arms r04o3 "$Q --stream-rates 10e6 --stream-paced-seconds 2 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
+    o2a= "o3a=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_o3.so;" "o3b=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_o3.so;" \
+    o2b= o2c= "o3c=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_o3.so;" ;;
 *)
-  sed -n '2,31p' "$0"; exit 2 ;;
+  sed -n '2,32p' "$0"; exit 2 ;;
 esac
