@@ -30,6 +30,8 @@
 #                     build (firedancer_amd/ab_vtile_old.so)
 #   pf_ab        pf   tile-loop prefetch distance 1 / 2 / 4 / 8 own frags, now that the loop bounds the max rate
 #   o3_ab        o3   the tile library at -O3 -march=x86-64-v3 (firedancer_amd/ab_vtile_o3.so) vs -O2
+#   first_ab     fi   stream legs before the bench process opens its own GPU queues (--stream-first): the paced
+#                     legs' occasional 0.5-1.7 ms gather-start stalls
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 
@@ -185,6 +187,9 @@ o3_ab)
   run_arms r04o3 "$Q --stream-rates 10e6 --stream-paced-seconds 2 --stream-seconds 5 --stream-unrel-seconds 1 --stream-prof" \
     o2a= "o3a=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_o3.so;" "o3b=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_o3.so;" \
     o2b= o2c= "o3c=ENV:FDGPU_VTILE_LIB=firedancer_amd/ab_vtile_o3.so;" ;;
+first_ab)
+  run_arms r04fi "$Q --stream-rates 5e6,10e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
+    b1= f1=--stream-first f2=--stream-first b2= b3= f3=--stream-first ;;
 *)
-  sed -n '2,32p' "$0"; exit 2 ;;
+  sed -n '2,33p' "$0"; exit 2 ;;
 esac
