@@ -32,6 +32,7 @@
 #   o3_ab        o3   the tile library at -O3 -march=x86-64-v3 (firedancer_amd/ab_vtile_o3.so) vs -O2
 #   first_ab     fi   stream legs before the bench process opens its own GPU queues (--stream-first): the paced
 #                     legs' occasional 0.5-1.7 ms gather-start stalls
+#   pcw_ab       pcw  the paced tile's copy wait (25 / 50 / 100 / 200 us): gather launches are ~12 % of its loop
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 
@@ -190,6 +191,10 @@ o3_ab)
 first_ab)
   run_arms r04fi "$Q --stream-rates 5e6,10e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
     b1= f1=--stream-first f2=--stream-first b2= b3= f3=--stream-first ;;
+pcw_ab)
+  run_arms r04pcw "$Q --stream-rates 7.5e6,10e6,12.5e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
+    c50a= "c100a=--stream-copy-wait-us 100" "c200a=--stream-copy-wait-us 200" "c25a=--stream-copy-wait-us 25" \
+    "c25b=--stream-copy-wait-us 25" "c200b=--stream-copy-wait-us 200" "c100b=--stream-copy-wait-us 100" c50b= ;;
 *)
-  sed -n '2,33p' "$0"; exit 2 ;;
+  sed -n '2,34p' "$0"; exit 2 ;;
 esac
