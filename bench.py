@@ -194,7 +194,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 # uncopied at most), max rate 25.7-25.8M vs 23.3-23.5M at ~2.6K (profiles/r04/gs); the paced and
                 # the unreliable legs keep the tile's defaults (a later copy leaves a frag exposed to overruns
                 # longer: unreliable goodput 17.0M vs 19.1M, profiles/r04/s)
-                copy_wait_ns=int((args.stream_tput_copy_wait_us if tput else args.stream_copy_wait_us) * 1000),
+                copy_wait_ns=int((args.stream_tput_copy_wait_us if tput else
+                                  args.stream_lat_copy_wait_us if paced else args.stream_copy_wait_us) * 1000),
                 gather_cus=args.stream_gather_cus,
                 max_uncopied=args.stream_tput_max_uncopied if tput else args.stream_max_uncopied,
                 copy_min=args.stream_tput_copy_min if tput else 0, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
@@ -387,6 +388,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-tput-copy-wait-us", str(args.stream_tput_copy_wait_us),
            "--stream-tput-max-uncopied", str(args.stream_tput_max_uncopied),
            "--stream-tput-copy-min", str(args.stream_tput_copy_min),
+           "--stream-lat-copy-wait-us", str(args.stream_lat_copy_wait_us),
            "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
         (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else []) + \
         (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else []) + \
@@ -676,12 +678,15 @@ def parse_args(argv=None) -> argparse.Namespace:
                          "copies (default), the batch's finish kernel (A/B), or nobody (DIAGNOSTIC: published records lack "
                          "their payload -- what the write-back costs; never a result)")
     ap.add_argument("--stream-copy-wait-us", type=float, default=0.0,
-                    help="paced / unreliable legs, zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
+                    help="unreliable legs, zero-copy intake: a tile starts the GPU copy of the frags it took once the oldest has "
                          "waited this long (0 = fdgpu_vtile default, FDGPU_VTILE_COPY_WAIT_NS)")
     ap.add_argument("--stream-tput-copy-wait-us", type=float, default=2000.0,
                     help="reliable max-rate legs (cal, max): --stream-copy-wait-us of their tiles (bigger gathers)")
     ap.add_argument("--stream-tput-max-uncopied", type=int, default=131072,
                     help="reliable max-rate legs (cal, max): --stream-max-uncopied of their tiles")
+    ap.add_argument("--stream-lat-copy-wait-us", type=float, default=25.0,
+                    help="paced legs: --stream-copy-wait-us of their tile (25 us: p99 at 10M frags/s 0.91 ms against "
+                         "0.92-0.95 at the tile's default 50 us, profiles/r04/pcw)")
     ap.add_argument("--stream-tput-copy-min", type=int, default=32768,
                     help="reliable max-rate legs (cal, max): a tile starts a copy once this many frags wait "
                          "(fdgpu_vtile_opts_t.copy_min; 0 = the tile's default, 4,096)")

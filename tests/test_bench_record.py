@@ -142,7 +142,9 @@ def test_leg_copy_settings():
         pytest.skip("bench.parse_args not available")
     for leg, tput in (("cal", True), ("max", True), ("paced@5000000.0", False), ("unrel", False)):
         cfg = bench._leg_cfg(args, leg, 1, 20e6)
-        assert cfg["copy_wait_ns"] == (int(args.stream_tput_copy_wait_us * 1000) if tput else 0), leg
+        want = int(args.stream_tput_copy_wait_us * 1000) if tput else \
+            int(args.stream_lat_copy_wait_us * 1000) if leg.startswith("paced") else 0
+        assert cfg["copy_wait_ns"] == want, leg
         assert cfg["max_uncopied"] == (args.stream_tput_max_uncopied if tput else 0), leg
     assert args.stream_tput_copy_wait_us == 2000.0 and args.stream_tput_max_uncopied == 131072
     assert bench._leg_cfg(args, "max", 1, 20e6)["copy_min"] == 32768 and bench._leg_cfg(args, "unrel", 1, 20e6)["copy_min"] == 0

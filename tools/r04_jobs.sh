@@ -33,6 +33,8 @@
 #   first_ab     fi   stream legs before the bench process opens its own GPU queues (--stream-first): the paced
 #                     legs' occasional 0.5-1.7 ms gather-start stalls
 #   pcw_ab       pcw  the paced tile's copy wait (25 / 50 / 100 / 200 us): gather launches are ~12 % of its loop
+#                     (run with --stream-copy-wait-us, which then covered the paced legs)
+#   pcw2_ab      pcw2 paced copy wait 25 (the new bench default) vs 12.5 us
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 
@@ -192,9 +194,12 @@ first_ab)
   run_arms r04fi "$Q --stream-rates 5e6,10e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
     b1= f1=--stream-first f2=--stream-first b2= b3= f3=--stream-first ;;
 pcw_ab)
-  run_arms r04pcw "$Q --stream-rates 7.5e6,10e6,12.5e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
-    c50a= "c100a=--stream-copy-wait-us 100" "c200a=--stream-copy-wait-us 200" "c25a=--stream-copy-wait-us 25" \
-    "c25b=--stream-copy-wait-us 25" "c200b=--stream-copy-wait-us 200" "c100b=--stream-copy-wait-us 100" c50b= ;;
+  run_arms r04pcw "$Q --stream-lat-copy-wait-us 50 --stream-rates 7.5e6,10e6,12.5e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
+    c50a= "c100a=--stream-lat-copy-wait-us 100" "c200a=--stream-lat-copy-wait-us 200" "c25a=--stream-lat-copy-wait-us 25" \
+    "c25b=--stream-lat-copy-wait-us 25" "c200b=--stream-lat-copy-wait-us 200" "c100b=--stream-lat-copy-wait-us 100" c50b= ;;
+pcw2_ab)
+  run_arms r04pcw2 "$Q --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
+    c25a= "c12a=--stream-lat-copy-wait-us 12.5" "c12b=--stream-lat-copy-wait-us 12.5" c25b= c25c= "c12c=--stream-lat-copy-wait-us 12.5" ;;
 *)
-  sed -n '2,34p' "$0"; exit 2 ;;
+  sed -n '2,35p' "$0"; exit 2 ;;
 esac
