@@ -1477,7 +1477,7 @@ static int cpu_first_of( char const * fmt, int cpu ) {          /* lowest CPU of
 /* Busy fraction of each CPU over `ms` milliseconds (/proc/stat): the cores another process keeps busy
    are not worth pinning a spinning tile to.  Returns 0 on success. */
 static int cpu_busy_sample( double * busy, int ms ) {
-  static ulong t0[ LINK_CPU_MAX ], i0[ LINK_CPU_MAX ];
+  ulong t0[ LINK_CPU_MAX ] = { 0 }, i0[ LINK_CPU_MAX ] = { 0 };   /* (on the stack: link_run may run in several threads) */
   for( int pass=0; pass<2; pass++ ) {
     FILE * f = fopen( "/proc/stat", "r" );
     if( !f ) return -1;
@@ -1513,7 +1513,7 @@ link_pick_cpus( int device, int proc, int n, int * out ) {
   }
   cpu_set_t aff; CPU_ZERO( &aff );
   if( sched_getaffinity( 0, sizeof(aff), &aff ) ) return 0;
-  static uchar node_set[ LINK_CPU_MAX ];
+  uchar node_set[ LINK_CPU_MAX ];
   memset( node_set, 0, sizeof(node_set) );
   int node = fdgpu_device_numa_node( device ), use_node = 0;
   if( node >= 0 ) {
@@ -1522,13 +1522,13 @@ link_pick_cpus( int device, int proc, int n, int * out ) {
   }
   /* a shared machine: skip cores (either hardware thread) that another process kept busy over a short
      sample, unless too few idle ones are left (FDGPU_LINK_PIN=lowest: no sample, the lowest cores) */
-  static double busy[ LINK_CPU_MAX ];
+  double busy[ LINK_CPU_MAX ];
   memset( busy, 0, sizeof(busy) );
   if( !( env && !strcmp( env, "lowest" ) ) ) cpu_busy_sample( busy, 30 );
   /* candidate cores: one hardware thread (the lowest sibling) of each allowed core */
   int cand[ LINK_CPU_MAX ], grp[ LINK_CPU_MAX ], nc = 0;
   uchar hot[ LINK_CPU_MAX ];
-  static uchar sib[ LINK_CPU_MAX ];
+  uchar sib[ LINK_CPU_MAX ];
   for( int pass=0; pass<2 && !nc; pass++ )                       /* pass 1: ignore the node if it has no allowed CPU */
     for( int c=0; c<LINK_CPU_MAX && c<CPU_SETSIZE; c++ ) {
       if( !CPU_ISSET( c, &aff ) || ( pass==0 && use_node && !node_set[c] ) ) continue;
