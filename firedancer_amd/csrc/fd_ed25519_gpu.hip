@@ -3618,20 +3618,28 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
     unsigned long k = sl.txn_cnt - sl.cursor;
     if( k > max - n ) k = max - n;
     unsigned long pf = (unsigned long)ctx->poll_pf;
+    /* the slot's arrays in locals: the out arrays could alias them as far as the compiler knows, which
+       would reload every field of the slot on every iteration */
+    unsigned long const * __restrict__ h_tags = sl.h_tags;
+    signed char const *   __restrict__ h_out  = (signed char const *)sl.h_txn_out;
+    unsigned short const * __restrict__ h_fp  = sl.h_fp;
+    unsigned long const * __restrict__ h_dtag = sl.h_dtag;
+    unsigned long const cur = sl.cursor, cnt = sl.txn_cnt;
+    int const mode = sl.mode, want_dtag = sl.mode && ctx->dedup;
     for( unsigned long t=0; t<k; t++ ) {
-      unsigned long u = sl.cursor + t;
+      unsigned long u = cur + t;
       /* the result arrays were written by the GPU over PCIe: their lines are not in the CPU's caches */
-      if( pf && !( u & 7UL ) && u + pf < sl.txn_cnt ) {
-        __builtin_prefetch( sl.h_tags + u + pf );
-        if( sl.mode ) { __builtin_prefetch( sl.h_dtag + u + pf ); __builtin_prefetch( sl.h_fp + u + 4*pf ); }
-        __builtin_prefetch( sl.h_txn_out + u + 8*pf );
+      if( pf && !( u & 7UL ) && u + pf < cnt ) {
+        __builtin_prefetch( h_tags + u + pf );
+        if( mode ) { __builtin_prefetch( h_dtag + u + pf ); __builtin_prefetch( h_fp + u + 4*pf ); }
+        __builtin_prefetch( h_out + u + 8*pf );
       }
-      out_tags[n+t]  = sl.h_tags[u];
-      out_codes[n+t] = sl.h_txn_out[u];
-      if( out_fp )  out_fp[n+t] = sl.mode ? sl.h_fp[u] : 0;
-      if( out_dtag ) out_dtag[n+t] = ( sl.mode && ctx->dedup ) ? sl.h_dtag[u] : 0UL;
-      if( out_img && sl.mode && sl.mode != 3 ) {   /* mode 3: the image is in the caller's out region */
-        unsigned fp = sl.h_fp[u];
+      out_tags[n+t]  = h_tags[u];
+      out_codes[n+t] = h_out[u];
+      if( out_fp )  out_fp[n+t] = mode ? h_fp[u] : 0;
+      if( out_dtag ) out_dtag[n+t] = want_dtag ? h_dtag[u] : 0UL;
+      if( out_img && mode && mode != 3 ) {         /* mode 3: the image is in the caller's out region */
+        unsigned fp = h_fp[u];
         memcpy( out_img + (n+t)*FDGPU_TXN_IMG_STRIDE, sl.h_img + u*FDGPU_TXN_IMG_STRIDE, fp );
       }
     }
