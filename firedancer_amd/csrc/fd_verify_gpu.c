@@ -1609,6 +1609,7 @@ link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, 
   /* bench accounting only (not after_frag): the signature count comes from
      the link's per-payload table, not from the (cold) record in the out dcache */
   ulong t = now_ns(), np = l->h->n_payload, Q = (ulong)l->h->cfg.producers;
+  ulong pmask = ( np & ( np - 1UL ) ) ? 0UL : np - 1UL;   /* a power-of-two payload count: a mask, not a division */
   for( ulong i=0; i<n; i++ ) {
     ulong lat = t - d[i].tsorig;
     lh[ lh_idx( lat ) ]++;
@@ -1617,7 +1618,7 @@ link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, 
     ulong s = d[i].seq;
     in[q].fin++;
     if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL )
-      *sigs += l->psig[ ( s * Q + (ulong)q ) % np ];
+      *sigs += l->psig[ pmask ? ( ( s * Q + (ulong)q ) & pmask ) : ( s * Q + (ulong)q ) % np ];
     if( __builtin_expect( d[i].result != FDGPU_VTILE_PUBLISH && d[i].result != FDGPU_VTILE_OVERRUN, 0 ) ) {
       ulong k = l->anom_cnt[idx]++;
       if( k < LINK_ANOM_MAX ) {                  /* rec_hash: the frag's payload index (the link's layout) */
