@@ -421,6 +421,22 @@ def _r(x, nd=4):
     return x
 
 
+PATH_NAMES = {8: "latency8", 4: "latency4", 2: "latency2", 1: "latency1", 0: "throughput", -1: "throughput_full",
+              -2: "none"}
+
+
+def anomaly_summary(anomalies: dict | None) -> tuple[int, dict | None]:
+    """(count, the first record) of a stream's anomalies (fdgpu_link_anomalies, merged per leg over ranks)."""
+    n, first = 0, None
+    for leg, v in (anomalies or {}).items():
+        n += int(v.get("count", 0))
+        if first is None and v.get("first"):
+            first = dict(v["first"][0], leg=leg)
+            if "path" in first:
+                first["path"] = PATH_NAMES.get(first["path"], first["path"])
+    return n, first
+
+
 def compact_record(full: dict, detail_path: str | None) -> dict:
     """The one JSON line the driver parses (printed last on stdout, <= HEADLINE_MAX_BYTES): the BASELINE
     metric, its roofline and CPU baseline, and one-number summaries of the side measurements.  Everything
@@ -473,10 +489,14 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
         rec["extra_configs"] = {k.split("_")[0]: [_r(v["sigs_per_s"]), v["results_ok"]] for k, v in ex.items()}
     st = full.get("stream")
     if st:
+        n_anom, first_anom = anomaly_summary(st.get("anomalies"))
         if "error" in st:
             rec["stream"] = {"error": str(st["error"])[-300:]}
+            rec["stream_ok"] = False
         elif "only_paced" in st:
-            rec["stream"] = {"only_paced": {k: [_r(v["p50_us"]), _r(v["p99_us"])] for k, v in st["only_paced"].items()}}
+            rec["stream"] = {"only_paced": {k: [_r(v["p50_us"]), _r(v["p99_us"])] for k, v in st["only_paced"].items()},
+                             "anomalies": n_anom, "anomaly_first": first_anom}
+            rec["stream_ok"] = n_anom == 0
         else:
             curve = st.get("latency_curve") or []
             rec["stream"] = {
@@ -490,7 +510,10 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 "tile_host_ns_per_frag": (st.get("max_rate") or {}).get("tile_host_ns_per_frag"),
                 "all_published": st.get("all_published"),
                 "host_cpu_share_min": _r(st.get("host_cpu_share_min")),
-                "anomalies": sum(v["count"] for v in (st.get("anomalies") or {}).values())}
+                # verdicts neither published nor overrun (none expected in these all-valid streams), and the
+                # first one with the GPU batch that produced it (leg, tile, ctx, seq, payload, code, path)
+                "anomalies": n_anom, "anomaly_first": first_anom}
+            rec["stream_ok"] = bool(st.get("all_published")) and n_anom == 0
     rec["detail"] = detail_path
     return rec
 

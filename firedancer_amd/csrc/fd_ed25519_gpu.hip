@@ -395,15 +395,23 @@ FD_DEV void hs_store_digits( u32 const c0[ 5 ], u32 const c1m[ 5 ], int c1neg, u
     digR[(size_t)i*n + s] = (i8)( c1neg ? -dr : dr );
     top = ( da | dr ) ? i : top;
   }
-  htop[s] = (unsigned char)top;                     /* highest window with a nonzero digit */
   int carry = 0;
 #pragma unroll
   for( int i=0; i<FD_BDIG; i++ ) {
     int bit = FD_BWIN*i;
     int v = (int)((sp[bit>>5] >> (bit&31)) & ((1u<<FD_BWIN)-1u)) + carry;
     carry = (v + (1<<(FD_BWIN-1))) >> FD_BWIN;
-    digB[(size_t)i*n + s] = (short)(v - (carry << FD_BWIN));
+    int db = v - (carry << FD_BWIN);
+    digB[(size_t)i*n + s] = (short)db;
+    /* the walks add s' digit i at window 4i (i < 8) or 4(i-8)+2 (i >= 8, the 2^120 B table): the top
+       window counts these too.  (Round 4 took it from c0 / c1 alone; a wave whose pending signatures all
+       had c0, c1 < 2^120 -- ~7.5e-6 of hash-distributed k, alone in a batch or in its last wave -- then
+       started below window 30, skipped s' digits 7 / 15 and rejected a valid signature with ERR_MSG:
+       tests/test_gpu_hs_top.py, tests/golden/hs_top.npz.) */
+    int wb = i < 8 ? 4*i : 4*(i-8) + 2;
+    top = ( db && wb > top ) ? wb : top;
   }
+  htop[s] = (unsigned char)top;                     /* highest window with a nonzero digit of c0, c1 or s' */
 }
 
 /* The wave's top window (half-size walks): the largest htop of its pending
@@ -913,8 +921,8 @@ fd_dsmh_kernel( u32                      nsig,
   int c = s < nsig ? (int)code[s] : FD_ED25519_ERR_SIG;
   if( rc && s < nsig ) c = result_code( c, pstat[2*s], pstat[2*s+1], semantics, 0 );
   int pend = c == FD_ED25519_SUCCESS && !( pstat[2*s] & FD_PSTAT_SLOW );
-  /* the walk starts at the wave's highest nonzero window (32 unless a lane's
-     scalar exceeds 2^131): every lane of the wave is still here */
+  /* the walk starts at the wave's highest nonzero window of c0, c1 and s' (31-32 unless a lane's
+     scalar exceeds 2^131; window 30 or above while s' >= 2^240): every lane of the wave is still here */
   int wtop = hs_wave_top( pend, htop, s );
   if( !pend ) { if( rc && s < nsig && c != FD_PEND_SLOW ) code[s] = (i8)c; return; }
   FD_CLK_BEGIN
@@ -2084,6 +2092,7 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   unsigned long *    hd_dtag;
   unsigned char *    hd_img;
   unsigned long      gt_target;/*         ... and the gathered count it ends at (the entry may be reused) */
+  int                path;     /* the engine path its batch ran (FDGPU_PATH_* or lanes, fdgpu_ed25519_front_batch) */
 };
 
 struct fdgpu_ed25519_ctx {
@@ -2111,6 +2120,8 @@ struct fdgpu_ed25519_ctx {
   int gather_nowb;               /* fdgpu_debug_opts_t.gather_no_writeback: 0 = the records' write-back in
                                     the gather kernel, 1 = none (diagnostic), 2 = in fd_finish_kernel (A/B) */
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
+  int last_path;                 /* the engine path launch_batch chose last (FDGPU_PATH_* or latency lanes) */
+  int           excl_mode;       /* fdgpu_ed25519_set_cu_exclusive's mode; -1: off, chosen by fdgpu_debug_opts_t */
   unsigned      excl_lds[ 7 ];   /* fdgpu_ed25519_set_cu_exclusive: dynamic LDS per workgroup of the latency path's
                                     prep<0,1>, prep<0,0>, dsm8, dsm4<0,1>, dsm4<0,0>, dsm2<0,1>, dsm2<0,0> (0 = none) */
   unsigned long nofold_max;      /* fd_dsm_kernel<0> (no carry fold) for batches of at most this many signatures */
@@ -2214,18 +2225,29 @@ fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long smal
    of the extra), so no second such workgroup -- of this batch or of another context's concurrent one -- shares
    its SIMDs.  A small batch runs under one wave per SIMD, its time the per-wave chain; a second wave on the
    SIMD stretches that chain (profiles/r04/n: prep 108 us alone, 206 us beside the other context's walk). */
-#define FD_EXCL_LDS ( 84u * 1024u )
+/* The reservation is derived from the device's LDS per CU (160 KiB on gfx950): mode 1 takes more than half
+   of it (84 KiB there), mode 2 more than a third (56 KiB: two fit, three do not).  The kernels' maximum
+   dynamic LDS (a process-wide function attribute) is raised once to what mode 1 needs, so contexts with
+   different modes never undo each other's; each context keeps its own choice in excl_lds. */
+static std::mutex g_excl_mu;
+static unsigned   g_excl_max[ 7 ];     /* per kernel: the dynamic LDS its attribute allows (0: not raised yet) */
 extern "C" int
 fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on ) {
   if( !ctx || on < 0 || on > 4 ) return -1;
   /* on (A/B): 1 prep and walk alone on their CU; 2 at most two per CU; 3 the walk alone; 4 the prep alone */
-  unsigned want = on == 2 ? 56u * 1024u : FD_EXCL_LDS;
   void const * f[ 7 ] = { (void const *)fd_prep_kernel<0,1>, (void const *)fd_prep_kernel<0,0>, (void const *)fd_dsm8_kernel<0>,
                           (void const *)fd_dsm4_kernel<0,1>, (void const *)fd_dsm4_kernel<0,0>,
                           (void const *)fd_dsm2_kernel<0,1>, (void const *)fd_dsm2_kernel<0,0> };
   unsigned v[ 7 ] = { 0u, 0u, 0u, 0u, 0u, 0u, 0u };
   if( on ) {
     HIPCHK( hipSetDevice( ctx->device ), -2 );
+    int lds = 0;
+    HIPCHK( hipDeviceGetAttribute( &lds, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, ctx->device ), -2 );
+    if( lds < 3 * 1024 ) { fd_err = "fdgpu_ed25519_set_cu_exclusive: no LDS size"; return -1; }
+    unsigned half = ( (unsigned)lds / 2u + 4096u ) & ~1023u;          /* > 1/2: one workgroup per CU */
+    unsigned third = ( (unsigned)lds / 3u + 2048u ) & ~1023u;         /* > 1/3, <= 1/2: two per CU */
+    unsigned want = on == 2 ? third : half;
+    std::lock_guard<std::mutex> lk( g_excl_mu );
     for( int i=0; i<7; i++ ) {
       hipFuncAttributes a;
       HIPCHK( hipFuncGetAttributes( &a, f[i] ), -2 );
@@ -2233,12 +2255,20 @@ fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on ) {
       int walk = i >= 2;
       if( ( on == 3 && !walk ) || ( on == 4 && walk ) ) continue;
       v[i] = st < want ? want - st : 0u;
-      if( v[i] ) HIPCHK( hipFuncSetAttribute( f[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)v[i] ), -2 );
+      unsigned top = st < half ? half - st : 0u;                        /* the most any mode asks of this kernel */
+      if( v[i] && g_excl_max[i] < top ) {
+        HIPCHK( hipFuncSetAttribute( f[i], hipFuncAttributeMaxDynamicSharedMemorySize, (int)top ), -2 );
+        g_excl_max[i] = top;
+      }
     }
   }
   for( int i=0; i<7; i++ ) ctx->excl_lds[i] = v[i];
+  ctx->excl_mode = on;
   return 0;
 }
+
+extern "C" int
+fdgpu_ed25519_get_cu_exclusive( fdgpu_ed25519_ctx_t const * ctx ) { return ctx ? ctx->excl_mode : 0; }
 
 extern "C" char const * fdgpu_last_error( void ) { return fd_err.c_str(); }
 
@@ -2261,6 +2291,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
   u32 nsig = (u32)sig_cnt;
   unsigned tg = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   unsigned sg = (unsigned)( (sig_cnt + FD_WG - 1) / FD_WG );
+  ctx->last_path = FDGPU_PATH_NONE;
   if( nsig ) {
     if( !( flags & 1 ) )
       hipLaunchKernelGGL( fd_expand_kernel, dim3(tg), dim3(FD_WG), 0, st, d_desc, (u32)txn_cnt, ctx->d_map, nsig,
@@ -2280,6 +2311,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM8_MAX && ctx->half ? 8 : nsig <= FD_DSM4_MAX ? 4 :
                                                   nsig <= FD_DSM2_MAX ? 2 : 1 );
       if( lanes == 8 && !ctx->half ) lanes = 4;       /* the term split needs the half-size walk */
+      ctx->last_path = lanes;
       int d2 = lanes > 1;
       if( hs )      /* half-size: the A and R lanes build both tables, the hash lane (c0, c1, s') */
         hipLaunchKernelGGL( (fd_prep_kernel<0,1>), dim3(3*sg), dim3(FD_WG), ctx->excl_lds[0], st, d_payload, d_desc, ctx->d_map, nsig,
@@ -2296,6 +2328,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
                               ctx->d_Axy, ctx->d_tab );
       }
     } else if( half ) {
+      ctx->last_path = FDGPU_PATH_THROUGHPUT;
       /* half-size scalars: decode A and R, result codes + hash + (c0, c1, s'), both tables */
       unsigned pg = (unsigned)( ( 2UL*sig_cnt + FD_WG - 1) / FD_WG );
 #if FD_HALF_FUSED_TABLE
@@ -2318,6 +2351,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
                           ctx->d_tab, ctx->d_tabR );
 #endif
     } else {
+      ctx->last_path = FDGPU_PATH_THROUGHPUT_FULL;
       unsigned pg = (unsigned)( ( (defer ? 1UL : 2UL)*sig_cnt + FD_WG - 1) / FD_WG );
       hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, !defer,
                           ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, (uint4 *)NULL, (uint4 *)NULL );
@@ -2509,7 +2543,8 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   memset( ctx->h_stamp, 0, ( 2*fdgpu_ed25519_ctx_t::NSLOT + 1 ) * sizeof(unsigned long) );
   HIPCHK( hipHostGetDevicePointer( (void **)&ctx->d_stamp, (void *)ctx->h_stamp, 0 ), -1 );
   ctx->last_gt = -1;
-  if( dbg.cu_exclusive && fdgpu_ed25519_set_cu_exclusive( ctx, dbg.cu_exclusive ) ) return -1;
+  if( dbg.cu_exclusive > 0 && fdgpu_ed25519_set_cu_exclusive( ctx, dbg.cu_exclusive ) ) return -1;
+  if( dbg.cu_exclusive < 0 ) ctx->excl_mode = -1;      /* explicitly off: a verify tile keeps it off too */
   /* slot 0 now (the synchronous host calls stage through it); the async
      pipeline's other slots on first use (slot_bufs) */
   if( max_payload_bytes && slot_bufs( ctx, 0 ) ) return -1;
@@ -3125,7 +3160,7 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
   hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + i, sl.token, ctx->d_stamp + 2*i + 1 );
   HIPCHK( hipGetLastError(), -2 );
   HIPCHK( hipEventRecord( sl.done, st ), -2 );
-  sl.state = 1; sl.cursor = 0;
+  sl.state = 1; sl.cursor = 0; sl.path = ctx->last_path;
   sl.launch_ns = sl.last_query = fd_now_ns();
   ctx->n_batches++; ctx->n_txns += sl.txn_cnt;
   ctx->inflight.push_back( i );
@@ -3281,27 +3316,34 @@ fdgpu_ed25519_submit_raw_ref( fdgpu_ed25519_ctx_t * ctx, unsigned char const * b
    entry's fields and then publish it with a release store of its size; a
    removed entry's size drops to 0 first. */
 #define FD_REGION_MAX 256
-struct fd_region { unsigned char const * h; unsigned char * d; std::atomic<unsigned long> sz; };
+struct fd_region { unsigned char const * h; unsigned char * d; std::atomic<unsigned long> sz; int refs; };
 static std::mutex g_reg_mu;
 static fd_region g_regions[ FD_REGION_MAX ];
 static std::atomic<int> g_region_cnt{ 0 };
 
-static void region_add( void * h, void * d, unsigned long sz ) {
-  std::lock_guard<std::mutex> lk( g_reg_mu );
+static void region_add_locked( void * h, void * d, unsigned long sz ) {
   int n = g_region_cnt.load( std::memory_order_relaxed ), i = 0;
   while( i < n && g_regions[i].sz.load( std::memory_order_relaxed ) ) i++;     /* reuse a removed entry */
   if( i == FD_REGION_MAX ) return;
-  g_regions[i].h = (unsigned char const *)h; g_regions[i].d = (unsigned char *)d;
+  g_regions[i].h = (unsigned char const *)h; g_regions[i].d = (unsigned char *)d; g_regions[i].refs = 1;
   g_regions[i].sz.store( sz, std::memory_order_release );
   if( i == n ) g_region_cnt.store( n + 1, std::memory_order_release );
 }
-static void region_del( void * h ) {
+static void region_add( void * h, void * d, unsigned long sz ) {
   std::lock_guard<std::mutex> lk( g_reg_mu );
+  region_add_locked( h, d, sz );
+}
+/* the live entry starting at h (-1: none); under g_reg_mu */
+static int region_find_locked( void const * h ) {
   int n = g_region_cnt.load( std::memory_order_relaxed );
   for( int i=0; i<n; i++ )
-    if( g_regions[i].h == (unsigned char const *)h && g_regions[i].sz.load( std::memory_order_relaxed ) ) {
-      g_regions[i].sz.store( 0UL, std::memory_order_release ); return;
-    }
+    if( g_regions[i].h == (unsigned char const *)h && g_regions[i].sz.load( std::memory_order_relaxed ) ) return i;
+  return -1;
+}
+static void region_del( void * h ) {
+  std::lock_guard<std::mutex> lk( g_reg_mu );
+  int i = region_find_locked( h );
+  if( i >= 0 ) g_regions[i].sz.store( 0UL, std::memory_order_release );
 }
 /* device address of [p, p+sz) if it lies inside one registered region, else NULL */
 static unsigned char * region_dev( void const * p, unsigned long sz ) {
@@ -3347,19 +3389,38 @@ fdgpu_host_alloc( unsigned long sz ) {
 
 extern "C" void fdgpu_host_free( void * p ) { if( p ) { region_del( p ); hipHostFree( p ); } }
 
+/* Registrations are counted: registering exactly the same range again (two handles on one mcache ring)
+   takes another reference, and the range stays registered until the last fdgpu_host_unregister. */
 extern "C" int
 fdgpu_host_register( void * p, unsigned long sz ) {
   if( !p || !sz ) { fd_err = "fdgpu_host_register: empty range"; return -1; }
+  std::lock_guard<std::mutex> lk( g_reg_mu );
+  int i = region_find_locked( p );
+  if( i >= 0 ) {
+    if( g_regions[i].sz.load( std::memory_order_relaxed ) != sz ) {
+      fd_err = "fdgpu_host_register: another range starting there is registered"; return -2;
+    }
+    g_regions[i].refs++;
+    return 0;
+  }
   HIPCHK( hipHostRegister( p, sz, hipHostRegisterMapped ), -2 );
   void * d = NULL;
   hipError_t e = hipHostGetDevicePointer( &d, p, 0 );
   if( e != hipSuccess ) { set_err( "hipHostGetDevicePointer", e ); (void)hipHostUnregister( p ); return -2; }
-  region_add( p, d, sz );
+  region_add_locked( p, d, sz );
   return 0;
 }
 
 extern "C" void
-fdgpu_host_unregister( void * p ) { if( p ) { region_del( p ); (void)hipHostUnregister( p ); } }
+fdgpu_host_unregister( void * p ) {
+  if( !p ) return;
+  std::lock_guard<std::mutex> lk( g_reg_mu );
+  int i = region_find_locked( p );
+  if( i < 0 ) return;
+  if( --g_regions[i].refs > 0 ) return;
+  g_regions[i].sz.store( 0UL, std::memory_order_release );
+  (void)hipHostUnregister( p );
+}
 
 extern "C" int
 fdgpu_device_numa_node( int device ) {
@@ -3688,6 +3749,14 @@ fdgpu_ed25519_front_remaining( fdgpu_ed25519_ctx_t const * ctx ) {
   if( ctx->inflight.empty() ) return 0UL;
   fd_slot const & sl = ctx->slot[ ctx->inflight.front() ];
   return sl.txn_cnt - sl.cursor;
+}
+
+extern "C" int
+fdgpu_ed25519_front_batch( fdgpu_ed25519_ctx_t const * ctx, unsigned long * txn_cnt, unsigned long * cursor, int * path ) {
+  if( ctx->inflight.empty() ) { *txn_cnt = 0UL; *cursor = 0UL; *path = FDGPU_PATH_NONE; return 0; }
+  fd_slot const & sl = ctx->slot[ ctx->inflight.front() ];
+  *txn_cnt = sl.txn_cnt; *cursor = sl.cursor; *path = sl.path;
+  return 1;
 }
 
 extern "C" void

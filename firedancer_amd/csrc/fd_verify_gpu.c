@@ -424,7 +424,9 @@ vt_ctx_new( fdgpu_vtile_t const * vt, int k ) {
     if( vt->opt.gather_cus && fdgpu_ed25519_reserve_cus( c, vt->opt.gather_cus, part, parts ) ) {
       fdgpu_ed25519_ctx_delete( c ); return NULL;
     }
-    int excl = vt->opt.cu_exclusive ? vt->opt.cu_exclusive : 1;         /* 0 = default: on */
+    /* 0 = default: on -- unless the engine's test hook (fdgpu_debug_opts_t.cu_exclusive) already chose a
+       mode for new contexts, which the tile then keeps (the tile tests' latency8 / latency8x paths) */
+    int excl = vt->opt.cu_exclusive ? vt->opt.cu_exclusive : ( fdgpu_ed25519_get_cu_exclusive( c ) ? 0 : 1 );
     if( excl > 0 && fdgpu_ed25519_set_cu_exclusive( c, excl ) ) { fdgpu_ed25519_ctx_delete( c ); return NULL; }
     fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
     /* every staging buffer and the gather stream now: batches then allocate nothing (the tile's sandbox
@@ -605,9 +607,17 @@ fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_
   /* the GPU re-reads each frag's mcache line after its copy: the lines must be mapped for it */
   for( int i=0; i<n; i++ ) {
     fdgpu_mcache_t * mc = (fdgpu_mcache_t *)in_mc[i];
-    if( !mc || fdgpu_host_dev_ptr( mc->line, mc->depth * sizeof(mc_line_t) ) ) continue;
-    /* the lines' whole pages (an fd_mcache's lines start 256 bytes into its region, not on a page) */
+    if( !mc || mc->reg ) continue;
+    /* the lines' whole pages (an fd_mcache's lines start 256 bytes into its region, not on a page).  Already
+       mapped by a larger registration (the integrator registered the mcache's workspace as a whole, as
+       INTEGRATION.md does): nothing to do.  Mapped by exactly these pages (another handle on the same ring):
+       one more reference, so deleting either handle leaves the other's mapping.  Partly mapped: refused --
+       registering the page range would overlap the other registration (register the workspace instead). */
     ulong lo = (ulong)mc->line & ~4095UL, hi = ( (ulong)mc->line + mc->depth * sizeof(mc_line_t) + 4095UL ) & ~4095UL;
+    void * b = NULL, * d = NULL; ulong rs = 0UL;
+    int have = !fdgpu_host_region( (void const *)lo, &b, &rs, &d ) && (ulong)b + rs >= hi;
+    if( have && !( (ulong)b == lo && rs == hi - lo ) ) continue;             /* inside a larger registration */
+    if( !have && fdgpu_host_dev_ptr( mc->line, mc->depth * sizeof(mc_line_t) ) ) continue;   /* lines covered */
     if( fdgpu_host_register( (void *)lo, hi - lo ) ) return -2;
     mc->reg = 1; mc->reg_base = (void *)lo;
   }
@@ -796,7 +806,8 @@ vt_submit_host_record( fdgpu_vtile_t * vt, uchar * dst, unsigned short payload_s
   return fdgpu_ed25519_submit_raw_ref( vt->ctx[ vt->fill ], vt->dcache, dst + FDGPU_TXNM_HDR_SZ, payload_sz, vt->pend_tail );
 }
 
-static int vt_during_gossip( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong seq, ulong tsorig );
+static int vt_during_gossip( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong readable, ulong seq,
+                             ulong tsorig );
 
 /* during_frag of an fd_txn_m_t record (QUIC, bundle and send in links) */
 static int
@@ -853,7 +864,8 @@ vt_during_txnm( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong
 int
 fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, ulong in_idx, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
   if( in_idx >= FDGPU_VTILE_IN_MAX ) return -4;
-  if( vt->in_kind[ in_idx ] == FDGPU_VTILE_IN_KIND_GOSSIP ) return vt_during_gossip( vt, (int)in_idx, frag, sz, seq, tsorig );
+  /* a frag given by pointer: only its sz bytes are known to be readable */
+  if( vt->in_kind[ in_idx ] == FDGPU_VTILE_IN_KIND_GOSSIP ) return vt_during_gossip( vt, (int)in_idx, frag, sz, sz, seq, tsorig );
   return vt_during_txnm( vt, (int)in_idx, frag, sz, seq, tsorig );
 }
 
@@ -864,7 +876,13 @@ fdgpu_vtile_during_frag_chunk( fdgpu_vtile_t * vt, ulong in_idx, ulong seq, ulon
   if( in_idx >= FDGPU_VTILE_IN_MAX || !vt->in_mem[ in_idx ] ) return -4;
   /* fd_verify_tile.c:75-76,89-90: a chunk outside the link's [chunk0, wmark] is corrupt (FD_LOG_ERR) */
   if( chunk < vt->in_chunk0[ in_idx ] || chunk > vt->in_wmark[ in_idx ] ) return -4;
-  return fdgpu_vtile_during_frag( vt, in_idx, vt->in_mem[ in_idx ] + chunk * FDGPU_CHUNK_SZ, sz, seq, tsorig );
+  uchar const * frag = vt->in_mem[ in_idx ] + chunk * FDGPU_CHUNK_SZ;
+  /* a gossip frame inside its link's dcache: the region holds FDGPU_GOSSIP_MSG_MAX bytes from any chunk up to
+     wmark (fdgpu_vtile_set_in), so vote.txn's whole 1232-byte array is readable past a shorter frame, as the
+     reference reads it (fd_verify_tile.c:91-95) */
+  if( vt->in_kind[ in_idx ] == FDGPU_VTILE_IN_KIND_GOSSIP )
+    return vt_during_gossip( vt, (int)in_idx, frag, sz, FDGPU_GOSSIP_MSG_MAX, seq, tsorig );
+  return fdgpu_vtile_during_frag( vt, in_idx, frag, sz, seq, tsorig );
 }
 
 int
@@ -908,15 +926,17 @@ fdgpu_vtile_before_frag( fdgpu_vtile_t const * vt, ulong in_idx, ulong seq, ulon
    overrun to check).  The reference leaves the record's other header
    fields as the chunk's previous frag left them; here they are zero. */
 static int
-vt_during_gossip( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
+vt_during_gossip( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong readable, ulong seq, ulong tsorig ) {
   if( sz > FDGPU_GOSSIP_MSG_MAX || sz < FDGPU_GOSSIP_VOTE_TXN_OFF ) return -4;   /* :89-90 */
   uchar const * msg = (uchar const *)frag;
   ulong txn_sz; memcpy( &txn_sz, msg + FDGPU_GOSSIP_VOTE_TXN_SZ_OFF, sizeof(ulong) );
   /* the reference copies vote.txn_sz bytes out of the 1232-byte vote.txn array unchecked
      (fd_verify_tile.c:91-95), also past the frame the gossip tile publishes (FD_GOSSIP_UPDATE_SZ_VOTE
-     = 1297 bytes ends 1225 bytes into vote.txn, fd_gossip_private.h:80): so does this.  Past the array
-     there is nothing defined to copy: refused as corrupt */
-  if( txn_sz > 1232UL ) return -4;
+     = 1297 bytes ends 1225 bytes into vote.txn, fd_gossip_private.h:80): so does this where the bytes
+     are known to be readable (`readable` from frag: the link's dcache on the chunk path, the frame
+     itself for a frag given by pointer).  Past the array there is nothing defined to copy: refused as
+     corrupt, as is a vote that would be read past the readable bytes */
+  if( txn_sz > 1232UL || FDGPU_GOSSIP_VOTE_TXN_OFF + txn_sz > readable ) return -4;
   int rc = vt_room( vt );
   if( rc ) return rc;
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
@@ -948,6 +968,7 @@ static int
 vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, unsigned fp, ulong tag,
           fdgpu_vtile_done_t * d ) {
   d->seq = p->seq; d->in_idx = (ulong)p->in_idx; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
+  d->code = code;
   /* zero-copy: the GPU re-read the frag's mcache line right after copying it and found it reused
      -- the stem's "overrun while reading" (fd_stem.c:667-686), decided at copy time: the frag
      never reaches after_frag in the reference, so no bundle state or metric changes */
@@ -1017,7 +1038,8 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
         vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
         fdgpu_vtile_done_t * d = &out[n];
         d->seq = p->seq; d->in_idx = (ulong)p->in_idx; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
-        d->result = FDGPU_VTILE_GPU_FAULT;
+        d->result = FDGPU_VTILE_GPU_FAULT; d->code = 0;
+        d->ctx = (unsigned)c; d->batch_txns = 0U; d->batch_pos = 0U; d->path = FDGPU_PATH_NONE;
         vt->gm.gpu_fault_frags++;
         vt_pop( vt, p ); n++;
       }
@@ -1029,6 +1051,8 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
     want = fdgpu_ed25519_front_remaining( vt->ctx[c] );
     if( want > lim ) want = lim;
     if( !want ) break;                         /* (a blocking call launched every filling batch above) */
+    ulong b_txns, b_cur; int b_path;              /* the batch these verdicts come from (diagnostics) */
+    fdgpu_ed25519_front_batch( vt->ctx[c], &b_txns, &b_cur, &b_path );
     ulong tw = now_ns();
     ulong k = fdgpu_ed25519_poll_raw( vt->ctx[c], vt->p_tags, vt->p_codes, vt->zc ? NULL : vt->p_img, vt->p_fp, vt->p_dtag,
                                       want, blocking );
@@ -1055,6 +1079,8 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
       /* tags are the pending counter: completions come back in order */
       out[n].result = vt_after( vt, p, (int)vt->p_codes[i], vt->p_img + i*FDGPU_TXN_IMG_STRIDE, vt->p_fp[i],
                                 vt->p_dtag[i], &out[n] );
+      out[n].ctx = (unsigned)c; out[n].batch_txns = (unsigned)b_txns; out[n].batch_pos = (unsigned)( b_cur + i );
+      out[n].path = b_path;
       vt_pop( vt, p ); n++;
     }
     vt->gm.after_ns += now_ns() - tp;
@@ -1157,7 +1183,7 @@ struct fdgpu_link {
   ulong            trace_cap, trace_cnt[ LINK_TILE_MAX ];
   /* fdgpu_link_anomalies: per tile of this process, the first LINK_ANOM_MAX verdicts that are neither
      published nor overrun (parse / verify / dedup / bundle failures), and how many there were */
-  fdgpu_link_trace_t anom[ LINK_TILE_MAX ][ LINK_ANOM_MAX ];
+  fdgpu_link_anomaly_t anom[ LINK_TILE_MAX ][ LINK_ANOM_MAX ];
   ulong            anom_cnt[ LINK_TILE_MAX ];
 };
 
@@ -1595,7 +1621,7 @@ static ulong own_in( ulong a, ulong b, ulong T, ulong idx ) {
 }
 
 ulong
-fdgpu_link_anomalies( fdgpu_link_t const * l, int tile, fdgpu_link_trace_t * out, ulong max ) {
+fdgpu_link_anomalies( fdgpu_link_t const * l, int tile, fdgpu_link_anomaly_t * out, ulong max ) {
   if( tile < 0 || tile >= LINK_TILE_MAX ) return 0UL;
   ulong n = l->anom_cnt[tile] < LINK_ANOM_MAX ? l->anom_cnt[tile] : LINK_ANOM_MAX;
   if( n > max ) n = max;
@@ -1621,10 +1647,11 @@ link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, 
       *sigs += l->psig[ pmask ? ( ( s * Q + (ulong)q ) & pmask ) : ( s * Q + (ulong)q ) % np ];
     if( __builtin_expect( d[i].result != FDGPU_VTILE_PUBLISH && d[i].result != FDGPU_VTILE_OVERRUN, 0 ) ) {
       ulong k = l->anom_cnt[idx]++;
-      if( k < LINK_ANOM_MAX ) {                  /* rec_hash: the frag's payload index (the link's layout) */
-        fdgpu_link_trace_t * e = &l->anom[idx][k];
-        e->seq = s; e->in_idx = d[i].in_idx; e->tag = d[i].tag; e->result = d[i].result;
-        e->rec_sz = (unsigned)d[i].sz; e->rec_hash = ( s * Q + (ulong)q ) % np;
+      if( k < LINK_ANOM_MAX ) {
+        fdgpu_link_anomaly_t * e = &l->anom[idx][k];
+        e->seq = s; e->in_idx = d[i].in_idx; e->tag = d[i].tag; e->result = d[i].result; e->code = d[i].code;
+        e->payload_idx = ( s * Q + (ulong)q ) % np;   /* the link's layout: producer q's frag s */
+        e->ctx = d[i].ctx; e->batch_txns = d[i].batch_txns; e->batch_pos = d[i].batch_pos; e->path = d[i].path;
       }
     }
   }

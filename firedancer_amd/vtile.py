@@ -50,7 +50,8 @@ class FragMeta(ctypes.Structure):
 
 class Done(ctypes.Structure):
     _fields_ = [("seq", ctypes.c_ulong), ("tsorig", ctypes.c_ulong), ("chunk", ctypes.c_ulong), ("sz", ctypes.c_ulong),
-                ("tag", ctypes.c_ulong), ("result", ctypes.c_int), ("in_idx", ctypes.c_ulong)]
+                ("tag", ctypes.c_ulong), ("result", ctypes.c_int), ("code", ctypes.c_int), ("in_idx", ctypes.c_ulong),
+                ("ctx", ctypes.c_uint), ("batch_txns", ctypes.c_uint), ("batch_pos", ctypes.c_uint), ("path", ctypes.c_int)]
 
 
 class GpuMetrics(ctypes.Structure):
@@ -211,6 +212,8 @@ def load():
 
 TRACE_DTYPE = np.dtype([("seq", "<u8"), ("tag", "<u8"), ("rec_hash", "<u8"), ("result", "<i4"), ("rec_sz", "<u4"),
                         ("in_idx", "<u8")])
+ANOM_DTYPE = np.dtype([("seq", "<u8"), ("in_idx", "<u8"), ("payload_idx", "<u8"), ("tag", "<u8"), ("result", "<i4"),
+                       ("code", "<i4"), ("ctx", "<u4"), ("batch_txns", "<u4"), ("batch_pos", "<u4"), ("path", "<i4")])
 
 
 def xxh64(seed: int, data: bytes) -> int:
@@ -479,10 +482,9 @@ class Link:
 
     def anomalies(self, tile: int) -> tuple[int, list[dict]]:
         """fdgpu_link_anomalies: (count, the first few) verdicts of `tile` neither published nor overrun."""
-        out = np.zeros(8, TRACE_DTYPE)
+        out = np.zeros(8, ANOM_DTYPE)
         n = int(self.L.fdgpu_link_anomalies(self.p, tile, out.ctypes.data, 8))
-        return n, [{"seq": int(e["seq"]), "in_idx": int(e["in_idx"]), "result": int(e["result"]),
-                    "payload_idx": int(e["rec_hash"])} for e in out[:min(n, 8)]]
+        return n, [{k: int(e[k]) for k in ANOM_DTYPE.names} for e in out[:min(n, 8)]]
 
     def result(self, timeout_s: float = 120.0) -> dict:
         st = StreamStats()

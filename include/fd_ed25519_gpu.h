@@ -376,6 +376,17 @@ fdgpu_ed25519_poll( fdgpu_ed25519_ctx_t * ctx,
 unsigned long
 fdgpu_ed25519_front_remaining( fdgpu_ed25519_ctx_t const * ctx );
 
+/* Engine path a batch ran (diagnostics): the latency path's lanes per signature in the walk (8, 4, 2, 1),
+   the throughput path's half-size walk, its full-length walk, or a batch with no signatures */
+#define FDGPU_PATH_THROUGHPUT       (0)
+#define FDGPU_PATH_THROUGHPUT_FULL  (-1)
+#define FDGPU_PATH_NONE             (-2)
+/* ctx's oldest launched batch: its transactions, how many a poll has returned, and its FDGPU_PATH_* (or
+   lanes); 0 if none is in flight */
+int
+fdgpu_ed25519_front_batch( fdgpu_ed25519_ctx_t const * ctx, unsigned long * txn_cnt, unsigned long * cursor,
+                           int * path );
+
 /* Pipeline occupancy: transactions in the slot being filled, and
    launched slots not yet fully drained by poll.  Lets a caller launch
    early when the GPU is idle and let batches grow while it is busy. */
@@ -421,7 +432,9 @@ void   fdgpu_host_free ( void * p );
 /* Page-lock an existing host range and map it for the GPU (a tile's in
    dcache: the workspace the producer writes frags into), so that
    fdgpu_ed25519_submit_raw_gather can read records there.  0 on
-   success. */
+   success.  Registrations are counted: the same (p, sz) again takes
+   another reference (-2 for another size at p), and the range stays
+   mapped until as many fdgpu_host_unregister( p ) calls. */
 int    fdgpu_host_register  ( void * p, unsigned long sz );
 void   fdgpu_host_unregister( void * p );
 
@@ -585,6 +598,10 @@ fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long smal
    4 = the prep only.  The throughput path is never affected.  0 or < 0. */
 int
 fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on );
+/* ctx's mode: 0 off (the default), 1..4 as set, -1 off as chosen by fdgpu_debug_opts_t.cu_exclusive (a
+   verify tile then does not apply its own default, fdgpu_vtile_opts_t.cu_exclusive) */
+int
+fdgpu_ed25519_get_cu_exclusive( fdgpu_ed25519_ctx_t const * ctx );
 
 /* Per-kernel timing, in milliseconds: the mean over the batches launched
    since fdgpu_ed25519_set_timing(ctx,1) (at most the last 64) of HIP
@@ -633,7 +650,8 @@ typedef struct fdgpu_debug_opts {
   int           gather_rpb;          /* records per workgroup of the gather kernel: 0 = default (4), 1 = one (A/B) */
   int           gather_cu_spread;    /* the CUs a tile context reserves for its gathers: 0 = the last n (default),
                                         1 = every (CUs/n)-th, 2 = the first n (A/B) */
-  int           cu_exclusive;        /* 1: new contexts start with fdgpu_ed25519_set_cu_exclusive( ctx, 1 ) */
+  int           cu_exclusive;        /* 1..4: new contexts start with fdgpu_ed25519_set_cu_exclusive( ctx, n ); -1: off,
+                                        also in verify tiles (whose default is on); 0: default */
 } fdgpu_debug_opts_t;
 
 void

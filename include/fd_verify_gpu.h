@@ -140,7 +140,14 @@ typedef struct fdgpu_vtile_done {
   unsigned long sz;       /* realized footprint (fd_txn_m_realized_footprint) when published */
   unsigned long tag;      /* HA dedup tag (0 for bundles) */
   int           result;   /* FDGPU_VTILE_* */
+  int           code;     /* the GPU's code for the txn: FD_ED25519_* (0, -1, -2, -3), FDGPU_ERR_PARSE / _OVERRUN;
+                             0 for a GPU fault */
   unsigned long in_idx;   /* the in link, as given to during_frag (the stem's in_idx) */
+  /* diagnostics of the GPU batch that verified the frag (a verdict can be traced to its batch) */
+  unsigned int  ctx;      /* the tile's engine context */
+  unsigned int  batch_txns;   /* transactions in the batch */
+  unsigned int  batch_pos;    /* the frag's position in it */
+  int           path;     /* the batch's engine path: FDGPU_PATH_* */
 } fdgpu_vtile_done_t;
 
 typedef struct fdgpu_vtile fdgpu_vtile_t;
@@ -223,8 +230,10 @@ unsigned char * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt );   /* chunk c is at
    full 64-bit seq on that link; so do these.  fdgpu_vtile_set_in records what the reference tile keeps
    per in link (ctx->in_kind[ in_idx ], ctx->in[ in_idx ].mem / chunk0 / wmark, fd_verify_tile.c:181-
    230): its kind (FDGPU_VTILE_IN_KIND_*; a link never set is QUIC) and its data region -- chunk c of
-   the link is at mem + 64 c (fd_chunk_to_laddr), valid for chunk0 <= c <= wmark.  Call while no frag
-   is pending; 0, or -1 for a bad in_idx / kind. */
+   the link is at mem + 64 c (fd_chunk_to_laddr), valid for chunk0 <= c <= wmark.  A gossip link's region
+   must hold FDGPU_GOSSIP_MSG_MAX readable bytes from every chunk up to wmark (a dcache sized for the
+   2048-byte frames fd_verify_tile.c:89-90 accepts).  Call while no frag is pending; 0, or -1 for a bad
+   in_idx / kind. */
 int             fdgpu_vtile_set_in( fdgpu_vtile_t * vt, unsigned long in_idx, int in_kind, void const * mem,
                                     unsigned long chunk0, unsigned long wmark );
 /* STEM_CALLBACK_DURING_FRAG( ctx, in_idx, seq, sig, chunk, sz, ctl ) (fd_verify_tile.c:65-101), plus the
@@ -239,8 +248,10 @@ int             fdgpu_vtile_during_frag_chunk( fdgpu_vtile_t * vt, unsigned long
    it) and its payload submitted; sz > FDGPU_TPU_RAW_MTU or a payload past the frag or past 1232 bytes is
    -4 (the reference's FD_LOG_ERR).  A gossip link's frag is an fd_gossip_update_message_t whose vote
    transaction becomes a fresh out-dcache record (payload_sz, bundle id 0, payload), copied by the host
-   as the reference does (sz > 2048 or a vote txn_sz past 1232: -4; as the reference, txn_sz bytes are read from vote.txn even past
-   the frame: the 1297-byte FD_GOSSIP_UPDATE_SZ_VOTE frame holds 1225 of them).  Returns 0, or -2 when
+   as the reference does (sz > 2048 or a vote txn_sz past 1232: -4).  Only the frame's sz bytes are read
+   here: a vote whose txn_sz reaches past the frame is -4.  (The reference reads vote.txn_sz bytes even
+   past the frame -- the 1297-byte FD_GOSSIP_UPDATE_SZ_VOTE frame holds 1225 of them -- because its
+   dcache continues there: fdgpu_vtile_during_frag_chunk does the same.)  Returns 0, or -2 when
    the out dcache or the GPU staging is full (call fdgpu_vtile_after_frags and retry), <= -3 on error. */
 int             fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, unsigned long in_idx, void const * frag, unsigned long sz,
                                          unsigned long seq, unsigned long tsorig );
@@ -464,8 +475,15 @@ int             fdgpu_link_set_trace( fdgpu_link_t * link, unsigned long cap );
 unsigned long   fdgpu_link_trace( fdgpu_link_t const * link, int tile, fdgpu_link_trace_t * out, unsigned long max );
 /* Always on, per tile this process runs: the first 8 verdicts that were neither published nor overrun
    (parse / verify / dedup / bundle failures; in the bench's all-valid streams each one is an anomaly),
-   with rec_hash holding the frag's payload index in the link; returns how many such verdicts there were. */
-unsigned long   fdgpu_link_anomalies( fdgpu_link_t const * link, int tile, fdgpu_link_trace_t * out, unsigned long max );
+   each with the frag's payload index in the link and the GPU batch that verified it; returns how many
+   such verdicts there were. */
+typedef struct fdgpu_link_anomaly {
+  unsigned long seq, in_idx, payload_idx, tag;
+  int           result, code;          /* FDGPU_VTILE_*, and the GPU's code (fdgpu_vtile_done_t.code) */
+  unsigned int  ctx, batch_txns, batch_pos;
+  int           path;                  /* FDGPU_PATH_* or latency lanes */
+} fdgpu_link_anomaly_t;
+unsigned long   fdgpu_link_anomalies( fdgpu_link_t const * link, int tile, fdgpu_link_anomaly_t * out, unsigned long max );
 
 /* one process, private link, every tile on `device` (G = 1) */
 int             fdgpu_stream_run( int device, fdgpu_stream_cfg_t const * cfg, unsigned char const * payload,

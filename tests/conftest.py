@@ -48,7 +48,9 @@ def engine_opts(path: str, **kw) -> dict:
     o = dict(small_batch_max=0 if path.startswith("throughput") else 2**63,
              half=0 if path == "throughput_full" else 1,
              dsm_lanes=int(path.rstrip("x")[-1]) if path.startswith("latency") else 0,
-             cu_exclusive=1 if path.endswith("x") else 0)   # "x": workgroups alone on their CUs (set_cu_exclusive)
+             # "x": workgroups alone on their CUs (set_cu_exclusive); the other latency paths explicitly off (-1),
+             # so verify tiles, whose default is on, run them as named too
+             cu_exclusive=1 if path.endswith("x") else (-1 if path.startswith("latency") else 0))
     o.update(kw)
     return o
 

@@ -29,6 +29,7 @@ DTYPES = [  # (C type, header, numpy dtype)
 ]
 if hasattr(vtile, "TRACE_DTYPE"):
     DTYPES.append(("fdgpu_link_trace_t", "fd_verify_gpu.h", vtile.TRACE_DTYPE))
+    DTYPES.append(("fdgpu_link_anomaly_t", "fd_verify_gpu.h", vtile.ANOM_DTYPE))
 
 
 def _c_layout(items):

@@ -77,6 +77,23 @@ def test_compact_line_fits_and_carries_the_contract(tmp_path):
     assert json.load(open(detail)) == full          # the detail file keeps everything
 
 
+def test_stream_ok_and_first_anomaly(tmp_path):
+    """A clean stream sets stream_ok; an anomaly (a verdict neither published nor overrun) clears it and the
+    compact line names the first one: leg, tile, seq, payload, the GPU's code and the batch that produced it."""
+    full = canned_full()
+    rec = json.loads(bench.emit_record(full, None))
+    assert rec["stream_ok"] is True and rec["stream"]["anomalies"] == 0 and rec["stream"]["anomaly_first"] is None
+    first = {"seq": 123457, "in_idx": 0, "payload_idx": 99, "tag": 7, "result": 2, "code": -3, "ctx": 1,
+             "batch_txns": 2049, "batch_pos": 2048, "path": 8, "tile": 0, "rank": 0}
+    full["stream"]["anomalies"] = {"paced@2000000": {"count": 1, "first": [first]}}
+    rec = json.loads(bench.emit_record(full, None))
+    assert rec["stream_ok"] is False and rec["stream"]["anomalies"] == 1
+    a = rec["stream"]["anomaly_first"]
+    assert a["leg"] == "paced@2000000" and a["path"] == "latency8" and a["code"] == -3 and a["batch_pos"] == 2048
+    full["stream"] = {"error": "child failed"}
+    assert json.loads(bench.emit_record(full, None))["stream_ok"] is False
+
+
 def test_oversized_summaries_are_dropped_not_the_headline(tmp_path):
     full = canned_full(n_gpus=8)
     full["stream"] = {"error": "e" * 10000}

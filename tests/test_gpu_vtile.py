@@ -8,6 +8,7 @@ dedup tags, over a stream with valid / invalid signatures, parse
 failures, HA duplicates (incl. tcache eviction) and bundles with failing
 members.  Without the reference build, the sequential model below (which
 tests/test_ref_tile.py pins to it) is the expectation."""
+import ctypes
 import os
 import sys
 import time
@@ -392,30 +393,40 @@ def test_vtile_gossip_vote_past_frame():
     """The gossip tile publishes every vote update as a 1297-byte frame (FD_GOSSIP_UPDATE_SZ_VOTE,
     fd_gossip_private.h:80), which holds 1225 bytes of vote.txn; the reference tile copies vote.txn_sz
     bytes regardless (fd_verify_tile.c:91-95).  A 1232-byte vote transaction in such a frame -- its last
-    7 bytes past the frame, where the update message's vote.txn array continues -- verifies and
-    publishes whole, as in the reference; a txn_sz past the 1232-byte array is corrupt (-4)."""
+    7 bytes past the frame, where the update message's vote.txn array continues in the link's dcache --
+    verifies and publishes whole through the stem's chunk path, as in the reference; a txn_sz past the
+    1232-byte array is corrupt (-4).  Given by pointer (only the frame's bytes known readable), the same
+    frame is refused (-4) without reading past it (a short frame must not be over-read)."""
     from firedancer_amd import synth, vtile
     payload, desc, _, _ = synth.make_batch(4, synth.LARGE_NOOP, seed=9)
     txns = [payload[d["payload_off"]: d["payload_off"] + d["payload_sz"]].tobytes() for d in desc]
     assert all(len(t) == 1232 for t in txns)
     vt = vtile.VTile(device=0, batch_txn=64, tcache_depth=1024)
-    assert vt.set_in(2, vtile.IN_GOSSIP) == 0
-    bufs = []
+    # the gossip link's dcache: one 2048-byte frame slot (32 chunks) per frag, room for an MTU frame past wmark
+    region = np.zeros(8 * 2048 + 2048, np.uint8)
+    assert vt.set_in(2, vtile.IN_GOSSIP, region.ctypes.data, 0, 7 * 32) == 0
     for i, t in enumerate(txns):
         msg = np.frombuffer(vtile.gossip_vote_msg(t), np.uint8)      # 72 + 1232 = 1304 bytes of message
         assert len(msg) == 1304
-        buf = np.zeros(2048, np.uint8)
-        buf[:1304] = msg
-        bufs.append(buf)
-        assert vt.during_frag_at(buf.ctypes.data, vtile.GOSSIP_MSG_SZ, i, in_idx=2) == 0
-    bad = bufs[0].copy()
-    bad[64:72] = np.frombuffer(np.uint64(1233).tobytes(), np.uint8)
-    assert vt.during_frag_at(bad.ctypes.data, vtile.GOSSIP_MSG_SZ, 9, in_idx=2) == -4
+        region[i * 2048: i * 2048 + 1304] = msg
+        assert vt.during_frag_chunk(2, i, vtile.GOSSIP_TAG_VOTE, i * 32, vtile.GOSSIP_MSG_SZ) == 0
+    bad = region[:2048].copy()
+    region[5 * 2048: 6 * 2048] = bad
+    region[5 * 2048 + 64: 5 * 2048 + 72] = np.frombuffer(np.uint64(1233).tobytes(), np.uint8)
+    assert vt.during_frag_chunk(2, 9, vtile.GOSSIP_TAG_VOTE, 5 * 32, vtile.GOSSIP_MSG_SZ) == -4
+    # by pointer: a short frame (the 1297-byte frame alone, nothing readable after it) claiming 1232 bytes
+    short = np.frombuffer(bad[:vtile.GOSSIP_MSG_SZ].tobytes(), np.uint8).copy()
+    assert vt.during_frag_at(short.ctypes.data, vtile.GOSSIP_MSG_SZ, 10, in_idx=2) == -4
+    # ... and a frame that holds its whole vote transaction is taken
+    whole = np.frombuffer(bytes(bad[:1304]), np.uint8).copy()
     got = _drain_all(vt)
     assert [g[1] for g in got] == [vtile.PUBLISH] * 4 and [g[5] for g in got] == [2] * 4
     for (seq, r, chunk, sz, tag, _), t in zip(got, txns):
         rec = vt.record(chunk, sz)
         assert rec[80:80 + 1232] == t and rec[8:10] == (1232).to_bytes(2, "little")
+    assert vt.during_frag_at(whole.ctypes.data, 1304, 11, in_idx=2) == 0
+    got = _drain_all(vt)
+    assert [g[1] for g in got] == [vtile.DEDUP_FAIL]          # (txns[0] again: an HA duplicate)
     vt.close()
 
 
@@ -600,3 +611,46 @@ def test_vtile_in_kinds_vs_reference(oracle, rr_idx, zero_copy):
     vt.close()
     if zero_copy:
         engine.host_unregister(buf)
+
+
+def test_host_register_counts_references():
+    """fdgpu_host_register is counted: the same range registered twice -- two handles on one
+    mcache ring -- stays mapped until both unregister; another size at the same start is refused."""
+    from firedancer_amd import engine
+    L = engine.load_library()
+    buf = np.zeros(3 * 4096, np.uint8)
+    base = buf.ctypes.data
+    off = (-base) % 4096                                   # a whole page-aligned range inside buf
+    p, n = base + off, 2 * 4096
+    assert L.fdgpu_host_register(ctypes.c_void_p(p), ctypes.c_ulong(n)) == 0
+    assert L.fdgpu_host_register(ctypes.c_void_p(p), ctypes.c_ulong(n)) == 0
+    assert L.fdgpu_host_register(ctypes.c_void_p(p), ctypes.c_ulong(4096)) == -2
+    assert L.fdgpu_host_dev_ptr(ctypes.c_void_p(p), n)
+    L.fdgpu_host_unregister(ctypes.c_void_p(p))
+    assert L.fdgpu_host_dev_ptr(ctypes.c_void_p(p), n), "the second reference keeps the range mapped"
+    L.fdgpu_host_unregister(ctypes.c_void_p(p))
+    assert not L.fdgpu_host_dev_ptr(ctypes.c_void_p(p), n)
+
+
+def test_two_handles_on_one_mcache_ring():
+    """Two tiles' handles wrapping one ring (fdgpu_mcache_wrap): each set_in_links maps the ring's pages once
+    more; deleting one handle leaves the other's mapping."""
+    from firedancer_amd import vtile
+    L = vtile.load()
+    depth = 1 << 10
+    ring = np.zeros(depth * 32 + 8192, np.uint8)
+    lines = ring.ctypes.data + ((-ring.ctypes.data) % 4096) + 256     # an fd_mcache's lines: 256 B into a page
+    m1, m2 = L.fdgpu_mcache_wrap(ctypes.c_void_p(lines), depth), L.fdgpu_mcache_wrap(ctypes.c_void_p(lines), depth)
+    assert m1 and m2
+    v1, v2 = vtile.VTile(device=0, batch_txn=64, tcache_depth=1024), vtile.VTile(device=0, batch_txn=64, tcache_depth=1024)
+    try:
+        assert v1.set_in_links([m1]) == 0 and v2.set_in_links([m2]) == 0
+        from firedancer_amd import engine
+        eng = engine.load_library()
+        assert eng.fdgpu_host_dev_ptr(ctypes.c_void_p(lines), depth * 32)
+        L.fdgpu_mcache_delete(m1)
+        assert eng.fdgpu_host_dev_ptr(ctypes.c_void_p(lines), depth * 32), "m2's mapping survives m1's delete"
+        L.fdgpu_mcache_delete(m2)
+        assert not eng.fdgpu_host_dev_ptr(ctypes.c_void_p(lines), depth * 32)
+    finally:
+        v1.close(); v2.close()
