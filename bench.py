@@ -143,6 +143,98 @@ def cpu_sweep_configs0(impl, kind, max_threads, gen_threads, point_s=0.6):
             "points": pts}
 
 
+# ---- host budget of the configs[4] stream at N GPUs -------------------------------------------------------
+# Each GPU's stream child spins one thread per verify tile plus one per producer link (the reference pins
+# every tile to a core of its own, src/app/fdctl/topology.c:167-170 sizes the verify stage by tile count).
+# Every record also crosses host DRAM twice (the GPU's gather reads it, the write-back lands in the out
+# dcache): ~34 GB/s each way per GPU at the measured 25.6M frags/s.
+HOST_GBS_PER_GPU_EACH_WAY = 34.0
+AMD_GPU_CLASSES = ("0x030000", "0x038000", "0x120000")
+
+
+def _cpulist(path: str) -> set[int]:
+    out = set()
+    try:
+        for part in open(path).read().strip().split(","):
+            if part:
+                a, _, b = part.partition("-")
+                out.update(range(int(a), int(b or a) + 1))
+    except (OSError, ValueError):
+        pass
+    return out
+
+
+def host_topology() -> tuple[dict, list]:
+    """({NUMA node: usable physical cores (one hardware thread each, within this process's affinity)},
+    [NUMA node of each AMD GPU in PCI order, or -1]) from sysfs."""
+    aff = os.sched_getaffinity(0)
+    nodes = {}
+    base = "/sys/devices/system/node"
+    names = sorted(n for n in (os.listdir(base) if os.path.isdir(base) else []) if n.startswith("node") and n[4:].isdigit())
+    for n in names:
+        cpus = _cpulist(f"{base}/{n}/cpulist") & aff
+        phys = {c for c in cpus
+                if min(_cpulist(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") & aff or {c}) == c}
+        if phys:
+            nodes[int(n[4:])] = len(phys)
+    if not nodes:
+        nodes = {0: len(aff)}
+    gpus = []
+    pci = "/sys/bus/pci/devices"
+    for d in sorted(os.listdir(pci) if os.path.isdir(pci) else []):
+        try:
+            if open(f"{pci}/{d}/vendor").read().strip() != "0x1002":
+                continue
+            if open(f"{pci}/{d}/class").read().strip() not in AMD_GPU_CLASSES:
+                continue
+            gpus.append(int(open(f"{pci}/{d}/numa_node").read().strip()))
+        except (OSError, ValueError):
+            continue
+    return nodes, gpus
+
+
+def host_plan(args, gpus: int, cores: int | None = None, nodes: dict | None = None,
+              gpu_nodes: list | None = None) -> dict:
+    """The host cores the configs[4] stream children of `gpus` GPUs need -- per GPU, its max-rate tiles or
+    its paced tiles, plus its producers, each a spinning thread on a core of its own -- against what this
+    job may use (affinity, cgroup quota, and per NUMA node: each child pins to its GPU's node first).  Where
+    they do not fit, tiles per GPU are lowered (never below 1) instead of oversubscribing, and the plan says
+    so.  cores / nodes / gpu_nodes override the probes (tests, --plan-cores)."""
+    if cores is None:
+        cores = usable_cores()[0] if not getattr(args, "plan_cores", 0) else int(args.plan_cores)
+    if nodes is None:
+        nodes, probed = host_topology()
+        if getattr(args, "plan_cores", 0):
+            nodes = {0: int(args.plan_cores)}
+        gpu_nodes = probed if gpu_nodes is None else gpu_nodes
+    nodes = {int(k): int(v) for k, v in nodes.items()}
+    node_ids = sorted(nodes)
+    gn = list(gpu_nodes or [])[:gpus]
+    if len(gn) < gpus or any(g not in nodes for g in gn):     # unknown placement: spread the GPUs over the nodes
+        gn = [node_ids[i * len(node_ids) // gpus] for i in range(gpus)]
+    P = args.stream_producers
+    want_t, want_l = args.stream_tiles, args.stream_lat_tiles
+    budget = max(1, cores // gpus)                          # the job's cores, an equal share per GPU
+    per_node = {n: sum(1 for g in gn if g == n) for n in node_ids}
+    node_budget = min(nodes[n] // per_node[n] for n in node_ids if per_node[n])
+    b = min(budget, max(1, node_budget))
+    tiles = min(want_t, max(1, b - P))
+    lat_tiles = min(want_l, max(1, b - P))
+    need = gpus * (max(want_t, want_l) + P)
+    used = gpus * (max(tiles, lat_tiles) + P)
+    capped = tiles < want_t or lat_tiles < want_l
+    plan = {"gpus": gpus, "usable_cores": cores, "cores_per_numa_node": {str(k): v for k, v in nodes.items()},
+            "gpu_numa_nodes": gn, "producers_per_gpu": P,
+            "requested": {"tiles_per_gpu": want_t, "paced_tiles_per_gpu": want_l, "cores": need},
+            "applied": {"tiles_per_gpu": tiles, "paced_tiles_per_gpu": lat_tiles, "cores": used},
+            "capped": capped, "oversubscribed": used > cores or b < 1 + P,
+            "host_dram_gbs_est": round(gpus * 2 * HOST_GBS_PER_GPU_EACH_WAY, 1)}
+    if capped:
+        plan["cap"] = (f"{cores} usable cores ({min(budget, node_budget)} per GPU, {P} producer(s) each): tiles per GPU "
+                       f"{want_t} -> {tiles}, paced {want_l} -> {lat_tiles}")
+    return plan
+
+
 # ---- BASELINE configs[4]: the verify stage as the reference wires it ------------------------------------
 # One producer link (mcache + in dcache) read by T = tiles_per_gpu x G verify tiles; tile i takes
 # seq % T == i (before_frag, fd_verify_tile.c:47-48) and drives GPU i % G from that GPU's process.  With
@@ -170,9 +262,9 @@ def _pow2_clamp(x: float, lo: int, hi: int) -> int:
 def _leg_cfg(args, leg, procs, cal_fps):
     # every tile and producer thread spins on its core: keep them within the host cores this job may
     # use (affinity and cgroup quota), split over the GPUs' processes
-    budget = max(2, usable_cores()[0] // procs)
-    T = min(args.stream_tiles, max(1, budget - args.stream_producers)) * procs
-    Tl = min(args.stream_lat_tiles, max(1, budget - args.stream_producers)) * procs
+    plan = host_plan(args, procs)
+    T = plan["applied"]["tiles_per_gpu"] * procs
+    Tl = plan["applied"]["paced_tiles_per_gpu"] * procs
     # the max-rate legs batch for throughput (a GPU batch under one wave per SIMD costs about one wave's
     # DSM chain, ~1 ms, whatever its size), the paced leg for latency
     paced = leg.startswith("paced@")
@@ -389,7 +481,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
            "--stream-tput-max-uncopied", str(args.stream_tput_max_uncopied),
            "--stream-tput-copy-min", str(args.stream_tput_copy_min),
            "--stream-lat-copy-wait-us", str(args.stream_lat_copy_wait_us),
-           "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist)] + \
+           "--stream-max-uncopied", str(args.stream_max_uncopied), "--stream-pf-dist", str(args.stream_pf_dist),
+           "--plan-cores", str(args.plan_cores)] + \
         (["--stream-prof"] if args.stream_prof else []) + (["--stream-no-huge"] if args.stream_no_huge else []) + \
         (["--stream-gather-rpb", str(args.stream_gather_rpb)] if args.stream_gather_rpb else []) + \
         (["--stream-gather-cu-spread", str(args.stream_gather_cu_spread)] if args.stream_gather_cu_spread else []) + \
@@ -514,6 +607,14 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 # first one with the GPU batch that produced it (leg, tile, ctx, seq, payload, code, path)
                 "anomalies": n_anom, "anomaly_first": first_anom}
             rec["stream_ok"] = bool(st.get("all_published")) and n_anom == 0
+    hp = full.get("host_plan")
+    if hp:      # the configs[4] stream's host budget at this N (cores for its spinning tiles and producers)
+        rec["host_plan"] = {"usable_cores": hp["usable_cores"], "need_cores": hp["requested"]["cores"],
+                            "used_cores": hp["applied"]["cores"], "tiles_per_gpu": hp["applied"]["tiles_per_gpu"],
+                            "paced_tiles_per_gpu": hp["applied"]["paced_tiles_per_gpu"], "capped": hp["capped"],
+                            "oversubscribed": hp["oversubscribed"], "host_dram_gbs_est": hp["host_dram_gbs_est"]}
+        if hp.get("cap"):
+            rec["host_plan"]["cap"] = hp["cap"]
     rec["detail"] = detail_path
     return rec
 
@@ -613,7 +714,8 @@ def dry_run_main(args) -> None:
                 "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": dt_max * 1e3 / args.steps,
                 "results_ok": ok, "roofline": {"bound": "valu", "frac_guide": 0.5, "peak_guide": GUIDE_MAD_PEAK / 1e9},
                 "per_gpu": [{"rank": int(r[0]), "sigs_per_s": nsig * args.steps / r[5], "frac_guide": r[3] / r[4],
-                             "frac": r[3] / r[4]} for r in rows]}
+                             "frac": r[3] / r[4]} for r in rows],
+                "host_plan": host_plan(args, world)}
         print(emit_record(full, args.detail_out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -626,6 +728,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
                     help="where the full record goes (stream legs, latency curve, sweeps); the stdout line is compact")
     ap.add_argument("--dry-run", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--plan-cores", type=int, default=0,
+                    help="(planning) host cores to budget the configs[4] stream children against instead of this "
+                         "job's usable cores (e.g. --gpus 8 --dry-run --plan-cores 16)")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--txns", type=int, default=1 << 20, help="txns per GPU per step (BASELINE configs[1]: 1M)")
@@ -1154,6 +1259,7 @@ def main():
             "latency": lat,
             "host_staged": host_staged,
             "stream": stream,
+            "host_plan": host_plan(args, world) if args.stream_frags != 0 else None,
             "extra_configs": extra,
             "headline_two_contexts": pipelined,
             "gen_s": t_gen,
