@@ -8,7 +8,9 @@ import this module.  It loads
 * ``oracle/_ref/libfdref_{avx512,portable}.so`` -- the reference's own
   verify sources compiled in place by ``oracle/Makefile ref`` (only
   where /root/reference existed at build time; the built .so travels to
-  the GPU box, the sources do not).
+  the GPU box, the sources do not);
+* ``oracle/_ref/libfdref_stem.so`` -- the reference's stem run loop with
+  the GPU tile's callbacks, a test harness.
 """
 from __future__ import annotations
 
@@ -237,6 +239,63 @@ class RefTile:
             raise RuntimeError(f"ref_tile_run_kinds: {rc}")
         recs = {i: rec[i, : int(rec_sz[i])].tobytes() for i in range(n) if res[i] == 0}
         return [int(x) for x in res], [int(x) for x in metrics], recs, [int(x) for x in tag]
+
+
+class _StemCfg(ctypes.Structure):
+    _fields_ = [("payload", ctypes.c_void_p), ("off", ctypes.c_void_p), ("sz", ctypes.c_void_p),
+                ("n_payload", ctypes.c_ulong), ("n_frags", ctypes.c_ulong), ("in_depth", ctypes.c_ulong),
+                ("out_depth", ctypes.c_ulong), ("batch_txn", ctypes.c_ulong), ("tcache_depth", ctypes.c_ulong),
+                ("seed", ctypes.c_ulong), ("rate_fps", ctypes.c_ulong), ("consumer_pause_every", ctypes.c_ulong),
+                ("consumer_pause_ns", ctypes.c_ulong), ("max_inflight", ctypes.c_ulong), ("device", ctypes.c_int),
+                ("nctx", ctypes.c_int), ("zero_copy", ctypes.c_int), ("_pad", ctypes.c_int),
+                ("tr_seq", ctypes.c_void_p), ("tr_res", ctypes.c_void_p), ("tr_tag", ctypes.c_void_p),
+                ("tr_cap", ctypes.c_ulong), ("c_seq_in", ctypes.c_void_p), ("c_hash", ctypes.c_void_p),
+                ("c_sz", ctypes.c_void_p), ("c_cap", ctypes.c_ulong), ("out", ctypes.c_ulong * 16),
+                ("tile_metrics", ctypes.c_ulong * 5)]
+
+
+class RefStem:
+    """INTEGRATION.md section 2's tile patch over the reference's own stem run loop (oracle/_ref/libfdref_stem.so:
+    src/disco/stem/fd_stem.c #included in place with the GPU tile's callbacks, reference tango objects and
+    metrics, a producer thread and a reliable downstream consumer; ref_stem_harness.c).  Needs a GPU."""
+
+    OUT_KEYS = ("verdicts", "consumed", "returned", "stem_overruns", "filtered", "taken", "published", "bursts",
+                "link_consumed", "link_filtered", "link_overrun_polling_frags", "link_overrun_reading_frags",
+                "backpressure_count", "traced", "err")
+
+    def __init__(self):
+        path = os.path.join(HERE, "_ref", "libfdref_stem.so")
+        if not os.path.exists(path):
+            raise FileNotFoundError(path)
+        self.lib = ctypes.CDLL(path)
+        self.lib.ref_stem_run.restype = ctypes.c_int
+        self.lib.ref_stem_run.argtypes = [ctypes.POINTER(_StemCfg)]
+
+    def run(self, payloads, n_frags: int, *, in_depth: int = 1 << 16, out_depth: int = 256, batch_txn: int = 1024,
+            tcache_depth: int = 1 << 16, seed: int = 0x5EED, rate_fps: int = 0, consumer_pause_every: int = 0,
+            consumer_pause_ns: int = 0, max_inflight: int = 1, device: int = 0, nctx: int = 1, zero_copy: bool = False):
+        """The producer publishes frag s = payloads[s % n]; returns (stats dict, the tile's verdicts
+        (seq, result, tag) in order, what the consumer received: (record xxh64, size) per published frag)."""
+        sz = np.array([len(p) for p in payloads], np.uint16)
+        off = np.zeros(len(payloads), np.uint32)
+        off[1:] = np.cumsum(sz[:-1].astype(np.int64))
+        arena = np.frombuffer(b"".join(payloads) + bytes(64), np.uint8).copy()
+        tr_seq = np.zeros(n_frags, np.uint64); tr_res = np.zeros(n_frags, np.int32); tr_tag = np.zeros(n_frags, np.uint64)
+        c_hash = np.zeros(n_frags, np.uint64); c_sz = np.zeros(n_frags, np.uint64); c_seq = np.zeros(n_frags, np.uint64)
+        c = _StemCfg(payload=arena.ctypes.data, off=off.ctypes.data, sz=sz.ctypes.data, n_payload=len(payloads),
+                     n_frags=n_frags, in_depth=in_depth, out_depth=out_depth, batch_txn=batch_txn,
+                     tcache_depth=tcache_depth, seed=seed, rate_fps=rate_fps, consumer_pause_every=consumer_pause_every,
+                     consumer_pause_ns=consumer_pause_ns, max_inflight=max_inflight, device=device, nctx=nctx,
+                     zero_copy=1 if zero_copy else 0, tr_seq=tr_seq.ctypes.data, tr_res=tr_res.ctypes.data,
+                     tr_tag=tr_tag.ctypes.data, tr_cap=n_frags, c_seq_in=c_seq.ctypes.data, c_hash=c_hash.ctypes.data,
+                     c_sz=c_sz.ctypes.data, c_cap=n_frags)
+        rc = self.lib.ref_stem_run(ctypes.byref(c))
+        st = {k: int(c.out[i]) for i, k in enumerate(self.OUT_KEYS)}
+        st["rc"] = rc
+        st["tile_metrics"] = [int(x) for x in c.tile_metrics]
+        n = min(st["traced"], n_frags)
+        m = min(st["consumed"], n_frags) if st["consumed"] < (1 << 63) else 0
+        return st, (tr_seq[:n], tr_res[:n], tr_tag[:n]), (c_hash[:m], c_sz[:m])
 
 
 class RefMcache:
