@@ -2574,6 +2574,10 @@ extern "C" void
 fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   if( !ctx ) return;
   (void)hipSetDevice( ctx->device );
+  /* every stream of the context drains before anything is freed: gathers of a slot that was still filling
+     (early copies, never launched) read its pinned descriptors and write its arena on the gather stream */
+  if( ctx->gstream ) (void)hipStreamSynchronize( ctx->gstream );
+  if( ctx->cstream ) (void)hipStreamSynchronize( ctx->cstream );
   if( ctx->stream ) (void)hipStreamSynchronize( ctx->stream );
   (void)hipFree( ctx->d_map ); (void)hipFree( ctx->d_code ); (void)hipFree( ctx->d_pstat ); (void)hipFree( ctx->d_tab );
   (void)hipFree( ctx->d_Rxy ); (void)hipFree( ctx->d_Axy ); (void)hipFree( ctx->d_digA ); (void)hipFree( ctx->d_digB );
@@ -3316,7 +3320,7 @@ fdgpu_ed25519_submit_raw_ref( fdgpu_ed25519_ctx_t * ctx, unsigned char const * b
    entry's fields and then publish it with a release store of its size; a
    removed entry's size drops to 0 first. */
 #define FD_REGION_MAX 256
-struct fd_region { unsigned char const * h; unsigned char * d; std::atomic<unsigned long> sz; int refs; };
+struct fd_region { unsigned char const * h; unsigned char * d; std::atomic<unsigned long> sz; int refs, shared; };
 static std::mutex g_reg_mu;
 static fd_region g_regions[ FD_REGION_MAX ];
 static std::atomic<int> g_region_cnt{ 0 };
@@ -3325,7 +3329,7 @@ static void region_add_locked( void * h, void * d, unsigned long sz ) {
   int n = g_region_cnt.load( std::memory_order_relaxed ), i = 0;
   while( i < n && g_regions[i].sz.load( std::memory_order_relaxed ) ) i++;     /* reuse a removed entry */
   if( i == FD_REGION_MAX ) return;
-  g_regions[i].h = (unsigned char const *)h; g_regions[i].d = (unsigned char *)d; g_regions[i].refs = 1;
+  g_regions[i].h = (unsigned char const *)h; g_regions[i].d = (unsigned char *)d; g_regions[i].refs = 1; g_regions[i].shared = 0;
   g_regions[i].sz.store( sz, std::memory_order_release );
   if( i == n ) g_region_cnt.store( n + 1, std::memory_order_release );
 }
@@ -3389,26 +3393,43 @@ fdgpu_host_alloc( unsigned long sz ) {
 
 extern "C" void fdgpu_host_free( void * p ) { if( p ) { region_del( p ); hipHostFree( p ); } }
 
-/* Registrations are counted: registering exactly the same range again (two handles on one mcache ring)
-   takes another reference, and the range stays registered until the last fdgpu_host_unregister. */
-extern "C" int
-fdgpu_host_register( void * p, unsigned long sz ) {
-  if( !p || !sz ) { fd_err = "fdgpu_host_register: empty range"; return -1; }
-  std::lock_guard<std::mutex> lk( g_reg_mu );
-  int i = region_find_locked( p );
-  if( i >= 0 ) {
-    if( g_regions[i].sz.load( std::memory_order_relaxed ) != sz ) {
-      fd_err = "fdgpu_host_register: another range starting there is registered"; return -2;
-    }
-    g_regions[i].refs++;
-    return 0;
-  }
+static int host_register_locked( void * p, unsigned long sz, int shared ) {
   HIPCHK( hipHostRegister( p, sz, hipHostRegisterMapped ), -2 );
   void * d = NULL;
   hipError_t e = hipHostGetDevicePointer( &d, p, 0 );
   if( e != hipSuccess ) { set_err( "hipHostGetDevicePointer", e ); (void)hipHostUnregister( p ); return -2; }
   region_add_locked( p, d, sz );
+  int i = region_find_locked( p );
+  if( i >= 0 ) g_regions[i].shared = shared;
   return 0;
+}
+
+extern "C" int
+fdgpu_host_register( void * p, unsigned long sz ) {
+  if( !p || !sz ) { fd_err = "fdgpu_host_register: empty range"; return -1; }
+  std::lock_guard<std::mutex> lk( g_reg_mu );
+  if( region_find_locked( p ) >= 0 ) { fd_err = "fdgpu_host_register: a range starting there is registered"; return -2; }
+  return host_register_locked( p, sz, 0 );
+}
+
+/* Holders that share one range (the verify tiles' handles on one mcache ring, fdgpu_vtile_set_in_links):
+   the first registers it, later ones with exactly the same (p, sz) take a reference, and the range is
+   unmapped at the last fdgpu_host_unregister.  A range an owner registered with fdgpu_host_register is
+   never shared: 1 (nothing taken, the owner keeps it mapped). */
+extern "C" int
+fdgpu_host_register_shared( void * p, unsigned long sz ) {
+  if( !p || !sz ) { fd_err = "fdgpu_host_register_shared: empty range"; return -1; }
+  std::lock_guard<std::mutex> lk( g_reg_mu );
+  int i = region_find_locked( p );
+  if( i >= 0 ) {
+    if( g_regions[i].sz.load( std::memory_order_relaxed ) != sz ) {
+      fd_err = "fdgpu_host_register_shared: another range starting there is registered"; return -2;
+    }
+    if( !g_regions[i].shared ) return 1;
+    g_regions[i].refs++;
+    return 0;
+  }
+  return host_register_locked( p, sz, 1 );
 }
 
 extern "C" void
@@ -3417,7 +3438,7 @@ fdgpu_host_unregister( void * p ) {
   std::lock_guard<std::mutex> lk( g_reg_mu );
   int i = region_find_locked( p );
   if( i < 0 ) return;
-  if( --g_regions[i].refs > 0 ) return;
+  if( g_regions[i].shared && --g_regions[i].refs > 0 ) return;
   g_regions[i].sz.store( 0UL, std::memory_order_release );
   (void)hipHostUnregister( p );
 }

@@ -618,8 +618,9 @@ fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_
     int have = !fdgpu_host_region( (void const *)lo, &b, &rs, &d ) && (ulong)b + rs >= hi;
     if( have && !( (ulong)b == lo && rs == hi - lo ) ) continue;             /* inside a larger registration */
     if( !have && fdgpu_host_dev_ptr( mc->line, mc->depth * sizeof(mc_line_t) ) ) continue;   /* lines covered */
-    if( fdgpu_host_register( (void *)lo, hi - lo ) ) return -2;
-    mc->reg = 1; mc->reg_base = (void *)lo;
+    int rc = fdgpu_host_register_shared( (void *)lo, hi - lo );            /* exactly these pages: shared */
+    if( rc < 0 ) return -2;
+    if( rc == 0 ) { mc->reg = 1; mc->reg_base = (void *)lo; }              /* (1: an owner's registration) */
   }
   vt->zc = 1; vt->n_in = n;
   for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) {
@@ -809,13 +810,19 @@ vt_submit_host_record( fdgpu_vtile_t * vt, uchar * dst, unsigned short payload_s
 static int vt_during_gossip( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong readable, ulong seq,
                              ulong tsorig );
 
-/* during_frag of an fd_txn_m_t record (QUIC, bundle and send in links) */
+/* during_frag of an fd_txn_m_t record (QUIC, bundle and send in links).  readable: bytes readable from frag
+   (its sz for a frag given by pointer; the link's MTU on the chunk path) */
 static int
-vt_during_txnm( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong seq, ulong tsorig ) {
+vt_during_txnm( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong readable, ulong seq, ulong tsorig ) {
   fdgpu_txnm_t const * in = (fdgpu_txnm_t const *)frag;
-  /* fd_verify_tile.c:75-85: the frag fits FD_TPU_RAW_MTU, holds its header + payload and the payload fits
-     the MTU (the reference FD_LOG_ERRs) */
-  if( sz > FDGPU_TPU_RAW_MTU || sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U || FDGPU_TXNM_HDR_SZ + in->payload_sz > sz )
+  /* fd_verify_tile.c:75-85: the frag fits FD_TPU_RAW_MTU and the payload fits the MTU (the reference
+     FD_LOG_ERRs).  The reference does not check the payload against sz: a frag whose header the producer
+     was rewriting while the stem read its line (a lapped consumer) may claim more than sz, and the stem's
+     seq re-check then drops it.  So on the chunk path a payload past sz is taken (its bytes lie in the
+     link's region; the stem's check, or the GPU copy's, marks the frag overrun); by pointer, where only the
+     frag's sz bytes are known readable, it is corrupt. */
+  if( sz > FDGPU_TPU_RAW_MTU || sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U ||
+      FDGPU_TXNM_HDR_SZ + in->payload_sz > readable )
     return -4;
   if( vt->zc && link >= vt->n_in ) return -4;            /* a link the zero-copy intake was not told about */
   int rc = vt_room( vt );
@@ -866,7 +873,7 @@ fdgpu_vtile_during_frag( fdgpu_vtile_t * vt, ulong in_idx, void const * frag, ul
   if( in_idx >= FDGPU_VTILE_IN_MAX ) return -4;
   /* a frag given by pointer: only its sz bytes are known to be readable */
   if( vt->in_kind[ in_idx ] == FDGPU_VTILE_IN_KIND_GOSSIP ) return vt_during_gossip( vt, (int)in_idx, frag, sz, sz, seq, tsorig );
-  return vt_during_txnm( vt, (int)in_idx, frag, sz, seq, tsorig );
+  return vt_during_txnm( vt, (int)in_idx, frag, sz, sz, seq, tsorig );
 }
 
 int
@@ -882,7 +889,7 @@ fdgpu_vtile_during_frag_chunk( fdgpu_vtile_t * vt, ulong in_idx, ulong seq, ulon
      reference reads it (fd_verify_tile.c:91-95) */
   if( vt->in_kind[ in_idx ] == FDGPU_VTILE_IN_KIND_GOSSIP )
     return vt_during_gossip( vt, (int)in_idx, frag, sz, FDGPU_GOSSIP_MSG_MAX, seq, tsorig );
-  return fdgpu_vtile_during_frag( vt, in_idx, frag, sz, seq, tsorig );
+  return vt_during_txnm( vt, (int)in_idx, frag, sz, FDGPU_TPU_RAW_MTU, seq, tsorig );
 }
 
 int

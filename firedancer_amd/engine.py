@@ -47,7 +47,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_poll", "fdgpu_ed25519_submit_raw", "fdgpu_ed25519_poll_raw", "fdgpu_ed25519_submit_raw_ref",
            "fdgpu_host_alloc", "fdgpu_host_free", "fdgpu_host_register", "fdgpu_host_unregister", "fdgpu_device_numa_node",
            "fdgpu_ed25519_submit_raw_gather", "fdgpu_ed25519_submit_raw_gather_chk", "fdgpu_ed25519_gather",
-           "fdgpu_ed25519_gathered", "fdgpu_ed25519_gather_launched", "fdgpu_ed25519_gather_wait", "fdgpu_host_dev_ptr",
+           "fdgpu_ed25519_gathered", "fdgpu_ed25519_gather_launched", "fdgpu_ed25519_gather_wait", "fdgpu_host_dev_ptr", "fdgpu_host_register_shared",
            "fdgpu_ed25519_reserve_gather_cus", "fdgpu_ed25519_reserve_cus", "fdgpu_ed25519_set_cu_exclusive", "fdgpu_ed25519_get_cu_exclusive", "fdgpu_ed25519_gather_stats", "fdgpu_ed25519_phase_stats", "fdgpu_ed25519_prepare", "fdgpu_ed25519_submit_raw_gather_dev", "fdgpu_host_region",
            "fdgpu_ed25519_dropin_init", "fdgpu_debug_set_opts",
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",

@@ -432,11 +432,16 @@ void   fdgpu_host_free ( void * p );
 /* Page-lock an existing host range and map it for the GPU (a tile's in
    dcache: the workspace the producer writes frags into), so that
    fdgpu_ed25519_submit_raw_gather can read records there.  0 on
-   success.  Registrations are counted: the same (p, sz) again takes
-   another reference (-2 for another size at p), and the range stays
-   mapped until as many fdgpu_host_unregister( p ) calls. */
-int    fdgpu_host_register  ( void * p, unsigned long sz );
-void   fdgpu_host_unregister( void * p );
+   success; -2 if a registered range already starts at p.
+   fdgpu_host_register_shared: for holders sharing one range (verify
+   tiles' handles on one mcache ring): the first registers it, each later
+   call with exactly the same (p, sz) takes another reference, and the
+   range stays mapped until as many fdgpu_host_unregister( p ) calls.  1
+   (nothing taken) if that range was registered by fdgpu_host_register
+   (its owner keeps it mapped); -2 for another size at p. */
+int    fdgpu_host_register       ( void * p, unsigned long sz );
+int    fdgpu_host_register_shared( void * p, unsigned long sz );
+void   fdgpu_host_unregister     ( void * p );
 
 /* NUMA node of HIP device `device` (its PCI function's numa_node in
    sysfs), -1 if unknown: where the threads that drive it and their pinned

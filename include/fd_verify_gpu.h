@@ -230,8 +230,9 @@ unsigned char * fdgpu_vtile_out_dcache( fdgpu_vtile_t * vt );   /* chunk c is at
    full 64-bit seq on that link; so do these.  fdgpu_vtile_set_in records what the reference tile keeps
    per in link (ctx->in_kind[ in_idx ], ctx->in[ in_idx ].mem / chunk0 / wmark, fd_verify_tile.c:181-
    230): its kind (FDGPU_VTILE_IN_KIND_*; a link never set is QUIC) and its data region -- chunk c of
-   the link is at mem + 64 c (fd_chunk_to_laddr), valid for chunk0 <= c <= wmark.  A gossip link's region
-   must hold FDGPU_GOSSIP_MSG_MAX readable bytes from every chunk up to wmark (a dcache sized for the
+   the link is at mem + 64 c (fd_chunk_to_laddr), valid for chunk0 <= c <= wmark.  The region must hold
+   an MTU of readable bytes from every chunk up to wmark (as a dcache sized by fd_dcache_req_data_sz
+   does): FDGPU_TPU_RAW_MTU for QUIC / bundle / send links, FDGPU_GOSSIP_MSG_MAX for a gossip link (the
    2048-byte frames fd_verify_tile.c:89-90 accepts).  Call while no frag is pending; 0, or -1 for a bad
    in_idx / kind. */
 int             fdgpu_vtile_set_in( fdgpu_vtile_t * vt, unsigned long in_idx, int in_kind, void const * mem,
@@ -246,7 +247,8 @@ int             fdgpu_vtile_during_frag_chunk( fdgpu_vtile_t * vt, unsigned long
 /* during_frag of the frag at `frag` (sz bytes) from in link in_idx.  QUIC / bundle / send links carry
    fd_txn_m_t records: the record is copied into the out dcache (or, zero-copy intake, the GPU copies
    it) and its payload submitted; sz > FDGPU_TPU_RAW_MTU or a payload past the frag or past 1232 bytes is
-   -4 (the reference's FD_LOG_ERR).  A gossip link's frag is an fd_gossip_update_message_t whose vote
+   -4 (the reference's FD_LOG_ERR; fdgpu_vtile_during_frag_chunk takes a payload past sz, which a lapped
+   read of a header being rewritten can show, and leaves it to the overrun checks, as the reference).  A gossip link's frag is an fd_gossip_update_message_t whose vote
    transaction becomes a fresh out-dcache record (payload_sz, bundle id 0, payload), copied by the host
    as the reference does (sz > 2048 or a vote txn_sz past 1232: -4).  Only the frame's sz bytes are read
    here: a vote whose txn_sz reaches past the frame is -4.  (The reference reads vote.txn_sz bytes even

@@ -613,23 +613,30 @@ def test_vtile_in_kinds_vs_reference(oracle, rr_idx, zero_copy):
         engine.host_unregister(buf)
 
 
-def test_host_register_counts_references():
-    """fdgpu_host_register is counted: the same range registered twice -- two handles on one
-    mcache ring -- stays mapped until both unregister; another size at the same start is refused."""
+def test_host_register_shared_counts_references():
+    """fdgpu_host_register_shared: the same range taken twice -- two handles on one mcache ring --
+    stays mapped until both unregister; another size at the same start is refused; a range an owner registered
+    with fdgpu_host_register is never shared (1: nothing taken) and goes at the owner's one unregister."""
     from firedancer_amd import engine
     L = engine.load_library()
     buf = np.zeros(3 * 4096, np.uint8)
     base = buf.ctypes.data
     off = (-base) % 4096                                   # a whole page-aligned range inside buf
     p, n = base + off, 2 * 4096
-    assert L.fdgpu_host_register(ctypes.c_void_p(p), ctypes.c_ulong(n)) == 0
-    assert L.fdgpu_host_register(ctypes.c_void_p(p), ctypes.c_ulong(n)) == 0
-    assert L.fdgpu_host_register(ctypes.c_void_p(p), ctypes.c_ulong(4096)) == -2
-    assert L.fdgpu_host_dev_ptr(ctypes.c_void_p(p), n)
-    L.fdgpu_host_unregister(ctypes.c_void_p(p))
-    assert L.fdgpu_host_dev_ptr(ctypes.c_void_p(p), n), "the second reference keeps the range mapped"
-    L.fdgpu_host_unregister(ctypes.c_void_p(p))
-    assert not L.fdgpu_host_dev_ptr(ctypes.c_void_p(p), n)
+    vp, ul = ctypes.c_void_p, ctypes.c_ulong
+    assert L.fdgpu_host_register_shared(vp(p), ul(n)) == 0
+    assert L.fdgpu_host_register_shared(vp(p), ul(n)) == 0
+    assert L.fdgpu_host_register_shared(vp(p), ul(4096)) == -2
+    assert L.fdgpu_host_register(vp(p), ul(n)) == -2
+    assert L.fdgpu_host_dev_ptr(vp(p), n)
+    L.fdgpu_host_unregister(vp(p))
+    assert L.fdgpu_host_dev_ptr(vp(p), n), "the second reference keeps the range mapped"
+    L.fdgpu_host_unregister(vp(p))
+    assert not L.fdgpu_host_dev_ptr(vp(p), n)
+    assert L.fdgpu_host_register(vp(p), ul(n)) == 0         # an owner's registration
+    assert L.fdgpu_host_register_shared(vp(p), ul(n)) == 1
+    L.fdgpu_host_unregister(vp(p))
+    assert not L.fdgpu_host_dev_ptr(vp(p), n)
 
 
 def test_two_handles_on_one_mcache_ring():
