@@ -156,7 +156,13 @@ def test_stream_parity_paced_latency_two_contexts(rate):
     assert st["batches"] > 0 and st["batch_txns"] / st["batches"] <= 8192
     seen = list(check_tiles(pays, traces, tiles=1))
     assert sum(k for _, k, _ in seen) == n
-    # the diagnostics every anomaly carries: each names a GPU batch on the latency path
+    # the diagnostics every non-published verdict carries (the payload set holds invalid and unparsable
+    # transactions): the GPU batch it came from and the GPU's own code for it
     cnt, first = anomalies[0]
+    assert cnt > 0
     for a in first:
-        assert a["batch_txns"] > a["batch_pos"] and a["ctx"] < 2 and a["path"] in (8, 4, 2, 1), a
+        assert a["batch_txns"] > a["batch_pos"] and a["ctx"] < 2 and a["path"] in (8, 4, 2, 1, 0, -1), a
+        if a["result"] == 2:                                    # FDGPU_VTILE_VERIFY_FAIL
+            assert a["code"] in (-1, -2, -3), a
+        elif a["result"] == 1:                                  # FDGPU_VTILE_PARSE_FAIL
+            assert a["code"] == -16, a
