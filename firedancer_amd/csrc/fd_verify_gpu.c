@@ -1632,7 +1632,7 @@ fdgpu_link_anomalies( fdgpu_link_t const * l, int tile, fdgpu_link_anomaly_t * o
   if( tile < 0 || tile >= LINK_TILE_MAX ) return 0UL;
   ulong n = l->anom_cnt[tile] < LINK_ANOM_MAX ? l->anom_cnt[tile] : LINK_ANOM_MAX;
   if( n > max ) n = max;
-  memcpy( out, l->anom[tile], n * sizeof(fdgpu_link_trace_t) );
+  memcpy( out, l->anom[tile], n * sizeof(fdgpu_link_anomaly_t) );
   return l->anom_cnt[tile];
 }
 
