@@ -632,6 +632,38 @@ fd_sha_kernel( unsigned char const *    __restrict__ payload,
    longest of them instead of their sum.  Every block has one role, so
    no wave diverges. */
 template<int FM, int HS>
+FD_DEV void prep_role( unsigned char const * __restrict__ payload, fdgpu_txn_desc_t const * __restrict__ desc,
+                       u32 const * __restrict__ map, u32 nsig, u32 role, u32 s, int semantics,
+                       unsigned char * __restrict__ pstat, uint4 * __restrict__ Rxy, uint4 * __restrict__ Axy,
+                       i8 * __restrict__ code_out, i8 * __restrict__ digA, short * __restrict__ digB,
+                       uint4 * __restrict__ tab, uint4 const * __restrict__ khash, uint4 * __restrict__ tabR,
+                       i8 * __restrict__ digR, u32 * __restrict__ slow, u32 * __restrict__ slow_cnt, u32 force_slow,
+                       unsigned char * __restrict__ htop ) {
+  if( role < 2u ) {
+    decode_one<FM>( payload, desc, map, s, role, pstat, Rxy, Axy );
+    /* tab != NULL: the A lane goes on to the -A table (for every A that
+       decoded; fd_dsm2_kernel applies the result-code procedure); HS: the R
+       lane to the -R table */
+    if( tab && role==0u && ( pstat[2u*s] & 3u )==0u ) atab_build<FM>( tab, s, Axy );
+    if( HS && role==1u && ( pstat[2u*s+1u] & 3u )==0u ) atab_build<FM>( tabR, s, Rxy );
+  }
+  else if( HS ) hashh_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digR, digB, slow, slow_cnt,
+                           khash, force_slow, htop );
+  else hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rxy, khash );
+}
+
+/* FD_PREP_PROBE builds (tools/prep_probe.py, A/B only): lane 0 of every wave of fd_prep_kernel records
+   its start and end on the 100 MHz real-time counter and its role, so the length of each role's
+   chain in a latency-path batch is measured (fdgpu_debug_prep_probe) */
+#ifndef FD_PREP_PROBE
+#define FD_PREP_PROBE 0
+#endif
+#if FD_PREP_PROBE
+#define FD_PP_WAVES 4096
+__device__ unsigned long long fd_pp_buf[ FD_PP_WAVES ][ 3 ];
+#endif
+
+template<int FM, int HS>
 __global__ void __launch_bounds__( FD_WG )
 fd_prep_kernel( unsigned char const *    __restrict__ payload,
                 fdgpu_txn_desc_t const * __restrict__ desc,
@@ -655,19 +687,37 @@ fd_prep_kernel( unsigned char const *    __restrict__ payload,
                 unsigned char *          __restrict__ htop ) {
   u32 role = blockIdx.x / sg, b = blockIdx.x - role*sg;
   u32 s = b * FD_WG + threadIdx.x;
-  if( s >= nsig ) return;
-  if( role < 2u ) {
-    decode_one<FM>( payload, desc, map, s, role, pstat, Rxy, Axy );
-    /* tab != NULL: the A lane goes on to the -A table (for every A that
-       decoded; fd_dsm2_kernel applies the result-code procedure); HS: the R
-       lane to the -R table */
-    if( tab && role==0u && ( pstat[2u*s] & 3u )==0u ) atab_build<FM>( tab, s, Axy );
-    if( HS && role==1u && ( pstat[2u*s+1u] & 3u )==0u ) atab_build<FM>( tabR, s, Rxy );
+#if FD_PREP_PROBE
+  unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  if( s < nsig ) prep_role<FM,HS>( payload, desc, map, nsig, role, s, semantics, pstat, Rxy, Axy, code_out, digA, digB,
+                                   tab, khash, tabR, digR, slow, slow_cnt, force_slow, htop );
+  unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  u32 wv = blockIdx.x * ( FD_WG / 64u ) + threadIdx.x / 64u;
+  if( ( threadIdx.x & 63u ) == 0u && wv < FD_PP_WAVES && s < nsig ) {
+    fd_pp_buf[ wv ][0] = t0; fd_pp_buf[ wv ][1] = t1; fd_pp_buf[ wv ][2] = role;
   }
-  else if( HS ) hashh_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digR, digB, slow, slow_cnt,
-                           khash, force_slow, htop );
-  else hash_one( payload, desc, map, s, nsig, semantics, 0, pstat, code_out, digA, digB, Rxy, khash );
+#else
+  if( s >= nsig ) return;
+  prep_role<FM,HS>( payload, desc, map, nsig, role, s, semantics, pstat, Rxy, Axy, code_out, digA, digB,
+                    tab, khash, tabR, digR, slow, slow_cnt, force_slow, htop );
+#endif
 }
+
+#if FD_PREP_PROBE
+/* the probe records of the last fd_prep_kernel launch (its waves in launch order): n of [start, end, role] */
+extern "C" int
+fdgpu_debug_prep_probe( unsigned long long * out, unsigned long n ) {
+  if( n > FD_PP_WAVES ) n = FD_PP_WAVES;
+  if( hipDeviceSynchronize() != hipSuccess ) return -1;
+  return hipMemcpyFromSymbol( out, HIP_SYMBOL( fd_pp_buf ), n * 3 * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost )
+         == hipSuccess ? 0 : -1;
+}
+extern "C" int
+fdgpu_debug_prep_probe_clear( void ) {
+  static unsigned long long z[ FD_PP_WAVES ][ 3 ];
+  return hipMemcpyToSymbol( HIP_SYMBOL( fd_pp_buf ), z, sizeof(z), 0, hipMemcpyHostToDevice ) == hipSuccess ? 0 : -1;
+}
+#endif
 
 /* Stage 3 -- table [0..8](-A) in cached form (fd_ed25519_point_neg + the
    odd-multiple table of fd_curve25519.c:118-131; here all multiples, for a
