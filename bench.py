@@ -214,24 +214,27 @@ def host_plan(args, gpus: int, cores: int | None = None, nodes: dict | None = No
         gn = [node_ids[i * len(node_ids) // gpus] for i in range(gpus)]
     P = args.stream_producers
     want_t, want_l = args.stream_tiles, args.stream_lat_tiles
+    want_lc = 1 if getattr(args, "stream_lat_launcher", 0) else 0   # paced tiles' launch threads: a core each
     budget = max(1, cores // gpus)                          # the job's cores, an equal share per GPU
     per_node = {n: sum(1 for g in gn if g == n) for n in node_ids}
     node_budget = min(nodes[n] // per_node[n] for n in node_ids if per_node[n])
     b = min(budget, max(1, node_budget))
     tiles = min(want_t, max(1, b - P))
-    lat_tiles = min(want_l, max(1, b - P))
-    need = gpus * (max(want_t, want_l) + P)
-    used = gpus * (max(tiles, lat_tiles) + P)
-    capped = tiles < want_t or lat_tiles < want_l
+    lc = want_lc if b - P >= 1 + want_lc else 0               # a launch thread only where a paced tile fits beside it
+    lat_tiles = min(want_l, max(1, (b - P) // (1 + lc)))
+    need = gpus * (max(want_t, want_l * (1 + want_lc)) + P)
+    used = gpus * (max(tiles, lat_tiles * (1 + lc)) + P)
+    capped = tiles < want_t or lat_tiles < want_l or lc < want_lc
     plan = {"gpus": gpus, "usable_cores": cores, "cores_per_numa_node": {str(k): v for k, v in nodes.items()},
             "gpu_numa_nodes": gn, "producers_per_gpu": P,
-            "requested": {"tiles_per_gpu": want_t, "paced_tiles_per_gpu": want_l, "cores": need},
-            "applied": {"tiles_per_gpu": tiles, "paced_tiles_per_gpu": lat_tiles, "cores": used},
+            "requested": {"tiles_per_gpu": want_t, "paced_tiles_per_gpu": want_l, "paced_launchers": want_lc,
+                          "cores": need},
+            "applied": {"tiles_per_gpu": tiles, "paced_tiles_per_gpu": lat_tiles, "paced_launchers": lc, "cores": used},
             "capped": capped, "oversubscribed": used > cores or b < 1 + P,
             "host_dram_gbs_est": round(gpus * 2 * HOST_GBS_PER_GPU_EACH_WAY, 1)}
     if capped:
         plan["cap"] = (f"{cores} usable cores ({min(budget, node_budget)} per GPU, {P} producer(s) each): tiles per GPU "
-                       f"{want_t} -> {tiles}, paced {want_l} -> {lat_tiles}")
+                       f"{want_t} -> {tiles}, paced {want_l} -> {lat_tiles}, paced launch threads {want_lc} -> {lc}")
     return plan
 
 
@@ -265,6 +268,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
     plan = host_plan(args, procs)
     T = plan["applied"]["tiles_per_gpu"] * procs
     Tl = plan["applied"]["paced_tiles_per_gpu"] * procs
+    Lc = plan["applied"]["paced_launchers"]
     # the max-rate legs batch for throughput (a GPU batch under one wave per SIMD costs about one wave's
     # DSM chain, ~1 ms, whatever its size), the paced leg for latency
     paced = leg.startswith("paced@")
@@ -293,7 +297,10 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 copy_min=args.stream_tput_copy_min if tput else 0, prof=1 if args.stream_prof else 0, pf_dist=args.stream_pf_dist,
                 no_huge_pages=1 if args.stream_no_huge else 0,
                 cu_split=(args.stream_lat_cu_split if paced else args.stream_cu_split),
-                cu_exclusive=args.stream_cu_exclusive)
+                cu_exclusive=args.stream_cu_exclusive,
+                # paced legs: each tile's batch launches and copies on a launch thread of its own (the tile's
+                # thread only queues them), when the host plan has the cores
+                launcher=Lc if paced else 0)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -386,7 +393,11 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
                          "tile_share_min": round(st["tile_cpu_share_min"], 4), "tile_nivcsw": st["tile_nivcsw"],
                          "producer_share": round(st["prod_cpu_ns"] / max(st["prod_wall_ns"], 1), 4),
                          "producer_nivcsw": st["prod_nivcsw"],
-                         "tile_cpus": [c for c in st["tile_cpu"][:min(cfg["tiles"], 8)]]}}
+                         "tile_cpus": [c for c in st["tile_cpu"][:min(cfg["tiles"], 8)]]},
+            # the tiles' launch threads (cfg launcher): commands, their ns per frag, deepest queue, full-queue waits
+            "launcher": ({"commands": st["launcher"][0], "busy_ns_per_frag": round(st["launcher"][1] / n, 1),
+                          "depth_max": st["launcher"][2], "full_waits": st["launcher"][3]}
+                         if cfg.get("launcher") else None)}
 
 
 def _anon_huge_mb() -> float | None:
@@ -488,7 +499,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
         (["--stream-gather-cu-spread", str(args.stream_gather_cu_spread)] if args.stream_gather_cu_spread else []) + \
         (["--stream-only-paced"] if args.stream_only_paced else []) + \
         ["--stream-cu-split", str(args.stream_cu_split), "--stream-lat-cu-split", str(args.stream_lat_cu_split),
-         "--stream-cu-exclusive", str(args.stream_cu_exclusive)]
+         "--stream-cu-exclusive", str(args.stream_cu_exclusive), "--stream-lat-launcher", str(args.stream_lat_launcher)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -611,7 +622,8 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
     if hp:      # the configs[4] stream's host budget at this N (cores for its spinning tiles and producers)
         rec["host_plan"] = {"usable_cores": hp["usable_cores"], "need_cores": hp["requested"]["cores"],
                             "used_cores": hp["applied"]["cores"], "tiles_per_gpu": hp["applied"]["tiles_per_gpu"],
-                            "paced_tiles_per_gpu": hp["applied"]["paced_tiles_per_gpu"], "capped": hp["capped"],
+                            "paced_tiles_per_gpu": hp["applied"]["paced_tiles_per_gpu"],
+                            "paced_launchers": hp["applied"]["paced_launchers"], "capped": hp["capped"],
                             "oversubscribed": hp["oversubscribed"], "host_dram_gbs_est": hp["host_dram_gbs_est"]}
         if hp.get("cap"):
             rec["host_plan"]["cap"] = hp["cap"]
@@ -830,6 +842,9 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="every leg: latency-path workgroups alone on their CU (fdgpu_vtile_opts_t.cu_exclusive; "
                          "0 = the tile's default, on; -1 off; A/B: 2 at most two per CU, 3 the walk only, 4 the prep "
                          "only; profiles/r04/p, q)")
+    ap.add_argument("--stream-lat-launcher", type=int, default=0, choices=(0, 1),
+                    help="paced legs: each tile's batch launches and copies on a launch thread of its own, a core "
+                         "each (fdgpu_vtile_opts_t.launcher; the host plan drops it when the cores are short)")
     ap.add_argument("--stream-only-paced", action="store_true",
                     help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",

@@ -46,6 +46,9 @@
 #include <string>
 #include <vector>
 #include <deque>
+#include <thread>
+#include <pthread.h>
+#include <sched.h>
 
 #define FD_WG 256
 #define FD_ATAB_ENTRIES 9          /* [0..8](-A), cached form, 128 B each */
@@ -2227,6 +2230,9 @@ struct fdgpu_ed25519_ctx {
   unsigned long * d_flag;
   unsigned long lat_hist[ FDGPU_LAT_BUCKETS ];    /* launch -> verdicts seen by poll, quarter-octave buckets */
   std::deque<int> inflight;      /* slot order */
+  struct fdgpu_launcher * launcher;               /* NULL: the caller's thread makes the batch's runtime calls;
+                                                     else its launch thread does (fdgpu_ed25519_set_launcher) */
+  char lerr[ 192 ];                               /* the launch thread's error, when it faulted the context */
 };
 
 /* Wait for everything queued on st in a synchronous host call.  A blocking
@@ -2331,6 +2337,21 @@ static int async_busy( fdgpu_ed25519_ctx_t const * ctx ) {
 }
 
 /* flags: 1 = the map is written already (fused into fd_parse_kernel), 2 = no reduce (fd_finish_kernel does it) */
+/* the engine path a batch of nsig signatures takes: latency-path lanes per signature in the walk (8, 4, 2,
+   1) or FDGPU_PATH_THROUGHPUT(_FULL) -- launch_batch's choice, also known before its launch (slot_launch_) */
+static int pick_path( fdgpu_ed25519_ctx_t const * ctx, unsigned long nsig ) {
+  if( !nsig ) return FDGPU_PATH_NONE;
+  if( nsig <= ctx->small_max ) {
+    /* lanes per signature in the DSM: 4 while a quad per signature still fits one wave per
+       SIMD (n <= 16K), 2 while a pair does (n <= 32K), else 1 (configs[0]'s 64K: 0.88 ms
+       against 0.92 on the throughput path and 1.08 with two lanes, tools/configs0_ab.py) */
+    int lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM8_MAX && ctx->half ? 8 : nsig <= FD_DSM4_MAX ? 4 :
+                                                    nsig <= FD_DSM2_MAX ? 2 : 1 );
+    return lanes == 8 && !ctx->half ? 4 : lanes;     /* the term split needs the half-size walk */
+  }
+  return ctx->half ? FDGPU_PATH_THROUGHPUT : FDGPU_PATH_THROUGHPUT_FULL;
+}
+
 static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payload, fdgpu_txn_desc_t const * d_desc,
                          unsigned long txn_cnt, unsigned long sig_cnt, i8 * d_txn_out, i8 * d_sig_out, hipStream_t st,
                          unsigned char const * d_pflag = NULL, int flags = 0 ) {
@@ -2355,12 +2376,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     int half = ctx->half && !small;            /* ... on the throughput path */
     int defer = FD_DEFER_R && !small && !half;
     if( small ) {
-      /* lanes per signature in the DSM: 4 while a quad per signature still fits one wave per
-         SIMD (n <= 16K), 2 while a pair does (n <= 32K), else 1 (configs[0]'s 64K: 0.88 ms
-         against 0.92 on the throughput path and 1.08 with two lanes, tools/configs0_ab.py) */
-      lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM8_MAX && ctx->half ? 8 : nsig <= FD_DSM4_MAX ? 4 :
-                                                  nsig <= FD_DSM2_MAX ? 2 : 1 );
-      if( lanes == 8 && !ctx->half ) lanes = 4;       /* the term split needs the half-size walk */
+      lanes = pick_path( ctx, nsig );
       ctx->last_path = lanes;
       int d2 = lanes > 1;
       if( hs )      /* half-size: the A and R lanes build both tables, the hash lane (c0, c1, s') */
@@ -2480,6 +2496,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
 }
 
 extern "C" void fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx );
+static void launcher_drain( fdgpu_launcher_t * L );
 
 /* Test / A/B options of contexts created from now on (fdgpu_debug_set_opts).
    Process-wide, behind a mutex; the defaults are the product's choices. */
@@ -2624,6 +2641,7 @@ extern "C" void
 fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   if( !ctx ) return;
   (void)hipSetDevice( ctx->device );
+  if( ctx->launcher ) launcher_drain( ctx->launcher );   /* its queued calls are made before the streams drain */
   /* every stream of the context drains before anything is freed: gathers of a slot that was still filling
      (early copies, never launched) read its pinned descriptors and write its arena on the gather stream */
   if( ctx->gstream ) (void)hipStreamSynchronize( ctx->gstream );
@@ -3134,7 +3152,21 @@ static int gather_init( fdgpu_ed25519_ctx_t * ctx ) {
   return 0;
 }
 
-static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
+/* A gather's launch, split in two: gather_prep does the host bookkeeping (counts, timing ring) on the
+   caller's thread, gather_issue the runtime call -- on the caller's thread, or on the context's launch
+   thread (fdgpu_ed25519_set_launcher) with the arguments prep captured */
+struct fd_gargs {
+  struct fd_gather const * g;
+  u32                      n;
+  unsigned char *          d_payload;
+  unsigned char *          wb;       /* the records' write-back base (NULL: none) */
+  unsigned char *          ovr;
+  unsigned long            target;
+  unsigned long *          gt;
+};
+
+/* the gather of slot sl's records not yet gathered: 0 if none, else how many (a filled) or < 0 */
+static long gather_prep( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl, fd_gargs * a ) {
   unsigned long n = sl.txn_cnt - sl.gathered;
   if( !n ) return 0;
   if( gather_init( ctx ) ) return -2;
@@ -3150,14 +3182,145 @@ static int gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
     gt = ctx->d_gtime + 2*i;
     ctx->last_gt = (long)i;
   } else { gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT; ctx->last_gt = -1; }   /* untimed: a scratch entry */
-  unsigned long rpb = ctx->gather_rpb == 1 ? 1UL : 4UL;
-  hipLaunchKernelGGL( ( rpb == 1UL ? fd_gather_kernel<1> : fd_gather_kernel<4> ), dim3( (unsigned)( ( n + rpb - 1UL ) / rpb ) ),
-                      dim3( 64UL * rpb ), 0, ctx->gstream, sl.g_dev + sl.gathered, (u32)n,
-                      sl.d_payload, ctx->gather_nowb == 0 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, sl.d_ovr + sl.gathered, ctx->d_gcnt,
-                      (unsigned long *)( ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT + 1 ), target, gt );
-  HIPCHK( hipGetLastError(), -2 );
+  a->g = sl.g_dev + sl.gathered; a->n = (u32)n; a->d_payload = sl.d_payload;
+  a->wb = ctx->gather_nowb == 0 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL;
+  a->ovr = sl.d_ovr + sl.gathered; a->target = target; a->gt = gt;
   ctx->g_launched = target; sl.gathered = sl.txn_cnt;
-  return (int)n;
+  return (long)n;
+}
+
+static int gather_issue( fdgpu_ed25519_ctx_t * ctx, fd_gargs const * a ) {
+  unsigned long rpb = ctx->gather_rpb == 1 ? 1UL : 4UL;
+  hipLaunchKernelGGL( ( rpb == 1UL ? fd_gather_kernel<1> : fd_gather_kernel<4> ), dim3( (unsigned)( ( a->n + rpb - 1UL ) / rpb ) ),
+                      dim3( 64UL * rpb ), 0, ctx->gstream, a->g, a->n, a->d_payload, a->wb, a->ovr, ctx->d_gcnt,
+                      (unsigned long *)( ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT + 1 ), a->target, a->gt );
+  HIPCHK( hipGetLastError(), -2 );
+  return 0;
+}
+
+/* ---- launch thread --------------------------------------------------------
+   A verify tile's host loop is the paced leg's bound near its knee: at 10M frags/s a 2.8K-frag batch's ~10
+   runtime calls (its last gather, the event hand-off, parse, prep, walk, slow list, finish, done, the
+   completion event) take ~43 us of the tile's thread and each early copy ~10 us (profiles/r04/final5: 15.3
+   and ~20 ns per frag of a 100 ns budget), during which it takes no frag and polls no verdict.  With a
+   launcher the tile only fills the slot and queues one command; a thread of its own, spinning on its own
+   core, makes the calls in queue order (one queue per launcher: a context's commands stay in order).  The
+   slot's host state (token, in-flight list, gather counts) stays with the caller, so polling is unchanged:
+   a batch is complete when fd_done_kernel's token appears.  A failed call faults the context (as a failed
+   batch does) and later commands of a faulted context are dropped. */
+struct fd_lcmd {
+  fdgpu_ed25519_ctx_t * ctx;
+  int                   kind;        /* 0: gather (g), 1: slot launch (slot, token, g if has_g) */
+  int                   slot, has_g;
+  unsigned long         token;
+  fd_gargs              g;
+};
+
+struct fdgpu_launcher {
+  enum { NCMD = 512 };
+  fd_lcmd                    cmd[ NCMD ];
+  alignas(64) std::atomic<unsigned long> tail{ 0 };   /* written by the queueing thread */
+  alignas(64) std::atomic<unsigned long> head{ 0 };   /* written by the launch thread */
+  alignas(64) std::atomic<int>           stop{ 0 };
+  int                        device, cpu;
+  std::thread                th;
+  unsigned long              n_cmd, busy_ns, depth_max;   /* launch thread's */
+  unsigned long              full_waits;                  /* queueing thread's */
+};
+
+static int slot_issue( fdgpu_ed25519_ctx_t * ctx, int i, unsigned long token, fd_gargs const * g );
+
+static void launcher_main( fdgpu_launcher_t * L ) {
+  if( L->cpu >= 0 ) {
+    cpu_set_t set; CPU_ZERO( &set ); CPU_SET( L->cpu, &set );
+    (void)pthread_setaffinity_np( pthread_self(), sizeof(set), &set );
+  }
+  (void)hipSetDevice( L->device );
+  for(;;) {
+    unsigned long h = L->head.load( std::memory_order_relaxed ), t = L->tail.load( std::memory_order_acquire );
+    if( h == t ) {
+      if( L->stop.load( std::memory_order_acquire ) ) break;
+      __builtin_ia32_pause();
+      continue;
+    }
+    if( t - h > L->depth_max ) L->depth_max = t - h;
+    fd_lcmd const & c = L->cmd[ h % fdgpu_launcher::NCMD ];
+    unsigned long t0 = fd_now_ns();
+    if( !__atomic_load_n( &c.ctx->fault, __ATOMIC_ACQUIRE ) ) {
+      int rc = c.kind == 0 ? gather_issue( c.ctx, &c.g ) : slot_issue( c.ctx, c.slot, c.token, c.has_g ? &c.g : NULL );
+      if( rc ) {
+        snprintf( c.ctx->lerr, sizeof(c.ctx->lerr), "launch thread: %s", fd_err.c_str() );
+        __atomic_store_n( &c.ctx->fault, 1, __ATOMIC_RELEASE );
+      }
+    }
+    L->busy_ns += fd_now_ns() - t0; L->n_cmd++;
+    L->head.store( h + 1, std::memory_order_release );
+  }
+}
+
+static void launcher_push( fdgpu_launcher_t * L, fd_lcmd const & c ) {
+  unsigned long t = L->tail.load( std::memory_order_relaxed );
+  if( t - L->head.load( std::memory_order_acquire ) >= fdgpu_launcher::NCMD ) {
+    L->full_waits++;
+    while( t - L->head.load( std::memory_order_acquire ) >= fdgpu_launcher::NCMD ) __builtin_ia32_pause();
+  }
+  L->cmd[ t % fdgpu_launcher::NCMD ] = c;
+  L->tail.store( t + 1, std::memory_order_release );
+}
+
+/* every command queued so far has been issued */
+static void launcher_drain( fdgpu_launcher_t * L ) {
+  unsigned long t = L->tail.load( std::memory_order_relaxed );
+  while( L->head.load( std::memory_order_acquire ) < t ) __builtin_ia32_pause();
+}
+
+extern "C" fdgpu_launcher_t *
+fdgpu_launcher_new( int device, int cpu ) {
+  fdgpu_launcher_t * L = new fdgpu_launcher_t();
+  L->device = device; L->cpu = cpu; L->n_cmd = L->busy_ns = L->depth_max = L->full_waits = 0UL;
+  try { L->th = std::thread( launcher_main, L ); }
+  catch( ... ) { delete L; fd_err = "fdgpu_launcher_new: no thread"; return NULL; }
+  return L;
+}
+
+extern "C" void
+fdgpu_launcher_delete( fdgpu_launcher_t * L ) {
+  if( !L ) return;
+  launcher_drain( L );
+  L->stop.store( 1, std::memory_order_release );
+  L->th.join();
+  delete L;
+}
+
+extern "C" void
+fdgpu_launcher_stats( fdgpu_launcher_t const * L, unsigned long out[ 4 ] ) {
+  out[0] = L->n_cmd; out[1] = L->busy_ns; out[2] = L->depth_max; out[3] = L->full_waits;
+}
+
+extern "C" int
+fdgpu_ed25519_set_launcher( fdgpu_ed25519_ctx_t * ctx, fdgpu_launcher_t * L ) {
+  if( !ctx ) return -1;
+  if( ctx->launcher == L ) return 0;
+  if( async_busy( ctx ) ) { fd_err = "fdgpu_ed25519_set_launcher: async batches pending or in flight"; return -1; }
+  if( L && L->device != ctx->device ) { fd_err = "fdgpu_ed25519_set_launcher: launcher of another device"; return -1; }
+  if( ctx->launcher ) launcher_drain( ctx->launcher );
+  if( L && gather_init( ctx ) ) return -2;     /* the gather stream now: the launch thread only issues */
+  ctx->launcher = L;
+  return 0;
+}
+
+/* the gather of the filling slot's new records, on the caller's thread or queued */
+static long gather_launch( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl ) {
+  fd_lcmd c;
+  long n = gather_prep( ctx, sl, &c.g );
+  if( n <= 0 ) return n;
+  if( ctx->launcher ) {
+    c.ctx = ctx; c.kind = 0; c.slot = -1; c.has_g = 1; c.token = 0UL;
+    launcher_push( ctx->launcher, c );
+    return n;
+  }
+  if( gather_issue( ctx, &c.g ) ) return -2;
+  return n;
 }
 
 static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i );
@@ -3167,24 +3330,21 @@ static int slot_launch( fdgpu_ed25519_ctx_t * ctx, int i ) {
   ctx->launch_ns += fd_now_ns() - t0;
   return rc;
 }
-static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
+
+/* the runtime calls of slot i's batch, in stream order (token: the value fd_done_kernel stores; g: the
+   batch's last gather, if any) */
+static int slot_issue( fdgpu_ed25519_ctx_t * ctx, int i, unsigned long token, fd_gargs const * g ) {
   fd_slot & sl = ctx->slot[i];
   hipStream_t st = ctx->stream;
   if( sl.mode==2 ) {   /* in place: one upload of the caller's region range, no host copy */
     HIPCHK( hipMemcpyAsync( sl.d_payload, sl.ref_base + sl.ref_lo, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
   } else if( sl.mode==3 ) {   /* gathered: the rest of the records, then this stream waits for every gather */
-    int g = gather_launch( ctx, sl );
-    if( g < 0 ) return g;
-    /* the batch's last gather (this one, or the last early copy): phase timing */
-    sl.gt_idx = ctx->last_gt; sl.gt_target = ctx->g_launched;
+    if( g && gather_issue( ctx, g ) ) return -2;
     HIPCHK( hipEventRecord( ctx->gev, ctx->gstream ), -2 );
     HIPCHK( hipStreamWaitEvent( st, ctx->gev, 0 ), -2 );
   } else {
-    memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
     HIPCHK( hipMemcpyAsync( sl.d_payload, sl.h_payload, sl.payload_used + FD_ARENA_SLACK, hipMemcpyHostToDevice, st ), -2 );
   }
-  ctx->h_stamp[ 2*i ] = 0UL; ctx->h_stamp[ 2*i + 1 ] = 0UL;
-  if( sl.mode != 3 ) sl.gt_idx = -1;
   if( sl.mode ) {
     /* raw batches: the parse kernel reads the descriptors from pinned host memory and stamps the start,
        fd_finish_kernel writes every result into pinned host memory -- four kernels fewer on the batch's
@@ -3210,11 +3370,36 @@ static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
     if( rc ) return rc;
     HIPCHK( hipMemcpyAsync( sl.h_txn_out, sl.d_txn_out, sl.txn_cnt, hipMemcpyDeviceToHost, st ), -2 );
   }
-  sl.token++;
-  hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + i, sl.token, ctx->d_stamp + 2*i + 1 );
+  hipLaunchKernelGGL( fd_done_kernel, dim3(1), dim3(1), 0, st, ctx->d_flag + i, token, ctx->d_stamp + 2*i + 1 );
   HIPCHK( hipGetLastError(), -2 );
   HIPCHK( hipEventRecord( sl.done, st ), -2 );
-  sl.state = 1; sl.cursor = 0; sl.path = ctx->last_path;
+  return 0;
+}
+
+static int slot_launch_( fdgpu_ed25519_ctx_t * ctx, int i ) {
+  fd_slot & sl = ctx->slot[i];
+  fd_lcmd c;
+  c.has_g = 0;
+  if( sl.mode==3 ) {            /* the batch's last gather (this one, or the last early copy): phase timing */
+    long n = gather_prep( ctx, sl, &c.g );
+    if( n < 0 ) return (int)n;
+    c.has_g = n > 0;
+    sl.gt_idx = ctx->last_gt; sl.gt_target = ctx->g_launched;
+  } else {
+    sl.gt_idx = -1;
+    if( sl.mode != 2 ) memset( sl.h_payload + sl.payload_used, 0, FD_ARENA_SLACK );
+  }
+  ctx->h_stamp[ 2*i ] = 0UL; ctx->h_stamp[ 2*i + 1 ] = 0UL;
+  unsigned long token = sl.token + 1UL;
+  if( ctx->launcher ) {
+    c.ctx = ctx; c.kind = 1; c.slot = i; c.token = token;
+    launcher_push( ctx->launcher, c );
+  } else {
+    int rc = slot_issue( ctx, i, token, c.has_g ? &c.g : NULL );
+    if( rc ) return rc;
+  }
+  sl.token = token;
+  sl.state = 1; sl.cursor = 0; sl.path = pick_path( ctx, sl.sig_cnt );
   sl.launch_ns = sl.last_query = fd_now_ns();
   ctx->n_batches++; ctx->n_txns += sl.txn_cnt;
   ctx->inflight.push_back( i );
@@ -3600,7 +3785,7 @@ fdgpu_ed25519_gather( fdgpu_ed25519_ctx_t * ctx ) {
   if( sl.state != 0 || sl.mode != 3 || sl.gathered == sl.txn_cnt ) return 0;
   HIPCHK( hipSetDevice( ctx->device ), -2 );
   unsigned long t0 = fd_now_ns();
-  int n = gather_launch( ctx, sl );
+  long n = gather_launch( ctx, sl );
   ctx->launch_ns += fd_now_ns() - t0;
   return n;
 }
@@ -3668,6 +3853,7 @@ fdgpu_ed25519_reserve_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n, unsigned part,
 extern "C" int
 fdgpu_ed25519_gather_wait( fdgpu_ed25519_ctx_t * ctx ) {
   if( !ctx || ctx->fault ) return -3;
+  if( ctx->launcher ) launcher_drain( ctx->launcher );   /* (a queued gather is not on its stream yet) */
   unsigned long t0 = fd_now_ns(), last = t0;
   while( fdgpu_ed25519_gathered( ctx ) != ctx->g_launched ) {
     unsigned long now = fd_now_ns();
@@ -3717,7 +3903,10 @@ fdgpu_ed25519_phase_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long out[ 9
 static unsigned long
 poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out_codes, unsigned char * out_img,
           unsigned short * out_fp, unsigned long * out_dtag, unsigned long max, int blocking ) {
-  if( ctx->fault ) return 0;             /* faulted: nothing more completes (never block on it) */
+  if( ctx->fault ) {                     /* faulted: nothing more completes (never block on it) */
+    if( ctx->lerr[0] ) fd_err = ctx->lerr;
+    return 0;
+  }
   unsigned long n = 0;
   while( n < max && !ctx->inflight.empty() ) {
     int i = ctx->inflight.front();

@@ -355,6 +355,7 @@ typedef struct {
 struct fdgpu_vtile {
   /* (fields below; ctx first so the watchdog can report pipeline state) */
   fdgpu_ed25519_ctx_t * ctx[ VT_NCTX_MAX ];
+  fdgpu_launcher_t *    launcher;        /* opt.launcher: the launch thread of every context (NULL: none) */
   int                   device, semantics;   /* to recreate a faulted context */
   int                   fault_seen[ VT_NCTX_MAX ];
   fdgpu_vtile_opts_t    opt;             /* with the defaults filled in */
@@ -432,6 +433,7 @@ vt_ctx_new( fdgpu_vtile_t const * vt, int k ) {
     /* every staging buffer and the gather stream now: batches then allocate nothing (the tile's sandbox
        allows no allocation it does not need, fd_verify_gpu_tile.seccomppolicy) */
     if( fdgpu_ed25519_prepare( c, 1 ) ) { fdgpu_ed25519_ctx_delete( c ); return NULL; }
+    if( vt->launcher && fdgpu_ed25519_set_launcher( c, vt->launcher ) ) { fdgpu_ed25519_ctx_delete( c ); return NULL; }
   }
   return c;
 }
@@ -463,6 +465,9 @@ fdgpu_vtile_new_opts( int device, ulong batch_txn, ulong tcache_depth, ulong see
   vt->device = device; vt->semantics = semantics; vt->batch = batch_txn; vt->seed = seed;
   vt->gpu_tag = !vt->opt.host_dedup_tag;
   vt->min_batch = vt->opt.min_batch; vt->max_wait_ns = vt->opt.max_wait_ns;
+  if( vt->opt.launcher && !( vt->launcher = fdgpu_launcher_new( device, vt->opt.launcher_core - 1 ) ) ) {
+    free( vt ); return NULL;
+  }
   int ctx_ok = 1;
   for( int k=0; k<vt->nctx; k++ ) if( !( vt->ctx[k] = vt_ctx_new( vt, k ) ) ) ctx_ok = 0;
   vt->tcache = fdgpu_tcache_new( tcache_depth );
@@ -490,6 +495,7 @@ void
 fdgpu_vtile_delete( fdgpu_vtile_t * vt ) {
   if( !vt ) return;
   for( int k=0; k<VT_NCTX_MAX; k++ ) if( vt->ctx[k] ) fdgpu_ed25519_ctx_delete( vt->ctx[k] );
+  fdgpu_launcher_delete( vt->launcher );       /* after its contexts: each drained its commands first */
   fdgpu_tcache_delete( vt->tcache );
   fdgpu_host_free( vt->dcache ); free( vt->pend ); free( vt->p_tags ); free( vt->p_dtag ); free( vt->p_codes ); free( vt->p_img );
   free( vt->p_fp );
@@ -590,6 +596,8 @@ fdgpu_vtile_gpu_metrics( fdgpu_vtile_t * vt, fdgpu_vtile_gpu_metrics_t * out ) {
     out->batches += b; out->batch_txns += t;
     for( int j=0; j<FDGPU_LAT_BUCKETS; j++ ) out->lat_hist[j] += h[j];
   }
+  if( vt->launcher ) fdgpu_launcher_stats( vt->launcher, out->launcher );
+  else memset( out->launcher, 0, sizeof(out->launcher) );
   out->inflight = infl;
   out->pending = vt->pend_tail - vt->pend_head;
   out->overruns = vt->overruns;
@@ -1596,7 +1604,7 @@ static void link_pin( int cpu ) {
     fprintf( stderr, "fdgpu_link: could not pin to CPU %d\n", cpu );
 }
 
-typedef struct { fdgpu_link_t * l; int idx, device, cpu; } link_tile_arg_t;
+typedef struct { fdgpu_link_t * l; int idx, device, cpu, lcpu; } link_tile_arg_t;   /* lcpu: its launch thread's */
 
 /* per-link state of a tile */
 typedef struct {
@@ -1681,6 +1689,7 @@ static void * link_tile( void * _a ) {
   memset( &vo, 0, sizeof(vo) );
   vo.nctx = c->nctx; vo.copy_wait_ns = c->copy_wait_ns; vo.copy_min = c->copy_min; vo.gather_cus = c->gather_cus;
   vo.max_uncopied = c->max_uncopied; vo.cu_split = c->cu_split; vo.cu_exclusive = c->cu_exclusive;
+  vo.launcher = c->launcher; vo.launcher_core = c->launcher && a->lcpu >= 0 ? a->lcpu + 1 : 0;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                              ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
@@ -1871,8 +1880,9 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   int mine[ LINK_TILE_MAX ], myq[ LINK_PROD_MAX ], np = 0;
   int nt = fdgpu_link_tiles_of( c->tiles, c->gpus, proc, mine );   /* tile i drives GPU i % G: this process's tiles */
   if( run_producer ) for( int q=0; q<c->producers; q++ ) if( q % c->gpus == proc ) myq[np++] = q;
-  int cpus[ LINK_TILE_MAX + LINK_PROD_MAX ];
-  int ncpu = link_pick_cpus( device, proc, nt + np, cpus );
+  int cpus[ 2*LINK_TILE_MAX + LINK_PROD_MAX ];
+  int nl = c->launcher ? nt : 0;                 /* the tiles' launch threads: a core each, after the tiles' */
+  int ncpu = link_pick_cpus( device, proc, nt + np + nl, cpus );
   if( getenv( "FDGPU_LINK_VERBOSE" ) ) {
     fprintf( stderr, "fdgpu_link: proc %d device %d numa %d producers %d tiles %d cpus:", proc, device,
              fdgpu_device_numa_node( device ), np, nt );
@@ -1882,6 +1892,7 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   for( int t=0; t<nt; t++ ) {
     args[t].l = l; args[t].idx = mine[t]; args[t].device = device;
     args[t].cpu = np + t < ncpu ? cpus[ np + t ] : -1;
+    args[t].lcpu = nl && np + nt + t < ncpu ? cpus[ np + nt + t ] : -1;
     pthread_create( &th[t], NULL, link_tile, &args[t] );
   }
   for( int i=0; i<np; i++ ) {
@@ -1929,6 +1940,8 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
       else st->phase[k] += r->gm.phase[k];
     }
     st->copy_backlog += r->gm.copy_backlog;
+    st->launcher[0] += r->gm.launcher[0]; st->launcher[1] += r->gm.launcher[1]; st->launcher[3] += r->gm.launcher[3];
+    if( r->gm.launcher[2] > st->launcher[2] ) st->launcher[2] = r->gm.launcher[2];
     st->tile_idle_ns += r->ns_idle;
     st->tile_cpu_ns += r->cpu_ns; st->tile_wall_ns += r->wall_ns; st->tile_nivcsw += r->nivcsw;
     double share = r->wall_ns ? (double)r->cpu_ns / (double)r->wall_ns : 1.;

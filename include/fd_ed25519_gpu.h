@@ -342,6 +342,21 @@ fdgpu_ed25519_batch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * batc
 void
 fdgpu_ed25519_launch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * launch_ns, unsigned long * launches );
 
+/* Launch thread (no reference counterpart: the reference's verify tile makes no runtime calls).  A
+   launcher is a thread, pinned to `cpu` (-1: not pinned), that makes the HIP runtime calls of the
+   async batches and copies of the contexts attached to it, in the order they were queued, so the
+   caller's thread spends a queue push per batch instead of the calls themselves (~40 us per latency-path
+   batch).  Polls are unchanged.  A failed call faults its context.  fdgpu_ed25519_set_launcher (L NULL:
+   detach) needs a context with nothing pending; a context is deleted before its launcher.  Commands are
+   queued by one thread at a time: the contexts of one launcher belong to one caller thread (a verify
+   tile).  Stats: commands issued, ns spent issuing them, the deepest queue seen, pushes that waited for
+   room. */
+typedef struct fdgpu_launcher fdgpu_launcher_t;
+fdgpu_launcher_t * fdgpu_launcher_new( int device, int cpu );
+void               fdgpu_launcher_delete( fdgpu_launcher_t * launcher );
+void               fdgpu_launcher_stats( fdgpu_launcher_t const * launcher, unsigned long out[ 4 ] );
+int                fdgpu_ed25519_set_launcher( fdgpu_ed25519_ctx_t * ctx, fdgpu_launcher_t * launcher );
+
 /* 1 once a batch of ctx has failed on the device (poll then returns 0
    without blocking and every submit returns -3: the in-flight
    transactions are lost; delete and recreate the ctx). */

@@ -178,6 +178,8 @@ typedef struct fdgpu_vtile_gpu_metrics {
                                      start -> end sum / max, ns) */
   unsigned long phase[ 9 ];       /* fdgpu_ed25519_phase_stats summed over the tile's contexts (maxima: max) */
   unsigned long copy_backlog;     /* during_frag calls refused with FDGPU_VTILE_COPY_BACKLOG */
+  unsigned long launcher[ 4 ];    /* the tile's launch thread (opts.launcher), fdgpu_launcher_stats: commands issued,
+                                     ns issuing them, deepest queue, pushes that waited for room (0s without one) */
 } fdgpu_vtile_gpu_metrics_t;
 
 /* device: HIP device; batch_txn: transactions per GPU batch (staging
@@ -216,6 +218,10 @@ typedef struct fdgpu_vtile_opts {
   int           cu_exclusive;    /* each context's latency-path workgroups alone on their CU
                                     (fdgpu_ed25519_set_cu_exclusive): 0 = default (on: paced p99 at 10M frags/s
                                     0.96 vs 1.06 ms, knee 10M vs 7.5M, profiles/r04/q); -1 = off; 1..4 explicit */
+  int           launcher;        /* 1: the tile's contexts make their batch launches and copies on a launch thread
+                                    of the tile's own (fdgpu_launcher_new): the tile's thread only queues them;
+                                    0: on the tile's thread */
+  int           launcher_core;   /* with launcher: 1 + the CPU its thread is pinned to (0: not pinned) */
 } fdgpu_vtile_opts_t;
 
 fdgpu_vtile_t * fdgpu_vtile_new( int device, unsigned long batch_txn, unsigned long tcache_depth, unsigned long seed,
@@ -398,6 +404,8 @@ typedef struct fdgpu_stream_cfg {
   int           no_huge_pages;   /* 1: the link region in 4 KiB pages (A/B); 0: 2 MiB transparent huge pages where the
                                     kernel allows them (madvise), as the reference's workspaces use huge pages (max rate
                                     +4 %, profiles/r04/i) */
+  int           launcher;        /* 1: every tile with a launch thread of its own (fdgpu_vtile_opts_t.launcher),
+                                    pinned to a core of its own next to the tiles' */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
@@ -434,6 +442,8 @@ typedef struct fdgpu_stream_stats {
   double        tile_cpu_share_min;                       /* the lowest tile's cpu_ns / wall_ns */
   long          tile_cpu[ 8 ];                            /* the CPUs tiles 0..7 were pinned to (-1: none) */
   unsigned long prod_cpu_ns, prod_wall_ns, prod_nivcsw;   /* summed over producers */
+  unsigned long launcher[ 4 ];   /* the tiles' launch threads (cfg.launcher): commands and ns issuing them (summed),
+                                    deepest queue (max), pushes that waited for room (summed) */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per

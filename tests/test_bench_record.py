@@ -182,6 +182,21 @@ def test_host_plan_caps_tiles_to_the_cores(cores, gpus, tiles, capped):
     assert plan["host_dram_gbs_est"] == pytest.approx(gpus * 68.0)
 
 
+@pytest.mark.parametrize("cores,gpus,launchers", [(128, 8, 1), (24, 8, 1), (16, 8, 0), (3, 1, 1), (2, 1, 0)])
+def test_host_plan_paced_launch_threads(cores, gpus, launchers):
+    """--stream-lat-launcher: a paced tile's launch thread takes a core of its own; where a GPU's share
+    cannot hold tile + launch thread + producer the plan drops the thread (and says so), never the tile."""
+    args = bench.parse_args(["--stream-lat-launcher", "1"])
+    plan = bench.host_plan(args, gpus, cores=cores, nodes={0: cores}, gpu_nodes=[0] * gpus)
+    assert plan["requested"]["paced_launchers"] == 1 and plan["applied"]["paced_launchers"] == launchers
+    assert plan["applied"]["paced_tiles_per_gpu"] == 1
+    assert plan["applied"]["cores"] == gpus * (max(plan["applied"]["tiles_per_gpu"], 1 + launchers) + 1)
+    assert plan["capped"] is (launchers == 0 or plan["applied"]["tiles_per_gpu"] < 2)
+    args = bench.parse_args(["--stream-lat-launcher", "1", "--plan-cores", str(cores)])
+    assert bench._leg_cfg(args, "paced@5000000.0", gpus, 20e6)["launcher"] == launchers
+    assert bench._leg_cfg(args, "max", gpus, 20e6)["launcher"] == 0
+
+
 def test_host_plan_per_numa_node():
     """Each child pins to its GPU's NUMA node first: 4 GPUs on a 6-core node and 4 on a 64-core node get the
     small node's share (1 tile each) rather than oversubscribing it."""

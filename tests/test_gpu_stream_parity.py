@@ -166,3 +166,28 @@ def test_stream_parity_paced_latency_two_contexts(rate):
             assert a["code"] in (-1, -2, -3), a
         elif a["result"] == 1:                                  # FDGPU_VTILE_PARSE_FAIL
             assert a["code"] == -16, a
+
+
+@pytest.mark.parametrize("rate", [7.5e6])
+def test_stream_parity_paced_launch_thread(rate):
+    """The paced leg with the tile's launch thread (fdgpu_vtile_opts_t.launcher, the bench's
+    --stream-lat-launcher): the tile's thread queues each batch launch and early copy, a thread of its own
+    makes the runtime calls.  Frag for frag the same as the reference tile, nothing lost or overrun."""
+    n = 250_000
+    pays = _with_hs_top(payload_set())
+    st, traces, _ = run_leg(pays, reliable=False, depth=1 << 18, n_frags=n, tiles=1, rate_fps=rate, nctx=2,
+                            max_inflight=1, gather_cus=16, copy_wait_ns=25_000, cu_exclusive=0, launcher=1)
+    assert st["lost"] == 0 and st["overruns"] == 0 and st["verdicts"] == n, (st["lost"], st["overruns"])
+    assert st["launcher"][0] >= st["batches"] > 0 and st["launcher"][1] > 0
+    seen = list(check_tiles(pays, traces, tiles=1))
+    assert sum(k for _, k, _ in seen) == n
+
+
+def test_stream_parity_reliable_launch_thread():
+    """Two reliable max-rate tiles, each with its launch thread: frag for frag the reference tile's."""
+    pays = payload_set()
+    st, traces, _ = run_leg(pays, reliable=True, depth=1 << 16, launcher=1)
+    assert st["verdicts"] == N_FRAGS and st["lost"] == 0 and st["overruns"] == 0
+    assert st["launcher"][0] >= st["batches"] > 0
+    seen = list(check_tiles(pays, traces))
+    assert sum(k for _, k, _ in seen) == N_FRAGS

@@ -180,18 +180,20 @@ def test_vtile_vs_model(oracle, batch, depth, zero_copy, engine_path):
         engine.host_unregister(buf)
 
 
+@pytest.mark.parametrize("launcher", [0, 1])
 @pytest.mark.parametrize("zero_copy", [False, True])
 @pytest.mark.parametrize("nctx", [1, 2, 3])
-def test_vtile_multictx_vs_model(oracle, nctx, zero_copy):
+def test_vtile_multictx_vs_model(oracle, nctx, zero_copy, launcher):
     """Adaptive batching over nctx engine contexts (fdgpu_vtile_opts_t) (housekeep launches batches into the
     contexts in turn, staggered): completions merged back into frag order must give exactly the
-    model's per-frag outcomes, metrics and published records."""
+    model's per-frag outcomes, metrics and published records.  launcher: the contexts' launches and early
+    copies made by the tile's launch thread (fdgpu_vtile_opts_t.launcher), the tile's thread only queueing."""
     pytest.importorskip("xxhash")
     from firedancer_amd import engine, vtile
     frags = make_stream(seed=12)
     seed, depth = 0x5eedbeef, 1 << 12
     want_res, want_m, want_recs, want_tags = expectation(oracle, frags, seed, depth)
-    vt = vtile.VTile(device=0, batch_txn=128, tcache_depth=depth, seed=seed, nctx=nctx)
+    vt = vtile.VTile(device=0, batch_txn=128, tcache_depth=depth, seed=seed, nctx=nctx, launcher=launcher)
     if zero_copy:
         fbs = [vtile.frag_bytes(p, b) for p, b in frags]
         buf, offs = in_dcache(fbs)
@@ -232,6 +234,8 @@ def test_vtile_multictx_vs_model(oracle, nctx, zero_copy):
     assert vt.metrics() == want_m
     assert bad == []
     assert launched > 20
+    lm = vt.gpu_metrics()["launcher"]
+    assert (lm[0] >= launched) if launcher else lm == [0, 0, 0, 0]
     vt.close()
     if zero_copy:
         engine.host_unregister(buf)

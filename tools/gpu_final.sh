@@ -8,7 +8,7 @@ B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --latency-batch 0 --s
 P="timeout -s KILL 120 rocprofv3 --kernel-include-regex fd_ -f csv"
 d="gpurun_out/prof_${tag}"
 bash "$(dirname "$0")/gpu_job.sh" \
-  "tests:1100:python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread" \
+  "tests:1100:python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread" \
   "smoke:300:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
   "bench:480:mkdir -p $d && python bench.py --steps 20 --warmup 5 --detail-out $d/bench_detail.json > gpurun_out/bench_${tag}.json" \
   "stats:180:rocprofv3 --kernel-trace --stats -f csv -d $d/stats -o run -- $B > $d/bench_under_rocprof.json" \

@@ -1,18 +1,37 @@
 #!/bin/bash
 # Round-5 GPU jobs: tools/r05_jobs.sh <job>   (each step under its own time limit via tools/gpu_job.sh)
-#   pp     : prep role lengths of latency-path batches (FD_PREP_PROBE variant, tools/prep_probe.py) + the
-#            chain's kernel trace at 2,800 txns, and the paced two-context stream parity tests
+#   pp     : prep role lengths of latency-path batches (FD_PREP_PROBE variant build/ab/pp.so,
+#            tools/prep_probe.py) at 1,000 / 2,800 / 8,192 txns, the chain's kernel trace at 2,800 txns,
+#            the paced stream parity tests and the launch-thread tests, then an interleaved A/B of the
+#            paced legs' launch thread (--stream-lat-launcher 0 / 1)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
 job="$1"; shift
-d="gpurun_out/r05_$job"; mkdir -p "$d"
+Q="--steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0"
+
+# run_arms <outdir> <common bench args> <name>=<extra args> ... : one gpu_job.sh step per arm
+run_arms() {
+  local out="$1" common="$2"; shift 2
+  mkdir -p "gpurun_out/$out"
+  local steps=() a name extra
+  for a in "$@"; do
+    name="${a%%=*}"; extra="${a#*=}"
+    steps+=( "$name:240:python3 bench.py $common $extra --detail-out gpurun_out/$out/$name.json > gpurun_out/$out/$name.out" )
+  done
+  bash tools/gpu_job.sh "${steps[@]}"
+}
+
 case "$job" in
   pp)
+    d="gpurun_out/r05_pp"; mkdir -p "$d"
     bash tools/gpu_job.sh \
-      "parity:900:python -u -m pytest tests/test_gpu_stream_parity.py -k paced -q --timeout 300 --timeout-method thread" \
-      "pp2800:120:TXNS=2800 python tools/prep_probe.py > $d/pp2800.json" \
-      "pp1000:120:TXNS=1000 python tools/prep_probe.py > $d/pp1000.json" \
-      "pp8192:120:TXNS=8192 python tools/prep_probe.py > $d/pp8192.json" \
-      "trace2800:180:FDGPU_LIB=firedancer_amd/libfdgpu_ed25519.so TXNS=2800 rocprofv3 --kernel-trace --stats -f csv -d $d/trace -o run -- python3 tools/prep_probe.py"
+      "parity:900:python -u -m pytest tests/test_gpu_stream_parity.py tests/test_gpu_vtile.py -k 'paced or launch or multictx' -q -rA --timeout 300 --timeout-method thread" \
+      "pp2800:120:TXNS=2800 FDGPU_LIB=build/ab/pp.so python tools/prep_probe.py > $d/pp2800.json" \
+      "pp1000:120:TXNS=1000 FDGPU_LIB=build/ab/pp.so python tools/prep_probe.py > $d/pp1000.json" \
+      "pp8192:120:TXNS=8192 FDGPU_LIB=build/ab/pp.so python tools/prep_probe.py > $d/pp8192.json" \
+      "trace2800:180:FDGPU_LIB=firedancer_amd/libfdgpu_ed25519.so TXNS=2800 rocprofv3 --kernel-trace --stats -f csv -d $d/trace -o run -- python3 tools/prep_probe.py" &&
+    run_arms r05_lc "$Q --stream-rates 5e6,7.5e6,10e6,12.5e6,15e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
+      "l0a=--stream-lat-launcher 0" "l1a=--stream-lat-launcher 1" "l1b=--stream-lat-launcher 1" "l0b=--stream-lat-launcher 0"
     ;;
-  *) echo "unknown job $job"; exit 2 ;;
+  *) sed -n '2,6p' "$0"; exit 2 ;;
 esac
