@@ -215,26 +215,30 @@ def host_plan(args, gpus: int, cores: int | None = None, nodes: dict | None = No
     P = args.stream_producers
     want_t, want_l = args.stream_tiles, args.stream_lat_tiles
     want_lc = 1 if getattr(args, "stream_lat_launcher", 0) else 0   # paced tiles' launch threads: a core each
+    want_h = int(getattr(args, "stream_copy_threads", 0) or 0)      # max-rate tiles' host copy threads: a core each
     budget = max(1, cores // gpus)                          # the job's cores, an equal share per GPU
     per_node = {n: sum(1 for g in gn if g == n) for n in node_ids}
     node_budget = min(nodes[n] // per_node[n] for n in node_ids if per_node[n])
     b = min(budget, max(1, node_budget))
-    tiles = min(want_t, max(1, b - P))
+    h = want_h if b - P >= 1 + want_h else max(0, b - P - 1)    # copy threads only beside at least one tile
+    tiles = min(want_t, max(1, (b - P) // (1 + h)))
     lc = want_lc if b - P >= 1 + want_lc else 0               # a launch thread only where a paced tile fits beside it
     lat_tiles = min(want_l, max(1, (b - P) // (1 + lc)))
-    need = gpus * (max(want_t, want_l * (1 + want_lc)) + P)
-    used = gpus * (max(tiles, lat_tiles * (1 + lc)) + P)
-    capped = tiles < want_t or lat_tiles < want_l or lc < want_lc
+    need = gpus * (max(want_t * (1 + want_h), want_l * (1 + want_lc)) + P)
+    used = gpus * (max(tiles * (1 + h), lat_tiles * (1 + lc)) + P)
+    capped = tiles < want_t or lat_tiles < want_l or lc < want_lc or h < want_h
     plan = {"gpus": gpus, "usable_cores": cores, "cores_per_numa_node": {str(k): v for k, v in nodes.items()},
             "gpu_numa_nodes": gn, "producers_per_gpu": P,
             "requested": {"tiles_per_gpu": want_t, "paced_tiles_per_gpu": want_l, "paced_launchers": want_lc,
-                          "cores": need},
-            "applied": {"tiles_per_gpu": tiles, "paced_tiles_per_gpu": lat_tiles, "paced_launchers": lc, "cores": used},
+                          "copy_threads_per_tile": want_h, "cores": need},
+            "applied": {"tiles_per_gpu": tiles, "paced_tiles_per_gpu": lat_tiles, "paced_launchers": lc,
+                        "copy_threads_per_tile": h, "cores": used},
             "capped": capped, "oversubscribed": used > cores or b < 1 + P,
             "host_dram_gbs_est": round(gpus * 2 * HOST_GBS_PER_GPU_EACH_WAY, 1)}
     if capped:
         plan["cap"] = (f"{cores} usable cores ({min(budget, node_budget)} per GPU, {P} producer(s) each): tiles per GPU "
-                       f"{want_t} -> {tiles}, paced {want_l} -> {lat_tiles}, paced launch threads {want_lc} -> {lc}")
+                       f"{want_t} -> {tiles}, paced {want_l} -> {lat_tiles}, paced launch threads {want_lc} -> {lc}, "
+                       f"copy threads per tile {want_h} -> {h}")
     return plan
 
 
@@ -269,6 +273,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
     T = plan["applied"]["tiles_per_gpu"] * procs
     Tl = plan["applied"]["paced_tiles_per_gpu"] * procs
     Lc = plan["applied"]["paced_launchers"]
+    H = plan["applied"]["copy_threads_per_tile"]
     # the max-rate legs batch for throughput (a GPU batch under one wave per SIMD costs about one wave's
     # DSM chain, ~1 ms, whatever its size), the paced leg for latency
     paced = leg.startswith("paced@")
@@ -300,7 +305,10 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 cu_exclusive=args.stream_cu_exclusive,
                 # paced legs: each tile's batch launches and copies on a launch thread of its own (the tile's
                 # thread only queues them), when the host plan has the cores
-                launcher=Lc if paced else 0)
+                launcher=Lc if paced else 0,
+                # max-rate and unreliable legs: host threads copy each record into the out dcache (the GPU copy only
+                # reads it), so a record crosses PCIe once (--stream-copy-threads)
+                copy_threads=0 if paced else H)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -377,8 +385,10 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
             "copy_backlog_refusals": st["copy_backlog"],
             # the host link at this leg's rate: each verdict's fd_txn_m_t record (80 + 1232 B) is read over PCIe
             # by the GPU copy and written back into the out dcache (plus its fd_txn_t image)
+            # (with copy threads the record is not written back: only the fd_txn_t image and txn_t_sz go out)
             "pcie": {"record_bytes": 1312, "in_gbs": st["frags_per_s"] * 1312 / 1e9,
-                     "out_gbs_at_least": st["frags_per_s"] * 1312 / 1e9, "peak_gbs_each_way": PCIE_GBS,
+                     "out_gbs_at_least": st["frags_per_s"] * (0 if cfg.get("copy_threads") else 1312) / 1e9,
+                     "peak_gbs_each_way": PCIE_GBS,
                      "frac_each_way": st["frags_per_s"] * 1312 / 1e9 / PCIE_GBS} if cfg.get("zero_copy") else None,
             # --stream-prof: rdtsc sections of the tile loop, ns per own frag (fdgpu_stream_stats_t.prof_ns)
             "tile_prof_ns_per_frag": (dict(zip(("mcache_poll", "during_frag", "prefetch_credit", "drain_after_frags",
@@ -394,6 +404,11 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
                          "producer_share": round(st["prod_cpu_ns"] / max(st["prod_wall_ns"], 1), 4),
                          "producer_nivcsw": st["prod_nivcsw"],
                          "tile_cpus": [c for c in st["tile_cpu"][:min(cfg["tiles"], 8)]]},
+            # the tiles' copy threads (cfg copy_threads): records copied, their ns per frag, overrun after the copy,
+            # ns per frag the tile waited for a copy
+            "host_copy": ({"records": st["host_copy"][0], "copy_ns_per_frag": round(st["host_copy"][1] / n, 1),
+                           "overrun": st["host_copy"][2], "tile_wait_ns_per_frag": round(st["host_copy"][3] / n, 1)}
+                          if cfg.get("copy_threads") else None),
             # the tiles' launch threads (cfg launcher): commands, their ns per frag, deepest queue, full-queue waits
             "launcher": ({"commands": st["launcher"][0], "busy_ns_per_frag": round(st["launcher"][1] / n, 1),
                           "depth_max": st["launcher"][2], "full_waits": st["launcher"][3]}
@@ -499,7 +514,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
         (["--stream-gather-cu-spread", str(args.stream_gather_cu_spread)] if args.stream_gather_cu_spread else []) + \
         (["--stream-only-paced"] if args.stream_only_paced else []) + \
         ["--stream-cu-split", str(args.stream_cu_split), "--stream-lat-cu-split", str(args.stream_lat_cu_split),
-         "--stream-cu-exclusive", str(args.stream_cu_exclusive), "--stream-lat-launcher", str(args.stream_lat_launcher)]
+         "--stream-cu-exclusive", str(args.stream_cu_exclusive), "--stream-lat-launcher", str(args.stream_lat_launcher),
+         "--stream-copy-threads", str(args.stream_copy_threads)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -845,6 +861,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-lat-launcher", type=int, default=0, choices=(0, 1),
                     help="paced legs: each tile's batch launches and copies on a launch thread of its own, a core "
                          "each (fdgpu_vtile_opts_t.launcher; the host plan drops it when the cores are short)")
+    ap.add_argument("--stream-copy-threads", type=int, default=0, choices=range(0, 9),
+                    help="max-rate and unreliable legs: host threads per tile that copy each record into the out dcache "
+                         "while the GPU copy only reads it (fdgpu_vtile_opts_t.copy_threads; a core each in the host plan)")
     ap.add_argument("--stream-only-paced", action="store_true",
                     help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",

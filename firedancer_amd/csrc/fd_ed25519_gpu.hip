@@ -1992,7 +1992,7 @@ __global__ void fd_stamp_kernel( unsigned long * stamp ) {
 struct fd_gather {             /* mode 3: copy sz bytes from src (host, device view) to arena / region offset dst */
   unsigned long src;
   unsigned int  dst;
-  unsigned int  sz;            /* multiple of 16 */
+  unsigned int  sz;            /* multiple of 16; bit 31: no write-back (the caller copies the record itself) */
   unsigned long seq_addr;      /* device view of the frag's in-mcache line seq word, 0 = no overrun check */
   unsigned long seq;           /* the seq that line held when the tile took the frag */
 };
@@ -2037,7 +2037,8 @@ fd_gather_kernel( fd_gather const * __restrict__ g, u32 n, unsigned char * __res
   uint4 const * src = (uint4 const *)r.src;
   uint4 * a = (uint4 *)( arena + r.dst );
   uint4 * o = (uint4 *)( out + r.dst );
-  u32 n16 = r.sz >> 4;
+  if( r.sz >> 31 ) out = NULL;                              /* FDGPU_GATHER_NO_WRITEBACK: the host copies it */
+  u32 n16 = ( r.sz & 0x7fffffffu ) >> 4;
   if( n16 <= 128u ) {          /* every fd_txn_m_t record (<= 80 + 1232 bytes): all loads, the re-check, then stores */
     uint4 v0 = make_uint4( 0u, 0u, 0u, 0u ), v1 = v0;
     if( i < n16 ) v0 = src[i];
@@ -3701,7 +3702,8 @@ fdgpu_device_numa_node( int device ) {
    addresses (a lower one starts a new batch), chunk aligned. */
 static int submit_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char const * dsrc,
                           unsigned char * dst_base, unsigned char * dst, unsigned long csz, unsigned short payload_off,
-                          unsigned short payload_sz, unsigned long tag, unsigned char const * dseq, unsigned long seq );
+                          unsigned short payload_sz, unsigned long tag, unsigned char const * dseq, unsigned long seq,
+                          unsigned flags );
 
 extern "C" int
 fdgpu_ed25519_submit_raw_gather_chk( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char * dst_base,
@@ -3720,7 +3722,7 @@ fdgpu_ed25519_submit_raw_gather_chk( fdgpu_ed25519_ctx_t * ctx, unsigned char co
   if( seq_addr && !( dseq = region_dev( seq_addr, sizeof(unsigned long) ) ) ) {
     fd_err = "fdgpu_ed25519_submit_raw_gather: seq_addr not in a registered region"; return -3;
   }
-  return submit_gather( ctx, src, dsrc, dst_base, dst, csz, payload_off, payload_sz, tag, dseq, seq );
+  return submit_gather( ctx, src, dsrc, dst_base, dst, csz, payload_off, payload_sz, tag, dseq, seq, 0u );
 }
 
 /* the same with the device addresses of src and seq_addr already known to the caller (a tile that
@@ -3737,12 +3739,28 @@ fdgpu_ed25519_submit_raw_gather_dev( fdgpu_ed25519_ctx_t * ctx, unsigned char co
     fd_err = "fdgpu_ed25519_submit_raw_gather: bad record"; return -1;
   }
   return submit_gather( ctx, src, src_dev, dst_base, dst, ( (unsigned long)copy_sz + 15UL ) & ~15UL, payload_off,
-                        payload_sz, tag, (unsigned char const *)seq_dev, seq );
+                        payload_sz, tag, (unsigned char const *)seq_dev, seq, 0u );
+}
+
+extern "C" int
+fdgpu_ed25519_submit_raw_gather_dev_f( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char const * src_dev,
+                                       unsigned char * dst_base, unsigned char * dst, unsigned short copy_sz,
+                                       unsigned short payload_off, unsigned short payload_sz, unsigned long tag,
+                                       unsigned long const * seq_dev, unsigned long seq, unsigned flags ) {
+  if( (unsigned)payload_off + payload_sz > copy_sz || ( (uintptr_t)src & 15 ) || ( (uintptr_t)src_dev & 15 ) ||
+      ( (uintptr_t)( dst - dst_base ) & 15 ) ||
+      ( ctx->rec_fp_off >= 0 && ( payload_off > 255u || (unsigned)ctx->rec_fp_off + 2u > payload_off ) ) ||
+      ( (uintptr_t)seq_dev & 7 ) || ( flags & ~(unsigned)FDGPU_GATHER_NO_WRITEBACK ) ) {
+    fd_err = "fdgpu_ed25519_submit_raw_gather: bad record"; return -1;
+  }
+  return submit_gather( ctx, src, src_dev, dst_base, dst, ( (unsigned long)copy_sz + 15UL ) & ~15UL, payload_off,
+                        payload_sz, tag, (unsigned char const *)seq_dev, seq, flags );
 }
 
 static int submit_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char const * dsrc,
                           unsigned char * dst_base, unsigned char * dst, unsigned long csz, unsigned short payload_off,
-                          unsigned short payload_sz, unsigned long tag, unsigned char const * dseq, unsigned long seq ) {
+                          unsigned short payload_sz, unsigned long tag, unsigned char const * dseq, unsigned long seq,
+                          unsigned flags ) {
   unsigned b0 = payload_sz ? src[ payload_off ] : 0u;
   unsigned lanes = ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u;
   size_t off = (size_t)( dst - dst_base );
@@ -3763,7 +3781,8 @@ static int submit_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, 
   r.payload_sz = payload_sz; r.sig_lanes = (unsigned char)lanes;
   r._pad[0] = (unsigned char)payload_off;      /* fd_img_scatter_kernel finds the record header from it */
   fd_gather & g = sl->h_gat[ sl->txn_cnt ];
-  g.src = (unsigned long)dsrc; g.dst = (unsigned)( off - sl->ref_lo ); g.sz = (unsigned)csz;
+  g.src = (unsigned long)dsrc; g.dst = (unsigned)( off - sl->ref_lo );
+  g.sz = (unsigned)csz | ( ( flags & FDGPU_GATHER_NO_WRITEBACK ) ? 0x80000000u : 0u );
   g.seq_addr = (unsigned long)dseq; g.seq = seq;
   sl->h_tags[ sl->txn_cnt ] = tag;
   sl->txn_cnt++; sl->sig_cnt += lanes;

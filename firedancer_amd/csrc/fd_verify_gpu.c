@@ -341,7 +341,41 @@ typedef struct {
   int   k;                               /* engine context the frag's batch went to */
   int   ovr;                             /* the caller's seq re-check failed after during_frag's host copy */
   int   in_idx;                          /* the in link it came from (the stem's in_idx) */
+  ulong cp;                              /* host copy threads: 1 + the frag's copy task (0: none) */
 } vt_pend_t;
+
+/* Host copy threads (fdgpu_vtile_opts_t.copy_threads).  With zero-copy intake the GPU copy reads each
+   record over PCIe for the verify kernels and, by default, writes it back into the out dcache: every
+   record crosses the link twice, and the device-to-host direction (the write-back's 64-B writes plus
+   the reads' requests) is what bounds the max-rate stream.  With copy threads the
+   GPU only reads (FDGPU_GATHER_NO_WRITEBACK) and the tile's own threads copy the record in -> out
+   dcache, as the reference's during_frag does with fd_memcpy (fd_verify_tile.c:96-101) -- off the
+   tile's loop.  Each copy is the stem's "copy, then re-check the line" (fd_stem.c:667-686): a thread
+   copies bytes [0, 10) and [12, sz) of the record (the GPU writes txn_t_sz, bytes 10-11, and the
+   fd_txn_t image behind the payload), then re-reads the frag's mcache line; a changed seq marks the
+   frag overrun (never published, as a frag the GPU found overrun).  Tasks go round robin to the
+   threads, each an SPSC ring with a completion counter; after_frag waits for the frag's copy (it has
+   long finished: the copy takes ~100 ns, the GPU batch ~1 ms) and a reliable link's credit stops at
+   the first frag whose copy (GPU or host) is not known complete. */
+typedef struct {
+  uchar const *  src;
+  uchar *        dst;
+  ulong          sz;
+  ulong const *  line_seq;               /* the frag's in-mcache line seq word (NULL: no check) */
+  ulong          seq;
+  int *          ovr;                    /* the frag's pending entry: set to 1 if the line changed */
+} vt_cp_task_t;
+
+typedef struct {
+  vt_cp_task_t *   ring;
+  ulong            mask;
+  _Atomic ulong    tail __attribute__(( aligned( 64 ) ));   /* tasks pushed (the tile) */
+  _Atomic ulong    done __attribute__(( aligned( 64 ) ));   /* tasks completed (the copy thread) */
+  _Atomic int      stop;
+  ulong            busy_ns, ovr_cnt;     /* the copy thread's */
+  int              cpu;
+  pthread_t        th;
+} vt_cp_t;
 
 /* Engine contexts per tile (fdgpu_vtile_opts_t.nctx, 1..VT_NCTX_MAX, default 2).
    A context runs its batches in order on one HIP stream, so with one
@@ -356,6 +390,9 @@ struct fdgpu_vtile {
   /* (fields below; ctx first so the watchdog can report pipeline state) */
   fdgpu_ed25519_ctx_t * ctx[ VT_NCTX_MAX ];
   fdgpu_launcher_t *    launcher;        /* opt.launcher: the launch thread of every context (NULL: none) */
+  vt_cp_t *             cp[ FDGPU_VTILE_COPY_THREADS_MAX ];   /* opt.copy_threads: the host copy threads */
+  int                   ncp;
+  ulong                 cp_cnt, cp_wait_ns;                   /* copy tasks pushed; time after_frags waited on one */
   int                   device, semantics;   /* to recreate a faulted context */
   int                   fault_seen[ VT_NCTX_MAX ];
   fdgpu_vtile_opts_t    opt;             /* with the defaults filled in */
@@ -405,6 +442,69 @@ struct fdgpu_vtile {
   uchar *               p_img;
   unsigned short *      p_fp;
 };
+
+static void * vt_cp_main( void * arg ) {
+  vt_cp_t * c = (vt_cp_t *)arg;
+  if( c->cpu >= 0 ) {
+    cpu_set_t set; CPU_ZERO( &set ); CPU_SET( c->cpu, &set );
+    (void)pthread_setaffinity_np( pthread_self(), sizeof(set), &set );
+  }
+  ulong j = atomic_load_explicit( &c->done, memory_order_relaxed );
+  for(;;) {
+    ulong t = atomic_load_explicit( &c->tail, memory_order_acquire );
+    if( j == t ) {
+      if( atomic_load_explicit( &c->stop, memory_order_acquire ) ) break;
+      _mm_pause();
+      continue;
+    }
+    ulong t0 = now_ns();
+    for( ; j < t; j++ ) {
+      vt_cp_task_t const * k = &c->ring[ j & c->mask ];
+      memcpy( k->dst, k->src, 10UL );                            /* around txn_t_sz (the GPU's) */
+      memcpy( k->dst + 12UL, k->src + 12UL, k->sz - 12UL );
+      if( k->line_seq ) {                                        /* the stem's re-check after its copy */
+        atomic_thread_fence( memory_order_acquire );
+        if( atomic_load_explicit( (_Atomic ulong const *)k->line_seq, memory_order_relaxed ) != k->seq ) {
+          *k->ovr = 1; c->ovr_cnt++;
+        }
+      }
+      atomic_store_explicit( &c->done, j + 1UL, memory_order_release );
+    }
+    c->busy_ns += now_ns() - t0;
+  }
+  return NULL;
+}
+
+static void vt_cp_delete( vt_cp_t * c ) {
+  if( !c ) return;
+  atomic_store_explicit( &c->stop, 1, memory_order_release );
+  pthread_join( c->th, NULL );
+  free( c->ring ); free( c );
+}
+
+static vt_cp_t * vt_cp_new( ulong cap, int cpu ) {
+  vt_cp_t * c = (vt_cp_t *)calloc( 1, sizeof(vt_cp_t) );
+  if( !c ) return NULL;
+  c->mask = pow2_up( cap ) - 1UL; c->cpu = cpu;
+  c->ring = (vt_cp_task_t *)calloc( c->mask + 1UL, sizeof(vt_cp_task_t) );
+  if( !c->ring || pthread_create( &c->th, NULL, vt_cp_main, c ) ) { free( c->ring ); free( c ); return NULL; }
+  return c;
+}
+
+/* copy task k (1-based, vt_pend_t.cp) has completed */
+static inline int vt_cp_done( fdgpu_vtile_t const * vt, ulong k ) {
+  ulong i = k - 1UL;
+  vt_cp_t * c = vt->cp[ i % (ulong)vt->ncp ];
+  return atomic_load_explicit( &c->done, memory_order_acquire ) > i / (ulong)vt->ncp;
+}
+
+/* wait for frag p's host copy, if it has one (copy threads; in practice long done) */
+static inline void vt_cp_wait( fdgpu_vtile_t * vt, vt_pend_t const * p ) {
+  if( !p->cp || vt_cp_done( vt, p->cp ) ) return;
+  ulong tw = now_ns();
+  while( !vt_cp_done( vt, p->cp ) ) _mm_pause();
+  vt->cp_wait_ns += now_ns() - tw;
+}
 
 /* one engine context of the tile.  Adaptive batching launches a partial
    batch when the GPU has room (low load: the latency path) and a full one
@@ -484,7 +584,15 @@ fdgpu_vtile_new_opts( int device, ulong batch_txn, ulong tcache_depth, ulong see
   vt->p_codes = (signed char *)malloc( batch_txn );
   vt->p_img = (uchar *)malloc( batch_txn * FDGPU_TXN_IMG_STRIDE );
   vt->p_fp = (unsigned short *)malloc( batch_txn * sizeof(unsigned short) );
-  if( !ctx_ok || !vt->tcache || !vt->dcache || !vt->pend || !vt->p_tags || !vt->p_dtag || !vt->p_codes || !vt->p_img || !vt->p_fp ) {
+  int cp_ok = 1;
+  if( vt->opt.copy_threads > FDGPU_VTILE_COPY_THREADS_MAX ) vt->opt.copy_threads = FDGPU_VTILE_COPY_THREADS_MAX;
+  if( vt->opt.copy_threads < 0 ) vt->opt.copy_threads = 0;
+  /* a thread's ring holds every task of the pending frags it may have (round robin: pend_cap / n + 1) */
+  for( int i=0; i<vt->opt.copy_threads && vt->pend && cp_ok; i++ ) {
+    if( !( vt->cp[i] = vt_cp_new( vt->pend_cap / (ulong)vt->opt.copy_threads + 2UL, vt->opt.copy_cores[i] - 1 ) ) ) cp_ok = 0;
+    else vt->ncp = i + 1;
+  }
+  if( !ctx_ok || !cp_ok || !vt->tcache || !vt->dcache || !vt->pend || !vt->p_tags || !vt->p_dtag || !vt->p_codes || !vt->p_img || !vt->p_fp ) {
     fdgpu_vtile_delete( vt );
     return NULL;
   }
@@ -496,6 +604,7 @@ fdgpu_vtile_delete( fdgpu_vtile_t * vt ) {
   if( !vt ) return;
   for( int k=0; k<VT_NCTX_MAX; k++ ) if( vt->ctx[k] ) fdgpu_ed25519_ctx_delete( vt->ctx[k] );
   fdgpu_launcher_delete( vt->launcher );       /* after its contexts: each drained its commands first */
+  for( int i=0; i<vt->ncp; i++ ) vt_cp_delete( vt->cp[i] );   /* (a thread finishes its queued copies first) */
   fdgpu_tcache_delete( vt->tcache );
   fdgpu_host_free( vt->dcache ); free( vt->pend ); free( vt->p_tags ); free( vt->p_dtag ); free( vt->p_codes ); free( vt->p_img );
   free( vt->p_fp );
@@ -598,6 +707,12 @@ fdgpu_vtile_gpu_metrics( fdgpu_vtile_t * vt, fdgpu_vtile_gpu_metrics_t * out ) {
   }
   if( vt->launcher ) fdgpu_launcher_stats( vt->launcher, out->launcher );
   else memset( out->launcher, 0, sizeof(out->launcher) );
+  memset( out->host_copy, 0, sizeof(out->host_copy) );
+  for( int i=0; i<vt->ncp; i++ ) {
+    out->host_copy[0] += atomic_load_explicit( &vt->cp[i]->done, memory_order_acquire );
+    out->host_copy[1] += vt->cp[i]->busy_ns; out->host_copy[2] += vt->cp[i]->ovr_cnt;
+  }
+  out->host_copy[3] = vt->cp_wait_ns;
   out->inflight = infl;
   out->pending = vt->pend_tail - vt->pend_head;
   out->overruns = vt->overruns;
@@ -675,6 +790,7 @@ static void vt_copy_poll( fdgpu_vtile_t * vt ) {
   while( vt->copy_cursor < vt->pend_tail ) {
     vt_pend_t const * p = &vt->pend[ vt->copy_cursor % vt->pend_cap ];
     if( p->cidx >= g[ p->k ] ) break;
+    if( p->cp && !vt_cp_done( vt, p->cp ) ) break;            /* its host copy (copy threads) not done yet */
     vt_copied( vt, p );
     vt->copy_cursor++;
   }
@@ -788,7 +904,7 @@ vt_room( fdgpu_vtile_t * vt ) {
 static void
 vt_taken( fdgpu_vtile_t * vt, int in_idx, ulong seq, ulong tsorig, ulong bundle_id, unsigned short payload_sz ) {
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
-  p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill; p->ovr = 0; p->in_idx = in_idx;
+  p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill; p->ovr = 0; p->in_idx = in_idx; p->cp = 0UL;
   if( vt->zc ) {
     p->cidx = vt->sub_cnt[ vt->fill ]++;
     vt->uncopied[ in_idx ]++; vt->uncopied_tot++;
@@ -863,10 +979,24 @@ vt_during_txnm( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong
       vt->src_lo = (uchar const *)b; vt->src_hi = (uchar const *)b + rs; vt->src_dev = (uchar const *)d;
       if( src + csz > vt->src_hi ) return -3;
     }
-    rc = fdgpu_ed25519_submit_raw_gather_dev( vt->ctx[ vt->fill ], src, vt->src_dev + ( src - vt->src_lo ), vt->dcache, dst,
-                                              (unsigned short)( FDGPU_TXNM_HDR_SZ + in->payload_sz ),
-                                              (unsigned short)FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail,
-                                              seq_dev, seq );
+    rc = fdgpu_ed25519_submit_raw_gather_dev_f( vt->ctx[ vt->fill ], src, vt->src_dev + ( src - vt->src_lo ), vt->dcache, dst,
+                                                (unsigned short)( FDGPU_TXNM_HDR_SZ + in->payload_sz ),
+                                                (unsigned short)FDGPU_TXNM_HDR_SZ, in->payload_sz, vt->pend_tail,
+                                                seq_dev, seq, vt->ncp ? FDGPU_GATHER_NO_WRITEBACK : 0U );
+    if( rc ) return rc;
+    vt_taken( vt, link, seq, tsorig, in->bundle_id, in->payload_sz );
+    if( vt->ncp ) {            /* the record's copy into the out dcache: one of the tile's copy threads */
+      vt_pend_t * p = &vt->pend[ ( vt->pend_tail - 1UL ) % vt->pend_cap ];
+      ulong i = vt->cp_cnt++;
+      vt_cp_t * cq = vt->cp[ i % (ulong)vt->ncp ];
+      ulong t = atomic_load_explicit( &cq->tail, memory_order_relaxed );
+      vt_cp_task_t * k = &cq->ring[ t & cq->mask ];
+      k->src = src; k->dst = dst; k->sz = FDGPU_TXNM_HDR_SZ + in->payload_sz;
+      k->line_seq = mc ? (ulong const *)&mc->line[ seq & ( mc->depth - 1UL ) ].seq : NULL; k->seq = seq; k->ovr = &p->ovr;
+      atomic_store_explicit( &cq->tail, t + 1UL, memory_order_release );
+      p->cp = i + 1UL;
+    }
+    return 0;
   } else {
     vt_copy( dst, (uchar const *)frag, FDGPU_TXNM_HDR_SZ + in->payload_sz );
     rc = vt_submit_host_record( vt, dst, in->payload_sz, seq );
@@ -1051,6 +1181,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
       if( !vt->fault_seen[c] ) { vt->fault_seen[c] = 1; vt->gm.faults++; }
       for( ulong i=0; i<want; i++ ) {
         vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
+        vt_cp_wait( vt, p );                   /* (its copy thread writes the entry's ovr: not reused before) */
         fdgpu_vtile_done_t * d = &out[n];
         d->seq = p->seq; d->in_idx = (ulong)p->in_idx; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
         d->result = FDGPU_VTILE_GPU_FAULT; d->code = 0;
@@ -1091,6 +1222,7 @@ fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max
         __builtin_prefetch( r, 1 );
       }
       vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
+      vt_cp_wait( vt, p );                     /* the record's host copy and its line re-check (copy threads) */
       /* tags are the pending counter: completions come back in order */
       out[n].result = vt_after( vt, p, (int)vt->p_codes[i], vt->p_img + i*FDGPU_TXN_IMG_STRIDE, vt->p_fp[i],
                                 vt->p_dtag[i], &out[n] );
@@ -1604,7 +1736,8 @@ static void link_pin( int cpu ) {
     fprintf( stderr, "fdgpu_link: could not pin to CPU %d\n", cpu );
 }
 
-typedef struct { fdgpu_link_t * l; int idx, device, cpu, lcpu; } link_tile_arg_t;   /* lcpu: its launch thread's */
+typedef struct { fdgpu_link_t * l; int idx, device, cpu, lcpu, ccpu[ FDGPU_VTILE_COPY_THREADS_MAX ]; } link_tile_arg_t;
+/* lcpu: its launch thread's CPU, ccpu: its copy threads' */
 
 /* per-link state of a tile */
 typedef struct {
@@ -1690,6 +1823,8 @@ static void * link_tile( void * _a ) {
   vo.nctx = c->nctx; vo.copy_wait_ns = c->copy_wait_ns; vo.copy_min = c->copy_min; vo.gather_cus = c->gather_cus;
   vo.max_uncopied = c->max_uncopied; vo.cu_split = c->cu_split; vo.cu_exclusive = c->cu_exclusive;
   vo.launcher = c->launcher; vo.launcher_core = c->launcher && a->lcpu >= 0 ? a->lcpu + 1 : 0;
+  vo.copy_threads = c->zero_copy ? c->copy_threads : 0;
+  for( int i=0; i<vo.copy_threads && i<FDGPU_VTILE_COPY_THREADS_MAX; i++ ) vo.copy_cores[i] = a->ccpu[i] >= 0 ? a->ccpu[i] + 1 : 0;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                              ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
@@ -1880,9 +2015,11 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   int mine[ LINK_TILE_MAX ], myq[ LINK_PROD_MAX ], np = 0;
   int nt = fdgpu_link_tiles_of( c->tiles, c->gpus, proc, mine );   /* tile i drives GPU i % G: this process's tiles */
   if( run_producer ) for( int q=0; q<c->producers; q++ ) if( q % c->gpus == proc ) myq[np++] = q;
-  int cpus[ 2*LINK_TILE_MAX + LINK_PROD_MAX ];
+  int cpus[ ( 2 + FDGPU_VTILE_COPY_THREADS_MAX )*LINK_TILE_MAX + LINK_PROD_MAX ];
   int nl = c->launcher ? nt : 0;                 /* the tiles' launch threads: a core each, after the tiles' */
-  int ncpu = link_pick_cpus( device, proc, nt + np + nl, cpus );
+  int H = c->zero_copy && c->copy_threads > 0 ? ( c->copy_threads < FDGPU_VTILE_COPY_THREADS_MAX ? c->copy_threads
+                                                                                                  : FDGPU_VTILE_COPY_THREADS_MAX ) : 0;
+  int ncpu = link_pick_cpus( device, proc, nt + np + nl + nt*H, cpus );   /* ... and their copy threads, after those */
   if( getenv( "FDGPU_LINK_VERBOSE" ) ) {
     fprintf( stderr, "fdgpu_link: proc %d device %d numa %d producers %d tiles %d cpus:", proc, device,
              fdgpu_device_numa_node( device ), np, nt );
@@ -1893,6 +2030,10 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
     args[t].l = l; args[t].idx = mine[t]; args[t].device = device;
     args[t].cpu = np + t < ncpu ? cpus[ np + t ] : -1;
     args[t].lcpu = nl && np + nt + t < ncpu ? cpus[ np + nt + t ] : -1;
+    for( int i=0; i<FDGPU_VTILE_COPY_THREADS_MAX; i++ ) {
+      int j = np + nt + nl + t*H + i;
+      args[t].ccpu[i] = i < H && j < ncpu ? cpus[j] : -1;
+    }
     pthread_create( &th[t], NULL, link_tile, &args[t] );
   }
   for( int i=0; i<np; i++ ) {
@@ -1942,6 +2083,7 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     st->copy_backlog += r->gm.copy_backlog;
     st->launcher[0] += r->gm.launcher[0]; st->launcher[1] += r->gm.launcher[1]; st->launcher[3] += r->gm.launcher[3];
     if( r->gm.launcher[2] > st->launcher[2] ) st->launcher[2] = r->gm.launcher[2];
+    for( int k=0; k<4; k++ ) st->host_copy[k] += r->gm.host_copy[k];
     st->tile_idle_ns += r->ns_idle;
     st->tile_cpu_ns += r->cpu_ns; st->tile_wall_ns += r->wall_ns; st->tile_nivcsw += r->nivcsw;
     double share = r->wall_ns ? (double)r->cpu_ns / (double)r->wall_ns : 1.;

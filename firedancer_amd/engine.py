@@ -53,7 +53,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_slow_count", "fdgpu_ed25519_set_dedup",
            "fdgpu_ed25519_set_record_fp_off", "fdgpu_ed25519_batch_stats", "fdgpu_ed25519_launch_stats", "fdgpu_ed25519_front_remaining", "fdgpu_ed25519_front_batch", "fdgpu_ed25519_verify_txn_ptrs",
-           "fdgpu_launcher_new", "fdgpu_launcher_delete", "fdgpu_launcher_stats", "fdgpu_ed25519_set_launcher",
+           "fdgpu_ed25519_submit_raw_gather_dev_f", "fdgpu_launcher_new", "fdgpu_launcher_delete", "fdgpu_launcher_stats", "fdgpu_ed25519_set_launcher",
            "fdgpu_last_error")
 
 _lib = None

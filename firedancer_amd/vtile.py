@@ -63,10 +63,11 @@ class GpuMetrics(ctypes.Structure):
                 ("launch_ns", ctypes.c_ulong), ("copies", ctypes.c_ulong), ("copy_lat_n", ctypes.c_ulong),
                 ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong),
                 ("gather_gpu", ctypes.c_ulong * 5), ("phase", ctypes.c_ulong * 9), ("copy_backlog", ctypes.c_ulong),
-                ("launcher", ctypes.c_ulong * 4)]
+                ("launcher", ctypes.c_ulong * 4), ("host_copy", ctypes.c_ulong * 4)]
 
     def as_dict(self) -> dict:
-        return {k: (list(getattr(self, k)) if k in ("lat_hist", "gather_gpu", "phase", "launcher") else int(getattr(self, k)))
+        return {k: (list(getattr(self, k)) if k in ("lat_hist", "gather_gpu", "phase", "launcher", "host_copy")
+                    else int(getattr(self, k)))
                 for k, _ in self._fields_}
 
 
@@ -76,7 +77,7 @@ class VTileOpts(ctypes.Structure):
                 ("min_batch", ctypes.c_ulong), ("max_wait_ns", ctypes.c_ulong), ("copy_wait_ns", ctypes.c_ulong),
                 ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint), ("max_uncopied", ctypes.c_ulong),
                 ("cu_split", ctypes.c_int), ("cu_exclusive", ctypes.c_int), ("launcher", ctypes.c_int),
-                ("launcher_core", ctypes.c_int)]
+                ("launcher_core", ctypes.c_int), ("copy_threads", ctypes.c_int), ("copy_cores", ctypes.c_int * 8)]
 
 
 class StreamCfg(ctypes.Structure):
@@ -86,7 +87,8 @@ class StreamCfg(ctypes.Structure):
                 ("nctx", ctypes.c_int), ("prof", ctypes.c_int), ("out_mult", ctypes.c_ulong),
                 ("copy_wait_ns", ctypes.c_ulong), ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint),
                 ("max_uncopied", ctypes.c_ulong), ("pf_dist", ctypes.c_int), ("cu_split", ctypes.c_int),
-                ("cu_exclusive", ctypes.c_int), ("no_huge_pages", ctypes.c_int), ("launcher", ctypes.c_int)]
+                ("cu_exclusive", ctypes.c_int), ("no_huge_pages", ctypes.c_int), ("launcher", ctypes.c_int),
+                ("copy_threads", ctypes.c_int)]
 
 
 class StreamStats(ctypes.Structure):
@@ -105,14 +107,14 @@ class StreamStats(ctypes.Structure):
                 ("tile_cpu_ns", ctypes.c_ulong), ("tile_wall_ns", ctypes.c_ulong), ("tile_nivcsw", ctypes.c_ulong),
                 ("tile_cpu_share_min", ctypes.c_double), ("tile_cpu", ctypes.c_long * 8),
                 ("prod_cpu_ns", ctypes.c_ulong), ("prod_wall_ns", ctypes.c_ulong), ("prod_nivcsw", ctypes.c_ulong),
-                ("launcher", ctypes.c_ulong * 4)]
+                ("launcher", ctypes.c_ulong * 4), ("host_copy", ctypes.c_ulong * 4)]
 
     def as_dict(self) -> dict:
         out = {}
         for k, _ in self._fields_:
             v = getattr(self, k)
             out[k] = list(v) if k in ("metrics", "tile_ns", "gpu_lat_hist", "prof_ns", "gather_gpu", "phase", "tile_cpu",
-                                      "launcher") else v
+                                      "launcher", "host_copy") else v
         return out
 
 
@@ -411,12 +413,12 @@ def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
 
 def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers=1, nctx=0, prof=0,
          out_mult=0, copy_wait_ns=0, copy_min=0, gather_cus=0, max_uncopied=0, pf_dist=0, no_huge_pages=0, cu_split=0, cu_exclusive=0,
-         launcher=0) -> StreamCfg:
+         launcher=0, copy_threads=0) -> StreamCfg:
     return StreamCfg(n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
                      gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0, producers=producers,
                      nctx=nctx, prof=prof, out_mult=out_mult, copy_wait_ns=copy_wait_ns, copy_min=copy_min,
                      gather_cus=gather_cus, max_uncopied=max_uncopied, pf_dist=pf_dist, no_huge_pages=no_huge_pages, cu_split=cu_split,
-                     cu_exclusive=cu_exclusive, launcher=launcher)
+                     cu_exclusive=cu_exclusive, launcher=launcher, copy_threads=copy_threads)
 
 
 def stream_run(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,

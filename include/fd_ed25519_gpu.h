@@ -561,6 +561,18 @@ int           fdgpu_ed25519_submit_raw_gather_dev( fdgpu_ed25519_ctx_t * ctx, un
                                                    unsigned char * dst, unsigned short copy_sz, unsigned short payload_off,
                                                    unsigned short payload_sz, unsigned long tag,
                                                    unsigned long const * seq_dev, unsigned long seq );
+/* ... with flags: FDGPU_GATHER_NO_WRITEBACK -- the GPU copies the record into its arena (and re-checks the
+   seq) but does not write it back to dst: the caller copies bytes [0, 10) and [12, copy_sz) of the record
+   there itself (host copy threads, fdgpu_vtile_opts_t.copy_threads), the GPU still writes the record's
+   txn_t_sz (bytes 10-11, with fdgpu_ed25519_set_record_fp_off 10) and its fd_txn_t image.  The record then
+   crosses PCIe once (read) instead of twice. */
+#define FDGPU_GATHER_NO_WRITEBACK (1U)
+int           fdgpu_ed25519_submit_raw_gather_dev_f( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src,
+                                                     unsigned char const * src_dev, unsigned char * dst_base,
+                                                     unsigned char * dst, unsigned short copy_sz,
+                                                     unsigned short payload_off, unsigned short payload_sz,
+                                                     unsigned long tag, unsigned long const * seq_dev,
+                                                     unsigned long seq, unsigned flags );
 /* the region registered with fdgpu_host_register / fdgpu_host_alloc that holds p: its host base, size and
    device base; 0, or -1 if p is in none */
 int           fdgpu_host_region( void const * p, void ** base, unsigned long * sz, void ** dev_base );

@@ -180,6 +180,8 @@ typedef struct fdgpu_vtile_gpu_metrics {
   unsigned long copy_backlog;     /* during_frag calls refused with FDGPU_VTILE_COPY_BACKLOG */
   unsigned long launcher[ 4 ];    /* the tile's launch thread (opts.launcher), fdgpu_launcher_stats: commands issued,
                                      ns issuing them, deepest queue, pushes that waited for room (0s without one) */
+  unsigned long host_copy[ 4 ];   /* the tile's copy threads (opts.copy_threads): records copied, ns copying (summed over
+                                     threads), records found overrun after their copy, ns the tile waited for a copy */
 } fdgpu_vtile_gpu_metrics_t;
 
 /* device: HIP device; batch_txn: transactions per GPU batch (staging
@@ -222,7 +224,14 @@ typedef struct fdgpu_vtile_opts {
                                     of the tile's own (fdgpu_launcher_new): the tile's thread only queues them;
                                     0: on the tile's thread */
   int           launcher_core;   /* with launcher: 1 + the CPU its thread is pinned to (0: not pinned) */
+  int           copy_threads;    /* zero-copy intake: 0 = the GPU copy writes each record into the out dcache as it
+                                    reads it (the record crosses PCIe twice); 1..FDGPU_VTILE_COPY_THREADS_MAX = that
+                                    many host threads of the tile copy the records in -> out dcache instead (as the
+                                    reference's during_frag does, fd_verify_tile.c:96-101), re-checking each frag's
+                                    mcache line after the copy, and the GPU only reads them */
+  int           copy_cores[ 8 ]; /* with copy_threads: 1 + the CPU copy thread i is pinned to (0: not pinned) */
 } fdgpu_vtile_opts_t;
+#define FDGPU_VTILE_COPY_THREADS_MAX 8
 
 fdgpu_vtile_t * fdgpu_vtile_new( int device, unsigned long batch_txn, unsigned long tcache_depth, unsigned long seed,
                                  unsigned long out_dcache_bytes, int semantics );
@@ -406,6 +415,7 @@ typedef struct fdgpu_stream_cfg {
                                     +4 %, profiles/r04/i) */
   int           launcher;        /* 1: every tile with a launch thread of its own (fdgpu_vtile_opts_t.launcher),
                                     pinned to a core of its own next to the tiles' */
+  int           copy_threads;    /* fdgpu_vtile_opts_t.copy_threads of every tile, each thread on a core of its own */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
@@ -444,6 +454,7 @@ typedef struct fdgpu_stream_stats {
   unsigned long prod_cpu_ns, prod_wall_ns, prod_nivcsw;   /* summed over producers */
   unsigned long launcher[ 4 ];   /* the tiles' launch threads (cfg.launcher): commands and ns issuing them (summed),
                                     deepest queue (max), pushes that waited for room (summed) */
+  unsigned long host_copy[ 4 ];  /* the tiles' copy threads (cfg.copy_threads), fdgpu_vtile_gpu_metrics_t.host_copy summed */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per

@@ -197,6 +197,19 @@ def test_host_plan_paced_launch_threads(cores, gpus, launchers):
     assert bench._leg_cfg(args, "max", gpus, 20e6)["launcher"] == 0
 
 
+@pytest.mark.parametrize("cores,gpus,h,tiles", [(128, 8, 2, 2), (56, 8, 2, 2), (40, 8, 2, 1), (24, 8, 1, 1), (16, 8, 0, 1)])
+def test_host_plan_copy_threads(cores, gpus, h, tiles):
+    """--stream-copy-threads 2: each max-rate tile's copy threads take a core each; short of cores the plan
+    lowers tiles first, then copy threads (never below one tile)."""
+    args = bench.parse_args(["--stream-copy-threads", "2", "--plan-cores", str(cores)])
+    plan = bench.host_plan(args, gpus, cores=cores, nodes={0: cores}, gpu_nodes=[0] * gpus)
+    assert plan["requested"]["cores"] == gpus * (2 * 3 + 1)
+    assert plan["applied"]["copy_threads_per_tile"] == h and plan["applied"]["tiles_per_gpu"] == tiles
+    assert plan["applied"]["cores"] <= max(cores, gpus * 2)
+    assert bench._leg_cfg(args, "max", gpus, 20e6)["copy_threads"] == h
+    assert bench._leg_cfg(args, "paced@5000000.0", gpus, 20e6)["copy_threads"] == 0
+
+
 def test_host_plan_per_numa_node():
     """Each child pins to its GPU's NUMA node first: 4 GPUs on a 6-core node and 4 on a 64-core node get the
     small node's share (1 tile each) rather than oversubscribing it."""

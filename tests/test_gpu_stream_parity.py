@@ -191,3 +191,22 @@ def test_stream_parity_reliable_launch_thread():
     assert st["launcher"][0] >= st["batches"] > 0
     seen = list(check_tiles(pays, traces))
     assert sum(k for _, k, _ in seen) == N_FRAGS
+
+
+@pytest.mark.parametrize("reliable", [True, False])
+def test_stream_parity_host_copy_threads(reliable):
+    """Two tiles whose copy threads write each record into the out dcache while the GPU copy only reads it
+    (fdgpu_vtile_opts_t.copy_threads = 2, the bench's --stream-copy-threads): reliable, and unreliable with
+    a producer lapping a 4096-line mcache (frags overrun at the poll or found overrun by a copy are never
+    published).  Frag for frag the reference tile's verdicts, tags and records."""
+    pays = payload_set()
+    st, traces, _ = run_leg(pays, reliable=reliable, depth=1 << 16 if reliable else 1 << 12, copy_threads=2)
+    if reliable:
+        assert st["verdicts"] == N_FRAGS and st["lost"] == 0 and st["overruns"] == 0
+    else:
+        assert st["verdicts"] + st["lost"] == N_FRAGS and st["lost"] > 0
+    assert st["host_copy"][0] == st["verdicts"]          # every frag a tile took was copied by a copy thread
+    n_ovr = sum(int((t["result"] == 5).sum()) for t in traces)
+    assert n_ovr == st["overruns"]
+    seen = list(check_tiles(pays, traces))
+    assert sum(k for _, k, _ in seen) == st["verdicts"] - st["overruns"]

@@ -121,13 +121,15 @@ def in_dcache(frag_list):
     return buf, [base + o for o in offs]
 
 
-@pytest.mark.parametrize("zero_copy", [False, True, "finish"])
+@pytest.mark.parametrize("zero_copy", [False, True, "finish", "host"])
 @pytest.mark.parametrize("batch,depth", [(64, 32), (512, 1 << 12)])
 def test_vtile_vs_model(oracle, batch, depth, zero_copy, engine_path):
     """zero_copy: the frags stay in a registered in dcache and the GPU gathers them into the out
     dcache records (fdgpu_vtile_set_in_link); outcomes and published records must not change.
     "finish": the same, with the records written into the out dcache by each batch's fd_finish_kernel
-    from the device arena instead of by the gather kernel (fdgpu_debug_opts_t.gather_no_writeback = 2)."""
+    from the device arena instead of by the gather kernel (fdgpu_debug_opts_t.gather_no_writeback = 2).
+    "host": the GPU copy only reads each record; two host copy threads of the tile write it into the out
+    dcache (fdgpu_vtile_opts_t.copy_threads, FDGPU_GATHER_NO_WRITEBACK)."""
     pytest.importorskip("xxhash")
     from firedancer_amd import engine, vtile
     if zero_copy == "finish":
@@ -136,7 +138,8 @@ def test_vtile_vs_model(oracle, batch, depth, zero_copy, engine_path):
     frags = make_stream()
     seed = 0x1234abcd
     want_res, want_m, want_recs, want_tags = expectation(oracle, frags, seed, depth)
-    vt = vtile.VTile(device=0, batch_txn=batch, tcache_depth=depth, seed=seed)
+    vt = vtile.VTile(device=0, batch_txn=batch, tcache_depth=depth, seed=seed,
+                     copy_threads=2 if zero_copy == "host" else 0)
     if zero_copy:
         fbs = [vtile.frag_bytes(p, b) for p, b in frags]
         buf, offs = in_dcache(fbs)
@@ -175,6 +178,8 @@ def test_vtile_vs_model(oracle, batch, depth, zero_copy, engine_path):
     assert vt.metrics() == want_m
     assert bad == []
     assert sum(want_m[:4]) > 100 and want_m[2] > 10 and want_m[3] > 0
+    hc = vt.gpu_metrics()["host_copy"]
+    assert (hc[0] == len(frags) and hc[2] == 0) if zero_copy == "host" else hc == [0, 0, 0, 0]
     vt.close()
     if zero_copy:
         engine.host_unregister(buf)
