@@ -308,7 +308,10 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 launcher=Lc if paced else 0,
                 # max-rate and unreliable legs: host threads copy each record into the out dcache (the GPU copy only
                 # reads it), so a record crosses PCIe once (--stream-copy-threads)
-                copy_threads=0 if paced else H)
+                copy_threads=0 if paced else H,
+                # max-rate legs: a partial batch waits (up to 2 ms) until it holds --stream-tput-min-batch frags, so
+                # it takes the throughput path (the latency path's 4-lane walk does twice the work per signature)
+                min_batch=args.stream_tput_min_batch if tput else 0)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -515,7 +518,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
         (["--stream-only-paced"] if args.stream_only_paced else []) + \
         ["--stream-cu-split", str(args.stream_cu_split), "--stream-lat-cu-split", str(args.stream_lat_cu_split),
          "--stream-cu-exclusive", str(args.stream_cu_exclusive), "--stream-lat-launcher", str(args.stream_lat_launcher),
-         "--stream-copy-threads", str(args.stream_copy_threads)]
+         "--stream-copy-threads", str(args.stream_copy_threads),
+         "--stream-tput-min-batch", str(args.stream_tput_min_batch)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -861,6 +865,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-lat-launcher", type=int, default=0, choices=(0, 1),
                     help="paced legs: each tile's batch launches and copies on a launch thread of its own, a core "
                          "each (fdgpu_vtile_opts_t.launcher; the host plan drops it when the cores are short)")
+    ap.add_argument("--stream-tput-min-batch", type=int, default=0,
+                    help="max-rate legs: batches wait (up to 2 ms) for at least this many frags (fdgpu_vtile_opts_t."
+                         "min_batch; 0 = launch when the GPU has room)")
     ap.add_argument("--stream-copy-threads", type=int, default=0, choices=range(0, 9),
                     help="max-rate and unreliable legs: host threads per tile that copy each record into the out dcache "
                          "while the GPU copy only reads it (fdgpu_vtile_opts_t.copy_threads; a core each in the host plan)")

@@ -369,8 +369,10 @@ typedef struct {
 typedef struct {
   vt_cp_task_t *   ring;
   ulong            mask;
-  _Atomic ulong    tail __attribute__(( aligned( 64 ) ));   /* tasks pushed (the tile) */
+  _Atomic ulong    tail __attribute__(( aligned( 64 ) ));   /* tasks published to the copy thread (the tile) */
   _Atomic ulong    done __attribute__(( aligned( 64 ) ));   /* tasks completed (the copy thread) */
+  ulong            ptail __attribute__(( aligned( 64 ) ));  /* the tile's: tasks written (published in groups) */
+  ulong            sdone;                                     /* the tile's: done as last seen */
   _Atomic int      stop;
   ulong            busy_ns, ovr_cnt;     /* the copy thread's */
   int              cpu;
@@ -443,6 +445,18 @@ struct fdgpu_vtile {
   unsigned short *      p_fp;
 };
 
+/* one record, bytes [0, 10) and [12, sz) of src -> dst (chunk aligned): plain stores for the first 16
+   bytes (around txn_t_sz, which the GPU writes) and the tail (the GPU writes the fd_txn_t image right
+   behind it), streaming 16-B stores between -- as the GPU's write-back was, straight to memory, no
+   read-for-ownership of the cold out dcache lines */
+static inline void vt_cp_record( uchar * dst, uchar const * src, ulong sz ) {
+  memcpy( dst, src, 10UL ); memcpy( dst + 12UL, src + 12UL, 4UL );
+  ulong n16 = sz >> 4;
+  for( ulong i=1UL; i<n16; i++ )
+    _mm_stream_si128( (__m128i *)( dst + 16UL*i ), _mm_load_si128( (__m128i const *)( src + 16UL*i ) ) );
+  if( sz & 15UL ) memcpy( dst + 16UL*n16, src + 16UL*n16, sz & 15UL );
+}
+
 static void * vt_cp_main( void * arg ) {
   vt_cp_t * c = (vt_cp_t *)arg;
   if( c->cpu >= 0 ) {
@@ -460,16 +474,20 @@ static void * vt_cp_main( void * arg ) {
     ulong t0 = now_ns();
     for( ; j < t; j++ ) {
       vt_cp_task_t const * k = &c->ring[ j & c->mask ];
-      memcpy( k->dst, k->src, 10UL );                            /* around txn_t_sz (the GPU's) */
-      memcpy( k->dst + 12UL, k->src + 12UL, k->sz - 12UL );
+      if( j + 1UL < t ) {                                      /* the next record's first lines */
+        uchar const * nx = c->ring[ ( j + 1UL ) & c->mask ].src;
+        __builtin_prefetch( nx ); __builtin_prefetch( nx + 64 ); __builtin_prefetch( nx + 128 );
+      }
+      vt_cp_record( k->dst, k->src, k->sz );
       if( k->line_seq ) {                                        /* the stem's re-check after its copy */
         atomic_thread_fence( memory_order_acquire );
         if( atomic_load_explicit( (_Atomic ulong const *)k->line_seq, memory_order_relaxed ) != k->seq ) {
           *k->ovr = 1; c->ovr_cnt++;
         }
       }
-      atomic_store_explicit( &c->done, j + 1UL, memory_order_release );
     }
+    _mm_sfence();                                                /* the streaming stores, before done */
+    atomic_store_explicit( &c->done, j, memory_order_release );
     c->busy_ns += now_ns() - t0;
   }
   return NULL;
@@ -491,11 +509,27 @@ static vt_cp_t * vt_cp_new( ulong cap, int cpu ) {
   return c;
 }
 
-/* copy task k (1-based, vt_pend_t.cp) has completed */
+/* copy task k (1-based, vt_pend_t.cp) has completed.  The tile keeps the last completion count it saw and
+   reads the thread's (a line the thread keeps writing) only when that is not enough: one cross-core read
+   per batch of verdicts instead of one per frag */
 static inline int vt_cp_done( fdgpu_vtile_t const * vt, ulong k ) {
   ulong i = k - 1UL;
   vt_cp_t * c = vt->cp[ i % (ulong)vt->ncp ];
-  return atomic_load_explicit( &c->done, memory_order_acquire ) > i / (ulong)vt->ncp;
+  ulong j = i / (ulong)vt->ncp;
+  if( c->sdone > j ) return 1;
+  if( c->ptail > atomic_load_explicit( &c->tail, memory_order_relaxed ) )   /* unpublished tasks: publish them */
+    atomic_store_explicit( &c->tail, c->ptail, memory_order_release );
+  c->sdone = atomic_load_explicit( &c->done, memory_order_acquire );
+  return c->sdone > j;
+}
+
+/* publish the tasks written so far to every copy thread (the tile publishes them in groups of 16) */
+static inline void vt_cp_publish( fdgpu_vtile_t const * vt ) {
+  for( int i=0; i<vt->ncp; i++ ) {
+    vt_cp_t * c = vt->cp[i];
+    if( c->ptail != atomic_load_explicit( &c->tail, memory_order_relaxed ) )
+      atomic_store_explicit( &c->tail, c->ptail, memory_order_release );
+  }
 }
 
 /* wait for frag p's host copy, if it has one (copy threads; in practice long done) */
@@ -854,6 +888,7 @@ vt_should_launch( fdgpu_vtile_t * vt, int f, ulong max_inflight, ulong now, ulon
 int
 fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
   ulong filling, now = now_ns();
+  vt_cp_publish( vt );                           /* copy tasks written since the last group of 16 */
   /* batch duration: a context's batches have drained (inflight counts
      launched slots not yet fully polled) */
   for( int k=0; k<vt->nctx; k++ ) {
@@ -989,11 +1024,12 @@ vt_during_txnm( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong
       vt_pend_t * p = &vt->pend[ ( vt->pend_tail - 1UL ) % vt->pend_cap ];
       ulong i = vt->cp_cnt++;
       vt_cp_t * cq = vt->cp[ i % (ulong)vt->ncp ];
-      ulong t = atomic_load_explicit( &cq->tail, memory_order_relaxed );
+      ulong t = cq->ptail;
       vt_cp_task_t * k = &cq->ring[ t & cq->mask ];
       k->src = src; k->dst = dst; k->sz = FDGPU_TXNM_HDR_SZ + in->payload_sz;
       k->line_seq = mc ? (ulong const *)&mc->line[ seq & ( mc->depth - 1UL ) ].seq : NULL; k->seq = seq; k->ovr = &p->ovr;
-      atomic_store_explicit( &cq->tail, t + 1UL, memory_order_release );
+      cq->ptail = t + 1UL;
+      if( !( cq->ptail & 15UL ) ) atomic_store_explicit( &cq->tail, cq->ptail, memory_order_release );
       p->cp = i + 1UL;
     }
     return 0;
@@ -1824,6 +1860,7 @@ static void * link_tile( void * _a ) {
   vo.max_uncopied = c->max_uncopied; vo.cu_split = c->cu_split; vo.cu_exclusive = c->cu_exclusive;
   vo.launcher = c->launcher; vo.launcher_core = c->launcher && a->lcpu >= 0 ? a->lcpu + 1 : 0;
   vo.copy_threads = c->zero_copy ? c->copy_threads : 0;
+  vo.min_batch = c->min_batch;
   for( int i=0; i<vo.copy_threads && i<FDGPU_VTILE_COPY_THREADS_MAX; i++ ) vo.copy_cores[i] = a->ccpu[i] >= 0 ? a->ccpu[i] + 1 : 0;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                              ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );

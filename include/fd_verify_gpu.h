@@ -416,6 +416,8 @@ typedef struct fdgpu_stream_cfg {
   int           launcher;        /* 1: every tile with a launch thread of its own (fdgpu_vtile_opts_t.launcher),
                                     pinned to a core of its own next to the tiles' */
   int           copy_threads;    /* fdgpu_vtile_opts_t.copy_threads of every tile, each thread on a core of its own */
+  unsigned long min_batch;       /* fdgpu_vtile_opts_t.min_batch of every tile (0: none; the max-rate legs: batches
+                                    above the latency path's limit, so they take the throughput path) */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {

@@ -4,6 +4,8 @@
 #            tools/prep_probe.py) at 1,000 / 2,800 / 8,192 txns, the chain's kernel trace at 2,800 txns,
 #            the paced stream parity tests and the launch-thread tests, then an interleaved A/B of the
 #            paced legs' launch thread (--stream-lat-launcher 0 / 1)
+#   hc     : host copy threads: their parity tests, then max-rate arms with 0 / 1 / 2 copy threads per tile on
+#            2, 3 and 4 tiles
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 job="$1"; shift
@@ -33,5 +35,25 @@ case "$job" in
     run_arms r05_lc "$Q --stream-rates 5e6,7.5e6,10e6,12.5e6,15e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
       "l0a=--stream-lat-launcher 0" "l1a=--stream-lat-launcher 1" "l1b=--stream-lat-launcher 1" "l0b=--stream-lat-launcher 0"
     ;;
-  *) sed -n '2,6p' "$0"; exit 2 ;;
+  hc)
+    # host copy threads (--stream-copy-threads): the parity tests, then max-rate arms on 2 and 3 tiles
+    bash tools/gpu_job.sh \
+      "parity:900:python -u -m pytest tests/test_gpu_stream_parity.py tests/test_gpu_vtile.py -k 'host or copy_threads or vs_model' -q -rA --timeout 300 --timeout-method thread" &&
+    run_arms r05_hc "$Q --stream-rates 10e6 --stream-paced-seconds 3 --stream-seconds 4 --stream-unrel-seconds 2" \
+      "b0a=" "h1a=--stream-copy-threads 1" "h2a=--stream-copy-threads 2" "t3h2a=--stream-tiles 3 --stream-copy-threads 2" \
+      "t3h1a=--stream-tiles 3 --stream-copy-threads 1" "t4h1a=--stream-tiles 4 --stream-copy-threads 1" \
+      "h2b=--stream-copy-threads 2" "b0b="
+    ;;
+  hc2)
+    # copy threads with streaming stores, grouped publishes and cached counters; max-rate batches held to the
+    # throughput path (--stream-tput-min-batch 40960)
+    M="--stream-tput-min-batch 40960"
+    bash tools/gpu_job.sh \
+      "parity:900:python -u -m pytest tests/test_gpu_stream_parity.py tests/test_gpu_vtile.py -k 'host or copy_threads' -q -rA --timeout 300 --timeout-method thread" &&
+    run_arms r05_hc2 "$Q --stream-rates 10e6 --stream-paced-seconds 3 --stream-seconds 4 --stream-unrel-seconds 2" \
+      "b0a=" "m0a=$M" "h2ma=--stream-copy-threads 2 $M" "t3h2ma=--stream-tiles 3 --stream-copy-threads 2 $M" \
+      "t3h1ma=--stream-tiles 3 --stream-copy-threads 1 $M" "t4h1ma=--stream-tiles 4 --stream-copy-threads 1 $M" \
+      "h3ma=--stream-copy-threads 3 $M" "h2mb=--stream-copy-threads 2 $M" "t3h2mb=--stream-tiles 3 --stream-copy-threads 2 $M" "b0b="
+    ;;
+  *) sed -n '2,8p' "$0"; exit 2 ;;
 esac
