@@ -311,7 +311,9 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 copy_threads=0 if paced else H,
                 # max-rate legs: a partial batch waits (up to 2 ms) until it holds --stream-tput-min-batch frags, so
                 # it takes the throughput path (the latency path's 4-lane walk does twice the work per signature)
-                min_batch=args.stream_tput_min_batch if tput else 0)
+                min_batch=args.stream_tput_min_batch if tput else 0,
+                # max-rate legs: batches above --stream-tput-small-max signatures take the throughput path
+                small_max=args.stream_tput_small_max if tput else 0)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -519,7 +521,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
         ["--stream-cu-split", str(args.stream_cu_split), "--stream-lat-cu-split", str(args.stream_lat_cu_split),
          "--stream-cu-exclusive", str(args.stream_cu_exclusive), "--stream-lat-launcher", str(args.stream_lat_launcher),
          "--stream-copy-threads", str(args.stream_copy_threads),
-         "--stream-tput-min-batch", str(args.stream_tput_min_batch)]
+         "--stream-tput-min-batch", str(args.stream_tput_min_batch),
+         "--stream-tput-small-max", str(args.stream_tput_small_max)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -868,6 +871,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-tput-min-batch", type=int, default=0,
                     help="max-rate legs: batches wait (up to 2 ms) for at least this many frags (fdgpu_vtile_opts_t."
                          "min_batch; 0 = launch when the GPU has room)")
+    ap.add_argument("--stream-tput-small-max", type=int, default=0,
+                    help="max-rate legs: batches of at most this many signatures take the latency path "
+                         "(fdgpu_vtile_opts_t.small_max; 0 = the tile's default, half the batch limit)")
     ap.add_argument("--stream-copy-threads", type=int, default=0, choices=range(0, 9),
                     help="max-rate and unreliable legs: host threads per tile that copy each record into the out dcache "
                          "while the GPU copy only reads it (fdgpu_vtile_opts_t.copy_threads; a core each in the host plan)")

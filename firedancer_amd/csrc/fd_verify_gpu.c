@@ -445,16 +445,13 @@ struct fdgpu_vtile {
   unsigned short *      p_fp;
 };
 
-/* one record, bytes [0, 10) and [12, sz) of src -> dst (chunk aligned): plain stores for the first 16
-   bytes (around txn_t_sz, which the GPU writes) and the tail (the GPU writes the fd_txn_t image right
-   behind it), streaming 16-B stores between -- as the GPU's write-back was, straight to memory, no
-   read-for-ownership of the cold out dcache lines */
+/* one record, bytes [0, 10) and [12, sz) of src -> dst: around txn_t_sz, which the GPU writes, and not
+   past sz (the GPU writes the fd_txn_t image right behind the payload), so the two never write the same
+   byte whatever their order.  (Streaming stores measured slower here: 165-180 vs 125-150 ns per record,
+   profiles/r05/hc2.) */
 static inline void vt_cp_record( uchar * dst, uchar const * src, ulong sz ) {
-  memcpy( dst, src, 10UL ); memcpy( dst + 12UL, src + 12UL, 4UL );
-  ulong n16 = sz >> 4;
-  for( ulong i=1UL; i<n16; i++ )
-    _mm_stream_si128( (__m128i *)( dst + 16UL*i ), _mm_load_si128( (__m128i const *)( src + 16UL*i ) ) );
-  if( sz & 15UL ) memcpy( dst + 16UL*n16, src + 16UL*n16, sz & 15UL );
+  memcpy( dst, src, 10UL );
+  memcpy( dst + 12UL, src + 12UL, sz - 12UL );
 }
 
 static void * vt_cp_main( void * arg ) {
@@ -474,9 +471,9 @@ static void * vt_cp_main( void * arg ) {
     ulong t0 = now_ns();
     for( ; j < t; j++ ) {
       vt_cp_task_t const * k = &c->ring[ j & c->mask ];
-      if( j + 1UL < t ) {                                      /* the next record's first lines */
-        uchar const * nx = c->ring[ ( j + 1UL ) & c->mask ].src;
-        __builtin_prefetch( nx ); __builtin_prefetch( nx + 64 ); __builtin_prefetch( nx + 128 );
+      if( j + 1UL < t ) {                                      /* the next record, whole (~21 lines, cold) */
+        vt_cp_task_t const * nk = &c->ring[ ( j + 1UL ) & c->mask ];
+        for( ulong o=0UL; o<nk->sz; o+=64UL ) __builtin_prefetch( nk->src + o );
       }
       vt_cp_record( k->dst, k->src, k->sz );
       if( k->line_seq ) {                                        /* the stem's re-check after its copy */
@@ -486,7 +483,6 @@ static void * vt_cp_main( void * arg ) {
         }
       }
     }
-    _mm_sfence();                                                /* the streaming stores, before done */
     atomic_store_explicit( &c->done, j, memory_order_release );
     c->busy_ns += now_ns() - t0;
   }
@@ -1860,7 +1856,7 @@ static void * link_tile( void * _a ) {
   vo.max_uncopied = c->max_uncopied; vo.cu_split = c->cu_split; vo.cu_exclusive = c->cu_exclusive;
   vo.launcher = c->launcher; vo.launcher_core = c->launcher && a->lcpu >= 0 ? a->lcpu + 1 : 0;
   vo.copy_threads = c->zero_copy ? c->copy_threads : 0;
-  vo.min_batch = c->min_batch;
+  vo.min_batch = c->min_batch; vo.small_max = c->small_max;
   for( int i=0; i<vo.copy_threads && i<FDGPU_VTILE_COPY_THREADS_MAX; i++ ) vo.copy_cores[i] = a->ccpu[i] >= 0 ? a->ccpu[i] + 1 : 0;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                              ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );

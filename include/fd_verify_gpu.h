@@ -418,6 +418,7 @@ typedef struct fdgpu_stream_cfg {
   int           copy_threads;    /* fdgpu_vtile_opts_t.copy_threads of every tile, each thread on a core of its own */
   unsigned long min_batch;       /* fdgpu_vtile_opts_t.min_batch of every tile (0: none; the max-rate legs: batches
                                     above the latency path's limit, so they take the throughput path) */
+  unsigned long small_max;       /* fdgpu_vtile_opts_t.small_max of every tile (0: its default, half the batch limit) */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {

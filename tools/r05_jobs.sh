@@ -55,5 +55,16 @@ case "$job" in
       "t3h1ma=--stream-tiles 3 --stream-copy-threads 1 $M" "t4h1ma=--stream-tiles 4 --stream-copy-threads 1 $M" \
       "h3ma=--stream-copy-threads 3 $M" "h2mb=--stream-copy-threads 2 $M" "t3h2mb=--stream-tiles 3 --stream-copy-threads 2 $M" "b0b="
     ;;
+  hc3)
+    # copy threads with plain copies and a whole-record prefetch; max-rate batches above 8K signatures on the
+    # throughput path (--stream-tput-small-max 8192)
+    S="--stream-tput-small-max 8192"
+    bash tools/gpu_job.sh \
+      "parity:900:python -u -m pytest tests/test_gpu_stream_parity.py tests/test_gpu_vtile.py -k 'host or copy_threads' -q -rA --timeout 300 --timeout-method thread" &&
+    run_arms r05_hc3 "$Q --stream-rates 10e6 --stream-paced-seconds 3 --stream-seconds 4 --stream-unrel-seconds 2" \
+      "b0a=" "s0a=$S" "h2sa=--stream-copy-threads 2 $S" "t3h2sa=--stream-tiles 3 --stream-copy-threads 2 $S" \
+      "t3h3sa=--stream-tiles 3 --stream-copy-threads 3 $S" "t4h2sa=--stream-tiles 4 --stream-copy-threads 2 $S" \
+      "t3h2sb=--stream-tiles 3 --stream-copy-threads 2 $S" "h2sb=--stream-copy-threads 2 $S" "b0b="
+    ;;
   *) sed -n '2,8p' "$0"; exit 2 ;;
 esac
