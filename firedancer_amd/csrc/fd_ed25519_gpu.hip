@@ -344,6 +344,9 @@ FD_DEV void sc_mul_5x8( u32 out[ 16 ], u32 const a[ 5 ], u32 const b[ 8 ] ) {
 FD_DEV int hs_prepare( u32 const k[ 8 ], u32 const Sw[ 8 ], u32 c0[ 5 ], u32 c1m[ 5 ], int & c1neg, u32 sp[ 8 ] ) {
   int ng = 0;
   if( !fd_lat_halfsize( c0, c1m, &ng, k ) ) return 0;
+#if defined(FD_PREP_PROBE) && FD_PREP_PROBE == 4     /* timing only (wrong codes): ... up to the lattice reduction */
+  return 0;
+#endif
   c1neg = ng;
   u32 c1lo = ng ? 0u - c1m[0] : c1m[0];
   if( ( c0[0] - c1lo * k[0] ) & 7u ) return 0;                       /* mod 8 */
@@ -555,8 +558,20 @@ FD_DEV void hashh_one( unsigned char const * __restrict__ payload, fdgpu_txn_des
 #pragma unroll
     for( int i=0; i<4; i++ ) { uint4 v = khash[4*(size_t)s + i]; h[4*i] = v.x; h[4*i+1] = v.y; h[4*i+2] = v.z; h[4*i+3] = v.w; }
   } else fd_sha512_RAM( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off );
+#if defined(FD_PREP_PROBE) && FD_PREP_PROBE == 2     /* timing only (wrong codes): the hash role up to SHA-512 */
+  code_out[s] = (i8)( h[0] & 1u ); return;
+#endif
   sc_reduce( k, h );
+#if defined(FD_PREP_PROBE) && FD_PREP_PROBE == 3     /* timing only (wrong codes): ... up to k mod l */
+  code_out[s] = (i8)( k[0] & 1u ); return;
+#endif
   u32 c0[5], c1m[5], sp[8]; int c1neg = 0;
+#if defined(FD_PREP_PROBE) && FD_PREP_PROBE == 4
+  { int ok = hs_prepare( k, Sw, c0, c1m, c1neg, sp ); code_out[s] = (i8)( ok + ( c0[0] & 1u ) ); return; }
+#endif
+#if defined(FD_PREP_PROBE) && FD_PREP_PROBE == 5     /* timing only (wrong codes): ... up to s' (no digits) */
+  { int ok = hs_prepare( k, Sw, c0, c1m, c1neg, sp ); code_out[s] = (i8)( ok + ( sp[0] & 1u ) + ( c0[0] & 1u ) ); return; }
+#endif
   if( !( force_slow && s % force_slow == 0u ) && hs_prepare( k, Sw, c0, c1m, c1neg, sp ) ) {
     hs_store_digits( c0, c1m, c1neg, sp, s, n, digA, digR, digB, htop );
     code_out[s] = FD_ED25519_SUCCESS;

@@ -52,7 +52,8 @@ for it in range(reps):
         r[role] = {"waves": int(len(b)), "mean_us": float(d.mean()), "max_us": float(d.max()),
                    "span_us": float((b[:, 1].max() - t0) / 100.0), "start_spread_us": float((b[:, 0].max() - t0) / 100.0)}
     rows.append(r)
-assert (out_d.cpu().numpy() == expect).all()
+if not os.environ.get("PROBE_NOCHECK"):       # FD_PREP_PROBE=2 / 3 builds stop the hash role early (wrong codes)
+    assert (out_d.cpu().numpy() == expect).all()
 summ = {}
 for role in range(3):
     v = [r[role] for r in rows[2:] if role in r]

@@ -60,11 +60,20 @@ case "$job" in
     # throughput path (--stream-tput-small-max 8192)
     S="--stream-tput-small-max 8192"
     bash tools/gpu_job.sh \
-      "parity:900:python -u -m pytest tests/test_gpu_stream_parity.py tests/test_gpu_vtile.py -k 'host or copy_threads' -q -rA --timeout 300 --timeout-method thread" &&
+      "parity:900:python -u -m pytest tests/test_gpu_stream_parity.py tests/test_gpu_vtile.py -k 'host or copy_threads' -q -rA --timeout 300 --timeout-method thread" \
+      "pp2:120:mkdir -p gpurun_out/r05_pp && PROBE_NOCHECK=1 TXNS=2800 FDGPU_LIB=build/ab/pp2.so python tools/prep_probe.py > gpurun_out/r05_pp/pp2800_sha_only.json" \
+      "pp3:120:PROBE_NOCHECK=1 TXNS=2800 FDGPU_LIB=build/ab/pp3.so python tools/prep_probe.py > gpurun_out/r05_pp/pp2800_to_k.json" &&
     run_arms r05_hc3 "$Q --stream-rates 10e6 --stream-paced-seconds 3 --stream-seconds 4 --stream-unrel-seconds 2" \
       "b0a=" "s0a=$S" "h2sa=--stream-copy-threads 2 $S" "t3h2sa=--stream-tiles 3 --stream-copy-threads 2 $S" \
       "t3h3sa=--stream-tiles 3 --stream-copy-threads 3 $S" "t4h2sa=--stream-tiles 4 --stream-copy-threads 2 $S" \
       "t3h2sb=--stream-tiles 3 --stream-copy-threads 2 $S" "h2sb=--stream-copy-threads 2 $S" "b0b="
+    ;;
+  pp45)
+    # the hash role split further: up to the lattice reduction (pp4), up to s' without the digits (pp5)
+    mkdir -p gpurun_out/r05_pp
+    bash tools/gpu_job.sh \
+      "pp4:120:PROBE_NOCHECK=1 TXNS=2800 FDGPU_LIB=build/ab/pp4.so python tools/prep_probe.py > gpurun_out/r05_pp/pp2800_to_lattice.json" \
+      "pp5:120:PROBE_NOCHECK=1 TXNS=2800 FDGPU_LIB=build/ab/pp5.so python tools/prep_probe.py > gpurun_out/r05_pp/pp2800_to_sprime.json"
     ;;
   *) sed -n '2,8p' "$0"; exit 2 ;;
 esac
