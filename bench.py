@@ -313,7 +313,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 # it takes the throughput path (the latency path's 4-lane walk does twice the work per signature)
                 min_batch=args.stream_tput_min_batch if tput else 0,
                 # max-rate legs: batches above --stream-tput-small-max signatures take the throughput path
-                small_max=args.stream_tput_small_max if tput else 0)
+                small_max=args.stream_tput_small_max if tput else 0,
+                hk_ns=int(args.stream_lat_hk_us * 1000) if paced else 0)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -522,7 +523,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
          "--stream-cu-exclusive", str(args.stream_cu_exclusive), "--stream-lat-launcher", str(args.stream_lat_launcher),
          "--stream-copy-threads", str(args.stream_copy_threads),
          "--stream-tput-min-batch", str(args.stream_tput_min_batch),
-         "--stream-tput-small-max", str(args.stream_tput_small_max)]
+         "--stream-tput-small-max", str(args.stream_tput_small_max), "--stream-lat-hk-us", str(args.stream_lat_hk_us)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -874,6 +875,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-tput-small-max", type=int, default=0,
                     help="max-rate legs: batches of at most this many signatures take the latency path "
                          "(fdgpu_vtile_opts_t.small_max; 0 = the tile's default, half the batch limit)")
+    ap.add_argument("--stream-lat-hk-us", type=float, default=0.0,
+                    help="paced legs: the tile loop's housekeeping (launch decision, copies, verdict poll) at most "
+                         "every this many us while frags flow (0 = the link's 10 us)")
     ap.add_argument("--stream-copy-threads", type=int, default=0, choices=range(0, 9),
                     help="max-rate and unreliable legs: host threads per tile that copy each record into the out dcache "
                          "while the GPU copy only reads it (fdgpu_vtile_opts_t.copy_threads; a core each in the host plan)")

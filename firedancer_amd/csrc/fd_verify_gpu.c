@@ -1890,6 +1890,7 @@ static void * link_tile( void * _a ) {
   ulong per_link = Q > 1UL ? ( 64UL / Q > 8UL ? 64UL / Q : 8UL ) : 64UL;   /* own frags per link per pass */
   ulong pfl = c->pf_dist > 0 ? (ulong)c->pf_dist : 1UL, pfh = pfl > 1UL ? pfl / 2UL : 1UL;   /* prefetch distances */
   ulong t_hk = 0UL, ns_in = 0UL, ns_after = 0UL, ns_hk = 0UL, ns_idle = 0UL, t_begin = now_ns(), cpu0, iv0;
+  ulong const hk_ns = c->hk_ns ? c->hk_ns : 10000UL;
   thread_usage( &cpu0, &iv0 );
   /* FDGPU_LINK_PROF=1: rdtsc section profile (mcache poll, during_frag, prefetch + credit, drain
      after_frags, housekeep after_frags, link_account, credit after a drain, housekeep) */
@@ -1985,7 +1986,7 @@ static void * link_tile( void * _a ) {
     }
     /* housekeeping: launch / drain at most every 10 us while frags flow
        (the HIP runtime calls behind them take locks shared by all tiles) */
-    if( backlog || t1 - t_hk >= 10000UL ) {
+    if( backlog || t1 - t_hk >= hk_ns ) {
       t_hk = t1;
       PROF_T0();
       fdgpu_vtile_housekeep( vt, c->max_inflight );                 /* adaptive batching */

@@ -419,6 +419,8 @@ typedef struct fdgpu_stream_cfg {
   unsigned long min_batch;       /* fdgpu_vtile_opts_t.min_batch of every tile (0: none; the max-rate legs: batches
                                     above the latency path's limit, so they take the throughput path) */
   unsigned long small_max;       /* fdgpu_vtile_opts_t.small_max of every tile (0: its default, half the batch limit) */
+  unsigned long hk_ns;           /* the tile loop's housekeeping (launch decision, copies, verdict poll) at most every
+                                    hk_ns while frags flow (0 = 10 us) */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {

@@ -75,5 +75,12 @@ case "$job" in
       "pp4:120:PROBE_NOCHECK=1 TXNS=2800 FDGPU_LIB=build/ab/pp4.so python tools/prep_probe.py > gpurun_out/r05_pp/pp2800_to_lattice.json" \
       "pp5:120:PROBE_NOCHECK=1 TXNS=2800 FDGPU_LIB=build/ab/pp5.so python tools/prep_probe.py > gpurun_out/r05_pp/pp2800_to_sprime.json"
     ;;
+  hk)
+    # the paced tile's housekeeping interval (launch decision, early copies, verdict poll): 10 (default) / 5 /
+    # 2.5 us, and 2.5 us with the launch thread (its launches then cost the tile a queue push)
+    run_arms r05_hk "$Q --stream-rates 7.5e6,10e6,12.5e6 --stream-paced-seconds 3 --stream-seconds 3 --stream-unrel-seconds 1" \
+      "k10a=" "k2a=--stream-lat-hk-us 2.5" "k5a=--stream-lat-hk-us 5" "k2la=--stream-lat-hk-us 2.5 --stream-lat-launcher 1" \
+      "k2lb=--stream-lat-hk-us 2.5 --stream-lat-launcher 1" "k5b=--stream-lat-hk-us 5" "k2b=--stream-lat-hk-us 2.5" "k10b="
+    ;;
   *) sed -n '2,8p' "$0"; exit 2 ;;
 esac
