@@ -866,9 +866,12 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="every leg: latency-path workgroups alone on their CU (fdgpu_vtile_opts_t.cu_exclusive; "
                          "0 = the tile's default, on; -1 off; A/B: 2 at most two per CU, 3 the walk only, 4 the prep "
                          "only; profiles/r04/p, q)")
-    ap.add_argument("--stream-lat-launcher", type=int, default=0, choices=(0, 1),
+    ap.add_argument("--stream-lat-launcher", type=int, default=1, choices=(0, 1),
                     help="paced legs: each tile's batch launches and copies on a launch thread of its own, a core "
-                         "each (fdgpu_vtile_opts_t.launcher; the host plan drops it when the cores are short)")
+                         "each (fdgpu_vtile_opts_t.launcher; the host plan drops it when the cores are short).  On by "
+                         "default: p99 neutral (profiles/r05/lc, hk), but it takes ~15 ns per frag of runtime calls "
+                         "off the single paced tile, which at 10M frags/s has no other headroom; 1 tile + 1 launch "
+                         "thread + 1 producer is the max-rate legs' 3 cores per GPU")
     ap.add_argument("--stream-tput-min-batch", type=int, default=0,
                     help="max-rate legs: batches wait (up to 2 ms) for at least this many frags (fdgpu_vtile_opts_t."
                          "min_batch; 0 = launch when the GPU has room)")
