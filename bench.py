@@ -314,7 +314,8 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 min_batch=args.stream_tput_min_batch if tput else 0,
                 # max-rate legs: batches above --stream-tput-small-max signatures take the throughput path
                 small_max=args.stream_tput_small_max if tput else 0,
-                hk_ns=int(args.stream_lat_hk_us * 1000) if paced else 0)
+                hk_ns=int(args.stream_lat_hk_us * 1000) if paced else 0,
+                lat_share=args.stream_lat_share)
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
@@ -432,6 +433,92 @@ def _anon_huge_mb() -> float | None:
     return None
 
 
+def _kfd_gpu_ids() -> set[str]:
+    """KFD gpu_ids of the GPUs this process sees (topology nodes with SIMDs)."""
+    ids, base = set(), "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for n in os.listdir(base):
+            try:
+                props = open(f"{base}/{n}/properties").read()
+                gid = open(f"{base}/{n}/gpu_id").read().strip()
+            except OSError:
+                continue
+            if any(l.split()[:2] == ["simd_count", "0"] for l in props.splitlines()) or gid in ("", "0"):
+                continue
+            ids.add(gid)
+    except OSError:
+        pass
+    return ids
+
+
+def kfd_queues() -> dict | None:
+    """The HSA user queues on this process's GPU(s) as KFD lists them (/sys/class/kfd/kfd/proc/<pid>/queues/
+    <q>/gpuid; pids of every process on the node, in the host's pid space): how many, of how many processes,
+    and the milliseconds those processes' queues have spent evicted (stats_<gpuid>/evicted_ms: KFD takes a
+    process's queues off the GPU while it re-validates its memory, e.g. when the kernel invalidates pages of
+    registered host memory).  A GPU maps at most num_cp_queues compute queues (24 on MI355X) at once."""
+    base, gids = "/sys/class/kfd/kfd/proc", _kfd_gpu_ids()
+    try:
+        pids = os.listdir(base)
+    except OSError:
+        return None
+    tot = procs = 0
+    ev = 0.0
+    for p in pids:
+        try:
+            qs = os.listdir(f"{base}/{p}/queues")
+        except OSError:
+            continue
+        n = 0
+        for q in qs:
+            try:
+                g = open(f"{base}/{p}/queues/{q}/gpuid").read().strip()
+            except OSError:
+                continue
+            n += (not gids) or g in gids
+        procs += n > 0
+        tot += n
+        for g in gids:
+            try:
+                ev += float(open(f"{base}/{p}/stats_{g}/evicted_ms").read().split()[0])
+            except (OSError, ValueError, IndexError):
+                pass
+    return {"queues": tot, "procs": procs, "evicted_ms": ev}
+
+
+class KfdSampler:
+    """Samples kfd_queues() every 50 ms on a thread while a leg runs (the tile threads run in C, without the
+    GIL); keeps the largest queue counts seen and the growth of the evicted time over the leg."""
+
+    def __init__(self):
+        import threading
+        self.peak, self._first, self._stop = None, None, threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while True:
+            stopped = self._stop.is_set()          # (one last sample after the leg)
+            q = kfd_queues()
+            if q is None:
+                return
+            if self._first is None:
+                self._first = q
+            self.peak = dict(queues=max(q["queues"], (self.peak or q)["queues"]),
+                             procs=max(q["procs"], (self.peak or q)["procs"]),
+                             evicted_ms=round(q["evicted_ms"] - self._first["evicted_ms"], 3))
+            if stopped:
+                return
+            self._stop.wait(0.05)
+
+    def __enter__(self):
+        self._t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        self._t.join(1.0)
+
+
 def stream_child_main(args) -> None:
     """--stream-child: the configs[4] legs for one process (one GPU); no torch GPU context here.  Process 0
     regenerates the payloads (same seed), creates each leg's link and runs the producer; the others join."""
@@ -470,10 +557,11 @@ def stream_child_main(args) -> None:
             link = vtile.Link(path, create=True, payload=payload, off=desc["payload_off"], sz=desc["payload_sz"], **cfg)
             huge_mb = _anon_huge_mb()
             try:
-                rc = link.run(0, dev, True)
-                if rc:
-                    raise RuntimeError(f"leg {leg}: fdgpu_link_run {rc}")
-                st = link.result(timeout_s=120.0)
+                with KfdSampler() as kq:
+                    rc = link.run(0, dev, True)
+                    if rc:
+                        raise RuntimeError(f"leg {leg}: fdgpu_link_run {rc}")
+                    st = link.result(timeout_s=120.0)
                 anomalies(link, leg)
             finally:
                 link.close()
@@ -482,7 +570,7 @@ def stream_child_main(args) -> None:
             if leg == "cal":
                 cal_fps = st["frags_per_s"]
             else:
-                out[leg] = dict(_leg_summary(st, cfg), anon_huge_mb=huge_mb)
+                out[leg] = dict(_leg_summary(st, cfg), anon_huge_mb=huge_mb, kfd_queues_peak=kq.peak)
         else:
             link = vtile.Link(path, create=False, timeout_s=180.0 if leg == "cal" else 120.0)   # bounded if process 0 failed
             try:
@@ -523,7 +611,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
          "--stream-cu-exclusive", str(args.stream_cu_exclusive), "--stream-lat-launcher", str(args.stream_lat_launcher),
          "--stream-copy-threads", str(args.stream_copy_threads),
          "--stream-tput-min-batch", str(args.stream_tput_min_batch),
-         "--stream-tput-small-max", str(args.stream_tput_small_max), "--stream-lat-hk-us", str(args.stream_lat_hk_us)]
+         "--stream-tput-small-max", str(args.stream_tput_small_max), "--stream-lat-hk-us", str(args.stream_lat_hk_us),
+         "--stream-lat-share", str(args.stream_lat_share)]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -866,6 +955,9 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="every leg: latency-path workgroups alone on their CU (fdgpu_vtile_opts_t.cu_exclusive; "
                          "0 = the tile's default, on; -1 off; A/B: 2 at most two per CU, 3 the walk only, 4 the prep "
                          "only; profiles/r04/p, q)")
+    ap.add_argument("--stream-lat-share", type=int, default=0,
+                    help="every leg: each engine context's exclusive latency-path walk fits 1/n of the CUs left by the "
+                         "gathers (fdgpu_vtile_opts_t.lat_share; 0 = the tile's default, 1/contexts; -1 = no limit, A/B)")
     ap.add_argument("--stream-lat-launcher", type=int, default=1, choices=(0, 1),
                     help="paced legs: each tile's batch launches and copies on a launch thread of its own, a core "
                          "each (fdgpu_vtile_opts_t.launcher; the host plan drops it when the cores are short).  On by "
@@ -939,6 +1031,7 @@ def main():
             dist.broadcast_object_list(obj, src=0)
             token = obj[0]
         res, err = None, None
+        kq0 = kfd_queues()            # the queues already open on the node when the tile processes start
         try:
             res = run_stream_child(args, dev, rank, world, token)
         except Exception as e:      # keep the headline line even if the stream leg fails
@@ -997,7 +1090,8 @@ def main():
                           # that steals it inflates that leg's latency tail; 1.0 = undisturbed)
                           "host_cpu_share_min": min((l.get("host_cpu") or {}).get("tile_share_min", 1.0)
                                                     for l in [mx, ur] + curve),
-                          "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host"}
+                          "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host",
+                          "kfd_queues_before": kq0}
             else:
                 stream = {"error": err or "a stream child failed on another rank"}
 

@@ -2191,6 +2191,7 @@ struct fdgpu_ed25519_ctx {
   unsigned long small_max;       /* batches of at most this many signatures take the latency path */
   int last_path;                 /* the engine path launch_batch chose last (FDGPU_PATH_* or latency lanes) */
   int           excl_mode;       /* fdgpu_ed25519_set_cu_exclusive's mode; -1: off, chosen by fdgpu_debug_opts_t */
+  unsigned long lat_cus;         /* fdgpu_ed25519_set_lat_share: CUs an exclusive walk may count on, 0 = no limit */
   unsigned      excl_lds[ 7 ];   /* fdgpu_ed25519_set_cu_exclusive: dynamic LDS per workgroup of the latency path's
                                     prep<0,1>, prep<0,0>, dsm8, dsm4<0,1>, dsm4<0,0>, dsm2<0,1>, dsm2<0,0> (0 = none) */
   unsigned long nofold_max;      /* fd_dsm_kernel<0> (no carry fold) for batches of at most this many signatures */
@@ -2342,6 +2343,18 @@ fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on ) {
 extern "C" int
 fdgpu_ed25519_get_cu_exclusive( fdgpu_ed25519_ctx_t const * ctx ) { return ctx ? ctx->excl_mode : 0; }
 
+extern "C" int
+fdgpu_ed25519_set_lat_share( fdgpu_ed25519_ctx_t * ctx, unsigned parts ) {
+  if( !ctx ) return -1;
+  if( !parts ) { ctx->lat_cus = 0UL; return 0; }
+  int ncu = 0;
+  HIPCHK( hipSetDevice( ctx->device ), -2 );
+  HIPCHK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, ctx->device ), -2 );
+  unsigned long free_cus = (unsigned long)ncu > ctx->gather_cus ? (unsigned long)ncu - ctx->gather_cus : 1UL;
+  ctx->lat_cus = free_cus / parts ? free_cus / parts : 1UL;
+  return 0;
+}
+
 extern "C" char const * fdgpu_last_error( void ) { return fd_err.c_str(); }
 
 /* the synchronous host calls stage through slot 0: only when the async
@@ -2363,7 +2376,16 @@ static int pick_path( fdgpu_ed25519_ctx_t const * ctx, unsigned long nsig ) {
        against 0.92 on the throughput path and 1.08 with two lanes, tools/configs0_ab.py) */
     int lanes = ctx->dsm_lanes ? ctx->dsm_lanes : ( nsig <= FD_DSM8_MAX && ctx->half ? 8 : nsig <= FD_DSM4_MAX ? 4 :
                                                     nsig <= FD_DSM2_MAX ? 2 : 1 );
-    return lanes == 8 && !ctx->half ? 4 : lanes;     /* the term split needs the half-size walk */
+    if( lanes == 8 && !ctx->half ) lanes = 4;        /* the term split needs the half-size walk */
+    /* an exclusive walk (one workgroup of 256 lanes per CU, two in mode 2) within the context's CU budget:
+       fewer lanes per signature, fewer workgroups (fdgpu_ed25519_set_lat_share) */
+    int excl_walk = ctx->excl_mode == 1 || ctx->excl_mode == 2 || ctx->excl_mode == 3;
+    if( !ctx->dsm_lanes && ctx->lat_cus && excl_walk ) {
+      unsigned long budget = ctx->lat_cus * ( ctx->excl_mode == 2 ? 2UL : 1UL );
+      unsigned long wg = ( nsig + FD_WG - 1UL ) / FD_WG;                 /* workgroups per lane of a signature */
+      while( lanes > 1 && (unsigned long)lanes * wg > budget ) lanes >>= 1;
+    }
+    return lanes;
   }
   return ctx->half ? FDGPU_PATH_THROUGHPUT : FDGPU_PATH_THROUGHPUT_FULL;
 }

@@ -559,6 +559,13 @@ vt_ctx_new( fdgpu_vtile_t const * vt, int k ) {
        mode for new contexts, which the tile then keeps (the tile tests' latency8 / latency8x paths) */
     int excl = vt->opt.cu_exclusive ? vt->opt.cu_exclusive : ( fdgpu_ed25519_get_cu_exclusive( c ) ? 0 : 1 );
     if( excl > 0 && fdgpu_ed25519_set_cu_exclusive( c, excl ) ) { fdgpu_ed25519_ctx_delete( c ); return NULL; }
+    /* each context's exclusive walk within its share of the CUs (the contexts' batches overlap; with cu_split
+       the share is the context's own part): a walk wider than its share would wait on the other context's
+       workgroups and hold the gathers queued behind it (profiles/r05/cb) */
+    unsigned share = vt->opt.lat_share > 0 ? (unsigned)vt->opt.lat_share : vt->opt.lat_share < 0 ? 0u : (unsigned)vt->nctx;
+    if( excl > 0 && fdgpu_ed25519_set_lat_share( c, share ) ) {
+      fdgpu_ed25519_ctx_delete( c ); return NULL;
+    }
     fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
     /* every staging buffer and the gather stream now: batches then allocate nothing (the tile's sandbox
        allows no allocation it does not need, fd_verify_gpu_tile.seccomppolicy) */
@@ -1856,7 +1863,7 @@ static void * link_tile( void * _a ) {
   vo.max_uncopied = c->max_uncopied; vo.cu_split = c->cu_split; vo.cu_exclusive = c->cu_exclusive;
   vo.launcher = c->launcher; vo.launcher_core = c->launcher && a->lcpu >= 0 ? a->lcpu + 1 : 0;
   vo.copy_threads = c->zero_copy ? c->copy_threads : 0;
-  vo.min_batch = c->min_batch; vo.small_max = c->small_max;
+  vo.min_batch = c->min_batch; vo.small_max = c->small_max; vo.lat_share = c->lat_share;
   for( int i=0; i<vo.copy_threads && i<FDGPU_VTILE_COPY_THREADS_MAX; i++ ) vo.copy_cores[i] = a->ccpu[i] >= 0 ? a->ccpu[i] + 1 : 0;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
                                              ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );

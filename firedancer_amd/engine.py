@@ -48,7 +48,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_host_alloc", "fdgpu_host_free", "fdgpu_host_register", "fdgpu_host_unregister", "fdgpu_device_numa_node",
            "fdgpu_ed25519_submit_raw_gather", "fdgpu_ed25519_submit_raw_gather_chk", "fdgpu_ed25519_gather",
            "fdgpu_ed25519_gathered", "fdgpu_ed25519_gather_launched", "fdgpu_ed25519_gather_wait", "fdgpu_host_dev_ptr", "fdgpu_host_register_shared",
-           "fdgpu_ed25519_reserve_gather_cus", "fdgpu_ed25519_reserve_cus", "fdgpu_ed25519_set_cu_exclusive", "fdgpu_ed25519_get_cu_exclusive", "fdgpu_ed25519_gather_stats", "fdgpu_ed25519_phase_stats", "fdgpu_ed25519_prepare", "fdgpu_ed25519_submit_raw_gather_dev", "fdgpu_host_region",
+           "fdgpu_ed25519_reserve_gather_cus", "fdgpu_ed25519_reserve_cus", "fdgpu_ed25519_set_cu_exclusive", "fdgpu_ed25519_get_cu_exclusive", "fdgpu_ed25519_set_lat_share", "fdgpu_ed25519_gather_stats", "fdgpu_ed25519_phase_stats", "fdgpu_ed25519_prepare", "fdgpu_ed25519_submit_raw_gather_dev", "fdgpu_host_region",
            "fdgpu_ed25519_dropin_init", "fdgpu_debug_set_opts",
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_slow_count", "fdgpu_ed25519_set_dedup",
@@ -130,6 +130,13 @@ def load_library():
         L.fdgpu_ed25519_set_record_fp_off.restype = ctypes.c_int
         L.fdgpu_ed25519_set_record_fp_off.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.fdgpu_ed25519_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.fdgpu_ed25519_set_cu_exclusive.restype = ctypes.c_int
+        L.fdgpu_ed25519_set_cu_exclusive.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.fdgpu_ed25519_set_lat_share.restype = ctypes.c_int
+        L.fdgpu_ed25519_set_lat_share.argtypes = [ctypes.c_void_p, ctypes.c_uint]
+        L.fdgpu_ed25519_front_batch.restype = ctypes.c_int
+        L.fdgpu_ed25519_front_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulong),
+                                                ctypes.POINTER(ctypes.c_ulong), ctypes.POINTER(ctypes.c_int)]
         L.fdgpu_ed25519_set_small_batch_max.restype = ctypes.c_ulong
         L.fdgpu_ed25519_set_small_batch_max.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
         L.fdgpu_ed25519_kernel_ms.restype = ctypes.c_float
@@ -308,6 +315,23 @@ class Engine:
     def set_small_batch_max(self, n: int) -> int:
         """Signatures per batch at or below which the latency path runs (0: never, 2**64-1: always)."""
         return int(self.L.fdgpu_ed25519_set_small_batch_max(self.ctx, ctypes.c_ulong(n)))
+
+    def set_cu_exclusive(self, mode: int) -> None:
+        """Latency-path workgroups alone on their CU (fdgpu_ed25519_set_cu_exclusive; 0 off)."""
+        if self.L.fdgpu_ed25519_set_cu_exclusive(self.ctx, mode):
+            raise RuntimeError(f"fdgpu_ed25519_set_cu_exclusive: {last_error()}")
+
+    def set_lat_share(self, parts: int) -> None:
+        """The exclusive walk within 1/parts of the CUs (fdgpu_ed25519_set_lat_share; 0 no limit)."""
+        if self.L.fdgpu_ed25519_set_lat_share(self.ctx, parts):
+            raise RuntimeError(f"fdgpu_ed25519_set_lat_share: {last_error()}")
+
+    def front_batch(self) -> tuple[int, int, int] | None:
+        """The oldest launched async batch: (txns, cursor, engine path), None if none is in flight."""
+        t, c, p = ctypes.c_ulong(), ctypes.c_ulong(), ctypes.c_int()
+        if not self.L.fdgpu_ed25519_front_batch(self.ctx, ctypes.byref(t), ctypes.byref(c), ctypes.byref(p)):
+            return None
+        return t.value, c.value, p.value
 
     def set_timing(self, on: bool = True):
         self.L.fdgpu_ed25519_set_timing(self.ctx, 1 if on else 0)

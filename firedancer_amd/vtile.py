@@ -77,7 +77,8 @@ class VTileOpts(ctypes.Structure):
                 ("min_batch", ctypes.c_ulong), ("max_wait_ns", ctypes.c_ulong), ("copy_wait_ns", ctypes.c_ulong),
                 ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint), ("max_uncopied", ctypes.c_ulong),
                 ("cu_split", ctypes.c_int), ("cu_exclusive", ctypes.c_int), ("launcher", ctypes.c_int),
-                ("launcher_core", ctypes.c_int), ("copy_threads", ctypes.c_int), ("copy_cores", ctypes.c_int * 8)]
+                ("launcher_core", ctypes.c_int), ("copy_threads", ctypes.c_int), ("copy_cores", ctypes.c_int * 8),
+                ("lat_share", ctypes.c_int)]
 
 
 class StreamCfg(ctypes.Structure):
@@ -89,7 +90,7 @@ class StreamCfg(ctypes.Structure):
                 ("max_uncopied", ctypes.c_ulong), ("pf_dist", ctypes.c_int), ("cu_split", ctypes.c_int),
                 ("cu_exclusive", ctypes.c_int), ("no_huge_pages", ctypes.c_int), ("launcher", ctypes.c_int),
                 ("copy_threads", ctypes.c_int), ("min_batch", ctypes.c_ulong), ("small_max", ctypes.c_ulong),
-                ("hk_ns", ctypes.c_ulong)]
+                ("hk_ns", ctypes.c_ulong), ("lat_share", ctypes.c_int)]
 
 
 class StreamStats(ctypes.Structure):
@@ -414,13 +415,13 @@ def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
 
 def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers=1, nctx=0, prof=0,
          out_mult=0, copy_wait_ns=0, copy_min=0, gather_cus=0, max_uncopied=0, pf_dist=0, no_huge_pages=0, cu_split=0, cu_exclusive=0,
-         launcher=0, copy_threads=0, min_batch=0, small_max=0, hk_ns=0) -> StreamCfg:
+         launcher=0, copy_threads=0, min_batch=0, small_max=0, hk_ns=0, lat_share=0) -> StreamCfg:
     return StreamCfg(n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
                      gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0, producers=producers,
                      nctx=nctx, prof=prof, out_mult=out_mult, copy_wait_ns=copy_wait_ns, copy_min=copy_min,
                      gather_cus=gather_cus, max_uncopied=max_uncopied, pf_dist=pf_dist, no_huge_pages=no_huge_pages, cu_split=cu_split,
                      cu_exclusive=cu_exclusive, launcher=launcher, copy_threads=copy_threads, min_batch=min_batch,
-                     small_max=small_max, hk_ns=hk_ns)
+                     small_max=small_max, hk_ns=hk_ns, lat_share=lat_share)
 
 
 def stream_run(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,

@@ -635,6 +635,18 @@ fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on );
 int
 fdgpu_ed25519_get_cu_exclusive( fdgpu_ed25519_ctx_t const * ctx );
 
+/* ctx's share of the CUs for its exclusive latency-path walk: with n > 0
+   the walk counts on (CUs - ctx's reserved gather CUs) / n of them; 0 (the
+   default): no limit.  With cu_exclusive on, a walk of more workgroups
+   than CUs free waits for CUs to drain, and the dispatcher holding its
+   tail holds the kernels queued behind it -- another context's walk,
+   gathers -- so a backlog grows batches and feeds itself.  Within a
+   share the latency path takes the most lanes per signature (8, 4, 2, 1)
+   whose walk fits: a tile with n contexts gives each 1/n.  After
+   fdgpu_ed25519_reserve_cus.  0 on success, -1 bad ctx, -2 HIP error. */
+int
+fdgpu_ed25519_set_lat_share( fdgpu_ed25519_ctx_t * ctx, unsigned parts );
+
 /* Per-kernel timing, in milliseconds: the mean over the batches launched
    since fdgpu_ed25519_set_timing(ctx,1) (at most the last 64) of HIP
    events recorded on the stream the kernels ran on.  idx: 0 = prep

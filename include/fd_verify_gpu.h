@@ -230,6 +230,9 @@ typedef struct fdgpu_vtile_opts {
                                     reference's during_frag does, fd_verify_tile.c:96-101), re-checking each frag's
                                     mcache line after the copy, and the GPU only reads them */
   int           copy_cores[ 8 ]; /* with copy_threads: 1 + the CPU copy thread i is pinned to (0: not pinned) */
+  int           lat_share;       /* with cu_exclusive: each context's latency-path walk fits 1/lat_share of the CUs
+                                    left by the gathers (fdgpu_ed25519_set_lat_share): 0 = default (1/nctx);
+                                    -1 = no limit (a walk may be wider than its share: A/B only) */
 } fdgpu_vtile_opts_t;
 #define FDGPU_VTILE_COPY_THREADS_MAX 8
 
@@ -421,6 +424,7 @@ typedef struct fdgpu_stream_cfg {
   unsigned long small_max;       /* fdgpu_vtile_opts_t.small_max of every tile (0: its default, half the batch limit) */
   unsigned long hk_ns;           /* the tile loop's housekeeping (launch decision, copies, verdict poll) at most every
                                     hk_ns while frags flow (0 = 10 us) */
+  int           lat_share;       /* fdgpu_vtile_opts_t.lat_share of every tile */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {

@@ -24,6 +24,14 @@ run_arms() {
 }
 
 case "$job" in
+  cb)
+    # the exclusive walk within each context's CU share (fdgpu_ed25519_set_lat_share, --stream-lat-share): its
+    # tests, the paced tile / stream parity tests, then interleaved paced-only arms, share 1/2 (default) vs none
+    bash tools/gpu_job.sh \
+      "tests:900:python -u -m pytest tests/test_gpu_lat_share.py tests/test_gpu_stream_parity.py tests/test_gpu_vtile.py -k 'lat_share or paced or multictx or cu_split or vs_model' -q -rA --timeout 300 --timeout-method thread" &&
+    run_arms r05_cb "$Q --stream-only-paced --stream-rates 2e6,5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
+      "s0a=" "s1a=--stream-lat-share -1" "s0b=" "s1b=--stream-lat-share -1" "s0c=" "s1c=--stream-lat-share -1"
+    ;;
   pp)
     d="gpurun_out/r05_pp"; mkdir -p "$d"
     bash tools/gpu_job.sh \
