@@ -313,7 +313,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
                 # it takes the throughput path (the latency path's 4-lane walk does twice the work per signature)
                 min_batch=args.stream_tput_min_batch if tput else 0,
                 # max-rate legs: batches above --stream-tput-small-max signatures take the throughput path
-                small_max=args.stream_tput_small_max if tput else 0,
+                small_max=args.stream_tput_small_max if tput else args.stream_lat_small_max if paced else 0,
                 hk_ns=int(args.stream_lat_hk_us * 1000) if paced else 0,
                 lat_share=args.stream_lat_share)
     if leg == "cal":
@@ -418,7 +418,8 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
                           if cfg.get("copy_threads") else None),
             # the tiles' launch threads (cfg launcher): commands, their ns per frag, deepest queue, full-queue waits
             "launcher": ({"commands": st["launcher"][0], "busy_ns_per_frag": round(st["launcher"][1] / n, 1),
-                          "depth_max": st["launcher"][2], "full_waits": st["launcher"][3]}
+                          "depth_max": st["launcher"][2], "full_waits": st["launcher"][3],
+                          "cmd_max_us": round(st["launcher"][4] * 1e-3, 1), "cmds_over_250us": st["launcher"][5]}
                          if cfg.get("launcher") else None)}
 
 
@@ -612,6 +613,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
          "--stream-copy-threads", str(args.stream_copy_threads),
          "--stream-tput-min-batch", str(args.stream_tput_min_batch),
          "--stream-tput-small-max", str(args.stream_tput_small_max), "--stream-lat-hk-us", str(args.stream_lat_hk_us),
+         "--stream-lat-small-max", str(args.stream_lat_small_max),
          "--stream-lat-share", str(args.stream_lat_share)]
     if args.stream_copy:
         cmd.append("--stream-copy")
@@ -970,6 +972,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-tput-small-max", type=int, default=0,
                     help="max-rate legs: batches of at most this many signatures take the latency path "
                          "(fdgpu_vtile_opts_t.small_max; 0 = the tile's default, half the batch limit)")
+    ap.add_argument("--stream-lat-small-max", type=int, default=0,
+                    help="paced legs: batches of at most this many signatures take the latency path (fdgpu_vtile_opts_t."
+                         "small_max; 0 = the tile's default, half the batch limit)")
     ap.add_argument("--stream-lat-hk-us", type=float, default=2.5,
                     help="paced legs: the tile loop's housekeeping (launch decision, copies, verdict poll) at most "
                          "every this many us while frags flow (0 = the link's 10 us; 2.5: verdicts seen ~5 us "

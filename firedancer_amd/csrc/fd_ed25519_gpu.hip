@@ -3263,6 +3263,7 @@ struct fdgpu_launcher {
   int                        device, cpu;
   std::thread                th;
   unsigned long              n_cmd, busy_ns, depth_max;   /* launch thread's */
+  unsigned long              max_ns, n_slow;              /* ... longest command, commands over 250 us */
   unsigned long              full_waits;                  /* queueing thread's */
 };
 
@@ -3291,7 +3292,10 @@ static void launcher_main( fdgpu_launcher_t * L ) {
         __atomic_store_n( &c.ctx->fault, 1, __ATOMIC_RELEASE );
       }
     }
-    L->busy_ns += fd_now_ns() - t0; L->n_cmd++;
+    unsigned long dt = fd_now_ns() - t0;
+    L->busy_ns += dt; L->n_cmd++;
+    if( dt > L->max_ns ) L->max_ns = dt;
+    L->n_slow += dt > 250000UL;
     L->head.store( h + 1, std::memory_order_release );
   }
 }
@@ -3315,7 +3319,7 @@ static void launcher_drain( fdgpu_launcher_t * L ) {
 extern "C" fdgpu_launcher_t *
 fdgpu_launcher_new( int device, int cpu ) {
   fdgpu_launcher_t * L = new fdgpu_launcher_t();
-  L->device = device; L->cpu = cpu; L->n_cmd = L->busy_ns = L->depth_max = L->full_waits = 0UL;
+  L->device = device; L->cpu = cpu; L->n_cmd = L->busy_ns = L->depth_max = L->full_waits = L->max_ns = L->n_slow = 0UL;
   try { L->th = std::thread( launcher_main, L ); }
   catch( ... ) { delete L; fd_err = "fdgpu_launcher_new: no thread"; return NULL; }
   return L;
@@ -3331,8 +3335,9 @@ fdgpu_launcher_delete( fdgpu_launcher_t * L ) {
 }
 
 extern "C" void
-fdgpu_launcher_stats( fdgpu_launcher_t const * L, unsigned long out[ 4 ] ) {
-  out[0] = L->n_cmd; out[1] = L->busy_ns; out[2] = L->depth_max; out[3] = L->full_waits;
+fdgpu_launcher_stats( fdgpu_launcher_t const * L, unsigned long out[ 6 ] ) {
+  out[0] = L->n_cmd; out[1] = L->busy_ns; out[2] = L->depth_max; out[3] = L->full_waits; out[4] = L->max_ns;
+  out[5] = L->n_slow;
 }
 
 extern "C" int

@@ -2123,7 +2123,9 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     }
     st->copy_backlog += r->gm.copy_backlog;
     st->launcher[0] += r->gm.launcher[0]; st->launcher[1] += r->gm.launcher[1]; st->launcher[3] += r->gm.launcher[3];
+    st->launcher[5] += r->gm.launcher[5];
     if( r->gm.launcher[2] > st->launcher[2] ) st->launcher[2] = r->gm.launcher[2];
+    if( r->gm.launcher[4] > st->launcher[4] ) st->launcher[4] = r->gm.launcher[4];
     for( int k=0; k<4; k++ ) st->host_copy[k] += r->gm.host_copy[k];
     st->tile_idle_ns += r->ns_idle;
     st->tile_cpu_ns += r->cpu_ns; st->tile_wall_ns += r->wall_ns; st->tile_nivcsw += r->nivcsw;

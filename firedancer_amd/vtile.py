@@ -63,7 +63,7 @@ class GpuMetrics(ctypes.Structure):
                 ("launch_ns", ctypes.c_ulong), ("copies", ctypes.c_ulong), ("copy_lat_n", ctypes.c_ulong),
                 ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong),
                 ("gather_gpu", ctypes.c_ulong * 5), ("phase", ctypes.c_ulong * 9), ("copy_backlog", ctypes.c_ulong),
-                ("launcher", ctypes.c_ulong * 4), ("host_copy", ctypes.c_ulong * 4)]
+                ("launcher", ctypes.c_ulong * 6), ("host_copy", ctypes.c_ulong * 4)]
 
     def as_dict(self) -> dict:
         return {k: (list(getattr(self, k)) if k in ("lat_hist", "gather_gpu", "phase", "launcher", "host_copy")
@@ -109,7 +109,7 @@ class StreamStats(ctypes.Structure):
                 ("tile_cpu_ns", ctypes.c_ulong), ("tile_wall_ns", ctypes.c_ulong), ("tile_nivcsw", ctypes.c_ulong),
                 ("tile_cpu_share_min", ctypes.c_double), ("tile_cpu", ctypes.c_long * 8),
                 ("prod_cpu_ns", ctypes.c_ulong), ("prod_wall_ns", ctypes.c_ulong), ("prod_nivcsw", ctypes.c_ulong),
-                ("launcher", ctypes.c_ulong * 4), ("host_copy", ctypes.c_ulong * 4)]
+                ("launcher", ctypes.c_ulong * 6), ("host_copy", ctypes.c_ulong * 4)]
 
     def as_dict(self) -> dict:
         out = {}

@@ -350,11 +350,11 @@ fdgpu_ed25519_launch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * lau
    detach) needs a context with nothing pending; a context is deleted before its launcher.  Commands are
    queued by one thread at a time: the contexts of one launcher belong to one caller thread (a verify
    tile).  Stats: commands issued, ns spent issuing them, the deepest queue seen, pushes that waited for
-   room. */
+   room, the longest single command (ns: a runtime call that blocked) and how many took over 250 us. */
 typedef struct fdgpu_launcher fdgpu_launcher_t;
 fdgpu_launcher_t * fdgpu_launcher_new( int device, int cpu );
 void               fdgpu_launcher_delete( fdgpu_launcher_t * launcher );
-void               fdgpu_launcher_stats( fdgpu_launcher_t const * launcher, unsigned long out[ 4 ] );
+void               fdgpu_launcher_stats( fdgpu_launcher_t const * launcher, unsigned long out[ 6 ] );
 int                fdgpu_ed25519_set_launcher( fdgpu_ed25519_ctx_t * ctx, fdgpu_launcher_t * launcher );
 
 /* 1 once a batch of ctx has failed on the device (poll then returns 0

@@ -178,8 +178,9 @@ typedef struct fdgpu_vtile_gpu_metrics {
                                      start -> end sum / max, ns) */
   unsigned long phase[ 9 ];       /* fdgpu_ed25519_phase_stats summed over the tile's contexts (maxima: max) */
   unsigned long copy_backlog;     /* during_frag calls refused with FDGPU_VTILE_COPY_BACKLOG */
-  unsigned long launcher[ 4 ];    /* the tile's launch thread (opts.launcher), fdgpu_launcher_stats: commands issued,
-                                     ns issuing them, deepest queue, pushes that waited for room (0s without one) */
+  unsigned long launcher[ 6 ];    /* the tile's launch thread (opts.launcher), fdgpu_launcher_stats: commands issued,
+                                     ns issuing them, deepest queue, pushes that waited for room, longest command (ns),
+                                     commands over 250 us (0s without one) */
   unsigned long host_copy[ 4 ];   /* the tile's copy threads (opts.copy_threads): records copied, ns copying (summed over
                                      threads), records found overrun after their copy, ns the tile waited for a copy */
 } fdgpu_vtile_gpu_metrics_t;
@@ -461,8 +462,9 @@ typedef struct fdgpu_stream_stats {
   double        tile_cpu_share_min;                       /* the lowest tile's cpu_ns / wall_ns */
   long          tile_cpu[ 8 ];                            /* the CPUs tiles 0..7 were pinned to (-1: none) */
   unsigned long prod_cpu_ns, prod_wall_ns, prod_nivcsw;   /* summed over producers */
-  unsigned long launcher[ 4 ];   /* the tiles' launch threads (cfg.launcher): commands and ns issuing them (summed),
-                                    deepest queue (max), pushes that waited for room (summed) */
+  unsigned long launcher[ 6 ];   /* the tiles' launch threads (cfg.launcher): commands and ns issuing them (summed),
+                                    deepest queue (max), pushes that waited for room (summed), longest command (max),
+                                    commands over 250 us (summed) */
   unsigned long host_copy[ 4 ];  /* the tiles' copy threads (cfg.copy_threads), fdgpu_vtile_gpu_metrics_t.host_copy summed */
 } fdgpu_stream_stats_t;
 

@@ -14,9 +14,12 @@ NCU = 256      # MI355X; the expectations below assume no CUs reserved for gathe
 
 @pytest.mark.parametrize("n,share,lanes", [(3000, 2, 8), (5000, 2, 4), (5000, 0, 8), (9000, 2, 2), (9000, 4, 1),
                                            (20000, 2, 1), (20000, 0, 2)])
-def test_lat_share_lanes(n, share, lanes):
+def test_lat_share_lanes(n, share, lanes, engine_path):
     import torch
-    from firedancer_amd import Engine, synth
+    from firedancer_amd import Engine, engine, synth
+    if engine_path != "throughput":
+        pytest.skip("sets its own path: runs once")
+    engine.debug_reset_opts()                          # the product's defaults (no forced lanes)
     if torch.cuda.get_device_properties(0).multi_processor_count != NCU:
         pytest.skip("expectations assume 256 CUs")
     payload, desc, expect, nsig = synth.make_batch(n, synth.LARGE_NOOP, 1, 0.1, seed=77 + n)

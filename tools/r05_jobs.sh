@@ -24,6 +24,20 @@ run_arms() {
 }
 
 case "$job" in
+  lq)
+    # the launch thread's longest runtime call per paced leg (default settings), four paced-only runs
+    run_arms r05_lq "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
+      "q1=" "m1=--stream-lat-small-max 8192" "q2=" "m2=--stream-lat-small-max 8192" "q3=" "m3=--stream-lat-small-max 8192" \
+      "q4=" "m4=--stream-lat-small-max 8192"
+    ;;
+  cb2)
+    # more interleaved pairs of the cb arms (share 1/2 vs none), after the share's own test
+    bash tools/gpu_job.sh \
+      "tests:300:python -u -m pytest tests/test_gpu_lat_share.py -q -rA --timeout 300 --timeout-method thread" &&
+    run_arms r05_cb2 "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
+      "s1d=--stream-lat-share -1" "s0d=" "s1e=--stream-lat-share -1" "s0e=" "s1f=--stream-lat-share -1" "s0f=" \
+      "s1g=--stream-lat-share -1" "s0g="
+    ;;
   cb)
     # the exclusive walk within each context's CU share (fdgpu_ed25519_set_lat_share, --stream-lat-share): its
     # tests, the paced tile / stream parity tests, then interleaved paced-only arms, share 1/2 (default) vs none
