@@ -385,7 +385,10 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
                            "launch_to_start_mean_us": st["gather_gpu"][1] / max(st["gather_gpu"][0], 1) * 1e-3,
                            "launch_to_start_max_us": st["gather_gpu"][2] * 1e-3,
                            "run_mean_us": st["gather_gpu"][3] / max(st["gather_gpu"][0], 1) * 1e-3,
-                           "run_max_us": st["gather_gpu"][4] * 1e-3},
+                           "run_max_us": st["gather_gpu"][4] * 1e-3,
+                           # the runtime call that issued it (the launch thread's, after its queue) -> start
+                           "issue_to_start_mean_us": st["gather_gpu"][5] / max(st["gather_gpu"][0], 1) * 1e-3,
+                           "issue_to_start_max_us": st["gather_gpu"][6] * 1e-3},
             # each batch's GPU time split (fdgpu_ed25519_phase_stats): launch -> its verify kernels start (its
             # gathers and the stream's earlier batch), kernels, end -> the tile saw it; launch -> last gather end
             "batch_phases_us": _phases(st["phase"]),

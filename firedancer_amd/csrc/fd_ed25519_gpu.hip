@@ -2228,11 +2228,13 @@ struct fdgpu_ed25519_ctx {
   enum { NGT = 64 };
   unsigned long * h_gtime;       /*   pinned [NGT][2]: GPU clock (100 MHz ticks) at a gather's start / end */
   unsigned long * d_gtime;
-  struct { unsigned long target, t_launch; } gt[ NGT ];   /* host side of those gathers: count they end at, launch ns */
+  struct { unsigned long target, t_launch, t_issue; } gt[ NGT ];   /* host side of those gathers: count they end at,
+                                                                       queued ns, issued ns (the runtime call) */
   unsigned long   gt_head, gt_tail;
   double          gclk_off_ns;   /*   GPU clock ns - host CLOCK_MONOTONIC ns (calibrated once) */
   int             gclk_ok;
   unsigned long   gs_n, gs_start_sum, gs_start_max, gs_run_sum, gs_run_max;   /* fdgpu_ed25519_gather_stats */
+  unsigned long   gs_issue_sum, gs_issue_max;
   long            last_gt;       /*   gt[] entry of the last gather launched (-1: untimed) */
   unsigned long * h_stamp;       /*   pinned [NSLOT][2] + 1: per slot the GPU clock when its verify kernels start
                                       (fd_stamp_kernel) and end (fd_done_kernel); [2 NSLOT]: clock calibration */
@@ -3165,6 +3167,11 @@ static void gather_times( fdgpu_ed25519_ctx_t * ctx, unsigned long gathered ) {
     if( ctx->gclk_ok && w[0] && w[1] >= w[0] ) {
       double st = (double)w[0] * 10.0 - ctx->gclk_off_ns - (double)ctx->gt[i].t_launch;
       unsigned long sd = st > 0. ? (unsigned long)st : 0UL, rn = ( w[1] - w[0] ) * 10UL;
+      unsigned long ti = __atomic_load_n( &ctx->gt[i].t_issue, __ATOMIC_ACQUIRE );
+      double si = ti ? (double)w[0] * 10.0 - ctx->gclk_off_ns - (double)ti : 0.;
+      unsigned long sdi = si > 0. ? (unsigned long)si : 0UL;
+      ctx->gs_issue_sum += sdi;
+      if( sdi > ctx->gs_issue_max ) ctx->gs_issue_max = sdi;
       ctx->gs_n++; ctx->gs_start_sum += sd; ctx->gs_run_sum += rn;
       if( sd > ctx->gs_start_max ) ctx->gs_start_max = sd;
       if( rn > ctx->gs_run_max ) ctx->gs_run_max = rn;
@@ -3201,6 +3208,7 @@ struct fd_gargs {
   unsigned char *          ovr;
   unsigned long            target;
   unsigned long *          gt;
+  long                     gti;      /* its timing-ring entry (the issue time goes there), -1: untimed */
 };
 
 /* the gather of slot sl's records not yet gathered: 0 if none, else how many (a filled) or < 0 */
@@ -3216,19 +3224,21 @@ static long gather_prep( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl, fd_gargs * a )
     unsigned long i = ctx->gt_tail % fdgpu_ed25519_ctx_t::NGT;
     ctx->h_gtime[ 2*i ] = 0UL; ctx->h_gtime[ 2*i + 1 ] = 0UL;
     ctx->gt[i].target = target; ctx->gt[i].t_launch = fd_now_ns();
+    __atomic_store_n( &ctx->gt[i].t_issue, 0UL, __ATOMIC_RELAXED );
     ctx->gt_tail++;
     gt = ctx->d_gtime + 2*i;
     ctx->last_gt = (long)i;
   } else { gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT; ctx->last_gt = -1; }   /* untimed: a scratch entry */
   a->g = sl.g_dev + sl.gathered; a->n = (u32)n; a->d_payload = sl.d_payload;
   a->wb = ctx->gather_nowb == 0 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL;
-  a->ovr = sl.d_ovr + sl.gathered; a->target = target; a->gt = gt;
+  a->ovr = sl.d_ovr + sl.gathered; a->target = target; a->gt = gt; a->gti = ctx->last_gt;
   ctx->g_launched = target; sl.gathered = sl.txn_cnt;
   return (long)n;
 }
 
 static int gather_issue( fdgpu_ed25519_ctx_t * ctx, fd_gargs const * a ) {
   unsigned long rpb = ctx->gather_rpb == 1 ? 1UL : 4UL;
+  if( a->gti >= 0 ) __atomic_store_n( &ctx->gt[ a->gti ].t_issue, fd_now_ns(), __ATOMIC_RELEASE );
   hipLaunchKernelGGL( ( rpb == 1UL ? fd_gather_kernel<1> : fd_gather_kernel<4> ), dim3( (unsigned)( ( a->n + rpb - 1UL ) / rpb ) ),
                       dim3( 64UL * rpb ), 0, ctx->gstream, a->g, a->n, a->d_payload, a->wb, a->ovr, ctx->d_gcnt,
                       (unsigned long *)( ctx->d_flag + fdgpu_ed25519_ctx_t::NSLOT + 1 ), a->target, a->gt );
@@ -3862,9 +3872,10 @@ extern "C" unsigned long
 fdgpu_ed25519_gather_launched( fdgpu_ed25519_ctx_t const * ctx ) { return ctx->g_launched; }
 
 extern "C" void
-fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 5 ] ) {
+fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 7 ] ) {
   gather_times( ctx, fdgpu_ed25519_gathered( ctx ) );
   out[0] = ctx->gs_n; out[1] = ctx->gs_start_sum; out[2] = ctx->gs_start_max; out[3] = ctx->gs_run_sum; out[4] = ctx->gs_run_max;
+  out[5] = ctx->gs_issue_sum; out[6] = ctx->gs_issue_max;
 }
 
 extern "C" int

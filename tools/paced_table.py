@@ -14,5 +14,6 @@ for d in sys.argv[1:]:
             r = float(k.split("@")[1])
             ok = ok and v["p99_us"] <= 1000.0 and v["lost"] == 0
             knee = r if ok else knee
-            row.append(f"{r / 1e6:g}M {v['p99_us'] / 1e3:.3f} b{v['mean_batch_txns']:.0f} g{v['gather_gpu']['launch_to_start_max_us']:.0f}")
+            row.append(f"{r / 1e6:g}M {v['p99_us'] / 1e3:.3f} b{v['mean_batch_txns']:.0f} g{v['gather_gpu']['launch_to_start_max_us']:.0f}"
+                       + (f"/i{v['gather_gpu']['issue_to_start_max_us']:.0f}" if 'issue_to_start_max_us' in v['gather_gpu'] else ""))
         print(f"{f.split('/')[-1]:10s} knee {knee / 1e6:g}M | " + " | ".join(row))

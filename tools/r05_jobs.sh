@@ -24,11 +24,18 @@ run_arms() {
 }
 
 case "$job" in
+  lq2)
+    # gather delays split at the runtime call (issue -> start on the GPU vs the launch thread's queue): default
+    # paced arms and arms without the launch thread
+    run_arms r05_lq2 "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
+      "q1=" "n1=--stream-lat-launcher 0" "q2=" "n2=--stream-lat-launcher 0" "q3=" "n3=--stream-lat-launcher 0"
+    ;;
   lq)
-    # the launch thread's longest runtime call per paced leg (default settings), four paced-only runs
+    # the launch thread's longest runtime call per paced leg; paced arms: default, latency path up to the batch
+    # limit (8192), three engine contexts per tile (each walk within 1/3 of the CUs), both
     run_arms r05_lq "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
-      "q1=" "m1=--stream-lat-small-max 8192" "q2=" "m2=--stream-lat-small-max 8192" "q3=" "m3=--stream-lat-small-max 8192" \
-      "q4=" "m4=--stream-lat-small-max 8192"
+      "q1=" "m1=--stream-lat-small-max 8192" "c1=--stream-lat-ctx 3" "cm1=--stream-lat-ctx 3 --stream-lat-small-max 8192" \
+      "q2=" "m2=--stream-lat-small-max 8192" "c2=--stream-lat-ctx 3" "cm2=--stream-lat-ctx 3 --stream-lat-small-max 8192"
     ;;
   cb2)
     # more interleaved pairs of the cb arms (share 1/2 vs none), after the share's own test
