@@ -491,7 +491,7 @@ def kfd_queues() -> dict | None:
 
 
 class KfdSampler:
-    """Samples kfd_queues() every 50 ms on a thread while a leg runs (the tile threads run in C, without the
+    """Samples kfd_queues() every 250 ms on a thread while a leg runs (the tile threads run in C, without the
     GIL); keeps the largest queue counts seen and the growth of the evicted time over the leg."""
 
     def __init__(self):
@@ -512,7 +512,7 @@ class KfdSampler:
                              evicted_ms=round(q["evicted_ms"] - self._first["evicted_ms"], 3))
             if stopped:
                 return
-            self._stop.wait(0.05)
+            self._stop.wait(0.25)
 
     def __enter__(self):
         self._t.start()
