@@ -24,6 +24,11 @@ run_arms() {
 }
 
 case "$job" in
+  pf)
+    # paced legs: the tile's prefetch distance (own frags ahead: mcache line and record header), 1 (default) vs 4 / 8
+    run_arms r05_pf "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
+      "p1a=" "p8a=--stream-pf-dist 8" "p4a=--stream-pf-dist 4" "p1b=" "p8b=--stream-pf-dist 8" "p4b=--stream-pf-dist 4"
+    ;;
   lq2)
     # gather delays split at the runtime call (issue -> start on the GPU vs the launch thread's queue): default
     # paced arms and arms without the launch thread
