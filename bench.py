@@ -727,6 +727,10 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 "knee_def": "highest offered frags/s per GPU with p99 <= 1 ms and no frag lost",
                 "paced_fps_p50_p99_us": [[_r(c["offered_frags_per_s_per_gpu"], 3), _r(c["p50_us"]), _r(c["p99_us"])]
                                          for c in curve],
+                # per paced leg, the longest a GPU copy waited on the GPU after the runtime call that issued it
+                # (a GPU-side pause holds every queue at once: DESIGN §12, the paced tail)
+                "paced_gpu_pause_max_us": [_r((c.get("gather_gpu") or {}).get("issue_to_start_max_us"), 3)
+                                           for c in curve],
                 "p99_us": _r(curve[0]["p99_us"]) if curve else None,
                 "unreliable_vs_max": _r(st.get("unreliable_goodput_vs_max"), 3),
                 "tile_host_ns_per_frag": (st.get("max_rate") or {}).get("tile_host_ns_per_frag"),
