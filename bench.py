@@ -540,10 +540,11 @@ def stream_child_main(args) -> None:
         if n:
             anom[leg] = {"count": n, "first": first[:8]}
     wb = {"gather": 0, "none": 1, "finish": 2}[args.stream_writeback]
-    if wb or args.stream_poll_prefetch or args.stream_gather_rpb or args.stream_gather_cu_spread:
+    if wb or args.stream_poll_prefetch or args.stream_gather_rpb or args.stream_gather_cu_spread or args.stream_quad_sha:
         from firedancer_amd import engine
         engine.debug_set_opts(gather_no_writeback=wb, poll_prefetch=args.stream_poll_prefetch,
-                              gather_rpb=args.stream_gather_rpb, gather_cu_spread=args.stream_gather_cu_spread)
+                              gather_rpb=args.stream_gather_rpb, gather_cu_spread=args.stream_gather_cu_spread,
+                              quad_sha=args.stream_quad_sha)
     payload = desc = None
     if proc == 0:
         from firedancer_amd import synth
@@ -616,7 +617,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
          "--stream-copy-threads", str(args.stream_copy_threads),
          "--stream-tput-min-batch", str(args.stream_tput_min_batch),
          "--stream-tput-small-max", str(args.stream_tput_small_max), "--stream-lat-hk-us", str(args.stream_lat_hk_us),
-         "--stream-lat-small-max", str(args.stream_lat_small_max),
+         "--stream-lat-small-max", str(args.stream_lat_small_max), "--stream-quad-sha", str(args.stream_quad_sha),
          "--stream-lat-share", str(args.stream_lat_share)]
     if args.stream_copy:
         cmd.append("--stream-copy")
@@ -979,6 +980,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-tput-small-max", type=int, default=0,
                     help="max-rate legs: batches of at most this many signatures take the latency path "
                          "(fdgpu_vtile_opts_t.small_max; 0 = the tile's default, half the batch limit)")
+    ap.add_argument("--stream-quad-sha", type=int, default=0, choices=(-1, 0),
+                    help="A/B: -1 = the latency path's hash role on one lane per signature instead of a quad "
+                         "(fdgpu_debug_opts_t.quad_sha; engine test hook)")
     ap.add_argument("--stream-lat-small-max", type=int, default=0,
                     help="paced legs: batches of at most this many signatures take the latency path (fdgpu_vtile_opts_t."
                          "small_max; 0 = the tile's default, half the batch limit)")

@@ -96,6 +96,10 @@
 #ifndef FD_DSM2_MAX
 #define FD_DSM2_MAX 32768UL          /* then two up to here, then one (fd_dsm_kernel, R compared at its end) */
 #endif
+#ifndef FD_QSHA_MAX
+#define FD_QSHA_MAX 8192UL           /* latency path: the prep's hash role on a quad of lanes per signature up to here
+                                        (fd_sha512_RAM_quad; 6 sg workgroups stay under one wave per SIMD) */
+#endif
 #define FD_STAGE_CHUNK ( 1UL << 20 )   /* host-staged batches: bytes per memcpy / H2D step */
 /* gathered batches: the fd_txn_t image of the last record may end this far past its record */
 #define FD_IMG_TAIL    1024UL
@@ -583,6 +587,46 @@ FD_DEV void hashh_one( unsigned char const * __restrict__ payload, fdgpu_txn_des
   }
 }
 
+/* The latency path's hash role on a quad of lanes (fd_prep_kernel<.,1,1>): the S check and the loads on all
+   four, SHA-512 shared (fd_sha512_RAM_quad), then lane q = 0 alone goes on as hashh_one does (rc = 0: S's
+   check only; the DSM applies the rest).  Every exit before the digest is the quad's together. */
+FD_DEV void hashh_one_q( unsigned char const * __restrict__ payload, fdgpu_txn_desc_t const * __restrict__ desc,
+                         u32 const * __restrict__ map, u32 s, size_t n, i8 * __restrict__ code_out,
+                         i8 * __restrict__ digA, i8 * __restrict__ digR, short * __restrict__ digB,
+                         u32 * __restrict__ slow, u32 * __restrict__ slow_cnt, uint4 const * __restrict__ khash,
+                         u32 force_slow, unsigned char * __restrict__ htop, u32 q, u32 qbase ) {
+  u32 m = map[s];
+  u32 t = m & 0xffffffu, j = m >> 24;
+  fdgpu_txn_desc_t d = desc[t];
+  if( !txn_desc_ok( d ) ) { if( !q ) code_out[s] = FD_ED25519_ERR_SIG; return; }
+  unsigned char const * base = payload + d.payload_off;
+  u32 Sw[8];
+  fd_load_words<8>( Sw, base + d.signature_off + 64u*j + 32u );
+  if( !sc_is_canonical( Sw ) ) { if( !q ) code_out[s] = FD_ED25519_ERR_SIG; return; }
+  u32 Rw[8], Aw[8];
+  fd_load_words<8>( Rw, base + d.signature_off + 64u*j );
+  fd_load_words<8>( Aw, base + d.acct_addr_off + 32u*j );
+  u32 h[16], k[8];
+  if( khash ) {                                  /* digests computed before (long messages): lane 0 reads its own */
+    if( q ) return;
+#pragma unroll
+    for( int i=0; i<4; i++ ) { uint4 v = khash[4*(size_t)s + i]; h[4*i] = v.x; h[4*i+1] = v.y; h[4*i+2] = v.z; h[4*i+3] = v.w; }
+  } else {
+    fd_sha512_RAM_quad( h, Rw, Aw, base + d.message_off, (u32)d.payload_sz - (u32)d.message_off, q, qbase );
+    if( q ) return;
+  }
+  sc_reduce( k, h );
+  u32 c0[5], c1m[5], sp[8]; int c1neg = 0;
+  if( !( force_slow && s % force_slow == 0u ) && hs_prepare( k, Sw, c0, c1m, c1neg, sp ) ) {
+    hs_store_digits( c0, c1m, c1neg, sp, s, n, digA, digR, digB, htop );
+    code_out[s] = FD_ED25519_SUCCESS;
+  } else {
+    store_digits( k, Sw, s, n, digA, digB );
+    code_out[s] = FD_PEND_SLOW;
+    slow[ atomicAdd( slow_cnt, 1u ) ] = s;
+  }
+}
+
 /* FD_HASHH_MINW: as FD_DECODE_MINW for fd_hashh_kernel (0: 159 VGPRs, 3 waves) */
 #ifndef FD_HASHH_MINW
 #define FD_HASHH_MINW 0
@@ -681,7 +725,9 @@ FD_DEV void prep_role( unsigned char const * __restrict__ payload, fdgpu_txn_des
 __device__ unsigned long long fd_pp_buf[ FD_PP_WAVES ][ 3 ];
 #endif
 
-template<int FM, int HS>
+/* QS = 1 (half-size walk, batches of at most FD_QSHA_MAX signatures): the hash role on a quad of lanes per
+   signature (hashh_one_q), blocks [2 sg, 6 sg) */
+template<int FM, int HS, int QS = 0>
 __global__ void __launch_bounds__( FD_WG )
 fd_prep_kernel( unsigned char const *    __restrict__ payload,
                 fdgpu_txn_desc_t const * __restrict__ desc,
@@ -703,19 +749,36 @@ fd_prep_kernel( unsigned char const *    __restrict__ payload,
                 u32 *                    __restrict__ slow_cnt,
                 u32                                   force_slow,
                 unsigned char *          __restrict__ htop ) {
-  u32 role = blockIdx.x / sg, b = blockIdx.x - role*sg;
-  u32 s = b * FD_WG + threadIdx.x;
+  u32 role, s;
+  if( QS && blockIdx.x >= 2u*sg ) {              /* a quad per signature */
+    role = 2u;
+    s = ( blockIdx.x - 2u*sg ) * ( FD_WG / 4u ) + ( threadIdx.x >> 2 );
+  } else {
+    role = blockIdx.x / sg;
+    s = ( blockIdx.x - role*sg ) * FD_WG + threadIdx.x;
+  }
 #if FD_PREP_PROBE
   unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  if( s < nsig ) prep_role<FM,HS>( payload, desc, map, nsig, role, s, semantics, pstat, Rxy, Axy, code_out, digA, digB,
-                                   tab, khash, tabR, digR, slow, slow_cnt, force_slow, htop );
+  if( s < nsig ) {
+    if( QS && role == 2u )
+      hashh_one_q( payload, desc, map, s, nsig, code_out, digA, digR, digB, slow, slow_cnt, khash, force_slow, htop,
+                   threadIdx.x & 3u, threadIdx.x & 60u );
+    else
+      prep_role<FM,HS>( payload, desc, map, nsig, role, s, semantics, pstat, Rxy, Axy, code_out, digA, digB,
+                        tab, khash, tabR, digR, slow, slow_cnt, force_slow, htop );
+  }
   unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
   u32 wv = blockIdx.x * ( FD_WG / 64u ) + threadIdx.x / 64u;
   if( ( threadIdx.x & 63u ) == 0u && wv < FD_PP_WAVES && s < nsig ) {
     fd_pp_buf[ wv ][0] = t0; fd_pp_buf[ wv ][1] = t1; fd_pp_buf[ wv ][2] = role;
   }
 #else
-  if( s >= nsig ) return;
+  if( s >= nsig ) return;                        /* (a quad's four lanes leave together) */
+  if( QS && role == 2u ) {
+    hashh_one_q( payload, desc, map, s, nsig, code_out, digA, digR, digB, slow, slow_cnt, khash, force_slow, htop,
+                 threadIdx.x & 3u, threadIdx.x & 60u );
+    return;
+  }
   prep_role<FM,HS>( payload, desc, map, nsig, role, s, semantics, pstat, Rxy, Axy, code_out, digA, digB,
                     tab, khash, tabR, digR, slow, slow_cnt, force_slow, htop );
 #endif
@@ -2192,7 +2255,8 @@ struct fdgpu_ed25519_ctx {
   int last_path;                 /* the engine path launch_batch chose last (FDGPU_PATH_* or latency lanes) */
   int           excl_mode;       /* fdgpu_ed25519_set_cu_exclusive's mode; -1: off, chosen by fdgpu_debug_opts_t */
   unsigned long lat_cus;         /* fdgpu_ed25519_set_lat_share: CUs an exclusive walk may count on, 0 = no limit */
-  unsigned      excl_lds[ 7 ];   /* fdgpu_ed25519_set_cu_exclusive: dynamic LDS per workgroup of the latency path's
+  int           quad_sha;        /* latency path: the hash role on quads up to FD_QSHA_MAX (fdgpu_debug_opts_t.quad_sha) */
+  unsigned      excl_lds[ 8 ];   /* fdgpu_ed25519_set_cu_exclusive: dynamic LDS per workgroup of the latency path's
                                     prep<0,1>, prep<0,0>, dsm8, dsm4<0,1>, dsm4<0,0>, dsm2<0,1>, dsm2<0,0> (0 = none) */
   unsigned long nofold_max;      /* fd_dsm_kernel<0> (no carry fold) for batches of at most this many signatures */
   u32 *   d_P;                   /* FD_DEFER_R: P = [k](-A)+[S]B, planar [30][max_sig] limbs */
@@ -2305,15 +2369,16 @@ fdgpu_ed25519_set_small_batch_max( fdgpu_ed25519_ctx_t * ctx, unsigned long smal
    dynamic LDS (a process-wide function attribute) is raised once to what mode 1 needs, so contexts with
    different modes never undo each other's; each context keeps its own choice in excl_lds. */
 static std::mutex g_excl_mu;
-static unsigned   g_excl_max[ 7 ];     /* per kernel: the dynamic LDS its attribute allows (0: not raised yet) */
+static unsigned   g_excl_max[ 8 ];     /* per kernel: the dynamic LDS its attribute allows (0: not raised yet) */
 extern "C" int
 fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on ) {
   if( !ctx || on < 0 || on > 4 ) return -1;
   /* on (A/B): 1 prep and walk alone on their CU; 2 at most two per CU; 3 the walk alone; 4 the prep alone */
-  void const * f[ 7 ] = { (void const *)fd_prep_kernel<0,1>, (void const *)fd_prep_kernel<0,0>, (void const *)fd_dsm8_kernel<0>,
+  void const * f[ 8 ] = { (void const *)fd_prep_kernel<0,1>, (void const *)fd_prep_kernel<0,0>, (void const *)fd_dsm8_kernel<0>,
                           (void const *)fd_dsm4_kernel<0,1>, (void const *)fd_dsm4_kernel<0,0>,
-                          (void const *)fd_dsm2_kernel<0,1>, (void const *)fd_dsm2_kernel<0,0> };
-  unsigned v[ 7 ] = { 0u, 0u, 0u, 0u, 0u, 0u, 0u };
+                          (void const *)fd_dsm2_kernel<0,1>, (void const *)fd_dsm2_kernel<0,0>,
+                          (void const *)fd_prep_kernel<0,1,1> };
+  unsigned v[ 8 ] = { 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u };
   if( on ) {
     HIPCHK( hipSetDevice( ctx->device ), -2 );
     int lds = 0;
@@ -2323,11 +2388,11 @@ fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on ) {
     unsigned third = ( (unsigned)lds / 3u + 2048u ) & ~1023u;         /* > 1/3, <= 1/2: two per CU */
     unsigned want = on == 2 ? third : half;
     std::lock_guard<std::mutex> lk( g_excl_mu );
-    for( int i=0; i<7; i++ ) {
+    for( int i=0; i<8; i++ ) {
       hipFuncAttributes a;
       HIPCHK( hipFuncGetAttributes( &a, f[i] ), -2 );
       unsigned st = (unsigned)a.sharedSizeBytes;
-      int walk = i >= 2;
+      int walk = i >= 2 && i <= 6;
       if( ( on == 3 && !walk ) || ( on == 4 && walk ) ) continue;
       v[i] = st < want ? want - st : 0u;
       unsigned top = st < half ? half - st : 0u;                        /* the most any mode asks of this kernel */
@@ -2337,7 +2402,7 @@ fdgpu_ed25519_set_cu_exclusive( fdgpu_ed25519_ctx_t * ctx, int on ) {
       }
     }
   }
-  for( int i=0; i<7; i++ ) ctx->excl_lds[i] = v[i];
+  for( int i=0; i<8; i++ ) ctx->excl_lds[i] = v[i];
   ctx->excl_mode = on;
   return 0;
 }
@@ -2419,7 +2484,13 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       lanes = pick_path( ctx, nsig );
       ctx->last_path = lanes;
       int d2 = lanes > 1;
-      if( hs )      /* half-size: the A and R lanes build both tables, the hash lane (c0, c1, s') */
+      int qs = hs && ctx->quad_sha >= 0 && nsig <= FD_QSHA_MAX;   /* the hash role on quads (fd_sha512_RAM_quad) */
+      if( qs )
+        hipLaunchKernelGGL( (fd_prep_kernel<0,1,1>), dim3(6*sg), dim3(FD_WG), ctx->excl_lds[7], st, d_payload, d_desc, ctx->d_map, nsig,
+                            (u32)sg, ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
+                            ctx->d_tab, (uint4 const *)ctx->d_khash, ctx->d_tabR, ctx->d_digR, ctx->d_slow,
+                            ctx->d_slow + ctx->max_sig, ctx->half_force_slow, ctx->d_htop );
+      else if( hs )      /* half-size: the A and R lanes build both tables, the hash lane (c0, c1, s') */
         hipLaunchKernelGGL( (fd_prep_kernel<0,1>), dim3(3*sg), dim3(FD_WG), ctx->excl_lds[0], st, d_payload, d_desc, ctx->d_map, nsig,
                             (u32)sg, ctx->semantics, ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, code, ctx->d_digA, ctx->d_digB,
                             ctx->d_tab, (uint4 const *)ctx->d_khash, ctx->d_tabR, ctx->d_digR, ctx->d_slow,
@@ -2541,14 +2612,14 @@ static void launcher_drain( fdgpu_launcher_t * L );
 /* Test / A/B options of contexts created from now on (fdgpu_debug_set_opts).
    Process-wide, behind a mutex; the defaults are the product's choices. */
 static std::mutex g_dbg_mu;
-static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L, 0, 0, 0, 0, 0 };
+static fdgpu_debug_opts_t g_dbg = { -1, 0u, -1L, 0, -1L, 0, 0, 0, 0, 0, 0 };
 static void debug_opts_get( fdgpu_debug_opts_t * o ) { std::lock_guard<std::mutex> lk( g_dbg_mu ); *o = g_dbg; }
 
 extern "C" void
 fdgpu_debug_set_opts( fdgpu_debug_opts_t const * opts ) {
   std::lock_guard<std::mutex> lk( g_dbg_mu );
   if( opts ) g_dbg = *opts;
-  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L, 0, 0, 0, 0, 0 };
+  else       g_dbg = fdgpu_debug_opts_t{ -1, 0u, -1L, 0, -1L, 0, 0, 0, 0, 0, 0 };
 }
 
 /* staging + device buffers of async slot i (once) */
@@ -2633,6 +2704,7 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->poll_pf = dbg.poll_prefetch > 0 ? dbg.poll_prefetch : 0;
   ctx->gather_rpb = dbg.gather_rpb == 1 ? 1 : 4;
   ctx->gather_cu_spread = dbg.gather_cu_spread;
+  ctx->quad_sha = dbg.quad_sha;
   for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
   for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;

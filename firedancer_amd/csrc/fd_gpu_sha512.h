@@ -142,6 +142,38 @@ FD_DEV void fd_sha512_block( u64 h[ 8 ], u64 w[ 16 ] ) {
   h[0]+=a; h[1]+=b; h[2]+=c; h[3]+=d; h[4]+=e; h[5]+=f; h[6]+=g; h[7]+=hh;
 }
 
+/* Message block b (of nb) of R || A || M with its padding and length, as 16 big-endian words; L = 64 + msg_sz
+   input bytes.  R, A: the 32-byte encodings as 8 LE words; M: msg_sz bytes at msg. */
+FD_DEV void fd_sha512_RAM_block( u64 w[ 16 ], u32 b, u32 nb, u32 L, u32 const R[ 8 ], u32 const A[ 8 ],
+                                 unsigned char const * msg ) {
+  u32 lw[32];
+  if( b==0 ) {
+#pragma unroll
+    for( int i=0; i<8; i++ ) { lw[i] = R[i]; lw[8+i] = A[i]; }
+    fd_load_words<16>( lw+16, msg );
+  } else {
+    fd_load_words<32>( lw, msg + (128u*b - 64u) );
+  }
+#pragma unroll
+  for( int i=0; i<16; i++ ) w[i] = ((u64)fd_bswap32( lw[2*i] ) << 32) | (u64)fd_bswap32( lw[2*i+1] );
+  if( 128u*(b+1u) > L ) {                       /* the message ends in this block: mask, pad, length */
+#pragma unroll
+    for( int i=0; i<16; i++ ) {
+      /* mask bytes past the end, insert 0x80, insert the bit length */
+      u64 x = w[i];
+      int pos = (int)(128u*b) + 8*i;
+      int nv  = (int)L - pos;                   /* valid bytes in this word */
+      if( b==0 && i<8 ) nv = 8;                 /* R||A always present */
+      u64 m = nv>=8 ? ~0UL : ( nv<=0 ? 0UL : ( ~0UL << (8*(8-nv)) ) );
+      x &= m;
+      if( nv>=0 && nv<8 ) x |= 0x80UL << (8*(7-nv));
+      if( b==nb-1u && i==15 ) x = (u64)L << 3;
+      if( b==nb-1u && i==14 ) x = 0UL;
+      w[i] = x;
+    }
+  }
+}
+
 /* SHA-512( R || A || M ) -> 64-byte digest as 16 little-endian words
    (byte order of the digest, i.e. the scalar k's LE bytes).
    R, A: the 32-byte encodings as 8 LE words; M: msg_sz bytes at msg. */
@@ -154,33 +186,81 @@ FD_DEV void fd_sha512_RAM( u32 out[ 16 ], u32 const R[ 8 ], u32 const A[ 8 ],
 #pragma unroll 1
   for( u32 b=0; b<nb; b++ ) {
     u64 w[16];
-    u32 lw[32];
-    if( b==0 ) {
-#pragma unroll
-      for( int i=0; i<8; i++ ) { lw[i] = R[i]; lw[8+i] = A[i]; }
-      fd_load_words<16>( lw+16, msg );
-    } else {
-      fd_load_words<32>( lw, msg + (128u*b - 64u) );
-    }
-#pragma unroll
-    for( int i=0; i<16; i++ ) w[i] = ((u64)fd_bswap32( lw[2*i] ) << 32) | (u64)fd_bswap32( lw[2*i+1] );
-    if( 128u*(b+1u) > L ) {                       /* the message ends in this block: mask, pad, length */
-#pragma unroll
-      for( int i=0; i<16; i++ ) {
-        /* mask bytes past the end, insert 0x80, insert the bit length */
-        u64 x = w[i];
-        int pos = (int)(128u*b) + 8*i;
-        int nv  = (int)L - pos;                   /* valid bytes in this word */
-        if( b==0 && i<8 ) nv = 8;                 /* R||A always present */
-        u64 m = nv>=8 ? ~0UL : ( nv<=0 ? 0UL : ( ~0UL << (8*(8-nv)) ) );
-        x &= m;
-        if( nv>=0 && nv<8 ) x |= 0x80UL << (8*(7-nv));
-        if( b==nb-1u && i==15 ) x = (u64)L << 3;
-        if( b==nb-1u && i==14 ) x = 0UL;
-        w[i] = x;
-      }
-    }
+    fd_sha512_RAM_block( w, b, nb, L, R, A, msg );
     fd_sha512_block( h, w );
+  }
+#pragma unroll
+  for( int i=0; i<8; i++ ) { out[2*i] = fd_bswap32( (u32)(h[i] >> 32) ); out[2*i+1] = fd_bswap32( (u32)h[i] ); }
+}
+
+/* The same digest on a quad of lanes (the latency path's hash role: a batch that leaves SIMDs idle runs as
+   long as its longest lane's instruction stream).  The rounds of a block depend on each other; its message
+   schedule depends only on the block.  So the four lanes of a quad (q = 0..3, quad base lane qbase within
+   the wave) each expand one block of a group of four into W_t + K_t (80 words, in registers), and then all
+   four run the group's blocks' rounds in turn, block j's schedule read from lane qbase + j with
+   ds_bpermute (issued four rounds ahead).  Per block the rounds' stream drops from 56 to 32 VALU
+   instructions a round (rounds 16-79: no schedule and no K add); the expansions of four blocks cost the
+   stream about what one block's schedule did.  All four lanes end with the digest. */
+FD_DEV u64 fd_bperm64( u64 x, int addr ) {
+  u32 lo = (u32)__builtin_amdgcn_ds_bpermute( addr, (int)(u32)x );
+  u32 hi = (u32)__builtin_amdgcn_ds_bpermute( addr, (int)(u32)( x >> 32 ) );
+  return fd_mk64( lo, hi );
+}
+
+#define FD_SHA512_ROUND_KW( kw ) do {                                               \
+    u64 S1 = fd_xor3_64( fd_rotr64( e,14 ), fd_rotr64( e,18 ), fd_rotr64( e,41 ) ); \
+    u64 ch = fd_ch64( e, f, g );                                                    \
+    u64 t1 = hh + S1 + ch + (kw);                                                   \
+    u64 S0 = fd_xor3_64( fd_rotr64( a,28 ), fd_rotr64( a,34 ), fd_rotr64( a,39 ) ); \
+    u64 mj = fd_maj64( a, b, c );                                                   \
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;      \
+  } while(0)
+
+FD_DEV void fd_sha512_RAM_quad( u32 out[ 16 ], u32 const R[ 8 ], u32 const A[ 8 ],
+                                unsigned char const * msg, u32 msg_sz, u32 q, u32 qbase ) {
+  u64 h[8] = { 0x6a09e667f3bcc908UL, 0xbb67ae8584caa73bUL, 0x3c6ef372fe94f82bUL, 0xa54ff53a5f1d36f1UL,
+               0x510e527fade682d1UL, 0x9b05688c2b3e6c1fUL, 0x1f83d9abfb41bd6bUL, 0x5be0cd19137e2179UL };
+  u32 L  = 64u + msg_sz;
+  u32 nb = ( L + 17u + 127u ) >> 7;
+#pragma unroll 1
+  for( u32 g0=0; g0<nb; g0+=4u ) {
+    u64 wk[80];
+    {
+      u32 bq = g0 + q;                          /* this lane's block of the group (none past the last) */
+      u64 w[16];
+      if( bq < nb ) fd_sha512_RAM_block( w, bq, nb, L, R, A, msg );
+      else {
+#pragma unroll
+        for( int i=0; i<16; i++ ) w[i] = 0UL;
+      }
+#pragma unroll
+      for( int t=0; t<16; t++ ) wk[t] = w[t];
+#pragma unroll
+      for( int t=16; t<80; t++ ) {
+        u64 w15 = wk[t-15], w2 = wk[t-2];
+        u64 s0 = fd_xor3_64( fd_rotr64( w15, 1 ), fd_rotr64( w15, 8 ), fd_shr64( w15, 7 ) );
+        u64 s1 = fd_xor3_64( fd_rotr64( w2, 19 ), fd_rotr64( w2, 61 ), fd_shr64( w2, 6 ) );
+        wk[t] = wk[t-16] + s0 + wk[t-7] + s1;
+      }
+#pragma unroll
+      for( int t=0; t<80; t++ ) wk[t] += fd_gpu_sha512_k[t];
+    }
+#pragma unroll 1
+    for( u32 j=0; j<4u && g0+j<nb; j++ ) {      /* (nb is the quad's: its four lanes agree) */
+      int addr = (int)( ( qbase + j ) << 2 );
+      u64 a=h[0], b=h[1], c=h[2], d=h[3], e=h[4], f=h[5], g=h[6], hh=h[7];
+      u64 pf[4];
+#pragma unroll
+      for( int t=0; t<4; t++ ) pf[t] = fd_bperm64( wk[t], addr );
+#pragma unroll
+      for( int t=0; t<80; t++ ) {
+        u64 kw = pf[t & 3];
+        if( t + 4 < 80 ) pf[t & 3] = fd_bperm64( wk[t + 4], addr );
+        FD_SHA512_ROUND_KW( kw );
+        if( (t & 3)==3 ) __builtin_amdgcn_sched_barrier( 0 );
+      }
+      h[0]+=a; h[1]+=b; h[2]+=c; h[3]+=d; h[4]+=e; h[5]+=f; h[6]+=g; h[7]+=hh;
+    }
   }
 #pragma unroll
   for( int i=0; i<8; i++ ) { out[2*i] = fd_bswap32( (u32)(h[i] >> 32) ); out[2*i+1] = fd_bswap32( (u32)h[i] ); }

@@ -189,18 +189,18 @@ class DebugOpts(ctypes.Structure):
     _fields_ = [("half", ctypes.c_int), ("half_force_slow", ctypes.c_uint), ("small_batch_max", ctypes.c_long),
                 ("dsm_lanes", ctypes.c_int), ("nofold_max", ctypes.c_long), ("gather_no_writeback", ctypes.c_int),
                 ("poll_prefetch", ctypes.c_int), ("gather_rpb", ctypes.c_int), ("gather_cu_spread", ctypes.c_int),
-                ("cu_exclusive", ctypes.c_int)]
+                ("cu_exclusive", ctypes.c_int), ("quad_sha", ctypes.c_int)]
 
 
 def debug_set_opts(half: int = -1, half_force_slow: int = 0, small_batch_max: int = -1, dsm_lanes: int = 0,
                    nofold_max: int = -1, gather_no_writeback: int = 0, poll_prefetch: int = 0,
-                   gather_rpb: int = 0, gather_cu_spread: int = 0, cu_exclusive: int = 0) -> None:
+                   gather_rpb: int = 0, gather_cu_spread: int = 0, cu_exclusive: int = 0, quad_sha: int = 0) -> None:
     """fdgpu_debug_set_opts: the engine path of every context created from now on (tests only; the
     defaults restore the product's choices).  small_batch_max >= 2**63 means "always the latency path"."""
     o = DebugOpts(half=half, half_force_slow=half_force_slow,
                   small_batch_max=min(small_batch_max, 2**63 - 1), dsm_lanes=dsm_lanes, nofold_max=nofold_max,
                   gather_no_writeback=gather_no_writeback, poll_prefetch=poll_prefetch, gather_rpb=gather_rpb,
-                  gather_cu_spread=gather_cu_spread, cu_exclusive=cu_exclusive)
+                  gather_cu_spread=gather_cu_spread, cu_exclusive=cu_exclusive, quad_sha=quad_sha)
     load_library().fdgpu_debug_set_opts(ctypes.byref(o))
 
 

@@ -698,6 +698,8 @@ typedef struct fdgpu_debug_opts {
                                         1 = every (CUs/n)-th, 2 = the first n (A/B) */
   int           cu_exclusive;        /* 1..4: new contexts start with fdgpu_ed25519_set_cu_exclusive( ctx, n ); -1: off,
                                         also in verify tiles (whose default is on); 0: default */
+  int           quad_sha;            /* latency path (half-size): 0 = default, the prep's hash role on a quad of lanes per
+                                        signature up to 8,192 signatures (fd_sha512_RAM_quad); -1 = one lane (A/B) */
 } fdgpu_debug_opts_t;
 
 void

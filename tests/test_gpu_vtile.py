@@ -240,7 +240,7 @@ def test_vtile_multictx_vs_model(oracle, nctx, zero_copy, launcher):
     assert bad == []
     assert launched > 20
     lm = vt.gpu_metrics()["launcher"]
-    assert (lm[0] >= launched) if launcher else lm == [0, 0, 0, 0]
+    assert (lm[0] >= launched) if launcher else not any(lm)
     vt.close()
     if zero_copy:
         engine.host_unregister(buf)

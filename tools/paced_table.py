@@ -7,7 +7,9 @@ import sys
 
 for d in sys.argv[1:]:
     for f in sorted(glob.glob(f"{d}/*.json")):
-        st = json.load(open(f))["stream"]
+        st = json.load(open(f)).get("stream")
+        if not st:                       # (other records in the same directory)
+            continue
         legs = st.get("only_paced") or {f"paced@{l['rate_fps']}": l for l in st.get("latency_curve", [])}
         row, knee, ok = [], 0.0, True
         for k, v in sorted(legs.items(), key=lambda kv: float(kv[0].split("@")[1])):

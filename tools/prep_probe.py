@@ -19,6 +19,9 @@ import torch  # noqa: E402
 from firedancer_amd import Engine, load_library, synth  # noqa: E402
 
 n = int(os.environ.get("TXNS", 2800))
+if os.environ.get("QUAD_SHA"):                # -1: the hash role on one lane per signature (fdgpu_debug_opts_t.quad_sha)
+    from firedancer_amd import engine as _engine
+    _engine.debug_set_opts(quad_sha=int(os.environ["QUAD_SHA"]))
 reps = int(os.environ.get("REPS", 20))
 payload, desc, expect, nsig = synth.make_batch(n, synth.LARGE_NOOP, seed=1234, threads=8)
 pay_d = torch.from_numpy(payload).cuda()
@@ -30,7 +33,7 @@ L = load_library()
 probe = hasattr(L, "fdgpu_debug_prep_probe")     # the plain library: just the batches (for a kernel trace)
 if probe:
     L.fdgpu_debug_prep_probe.argtypes = [ctypes.c_void_p, ctypes.c_ulong]
-nw = 3 * ((nsig + 255) // 256) * 4
+nw = min(6 * ((nsig + 255) // 256) * 4, 4096)     # waves of the launch (6 sg blocks with the quad hash role)
 rows = []
 for it in range(reps):
     if probe:

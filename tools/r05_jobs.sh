@@ -24,6 +24,23 @@ run_arms() {
 }
 
 case "$job" in
+  qs)
+    # the latency path's hash role on a quad of lanes (fd_sha512_RAM_quad): the engine-path parity tests (every
+    # latency path; latency4s keeps the one-lane role), prep role lengths quad vs one lane (FD_PREP_PROBE build
+    # build/ab/pp.so: tools/ab_build.sh pp -DFD_PREP_PROBE=1), then paced arms
+    d="gpurun_out/r05_qs"; mkdir -p "$d"
+    bash tools/gpu_job.sh \
+      "tests:900:python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_hs_top.py tests/test_gpu_edges.py tests/test_gpu_torsion.py tests/test_gpu_callers.py tests/test_gpu_txn.py tests/test_gpu_lat_share.py tests/test_gpu_vtile.py tests/test_gpu_stream_parity.py -q -rA --timeout 300 --timeout-method thread" \
+      "pq2800:120:TXNS=2800 FDGPU_LIB=build/ab/pp.so python tools/prep_probe.py > $d/pq2800.json" \
+      "po2800:120:QUAD_SHA=-1 TXNS=2800 FDGPU_LIB=build/ab/pp.so python tools/prep_probe.py > $d/po2800.json" \
+      "pq1000:120:TXNS=1000 FDGPU_LIB=build/ab/pp.so python tools/prep_probe.py > $d/pq1000.json" \
+      "po1000:120:QUAD_SHA=-1 TXNS=1000 FDGPU_LIB=build/ab/pp.so python tools/prep_probe.py > $d/po1000.json" \
+      "pq8192:120:TXNS=8192 FDGPU_LIB=build/ab/pp.so python tools/prep_probe.py > $d/pq8192.json" \
+      "po8192:120:QUAD_SHA=-1 TXNS=8192 FDGPU_LIB=build/ab/pp.so python tools/prep_probe.py > $d/po8192.json" \
+      "trace2800:180:FDGPU_LIB=firedancer_amd/libfdgpu_ed25519.so TXNS=2800 rocprofv3 --kernel-trace --stats -f csv -d $d/trace -o run -- python3 tools/prep_probe.py" &&
+    run_arms r05_qs "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
+      "q1=" "o1=--stream-quad-sha -1" "q2=" "o2=--stream-quad-sha -1"
+    ;;
   pf)
     # paced legs: the tile's prefetch distance (own frags ahead: mcache line and record header), 1 (default) vs 4 / 8
     run_arms r05_pf "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
