@@ -388,7 +388,8 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
                            "run_max_us": st["gather_gpu"][4] * 1e-3,
                            # the runtime call that issued it (the launch thread's, after its queue) -> start
                            "issue_to_start_mean_us": st["gather_gpu"][5] / max(st["gather_gpu"][0], 1) * 1e-3,
-                           "issue_to_start_max_us": st["gather_gpu"][6] * 1e-3},
+                           "issue_to_start_max_us": st["gather_gpu"][6] * 1e-3,
+                           "issue_to_start_over_250us": st["gather_gpu"][7]},
             # each batch's GPU time split (fdgpu_ed25519_phase_stats): launch -> its verify kernels start (its
             # gathers and the stream's earlier batch), kernels, end -> the tile saw it; launch -> last gather end
             "batch_phases_us": _phases(st["phase"]),
@@ -732,6 +733,8 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 # (a GPU-side pause holds every queue at once: DESIGN §12, the paced tail)
                 "paced_gpu_pause_max_us": [_r((c.get("gather_gpu") or {}).get("issue_to_start_max_us"), 3)
                                            for c in curve],
+                "paced_gpu_pauses_over_250us": [(c.get("gather_gpu") or {}).get("issue_to_start_over_250us")
+                                                for c in curve],
                 "p99_us": _r(curve[0]["p99_us"]) if curve else None,
                 "unreliable_vs_max": _r(st.get("unreliable_goodput_vs_max"), 3),
                 "tile_host_ns_per_frag": (st.get("max_rate") or {}).get("tile_host_ns_per_frag"),

@@ -2298,7 +2298,7 @@ struct fdgpu_ed25519_ctx {
   double          gclk_off_ns;   /*   GPU clock ns - host CLOCK_MONOTONIC ns (calibrated once) */
   int             gclk_ok;
   unsigned long   gs_n, gs_start_sum, gs_start_max, gs_run_sum, gs_run_max;   /* fdgpu_ed25519_gather_stats */
-  unsigned long   gs_issue_sum, gs_issue_max;
+  unsigned long   gs_issue_sum, gs_issue_max, gs_issue_slow;
   long            last_gt;       /*   gt[] entry of the last gather launched (-1: untimed) */
   unsigned long * h_stamp;       /*   pinned [NSLOT][2] + 1: per slot the GPU clock when its verify kernels start
                                       (fd_stamp_kernel) and end (fd_done_kernel); [2 NSLOT]: clock calibration */
@@ -3244,6 +3244,7 @@ static void gather_times( fdgpu_ed25519_ctx_t * ctx, unsigned long gathered ) {
       unsigned long sdi = si > 0. ? (unsigned long)si : 0UL;
       ctx->gs_issue_sum += sdi;
       if( sdi > ctx->gs_issue_max ) ctx->gs_issue_max = sdi;
+      ctx->gs_issue_slow += sdi > 250000UL;
       ctx->gs_n++; ctx->gs_start_sum += sd; ctx->gs_run_sum += rn;
       if( sd > ctx->gs_start_max ) ctx->gs_start_max = sd;
       if( rn > ctx->gs_run_max ) ctx->gs_run_max = rn;
@@ -3944,10 +3945,10 @@ extern "C" unsigned long
 fdgpu_ed25519_gather_launched( fdgpu_ed25519_ctx_t const * ctx ) { return ctx->g_launched; }
 
 extern "C" void
-fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 7 ] ) {
+fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 8 ] ) {
   gather_times( ctx, fdgpu_ed25519_gathered( ctx ) );
   out[0] = ctx->gs_n; out[1] = ctx->gs_start_sum; out[2] = ctx->gs_start_max; out[3] = ctx->gs_run_sum; out[4] = ctx->gs_run_max;
-  out[5] = ctx->gs_issue_sum; out[6] = ctx->gs_issue_max;
+  out[5] = ctx->gs_issue_sum; out[6] = ctx->gs_issue_max; out[7] = ctx->gs_issue_slow;
 }
 
 extern "C" int

@@ -730,8 +730,9 @@ fdgpu_vtile_gpu_metrics( fdgpu_vtile_t * vt, fdgpu_vtile_gpu_metrics_t * out ) {
     ulong b, t, h[ FDGPU_LAT_BUCKETS ];
     fdgpu_ed25519_batch_stats( vt->ctx[k], &b, &t, h );
     ulong lns, nl; fdgpu_ed25519_launch_stats( vt->ctx[k], &lns, &nl ); out->launch_ns += lns;
-    ulong gs[7]; fdgpu_ed25519_gather_stats( vt->ctx[k], gs );
+    ulong gs[8]; fdgpu_ed25519_gather_stats( vt->ctx[k], gs );
     out->gather_gpu[0] += gs[0]; out->gather_gpu[1] += gs[1]; out->gather_gpu[3] += gs[3]; out->gather_gpu[5] += gs[5];
+    out->gather_gpu[7] += gs[7];
     if( gs[2] > out->gather_gpu[2] ) out->gather_gpu[2] = gs[2];
     if( gs[4] > out->gather_gpu[4] ) out->gather_gpu[4] = gs[4];
     if( gs[6] > out->gather_gpu[6] ) out->gather_gpu[6] = gs[6];
@@ -2114,7 +2115,7 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     st->launch_ns += r->gm.launch_ns;
     st->copies += r->gm.copies; st->copy_lat_n += r->gm.copy_lat_n; st->copy_lat_ns_sum += r->gm.copy_lat_ns_sum;
     if( r->gm.copy_lat_ns_max > st->copy_lat_ns_max ) st->copy_lat_ns_max = r->gm.copy_lat_ns_max;
-    for( int k=0; k<7; k++ ) {
+    for( int k=0; k<8; k++ ) {
       if( k == 2 || k == 4 || k == 6 ) { if( r->gm.gather_gpu[k] > st->gather_gpu[k] ) st->gather_gpu[k] = r->gm.gather_gpu[k]; }
       else st->gather_gpu[k] += r->gm.gather_gpu[k];
     }

@@ -62,7 +62,7 @@ class GpuMetrics(ctypes.Structure):
                 ("poll_ns", ctypes.c_ulong), ("after_ns", ctypes.c_ulong),
                 ("launch_ns", ctypes.c_ulong), ("copies", ctypes.c_ulong), ("copy_lat_n", ctypes.c_ulong),
                 ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong),
-                ("gather_gpu", ctypes.c_ulong * 7), ("phase", ctypes.c_ulong * 9), ("copy_backlog", ctypes.c_ulong),
+                ("gather_gpu", ctypes.c_ulong * 8), ("phase", ctypes.c_ulong * 9), ("copy_backlog", ctypes.c_ulong),
                 ("launcher", ctypes.c_ulong * 6), ("host_copy", ctypes.c_ulong * 4)]
 
     def as_dict(self) -> dict:
@@ -105,7 +105,7 @@ class StreamStats(ctypes.Structure):
                 ("launch_ns", ctypes.c_ulong), ("tile_idle_ns", ctypes.c_ulong), ("prod_seconds", ctypes.c_double),
                 ("prod_wait_ns", ctypes.c_ulong), ("prof_ns", ctypes.c_ulong * 8), ("copies", ctypes.c_ulong),
                 ("copy_lat_n", ctypes.c_ulong), ("copy_lat_ns_sum", ctypes.c_ulong), ("copy_lat_ns_max", ctypes.c_ulong),
-                ("gather_gpu", ctypes.c_ulong * 7), ("phase", ctypes.c_ulong * 9), ("copy_backlog", ctypes.c_ulong),
+                ("gather_gpu", ctypes.c_ulong * 8), ("phase", ctypes.c_ulong * 9), ("copy_backlog", ctypes.c_ulong),
                 ("tile_cpu_ns", ctypes.c_ulong), ("tile_wall_ns", ctypes.c_ulong), ("tile_nivcsw", ctypes.c_ulong),
                 ("tile_cpu_share_min", ctypes.c_double), ("tile_cpu", ctypes.c_long * 8),
                 ("prod_cpu_ns", ctypes.c_ulong), ("prod_wall_ns", ctypes.c_ulong), ("prod_nivcsw", ctypes.c_ulong),

@@ -541,8 +541,8 @@ int           fdgpu_ed25519_reserve_cus( fdgpu_ed25519_ctx_t * ctx, unsigned n, 
    start, out[3] / out[4] the sum / max of first block's start -> last
    block's end, out[5] / out[6] the sum / max of the runtime call that
    issued it (on the launch thread, if any: after its queue) -> first
-   block's start, ns */
-void          fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 7 ] );
+   block's start, ns, out[7] how many of those took over 250 us */
+void          fdgpu_ed25519_gather_stats( fdgpu_ed25519_ctx_t * ctx, unsigned long out[ 8 ] );
 /* where the async batches' time goes, from GPU clock stamps at each batch's
    verify kernels' start and end (mapped to host time once, at context
    creation): out[0] batches timed; out[1] / out[2] sum / max of host launch

@@ -173,9 +173,9 @@ typedef struct fdgpu_vtile_gpu_metrics {
   unsigned long launch_ns;        /* host time inside batch launches and early copies (in during_frag, housekeep or a drain) */
   unsigned long copies;           /* zero-copy: early GPU copies started (housekeep, fdgpu_vtile_copy) */
   unsigned long copy_lat_n, copy_lat_ns_sum, copy_lat_ns_max;   /* ... of them timed: launch -> completion seen */
-  unsigned long gather_gpu[ 7 ];  /* every GPU copy (early or at a batch launch), on the GPU clock, summed over the
+  unsigned long gather_gpu[ 8 ];  /* every GPU copy (early or at a batch launch), on the GPU clock, summed over the
                                      tile's contexts: fdgpu_ed25519_gather_stats (count, launch -> start sum / max,
-                                     start -> end sum / max, issue -> start sum / max, ns) */
+                                     start -> end sum / max, issue -> start sum / max, ns, issue -> start over 250 us) */
   unsigned long phase[ 9 ];       /* fdgpu_ed25519_phase_stats summed over the tile's contexts (maxima: max) */
   unsigned long copy_backlog;     /* during_frag calls refused with FDGPU_VTILE_COPY_BACKLOG */
   unsigned long launcher[ 6 ];    /* the tile's launch thread (opts.launcher), fdgpu_launcher_stats: commands issued,
@@ -453,7 +453,7 @@ typedef struct fdgpu_stream_stats {
                                     after_frags, housekeep (launch decisions) */
   unsigned long copies, copy_lat_n, copy_lat_ns_sum, copy_lat_ns_max;   /* zero-copy: early GPU copies (summed over
                                     tiles; max over tiles), as fdgpu_vtile_gpu_metrics_t */
-  unsigned long gather_gpu[ 7 ];  /* fdgpu_vtile_gpu_metrics_t.gather_gpu, summed (maxima: max) over tiles */
+  unsigned long gather_gpu[ 8 ];  /* fdgpu_vtile_gpu_metrics_t.gather_gpu, summed (maxima: max) over tiles */
   unsigned long phase[ 9 ];       /* fdgpu_vtile_gpu_metrics_t.phase, summed (maxima: max) over tiles */
   unsigned long copy_backlog;     /* fdgpu_vtile_gpu_metrics_t.copy_backlog, summed over tiles */
   /* host contention (a shared machine): the threads' CPU time against their loops' wall time, and the
