@@ -24,6 +24,12 @@ run_arms() {
 }
 
 case "$job" in
+  sf)
+    # GPU pauses in the paced legs (paced_gpu_pauses_over_250us) with the bench process's own GPU context open
+    # (default: headline first) or not yet (--stream-first: the tile processes run before it touches the GPU)
+    run_arms r05_sf "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
+      "d1=" "f1=--stream-first" "d2=" "f2=--stream-first" "d3=" "f3=--stream-first"
+    ;;
   qs)
     # the latency path's hash role on a quad of lanes (fd_sha512_RAM_quad): the engine-path parity tests (every
     # latency path; latency4s keeps the one-lane role), prep role lengths quad vs one lane (FD_PREP_PROBE build
