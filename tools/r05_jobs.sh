@@ -24,6 +24,12 @@ run_arms() {
 }
 
 case "$job" in
+  pt)
+    # paced tiles: 1 tile x 2 contexts (default) / 2 tiles x 1 context / 2 tiles x 2 contexts (each walk in 1/4)
+    run_arms r05_pt "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
+      "a1=" "b1=--stream-lat-tiles 2 --stream-lat-ctx 1" "c1=--stream-lat-tiles 2 --stream-lat-share 4" \
+      "a2=" "b2=--stream-lat-tiles 2 --stream-lat-ctx 1" "c2=--stream-lat-tiles 2 --stream-lat-share 4"
+    ;;
   sf)
     # GPU pauses in the paced legs (paced_gpu_pauses_over_250us) with the bench process's own GPU context open
     # (default: headline first) or not yet (--stream-first: the tile processes run before it touches the GPU)
