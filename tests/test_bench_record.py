@@ -18,6 +18,7 @@ def _leg(rate):
             "overruns_at_verdict": 0, "p50_us": 512.123456, "p99_us": 812.987654, "max_us": 1999.1,
             "published": 10 ** 8, "metrics": [0, 0, 0, 0, 10 ** 8], "tile_host_ns_per_frag": [30.8, 46.7, 10.9, 92.3],
             "sigs_per_s": rate, "frags_per_s": rate, "batch_limit": 8192, "offered_frags_per_s_per_gpu": rate,
+            "gather_gpu": {"n": 90000, "issue_to_start_max_us": 850.123456, "issue_to_start_over_250us": 3},
             "padding": "x" * 1500}
 
 
@@ -74,6 +75,9 @@ def test_compact_line_fits_and_carries_the_contract(tmp_path):
     assert rec["cpu_baseline"]["cores"] == 16 and rec["cpu_baseline"]["kind"] == "reference"
     assert len(rec["per_gpu"]) == 8
     assert rec["stream"]["knee"] == 7.5e6 and len(rec["stream"]["paced_fps_p50_p99_us"]) == 5
+    # per paced leg: the longest GPU-side hold of a copy and how many were held over 250 us (the GPU pauses)
+    assert rec["stream"]["paced_gpu_pause_max_us"] == [850.0] * 5
+    assert rec["stream"]["paced_gpu_pauses_over_250us"] == [3] * 5
     assert json.load(open(detail)) == full          # the detail file keeps everything
 
 
@@ -231,3 +235,14 @@ def test_dry_run_prints_the_plan(tmp_path):
     hp = json.loads(r.stdout.strip().splitlines()[-1])["host_plan"]
     assert hp["need_cores"] == 24 and hp["used_cores"] == 16 and hp["tiles_per_gpu"] == 1 and hp["capped"]
     assert "2 -> 1" in hp["cap"]
+
+
+def test_kfd_queues_without_kfd():
+    """The KFD queue / eviction sampler reads only sysfs: off a GPU host (no /sys/class/kfd) it reports
+    nothing and its thread ends at once."""
+    q = bench.kfd_queues()
+    assert q is None or set(q) == {"queues", "procs", "evicted_ms"}
+    with bench.KfdSampler() as s:
+        pass
+    assert s.peak is None or s.peak["evicted_ms"] >= 0.0
+
