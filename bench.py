@@ -524,6 +524,30 @@ class KfdSampler:
         self._t.join(1.0)
 
 
+def gpu_pause_log(reset: bool = True) -> dict | None:
+    """The engine's GPU pause log (fdgpu_debug_gather_pauses, read through the tile library this process has
+    loaded, without torch): copies held over 250 us on the GPU after their runtime call, grouped into episodes
+    (events within 2 ms of each other): [start ms from the first, longest hold us, copies]."""
+    import ctypes
+    from firedancer_amd import vtile
+    L = vtile.load()
+    f = getattr(L, "fdgpu_debug_gather_pauses", None)
+    if f is None:
+        return None
+    f.restype, f.argtypes = ctypes.c_ulong, [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int]
+    buf = (ctypes.c_ulong * 1024)()
+    tot = int(f(buf, 512, 1 if reset else 0))
+    ev = sorted((buf[2 * i], buf[2 * i + 1]) for i in range(min(tot, 512)))
+    eps = []
+    for t, d in ev:
+        if eps and t - eps[-1][3] <= 2_000_000:
+            eps[-1][1] = max(eps[-1][1], d); eps[-1][2] += 1; eps[-1][3] = t
+        else:
+            eps.append([t, d, 1, t])
+    t0 = eps[0][0] if eps else 0
+    return {"copies": tot, "episodes": [[round((e[0] - t0) * 1e-6, 2), round(e[1] * 1e-3), e[2]] for e in eps[:40]]}
+
+
 def stream_child_main(args) -> None:
     """--stream-child: the configs[4] legs for one process (one GPU); no torch GPU context here.  Process 0
     regenerates the payloads (same seed), creates each leg's link and runs the producer; the others join."""
@@ -562,6 +586,7 @@ def stream_child_main(args) -> None:
             cfg = _leg_cfg(args, leg, procs, cal_fps)
             link = vtile.Link(path, create=True, payload=payload, off=desc["payload_off"], sz=desc["payload_sz"], **cfg)
             huge_mb = _anon_huge_mb()
+            gpu_pause_log(reset=True)                 # (a fresh log for this leg)
             try:
                 with KfdSampler() as kq:
                     rc = link.run(0, dev, True)
@@ -576,7 +601,8 @@ def stream_child_main(args) -> None:
             if leg == "cal":
                 cal_fps = st["frags_per_s"]
             else:
-                out[leg] = dict(_leg_summary(st, cfg), anon_huge_mb=huge_mb, kfd_queues_peak=kq.peak)
+                out[leg] = dict(_leg_summary(st, cfg), anon_huge_mb=huge_mb, kfd_queues_peak=kq.peak,
+                                gpu_pauses=gpu_pause_log(reset=True))
         else:
             link = vtile.Link(path, create=False, timeout_s=180.0 if leg == "cal" else 120.0)   # bounded if process 0 failed
             try:

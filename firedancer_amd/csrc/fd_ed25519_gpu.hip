@@ -3231,6 +3231,12 @@ fdgpu_ed25519_verify_raw_host( fdgpu_ed25519_ctx_t * ctx, unsigned char const * 
    contexts, one per verify tile.) */
 /* launch the gather of slot sl's records not yet gathered (mode 3) on the
    context's gather stream; returns how many, or < 0 */
+/* GPU pauses, process-wide (fdgpu_debug_gather_pauses): the first FD_PAUSE_LOG timed gathers that waited over
+   250 us on the GPU after their runtime call -- host time of the call and the wait, ns */
+#define FD_PAUSE_LOG 512
+static unsigned long             g_pause[ FD_PAUSE_LOG ][ 2 ];
+static std::atomic<unsigned long> g_pause_n{ 0 };
+
 /* account the timed gathers whose count has been reached */
 static void gather_times( fdgpu_ed25519_ctx_t * ctx, unsigned long gathered ) {
   while( ctx->gt_head < ctx->gt_tail && ctx->gt[ ctx->gt_head % fdgpu_ed25519_ctx_t::NGT ].target <= gathered ) {
@@ -3245,6 +3251,10 @@ static void gather_times( fdgpu_ed25519_ctx_t * ctx, unsigned long gathered ) {
       ctx->gs_issue_sum += sdi;
       if( sdi > ctx->gs_issue_max ) ctx->gs_issue_max = sdi;
       ctx->gs_issue_slow += sdi > 250000UL;
+      if( sdi > 250000UL ) {
+        unsigned long e = g_pause_n.fetch_add( 1UL, std::memory_order_relaxed );
+        if( e < FD_PAUSE_LOG ) { g_pause[e][0] = ti; g_pause[e][1] = sdi; }
+      }
       ctx->gs_n++; ctx->gs_start_sum += sd; ctx->gs_run_sum += rn;
       if( sd > ctx->gs_start_max ) ctx->gs_start_max = sd;
       if( rn > ctx->gs_run_max ) ctx->gs_run_max = rn;
@@ -3415,6 +3425,17 @@ fdgpu_launcher_delete( fdgpu_launcher_t * L ) {
   L->stop.store( 1, std::memory_order_release );
   L->th.join();
   delete L;
+}
+
+extern "C" unsigned long
+fdgpu_debug_gather_pauses( unsigned long * out, unsigned long n, int reset ) {
+  unsigned long m = g_pause_n.load( std::memory_order_acquire );
+  if( m > FD_PAUSE_LOG ) m = FD_PAUSE_LOG;
+  if( m > n ) m = n;
+  for( unsigned long i=0; i<m; i++ ) { out[2*i] = g_pause[i][0]; out[2*i+1] = g_pause[i][1]; }
+  unsigned long tot = g_pause_n.load( std::memory_order_acquire );
+  if( reset ) g_pause_n.store( 0UL, std::memory_order_release );
+  return tot;
 }
 
 extern "C" void

@@ -49,7 +49,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_submit_raw_gather", "fdgpu_ed25519_submit_raw_gather_chk", "fdgpu_ed25519_gather",
            "fdgpu_ed25519_gathered", "fdgpu_ed25519_gather_launched", "fdgpu_ed25519_gather_wait", "fdgpu_host_dev_ptr", "fdgpu_host_register_shared",
            "fdgpu_ed25519_reserve_gather_cus", "fdgpu_ed25519_reserve_cus", "fdgpu_ed25519_set_cu_exclusive", "fdgpu_ed25519_get_cu_exclusive", "fdgpu_ed25519_set_lat_share", "fdgpu_ed25519_gather_stats", "fdgpu_ed25519_phase_stats", "fdgpu_ed25519_prepare", "fdgpu_ed25519_submit_raw_gather_dev", "fdgpu_host_region",
-           "fdgpu_ed25519_dropin_init", "fdgpu_debug_set_opts",
+           "fdgpu_ed25519_dropin_init", "fdgpu_debug_set_opts", "fdgpu_debug_gather_pauses",
            "fdgpu_ed25519_pipeline_state", "fdgpu_ed25519_verify_many_host", "fdgpu_sha512_batch_device", "fdgpu_sha512_batch_host", "fdgpu_ed25519_set_timing", "fdgpu_ed25519_set_small_batch_max", "fdgpu_ed25519_kernel_ms", "fdgpu_mad_peak_per_s",
            "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_slow_count", "fdgpu_ed25519_set_dedup",
            "fdgpu_ed25519_set_record_fp_off", "fdgpu_ed25519_batch_stats", "fdgpu_ed25519_launch_stats", "fdgpu_ed25519_front_remaining", "fdgpu_ed25519_front_batch", "fdgpu_ed25519_verify_txn_ptrs",
@@ -202,6 +202,17 @@ def debug_set_opts(half: int = -1, half_force_slow: int = 0, small_batch_max: in
                   gather_no_writeback=gather_no_writeback, poll_prefetch=poll_prefetch, gather_rpb=gather_rpb,
                   gather_cu_spread=gather_cu_spread, cu_exclusive=cu_exclusive, quad_sha=quad_sha)
     load_library().fdgpu_debug_set_opts(ctypes.byref(o))
+
+
+def gather_pauses(reset: bool = True, n: int = 512) -> tuple[int, list]:
+    """fdgpu_debug_gather_pauses: (how many, [(host ns of the issuing call, ns held on the GPU), ...])."""
+    L = load_library()
+    L.fdgpu_debug_gather_pauses.restype = ctypes.c_ulong
+    L.fdgpu_debug_gather_pauses.argtypes = [ctypes.c_void_p, ctypes.c_ulong, ctypes.c_int]
+    buf = np.zeros(2 * n, np.uint64)
+    tot = int(L.fdgpu_debug_gather_pauses(buf.ctypes.data, n, 1 if reset else 0))
+    m = min(tot, n)
+    return tot, [(int(buf[2 * i]), int(buf[2 * i + 1])) for i in range(m)]
 
 
 def debug_reset_opts() -> None:

@@ -705,6 +705,13 @@ typedef struct fdgpu_debug_opts {
 void
 fdgpu_debug_set_opts( fdgpu_debug_opts_t const * opts );
 
+/* Diagnostics: the GPU pauses seen by this process's gather timing -- up to n of the first 512 timed gathers
+   (any context) that waited over 250 us on the GPU after the runtime call that issued them, as pairs (host
+   CLOCK_MONOTONIC ns of the call, ns waited) in out[2 n].  Returns how many there were (all, not only those
+   copied); reset 1 starts a new log. */
+unsigned long
+fdgpu_debug_gather_pauses( unsigned long * out, unsigned long n, int reset );
+
 /* Last error string of the calling thread (never NULL). */
 char const *
 fdgpu_last_error( void );
