@@ -24,6 +24,10 @@ run_arms() {
 }
 
 case "$job" in
+  pl)
+    # the GPU pause log per paced leg (episodes: start ms, longest hold us, copies), default settings
+    run_arms r05_pl "$Q --stream-only-paced --stream-rates 2e6,5e6,7.5e6,10e6 --stream-paced-seconds 5" "l1=" "l2=" "l3="
+    ;;
   pt)
     # paced tiles: 1 tile x 2 contexts (default) / 2 tiles x 1 context / 2 tiles x 2 contexts (each walk in 1/4)
     run_arms r05_pt "$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3" \
