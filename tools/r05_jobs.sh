@@ -24,6 +24,14 @@ run_arms() {
 }
 
 case "$job" in
+  db)
+    # default bench runs of the final build (the driver's command), each with its detail record
+    mkdir -p gpurun_out/r05_db
+    bash tools/gpu_job.sh \
+      "b1:300:python bench.py --detail-out gpurun_out/r05_db/b1.json > gpurun_out/r05_db/b1.line" \
+      "b2:300:python bench.py --detail-out gpurun_out/r05_db/b2.json > gpurun_out/r05_db/b2.line" \
+      "b3:300:python bench.py --detail-out gpurun_out/r05_db/b3.json > gpurun_out/r05_db/b3.line"
+    ;;
   pl)
     # the GPU pause log per paced leg (episodes: start ms, longest hold us, copies), default settings
     run_arms r05_pl "$Q --stream-only-paced --stream-rates 2e6,5e6,7.5e6,10e6 --stream-paced-seconds 5" "l1=" "l2=" "l3="
