@@ -24,6 +24,14 @@ run_arms() {
 }
 
 case "$job" in
+  tc)
+    # kernel trace of one paced leg at 10M frags/s (the stream child alone, under rocprofv3): the batch chain's
+    # kernels and the dispatch gaps between them (tools/trace_chain.py)
+    d=gpurun_out/r05_tc; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "ktrace:300:rocprofv3 --kernel-trace -f csv -d $d/t -o run -- python bench.py --stream-child --stream-token tc --stream-procs 1 --stream-only-paced --stream-rates 10e6 --stream-paced-seconds 2 > $d/legs.json" \
+      "reduce:200:python tools/trace_chain.py $d > $d/chain.json && rm -rf $d/t"
+    ;;
   db)
     # default bench runs of the final build (the driver's command), each with its detail record
     mkdir -p gpurun_out/r05_db
