@@ -975,20 +975,31 @@ fd_dsm_slow_kernel( u32 nsig, uint4 const * __restrict__ tab, uint4 const * __re
 }
 
 /* Latency half-size path: the slow list after the walks, the result-code
-   procedure first (fd_prep_kernel ran it beside the decodes: S only). */
+   procedure first (fd_prep_kernel ran it beside the decodes: S only).  The 8/4/2-lane walk kernels run it
+   at their end (one kernel less on a batch's chain: a launch costs the chain ~5-10 us, profiles/r05/tc);
+   fd_dsm_slowl_kernel after the one-lane walk.  Thread i of the grid takes entries i, i + grid, ... */
+template<int FM>
+FD_DEV void slowl_tail( u32 nsig, uint4 const * __restrict__ tab, uint4 const * __restrict__ Rxy,
+                        i8 const * __restrict__ digA, short const * __restrict__ digB, uint4 const * __restrict__ btab,
+                        i8 * __restrict__ code, u32 const * __restrict__ slow, u32 const * __restrict__ slow_cnt,
+                        int semantics, unsigned char const * __restrict__ pstat ) {
+  u32 n = *slow_cnt;
+  for( u32 i = blockIdx.x * FD_WG + threadIdx.x; i < n; i += gridDim.x * FD_WG ) {
+    u32 s = slow[i];
+    if( code[s] != FD_PEND_SLOW ) continue;
+    int c = result_code( FD_ED25519_SUCCESS, pstat[2*s], pstat[2*s+1], semantics, 0 );
+    if( c != FD_ED25519_SUCCESS ) { code[s] = (i8)c; continue; }
+    dsm_one<FM>( s, nsig, tab, Rxy, digA, digB, btab, code, (u32 *)0, 0 );
+  }
+}
+
 template<int FM>
 __global__ void __launch_bounds__( FD_WG )
 fd_dsm_slowl_kernel( u32 nsig, uint4 const * __restrict__ tab, uint4 const * __restrict__ Rxy,
                      i8 const * __restrict__ digA, short const * __restrict__ digB, uint4 const * __restrict__ btab,
                      i8 * __restrict__ code, u32 const * __restrict__ slow, u32 const * __restrict__ slow_cnt,
                      int semantics, unsigned char const * __restrict__ pstat ) {
-  u32 i = blockIdx.x * FD_WG + threadIdx.x;
-  if( i >= *slow_cnt ) return;
-  u32 s = slow[i];
-  if( code[s] != FD_PEND_SLOW ) return;
-  int c = result_code( FD_ED25519_SUCCESS, pstat[2*s], pstat[2*s+1], semantics, 0 );
-  if( c != FD_ED25519_SUCCESS ) { code[s] = (i8)c; return; }
-  dsm_one<FM>( s, nsig, tab, Rxy, digA, digB, btab, code, (u32 *)0, 0 );
+  slowl_tail<FM>( nsig, tab, Rxy, digA, digB, btab, code, slow, slow_cnt, semantics, pstat );
 }
 
 /* Half-size path tables: blocks [0,sg) build [0..8](-A) for every pending
@@ -1272,10 +1283,11 @@ FD_DEV void pair_add( fe & E, fe & F, fe & G, fe & H, int h, fe const & m0, fe c
    half-size walk (fd_gpu_lattice.h) Q = [s']B + [c0](-A) + [c1](-R) from
    the wave's top window, -A and -R added in every window, one base-point
    entry per even window ([0..32768]B / 2^120 B), Q == O at the end.
-   Signatures on the slow list (FD_PEND_SLOW) are left to fd_dsm_slowl_kernel. */
+   Signatures on the slow list (FD_PEND_SLOW) are left to slowl_tail (run by fd_dsm2_kernel<.,1> after
+   the walk). */
 template<int FM, int HS>
-__global__ void __launch_bounds__( FD_WG )
-fd_dsm2_kernel( u32                      nsig,
+FD_DEV void
+fd_dsm2_walk( u32                      nsig,
                 uint4 const * __restrict__ tab,
                 uint4 const * __restrict__ Rxy,
                 i8 const *    __restrict__ digA,
@@ -1381,6 +1393,27 @@ fd_dsm2_kernel( u32                      nsig,
   if( !h ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
+template<int FM, int HS>
+__global__ void __launch_bounds__( FD_WG )
+fd_dsm2_kernel( u32                      nsig,
+                uint4 const * __restrict__ tab,
+                uint4 const * __restrict__ Rxy,
+                i8 const *    __restrict__ digA,
+                short const * __restrict__ digB,
+                uint4 const * __restrict__ btab_g,
+                i8 *          __restrict__ code,
+                int                        semantics,
+                unsigned char const * __restrict__ pstat,
+                uint4 const * __restrict__ tabR,
+                i8 const *    __restrict__ digR,
+                uint4 const * __restrict__ btab2,
+                unsigned char const * __restrict__ htop ,
+                u32 const *   __restrict__ slow,
+                u32 const *   __restrict__ slow_cnt ) {
+  fd_dsm2_walk<FM, HS>( nsig, tab, Rxy, digA, digB, btab_g, code, semantics, pstat, tabR, digR, btab2, htop );
+  if constexpr( HS != 0 ) slowl_tail<FM>( nsig, tab, Rxy, digA, digB, btab_g, code, slow, slow_cnt, semantics, pstat );
+}
+
 /* ---- latency path: four lanes per signature -----------------------------
    The same split taken one step further for the smallest batches: the
    four lanes q = 0..3 of a DPP quad share signature s, and every
@@ -1467,8 +1500,8 @@ FD_DEV void quad_add( fe & E, fe & F, fe & G, fe & H, int q, fe const & m, fe co
 }
 
 template<int FM, int HS>
-__global__ void __launch_bounds__( FD_WG )
-fd_dsm4_kernel( u32                      nsig,
+FD_DEV void
+fd_dsm4_walk( u32                      nsig,
                 uint4 const * __restrict__ tab,
                 uint4 const * __restrict__ Rxy,
                 i8 const *    __restrict__ digA,
@@ -1567,6 +1600,27 @@ fd_dsm4_kernel( u32                      nsig,
   if( !q ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
+template<int FM, int HS>
+__global__ void __launch_bounds__( FD_WG )
+fd_dsm4_kernel( u32                      nsig,
+                uint4 const * __restrict__ tab,
+                uint4 const * __restrict__ Rxy,
+                i8 const *    __restrict__ digA,
+                short const * __restrict__ digB,
+                uint4 const * __restrict__ btab_g,
+                i8 *          __restrict__ code,
+                int                        semantics,
+                unsigned char const * __restrict__ pstat,
+                uint4 const * __restrict__ tabR,
+                i8 const *    __restrict__ digR,
+                uint4 const * __restrict__ btab2,
+                unsigned char const * __restrict__ htop ,
+                u32 const *   __restrict__ slow,
+                u32 const *   __restrict__ slow_cnt ) {
+  fd_dsm4_walk<FM, HS>( nsig, tab, Rxy, digA, digB, btab_g, code, semantics, pstat, tabR, digR, btab2, htop );
+  if constexpr( HS != 0 ) slowl_tail<FM>( nsig, tab, Rxy, digA, digB, btab_g, code, slow, slow_cnt, semantics, pstat );
+}
+
 /* ---- latency path: eight lanes per signature (half-size walk) -------------
    For batches that leave SIMDs idle even at four lanes per signature
    (<= FD_DSM8_MAX), the half-size walk's terms are split over two quads:
@@ -1594,8 +1648,8 @@ FD_DEV void fe_from_upper_quad( fe & r, fe const & a ) {   /* lanes 0-3 of a gro
 }
 
 template<int FM>
-__global__ void __launch_bounds__( FD_WG )
-fd_dsm8_kernel( u32                      nsig,
+FD_DEV void
+fd_dsm8_walk( u32                      nsig,
                 uint4 const * __restrict__ tabA,
                 uint4 const * __restrict__ tabR,
                 i8 const *    __restrict__ digA,
@@ -1680,6 +1734,27 @@ fd_dsm8_kernel( u32                      nsig,
   u32 ok = q==0 ? (u32)fe_is_zero( m ) : ( q==1 ? (u32)fe_eq( m, z ) : 1u );
   ok = fd_bcast0( ok ) & fd_bcast1( ok );
   if( !half && !q ) code[s] = ok ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+template<int FM>
+__global__ void __launch_bounds__( FD_WG )
+fd_dsm8_kernel( u32                      nsig,
+                uint4 const * __restrict__ tabA,
+                uint4 const * __restrict__ tabR,
+                i8 const *    __restrict__ digA,
+                i8 const *    __restrict__ digR,
+                short const * __restrict__ digB,
+                uint4 const * __restrict__ btab,
+                uint4 const * __restrict__ btab2,
+                i8 *          __restrict__ code,
+                int                        semantics,
+                unsigned char const * __restrict__ pstat,
+                unsigned char const * __restrict__ htop ,
+                uint4 const * __restrict__ Rxy,
+                u32 const *   __restrict__ slow,
+                u32 const *   __restrict__ slow_cnt ) {
+  fd_dsm8_walk<FM>( nsig, tabA, tabR, digA, digR, digB, btab, btab2, code, semantics, pstat, htop );
+  slowl_tail<FM>( nsig, tabA, Rxy, digA, digB, btab, code, slow, slow_cnt, semantics, pstat );
 }
 
 /* ---- deferred R check (FD_DEFER_R) ---------------------------------------
@@ -2542,17 +2617,17 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
     if( small && lanes==8 )
       hipLaunchKernelGGL( fd_dsm8_kernel<0>, dim3(8*sg), dim3(FD_WG), ctx->excl_lds[2], st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
                           ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->semantics, ctx->d_pstat,
-                          ctx->d_htop );
+                          ctx->d_htop, ctx->d_Rxy, ctx->d_slow, ctx->d_slow + ctx->max_sig );
     else if( small && lanes==4 )
       hipLaunchKernelGGL( (hs ? fd_dsm4_kernel<0,1> : fd_dsm4_kernel<0,0>), dim3(4*sg), dim3(FD_WG),
                           ctx->excl_lds[ hs ? 3 : 4 ], st, nsig, ctx->d_tab,
                           ctx->d_Rxy, ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat,
-                          ctx->d_tabR, ctx->d_digR, ctx->d_btab2, ctx->d_htop );
+                          ctx->d_tabR, ctx->d_digR, ctx->d_btab2, ctx->d_htop, ctx->d_slow, ctx->d_slow + ctx->max_sig );
     else if( small && lanes==2 )
       hipLaunchKernelGGL( (hs ? fd_dsm2_kernel<0,1> : fd_dsm2_kernel<0,0>), dim3(2*sg), dim3(FD_WG),
                           ctx->excl_lds[ hs ? 5 : 6 ], st, nsig, ctx->d_tab,
                           ctx->d_Rxy, ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->semantics, ctx->d_pstat,
-                          ctx->d_tabR, ctx->d_digR, ctx->d_btab2, ctx->d_htop );
+                          ctx->d_tabR, ctx->d_digR, ctx->d_btab2, ctx->d_htop, ctx->d_slow, ctx->d_slow + ctx->max_sig );
     else if( hs )                              /* one lane: the half-size walk, result codes at its start */
       hipLaunchKernelGGL( fd_dsmh_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
                           ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->d_Rxy, ctx->d_slow,
@@ -2585,7 +2660,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       hipLaunchKernelGGL( fd_dsm_kernel<1>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy,
                           ctx->d_digA, ctx->d_digB, ctx->d_btab, code, ctx->d_P, defer );
     if( ctx->timing && !half ) hipEventRecord( ev[2], st );
-    if( hs )                                   /* slow list (normally empty) */
+    if( hs && !( small && lanes > 1 ) )        /* slow list (normally empty); the 8/4/2-lane walks ran it */
       hipLaunchKernelGGL( fd_dsm_slowl_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy, ctx->d_digA,
                           ctx->d_digB, ctx->d_btab, code, ctx->d_slow, ctx->d_slow + ctx->max_sig, ctx->semantics,
                           ctx->d_pstat );

@@ -165,5 +165,23 @@ case "$job" in
       "k10a=" "k2a=--stream-lat-hk-us 2.5" "k5a=--stream-lat-hk-us 5" "k2la=--stream-lat-hk-us 2.5 --stream-lat-launcher 1" \
       "k2lb=--stream-lat-hk-us 2.5 --stream-lat-launcher 1" "k5b=--stream-lat-hk-us 5" "k2b=--stream-lat-hk-us 2.5" "k10b="
     ;;
+  sl)
+    # the latency path's slow list run at the end of the 8/4/2-lane walks (one kernel less on the chain): the
+    # engine-path parity tests, then interleaved A/B against the previous build (build/ab/old: engine + tile)
+    # -- device batch latency (tools/latency_probe.py) and paced legs
+    d=gpurun_out/r05_sl; mkdir -p $d
+    O="FDGPU_LIB=build/ab/old/libfdgpu_ed25519.so FDGPU_VTILE_LIB=build/ab/old/libfdgpu_vtile.so"
+    P="$Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6,12.5e6 --stream-paced-seconds 3"
+    bash tools/gpu_job.sh \
+      "tests:900:python -u -m pytest tests/test_gpu_edges.py tests/test_gpu_parity.py tests/test_gpu_hs_top.py tests/test_gpu_lat_share.py tests/test_gpu_vtile.py tests/test_gpu_stream_parity.py -q -rA --timeout 300 --timeout-method thread" \
+      "lpn1:200:python tools/latency_probe.py 1024 2800 8192 > $d/lpn1.out" \
+      "lpo1:200:env $O python tools/latency_probe.py 1024 2800 8192 > $d/lpo1.out" \
+      "lpn2:200:python tools/latency_probe.py 1024 2800 8192 > $d/lpn2.out" \
+      "lpo2:200:env $O python tools/latency_probe.py 1024 2800 8192 > $d/lpo2.out" \
+      "n1:240:python3 bench.py $P --detail-out $d/n1.json > $d/n1.out" \
+      "o1:240:env $O python3 bench.py $P --detail-out $d/o1.json > $d/o1.out" \
+      "n2:240:python3 bench.py $P --detail-out $d/n2.json > $d/n2.out" \
+      "o2:240:env $O python3 bench.py $P --detail-out $d/o2.json > $d/o2.out"
+    ;;
   *) sed -n '2,8p' "$0"; exit 2 ;;
 esac
