@@ -127,6 +127,34 @@ def test_half_size_slow_list(fa, oracle, every, ntx):
     np.testing.assert_array_equal(s, os_)
 
 
+@pytest.mark.parametrize("every", [1, 5])
+def test_half_size_slow_list_engine_paths(fa, oracle, engine_path, every):
+    """The forced slow list on every engine path at a latency-path batch size (~6K signatures): the 8-, 4-
+    and 2-lane walk kernels verify the list at their end (slowl_tail), the one-lane walk in
+    fd_dsm_slowl_kernel, the throughput path in fd_dsmh_kernel's head blocks.  Every signature (1) or every
+    5th, in adversarial multi-signer batches: codes equal the oracle's, and the list holds the forced
+    signatures that passed the S check."""
+    from conftest import engine_opts
+    from firedancer_amd import engine, synth
+    payload, desc, expect, nsig = synth.make_batch(2500, synth.MULTI, max_signers=4, invalid_frac=0.3,
+                                                   seed=131 + every, threads=16)
+    assert nsig <= 8192                                 # every lane count's batch limit (FD_DSM8_MAX)
+    engine.debug_set_opts(**engine_opts(engine_path, half_force_slow=every))
+    try:
+        eng = fa.Engine(device=0, max_txn=len(desc), max_sig=nsig, max_payload=payload.nbytes)
+    finally:
+        engine.debug_set_opts(**engine_opts(engine_path))
+    try:
+        t, s = eng.verify_txns_host(payload, desc)
+        if engine_path != "throughput_full":        # (a signature whose S check fails never reaches the list)
+            assert (nsig + every - 1) // every // 2 < eng.slow_count() <= (nsig + every - 1) // every
+    finally:
+        eng.close()
+    np.testing.assert_array_equal(t, expect)
+    ot, os_ = oracle.verify_txns(payload, desc, nsig, threads=16)
+    np.testing.assert_array_equal(s, os_)
+
+
 @pytest.mark.parametrize("path", ["throughput", "latency"])
 def test_half_size_no_silent_fallback(fa, path):
     """Hash-distributed k always has a short (c0, c1) within 2^159: a valid batch takes the half-size walk

@@ -183,5 +183,18 @@ case "$job" in
       "n2:240:python3 bench.py $P --detail-out $d/n2.json > $d/n2.out" \
       "o2:240:env $O python3 bench.py $P --detail-out $d/o2.json > $d/o2.out"
     ;;
+  fin)
+    # round-end evidence, second half (the GPU suite and smoke ran in a call of their own, profiles/r05/final5):
+    # tools/gpu_final.sh's bench, rocprof stats and PMC passes
+    tag=final5; d="gpurun_out/prof_$tag"; mkdir -p $d
+    B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
+    P="timeout -s KILL 120 rocprofv3 --kernel-include-regex fd_ -f csv"
+    bash tools/gpu_job.sh \
+      "bench:480:python bench.py --steps 20 --warmup 5 --detail-out $d/bench_detail.json > gpurun_out/bench_$tag.json" \
+      "stats:180:rocprofv3 --kernel-trace --stats -f csv -d $d/stats -o run -- $B > $d/bench_under_rocprof.json" \
+      "pmc_fetch:150:$P --pmc FETCH_SIZE -d $d/fetch -o run -- $B" \
+      "pmc_write:150:$P --pmc WRITE_SIZE -d $d/write -o run -- $B" \
+      "pmc_sq:150:$P --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE -d $d/sq -o run -- $B"
+    ;;
   *) sed -n '2,8p' "$0"; exit 2 ;;
 esac
