@@ -44,6 +44,8 @@ DSM_MAC = DSM_MUL * MAC_PER_MUL + DSM_SQR * MAC_PER_SQR
 HS_MUL, HS_SQR = 128 * 3 + 66 * 8 + 16 * 7, 128 * 4
 HS_MAC = HS_MUL * MAC_PER_MUL + HS_SQR * MAC_PER_SQR
 HALF = os.environ.get("FDGPU_HALF", "1") != "0"
+# A/B: the largest batch that takes the unfolded (FM = 0, two waves per SIMD) throughput walk; -1 the engine's default
+NOFOLD_MAX = int(os.environ.get("FDGPU_NOFOLD_MAX", "-1"))
 WALK_MAC = HS_MAC if HALF else DSM_MAC
 # MI355X_MICROARCH.md: 157.3 TF FP32 vector FMA = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz x 2 flops, i.e. a
 # wave64 VALU instruction issues in 2 cycles per SIMD: 78.6 T lane-instructions/s for the whole chip
@@ -1158,9 +1160,9 @@ def main():
     pay_d = torch.from_numpy(payload).cuda()
     desc_d = torch.from_numpy(desc.view(np.uint8)).cuda()
     out_d = torch.empty(n, dtype=torch.int8, device="cuda")
-    if not HALF:                 # A/B: the full-length walk (the engine's explicit test hook, not an env read)
-        from firedancer_amd import engine as _engine
-        _engine.debug_set_opts(half=0)
+    if not HALF or NOFOLD_MAX >= 0:   # A/B: the full-length walk / the unfolded walk's batch limit (the
+        from firedancer_amd import engine as _engine   # engine's explicit test hook, not an env read)
+        _engine.debug_set_opts(half=1 if HALF else 0, nofold_max=NOFOLD_MAX)
     eng = Engine(device=dev, max_txn=n, max_sig=nsig)
     st = torch.cuda.current_stream().cuda_stream
     # --pipe P: consecutive steps alternate over P engine contexts, each on its own stream, so one batch's

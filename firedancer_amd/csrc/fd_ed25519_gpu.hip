@@ -1027,6 +1027,12 @@ fd_tableh_kernel( u32 nsig, u32 sg, i8 const * __restrict__ code, uint4 const * 
 #ifndef FD_DSMH_MINW
 #define FD_DSMH_MINW 3
 #endif
+/* FD_DSMH_LDS: dynamic LDS (bytes, <= 64 KiB) reserved per workgroup of the throughput walk, which uses none:
+   a cap on its workgroups per CU below the register limit's 3 (A/B: 57344 -> 2 per CU, so a 1M batch's
+   16 waves per SIMD run in 8 full rounds instead of 5 and a lone wave) */
+#ifndef FD_DSMH_LDS
+#define FD_DSMH_LDS 0
+#endif
 template<int FM>
 __global__ void __launch_bounds__( FD_WG, FM ? FD_DSMH_MINW : 1 )
 fd_dsmh_kernel( u32                      nsig,
@@ -2645,7 +2651,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
         hipLaunchKernelGGL( fd_dsm_slow_kernel<0>, dim3(sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_Rxy, ctx->d_digA,
                             ctx->d_digB, ctx->d_btab, code, ctx->d_slow, slow_cnt, nsb * FD_WG );
       } else {
-        hipLaunchKernelGGL( fd_dsmh_kernel<1>, dim3(nsb + sg), dim3(FD_WG), 0, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
+        hipLaunchKernelGGL( fd_dsmh_kernel<1>, dim3(nsb + sg), dim3(FD_WG), FD_DSMH_LDS, st, nsig, ctx->d_tab, ctx->d_tabR, ctx->d_digA,
                             ctx->d_digR, ctx->d_digB, ctx->d_btab, ctx->d_btab2, code, ctx->d_Rxy, ctx->d_slow, slow_cnt, nsb,
                             ctx->d_pstat, ctx->d_htop, 0, ctx->semantics );
         if( ctx->timing ) hipEventRecord( ev[2], st );

@@ -183,6 +183,22 @@ case "$job" in
       "n2:240:python3 bench.py $P --detail-out $d/n2.json > $d/n2.out" \
       "o2:240:env $O python3 bench.py $P --detail-out $d/o2.json > $d/o2.out"
     ;;
+  lw)
+    # the throughput walk's last partial round: a 1M batch is 16 waves per SIMD, which at the register limit's
+    # 3 waves per SIMD run as 5 rounds and a lone wave.  Arms: default; 2 workgroups per CU by an LDS
+    # reservation (build/ab/l2.so, FD_DSMH_LDS=57344: 8 full rounds); the unfolded walk (2 waves per SIMD by
+    # its registers, FDGPU_NOFOLD_MAX)
+    d=gpurun_out/r05_lw; mkdir -p $d
+    H="python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
+    bash tools/gpu_job.sh \
+      "b1:200:$H --detail-out $d/b1.json > $d/b1.out" \
+      "l1:200:FDGPU_LIB=build/ab/l2.so $H --detail-out $d/l1.json > $d/l1.out" \
+      "n1:200:FDGPU_NOFOLD_MAX=2000000 $H --detail-out $d/n1.json > $d/n1.out" \
+      "b2:200:$H --detail-out $d/b2.json > $d/b2.out" \
+      "l2:200:FDGPU_LIB=build/ab/l2.so $H --detail-out $d/l2.json > $d/l2.out" \
+      "n2:200:FDGPU_NOFOLD_MAX=2000000 $H --detail-out $d/n2.json > $d/n2.out" \
+      "ktl:200:FDGPU_LIB=build/ab/l2.so rocprofv3 --kernel-trace --stats -f csv -d $d/kl -o run -- $H > $d/kl.out"
+    ;;
   fin)
     # round-end evidence, second half (the GPU suite and smoke ran in a call of their own, profiles/r05/final5):
     # tools/gpu_final.sh's bench, rocprof stats and PMC passes
