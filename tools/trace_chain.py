@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Reduce a rocprofv3 --kernel-trace CSV of paced stream legs to the batch chain's parts: per kernel, its
 duration; per consecutive pair on one queue, the gap between the first's end and the second's start (the
-dispatch of a dependent kernel; gaps over 1 ms, a queue idle between batches, are left out).
+dispatch of a dependent kernel; gaps over 1 ms, a queue idle between batches, are left out); and per batch,
+its whole chain on its queue: fd_parse_kernel's start to the next fd_done_kernel's end.
 
 usage: trace_chain.py <dir with *kernel_trace.csv>"""
 import collections
@@ -28,9 +29,16 @@ def main():
         for r in csv.DictReader(f):
             name = r["Kernel_Name"].split("(")[0].replace("void ", "")
             q[int(r.get("Queue_Id", 0) or 0)].append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
-    dur, gap = collections.defaultdict(list), collections.defaultdict(list)
+    dur, gap, chain = collections.defaultdict(list), collections.defaultdict(list), []
     for ks in q.values():
         ks.sort()
+        t0 = None
+        for s, e, n in ks:
+            if n == "fd_parse_kernel":
+                t0 = s
+            elif n == "fd_done_kernel" and t0 is not None:
+                chain.append((e - t0) / 1e3)
+                t0 = None
         for i, (s, e, n) in enumerate(ks):
             dur[n].append((e - s) / 1e3)
             if i:
@@ -38,7 +46,7 @@ def main():
                 g = (s - pe) / 1e3
                 if 0 <= g < 1000:
                     gap[f"{pn} -> {n}"].append(g)
-    print(json.dumps({"duration_us": {k: pct(v) for k, v in sorted(dur.items())},
+    print(json.dumps({"chain_us": pct(chain), "duration_us": {k: pct(v) for k, v in sorted(dur.items())},
                       "gap_us": {k: pct(v) for k, v in sorted(gap.items()) if len(v) > 20}}, indent=1))
 
 
