@@ -40,6 +40,14 @@ case "$job" in
       "b2:300:python bench.py --detail-out gpurun_out/r05_db/b2.json > gpurun_out/r05_db/b2.line" \
       "b3:300:python bench.py --detail-out gpurun_out/r05_db/b3.json > gpurun_out/r05_db/b3.line"
     ;;
+  db2)
+    # default bench runs of the last engine build (slow list in the walk kernels), each with its detail record
+    mkdir -p gpurun_out/r05_db2
+    bash tools/gpu_job.sh \
+      "b1:300:python bench.py --detail-out gpurun_out/r05_db2/b1.json > gpurun_out/r05_db2/b1.line" \
+      "b2:300:python bench.py --detail-out gpurun_out/r05_db2/b2.json > gpurun_out/r05_db2/b2.line" \
+      "b3:300:python bench.py --detail-out gpurun_out/r05_db2/b3.json > gpurun_out/r05_db2/b3.line"
+    ;;
   pl)
     # the GPU pause log per paced leg (episodes: start ms, longest hold us, copies), default settings
     run_arms r05_pl "$Q --stream-only-paced --stream-rates 2e6,5e6,7.5e6,10e6 --stream-paced-seconds 5" "l1=" "l2=" "l3="
