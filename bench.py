@@ -354,6 +354,28 @@ def _phases(ph) -> dict:
             "launch_to_last_gather_end_mean": ph[7] / ng * 1e-3 if ph[8] else None}
 
 
+def cpu_place(cpu: int) -> dict | None:
+    """Where a CPU sits: its L3 group (the lowest CPU sharing its L3: one CCD on EPYC) and NUMA node, from sysfs."""
+    if cpu is None or cpu < 0:
+        return None
+    l3 = _cpulist(f"/sys/devices/system/cpu/cpu{cpu}/cache/index3/shared_cpu_list")
+    base = "/sys/devices/system/node"
+    node = next((int(n[4:]) for n in (os.listdir(base) if os.path.isdir(base) else [])
+                 if n.startswith("node") and n[4:].isdigit() and cpu in _cpulist(f"{base}/{n}/cpulist")), None)
+    return {"cpu": cpu, "l3": min(l3) if l3 else None, "node": node}
+
+
+def _pair_place(st: dict) -> dict:
+    """Producer 0 and tile 0 (a paced leg's one link): their CPUs, and whether they share an L3 / a NUMA node --
+    a frag's mcache line and record header cross from the producer's core to the tile's, each a coherence miss
+    that costs more across L3 groups (the tile's intake ns per frag)."""
+    pc = (st.get("prod_cpu") or [-1])[0]
+    tc = (st.get("tile_cpu") or [-1])[0]
+    p, t = cpu_place(pc), cpu_place(tc)
+    same = (lambda k: (p[k] == t[k]) if p and t and p[k] is not None and t[k] is not None else None)
+    return {"producer": p, "tile": t, "same_l3": same("l3"), "same_node": same("node")}
+
+
 def _leg_summary(st: dict, cfg: dict) -> dict:
     n = max(st["verdicts"], 1)
     hist = st["gpu_lat_hist"]
@@ -416,7 +438,9 @@ def _leg_summary(st: dict, cfg: dict) -> dict:
                          "tile_share_min": round(st["tile_cpu_share_min"], 4), "tile_nivcsw": st["tile_nivcsw"],
                          "producer_share": round(st["prod_cpu_ns"] / max(st["prod_wall_ns"], 1), 4),
                          "producer_nivcsw": st["prod_nivcsw"],
-                         "tile_cpus": [c for c in st["tile_cpu"][:min(cfg["tiles"], 8)]]},
+                         "tile_cpus": [c for c in st["tile_cpu"][:min(cfg["tiles"], 8)]],
+                         "producer_cpus": [c for c in (st.get("prod_cpu") or []) if c >= 0],
+                         "producer_tile": _pair_place(st)},
             # the tiles' copy threads (cfg copy_threads): records copied, their ns per frag, overrun after the copy,
             # ns per frag the tile waited for a copy
             "host_copy": ({"records": st["host_copy"][0], "copy_ns_per_frag": round(st["host_copy"][1] / n, 1),
@@ -766,6 +790,11 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 "p99_us": _r(curve[0]["p99_us"]) if curve else None,
                 "unreliable_vs_max": _r(st.get("unreliable_goodput_vs_max"), 3),
                 "tile_host_ns_per_frag": (st.get("max_rate") or {}).get("tile_host_ns_per_frag"),
+                # per paced leg, the tile loop's intake ns per frag, and whether its producer shared the tile's L3
+                # (a host that runs the intake at half speed laps the paced tile from 7.5M on: DESIGN §12)
+                "paced_intake_ns_per_frag": [_r((c.get("tile_host_ns_per_frag") or [None])[0], 3) for c in curve],
+                "paced_producer_tile_same_l3": [((c.get("host_cpu") or {}).get("producer_tile") or {}).get("same_l3")
+                                                for c in curve],
                 "all_published": st.get("all_published"),
                 "host_cpu_share_min": _r(st.get("host_cpu_share_min")),
                 # verdicts neither published nor overrun (none expected in these all-valid streams), and the

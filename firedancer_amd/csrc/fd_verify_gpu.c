@@ -1349,6 +1349,7 @@ typedef struct {
   ulong         t_start;
   ulong         prod_end[ LINK_PROD_MAX ], prod_wait_ns[ LINK_PROD_MAX ];   /* per producer: last publish, credit waits */
   ulong         prod_cpu_ns[ LINK_PROD_MAX ], prod_wall_ns[ LINK_PROD_MAX ], prod_nivcsw[ LINK_PROD_MAX ];
+  long          prod_cpu[ LINK_PROD_MAX ];     /* the CPU each producer was pinned to (-1: none) */
   struct { _Atomic ulong v; uchar pad[56]; } fseq[ LINK_PROD_MAX ][ LINK_TILE_MAX ];   /* per link: next seq each tile may lose */
 } link_hdr_t;
 
@@ -1597,6 +1598,7 @@ static void * link_producer( void * _a ) {
   link_pin( a->cpu );
   fdgpu_link_t * l = a->l;
   link_hdr_t * h = l->h;
+  h->prod_cpu[ a->q ] = a->cpu;
   fdgpu_stream_cfg_t const * c = &h->cfg;
   ulong const q = (ulong)a->q, Q = (ulong)c->producers;
   ulong T = (ulong)c->tiles, mask = h->depth - 1UL, n_q = prod_frags( c->n_frags, Q, q );
@@ -1715,8 +1717,14 @@ static int cpu_busy_sample( double * busy, int ms ) {
   return 0;
 }
 
+/* n CPUs for this process's link threads, in the order producers, tiles, launch threads, copy threads:
+   one hardware thread per core, on the GPU's NUMA node when it has them, idle cores first, filling one L3
+   group (a CCD) after another from group proc (so processes spread).  n_pair: the producers plus tiles --
+   a frag's mcache line and record header move from the producer's core to a tile's, a coherence miss per
+   frag that costs about twice as much across L3 groups -- so the first group taken is the first, from
+   proc's, with n_pair idle cores, when there is one. */
 static int
-link_pick_cpus( int device, int proc, int n, int * out ) {
+link_pick_cpus( int device, int proc, int n, int n_pair, int * out ) {
   char const * env = getenv( "FDGPU_LINK_PIN" );
   if( env && !strcmp( env, "0" ) ) return 0;
   int got = 0;
@@ -1759,9 +1767,15 @@ link_pick_cpus( int device, int proc, int n, int * out ) {
   if( !nc ) return 0;
   int gid[ LINK_CPU_MAX ], ng = 0;                               /* L3 groups in CPU order */
   for( int i=0; i<nc; i++ ) { int k=0; while( k<ng && gid[k] != grp[i] ) k++; if( k==ng ) gid[ng++] = grp[i]; }
+  int r0 = 0;                                                    /* the first group with room for the pairs */
+  for( int r=0; r<ng; r++ ) {
+    int g = gid[ ( proc + r ) % ng ], idle = 0;
+    for( int i=0; i<nc; i++ ) idle += grp[i] == g && !hot[i];
+    if( idle >= n_pair ) { r0 = r; break; }
+  }
   for( int pass=0; pass<2 && got<n; pass++ )                    /* pass 0: idle cores only, then the rest */
     for( int r=0; r<ng && got<n; r++ ) {
-      int g = gid[ ( proc + r ) % ng ];
+      int g = gid[ ( proc + r0 + r ) % ng ];
       for( int i=0; i<nc && got<n; i++ ) {
         if( grp[i] != g || ( pass==0 && hot[i] ) ) continue;
         int dup = 0; for( int k=0; k<got; k++ ) dup |= out[k] == cand[i];
@@ -2062,7 +2076,7 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   int nl = c->launcher ? nt : 0;                 /* the tiles' launch threads: a core each, after the tiles' */
   int H = c->zero_copy && c->copy_threads > 0 ? ( c->copy_threads < FDGPU_VTILE_COPY_THREADS_MAX ? c->copy_threads
                                                                                                   : FDGPU_VTILE_COPY_THREADS_MAX ) : 0;
-  int ncpu = link_pick_cpus( device, proc, nt + np + nl + nt*H, cpus );   /* ... and their copy threads, after those */
+  int ncpu = link_pick_cpus( device, proc, nt + np + nl + nt*H, np + nt, cpus );   /* ... and their copy threads, after those */
   if( getenv( "FDGPU_LINK_VERBOSE" ) ) {
     fprintf( stderr, "fdgpu_link: proc %d device %d numa %d producers %d tiles %d cpus:", proc, device,
              fdgpu_device_numa_node( device ), np, nt );
@@ -2100,6 +2114,7 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     usleep( 1000 );
   }
   memset( st, 0, sizeof(*st) );
+  for( int q=0; q<4; q++ ) st->prod_cpu[q] = -1L;
   ulong * lh = (ulong *)calloc( LH_N, sizeof(ulong) );
   if( !lh ) return -3;
   ulong t_end = 0UL, lmax = 0UL;
@@ -2144,6 +2159,7 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     if( h->prod_end[q] > prod_end ) prod_end = h->prod_end[q];
     st->prod_wait_ns += h->prod_wait_ns[q];
     st->prod_cpu_ns += h->prod_cpu_ns[q]; st->prod_wall_ns += h->prod_wall_ns[q]; st->prod_nivcsw += h->prod_nivcsw[q];
+    if( q < 4 ) st->prod_cpu[q] = h->prod_cpu[q];
   }
   st->seconds = t_end > h->t_start ? (double)( t_end - h->t_start ) * 1e-9 : 0.;
   st->prod_seconds = prod_end > h->t_start ? (double)( prod_end - h->t_start ) * 1e-9 : 0.;

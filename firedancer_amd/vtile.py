@@ -109,14 +109,14 @@ class StreamStats(ctypes.Structure):
                 ("tile_cpu_ns", ctypes.c_ulong), ("tile_wall_ns", ctypes.c_ulong), ("tile_nivcsw", ctypes.c_ulong),
                 ("tile_cpu_share_min", ctypes.c_double), ("tile_cpu", ctypes.c_long * 8),
                 ("prod_cpu_ns", ctypes.c_ulong), ("prod_wall_ns", ctypes.c_ulong), ("prod_nivcsw", ctypes.c_ulong),
-                ("launcher", ctypes.c_ulong * 6), ("host_copy", ctypes.c_ulong * 4)]
+                ("launcher", ctypes.c_ulong * 6), ("host_copy", ctypes.c_ulong * 4), ("prod_cpu", ctypes.c_long * 4)]
 
     def as_dict(self) -> dict:
         out = {}
         for k, _ in self._fields_:
             v = getattr(self, k)
             out[k] = list(v) if k in ("metrics", "tile_ns", "gpu_lat_hist", "prof_ns", "gather_gpu", "phase", "tile_cpu",
-                                      "launcher", "host_copy") else v
+                                      "launcher", "host_copy", "prod_cpu") else v
         return out
 
 

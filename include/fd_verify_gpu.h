@@ -466,6 +466,7 @@ typedef struct fdgpu_stream_stats {
                                     deepest queue (max), pushes that waited for room (summed), longest command (max),
                                     commands over 250 us (summed) */
   unsigned long host_copy[ 4 ];  /* the tiles' copy threads (cfg.copy_threads), fdgpu_vtile_gpu_metrics_t.host_copy summed */
+  long          prod_cpu[ 4 ];   /* the CPUs producers 0..3 were pinned to (-1: none or not run) */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per

@@ -246,3 +246,16 @@ def test_kfd_queues_without_kfd():
         pass
     assert s.peak is None or s.peak["evicted_ms"] >= 0.0
 
+
+
+def test_producer_tile_placement():
+    """_pair_place: the paced link's producer 0 and tile 0 CPUs, their L3 group and NUMA node from sysfs, and
+    whether they share them (None where a CPU is unknown)."""
+    cpus = sorted(os.sched_getaffinity(0))
+    p = bench._pair_place({"prod_cpu": [cpus[0], -1, -1, -1], "tile_cpu": [cpus[0]] + [0] * 7})
+    assert p["producer"]["cpu"] == cpus[0] and p["tile"]["cpu"] == cpus[0]
+    if p["producer"]["l3"] is not None:
+        assert p["same_l3"] is True
+    q = bench._pair_place({"prod_cpu": [-1] * 4, "tile_cpu": [cpus[0]] + [0] * 7})
+    assert q["producer"] is None and q["same_l3"] is None and q["same_node"] is None
+    assert bench.cpu_place(-1) is None

@@ -40,6 +40,15 @@ case "$job" in
       "b2:300:python bench.py --detail-out gpurun_out/r05_db/b2.json > gpurun_out/r05_db/b2.line" \
       "b3:300:python bench.py --detail-out gpurun_out/r05_db/b3.json > gpurun_out/r05_db/b3.line"
     ;;
+  pin)
+    # the link's CPU choice (an L3 group with room for the producer and the tiles) and the producer / tile
+    # placement in each leg: the stream / tile parity tests, then two default bench runs
+    mkdir -p gpurun_out/r05_pin
+    bash tools/gpu_job.sh \
+      "tests:900:python -u -m pytest tests/test_gpu_stream_parity.py tests/test_gpu_stem.py tests/test_gpu_vtile.py -q -rA --timeout 300 --timeout-method thread" \
+      "b1:300:FDGPU_LINK_VERBOSE=1 python bench.py --detail-out gpurun_out/r05_pin/b1.json > gpurun_out/r05_pin/b1.line" \
+      "b2:300:python bench.py --detail-out gpurun_out/r05_pin/b2.json > gpurun_out/r05_pin/b2.line"
+    ;;
   db2)
     # default bench runs of the last engine build (slow list in the walk kernels), each with its detail record
     mkdir -p gpurun_out/r05_db2
