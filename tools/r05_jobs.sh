@@ -40,6 +40,17 @@ case "$job" in
       "b2:300:python bench.py --detail-out gpurun_out/r05_db/b2.json > gpurun_out/r05_db/b2.line" \
       "b3:300:python bench.py --detail-out gpurun_out/r05_db/b3.json > gpurun_out/r05_db/b3.line"
     ;;
+  pz)
+    # GPU pauses without this repository's engine, tile or PyTorch: tools/pauseprobe (plain HIP, a one-wave
+    # kernel every 50 us, its launch -> start delay) idle and under load, around a paced-only bench run
+    d=gpurun_out/r05_pz; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "pi1:60:tools/pauseprobe/pause_probe i 10 50 > $d/pi1.json" \
+      "pb1:60:tools/pauseprobe/pause_probe b 10 50 > $d/pb1.json" \
+      "paced:240:python3 bench.py $Q --stream-only-paced --stream-rates 5e6,7.5e6,10e6 --stream-paced-seconds 5 --detail-out $d/paced.json > $d/paced.out" \
+      "pb2:60:tools/pauseprobe/pause_probe b 10 50 > $d/pb2.json" \
+      "pi2:60:tools/pauseprobe/pause_probe i 10 50 > $d/pi2.json"
+    ;;
   pin)
     # the link's CPU choice (an L3 group with room for the producer and the tiles) and the producer / tile
     # placement in each leg: the stream / tile parity tests, then two default bench runs
