@@ -212,6 +212,10 @@ fd_expand_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 *
   }
 }
 
+/* FD_ATAB_MADD: the table's additions of -A in affine form (A/B knob; 0: the cached-form addition) */
+#ifndef FD_ATAB_MADD
+#define FD_ATAB_MADD 1
+#endif
 /* [0..8](-A) in cached form from A's canonical affine coordinates */
 template<int FM = FD_CARRY_FOLD>
 FD_DEV void atab_build( uint4 * __restrict__ tab, u32 s, uint4 const * __restrict__ Axy ) {
@@ -225,11 +229,19 @@ FD_DEV void atab_build( uint4 * __restrict__ tab, u32 s, uint4 const * __restric
   ge_cached c1, c;
   ge_p3_to_cached<FM>( c1, A );
   atab_store( tab, s, 1, c1 );
+#if FD_ATAB_MADD
+  /* -A has Z = 1: each step adds it in affine form (ge_add_precomp: 3 multiplications instead of 4) */
+  ge_precomp a1; a1.ypx = c1.YpX; a1.ymx = c1.YmX; a1.xy2d = c1.T2d;
+#endif
   ge_p3 cur = A;
 #pragma unroll 1
   for( int e=2; e<FD_ATAB_ENTRIES; e++ ) {
     ge_p1p1 tt;
+#if FD_ATAB_MADD
+    ge_add_precomp<FM>( tt, cur, a1 );
+#else
     ge_add_cached<FM>( tt, cur, c1 );
+#endif
     ge_p1p1_to_p3<FM>( cur, tt );
     ge_p3_to_cached<FM>( c, cur );
     atab_store( tab, s, e, c );

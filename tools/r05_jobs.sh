@@ -40,6 +40,24 @@ case "$job" in
       "b2:300:python bench.py --detail-out gpurun_out/r05_db/b2.json > gpurun_out/r05_db/b2.line" \
       "b3:300:python bench.py --detail-out gpurun_out/r05_db/b3.json > gpurun_out/r05_db/b3.line"
     ;;
+  ma)
+    # the -A / -R table's additions in affine form (FD_ATAB_MADD=1, now the default) vs the cached form
+    # (build/ab/cadd.so): engine-path parity tests, then interleaved headline runs and a kernel trace of each
+    d=gpurun_out/r05_ma; mkdir -p $d
+    H="python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
+    bash tools/gpu_job.sh \
+      "tests:900:python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_edges.py tests/test_gpu_hs_top.py tests/test_gpu_torsion.py -q -rA --timeout 300 --timeout-method thread" \
+      "m1:200:$H --detail-out $d/m1.json > $d/m1.out" \
+      "c1:200:FDGPU_LIB=build/ab/cadd.so $H --detail-out $d/c1.json > $d/c1.out" \
+      "m2:200:$H --detail-out $d/m2.json > $d/m2.out" \
+      "c2:200:FDGPU_LIB=build/ab/cadd.so $H --detail-out $d/c2.json > $d/c2.out" \
+      "m3:200:$H --detail-out $d/m3.json > $d/m3.out" \
+      "c3:200:FDGPU_LIB=build/ab/cadd.so $H --detail-out $d/c3.json > $d/c3.out" \
+      "km:200:rocprofv3 --kernel-trace --stats -f csv -d $d/km -o run -- $H > $d/km.out" \
+      "kc:200:FDGPU_LIB=build/ab/cadd.so rocprofv3 --kernel-trace --stats -f csv -d $d/kc -o run -- $H > $d/kc.out" \
+      "lm:200:python tools/latency_probe.py 1024 2800 8192 > $d/lm.out" \
+      "lc:200:FDGPU_LIB=build/ab/cadd.so python tools/latency_probe.py 1024 2800 8192 > $d/lc.out"
+    ;;
   pz)
     # GPU pauses without this repository's engine, tile or PyTorch: tools/pauseprobe (plain HIP, a one-wave
     # kernel every 50 us, its launch -> start delay) idle and under load, around a paced-only bench run
