@@ -247,8 +247,13 @@ case "$job" in
     ;;
   fin)
     # round-end evidence, second half (the GPU suite and smoke ran in a call of their own, profiles/r05/final5):
-    # tools/gpu_final.sh's bench, rocprof stats and PMC passes
-    tag=final5; d="gpurun_out/prof_$tag"; mkdir -p $d
+    # tools/gpu_final.sh's bench, rocprof stats and PMC passes (TAG=final7: the GPU suite and smoke first)
+    tag=${TAG:-final5}; d="gpurun_out/prof_$tag"; mkdir -p $d
+    if [ -n "$TAG" ]; then
+      bash tools/gpu_job.sh \
+        "tests:900:python -u -m pytest tests -m gpu -q -rA --timeout 300 --timeout-method thread" \
+        "smoke:200:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" || exit $?
+    fi
     B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
     P="timeout -s KILL 120 rocprofv3 --kernel-include-regex fd_ -f csv"
     bash tools/gpu_job.sh \
