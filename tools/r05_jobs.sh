@@ -78,13 +78,14 @@ case "$job" in
       "b1:300:FDGPU_LINK_VERBOSE=1 python bench.py --detail-out gpurun_out/r05_pin/b1.json > gpurun_out/r05_pin/b1.line" \
       "b2:300:python bench.py --detail-out gpurun_out/r05_pin/b2.json > gpurun_out/r05_pin/b2.line"
     ;;
-  db2)
-    # default bench runs of the last engine build (slow list in the walk kernels), each with its detail record
-    mkdir -p gpurun_out/r05_db2
+  db2|db3)
+    # default bench runs of the last engine build (db2: slow list in the walk kernels; db3: the final build),
+    # each with its detail record
+    o=gpurun_out/r05_$job; mkdir -p $o
     bash tools/gpu_job.sh \
-      "b1:300:python bench.py --detail-out gpurun_out/r05_db2/b1.json > gpurun_out/r05_db2/b1.line" \
-      "b2:300:python bench.py --detail-out gpurun_out/r05_db2/b2.json > gpurun_out/r05_db2/b2.line" \
-      "b3:300:python bench.py --detail-out gpurun_out/r05_db2/b3.json > gpurun_out/r05_db2/b3.line"
+      "b1:300:python bench.py --detail-out $o/b1.json > $o/b1.line" \
+      "b2:300:python bench.py --detail-out $o/b2.json > $o/b2.line" \
+      "b3:300:python bench.py --detail-out $o/b3.json > $o/b3.line"
     ;;
   pl)
     # the GPU pause log per paced leg (episodes: start ms, longest hold us, copies), default settings
