@@ -843,6 +843,20 @@ def _free_port() -> int:
     return p
 
 
+class _stdout_to_stderr:
+    """fd 1 -> fd 2 for the block (C++ libraries' prints, e.g. gloo's "[Gloo] Rank r is connected ..." at
+    init_process_group, which torchrun passes through on the ranks' shared stdout)."""
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def launch_ranks(n: int, argv: list[str], script: str | None = None, timeout_s: float = 3000.0) -> int:
     """`bench.py --gpus N` without torchrun: start N rank processes of this script, one per GPU, with the
     torch.distributed env (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), as the
@@ -895,7 +909,8 @@ def dry_run_main(args) -> None:
     from firedancer_amd import shard
     rank, world, _ = rank_env(args.gpus)
     if world > 1:
-        dist.init_process_group("gloo")
+        with _stdout_to_stderr():
+            dist.init_process_group("gloo")
     dd = dist if world > 1 else None
     nsig = args.txns
 
@@ -1090,7 +1105,8 @@ def main():
     # The data path has no collective (independent shards); the measurement reductions (MAX of time, MIN of
     # the results flag, SUM of signatures) are a few scalars, so they go over gloo on CPU tensors: no RCCL.
     if world > 1:
-        dist.init_process_group("gloo")
+        with _stdout_to_stderr():       # gloo's connection notes: stdout carries only rank 0's bench line
+            dist.init_process_group("gloo")
     dd = dist if world > 1 else None
 
     def barrier():
