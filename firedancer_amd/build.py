@@ -43,13 +43,26 @@ def build_synth(force: bool = False) -> str:
 
 
 def build_vtile(force: bool = False) -> str:
-    """libfdgpu_vtile.so: the verify tile over the engine (host C, links libfdgpu_ed25519.so)."""
+    """libfdgpu_vtile.so: the verify tile and the verify service over the engine (host C, links libfdgpu_ed25519.so)."""
     out = os.path.join(PKG, "libfdgpu_vtile.so")
     eng = os.path.join(PKG, "libfdgpu_ed25519.so")
-    if force or _stale(out, ["fd_verify_gpu.c", "../../include/fd_verify_gpu.h", "../../include/fd_ed25519_gpu.h"]) \
+    if force or _stale(out, ["fd_verify_gpu.c", "fd_vsvc.c", "fd_vsvc_private.h", "../../include/fd_verify_gpu.h",
+                             "../../include/fd_ed25519_gpu.h"]) \
             or os.path.getmtime(eng) > os.path.getmtime(out):
         subprocess.run(["gcc", "-std=gnu11", "-O2", "-fPIC", "-shared", "-pthread", "-Wall", "-Wextra",
-                        "-o", out, os.path.join(CSRC, "fd_verify_gpu.c"), eng, "-Wl,-rpath,$ORIGIN"], check=True)
+                        "-o", out, os.path.join(CSRC, "fd_verify_gpu.c"), os.path.join(CSRC, "fd_vsvc.c"), eng,
+                        "-Wl,-rpath,$ORIGIN"], check=True)
+    return out
+
+
+def build_tile_prog(force: bool = False) -> str:
+    """fdgpu_tile: a served verify tile as a program of its own (fd_vtile_main.c over libfdgpu_vtile.so); the verify
+    service's process starts one per tile (fdgpu_link_run with cfg.svc)."""
+    out = os.path.join(PKG, "fdgpu_tile")
+    lib = os.path.join(PKG, "libfdgpu_vtile.so")
+    if force or _stale(out, ["fd_vtile_main.c", "../../include/fd_verify_gpu.h"]) or os.path.getmtime(lib) > os.path.getmtime(out):
+        subprocess.run(["gcc", "-std=gnu11", "-O2", "-Wall", "-Wextra", "-o", out, os.path.join(CSRC, "fd_vtile_main.c"),
+                        lib, "-Wl,-rpath,$ORIGIN"], check=True)
     return out
 
 
@@ -68,6 +81,7 @@ def build_all(force: bool = False) -> None:
     build_lattice_host(force)
     build_engine(force)
     build_vtile(force)
+    build_tile_prog(force)
 
 
 if __name__ == "__main__":

@@ -1945,6 +1945,16 @@ fd_reduce_kernel( fdgpu_txn_desc_t const * __restrict__ desc, u32 txn_cnt, u32 n
   txn_out[t] = (i8)txn_code( desc[t], t, nsig, code, pflag );
 }
 
+struct fd_gather {             /* mode 3: copy sz bytes from src (host, device view) to arena / region offset dst */
+  unsigned long src;
+  unsigned int  dst;
+  unsigned int  sz;            /* multiple of 16; bit 31: no write-back (the caller copies the record itself) */
+  unsigned long seq_addr;      /* device view of the frag's in-mcache line seq word, 0 = no overrun check */
+  unsigned long seq;           /* the seq that line held when the tile took the frag */
+  unsigned long wb;            /* per-record batches (fdgpu_ed25519_submit_raw_gather_to): device view of the record's
+                                  place in its own out region; 0 = the batch's region at offset dst */
+};
+
 /* The async raw batches' last work kernel (fdgpu_ed25519_submit_raw*): the reduce, then every result
    straight into the slot's pinned host arrays (device views), so no copy commands follow the batch.
    Blocks [0, tg): one thread per transaction writes its code, footprint and dedup tag (consecutive
@@ -1960,7 +1970,7 @@ fd_finish_kernel( fdgpu_txn_desc_t const * __restrict__ desc, fdgpu_txn_raw_t co
                   unsigned char const * __restrict__ img, u32 stride,
                   i8 * __restrict__ h_out, unsigned short * __restrict__ h_fp, u64 * __restrict__ h_dtag,
                   unsigned char * __restrict__ out_region, int rec_fp_off, unsigned char * __restrict__ h_img,
-                  u32 tg, unsigned char const * __restrict__ arena ) {
+                  u32 tg, unsigned char const * __restrict__ arena, fd_gather const * __restrict__ grec ) {
   if( blockIdx.x < tg ) {
     u32 t = blockIdx.x * FD_WG + threadIdx.x;
     if( t >= txn_cnt ) return;
@@ -1975,17 +1985,20 @@ fd_finish_kernel( fdgpu_txn_desc_t const * __restrict__ desc, fdgpu_txn_raw_t co
   u32 n = fp[u];
   if( !n ) return;
   unsigned char * dst;
-  if( out_region ) {
+  if( out_region || grec ) {
     fdgpu_txn_raw_t r = raw[u];
-    u32 rec = r.payload_off - (u32)r._pad[0];        /* the record's offset in the arena and in the out region */
-    dst = out_region + ( ( r.payload_off + (u32)r.payload_sz + 1u ) & ~1u );
+    u32 rec = r.payload_off - (u32)r._pad[0];        /* the record's offset in the arena (and in the out region) */
+    /* where the record lies on the host: at rec in the batch's out region, or (per-record batches, grec) at
+       its own place, which the gather record carries */
+    unsigned char * rb = grec ? (unsigned char *)grec[u].wb : out_region + rec;
+    dst = rb + ( ( (u32)r._pad[0] + (u32)r.payload_sz + 1u ) & ~1u );
     if( arena ) {
       /* the record's write-back into the out region, deferred from its gather to here (the gather then
          only reads over PCIe): header + payload exactly as copied at gather time -- whole 16-B pieces,
          then the tail bytes, so nothing lands where the fd_txn_t goes -- with txn_t_sz set */
       u32 end = r.payload_off + (u32)r.payload_sz - rec, n16 = end >> 4;
       uint4 const * a = (uint4 const *)( arena + rec );
-      uint4 * o = (uint4 *)( out_region + rec );
+      uint4 * o = (uint4 *)rb;
       uint4 w0 = make_uint4( 0u, 0u, 0u, 0u ), w1 = w0;
       if( lane < n16 ) w0 = a[lane];
       if( lane + 64u < n16 ) w1 = a[lane + 64u];
@@ -1994,13 +2007,13 @@ fd_finish_kernel( fdgpu_txn_desc_t const * __restrict__ desc, fdgpu_txn_raw_t co
       if( lane < n16 ) o[lane] = w0;
       if( lane + 64u < n16 ) o[lane + 64u] = w1;
       for( u32 i=lane+128u; i<n16; i+=64u ) o[i] = a[i];      /* (records past 2 KB: none from a tile) */
-      for( u32 b=( n16 << 4 ) + lane; b<end; b+=64u ) out_region[ rec + b ] = arena[ rec + b ];
+      for( u32 b=( n16 << 4 ) + lane; b<end; b+=64u ) rb[ b ] = arena[ rec + b ];
       if( !fix && rec_fp_off >= 0 && lane==0u ) {
         __builtin_amdgcn_s_waitcnt( 0 );                     /* (after this lane's own copy stores) */
-        *(unsigned short *)( out_region + rec + (u32)rec_fp_off ) = (unsigned short)n;
+        *(unsigned short *)( rb + (u32)rec_fp_off ) = (unsigned short)n;
       }
     } else if( rec_fp_off >= 0 && lane==0u )
-      *(unsigned short *)( out_region + rec + (u32)rec_fp_off ) = (unsigned short)n;
+      *(unsigned short *)( rb + (u32)rec_fp_off ) = (unsigned short)n;
   } else dst = h_img + (size_t)u*stride;
   unsigned short const * s16 = (unsigned short const *)( img + (size_t)u*stride );
   unsigned short v[ 7 ];                          /* up to 852 B: 426 shorts, 7 per lane, all loads first */
@@ -2043,6 +2056,11 @@ FD_DEV u64 fd_xxh64_64( u64 seed, unsigned char const * p ) {
   return h;
 }
 
+/* the HA dedup seeds of a batch (kernel argument): seed[0], or with nseed > 0 seed[ the record's seed index ]
+   (the verify service's batches hold several tiles' frags, each tile with its own secure seed,
+   fd_verify_tile.c:166) */
+struct fd_seeds { u64 seed[ 16 ]; u32 nseed; };
+
 __global__ void __launch_bounds__( FD_WG )
 fd_parse_kernel( unsigned char const *    __restrict__ payload,
                  fdgpu_txn_raw_t const *  __restrict__ raw,
@@ -2052,7 +2070,7 @@ fd_parse_kernel( unsigned char const *    __restrict__ payload,
                  unsigned char *          __restrict__ img,
                  u32                                    img_stride,
                  unsigned short *         __restrict__ fp_out,
-                 u64                                    dedup_seed,
+                 fd_seeds                               dseeds,
                  u64 *                    __restrict__ dtag_out,
                  unsigned char const *    __restrict__ ovr,
                  u32 *                    __restrict__ map,       /* fused fd_expand_kernel (async batches), or NULL */
@@ -2084,7 +2102,10 @@ fd_parse_kernel( unsigned char const *    __restrict__ payload,
   if( fp_out ) fp_out[t] = (unsigned short)fp;
   /* the HA dedup tag of a parsed transaction (its first signature), so the
      tile's after_frag never reads the payload */
-  if( dtag_out ) dtag_out[t] = fp ? fd_xxh64_64( dedup_seed, payload + r.payload_off + h.sig_off ) : 0UL;
+  if( dtag_out ) {
+    u64 seed = dseeds.nseed ? dseeds.seed[ r._pad[1] & 15u ] : dseeds.seed[0];
+    dtag_out[t] = fp ? fd_xxh64_64( seed, payload + r.payload_off + h.sig_off ) : 0UL;
+  }
   if( !desc_out ) return;
   fdgpu_txn_desc_t d;
   d.payload_off = r.payload_off; d.sig_base = r.sig_base;
@@ -2160,13 +2181,6 @@ __global__ void fd_stamp_kernel( unsigned long * stamp ) {
   __hip_atomic_store( stamp, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
 }
 
-struct fd_gather {             /* mode 3: copy sz bytes from src (host, device view) to arena / region offset dst */
-  unsigned long src;
-  unsigned int  dst;
-  unsigned int  sz;            /* multiple of 16; bit 31: no write-back (the caller copies the record itself) */
-  unsigned long seq_addr;      /* device view of the frag's in-mcache line seq word, 0 = no overrun check */
-  unsigned long seq;           /* the seq that line held when the tile took the frag */
-};
 
 /* Gathered raw batches (fdgpu_ed25519_submit_raw_gather) -- the GPU side of
    the stem's during_frag copy (src/disco/stem/fd_stem.c:667-686): one
@@ -2207,7 +2221,8 @@ fd_gather_kernel( fd_gather const * __restrict__ g, u32 n, unsigned char * __res
   fd_gather r = g[ rec ];
   uint4 const * src = (uint4 const *)r.src;
   uint4 * a = (uint4 *)( arena + r.dst );
-  uint4 * o = (uint4 *)( out + r.dst );
+  uint4 * o = r.wb ? (uint4 *)r.wb : (uint4 *)( out + r.dst );   /* (per-record batches: the record's own place) */
+  if( r.wb ) out = (unsigned char *)r.wb;
   if( r.sz >> 31 ) out = NULL;                              /* FDGPU_GATHER_NO_WRITEBACK: the host copies it */
   u32 n16 = ( r.sz & 0x7fffffffu ) >> 4;
   if( n16 <= 128u ) {          /* every fd_txn_m_t record (<= 80 + 1232 bytes): all loads, the re-check, then stores */
@@ -2304,6 +2319,8 @@ struct fd_slot {               /* one in-flight host batch of the async pipeline
   unsigned char const * ref_base; /* mode 2, 3: the caller's pinned region; payloads at [ref_lo, ref_hi) */
   size_t             ref_lo, ref_hi;
   unsigned char *    ref_dev;  /* mode 3: the device address of ref_base (the gather kernel writes the records back) */
+  int                per_rec;  /* mode 3: records go back to places of their own (fdgpu_ed25519_submit_raw_gather_to;
+                                  ref_base unused, arena offsets allocated in submission order) */
   struct fd_gather * h_gat;    /* mode 3: one gather record per transaction (pinned; the kernel reads it over PCIe) */
   struct fd_gather * g_dev;    /*         its device view */
   unsigned char *    d_ovr;    /*         per transaction: 1 = overrun while gathered */
@@ -2374,8 +2391,11 @@ struct fdgpu_ed25519_ctx {
   fd_slot slot[ NSLOT ];
   int cur;                       /* slot being filled */
   int fault;                     /* a batch failed on the device: the pipeline refuses new work */
+  int dbg_fail_issue;            /* test hook (fdgpu_ed25519_debug_fail_launch): the launch thread fails batch launches */
   int dedup;                     /* raw batches also return HA dedup tags (fdgpu_ed25519_set_dedup) */
   unsigned long dedup_seed;
+  unsigned long dedup_seeds[ 16 ];   /* fdgpu_ed25519_set_dedup_seeds: per-record seeds (verify service) */
+  int           dedup_nseed;
   int rec_fp_off;                /* gathered records: offset of a u16 footprint field, -1 = none */
   hipStream_t gstream;           /* gathered batches: the copies (fd_gather_kernel), ahead of the batch's kernels */
   hipEvent_t  gev;               /*   recorded behind a batch's last gather; the ctx stream waits for it */
@@ -3229,7 +3249,7 @@ fdgpu_txn_parse_device( unsigned char const * d_payload, fdgpu_txn_raw_t const *
   if( txn_cnt >= (1UL<<31) || ( d_img && ( img_stride < 852UL || img_stride > 0xffffffffUL ) ) ) { fd_err = "bad arguments"; return -1; }
   unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
   hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, (hipStream_t)stream, d_payload, d_raw, (u32)txn_cnt,
-                      (fdgpu_txn_desc_t *)NULL, (unsigned char *)NULL, d_img, (u32)img_stride, d_fp, 0UL, (u64 *)NULL,
+                      (fdgpu_txn_desc_t *)NULL, (unsigned char *)NULL, d_img, (u32)img_stride, d_fp, fd_seeds{}, (u64 *)NULL,
                       (unsigned char const *)NULL , (u32 *)NULL, 0u, (u32 *)NULL, (unsigned long *)NULL);
   HIPCHK( hipGetLastError(), -3 );
   return 0;
@@ -3243,8 +3263,12 @@ static int launch_raw( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payloa
                        unsigned char const * d_ovr = NULL, int fused = 0, unsigned long * stamp = NULL ) {
   if( !txn_cnt ) return 0;
   unsigned g = (unsigned)( (txn_cnt + FD_WG - 1) / FD_WG );
+  fd_seeds ds;
+  memset( &ds, 0, sizeof(ds) );
+  ds.seed[0] = (u64)ctx->dedup_seed;
+  if( ctx->dedup_nseed ) { memcpy( ds.seed, ctx->dedup_seeds, sizeof(ds.seed) ); ds.nseed = (u32)ctx->dedup_nseed; }
   hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, st, d_payload, d_raw, (u32)txn_cnt,
-                      ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp, (u64)ctx->dedup_seed, d_dtag, d_ovr,
+                      ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp, ds, d_dtag, d_ovr,
                       fused ? ctx->d_map : (u32 *)NULL, (u32)sig_cnt, fused ? ctx->d_slow + ctx->max_sig : (u32 *)NULL,
                       stamp );
   HIPCHK( hipGetLastError(), -3 );
@@ -3406,7 +3430,7 @@ static long gather_prep( fdgpu_ed25519_ctx_t * ctx, fd_slot & sl, fd_gargs * a )
     ctx->last_gt = (long)i;
   } else { gt = ctx->d_gtime + 2*fdgpu_ed25519_ctx_t::NGT; ctx->last_gt = -1; }   /* untimed: a scratch entry */
   a->g = sl.g_dev + sl.gathered; a->n = (u32)n; a->d_payload = sl.d_payload;
-  a->wb = ctx->gather_nowb == 0 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL;
+  a->wb = ctx->gather_nowb == 0 && !sl.per_rec ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL;
   a->ovr = sl.d_ovr + sl.gathered; a->target = target; a->gt = gt; a->gti = ctx->last_gt;
   ctx->g_launched = target; sl.gathered = sl.txn_cnt;
   return (long)n;
@@ -3472,7 +3496,10 @@ static void launcher_main( fdgpu_launcher_t * L ) {
     fd_lcmd const & c = L->cmd[ h % fdgpu_launcher::NCMD ];
     unsigned long t0 = fd_now_ns();
     if( !__atomic_load_n( &c.ctx->fault, __ATOMIC_ACQUIRE ) ) {
-      int rc = c.kind == 0 ? gather_issue( c.ctx, &c.g ) : slot_issue( c.ctx, c.slot, c.token, c.has_g ? &c.g : NULL );
+      int rc;
+      if( c.kind != 0 && __atomic_load_n( &c.ctx->dbg_fail_issue, __ATOMIC_ACQUIRE ) ) {   /* test hook */
+        fd_err = "slot_issue: injected by fdgpu_ed25519_debug_fail_launch"; rc = -2;
+      } else rc = c.kind == 0 ? gather_issue( c.ctx, &c.g ) : slot_issue( c.ctx, c.slot, c.token, c.has_g ? &c.g : NULL );
       if( rc ) {
         snprintf( c.ctx->lerr, sizeof(c.ctx->lerr), "launch thread: %s", fd_err.c_str() );
         __atomic_store_n( &c.ctx->fault, 1, __ATOMIC_RELEASE );
@@ -3599,9 +3626,10 @@ static int slot_issue( fdgpu_ed25519_ctx_t * ctx, int i, unsigned long token, fd
                         (u32)sl.txn_cnt, (u32)sl.sig_cnt, ctx->d_code, ctx->d_pflag, sl.d_fp,
                         ctx->dedup ? (u64 const *)sl.d_dtag : (u64 const *)NULL, sl.d_img, (u32)FDGPU_TXN_IMG_STRIDE,
                         sl.hd_txn_out, sl.hd_fp, ctx->dedup ? (u64 *)sl.hd_dtag : (u64 *)NULL,
-                        sl.mode==3 ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, ctx->rec_fp_off,
+                        sl.mode==3 && !sl.per_rec ? sl.ref_dev + sl.ref_lo : (unsigned char *)NULL, ctx->rec_fp_off,
                         sl.mode==3 ? (unsigned char *)NULL : sl.hd_img, tg,
-                        sl.mode==3 && ctx->gather_nowb == 2 ? (unsigned char const *)sl.d_payload : (unsigned char const *)NULL );
+                        sl.mode==3 && ctx->gather_nowb == 2 ? (unsigned char const *)sl.d_payload : (unsigned char const *)NULL,
+                        sl.mode==3 && sl.per_rec ? (fd_gather const *)sl.g_dev : (fd_gather const *)NULL );
     HIPCHK( hipGetLastError(), -2 );
   } else {
     HIPCHK( hipMemcpyAsync( sl.d_desc, sl.h_desc, sl.txn_cnt * sizeof(fdgpu_txn_desc_t), hipMemcpyHostToDevice, st ), -2 );
@@ -4002,31 +4030,62 @@ static int submit_gather( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, 
                           unsigned flags ) {
   unsigned b0 = payload_sz ? src[ payload_off ] : 0u;
   unsigned lanes = ( b0 >= 1u && b0 <= 16u ) ? b0 : 0u;
-  size_t off = (size_t)( dst - dst_base );
+  /* per-record (dst_base NULL): the record goes back to dst_dev, a place of its own; its arena offset is
+     the next free one of the batch.  Else its arena offset mirrors its offset in the batch's out region. */
+  int per_rec = !dst_base;
+  size_t off = per_rec ? 0UL : (size_t)( dst - dst_base );
   int rc; fd_slot * sl = slot_for( ctx, csz, lanes, 3, &rc );
   if( !sl ) return rc;
-  if( sl->txn_cnt && ( sl->ref_base != dst_base || off < sl->ref_hi || off + csz - sl->ref_lo + 8UL > ctx->max_payload ) ) {
+  if( sl->txn_cnt && ( sl->per_rec != per_rec ||
+                       ( !per_rec && ( sl->ref_base != dst_base || off < sl->ref_hi ||
+                                       off + csz - sl->ref_lo + 8UL > ctx->max_payload ) ) ) ) {
     if( ( rc = fdgpu_ed25519_flush( ctx ) ) ) return rc;
     if( !( sl = slot_for( ctx, csz, lanes, 3, &rc ) ) ) return rc;
   }
   if( slot_raw_bufs( ctx, sl ) ) return -3;
   if( !sl->txn_cnt ) {
-    unsigned char * d = region_dev( dst_base, 1UL );
-    if( !d ) { fd_err = "fdgpu_ed25519_submit_raw_gather: dst_base not from fdgpu_host_alloc"; return -3; }
-    sl->ref_base = dst_base; sl->ref_dev = d; sl->ref_lo = off;
+    sl->per_rec = per_rec;
+    if( per_rec ) { sl->ref_base = NULL; sl->ref_dev = NULL; sl->ref_lo = 0UL; sl->ref_hi = 0UL; }
+    else {
+      unsigned char * d = region_dev( dst_base, 1UL );
+      if( !d ) { fd_err = "fdgpu_ed25519_submit_raw_gather: dst_base not from fdgpu_host_alloc"; return -3; }
+      sl->ref_base = dst_base; sl->ref_dev = d; sl->ref_lo = off;
+    }
   }
+  if( per_rec ) off = sl->ref_hi;                /* (arena offsets stay 16-B aligned: csz is) */
   fdgpu_txn_raw_t & r = ((fdgpu_txn_raw_t *)sl->h_desc)[ sl->txn_cnt ];
   r.payload_off = (unsigned)( off - sl->ref_lo + payload_off ); r.sig_base = (unsigned)sl->sig_cnt;
   r.payload_sz = payload_sz; r.sig_lanes = (unsigned char)lanes;
   r._pad[0] = (unsigned char)payload_off;      /* fd_img_scatter_kernel finds the record header from it */
+  r._pad[1] = (unsigned char)( ( flags >> 8 ) & 15u );   /* its HA dedup seed (FDGPU_GATHER_SEED) */
   fd_gather & g = sl->h_gat[ sl->txn_cnt ];
   g.src = (unsigned long)dsrc; g.dst = (unsigned)( off - sl->ref_lo );
-  g.sz = (unsigned)csz | ( ( flags & FDGPU_GATHER_NO_WRITEBACK ) ? 0x80000000u : 0u );
+  /* a per-record batch writes its records back at the gather unless the write-back is off or deferred to the
+     finish kernel (fdgpu_debug_opts_t.gather_no_writeback, whose A/B applies to both forms) */
+  unsigned nowb = ( flags & FDGPU_GATHER_NO_WRITEBACK ) || ( per_rec && ctx->gather_nowb );
+  g.sz = (unsigned)csz | ( nowb ? 0x80000000u : 0u );
   g.seq_addr = (unsigned long)dseq; g.seq = seq;
+  g.wb = per_rec ? (unsigned long)dst : 0UL;
   sl->h_tags[ sl->txn_cnt ] = tag;
   sl->txn_cnt++; sl->sig_cnt += lanes;
   sl->ref_hi = off + csz; sl->payload_used = sl->ref_hi - sl->ref_lo;
   return 0;
+}
+
+extern "C" int
+fdgpu_ed25519_submit_raw_gather_to( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src, unsigned char const * src_dev,
+                                    unsigned char * dst_dev, unsigned short copy_sz, unsigned short payload_off,
+                                    unsigned short payload_sz, unsigned long tag, unsigned long const * seq_dev,
+                                    unsigned long seq, unsigned flags ) {
+  if( (unsigned)payload_off + payload_sz > copy_sz || ( (uintptr_t)src & 15 ) || ( (uintptr_t)src_dev & 15 ) ||
+      !dst_dev || ( (uintptr_t)dst_dev & 15 ) ||
+      ( ctx->rec_fp_off >= 0 && ( payload_off > 255u || (unsigned)ctx->rec_fp_off + 2u > payload_off ) ) ||
+      ( (uintptr_t)seq_dev & 7 ) || ( flags & ~( (unsigned)FDGPU_GATHER_NO_WRITEBACK | 0xf00u ) ) ) {
+    fd_err = "fdgpu_ed25519_submit_raw_gather_to: bad record"; return -1;
+  }
+  /* (dst_base NULL selects the per-record form; dst carries the device address) */
+  return submit_gather( ctx, src, src_dev, NULL, dst_dev, ( (unsigned long)copy_sz + 15UL ) & ~15UL, payload_off,
+                        payload_sz, tag, (unsigned char const *)seq_dev, seq, flags );
 }
 
 extern "C" int
@@ -4177,6 +4236,10 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
       int ready = 0;
       for(;;) {
         if( ctx->h_flag[i] == sl.token ) { ready = 1; break; }
+        /* the context's launch thread faults it when one of its calls fails, and the batch's done kernel and
+           event are then never issued: the token never comes and the event (unrecorded, or still holding the
+           slot's previous batch) reads complete -- so a blocking wait must see that fault itself */
+        if( __atomic_load_n( &ctx->fault, __ATOMIC_ACQUIRE ) ) break;
         unsigned long now = fd_now_ns();
         if( now - sl.launch_ns > 2000000UL && now - sl.last_query > 1000000UL ) {
           sl.last_query = now;
@@ -4188,7 +4251,7 @@ poll_any( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, signed char * out
         if( !blocking ) break;
         __builtin_ia32_pause();
       }
-      if( ctx->fault ) break;
+      if( __atomic_load_n( &ctx->fault, __ATOMIC_ACQUIRE ) ) { if( ctx->lerr[0] ) fd_err = ctx->lerr; break; }
       if( !ready ) break;
       std::atomic_thread_fence( std::memory_order_acquire );
       unsigned long now = fd_now_ns();
@@ -4248,6 +4311,11 @@ fdgpu_ed25519_batch_stats( fdgpu_ed25519_ctx_t const * ctx, unsigned long * batc
 
 /* host-side test hook: the context behaves exactly as after a failed batch */
 extern "C" void
+fdgpu_ed25519_debug_fail_launch( fdgpu_ed25519_ctx_t * ctx, int on ) {
+  __atomic_store_n( &ctx->dbg_fail_issue, on ? 1 : 0, __ATOMIC_RELEASE );
+}
+
+extern "C" void
 fdgpu_ed25519_debug_fault( fdgpu_ed25519_ctx_t * ctx ) {
   if( !ctx ) return;
   ctx->fault = 1;
@@ -4300,6 +4368,15 @@ fdgpu_ed25519_poll_raw( fdgpu_ed25519_ctx_t * ctx, unsigned long * out_tags, sig
 extern "C" void
 fdgpu_ed25519_set_dedup( fdgpu_ed25519_ctx_t * ctx, int enable, unsigned long seed ) {
   ctx->dedup = enable ? 1 : 0; ctx->dedup_seed = seed;
+}
+
+extern "C" int
+fdgpu_ed25519_set_dedup_seeds( fdgpu_ed25519_ctx_t * ctx, unsigned long const * seeds, int n ) {
+  if( n < 0 || n > 16 || ( n && !seeds ) ) { fd_err = "fdgpu_ed25519_set_dedup_seeds: 0..16 seeds"; return -1; }
+  memset( ctx->dedup_seeds, 0, sizeof(ctx->dedup_seeds) );
+  if( n ) memcpy( ctx->dedup_seeds, seeds, (size_t)n * sizeof(unsigned long) );
+  ctx->dedup_nseed = n; ctx->dedup = 1;
+  return 0;
 }
 
 extern "C" int

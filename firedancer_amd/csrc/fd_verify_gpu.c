@@ -6,6 +6,7 @@
 #define _GNU_SOURCE
 #include "../../include/fd_verify_gpu.h"
 #include "../../include/fd_ed25519_gpu.h"
+#include "fd_vsvc_private.h"
 
 #include <fcntl.h>
 #include <pthread.h>
@@ -15,6 +16,10 @@
 #include <sys/mman.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
+#include <dirent.h>
+#include <dlfcn.h>
+#include <spawn.h>
 #include <unistd.h>
 #include <stdatomic.h>
 #include <stdint.h>
@@ -394,6 +399,7 @@ struct fdgpu_vtile {
   fdgpu_launcher_t *    launcher;        /* opt.launcher: the launch thread of every context (NULL: none) */
   vt_cp_t *             cp[ FDGPU_VTILE_COPY_THREADS_MAX ];   /* opt.copy_threads: the host copy threads */
   int                   ncp;
+  int                   ncp_want;        /* opt.copy_threads: started when zero-copy intake turns on (set_in_links) */
   ulong                 cp_cnt, cp_wait_ns;                   /* copy tasks pushed; time after_frags waited on one */
   int                   device, semantics;   /* to recreate a faulted context */
   int                   fault_seen[ VT_NCTX_MAX ];
@@ -436,6 +442,19 @@ struct fdgpu_vtile {
   uchar const *         in_mem[ FDGPU_VTILE_IN_MAX ];
   ulong                 in_chunk0[ FDGPU_VTILE_IN_MAX ], in_wmark[ FDGPU_VTILE_IN_MAX ];
   ulong                 overruns;
+  /* served by a verify service (fdgpu_vtile_new_svc): no engine contexts (nctx 0); requests and completions
+     through the service's rings */
+  fdgpu_vsvc_t *        svc;
+  vsvc_client_t *       sc;
+  vsvc_req_t *          sreq;
+  vsvc_cpl_t const *    scpl;
+  ulong                 smask, req_pub, cpl_seen;
+  int                   client, svc_dead;
+  int                   gpu_rec;         /* the GPU writes each record's txn_t_sz and fd_txn_t image (zero-copy or served) */
+  uchar const *         rgn_lo[ FDGPU_VSVC_RGN_MAX ];      /* the service's regions in this process */
+  ulong                 rgn_sz[ FDGPU_VSVC_RGN_MAX ];
+  int                   rgn_last;
+  ulong                 in_line_ref[ FDGPU_VTILE_IN_MAX ]; /* each in link's mcache lines: region << 56 | offset (~0: none) */
   /* poll scratch */
   ulong                 batch;
   ulong *               p_tags;
@@ -536,6 +555,51 @@ static inline void vt_cp_wait( fdgpu_vtile_t * vt, vt_pend_t const * p ) {
   vt->cp_wait_ns += now_ns() - tw;
 }
 
+/* ---- a tile served by a verify service (fdgpu_vtile_new_svc) ----------------------------------------
+   during_frag writes one request per frag (index = the frag's pending index) and publishes the ring's
+   tail in groups of 16 and at every housekeep / flush / drain; after_frags reads the completions, which
+   come back in request order. */
+
+static inline void vt_svc_publish( fdgpu_vtile_t * vt ) {
+  if( vt->req_pub != vt->pend_tail ) {
+    vt->req_pub = vt->pend_tail;
+    atomic_store_explicit( &vt->sc->req_tail, vt->req_pub, memory_order_release );
+  }
+}
+
+/* 1 if the service failed to start or stopped beating: nothing more will complete */
+static int vt_svc_dead( fdgpu_vtile_t * vt ) {
+  if( vt->svc_dead ) return 1;
+  vsvc_hdr_t * h = vt->svc->h;
+  int r = atomic_load_explicit( &h->ready, memory_order_acquire );
+  if( r < 0 ) { vt->svc_dead = 1; return 1; }
+  if( r == 0 ) return 0;                               /* not started yet: requests wait */
+  ulong hb = atomic_load_explicit( &h->heartbeat, memory_order_acquire ), now = now_ns();
+  if( now > hb && now - hb > VSVC_DEAD_NS ) { vt->svc_dead = 1; return 1; }
+  return 0;
+}
+
+/* the request of the frag about to be taken (pending index pend_tail) */
+static inline void vt_svc_req( fdgpu_vtile_t * vt, ulong src, ulong line, ulong seq, ulong rec_sz, unsigned flags ) {
+  vsvc_req_t * r = &vt->sreq[ vt->pend_tail & vt->smask ];
+  r->seq = seq; r->src = src; r->line = line; r->dst_chunk = (unsigned)vt->out_chunk;
+  r->rec_sz = (unsigned short)rec_sz; r->flags = (unsigned short)flags;
+}
+
+/* region id << 56 | offset of [p, p+n) among the service's regions as this process maps them, ~0UL if outside */
+static ulong vt_svc_ref( fdgpu_vtile_t * vt, void const * p, ulong n ) {
+  uchar const * q = (uchar const *)p;
+  int i = vt->rgn_last;
+  if( vt->rgn_lo[i] && q >= vt->rgn_lo[i] && q + n <= vt->rgn_lo[i] + vt->rgn_sz[i] )
+    return ( (ulong)i << 56 ) | (ulong)( q - vt->rgn_lo[i] );
+  for( i=0; i<FDGPU_VSVC_RGN_MAX; i++ )
+    if( vt->rgn_lo[i] && q >= vt->rgn_lo[i] && q + n <= vt->rgn_lo[i] + vt->rgn_sz[i] ) {
+      vt->rgn_last = i;
+      return ( (ulong)i << 56 ) | (ulong)( q - vt->rgn_lo[i] );
+    }
+  return ~0UL;
+}
+
 /* one engine context of the tile.  Adaptive batching launches a partial
    batch when the GPU has room (low load: the latency path) and a full one
    when frags back up (high load: the throughput path, whose per-signature
@@ -624,11 +688,10 @@ fdgpu_vtile_new_opts( int device, ulong batch_txn, ulong tcache_depth, ulong see
   int cp_ok = 1;
   if( vt->opt.copy_threads > FDGPU_VTILE_COPY_THREADS_MAX ) vt->opt.copy_threads = FDGPU_VTILE_COPY_THREADS_MAX;
   if( vt->opt.copy_threads < 0 ) vt->opt.copy_threads = 0;
-  /* a thread's ring holds every task of the pending frags it may have (round robin: pend_cap / n + 1) */
-  for( int i=0; i<vt->opt.copy_threads && vt->pend && cp_ok; i++ ) {
-    if( !( vt->cp[i] = vt_cp_new( vt->pend_cap / (ulong)vt->opt.copy_threads + 2UL, vt->opt.copy_cores[i] - 1 ) ) ) cp_ok = 0;
-    else vt->ncp = i + 1;
-  }
+  /* the copy threads only serve zero-copy intake: they start with it (fdgpu_vtile_set_in_links), so a tile
+     without it has none spinning */
+  vt->ncp_want = vt->opt.copy_threads;
+  vt->gpu_rec = 0;
   if( !ctx_ok || !cp_ok || !vt->tcache || !vt->dcache || !vt->pend || !vt->p_tags || !vt->p_dtag || !vt->p_codes || !vt->p_img || !vt->p_fp ) {
     fdgpu_vtile_delete( vt );
     return NULL;
@@ -636,9 +699,69 @@ fdgpu_vtile_new_opts( int device, ulong batch_txn, ulong tcache_depth, ulong see
   return vt;
 }
 
+fdgpu_vtile_t *
+fdgpu_vtile_new_svc( fdgpu_vsvc_t * svc, int client, ulong tcache_depth, ulong seed, fdgpu_vtile_opts_t const * opts ) {
+  if( !svc || client < 0 || client >= svc->h->clients || !tcache_depth ) return NULL;
+  vsvc_client_t * k = &svc->h->client[ client ];
+  int want = 0;
+  if( !atomic_compare_exchange_strong( &k->state, &want, 3 ) ) return NULL;     /* 3: being attached */
+  fdgpu_vtile_t * vt = (fdgpu_vtile_t *)calloc( 1, sizeof(fdgpu_vtile_t) );
+  if( !vt ) { atomic_store( &k->state, 0 ); return NULL; }
+  if( opts ) vt->opt = *opts;
+  if( !vt->opt.copy_wait_ns ) vt->opt.copy_wait_ns = FDGPU_VTILE_COPY_WAIT_NS;
+  if( !vt->opt.copy_min )     vt->opt.copy_min = FDGPU_VTILE_COPY_MIN;
+  if( !vt->opt.max_uncopied ) vt->opt.max_uncopied = FDGPU_VTILE_MAX_UNCOPIED;
+  vt->svc = svc; vt->sc = k; vt->client = client; vt->nctx = 0; vt->opt.nctx = 0;
+  vt->sreq = (vsvc_req_t *)( svc->base + k->off_req ); vt->scpl = (vsvc_cpl_t const *)( svc->base + k->off_cpl );
+  vt->smask = k->ring_cap - 1UL;
+  vt->req_pub = vt->cpl_seen = 0UL;
+  vt->gpu_tag = !vt->opt.host_dedup_tag; vt->gpu_rec = 1;
+  vt->seed = seed; vt->batch = 0UL; vt->device = -1;
+  for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) vt->in_line_ref[i] = ~0UL;
+  vt->tcache = fdgpu_tcache_new( tcache_depth );
+  vt->dcache = svc->base + k->off_out;
+  ulong nchunk = ( k->out_sz / FDGPU_CHUNK_SZ ) & ~1UL;
+  ulong rchunk = ( ( VT_RESERVE_MAX + 127UL ) >> 7 ) << 1;
+  vt->chunk0 = 0UL; vt->wmark = nchunk - rchunk; vt->out_chunk = 0UL;
+  vt->pend_cap = nchunk / rchunk - 2UL;                 /* (the service sized the rings for exactly this) */
+  vt->pend = (vt_pend_t *)calloc( vt->pend_cap, sizeof(vt_pend_t) );
+  int cp_ok = 1;
+  if( vt->opt.copy_threads > FDGPU_VTILE_COPY_THREADS_MAX ) vt->opt.copy_threads = FDGPU_VTILE_COPY_THREADS_MAX;
+  if( vt->opt.copy_threads < 0 ) vt->opt.copy_threads = 0;
+  if( !vt->tcache || !vt->pend || vt->pend_cap + 2UL > k->ring_cap ) cp_ok = 0;
+  if( cp_ok ) vt->ncp_want = vt->opt.copy_threads;      /* started with zero-copy intake (fdgpu_vtile_set_in_links) */
+  if( !cp_ok ) {
+    fdgpu_tcache_delete( vt->tcache ); free( vt->pend ); free( vt );
+    atomic_store( &k->state, 0 );
+    return NULL;
+  }
+  k->seed = seed; k->pid = (long)getpid();
+  atomic_store_explicit( &k->state, 1, memory_order_release );
+  return vt;
+}
+
+int
+fdgpu_vtile_set_svc_region( fdgpu_vtile_t * vt, int id, void const * base, ulong sz ) {
+  if( !vt->svc || id < 0 || id >= FDGPU_VSVC_RGN_MAX || !base ) return -1;
+  if( vt->pend_tail != vt->pend_head ) return -1;      /* only while idle */
+  ulong have = vt->svc->h->rgn_sz[ id ];
+  if( have && sz > have ) return -1;                     /* larger than the service's region */
+  vt->rgn_lo[ id ] = (uchar const *)base; vt->rgn_sz[ id ] = sz;
+  return 0;
+}
+
 void
 fdgpu_vtile_delete( fdgpu_vtile_t * vt ) {
   if( !vt ) return;
+  if( vt->svc ) {                                        /* served: no contexts, the out dcache is the segment's */
+    vt_svc_publish( vt );
+    for( int i=0; i<vt->ncp; i++ ) vt_cp_delete( vt->cp[i] );
+    fdgpu_tcache_delete( vt->tcache );
+    free( vt->pend );
+    atomic_store_explicit( &vt->sc->state, 2, memory_order_release );
+    free( vt );
+    return;
+  }
   for( int k=0; k<VT_NCTX_MAX; k++ ) if( vt->ctx[k] ) fdgpu_ed25519_ctx_delete( vt->ctx[k] );
   fdgpu_launcher_delete( vt->launcher );       /* after its contexts: each drained its commands first */
   for( int i=0; i<vt->ncp; i++ ) vt_cp_delete( vt->cp[i] );   /* (a thread finishes its queued copies first) */
@@ -664,6 +787,11 @@ vt_launched( fdgpu_vtile_t * vt, int k, ulong now, ulong filling ) {
 int
 fdgpu_vtile_flush( fdgpu_vtile_t * vt ) {
   vt_fence();
+  if( vt->svc ) {                                   /* the service launches its filling batches */
+    vt_svc_publish( vt );
+    atomic_fetch_add_explicit( &vt->sc->flush, 1UL, memory_order_release );
+    return vt_svc_dead( vt ) ? -1 : 0;
+  }
   int rc = 0;
   for( int i=0; i<vt->nctx; i++ ) {            /* oldest first: the fill context's batch is the newest */
     int k = ( vt->fill + 1 + i ) % vt->nctx;
@@ -680,6 +808,12 @@ fdgpu_vtile_flush( fdgpu_vtile_t * vt ) {
 void
 fdgpu_vtile_pipeline_state( fdgpu_vtile_t const * vt, ulong * filling, ulong * inflight ) {
   *filling = 0UL; *inflight = 0UL;
+  if( vt->svc ) {                                   /* served: not yet taken by the service / taken, no verdict yet */
+    ulong tk = atomic_load_explicit( &vt->sc->taken, memory_order_relaxed );
+    ulong cp = atomic_load_explicit( &vt->sc->cpl_tail, memory_order_relaxed );
+    *filling = vt->pend_tail > tk ? vt->pend_tail - tk : 0UL; *inflight = tk > cp ? tk - cp : 0UL;
+    return;
+  }
   for( int k=0; k<vt->nctx; k++ ) {
     ulong f, i;
     fdgpu_ed25519_pipeline_state( vt->ctx[k], &f, &i );
@@ -690,6 +824,8 @@ ulong   fdgpu_vtile_overruns( fdgpu_vtile_t const * vt ) { return vt->overruns; 
 
 int
 fdgpu_vtile_faulted( fdgpu_vtile_t const * vt ) {
+  if( vt->svc )                                     /* the service's contexts faulted now (+1: the service is gone) */
+    return atomic_load_explicit( &vt->svc->h->faulted, memory_order_relaxed ) + ( vt->svc_dead ? 1 : 0 );
   int n = 0;
   for( int k=0; k<vt->nctx; k++ ) n += fdgpu_ed25519_faulted( vt->ctx[k] ) != 0;
   return n;
@@ -697,6 +833,7 @@ fdgpu_vtile_faulted( fdgpu_vtile_t const * vt ) {
 
 int
 fdgpu_vtile_recover( fdgpu_vtile_t * vt ) {
+  if( vt->svc ) return vt->svc_dead ? -2 : 0;       /* the service recreates its faulted contexts itself */
   int rc = 0;
   for( int k=0; k<vt->nctx; k++ ) {
     if( !fdgpu_ed25519_faulted( vt->ctx[k] ) ) continue;
@@ -714,7 +851,15 @@ fdgpu_vtile_recover( fdgpu_vtile_t * vt ) {
 }
 
 void
-fdgpu_vtile_debug_fault( fdgpu_vtile_t * vt, int k ) { if( k >= 0 && k < vt->nctx ) fdgpu_ed25519_debug_fault( vt->ctx[k] ); }
+fdgpu_vtile_debug_fault( fdgpu_vtile_t * vt, int k ) {
+  if( vt->svc ) { if( k >= 0 && k < VSVC_NCTX_MAX ) atomic_store_explicit( &vt->sc->dbg_fault, k + 1, memory_order_release ); return; }
+  if( k >= 0 && k < vt->nctx ) fdgpu_ed25519_debug_fault( vt->ctx[k] );
+}
+
+void
+fdgpu_vtile_debug_fail_launch( fdgpu_vtile_t * vt, int k ) {
+  if( !vt->svc && k >= 0 && k < vt->nctx ) fdgpu_ed25519_debug_fail_launch( vt->ctx[k], 1 );
+}
 
 void
 fdgpu_vtile_gpu_metrics( fdgpu_vtile_t * vt, fdgpu_vtile_gpu_metrics_t * out ) {
@@ -766,8 +911,15 @@ int
 fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_mc, int n ) {
   if( vt->pend_tail != vt->pend_head ) return -1;       /* switch only while idle */
   if( n < 1 || n > FDGPU_VTILE_IN_MAX ) return -1;
+  /* served: the service maps the lines (no GPU call here); each in link's lines must lie in one of its
+     regions (fdgpu_vtile_set_svc_region) */
+  for( int i=0; i<n && vt->svc; i++ ) {
+    fdgpu_mcache_t const * mc = in_mc[i];
+    vt->in_line_ref[i] = mc ? vt_svc_ref( vt, mc->line, mc->depth * sizeof(mc_line_t) ) : ~0UL;
+    if( mc && vt->in_line_ref[i] == ~0UL ) return -2;
+  }
   /* the GPU re-reads each frag's mcache line after its copy: the lines must be mapped for it */
-  for( int i=0; i<n; i++ ) {
+  for( int i=0; i<n && !vt->svc; i++ ) {
     fdgpu_mcache_t * mc = (fdgpu_mcache_t *)in_mc[i];
     if( !mc || mc->reg ) continue;
     /* the lines' whole pages (an fd_mcache's lines start 256 bytes into its region, not on a page).  Already
@@ -784,7 +936,13 @@ fdgpu_vtile_set_in_links( fdgpu_vtile_t * vt, fdgpu_mcache_t const * const * in_
     if( rc < 0 ) return -2;
     if( rc == 0 ) { mc->reg = 1; mc->reg_base = (void *)lo; }              /* (1: an owner's registration) */
   }
-  vt->zc = 1; vt->n_in = n;
+  /* the copy threads (opt.copy_threads), now that zero-copy intake needs them: a thread's ring holds every
+     task of the pending frags it may have (round robin: pend_cap / n + 1) */
+  for( int i=vt->ncp; i<vt->ncp_want; i++ ) {
+    if( !( vt->cp[i] = vt_cp_new( vt->pend_cap / (ulong)vt->ncp_want + 2UL, vt->opt.copy_cores[i] - 1 ) ) ) return -3;
+    vt->ncp = i + 1;
+  }
+  vt->zc = 1; vt->n_in = n; vt->gpu_rec = 1;
   for( int i=0; i<FDGPU_VTILE_IN_MAX; i++ ) {
     vt->in_mcs[i] = i < n ? in_mc[i] : NULL;
     vt->in_mc_dev[i] = vt->in_mcs[i] ? (uchar const *)fdgpu_host_dev_ptr( vt->in_mcs[i]->line, 8UL ) : NULL;
@@ -814,6 +972,17 @@ static void vt_copy_launched( fdgpu_vtile_t * vt, int k ) {
 /* advance copy_cursor over the frags whose gathers have completed */
 static void vt_copy_poll( fdgpu_vtile_t * vt ) {
   if( !vt->zc ) return;
+  if( vt->svc ) {                                   /* the service's copied prefix of this tile's requests */
+    ulong g = atomic_load_explicit( &vt->sc->copied, memory_order_acquire );
+    if( vt->copy_cursor < vt->pend_head ) vt->copy_cursor = vt->pend_head;
+    while( vt->copy_cursor < vt->pend_tail && vt->copy_cursor < g ) {
+      vt_pend_t const * p = &vt->pend[ vt->copy_cursor % vt->pend_cap ];
+      if( p->cp && !vt_cp_done( vt, p->cp ) ) break;
+      vt_copied( vt, p );
+      vt->copy_cursor++;
+    }
+    return;
+  }
   ulong g[ VT_NCTX_MAX ], now = 0UL;
   for( int k=0; k<vt->nctx; k++ ) {
     g[k] = fdgpu_ed25519_gathered( vt->ctx[k] );
@@ -838,6 +1007,19 @@ static void vt_copy_poll( fdgpu_vtile_t * vt ) {
 int
 fdgpu_vtile_copy( fdgpu_vtile_t * vt, int blocking ) {
   if( !vt->zc ) return 0;
+  if( vt->svc ) {
+    vt_cp_publish( vt );
+    vt_svc_publish( vt );
+    atomic_fetch_add_explicit( &vt->sc->gather, 1UL, memory_order_release );
+    vt->copy_t0 = 0UL;
+    vt_copy_poll( vt );
+    while( blocking && vt->copy_cursor < vt->pend_tail ) {
+      if( vt_svc_dead( vt ) ) return -3;
+      _mm_pause();
+      vt_copy_poll( vt );
+    }
+    return 0;
+  }
   int rc = 0;
   for( int k=0; k<vt->nctx; k++ ) {
     if( fdgpu_ed25519_faulted( vt->ctx[k] ) ) continue;
@@ -894,6 +1076,11 @@ int
 fdgpu_vtile_housekeep( fdgpu_vtile_t * vt, ulong max_inflight ) {
   ulong filling, now = now_ns();
   vt_cp_publish( vt );                           /* copy tasks written since the last group of 16 */
+  if( vt->svc ) {                                /* served: the service decides launches and copies */
+    vt_svc_publish( vt );
+    vt_copy_poll( vt );
+    return 0;
+  }
   /* batch duration: a context's batches have drained (inflight counts
      launched slots not yet fully polled) */
   for( int k=0; k<vt->nctx; k++ ) {
@@ -932,6 +1119,7 @@ static int
 vt_room( fdgpu_vtile_t * vt ) {
   if( !vt->zc ) vt_fence();                      /* (zero-copy intake makes no streaming stores) */
   if( vt->pend_tail - vt->pend_head >= vt->pend_cap ) { fdgpu_vtile_flush( vt ); return -2; }
+  if( vt->svc ) return 0;                        /* (a served tile's frags complete as faults if the service's batch fails) */
   /* a faulted context takes no more frags: fill the next healthy one (none: -3) */
   if( __builtin_expect( fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ), 0 ) ) {
     for( int i=0; i<vt->nctx && fdgpu_ed25519_faulted( vt->ctx[ vt->fill ] ); i++ ) vt->fill = ( vt->fill + 1 ) % vt->nctx;
@@ -946,11 +1134,11 @@ vt_taken( fdgpu_vtile_t * vt, int in_idx, ulong seq, ulong tsorig, ulong bundle_
   vt_pend_t * p = &vt->pend[ vt->pend_tail % vt->pend_cap ];
   p->seq = seq; p->tsorig = tsorig; p->chunk = vt->out_chunk; p->k = vt->fill; p->ovr = 0; p->in_idx = in_idx; p->cp = 0UL;
   if( vt->zc ) {
-    p->cidx = vt->sub_cnt[ vt->fill ]++;
+    p->cidx = vt->svc ? 0UL : vt->sub_cnt[ vt->fill ]++;
     vt->uncopied[ in_idx ]++; vt->uncopied_tot++;
     if( !vt->copy_t0 ) vt->copy_t0 = now_ns();
   }
-  if( vt->min_batch ) {                          /* first frag of the filling batch: its wait starts */
+  if( vt->min_batch && !vt->svc ) {                          /* first frag of the filling batch: its wait starts */
     ulong f, i; fdgpu_ed25519_pipeline_state( vt->ctx[ vt->fill ], &f, &i );
     if( f == 1UL ) vt->fill_t0 = now_ns();
   }
@@ -958,11 +1146,17 @@ vt_taken( fdgpu_vtile_t * vt, int in_idx, ulong seq, ulong tsorig, ulong bundle_
   vt->pend_tail++;
   ulong reserve = ( ( FDGPU_TXNM_HDR_SZ + payload_sz + 1UL ) & ~1UL ) + 852UL;
   vt->out_chunk = fdgpu_dcache_compact_next( vt->out_chunk, reserve, vt->chunk0, vt->wmark );
+  if( vt->svc && vt->pend_tail - vt->req_pub >= 16UL ) vt_svc_publish( vt );   /* requests in groups of 16 */
 }
 
 /* submit the record the host has just written at dst (the out dcache's out_chunk) */
 static int
 vt_submit_host_record( fdgpu_vtile_t * vt, uchar * dst, unsigned short payload_sz, ulong seq ) {
+  if( vt->svc ) {        /* served: the GPU reads the record where the tile wrote it (its out dcache) */
+    vt_svc_req( vt, ( VSVC_RGN_OUT << 56 ) | (ulong)( dst - vt->dcache ), VSVC_LINE_NONE, seq, FDGPU_TXNM_HDR_SZ + payload_sz,
+                VSVC_REQ_HOSTCOPY );
+    return 0;
+  }
   if( vt->zc )   /* keep the batch in gathered mode: the GPU "gathers" the record from where it already is */
     return fdgpu_ed25519_submit_raw_gather_chk( vt->ctx[ vt->fill ], dst, vt->dcache, dst,
                                                 (unsigned short)( FDGPU_TXNM_HDR_SZ + payload_sz ),
@@ -994,6 +1188,7 @@ vt_during_txnm( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong
   if( vt->zc && vt->uncopied_tot >= vt->opt.max_uncopied ) {   /* copy backlog: start the copies, take nothing */
     vt_copy_poll( vt );
     if( vt->uncopied_tot >= vt->opt.max_uncopied ) {
+      if( vt->svc ) { vt_svc_publish( vt ); atomic_fetch_add_explicit( &vt->sc->gather, 1UL, memory_order_release ); }
       for( int k=0; k<vt->nctx; k++ )
         if( !fdgpu_ed25519_faulted( vt->ctx[k] ) && fdgpu_ed25519_gather( vt->ctx[k] ) > 0 ) vt_copy_launched( vt, k );
       vt->copy_t0 = 0UL;
@@ -1002,6 +1197,29 @@ vt_during_txnm( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong
     }
   }
   uchar * dst = vt->dcache + vt->out_chunk * FDGPU_CHUNK_SZ;
+  if( vt->zc && vt->svc ) {   /* served: the request names the frag's and its line's places in the service's regions */
+    fdgpu_mcache_t const * mc = vt->in_mcs[ link ];
+    ulong rsz = FDGPU_TXNM_HDR_SZ + in->payload_sz;
+    ulong src = vt_svc_ref( vt, frag, ( rsz + 15UL ) & ~15UL );
+    if( src == ~0UL || ( (ulong)frag & 15UL ) ) return -3;            /* not in a region of the service */
+    ulong line = VSVC_LINE_NONE;
+    if( mc ) line = vt->in_line_ref[ link ] + ( seq & ( mc->depth - 1UL ) ) * sizeof(mc_line_t);
+    vt_svc_req( vt, src, line, seq, rsz, vt->ncp ? VSVC_REQ_HOSTCOPY : 0U );
+    vt_taken( vt, link, seq, tsorig, in->bundle_id, in->payload_sz );
+    if( vt->ncp ) {            /* the record's copy into the out dcache: one of the tile's copy threads */
+      vt_pend_t * p = &vt->pend[ ( vt->pend_tail - 1UL ) % vt->pend_cap ];
+      ulong i = vt->cp_cnt++;
+      vt_cp_t * cq = vt->cp[ i % (ulong)vt->ncp ];
+      ulong t = cq->ptail;
+      vt_cp_task_t * k = &cq->ring[ t & cq->mask ];
+      k->src = (uchar const *)frag; k->dst = dst; k->sz = rsz;
+      k->line_seq = mc ? (ulong const *)&mc->line[ seq & ( mc->depth - 1UL ) ].seq : NULL; k->seq = seq; k->ovr = &p->ovr;
+      cq->ptail = t + 1UL;
+      if( !( cq->ptail & 15UL ) ) atomic_store_explicit( &cq->tail, cq->ptail, memory_order_release );
+      p->cp = i + 1UL;
+    }
+    return 0;
+  }
   if( vt->zc ) {   /* the GPU copies the frag into dst itself (no host copy) and re-checks its mcache line */
     fdgpu_mcache_t const * mc = vt->in_mcs[ link ];
     /* device views: the mcache lines' translated once (set_in_links), the frag's region cached */
@@ -1160,7 +1378,7 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
      never reaches after_frag in the reference, so no bundle state or metric changes */
   if( code == FDGPU_ERR_OVERRUN || p->ovr ) { vt->overruns++; return FDGPU_VTILE_OVERRUN; }
   fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( vt->dcache + p->chunk * FDGPU_CHUNK_SZ );
-  if( !vt->zc ) txnm->txn_t_sz = (unsigned short)fp;
+  if( !vt->gpu_rec ) txnm->txn_t_sz = (unsigned short)fp;
   int is_bundle = p->bundle_id != 0UL;
   if( is_bundle && p->bundle_id != vt->bundle_id ) { vt->bundle_failed = 0; vt->bundle_id = p->bundle_id; }
   if( is_bundle && vt->bundle_failed ) { vt->metrics[3]++; return FDGPU_VTILE_BUNDLE_PEER_FAIL; }
@@ -1171,7 +1389,7 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
   }
   if( !vt->gpu_tag ) {        /* host XXH64 of the first signature (A/B knob; reads payload and image) */
     uchar const * payload = (uchar const *)txnm + FDGPU_TXNM_HDR_SZ;
-    uchar const * im = vt->zc ? (uchar const *)txnm + ( ( FDGPU_TXNM_HDR_SZ + p->payload_sz + 1UL ) & ~1UL ) : img;
+    uchar const * im = vt->gpu_rec ? (uchar const *)txnm + ( ( FDGPU_TXNM_HDR_SZ + p->payload_sz + 1UL ) & ~1UL ) : img;
     tag = xxh64_64( vt->seed, payload + ( (unsigned)im[2] | ((unsigned)im[3] << 8) ) );
   }
   /* fd_txn_verify (fd_verify_tile.h:59-108): dedup query, verify, insert */
@@ -1188,7 +1406,7 @@ vt_after( fdgpu_vtile_t * vt, vt_pend_t const * p, int code, uchar const * img, 
   }
   /* publish: fd_txn_t behind the payload at a 2-byte boundary */
   ulong t_off = ( FDGPU_TXNM_HDR_SZ + p->payload_sz + 1UL ) & ~1UL;
-  if( !vt->zc ) memcpy( (uchar *)txnm + t_off, img, fp );
+  if( !vt->gpu_rec ) memcpy( (uchar *)txnm + t_off, img, fp );
   d->sz = t_off + fp;                                  /* fd_txn_m_realized_footprint( txnm, 1, 0 ) */
   d->tag = is_bundle ? 0UL : tag;
   vt->metrics[4]++;
@@ -1201,8 +1419,74 @@ static inline void vt_pop( fdgpu_vtile_t * vt, vt_pend_t const * p ) {
   vt->pend_head++;
 }
 
+/* after_frags of a served tile: the service's completions, in request (= pending) order */
+static ulong
+vt_after_frags_svc( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max, int blocking ) {
+  ulong n = 0UL;
+  vsvc_client_t * sc = vt->sc;
+  vt_cp_publish( vt );
+  vt_svc_publish( vt );
+  if( blocking ) atomic_fetch_add_explicit( &sc->flush, 1UL, memory_order_release );   /* never wait on an unlaunched batch */
+  while( n < max && vt->pend_head < vt->pend_tail ) {
+    ulong tw = now_ns();
+    ulong tail = atomic_load_explicit( &sc->cpl_tail, memory_order_acquire );
+    if( tail == vt->cpl_seen ) {
+      if( vt_svc_dead( vt ) ) {
+        /* the service is gone: no verdict will come.  The pending frags complete, in order, as
+           FDGPU_VTILE_GPU_FAULT (never published, never blocked on), as a faulted context's do */
+        while( n < max && vt->pend_head < vt->pend_tail ) {
+          vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
+          vt_cp_wait( vt, p );
+          fdgpu_vtile_done_t * d = &out[n];
+          d->seq = p->seq; d->in_idx = (ulong)p->in_idx; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
+          d->result = FDGPU_VTILE_GPU_FAULT; d->code = 0; d->ctx = 255U; d->batch_txns = 0U; d->batch_pos = 0U;
+          d->path = FDGPU_PATH_NONE;
+          vt->gm.gpu_fault_frags++;
+          vt_pop( vt, p ); n++;
+        }
+        break;
+      }
+      if( !blocking ) break;
+      ulong t_spin = now_ns();
+      while( atomic_load_explicit( &sc->cpl_tail, memory_order_acquire ) == vt->cpl_seen && now_ns() - t_spin < 1000000UL )
+        _mm_pause();
+      vt->gm.wait_ns += now_ns() - tw;
+      continue;
+    }
+    ulong tp = now_ns();
+    vt->gm.poll_ns += tp - tw;
+    ulong k = tail - vt->cpl_seen;
+    if( k > max - n ) k = max - n;
+    for( ulong i=0; i<k; i++ ) {
+      vsvc_cpl_t const * c = &vt->scpl[ vt->cpl_seen & vt->smask ];
+      if( c->req != (unsigned)vt->pend_head ) {   /* completions come back in request order */
+        fprintf( stderr, "fdgpu_vtile_after_frags: service completion %u != pending frag %lu\n", c->req, vt->pend_head );
+        abort();
+      }
+      if( i + 8UL < k && vt->gpu_tag ) tc_prefetch( vt->tcache, vt->scpl[ ( vt->cpl_seen + 8UL ) & vt->smask ].dtag, 8UL );
+      vt_pend_t const * p = &vt->pend[ vt->pend_head % vt->pend_cap ];
+      vt_cp_wait( vt, p );
+      fdgpu_vtile_done_t * d = &out[n];
+      if( c->code == VSVC_CODE_FAULT ) {               /* its batch failed in the service: no verdict */
+        d->seq = p->seq; d->in_idx = (ulong)p->in_idx; d->tsorig = p->tsorig; d->chunk = p->chunk; d->sz = 0UL; d->tag = 0UL;
+        d->result = FDGPU_VTILE_GPU_FAULT; d->code = 0;
+        vt->gm.gpu_fault_frags++;
+      } else {
+        d->result = vt_after( vt, p, (int)c->code, NULL, c->fp, c->dtag, d );
+      }
+      d->ctx = c->ctx; d->batch_txns = c->batch_txns; d->batch_pos = c->batch_pos; d->path = c->path;
+      vt_pop( vt, p ); n++;
+      vt->cpl_seen++;
+    }
+    vt->gm.after_ns += now_ns() - tp;
+    blocking = 0;
+  }
+  return n;
+}
+
 ulong
 fdgpu_vtile_after_frags( fdgpu_vtile_t * vt, fdgpu_vtile_done_t * out, ulong max, int blocking ) {
+  if( vt->svc ) return vt_after_frags_svc( vt, out, max, blocking );
   ulong n = 0UL;
   if( blocking ) fdgpu_vtile_flush( vt );      /* a blocking drain must not wait on an unlaunched batch */
   while( n < max && vt->pend_head < vt->pend_tail ) {
@@ -1335,16 +1619,23 @@ typedef struct {                 /* one tile's results, written once when it fin
   ulong device;
   ulong cpu_ns, wall_ns, nivcsw; /* the tile thread's CPU time over its loop's wall time, involuntary switches */
   long  cpu;                     /* the CPU it was pinned to (-1: none) */
+  /* written as the tile runs (fdgpu_link_trace / fdgpu_link_anomalies): its verdicts traced so far, and the first
+     LINK_ANOM_MAX verdicts that were neither published nor overrun (parse / verify / dedup / bundle failures)
+     with how many there were -- in the link, so a tile in a process of its own (served tiles) reports them too */
+  ulong trace_cnt;
+  ulong anom_cnt;
+  fdgpu_link_anomaly_t anom[ LINK_ANOM_MAX ];
 } link_res_t;
 
 #define LINK_PROD_MAX FDGPU_VTILE_IN_MAX
+
 
 typedef struct {
   _Atomic ulong magic;           /* set last by the creator (release) */
   ulong         total_sz;
   fdgpu_stream_cfg_t cfg;        /* (cfg.producers normalised to 1..LINK_PROD_MAX) */
   ulong         depth, n_payload, in_bytes;
-  ulong         off_mcache[ LINK_PROD_MAX ], off_dcache, off_chunk, off_sz, off_psig, off_res, off_hist;
+  ulong         off_mcache[ LINK_PROD_MAX ], off_dcache, off_chunk, off_sz, off_psig, off_res, off_hist, off_trace;
   _Atomic ulong joined, tiles_ready, tiles_done, go, fail;
   ulong         t_start;
   ulong         prod_end[ LINK_PROD_MAX ], prod_wait_ns[ LINK_PROD_MAX ];   /* per producer: last publish, credit waits */
@@ -1368,12 +1659,13 @@ struct fdgpu_link {
   link_res_t *     res;
   ulong *          hist;
   fdgpu_mcache_t   mc[ LINK_PROD_MAX ];   /* local views of the shared lines (the tiles' in links) */
-  fdgpu_link_trace_t * trace[ LINK_TILE_MAX ];   /* fdgpu_link_set_trace: this process's tiles' verdicts, in order */
-  ulong            trace_cap, trace_cnt[ LINK_TILE_MAX ];
-  /* fdgpu_link_anomalies: per tile of this process, the first LINK_ANOM_MAX verdicts that are neither
-     published nor overrun (parse / verify / dedup / bundle failures), and how many there were */
-  fdgpu_link_anomaly_t anom[ LINK_TILE_MAX ][ LINK_ANOM_MAX ];
-  ulong            anom_cnt[ LINK_TILE_MAX ];
+  fdgpu_link_trace_t * trace[ LINK_TILE_MAX ];   /* the tiles' verdicts, in order: this process's own arrays
+                                                    (fdgpu_link_set_trace) or the link's (cfg.trace_cap) */
+  ulong            trace_cap;
+  int              trace_own;
+  char             path[ 256 ];                   /* a shared link's file ("" for private memory) */
+  fdgpu_vsvc_stats_t svc_stats;                   /* served tiles: this process's service, after fdgpu_link_run */
+  int              svc_cpu;
 };
 
 static ulong al64( ulong x ) { return ( x + 63UL ) & ~63UL; }
@@ -1390,6 +1682,11 @@ static void link_view( fdgpu_link_t * l ) {
   l->psig   = l->base + h->off_psig;
   l->res    = (link_res_t *)( l->base + h->off_res );
   l->hist   = (ulong *)( l->base + h->off_hist );
+  if( h->cfg.trace_cap ) {                       /* the tiles' traces in the link itself (any process may run a tile) */
+    l->trace_cap = h->cfg.trace_cap; l->trace_own = 0;
+    for( int i=0; i<h->cfg.tiles && i<LINK_TILE_MAX; i++ )
+      l->trace[i] = (fdgpu_link_trace_t *)( l->base + h->off_trace ) + (ulong)i * h->cfg.trace_cap;
+  }
 }
 
 /* frags producer q of Q publishes: n / Q, the first n % Q producers one more */
@@ -1418,6 +1715,7 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   ulong off_psig   = o;  o = al64( o + n_payload );
   ulong off_res    = o;  o = al64( o + T * sizeof(link_res_t) );
   ulong off_hist   = o;  o = al64( o + T * LH_N * sizeof(ulong) );
+  ulong off_trace  = o;  o = al64( o + T * cfg->trace_cap * sizeof(fdgpu_link_trace_t) );
   o = ( o + 4095UL ) & ~4095UL;
   ulong off_dcache = o;  o += in_bytes + 4096UL;
   ulong total = ( o + 4095UL ) & ~4095UL;
@@ -1452,13 +1750,14 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   fdgpu_link_t * l = (fdgpu_link_t *)calloc( 1, sizeof(fdgpu_link_t) );
   if( !l ) { munmap( map, map_sz ); return NULL; }
   l->base = base; l->sz = total; l->map = map; l->map_sz = map_sz; l->shared = shared; l->h = (link_hdr_t *)base;
+  if( shared ) snprintf( l->path, sizeof(l->path), "%s", path );
   link_hdr_t * h = l->h;
   memset( (void *)h, 0, sizeof(link_hdr_t) );
   h->total_sz = total; h->cfg = *cfg; h->cfg.producers = (int)Q;
   h->depth = depth; h->n_payload = n_payload; h->in_bytes = in_bytes;
   for( ulong q=0; q<Q; q++ ) h->off_mcache[q] = off_mcache[q];
   h->off_dcache = off_dcache; h->off_chunk = off_chunk; h->off_sz = off_sz; h->off_psig = off_psig;
-  h->off_res = off_res; h->off_hist = off_hist;
+  h->off_res = off_res; h->off_hist = off_hist; h->off_trace = off_trace;
   link_view( l );
   for( ulong q=0; q<Q; q++ ) mc_init_lines( l->line[q], depth, 0UL );
   memset( (void *)l->res, 0, T * sizeof(link_res_t) );
@@ -1497,6 +1796,7 @@ fdgpu_link_join( char const * path, double timeout_s ) {
             if( base == MAP_FAILED ) return NULL;
             fdgpu_link_t * l = (fdgpu_link_t *)calloc( 1, sizeof(fdgpu_link_t) );
             if( !l ) { munmap( base, total ); return NULL; }
+            snprintf( l->path, sizeof(l->path), "%s", path );
             l->base = base; l->sz = total; l->map = base; l->map_sz = total; l->shared = 1; l->h = (link_hdr_t *)base;
             link_view( l );
             atomic_fetch_add( &l->h->joined, 1UL );
@@ -1519,14 +1819,19 @@ fdgpu_link_delete( fdgpu_link_t * l ) {
     for( int q=0; q<l->h->cfg.producers; q++ ) fdgpu_host_unregister( l->line[q] );
   }
   munmap( l->map, l->map_sz );
-  for( int i=0; i<LINK_TILE_MAX; i++ ) free( l->trace[i] );
+  if( l->trace_own ) for( int i=0; i<LINK_TILE_MAX; i++ ) free( l->trace[i] );
   free( l );
 }
 
 int
 fdgpu_link_set_trace( fdgpu_link_t * l, ulong cap ) {
-  for( int i=0; i<LINK_TILE_MAX; i++ ) { free( l->trace[i] ); l->trace[i] = NULL; l->trace_cnt[i] = 0UL; }
-  l->trace_cap = 0UL;
+  if( l->h->cfg.trace_cap ) return cap == l->h->cfg.trace_cap ? 0 : -1;   /* the link's own traces (cfg.trace_cap) */
+  for( int i=0; i<LINK_TILE_MAX; i++ ) {
+    if( l->trace_own ) free( l->trace[i] );
+    l->trace[i] = NULL;
+  }
+  for( int i=0; i<l->h->cfg.tiles && i<LINK_TILE_MAX; i++ ) l->res[i].trace_cnt = 0UL;
+  l->trace_cap = 0UL; l->trace_own = 1;
   if( !cap ) return 0;
   for( int i=0; i<l->h->cfg.tiles && i<LINK_TILE_MAX; i++ )
     if( !( l->trace[i] = (fdgpu_link_trace_t *)calloc( cap, sizeof(fdgpu_link_trace_t) ) ) ) return -1;
@@ -1537,7 +1842,7 @@ fdgpu_link_set_trace( fdgpu_link_t * l, ulong cap ) {
 ulong
 fdgpu_link_trace( fdgpu_link_t const * l, int tile, fdgpu_link_trace_t * out, ulong max ) {
   if( tile < 0 || tile >= LINK_TILE_MAX || !l->trace[tile] ) return 0UL;
-  ulong n = l->trace_cnt[tile] < max ? l->trace_cnt[tile] : max;
+  ulong c = l->res[tile].trace_cnt, n = c < max ? c : max;
   memcpy( out, l->trace[tile], n * sizeof(fdgpu_link_trace_t) );
   return n;
 }
@@ -1550,8 +1855,8 @@ link_trace( fdgpu_link_t * l, int idx, fdgpu_vtile_t * vt, fdgpu_vtile_done_t co
   fdgpu_link_trace_t * t = l->trace[idx];
   if( !t ) return;
   uchar const * out = fdgpu_vtile_out_dcache( vt );
-  for( ulong i=0; i<n && l->trace_cnt[idx] < l->trace_cap; i++ ) {
-    fdgpu_link_trace_t * e = &t[ l->trace_cnt[idx]++ ];
+  for( ulong i=0; i<n && l->res[idx].trace_cnt < l->trace_cap; i++ ) {
+    fdgpu_link_trace_t * e = &t[ l->res[idx].trace_cnt++ ];
     e->seq = d[i].seq; e->in_idx = d[i].in_idx; e->tag = d[i].tag; e->result = d[i].result; e->rec_sz = (unsigned)d[i].sz;
     e->rec_hash = 0UL;
     if( d[i].result == FDGPU_VTILE_PUBLISH && d[i].sz <= VT_RESERVE_MAX ) {
@@ -1717,6 +2022,76 @@ static int cpu_busy_sample( double * busy, int ms ) {
   return 0;
 }
 
+/* HIP device -> NUMA node from sysfs alone (fdgpu_gpu_numa_node_sysfs, include/fd_verify_gpu.h).  HIP
+   numbers the GPU agents of the KFD topology (nodes with SIMDs) in node order, after ROCR_VISIBLE_DEVICES
+   (indices into all of them) and then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES (indices into what ROCr
+   shows).  A node's location_id is its PCI bus << 8 | devfn and `domain` its PCI domain. */
+static int visible_pick( char const * env, int * ids, int n ) {   /* ids[0..n) filtered by a comma list of indices */
+  if( !env || !*env ) return n;
+  int out[ 64 ], m = 0;
+  char const * c = env;
+  while( *c && m < 64 ) {
+    char * e; long v = strtol( c, &e, 10 );
+    if( e == c ) return -1;                                       /* (UUIDs: not resolved here) */
+    if( v >= 0 && v < n ) out[m++] = ids[v];
+    c = *e == ',' ? e + 1 : e;
+    if( *e && *e != ',' ) return -1;
+  }
+  for( int i=0; i<m; i++ ) ids[i] = out[i];
+  return m;
+}
+
+static long sysfs_prop( char const * path, char const * key ) {
+  FILE * f = fopen( path, "r" );
+  if( !f ) return -1L;
+  char line[ 256 ]; long v = -1L; size_t kl = strlen( key );
+  while( fgets( line, sizeof(line), f ) )
+    if( !strncmp( line, key, kl ) && line[kl] == ' ' ) { v = strtol( line + kl + 1, NULL, 10 ); break; }
+  fclose( f );
+  return v;
+}
+
+int
+fdgpu_gpu_numa_node_sysfs( char const * root, int device ) {
+  if( !root ) root = "/sys";
+  if( device < 0 ) return -1;
+  char path[ 512 ];
+  snprintf( path, sizeof(path), "%s/class/kfd/kfd/topology/nodes", root );
+  DIR * d = opendir( path );
+  if( !d ) return -1;
+  int nodes[ 64 ], nn = 0;
+  struct dirent * e;
+  while( ( e = readdir( d ) ) && nn < 64 ) {
+    char * end; long v = strtol( e->d_name, &end, 10 );
+    if( end == e->d_name || *end ) continue;
+    nodes[nn++] = (int)v;
+  }
+  closedir( d );
+  for( int i=1; i<nn; i++ ) for( int j=i; j>0 && nodes[j-1] > nodes[j]; j-- ) { int t = nodes[j]; nodes[j] = nodes[j-1]; nodes[j-1] = t; }
+  int gpus[ 64 ], ng = 0;
+  for( int i=0; i<nn; i++ ) {
+    snprintf( path, sizeof(path), "%s/class/kfd/kfd/topology/nodes/%d/properties", root, nodes[i] );
+    if( sysfs_prop( path, "simd_count" ) > 0 ) gpus[ng++] = nodes[i];
+  }
+  ng = visible_pick( getenv( "ROCR_VISIBLE_DEVICES" ), gpus, ng );
+  char const * hv = getenv( "HIP_VISIBLE_DEVICES" );
+  if( !hv || !*hv ) hv = getenv( "CUDA_VISIBLE_DEVICES" );
+  if( ng > 0 ) ng = visible_pick( hv, gpus, ng );
+  if( ng <= 0 || device >= ng ) return -1;
+  snprintf( path, sizeof(path), "%s/class/kfd/kfd/topology/nodes/%d/properties", root, gpus[device] );
+  long loc = sysfs_prop( path, "location_id" ), dom = sysfs_prop( path, "domain" );
+  if( loc < 0 ) return -1;
+  if( dom < 0 ) dom = 0;
+  snprintf( path, sizeof(path), "%s/bus/pci/devices/%04lx:%02lx:%02lx.%lx/numa_node", root, (ulong)dom,
+            ( (ulong)loc >> 8 ) & 0xffUL, ( (ulong)loc >> 3 ) & 0x1fUL, (ulong)loc & 7UL );
+  FILE * f = fopen( path, "r" );
+  if( !f ) return -1;
+  int node = -1;
+  if( fscanf( f, "%d", &node ) != 1 ) node = -1;
+  fclose( f );
+  return node;
+}
+
 /* n CPUs for this process's link threads, in the order producers, tiles, launch threads, copy threads:
    one hardware thread per core, on the GPU's NUMA node when it has them, idle cores first, filling one L3
    group (a CCD) after another from group proc (so processes spread).  n_pair: the producers plus tiles --
@@ -1724,7 +2099,7 @@ static int cpu_busy_sample( double * busy, int ms ) {
    frag that costs about twice as much across L3 groups -- so the first group taken is the first, from
    proc's, with n_pair idle cores, when there is one. */
 static int
-link_pick_cpus( int device, int proc, int n, int n_pair, int * out ) {
+link_pick_cpus( int device, int proc, int n, int n_pair, int * out, int gpu_calls ) {
   char const * env = getenv( "FDGPU_LINK_PIN" );
   if( env && !strcmp( env, "0" ) ) return 0;
   int got = 0;
@@ -1737,7 +2112,9 @@ link_pick_cpus( int device, int proc, int n, int n_pair, int * out ) {
   if( sched_getaffinity( 0, sizeof(aff), &aff ) ) return 0;
   uchar node_set[ LINK_CPU_MAX ];
   memset( node_set, 0, sizeof(node_set) );
-  int node = fdgpu_device_numa_node( device ), use_node = 0;
+  /* the device's node: from its bus id (a GPU call), or from sysfs alone in a process that must not touch the
+     GPU before it forks its tiles (served tiles) */
+  int node = gpu_calls ? fdgpu_device_numa_node( device ) : fdgpu_gpu_numa_node_sysfs( NULL, device ), use_node = 0;
   if( node >= 0 ) {
     char path[ 96 ]; snprintf( path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node );
     use_node = !cpulist_read( path, node_set );
@@ -1791,7 +2168,10 @@ static void link_pin( int cpu ) {
     fprintf( stderr, "fdgpu_link: could not pin to CPU %d\n", cpu );
 }
 
-typedef struct { fdgpu_link_t * l; int idx, device, cpu, lcpu, ccpu[ FDGPU_VTILE_COPY_THREADS_MAX ]; } link_tile_arg_t;
+typedef struct {
+  fdgpu_link_t * l; int idx, device, cpu, lcpu, ccpu[ FDGPU_VTILE_COPY_THREADS_MAX ];
+  fdgpu_vsvc_t * svc; int client;                /* served tiles (cfg.svc): the service and this tile's client slot */
+} link_tile_arg_t;
 /* lcpu: its launch thread's CPU, ccpu: its copy threads' */
 
 /* per-link state of a tile */
@@ -1826,10 +2206,12 @@ static ulong own_in( ulong a, ulong b, ulong T, ulong idx ) {
 ulong
 fdgpu_link_anomalies( fdgpu_link_t const * l, int tile, fdgpu_link_anomaly_t * out, ulong max ) {
   if( tile < 0 || tile >= LINK_TILE_MAX ) return 0UL;
-  ulong n = l->anom_cnt[tile] < LINK_ANOM_MAX ? l->anom_cnt[tile] : LINK_ANOM_MAX;
+  if( tile >= l->h->cfg.tiles ) return 0UL;
+  link_res_t const * r = &l->res[tile];
+  ulong n = r->anom_cnt < LINK_ANOM_MAX ? r->anom_cnt : LINK_ANOM_MAX;
   if( n > max ) n = max;
-  memcpy( out, l->anom[tile], n * sizeof(fdgpu_link_anomaly_t) );
-  return l->anom_cnt[tile];
+  memcpy( out, r->anom, n * sizeof(fdgpu_link_anomaly_t) );
+  return r->anom_cnt;
 }
 
 static void
@@ -1849,9 +2231,9 @@ link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, 
     if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL )
       *sigs += l->psig[ pmask ? ( ( s * Q + (ulong)q ) & pmask ) : ( s * Q + (ulong)q ) % np ];
     if( __builtin_expect( d[i].result != FDGPU_VTILE_PUBLISH && d[i].result != FDGPU_VTILE_OVERRUN, 0 ) ) {
-      ulong k = l->anom_cnt[idx]++;
+      ulong k = l->res[idx].anom_cnt++;
       if( k < LINK_ANOM_MAX ) {
-        fdgpu_link_anomaly_t * e = &l->anom[idx][k];
+        fdgpu_link_anomaly_t * e = &l->res[idx].anom[k];
         e->seq = s; e->in_idx = d[i].in_idx; e->tag = d[i].tag; e->result = d[i].result; e->code = d[i].code;
         e->payload_idx = ( s * Q + (ulong)q ) % np;   /* the link's layout: producer q's frag s */
         e->ctx = d[i].ctx; e->batch_txns = d[i].batch_txns; e->batch_pos = d[i].batch_pos; e->path = d[i].path;
@@ -1881,15 +2263,33 @@ static void * link_tile( void * _a ) {
   vo.copy_threads = c->zero_copy ? c->copy_threads : 0;
   vo.min_batch = c->min_batch; vo.small_max = c->small_max; vo.lat_share = c->lat_share;
   for( int i=0; i<vo.copy_threads && i<FDGPU_VTILE_COPY_THREADS_MAX; i++ ) vo.copy_cores[i] = a->ccpu[i] >= 0 ? a->ccpu[i] + 1 : 0;
-  fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
-                                             ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );
+  fdgpu_vtile_t * vt = a->svc ? fdgpu_vtile_new_svc( a->svc, a->client, 1UL<<16, 0x5eedUL + (ulong)idx, &vo )
+                              : fdgpu_vtile_new_opts( a->device, c->batch_txn, 1UL<<16, 0x5eedUL + (ulong)idx,
+                                                      ( mult*c->batch_txn + 64UL ) * 2304UL, FDGPU_SEMANTICS_AVX512, &vo );
   if( !vt ) { fprintf( stderr, "fdgpu_link: tile %d: %s\n", idx, fdgpu_last_error() ); atomic_store( &h->fail, 1 ); return NULL; }
+  if( a->svc ) {                               /* where the service's regions lie here: the in dcache, each link's lines */
+    int bad = fdgpu_vtile_set_svc_region( vt, 0, l->dcache, h->in_bytes + 4096UL );
+    for( ulong q=0; q<Q; q++ ) bad |= fdgpu_vtile_set_svc_region( vt, 1 + (int)q, l->line[q], mc_bytes( h->depth ) );
+    if( bad ) { fprintf( stderr, "fdgpu_link: tile %d: service regions\n", idx ); atomic_store( &h->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL; }
+  }
   /* zero-copy intake from every producer's link; the overrun check only on unreliable links (a
      reliable producer never reuses a line before the tile's credit passes its pending frags) */
   if( c->zero_copy ) {
     fdgpu_mcache_t const * mcs[ LINK_PROD_MAX ];
     for( ulong q=0; q<Q; q++ ) mcs[q] = c->reliable ? NULL : &l->mc[q];
     if( fdgpu_vtile_set_in_links( vt, mcs, (int)Q ) ) { atomic_store( &h->fail, 1 ); fdgpu_vtile_delete( vt ); return NULL; }
+  }
+  if( a->svc ) {                               /* served: its GPU context is the service's */
+    ulong t_sv = now_ns();
+    int r;
+    while( !( r = fdgpu_vsvc_ready( a->svc ) ) ) {
+      if( atomic_load( &h->fail ) || now_ns() - t_sv > 120000000000UL ) { r = -1; break; }
+      usleep( 1000 );
+    }
+    if( r < 0 ) {
+      fprintf( stderr, "fdgpu_link: tile %d: the verify service did not start\n", idx );
+      atomic_store( &h->fail, 9 ); fdgpu_vtile_delete( vt ); return NULL;
+    }
   }
   atomic_fetch_add( &h->tiles_ready, 1UL );    /* the producers start once every tile has its GPU context */
   {
@@ -2042,7 +2442,8 @@ static void * link_tile( void * _a ) {
   thread_usage( &cpu1, &iv1 );
   r->cpu_ns = cpu1 - cpu0; r->wall_ns = t_end - t_begin; r->nivcsw = iv1 - iv0; r->cpu = a->cpu;
   memcpy( l->hist + (ulong)idx * LH_N, lh, LH_N * sizeof(ulong) );
-  atomic_fetch_add_explicit( &h->tiles_done, 1UL, memory_order_release );
+  /* (a served tile is counted done by its service's process, once it has added the GPU side's metrics) */
+  if( !a->svc ) atomic_fetch_add_explicit( &h->tiles_done, 1UL, memory_order_release );
   free( done ); free( lh );
   fdgpu_vtile_delete( vt );
   return NULL;
@@ -2050,11 +2451,14 @@ static void * link_tile( void * _a ) {
 
 /* Each process runs its tiles (i % G == proc) and, with run_producer, its
    producers (q % G == proc). */
+static int link_run_svc( fdgpu_link_t * l, int proc, int device, int run_producer );
+
 int
 fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   link_hdr_t * h = l->h;
   fdgpu_stream_cfg_t const * c = &h->cfg;
   if( proc < 0 || proc >= c->gpus ) return -1;
+  if( c->svc ) return link_run_svc( l, proc, device, run_producer );
   if( c->zero_copy && !l->registered ) {
     if( fdgpu_host_register( l->dcache, h->in_bytes + 4096UL ) ) { atomic_store( &h->fail, 7 ); return -3; }
     for( int q=0; q<c->producers; q++ )          /* the gather re-reads each frag's line after its copy */
@@ -2076,7 +2480,7 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   int nl = c->launcher ? nt : 0;                 /* the tiles' launch threads: a core each, after the tiles' */
   int H = c->zero_copy && c->copy_threads > 0 ? ( c->copy_threads < FDGPU_VTILE_COPY_THREADS_MAX ? c->copy_threads
                                                                                                   : FDGPU_VTILE_COPY_THREADS_MAX ) : 0;
-  int ncpu = link_pick_cpus( device, proc, nt + np + nl + nt*H, np + nt, cpus );   /* ... and their copy threads, after those */
+  int ncpu = link_pick_cpus( device, proc, nt + np + nl + nt*H, np + nt, cpus, 1 );   /* ... and their copy threads, after those */
   if( getenv( "FDGPU_LINK_VERBOSE" ) ) {
     fprintf( stderr, "fdgpu_link: proc %d device %d numa %d producers %d tiles %d cpus:", proc, device,
              fdgpu_device_numa_node( device ), np, nt );
@@ -2101,6 +2505,175 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   for( int t=0; t<nt; t++ ) pthread_join( th[t], NULL );
   int rc = (int)atomic_load( &h->fail );
   return rc ? -rc - 10 : 0;
+}
+
+/* Served tiles (cfg.svc): each tile of this process's GPU runs as a process of its own -- the tile program
+   (fdgpu_tile, fd_vtile_main.c), started here, which joins the link and the service segment by their files and
+   runs link_tile's loop with no GPU context (fdgpu_link_run_tile) -- and this process is their verify service
+   (fdgpu_vsvc_*, one thread) and runs its producers.  The GPU side's metrics (batches, latency histogram,
+   gathers, phases) are the service's: they are added to this process's first tile's results before its tiles
+   are counted done. */
+typedef struct { fdgpu_vsvc_t * svc; link_hdr_t * h; int device, cpu; _Atomic int stop; } link_svc_arg_t;
+
+static void * link_svc_main( void * _a ) {
+  link_svc_arg_t * a = (link_svc_arg_t *)_a;
+  link_pin( a->cpu );
+  if( fdgpu_vsvc_start( a->svc, a->device ) ) { atomic_store( &a->h->fail, 7 ); return NULL; }
+  while( !atomic_load_explicit( &a->stop, memory_order_acquire ) )
+    if( !fdgpu_vsvc_poll( a->svc ) ) _mm_pause();
+  return NULL;
+}
+
+/* the tile program, next to this library */
+static int tile_prog_path( char * out, ulong n ) {
+  Dl_info di;
+  if( !dladdr( (void *)fdgpu_link_run_tile, &di ) || !di.dli_fname ) return -1;
+  char const * sl = strrchr( di.dli_fname, '/' );
+  int dl = sl ? (int)( sl - di.dli_fname ) : 1;
+  if( snprintf( out, n, "%.*s/fdgpu_tile", dl, sl ? di.dli_fname : "." ) >= (int)n ) return -1;
+  return access( out, X_OK ) ? -1 : 0;
+}
+
+extern char ** environ;
+
+static int
+link_run_svc( fdgpu_link_t * l, int proc, int device, int run_producer ) {
+  link_hdr_t * h = l->h;
+  fdgpu_stream_cfg_t const * c = &h->cfg;
+  int mine[ LINK_TILE_MAX ], myq[ LINK_PROD_MAX ], np = 0;
+  int nt = fdgpu_link_tiles_of( c->tiles, c->gpus, proc, mine );
+  if( nt < 1 || nt > FDGPU_VSVC_CLIENT_MAX || !l->shared ) return -1;
+  char prog[ 512 ];
+  if( tile_prog_path( prog, sizeof(prog) ) ) { fprintf( stderr, "fdgpu_link: the tile program fdgpu_tile is missing\n" ); return -1; }
+  if( run_producer ) for( int q=0; q<c->producers; q++ ) if( q % c->gpus == proc ) myq[np++] = q;
+  int nl = c->launcher ? 1 : 0;
+  int H = c->zero_copy && c->copy_threads > 0 ? ( c->copy_threads < FDGPU_VTILE_COPY_THREADS_MAX ? c->copy_threads
+                                                                                                  : FDGPU_VTILE_COPY_THREADS_MAX ) : 0;
+  /* CPUs: producers, tiles, the service, its launch thread, the tiles' copy threads */
+  int cpus[ ( 2 + FDGPU_VTILE_COPY_THREADS_MAX )*LINK_TILE_MAX + LINK_PROD_MAX + 2 ];
+  int ncpu = link_pick_cpus( device, proc, np + nt + 1 + nl + nt*H, np + nt, cpus, 1 );
+  int svc_cpu = np + nt < ncpu ? cpus[ np + nt ] : -1, lcpu = nl && np + nt + 1 < ncpu ? cpus[ np + nt + 1 ] : -1;
+  if( getenv( "FDGPU_LINK_VERBOSE" ) ) {
+    fprintf( stderr, "fdgpu_link: served: proc %d device %d producers %d tiles %d service cpu %d cpus:", proc, device, np, nt, svc_cpu );
+    for( int i=0; i<ncpu; i++ ) fprintf( stderr, " %d", cpus[i] );
+    fprintf( stderr, "\n" );
+  }
+  ulong mult = c->out_mult ? c->out_mult : 6UL;
+  fdgpu_vsvc_cfg_t sc;
+  memset( &sc, 0, sizeof(sc) );
+  sc.clients = nt; sc.out_dcache_bytes = ( mult*c->batch_txn + 64UL ) * 2304UL; sc.batch_txn = c->batch_txn;
+  sc.max_inflight = c->max_inflight; sc.semantics = FDGPU_SEMANTICS_AVX512; sc.nctx = c->nctx; sc.small_max = c->small_max;
+  sc.min_batch = c->min_batch; sc.copy_wait_ns = c->copy_wait_ns; sc.copy_min = c->copy_min; sc.gather_cus = c->gather_cus;
+  sc.cu_split = c->cu_split; sc.cu_exclusive = c->cu_exclusive; sc.lat_share = c->lat_share;
+  sc.launcher = c->launcher; sc.launcher_core = lcpu >= 0 ? lcpu + 1 : 0;
+  char spath[ 300 ];
+  snprintf( spath, sizeof(spath), "%s.svc%d", l->path, proc );
+  fdgpu_vsvc_t * svc = fdgpu_vsvc_new( spath, &sc );
+  if( !svc ) { fprintf( stderr, "fdgpu_link: service segment %s\n", spath ); atomic_store( &h->fail, 7 ); return -3; }
+  /* the service's regions: the in dcache (0) and each producer's mcache lines (1 + q) */
+  int bad = fdgpu_vsvc_add_region( svc, 0, l->dcache, h->in_bytes + 4096UL );
+  for( int q=0; q<c->producers; q++ ) bad |= fdgpu_vsvc_add_region( svc, 1 + q, l->line[q], mc_bytes( h->depth ) );
+  if( bad ) { fdgpu_vsvc_delete( svc ); atomic_store( &h->fail, 7 ); return -3; }
+  /* the tile processes: fdgpu_tile <link> <service> <tile> <cpu> [copy thread cpus] */
+  pid_t pid[ LINK_TILE_MAX ];
+  int nspawn = 0;
+  for( int t=0; t<nt; t++ ) {
+    char a_tile[ 16 ], a_cpu[ 16 ], a_cc[ FDGPU_VTILE_COPY_THREADS_MAX ][ 16 ];
+    char * argv[ 6 + FDGPU_VTILE_COPY_THREADS_MAX ];
+    int na = 0;
+    snprintf( a_tile, sizeof(a_tile), "%d", mine[t] );
+    snprintf( a_cpu, sizeof(a_cpu), "%d", np + t < ncpu ? cpus[ np + t ] : -1 );
+    argv[na++] = prog; argv[na++] = l->path; argv[na++] = spath; argv[na++] = a_tile; argv[na++] = a_cpu;
+    for( int i=0; i<H; i++ ) {
+      int j = np + nt + 1 + nl + t*H + i;
+      snprintf( a_cc[i], sizeof(a_cc[i]), "%d", j < ncpu ? cpus[j] : -1 );
+      argv[na++] = a_cc[i];
+    }
+    argv[na] = NULL;
+    pid_t p;
+    if( posix_spawn( &p, prog, NULL, NULL, argv, environ ) ) { atomic_store( &h->fail, 12 ); break; }
+    pid[ nspawn++ ] = p;
+  }
+  /* this process: the service, then the producers */
+  link_svc_arg_t sa;
+  memset( &sa, 0, sizeof(sa) );
+  sa.svc = svc; sa.h = h; sa.device = device; sa.cpu = svc_cpu;
+  pthread_t sth, prod[ LINK_PROD_MAX ];
+  link_prod_arg_t pargs[ LINK_PROD_MAX ];
+  int sth_ok = !pthread_create( &sth, NULL, link_svc_main, &sa );
+  if( !sth_ok ) atomic_store( &h->fail, 7 );
+  for( int i=0; i<np; i++ ) {
+    pargs[i].l = l; pargs[i].q = myq[i]; pargs[i].cpu = i < ncpu ? cpus[i] : -1;
+    pthread_create( &prod[i], NULL, link_producer, &pargs[i] );
+  }
+  /* wait for the tile processes (a tile that dies fails the run: the others see h->fail and stop) */
+  int left = nspawn;
+  while( left ) {
+    for( int t=0; t<nspawn; t++ ) {
+      if( pid[t] < 0 ) continue;
+      int st = 0;
+      pid_t p = waitpid( pid[t], &st, WNOHANG );
+      if( p == 0 ) continue;
+      pid[t] = -1; left--;
+      if( p < 0 || !WIFEXITED( st ) || WEXITSTATUS( st ) ) {
+        fprintf( stderr, "fdgpu_link: served tile process %d ended with status %d\n", t, st );
+        if( !atomic_load( &h->fail ) ) atomic_store( &h->fail, 13 );
+      }
+    }
+    if( left ) usleep( 1000 );
+  }
+  for( int i=0; i<np; i++ ) pthread_join( prod[i], NULL );
+  atomic_store_explicit( &sa.stop, 1, memory_order_release );
+  if( sth_ok ) pthread_join( sth, NULL );
+  /* the GPU side's metrics into this process's first tile's results, then its tiles are done */
+  fdgpu_vsvc_stats_t ss;
+  fdgpu_vsvc_stats( svc, &ss );
+  fdgpu_vtile_gpu_metrics_t * gm = &l->res[ mine[0] ].gm;
+  gm->batches += ss.gm.batches; gm->batch_txns += ss.gm.batch_txns;
+  if( ss.gm.inflight_max > gm->inflight_max ) gm->inflight_max = ss.gm.inflight_max;
+  for( ulong k=0; k<FDGPU_VTILE_LAT_BUCKETS; k++ ) gm->lat_hist[k] += ss.gm.lat_hist[k];
+  gm->launch_ns += ss.gm.launch_ns; gm->copies += ss.gm.copies;
+  for( int k=0; k<8; k++ ) gm->gather_gpu[k] = ss.gm.gather_gpu[k];
+  for( int k=0; k<9; k++ ) gm->phase[k] = ss.gm.phase[k];
+  for( int k=0; k<6; k++ ) gm->launcher[k] = ss.gm.launcher[k];
+  gm->faults += ss.gm.faults;
+  l->svc_stats = ss;
+  l->svc_cpu = svc_cpu;
+  atomic_fetch_add_explicit( &h->tiles_done, (ulong)nt, memory_order_release );
+  fdgpu_vsvc_delete( svc );
+  int rc = (int)atomic_load( &h->fail );
+  return rc ? -rc - 10 : 0;
+}
+
+/* the tile program's body: tile `tile` of a shared link, served by the service segment at svc_path (made by the
+   process that runs the tile's GPU, proc = tile % G).  No GPU call. */
+int
+fdgpu_link_run_tile( fdgpu_link_t * l, int tile, char const * svc_path, int cpu, int const * copy_cpus, int ncopy ) {
+  link_hdr_t * h = l->h;
+  fdgpu_stream_cfg_t const * c = &h->cfg;
+  if( tile < 0 || tile >= c->tiles ) return -1;
+  int proc = tile % c->gpus, mine[ LINK_TILE_MAX ];
+  int nt = fdgpu_link_tiles_of( c->tiles, c->gpus, proc, mine ), client = -1;
+  for( int i=0; i<nt; i++ ) if( mine[i] == tile ) client = i;
+  if( client < 0 ) return -1;
+  fdgpu_vsvc_t * svc = fdgpu_vsvc_join( svc_path, 60. );
+  if( !svc ) { fprintf( stderr, "fdgpu_tile %d: no service segment %s\n", tile, svc_path ); atomic_store( &h->fail, 9 ); return -9; }
+  link_tile_arg_t a;
+  memset( &a, 0, sizeof(a) );
+  a.l = l; a.idx = tile; a.device = -1; a.cpu = cpu; a.lcpu = -1;
+  for( int i=0; i<FDGPU_VTILE_COPY_THREADS_MAX; i++ ) a.ccpu[i] = copy_cpus && i < ncopy ? copy_cpus[i] : -1;
+  a.svc = svc; a.client = client;
+  link_tile( &a );
+  fdgpu_vsvc_delete( svc );
+  int rc = (int)atomic_load( &h->fail );
+  return rc ? -rc - 10 : 0;
+}
+
+int
+fdgpu_link_svc_stats( fdgpu_link_t const * l, fdgpu_vsvc_stats_t * out, int * svc_cpu ) {
+  *out = l->svc_stats;
+  if( svc_cpu ) *svc_cpu = l->svc_cpu;
+  return 0;
 }
 
 int
@@ -2183,11 +2756,16 @@ fdgpu_stream_run( int device, fdgpu_stream_cfg_t const * cfg, uchar const * payl
                   unsigned short const * sz, ulong n_payload, ulong mcache_depth, fdgpu_stream_stats_t * st ) {
   fdgpu_stream_cfg_t c = *cfg;
   c.gpus = 1;
-  fdgpu_link_t * l = fdgpu_link_new( NULL, &c, payload, off, sz, n_payload, mcache_depth );
+  /* served tiles join the link from processes of their own: a file then */
+  static _Atomic ulong seq = 0UL;
+  char path[ 128 ];
+  if( c.svc ) snprintf( path, sizeof(path), "/dev/shm/fdgpu_stream_%d_%lu", (int)getpid(), atomic_fetch_add( &seq, 1UL ) );
+  fdgpu_link_t * l = fdgpu_link_new( c.svc ? path : NULL, &c, payload, off, sz, n_payload, mcache_depth );
   if( !l ) return -1;
   int rc = fdgpu_link_run( l, 0, device, 1 );
   if( !rc ) rc = fdgpu_link_result( l, 60., st );
   fdgpu_link_delete( l );
+  if( c.svc ) unlink( path );
   return rc;
 }
 

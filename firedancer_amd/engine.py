@@ -54,6 +54,7 @@ EXPORTS = ("fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed2551
            "fdgpu_ed25519_faulted", "fdgpu_ed25519_debug_fault", "fdgpu_ed25519_slow_count", "fdgpu_ed25519_set_dedup",
            "fdgpu_ed25519_set_record_fp_off", "fdgpu_ed25519_batch_stats", "fdgpu_ed25519_launch_stats", "fdgpu_ed25519_front_remaining", "fdgpu_ed25519_front_batch", "fdgpu_ed25519_verify_txn_ptrs",
            "fdgpu_ed25519_submit_raw_gather_dev_f", "fdgpu_launcher_new", "fdgpu_launcher_delete", "fdgpu_launcher_stats", "fdgpu_ed25519_set_launcher",
+           "fdgpu_ed25519_submit_raw_gather_to", "fdgpu_ed25519_set_dedup_seeds", "fdgpu_ed25519_debug_fail_launch",
            "fdgpu_last_error")
 
 _lib = None

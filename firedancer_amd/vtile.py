@@ -35,7 +35,11 @@ EXPORTS = ("fdgpu_dedup_tag", "fdgpu_xxh64", "fdgpu_link_set_trace", "fdgpu_link
            "fdgpu_vtile_during_frag_chunk",
            "fdgpu_link_new", "fdgpu_link_join", "fdgpu_link_delete", "fdgpu_link_joined", "fdgpu_link_cfg",
            "fdgpu_link_run", "fdgpu_link_tiles_of", "fdgpu_link_mcache", "fdgpu_link_dcache", "fdgpu_link_result",
-           "fdgpu_stream_run", "fdgpu_stream_bench")
+           "fdgpu_stream_run", "fdgpu_stream_bench", "fdgpu_vsvc_new", "fdgpu_vsvc_join", "fdgpu_vsvc_add_region",
+           "fdgpu_vsvc_start", "fdgpu_vsvc_ready", "fdgpu_vsvc_poll", "fdgpu_vsvc_run", "fdgpu_vsvc_stop",
+           "fdgpu_vsvc_pending", "fdgpu_vsvc_stats", "fdgpu_vsvc_delete", "fdgpu_vtile_new_svc",
+           "fdgpu_vtile_set_svc_region", "fdgpu_gpu_numa_node_sysfs", "fdgpu_link_svc_stats", "fdgpu_link_run_tile",
+           "fdgpu_vtile_debug_fail_launch", "fdgpu_vsvc_debug_serve")
 
 TXNM_DTYPE = np.dtype([("reference_slot", "<u8"), ("payload_sz", "<u2"), ("txn_t_sz", "<u2"), ("source_ipv4", "<u4"),
                        ("source_tpu", "u1"), ("_pad0", "u1", (7,)), ("bundle_id", "<u8"), ("bundle_txn_cnt", "<u8"),
@@ -90,7 +94,30 @@ class StreamCfg(ctypes.Structure):
                 ("max_uncopied", ctypes.c_ulong), ("pf_dist", ctypes.c_int), ("cu_split", ctypes.c_int),
                 ("cu_exclusive", ctypes.c_int), ("no_huge_pages", ctypes.c_int), ("launcher", ctypes.c_int),
                 ("copy_threads", ctypes.c_int), ("min_batch", ctypes.c_ulong), ("small_max", ctypes.c_ulong),
-                ("hk_ns", ctypes.c_ulong), ("lat_share", ctypes.c_int)]
+                ("hk_ns", ctypes.c_ulong), ("lat_share", ctypes.c_int), ("svc", ctypes.c_int),
+                ("trace_cap", ctypes.c_ulong)]
+
+
+class VsvcCfg(ctypes.Structure):
+    """fdgpu_vsvc_cfg_t (0 = default everywhere but clients / out_dcache_bytes / batch_txn)."""
+    _fields_ = [("clients", ctypes.c_int), ("out_dcache_bytes", ctypes.c_ulong), ("batch_txn", ctypes.c_ulong),
+                ("max_inflight", ctypes.c_ulong), ("semantics", ctypes.c_int), ("nctx", ctypes.c_int),
+                ("small_max", ctypes.c_ulong), ("min_batch", ctypes.c_ulong), ("max_wait_ns", ctypes.c_ulong),
+                ("copy_wait_ns", ctypes.c_ulong), ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint),
+                ("cu_split", ctypes.c_int), ("cu_exclusive", ctypes.c_int), ("lat_share", ctypes.c_int),
+                ("launcher", ctypes.c_int), ("launcher_core", ctypes.c_int)]
+
+
+class VsvcStats(ctypes.Structure):
+    _fields_ = [("gm", GpuMetrics), ("taken", ctypes.c_ulong), ("completed", ctypes.c_ulong),
+                ("fault_completions", ctypes.c_ulong), ("busy_polls", ctypes.c_ulong), ("polls", ctypes.c_ulong),
+                ("faults", ctypes.c_ulong), ("recovered", ctypes.c_ulong), ("loop_ns", ctypes.c_ulong),
+                ("busy_ns", ctypes.c_ulong)]
+
+    def as_dict(self) -> dict:
+        d = {k: int(getattr(self, k)) for k, _ in self._fields_ if k != "gm"}
+        d["gm"] = self.gm.as_dict()
+        return d
 
 
 class StreamStats(ctypes.Structure):
@@ -214,6 +241,28 @@ def load():
                                        ctypes.POINTER(StreamStats)]
         L.fdgpu_stream_bench.argtypes = [ctypes.c_int, vp, vp, vp, ul, ul, ctypes.c_int, ul, ul, ul, ctypes.c_double,
                                          ctypes.c_int, ctypes.POINTER(StreamStats)]
+        L.fdgpu_vsvc_new.restype = vp
+        L.fdgpu_vsvc_new.argtypes = [ctypes.c_char_p, ctypes.POINTER(VsvcCfg)]
+        L.fdgpu_vsvc_join.restype = vp
+        L.fdgpu_vsvc_join.argtypes = [ctypes.c_char_p, ctypes.c_double]
+        L.fdgpu_vsvc_add_region.argtypes = [vp, ctypes.c_int, vp, ul]
+        L.fdgpu_vsvc_start.argtypes = [vp, ctypes.c_int]
+        L.fdgpu_vsvc_ready.argtypes = [vp]
+        L.fdgpu_vsvc_poll.argtypes = [vp]
+        L.fdgpu_vsvc_run.argtypes = [vp]
+        L.fdgpu_vsvc_stop.argtypes = [vp]
+        L.fdgpu_vsvc_pending.restype = ul
+        L.fdgpu_vsvc_pending.argtypes = [vp]
+        L.fdgpu_vsvc_stats.argtypes = [vp, ctypes.POINTER(VsvcStats)]
+        L.fdgpu_vsvc_delete.argtypes = [vp]
+        L.fdgpu_vsvc_debug_serve.restype = ul
+        L.fdgpu_vsvc_debug_serve.argtypes = [vp, vp, ul, ul]
+        L.fdgpu_vtile_new_svc.restype = vp
+        L.fdgpu_vtile_new_svc.argtypes = [vp, ctypes.c_int, ul, ul, ctypes.POINTER(VTileOpts)]
+        L.fdgpu_vtile_set_svc_region.argtypes = [vp, ctypes.c_int, vp, ul]
+        L.fdgpu_vtile_debug_fail_launch.argtypes = [vp, ctypes.c_int]
+        L.fdgpu_gpu_numa_node_sysfs.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        L.fdgpu_link_svc_stats.argtypes = [vp, ctypes.POINTER(VsvcStats), ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -273,14 +322,20 @@ class VTile:
     """One GPU verify tile (fdgpu_vtile_t)."""
 
     def __init__(self, device: int = 0, batch_txn: int = 1024, tcache_depth: int = 1 << 16, seed: int = 0x5eed,
-                 out_dcache_bytes: int | None = None, semantics: int = 0, **opts):
+                 out_dcache_bytes: int | None = None, semantics: int = 0, service: "Service | None" = None,
+                 client: int = 0, **opts):
         """opts: fdgpu_vtile_opts_t fields (nctx, host_dedup_tag, small_max, min_batch, max_wait_ns,
-        copy_wait_ns, copy_min); 0 / absent = default."""
+        copy_wait_ns, copy_min); 0 / absent = default.  service: a tile served by that verify service as
+        `client` (fdgpu_vtile_new_svc: no GPU call in this tile)."""
         self.L = load()
         out_dcache_bytes = out_dcache_bytes or (6 * batch_txn + 64) * 2304
         o = VTileOpts(**opts)
-        self.p = self.L.fdgpu_vtile_new_opts(device, batch_txn, tcache_depth, seed, out_dcache_bytes, semantics,
-                                             ctypes.byref(o))
+        self.service = service
+        if service is not None:
+            self.p = self.L.fdgpu_vtile_new_svc(service.p, client, tcache_depth, seed, ctypes.byref(o))
+        else:
+            self.p = self.L.fdgpu_vtile_new_opts(device, batch_txn, tcache_depth, seed, out_dcache_bytes, semantics,
+                                                 ctypes.byref(o))
         if not self.p:
             raise RuntimeError("fdgpu_vtile_new failed: " + load_engine().fdgpu_last_error().decode())
         self.seed = seed
@@ -376,6 +431,13 @@ class VTile:
     def debug_fault(self, k: int):
         self.L.fdgpu_vtile_debug_fault(self.p, k)
 
+    def debug_fail_launch(self, k: int):
+        """Test hook: the tile's launch thread fails every batch launch of engine context k from now on."""
+        self.L.fdgpu_vtile_debug_fail_launch(self.p, k)
+
+    def set_svc_region(self, rid: int, base: int, sz: int) -> int:
+        return int(self.L.fdgpu_vtile_set_svc_region(self.p, rid, base, sz))
+
     def record(self, chunk: int, sz: int) -> bytes:
         return ctypes.string_at(self.dcache + chunk * CHUNK_SZ, sz)
 
@@ -406,6 +468,60 @@ def stream_bench(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: 
     return st.as_dict()
 
 
+def gpu_numa_node(device: int, sysfs_root: str | None = None) -> int:
+    """fdgpu_gpu_numa_node_sysfs: HIP device -> NUMA node from sysfs alone (no GPU call), -1 if unknown."""
+    return int(load().fdgpu_gpu_numa_node_sysfs(sysfs_root.encode() if sysfs_root else None, device))
+
+
+class Service:
+    """A verify service segment (fdgpu_vsvc_t): create (the service's process) or join (a tile process)."""
+
+    def __init__(self, path: str | None, *, create: bool, clients: int = 1, batch_txn: int = 8192,
+                 out_dcache_bytes: int | None = None, timeout_s: float = 30.0, **cfg):
+        self.L = load()
+        if create:
+            c = VsvcCfg(clients=clients, batch_txn=batch_txn,
+                        out_dcache_bytes=out_dcache_bytes or (6 * batch_txn + 64) * 2304, **cfg)
+            self.p = self.L.fdgpu_vsvc_new(path.encode() if path else None, ctypes.byref(c))
+        else:
+            self.p = self.L.fdgpu_vsvc_join(path.encode(), timeout_s)
+        if not self.p:
+            raise RuntimeError(f"fdgpu_vsvc_{'new' if create else 'join'}({path}) failed")
+
+    def add_region(self, rid: int, base: int, sz: int) -> int:
+        return int(self.L.fdgpu_vsvc_add_region(self.p, rid, base, sz))
+
+    def start(self, device: int = 0) -> int:
+        return int(self.L.fdgpu_vsvc_start(self.p, device))
+
+    def poll(self) -> int:
+        return int(self.L.fdgpu_vsvc_poll(self.p))
+
+    def pending(self) -> int:
+        return int(self.L.fdgpu_vsvc_pending(self.p))
+
+    def debug_serve(self, codes: np.ndarray, fp: int = 100) -> int:
+        """CPU loopback (no GPU): complete every request taken so far with codes[request index % len(codes)]."""
+        codes = np.ascontiguousarray(codes, np.int32)
+        return int(self.L.fdgpu_vsvc_debug_serve(self.p, codes.ctypes.data, len(codes), fp))
+
+    def stats(self) -> dict:
+        st = VsvcStats()
+        self.L.fdgpu_vsvc_stats(self.p, ctypes.byref(st))
+        return st.as_dict()
+
+    def close(self):
+        if getattr(self, "p", None):
+            self.L.fdgpu_vsvc_delete(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
     """The verify tiles process `proc` runs (tile i drives GPU i % gpus)."""
     out = (ctypes.c_int * max(tiles, 1))()
@@ -415,13 +531,13 @@ def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
 
 def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers=1, nctx=0, prof=0,
          out_mult=0, copy_wait_ns=0, copy_min=0, gather_cus=0, max_uncopied=0, pf_dist=0, no_huge_pages=0, cu_split=0, cu_exclusive=0,
-         launcher=0, copy_threads=0, min_batch=0, small_max=0, hk_ns=0, lat_share=0) -> StreamCfg:
+         launcher=0, copy_threads=0, min_batch=0, small_max=0, hk_ns=0, lat_share=0, svc=0, trace_cap=0) -> StreamCfg:
     return StreamCfg(n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
                      gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0, producers=producers,
                      nctx=nctx, prof=prof, out_mult=out_mult, copy_wait_ns=copy_wait_ns, copy_min=copy_min,
                      gather_cus=gather_cus, max_uncopied=max_uncopied, pf_dist=pf_dist, no_huge_pages=no_huge_pages, cu_split=cu_split,
                      cu_exclusive=cu_exclusive, launcher=launcher, copy_threads=copy_threads, min_batch=min_batch,
-                     small_max=small_max, hk_ns=hk_ns, lat_share=lat_share)
+                     small_max=small_max, hk_ns=hk_ns, lat_share=lat_share, svc=1 if svc else 0, trace_cap=trace_cap)
 
 
 def stream_run(payload: np.ndarray, off: np.ndarray, sz: np.ndarray, n_frags: int, tiles: int = 4,
@@ -495,6 +611,12 @@ class Link:
         out = np.zeros(8, ANOM_DTYPE)
         n = int(self.L.fdgpu_link_anomalies(self.p, tile, out.ctypes.data, 8))
         return n, [{k: int(e[k]) for k in ANOM_DTYPE.names} for e in out[:min(n, 8)]]
+
+    def svc_stats(self) -> dict:
+        """Served tiles (cfg svc): this process's verify service after run (fdgpu_link_svc_stats)."""
+        st, cpu = VsvcStats(), ctypes.c_int(-1)
+        self.L.fdgpu_link_svc_stats(self.p, ctypes.byref(st), ctypes.byref(cpu))
+        return dict(st.as_dict(), cpu=int(cpu.value))
 
     def result(self, timeout_s: float = 120.0) -> dict:
         st = StreamStats()

@@ -367,6 +367,10 @@ fdgpu_ed25519_faulted( fdgpu_ed25519_ctx_t const * ctx );
    failed batch. */
 void
 fdgpu_ed25519_debug_fault( fdgpu_ed25519_ctx_t * ctx );
+/* Test hook: with on, ctx's launch thread (fdgpu_ed25519_set_launcher) fails every batch launch it makes
+   from now on, as a failed runtime call would -- the context faults asynchronously, on that thread. */
+void
+fdgpu_ed25519_debug_fail_launch( fdgpu_ed25519_ctx_t * ctx, int on );
 
 /* Signatures of the last batch launched on ctx that took the full 253-bit
    walk instead of the half-size one (no short (c0, c1) pair, or forced by
@@ -575,6 +579,23 @@ int           fdgpu_ed25519_submit_raw_gather_dev_f( fdgpu_ed25519_ctx_t * ctx, 
                                                      unsigned short payload_off, unsigned short payload_sz,
                                                      unsigned long tag, unsigned long const * seq_dev,
                                                      unsigned long seq, unsigned flags );
+/* Per-record form (the verify service, fdgpu_vsvc_*: one batch takes the frags of several verify tiles,
+   and each record goes back into its own tile's out dcache): as fdgpu_ed25519_submit_raw_gather_dev_f, but
+   the record's place on the host is given by its device address dst_dev alone (16-B aligned, inside a
+   registered range, room for copy_sz rounded up to 16 plus 852 bytes of fd_txn_t image), with no order
+   between the records of a batch.  The batch arena takes records in submission order.  A batch holds
+   records of one form: switching forms launches the filling batch.  Same results.  flags may also carry
+   FDGPU_GATHER_SEED( i ): the record's HA dedup tag is computed with seed i of
+   fdgpu_ed25519_set_dedup_seeds (each verify tile has a secure seed of its own, fd_verify_tile.c:166). */
+#define FDGPU_GATHER_SEED( i ) ( ( (unsigned)(i) & 15u ) << 8 )
+/* n (0..16) per-record HA dedup seeds (0: back to the single seed of fdgpu_ed25519_set_dedup); turns the
+   dedup tags on.  0, or -1 */
+int           fdgpu_ed25519_set_dedup_seeds( fdgpu_ed25519_ctx_t * ctx, unsigned long const * seeds, int n );
+int           fdgpu_ed25519_submit_raw_gather_to( fdgpu_ed25519_ctx_t * ctx, unsigned char const * src,
+                                                  unsigned char const * src_dev, unsigned char * dst_dev,
+                                                  unsigned short copy_sz, unsigned short payload_off,
+                                                  unsigned short payload_sz, unsigned long tag,
+                                                  unsigned long const * seq_dev, unsigned long seq, unsigned flags );
 /* the region registered with fdgpu_host_register / fdgpu_host_alloc that holds p: its host base, size and
    device base; 0, or -1 if p is in none */
 int           fdgpu_host_region( void const * p, void ** base, unsigned long * sz, void ** dev_base );

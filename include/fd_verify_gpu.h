@@ -381,10 +381,111 @@ int             fdgpu_vtile_faulted( fdgpu_vtile_t const * vt );
 int             fdgpu_vtile_recover( fdgpu_vtile_t * vt );
 /* host-side test hook: engine context k of the tile fails (fdgpu_ed25519_debug_fault) */
 void            fdgpu_vtile_debug_fault( fdgpu_vtile_t * vt, int k );
+/* host-side test hook: the launch thread (fdgpu_vtile_opts_t.launcher) fails every batch launch of engine
+   context k from now on (fdgpu_ed25519_debug_fail_launch): the context faults asynchronously, on that thread */
+void            fdgpu_vtile_debug_fail_launch( fdgpu_vtile_t * vt, int k );
 void            fdgpu_vtile_gpu_metrics( fdgpu_vtile_t * vt, fdgpu_vtile_gpu_metrics_t * out );
 /* metrics: [0] parse_fail [1] verify_fail [2] dedup_fail
    [3] bundle_peer_fail [4] published (fd_verify_tile.c:29-34) */
 void            fdgpu_vtile_metrics( fdgpu_vtile_t const * vt, unsigned long out[ 5 ] );
+
+/* ---- the verify service: several verify-tile processes on one GPU -------
+
+   The reference runs each verify tile as a sandboxed process of its own, six by default
+   (src/disco/topo/fd_topo_run.c:66-153, src/app/fdctl/config/default.toml:788).  Tile processes that
+   each open a HIP context of their own contend for the GPU's queues and CUs as strangers: their batch
+   chains collide (profiles/r05/n2b: two such processes per GPU lowered the paced knee from 10M to 4M
+   frags/s per device).  The verify service is one process per GPU that owns the GPU: it maps the tiles'
+   in links and out dcaches, takes the frags of all of its tiles from shared-memory request rings, batches
+   them together (one batch holds frags of several tiles; each record still goes back into its own tile's
+   out dcache and its HA dedup tag is computed with its tile's seed) and returns every verdict into its
+   tile's completion ring, in the tile's order.  A tile then makes no GPU runtime call at all: its
+   during_frag writes a 32-byte request, its after_frags reads 32-byte completions and does the
+   order-dependent half of after_frag itself, exactly as with engine contexts of its own (same
+   fdgpu_vtile_* calls, same published stream).  Precedent: WireDancer's request / response rings
+   (src/wiredancer/c/wd_f1.h:71-113).
+
+   The service's shared segment: a header, per tile a request ring, a completion ring and the tile's out
+   dcache.  The service process creates it (fdgpu_vsvc_new: a file at `path`, or anonymous shared memory
+   inherited by tile processes forked before fdgpu_vsvc_start), names the in regions it will map
+   (fdgpu_vsvc_add_region: the in links' dcaches and mcaches, each a region id), then
+   fdgpu_vsvc_start( device ) -- from here on it is the only process with a GPU context -- and calls
+   fdgpu_vsvc_poll in its loop.  A tile process joins (fdgpu_vsvc_join, or the inherited handle),
+   creates its tile with fdgpu_vtile_new_svc( svc, client ), tells it where the same regions lie in its
+   own address space (fdgpu_vtile_set_svc_region) and uses it as any tile. */
+#define FDGPU_VSVC_CLIENT_MAX 16
+#define FDGPU_VSVC_RGN_MAX    16
+typedef struct fdgpu_vsvc fdgpu_vsvc_t;
+typedef struct fdgpu_vsvc_cfg {
+  int           clients;          /* verify tiles served, 1..FDGPU_VSVC_CLIENT_MAX */
+  unsigned long out_dcache_bytes; /* each tile's out dcache (fd_txn_m_t records, 64-B chunks) */
+  unsigned long batch_txn;        /* transactions per GPU batch */
+  unsigned long max_inflight;     /* adaptive batching: launch the filling batch while fewer than this many are on the
+                                     GPU (1..3; 0 = 2), as fdgpu_vtile_housekeep */
+  int           semantics;        /* FDGPU_SEMANTICS_* */
+  /* the service's engine contexts, as a tile's (fdgpu_vtile_opts_t; 0 = the same defaults) */
+  int           nctx;
+  unsigned long small_max, min_batch, max_wait_ns, copy_wait_ns, copy_min;
+  unsigned int  gather_cus;
+  int           cu_split, cu_exclusive, lat_share;
+  int           launcher;         /* 1: the batch launches and copies on a launch thread of the service's own */
+  int           launcher_core;    /* with launcher: 1 + its CPU (0: not pinned) */
+} fdgpu_vsvc_cfg_t;
+
+/* metrics of a service, as a tile's GPU metrics: batches, transactions batched, in-flight
+   high-water, latency histogram, gathers, phases, launch thread; plus frags taken / completed, passes
+   of the loop that did some work, and engine contexts faulted */
+typedef struct fdgpu_vsvc_stats {
+  fdgpu_vtile_gpu_metrics_t gm;
+  unsigned long taken, completed, fault_completions, busy_polls, polls, faults, recovered;
+  unsigned long loop_ns, busy_ns;   /* fdgpu_vsvc_poll time in all passes / in the passes that did work */
+} fdgpu_vsvc_stats_t;
+
+/* create the segment (no GPU call): path NULL = anonymous shared memory (for tile processes forked from
+   this one).  NULL on failure. */
+fdgpu_vsvc_t *  fdgpu_vsvc_new( char const * path, fdgpu_vsvc_cfg_t const * cfg );
+/* a tile process: map the service segment at path (waiting up to timeout_s for it to appear) */
+fdgpu_vsvc_t *  fdgpu_vsvc_join( char const * path, double timeout_s );
+/* service: region id (0..FDGPU_VSVC_RGN_MAX-1) is [base, base+sz) in this process (an in link's dcache or
+   mcache lines); registered with the GPU by fdgpu_vsvc_start.  Before start; 0 or -1. */
+int             fdgpu_vsvc_add_region( fdgpu_vsvc_t * svc, int id, void * base, unsigned long sz );
+/* service: the GPU side -- engine contexts on device, the regions and out dcaches registered -- then the
+   segment reads ready (tiles may take frags before: their requests wait).  0 or < 0. */
+int             fdgpu_vsvc_start( fdgpu_vsvc_t * svc, int device );
+/* 1 once the service is started, -1 if its start failed, 0 before */
+int             fdgpu_vsvc_ready( fdgpu_vsvc_t const * svc );
+/* service: one pass of its loop (take requests, launch, copy, drain verdicts into the tiles' rings,
+   recreate faulted contexts once drained); returns 1 if it did any work */
+int             fdgpu_vsvc_poll( fdgpu_vsvc_t * svc );
+/* service: poll until fdgpu_vsvc_stop (any process); returns 0 */
+int             fdgpu_vsvc_run( fdgpu_vsvc_t * svc );
+void            fdgpu_vsvc_stop( fdgpu_vsvc_t * svc );
+/* frags taken from the tiles and not yet returned to them */
+unsigned long   fdgpu_vsvc_pending( fdgpu_vsvc_t const * svc );
+void            fdgpu_vsvc_stats( fdgpu_vsvc_t * svc, fdgpu_vsvc_stats_t * out );
+/* unmap (the service also deletes its contexts and unregisters its regions; the creator of a path
+   unlinks it) */
+void            fdgpu_vsvc_delete( fdgpu_vsvc_t * svc );
+
+/* test hook (no GPU call): a CPU stand-in for the GPU side of a service not started -- completes every request
+   published so far with codes[ request index % ncodes ], footprint fp, the record copied into the tile's out
+   dcache after the overrun check, and the HA dedup tag of its first signature; returns how many */
+unsigned long   fdgpu_vsvc_debug_serve( fdgpu_vsvc_t * svc, int const * codes, unsigned long ncodes, unsigned long fp );
+
+/* a verify tile served by svc as client (0..clients-1): no GPU call here or later.  Its out dcache is
+   the segment's (fdgpu_vtile_out_dcache).  opts: the tile's own options (copy backlog, copy threads,
+   host dedup tag); the GPU-side ones are the service's.  NULL on failure. */
+fdgpu_vtile_t * fdgpu_vtile_new_svc( fdgpu_vsvc_t * svc, int client, unsigned long tcache_depth, unsigned long seed,
+                                     fdgpu_vtile_opts_t const * opts );
+/* served tile: region id lies at [base, base+sz) in this process (the same region the service added) */
+int             fdgpu_vtile_set_svc_region( fdgpu_vtile_t * vt, int id, void const * base, unsigned long sz );
+
+/* NUMA node of HIP device `device` from sysfs alone (no GPU call, so a process may ask before it forks
+   its tile processes): the device-th GPU node of the KFD topology (sysfs_root/class/kfd/kfd/topology/nodes,
+   nodes with SIMDs, after ROCR_VISIBLE_DEVICES and then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES), whose
+   PCI function's numa_node it reads (sysfs_root/bus/pci/devices/...).  sysfs_root NULL = "/sys".  -1 if
+   unknown.  Agrees with fdgpu_device_numa_node (tests/test_gpu_vsvc.py). */
+int             fdgpu_gpu_numa_node_sysfs( char const * sysfs_root, int device );
 
 /* ---- the configs[4] stream (BASELINE configs[4]) ------------------- */
 
@@ -426,6 +527,12 @@ typedef struct fdgpu_stream_cfg {
   unsigned long hk_ns;           /* the tile loop's housekeeping (launch decision, copies, verdict poll) at most every
                                     hk_ns while frags flow (0 = 10 us) */
   int           lat_share;       /* fdgpu_vtile_opts_t.lat_share of every tile */
+  int           svc;             /* 1: every tile is a process of its own, with no GPU context, served by one verify
+                                    service process per GPU (fdgpu_vsvc_*) that batches the frags of all of that GPU's
+                                    tiles together; 0: the tiles are threads of one process per GPU, each with its own
+                                    engine contexts.  Needs a shared link (a path): the tile processes join it */
+  unsigned long trace_cap;       /* > 0: every tile records up to this many verdicts in the link itself (fdgpu_link_trace,
+                                    from any process; served tiles need it), instead of fdgpu_link_set_trace's arrays */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
@@ -519,6 +626,15 @@ typedef struct fdgpu_link_anomaly {
   int           path;                  /* FDGPU_PATH_* or latency lanes */
 } fdgpu_link_anomaly_t;
 unsigned long   fdgpu_link_anomalies( fdgpu_link_t const * link, int tile, fdgpu_link_anomaly_t * out, unsigned long max );
+
+/* served tiles (cfg.svc): this process's verify service after fdgpu_link_run -- its metrics and the CPU its
+   loop ran on */
+int             fdgpu_link_svc_stats( fdgpu_link_t const * link, fdgpu_vsvc_stats_t * out, int * svc_cpu );
+/* served tiles: the tile program's body (fdgpu_tile <link> <service segment> <tile> <cpu> [copy cpus]): runs
+   tile `tile` of the shared link in this process, served by the service segment at svc_path, with no GPU
+   call; pinned to cpu (-1: not pinned).  0, or < 0 (the link's failure code, -10 - code). */
+int             fdgpu_link_run_tile( fdgpu_link_t * link, int tile, char const * svc_path, int cpu, int const * copy_cpus,
+                                     int ncopy );
 
 /* one process, private link, every tile on `device` (G = 1) */
 int             fdgpu_stream_run( int device, fdgpu_stream_cfg_t const * cfg, unsigned char const * payload,
