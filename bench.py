@@ -252,7 +252,7 @@ def host_plan(args, gpus: int, cores: int | None = None, nodes: dict | None = No
 def stream_legs(args) -> list[str]:
     """cal, max, one paced leg per --stream-rates entry (frags/s per GPU), unrel (--stream-only-paced: the paced
     legs alone, e.g. under a kernel trace)"""
-    if getattr(args, "stream_only_paced", False):
+    if getattr(args, "stream_only_paced", False) or getattr(args, "stream_svc", 0):
         return [f"paced@{r}" for r in _rates(args)]
     return ["cal", "max"] + [f"paced@{r}" for r in _rates(args)] + ["unrel"]
 
@@ -324,6 +324,11 @@ def _leg_cfg(args, leg, procs, cal_fps):
     if leg == "max":            # credit-based: the sustained rate with no frag lost
         n = args.stream_frags if args.stream_frags > 0 else int(1.2 * cal_fps * args.stream_seconds)
         return dict(base, tiles=T, n_frags=n, rate_fps=0.0, reliable=True)
+    if paced and getattr(args, "stream_svc", 0):
+        # served tiles: T verify-tile processes per GPU (no GPU context each), one verify service process per
+        # GPU batching all of their frags -- at the same offered load per GPU as the one-process paced legs
+        n = args.stream_frags if args.stream_frags > 0 else int(rate * procs * args.stream_paced_seconds)
+        return dict(base, tiles=args.stream_svc * procs, n_frags=n, rate_fps=rate * procs, reliable=False, svc=1)
     if paced:                   # the reference's unreliable link at a fixed offered load (per GPU)
         n = args.stream_frags if args.stream_frags > 0 else int(rate * procs * args.stream_paced_seconds)
         return dict(base, tiles=Tl, n_frags=n, rate_fps=rate * procs, reliable=False)
@@ -344,6 +349,31 @@ def knee_of(curve: list) -> float | None:
             break
         knee = c["offered_frags_per_s_per_gpu"]
     return knee
+
+
+def served_summary(args, raw: dict, knee_one_process) -> dict:
+    """stream.served: per T tile processes per GPU (one verify service each GPU), the paced curve and knee next
+    to the one-process knee (the same offered loads per GPU)."""
+    out = {"def": "T verify-tile processes per GPU (fdgpu_tile: no GPU context) + one verify service process per GPU "
+                  "batching all of their frags (fdgpu_vsvc_*); paced unreliable link, offered frags/s per GPU",
+           "knee_one_process": knee_one_process, "by_tiles": {}}
+    for T, r in raw.items():
+        if "error" in r:
+            out["by_tiles"][str(T)] = {"error": r["error"][-400:]}
+            continue
+        legs = r["legs"]
+        curve = [dict(legs[f"paced@{x}"], offered_frags_per_s_per_gpu=x) for x in _rates(args)]
+        out["by_tiles"][str(T)] = {
+            "knee": knee_of(curve),
+            "paced_fps_p50_p99_us": [[c["offered_frags_per_s_per_gpu"], c["p50_us"], c["p99_us"]] for c in curve],
+            "lost": [c["lost"] for c in curve], "overruns": [c["overruns_at_verdict"] for c in curve],
+            "all_published": all(c["metrics"][:4] == [0, 0, 0, 0] for c in curve),
+            "anomalies": sum(v["count"] for v in (r.get("anomalies") or {}).values()),
+            "gpu_pauses_over_250us": [(c.get("gather_gpu") or {}).get("issue_to_start_over_250us") for c in curve],
+            "mean_batch_txns": [round(c["mean_batch_txns"], 1) for c in curve],
+            "served": [c.get("served") for c in curve],
+            "curve": curve}
+    return out
 
 
 def _phases(ph) -> dict:
@@ -606,8 +636,11 @@ def stream_child_main(args) -> None:
         n_pay = max(args.txns, 2 * tiles * (1 << 16))
         payload, desc, _, _ = synth.make_batch(n_pay, synth.LARGE_NOOP, seed=args.stream_seed,
                                                threads=min(16, os.cpu_count() or 1))
+    svc_stats = {}
     for leg in stream_legs(args):
-        path = f"/dev/shm/fdgpu_link_{args.stream_token}_{leg.replace('@', '_')}" if procs > 1 else None
+        # (served tiles are processes of their own that join the link by its file)
+        path = (f"/dev/shm/fdgpu_link_{args.stream_token}_{leg.replace('@', '_')}"
+                if procs > 1 or args.stream_svc else None)
         if proc == 0:
             cfg = _leg_cfg(args, leg, procs, cal_fps)
             link = vtile.Link(path, create=True, payload=payload, off=desc["payload_off"], sz=desc["payload_sz"], **cfg)
@@ -620,6 +653,8 @@ def stream_child_main(args) -> None:
                         raise RuntimeError(f"leg {leg}: fdgpu_link_run {rc}")
                     st = link.result(timeout_s=120.0)
                 anomalies(link, leg)
+                if args.stream_svc:
+                    svc_stats[leg] = link.svc_stats()
             finally:
                 link.close()
                 if path and os.path.exists(path):
@@ -629,6 +664,13 @@ def stream_child_main(args) -> None:
             else:
                 out[leg] = dict(_leg_summary(st, cfg), anon_huge_mb=huge_mb, kfd_queues_peak=kq.peak,
                                 gpu_pauses=gpu_pause_log(reset=True))
+                if args.stream_svc:
+                    sv = svc_stats[leg]
+                    out[leg]["served"] = {"tile_processes": cfg["tiles"], "tiles_gpu_open": st["tiles_gpu_open"],
+                                          "service_cpu": sv["cpu"], "mixed_batches": sv["mixed_batches"],
+                                          "batches": sv["gm"]["batches"], "fault_completions": sv["fault_completions"],
+                                          "service_busy_ns_per_frag": round(sv["busy_ns"] / max(sv["completed"], 1), 1),
+                                          "service_loop_ns_per_frag": round(sv["loop_ns"] / max(sv["completed"], 1), 1)}
         else:
             link = vtile.Link(path, create=False, timeout_s=180.0 if leg == "cal" else 120.0)   # bounded if process 0 failed
             try:
@@ -671,7 +713,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
          "--stream-tput-min-batch", str(args.stream_tput_min_batch),
          "--stream-tput-small-max", str(args.stream_tput_small_max), "--stream-lat-hk-us", str(args.stream_lat_hk_us),
          "--stream-lat-small-max", str(args.stream_lat_small_max), "--stream-quad-sha", str(args.stream_quad_sha),
-         "--stream-lat-share", str(args.stream_lat_share)]
+         "--stream-lat-share", str(args.stream_lat_share), "--stream-svc", str(getattr(args, "stream_svc", 0))]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -801,6 +843,14 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 # first one with the GPU batch that produced it (leg, tile, ctx, seq, payload, code, path)
                 "anomalies": n_anom, "anomaly_first": first_anom}
             rec["stream_ok"] = bool(st.get("all_published")) and n_anom == 0
+            sv = st.get("served")
+            if sv:   # T tile processes per GPU served by one verify service: knee and p99 per offered rate
+                rec["stream"]["served"] = {
+                    T: ({"error": v["error"][-200:]} if "error" in v else
+                        {"knee": v["knee"], "p99_us": [_r(x[2]) for x in v["paced_fps_p50_p99_us"]],
+                         "all_published": v["all_published"], "anomalies": v["anomalies"],
+                         "tiles_gpu_open": sum((x or {}).get("tiles_gpu_open", 0) for x in v["served"])})
+                    for T, v in sv["by_tiles"].items()}
     hp = full.get("host_plan")
     if hp:      # the configs[4] stream's host budget at this N (cores for its spinning tiles and producers)
         rec["host_plan"] = {"usable_cores": hp["usable_cores"], "need_cores": hp["requested"]["cores"],
@@ -1068,6 +1118,11 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-copy-threads", type=int, default=0, choices=range(0, 9),
                     help="max-rate and unreliable legs: host threads per tile that copy each record into the out dcache "
                          "while the GPU copy only reads it (fdgpu_vtile_opts_t.copy_threads; a core each in the host plan)")
+    ap.add_argument("--stream-svc-tiles", default="",
+                    help="served paced legs: for each T in this comma list, T verify-tile processes per GPU (the fdgpu_tile "
+                         "program, no GPU context each) served by one verify service process per GPU (fdgpu_vsvc_*), at "
+                         "the --stream-rates offered loads per GPU; stream.served[T] holds the curve and knee (empty: skip)")
+    ap.add_argument("--stream-svc", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--stream-only-paced", action="store_true",
                     help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",
@@ -1128,6 +1183,17 @@ def main():
             res = run_stream_child(args, dev, rank, world, token)
         except Exception as e:      # keep the headline line even if the stream leg fails
             err = str(e)[-2000:]
+        # served paced legs (--stream-svc-tiles): T tile processes + one verify service process per GPU, a fresh
+        # stream child per T, every rank in step
+        served_raw = {}
+        for T in [int(x) for x in str(args.stream_svc_tiles).split(",") if x.strip()]:
+            a2 = argparse.Namespace(**vars(args))
+            a2.stream_svc = T
+            try:
+                served_raw[T] = run_stream_child(a2, dev, rank, world, f"{token}_s{T}")
+            except Exception as e:
+                served_raw[T] = {"error": str(e)[-1500:]}
+            barrier()
         # every rank takes part in the same collectives, whatever happened locally
         _, stream_ok = shard.reduce_max_min(dd, 0.0, err is None, "cpu")
         mine = (res or {}).get("anomalies", {})
@@ -1186,6 +1252,8 @@ def main():
                           "kfd_queues_before": kq0}
             else:
                 stream = {"error": err or "a stream child failed on another rank"}
+            if served_raw:
+                stream["served"] = served_summary(args, served_raw, (stream.get("knee") or {}).get("frags_per_s_per_gpu"))
 
         return stream
 

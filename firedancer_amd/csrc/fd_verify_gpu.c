@@ -1624,6 +1624,7 @@ typedef struct {                 /* one tile's results, written once when it fin
      with how many there were -- in the link, so a tile in a process of its own (served tiles) reports them too */
   ulong trace_cnt;
   ulong anom_cnt;
+  ulong gpu_open;                /* the tile's process had the GPU open (/dev/kfd, /dev/dri) when it finished */
   fdgpu_link_anomaly_t anom[ LINK_ANOM_MAX ];
 } link_res_t;
 
@@ -2243,6 +2244,24 @@ link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, 
   if( n ) *t_last = t;
 }
 
+/* 1 if this process has the GPU open: a descriptor on /dev/kfd or a /dev/dri node (a HIP context's) */
+static int proc_has_gpu_open( void ) {
+  DIR * d = opendir( "/proc/self/fd" );
+  if( !d ) return -1;
+  int found = 0;
+  struct dirent * e;
+  while( ( e = readdir( d ) ) && !found ) {
+    char p[ 320 ], t[ 256 ];
+    snprintf( p, sizeof(p), "/proc/self/fd/%s", e->d_name );
+    ssize_t n = readlink( p, t, sizeof(t) - 1 );
+    if( n <= 0 ) continue;
+    t[n] = 0;
+    found = !strncmp( t, "/dev/kfd", 8 ) || !strncmp( t, "/dev/dri/", 9 );
+  }
+  closedir( d );
+  return found;
+}
+
 static void * link_tile( void * _a ) {
   link_tile_arg_t * a = (link_tile_arg_t *)_a;
   link_pin( a->cpu );                          /* before any allocation: first touch on the tile's node */
@@ -2441,6 +2460,7 @@ static void * link_tile( void * _a ) {
   ulong cpu1, iv1;
   thread_usage( &cpu1, &iv1 );
   r->cpu_ns = cpu1 - cpu0; r->wall_ns = t_end - t_begin; r->nivcsw = iv1 - iv0; r->cpu = a->cpu;
+  r->gpu_open = proc_has_gpu_open() > 0;
   memcpy( l->hist + (ulong)idx * LH_N, lh, LH_N * sizeof(ulong) );
   /* (a served tile is counted done by its service's process, once it has added the GPU side's metrics) */
   if( !a->svc ) atomic_fetch_add_explicit( &h->tiles_done, 1UL, memory_order_release );
@@ -2717,6 +2737,7 @@ fdgpu_link_result( fdgpu_link_t * l, double timeout_s, fdgpu_stream_stats_t * st
     if( r->gm.launcher[2] > st->launcher[2] ) st->launcher[2] = r->gm.launcher[2];
     if( r->gm.launcher[4] > st->launcher[4] ) st->launcher[4] = r->gm.launcher[4];
     for( int k=0; k<4; k++ ) st->host_copy[k] += r->gm.host_copy[k];
+    st->tiles_gpu_open += r->gpu_open;
     st->tile_idle_ns += r->ns_idle;
     st->tile_cpu_ns += r->cpu_ns; st->tile_wall_ns += r->wall_ns; st->tile_nivcsw += r->nivcsw;
     double share = r->wall_ns ? (double)r->cpu_ns / (double)r->wall_ns : 1.;

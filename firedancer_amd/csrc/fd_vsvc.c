@@ -424,6 +424,11 @@ fdgpu_vsvc_poll( fdgpu_vsvc_t * s ) {
     fdgpu_ed25519_front_batch( s->ctx[k], &bt, &bc, &bp );
     ulong got = fdgpu_ed25519_poll_raw( s->ctx[k], s->p_tags, s->p_codes, NULL, s->p_fp, s->p_dtag, want, 0 );
     if( !got ) break;                                      /* (faulted just now: completed on the next pass) */
+    if( !bc ) {                                            /* a batch's first verdicts: did it hold several tiles' frags? */
+      unsigned c0 = e->client;
+      for( ulong i=1; i<bt && s->phead + i < s->ptail; i++ )
+        if( s->pend[ ( s->phead + i ) % s->pcap ].client != c0 ) { s->st.mixed_batches++; break; }
+    }
     for( ulong i=0; i<got; i++ ) {
       e = &s->pend[ s->phead % s->pcap ];
       if( s->p_tags[i] != s->phead ) {

@@ -111,7 +111,8 @@ class VsvcCfg(ctypes.Structure):
 class VsvcStats(ctypes.Structure):
     _fields_ = [("gm", GpuMetrics), ("taken", ctypes.c_ulong), ("completed", ctypes.c_ulong),
                 ("fault_completions", ctypes.c_ulong), ("busy_polls", ctypes.c_ulong), ("polls", ctypes.c_ulong),
-                ("faults", ctypes.c_ulong), ("recovered", ctypes.c_ulong), ("loop_ns", ctypes.c_ulong),
+                ("faults", ctypes.c_ulong), ("recovered", ctypes.c_ulong), ("mixed_batches", ctypes.c_ulong),
+                ("loop_ns", ctypes.c_ulong),
                 ("busy_ns", ctypes.c_ulong)]
 
     def as_dict(self) -> dict:
@@ -136,7 +137,8 @@ class StreamStats(ctypes.Structure):
                 ("tile_cpu_ns", ctypes.c_ulong), ("tile_wall_ns", ctypes.c_ulong), ("tile_nivcsw", ctypes.c_ulong),
                 ("tile_cpu_share_min", ctypes.c_double), ("tile_cpu", ctypes.c_long * 8),
                 ("prod_cpu_ns", ctypes.c_ulong), ("prod_wall_ns", ctypes.c_ulong), ("prod_nivcsw", ctypes.c_ulong),
-                ("launcher", ctypes.c_ulong * 6), ("host_copy", ctypes.c_ulong * 4), ("prod_cpu", ctypes.c_long * 4)]
+                ("launcher", ctypes.c_ulong * 6), ("host_copy", ctypes.c_ulong * 4), ("prod_cpu", ctypes.c_long * 4),
+                ("tiles_gpu_open", ctypes.c_ulong)]
 
     def as_dict(self) -> dict:
         out = {}

@@ -438,6 +438,7 @@ typedef struct fdgpu_vsvc_cfg {
 typedef struct fdgpu_vsvc_stats {
   fdgpu_vtile_gpu_metrics_t gm;
   unsigned long taken, completed, fault_completions, busy_polls, polls, faults, recovered;
+  unsigned long mixed_batches;      /* batches that held the frags of more than one tile */
   unsigned long loop_ns, busy_ns;   /* fdgpu_vsvc_poll time in all passes / in the passes that did work */
 } fdgpu_vsvc_stats_t;
 
@@ -574,6 +575,8 @@ typedef struct fdgpu_stream_stats {
                                     commands over 250 us (summed) */
   unsigned long host_copy[ 4 ];  /* the tiles' copy threads (cfg.copy_threads), fdgpu_vtile_gpu_metrics_t.host_copy summed */
   long          prod_cpu[ 4 ];   /* the CPUs producers 0..3 were pinned to (-1: none or not run) */
+  unsigned long tiles_gpu_open;  /* tiles whose process had the GPU open (/dev/kfd or a /dev/dri node) when the tile
+                                    finished: every tile with engine contexts of its own, no served tile */
 } fdgpu_stream_stats_t;
 
 /* The link -- mcache, in dcache (one prefilled fd_txn_m_t record per

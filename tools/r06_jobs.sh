@@ -13,5 +13,13 @@ case "$job" in
       "bench:400:python bench.py --detail-out $d/bench_detail.json > $d/bench_line.json" \
       "tests:600:$T tests/test_gpu_stream_parity.py tests/test_gpu_vtile.py tests/test_gpu_stem.py"
     ;;
+  svc)
+    # the verify service: its GPU tests (served tile processes against the reference tile, fault path, numa lookup,
+    # the launch-thread failure), then paced curves with T = 1, 2, 3 tile processes per GPU next to the default legs
+    d=gpurun_out/r06_svc; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "tests:700:$T tests/test_gpu_vsvc.py" \
+      "bench:600:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-svc-tiles 1,2,3 --detail-out $d/detail.json > $d/line.json"
+    ;;
   *) echo "unknown job $job"; exit 2 ;;
 esac
