@@ -852,7 +852,7 @@ fdgpu_vtile_recover( fdgpu_vtile_t * vt ) {
 
 void
 fdgpu_vtile_debug_fault( fdgpu_vtile_t * vt, int k ) {
-  if( vt->svc ) { if( k >= 0 && k < VSVC_NCTX_MAX ) atomic_store_explicit( &vt->sc->dbg_fault, k + 1, memory_order_release ); return; }
+  if( vt->svc ) { if( k >= 0 && k < VSVC_NCTX_MAX ) atomic_fetch_or_explicit( &vt->sc->dbg_fault, 1 << k, memory_order_release ); return; }
   if( k >= 0 && k < vt->nctx ) fdgpu_ed25519_debug_fault( vt->ctx[k] );
 }
 

@@ -48,7 +48,7 @@ typedef struct __attribute__(( aligned( 64 ) )) {
   _Atomic unsigned long flush;      /* bumped: launch the filling batches now (fdgpu_vtile_flush, a blocking drain) */
   _Atomic unsigned long gather;     /* bumped: start the copies of every frag taken (fdgpu_vtile_copy) */
   _Atomic int           state;      /* 0 free, 1 attached, 2 detached */
-  _Atomic int           dbg_fault;  /* test hook: 1 + the service's engine context to fault (fdgpu_vtile_debug_fault) */
+  _Atomic int           dbg_fault;  /* test hook: bit k = fault the service's engine context k (fdgpu_vtile_debug_fault) */
   unsigned long         seed;       /* the tile's HA dedup seed (written before state = 1) */
   long                  pid;
   unsigned char         _pad0[ 8 ];

@@ -335,6 +335,8 @@ class VTile:
         self.service = service
         if service is not None:
             self.p = self.L.fdgpu_vtile_new_svc(service.p, client, tcache_depth, seed, ctypes.byref(o))
+            if self.p:
+                service._tiles.add(self)
         else:
             self.p = self.L.fdgpu_vtile_new_opts(device, batch_txn, tcache_depth, seed, out_dcache_bytes, semantics,
                                                  ctypes.byref(o))
@@ -489,6 +491,8 @@ class Service:
             self.p = self.L.fdgpu_vsvc_join(path.encode(), timeout_s)
         if not self.p:
             raise RuntimeError(f"fdgpu_vsvc_{'new' if create else 'join'}({path}) failed")
+        import weakref
+        self._tiles = weakref.WeakSet()      # served tiles of this process: closed before the segment is unmapped
 
     def add_region(self, rid: int, base: int, sz: int) -> int:
         return int(self.L.fdgpu_vsvc_add_region(self.p, rid, base, sz))
@@ -514,6 +518,8 @@ class Service:
 
     def close(self):
         if getattr(self, "p", None):
+            for t in list(getattr(self, "_tiles", ())):
+                t.close()
             self.L.fdgpu_vsvc_delete(self.p)
             self.p = None
 

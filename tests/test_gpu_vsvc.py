@@ -159,6 +159,13 @@ def test_served_in_process_codes_and_fault_recovery():
     pays = [payload[d["payload_off"]: d["payload_off"] + d["payload_sz"]].tobytes() for d in desc]
     want = [0 if e == 0 else 2 for e in expect]          # FDGPU_VTILE_PUBLISH / _VERIFY_FAIL
     r = _InProc()
+    try:
+        _in_process_phases(r, pays, want)
+    finally:                                             # (before the interpreter's exit tears HIP down)
+        r.tile.close(); r.svc.close()
+
+
+def _in_process_phases(r, pays, want):
     r.feed(pays[:200])
     out = r.drain(200)
     assert [d[0] for d in out] == list(range(200)) and [d[1] for d in out] == want[:200]
@@ -175,7 +182,6 @@ def test_served_in_process_codes_and_fault_recovery():
     assert [d[1] for d in out] == want[400:600]
     st = r.svc.stats()
     assert st["recovered"] >= 1 and st["fault_completions"] == res.count(6)
-    r.tile.close(); r.svc.close()
 
 
 def test_launch_thread_failure_does_not_hang_blocking_drain():
@@ -185,10 +191,12 @@ def test_launch_thread_failure_does_not_hang_blocking_drain():
     payload, desc, _, _ = synth.make_batch(64, synth.LARGE_NOOP, seed=9)
     pays = [payload[d["payload_off"]: d["payload_off"] + d["payload_sz"]].tobytes() for d in desc]
     t = vtile.VTile(device=0, batch_txn=256, nctx=1, launcher=1)
-    t.debug_fail_launch(0)
-    for s, p in enumerate(pays):
-        assert t.during_frag(vtile.frag_bytes(p), s) == 0
-    out = t.after_frags(256, blocking=True)               # (pytest's timeout ends a hang)
-    assert [d[0] for d in out] == list(range(64)) and all(d[1] == vtile.GPU_FAULT for d in out)
-    assert t.faulted() == 1
-    t.close()
+    try:
+        t.debug_fail_launch(0)
+        for s, p in enumerate(pays):
+            assert t.during_frag(vtile.frag_bytes(p), s) == 0
+        out = t.after_frags(256, blocking=True)           # (pytest's timeout ends a hang)
+        assert [d[0] for d in out] == list(range(64)) and all(d[1] == vtile.GPU_FAULT for d in out)
+        assert t.faulted() == 1
+    finally:
+        t.close()
