@@ -494,6 +494,21 @@ def _anon_huge_mb() -> float | None:
     return None
 
 
+def page_config() -> dict:
+    """The host's page setup the links live on: transparent huge pages for anonymous memory (a one-process link)
+    and for shared memory (/dev/shm: the link of several processes, the verify service's segment), and
+    reserved hugetlb pages (none: shared memory is then in 4 KiB pages)."""
+    def rd(p):
+        try:
+            return open(p).read().strip()
+        except OSError:
+            return None
+    sel = lambda v: (v.split("[")[1].split("]")[0] if v and "[" in v else v)
+    return {"thp": sel(rd("/sys/kernel/mm/transparent_hugepage/enabled")),
+            "shmem_thp": sel(rd("/sys/kernel/mm/transparent_hugepage/shmem_enabled")),
+            "hugetlb_pages": rd("/proc/sys/vm/nr_hugepages")}
+
+
 def _kfd_gpu_ids() -> set[str]:
     """KFD gpu_ids of the GPUs this process sees (topology nodes with SIMDs)."""
     ids, base = set(), "/sys/class/kfd/kfd/topology/nodes"
@@ -1249,7 +1264,7 @@ def main():
                           "host_cpu_share_min": min((l.get("host_cpu") or {}).get("tile_share_min", 1.0)
                                                     for l in [mx, ur] + curve),
                           "latency_def": "producer mcache publish (tsorig) -> after_frag verdict on the host",
-                          "kfd_queues_before": kq0}
+                          "kfd_queues_before": kq0, "pages": page_config()}
             else:
                 stream = {"error": err or "a stream child failed on another rank"}
             if served_raw:

@@ -112,6 +112,14 @@ fdgpu_vsvc_join( char const * path, double timeout_s ) {
             fdgpu_vsvc_t * s = (fdgpu_vsvc_t *)calloc( 1, sizeof(fdgpu_vsvc_t) );
             if( !s ) { munmap( base, total ); return NULL; }
             s->h = (vsvc_hdr_t *)base; s->base = base; s->sz = total; strcpy( s->path, path );
+            /* the rings' pages now (a tile writes requests and reads completions from its first frag on; the
+               out dcaches, which only the GPU and the tile's readers touch, are left to fault in) */
+            for( int c=0; c<s->h->clients; c++ ) {
+              vsvc_client_t const * k = &s->h->client[c];
+              ulong lo = k->off_req & ~4095UL, hi = k->off_cpl + k->ring_cap * sizeof(vsvc_cpl_t);
+              (void)madvise( base + lo, hi - lo, MADV_WILLNEED );
+              for( ulong o=lo; o<hi; o+=4096UL ) (void)*(volatile uchar const *)( base + o );
+            }
             atomic_fetch_add( &s->h->joined, 1UL );
             return s;
           }

@@ -21,6 +21,12 @@ case "$job" in
       "tests:700:$T tests/test_gpu_vsvc.py" \
       "bench:600:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-svc-tiles 1,2,3 --detail-out $d/detail.json > $d/line.json"
     ;;
+  svc2)
+    d=gpurun_out/r06_svc2; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "bench:600:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-svc-tiles 1,2,3 --detail-out $d/detail.json > $d/line.json" \
+      "tests:600:$T tests/test_gpu_stream_parity.py -k 'reliable and not launch and not host'"
+    ;;
   svcdbg)
     bash tools/gpu_job.sh \
       "tests:300:$T -x tests/test_gpu_vsvc.py -k 'in_process or launch_thread'"
