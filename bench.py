@@ -151,7 +151,6 @@ def cpu_sweep_configs0(impl, kind, max_threads, gen_threads, point_s=0.6):
 # Every record also crosses host DRAM twice (the GPU's gather reads it, the write-back lands in the out
 # dcache): ~34 GB/s each way per GPU at the measured 25.6M frags/s.
 HOST_GBS_PER_GPU_EACH_WAY = 34.0
-AMD_GPU_CLASSES = ("0x030000", "0x038000", "0x120000")
 
 
 def _cpulist(path: str) -> set[int]:
@@ -166,33 +165,30 @@ def _cpulist(path: str) -> set[int]:
     return out
 
 
-def host_topology() -> tuple[dict, list]:
+def host_topology(gpus: int = 8, sysfs_root: str = "/sys") -> tuple[dict, list]:
     """({NUMA node: usable physical cores (one hardware thread each, within this process's affinity)},
-    [NUMA node of each AMD GPU in PCI order, or -1]) from sysfs."""
+    [NUMA node of HIP devices 0..gpus-1, or -1]) from sysfs.  A device's node is that of its own PCI function,
+    found as HIP numbers the devices -- the KFD topology's GPU nodes in order after ROCR_VISIBLE_DEVICES and
+    HIP_VISIBLE_DEVICES (fdgpu_gpu_numa_node_sysfs, the same lookup the link's CPU choice makes) -- not the
+    host's PCI order of every AMD GPU, which named the wrong node for a one-GPU job."""
     aff = os.sched_getaffinity(0)
     nodes = {}
-    base = "/sys/devices/system/node"
+    base = f"{sysfs_root}/devices/system/node"
     names = sorted(n for n in (os.listdir(base) if os.path.isdir(base) else []) if n.startswith("node") and n[4:].isdigit())
     for n in names:
         cpus = _cpulist(f"{base}/{n}/cpulist") & aff
         phys = {c for c in cpus
-                if min(_cpulist(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") & aff or {c}) == c}
+                if min(_cpulist(f"{sysfs_root}/devices/system/cpu/cpu{c}/topology/thread_siblings_list") & aff or {c}) == c}
         if phys:
             nodes[int(n[4:])] = len(phys)
     if not nodes:
         nodes = {0: len(aff)}
-    gpus = []
-    pci = "/sys/bus/pci/devices"
-    for d in sorted(os.listdir(pci) if os.path.isdir(pci) else []):
-        try:
-            if open(f"{pci}/{d}/vendor").read().strip() != "0x1002":
-                continue
-            if open(f"{pci}/{d}/class").read().strip() not in AMD_GPU_CLASSES:
-                continue
-            gpus.append(int(open(f"{pci}/{d}/numa_node").read().strip()))
-        except (OSError, ValueError):
-            continue
-    return nodes, gpus
+    try:
+        from firedancer_amd import vtile
+        gn = [vtile.gpu_numa_node(d, sysfs_root) for d in range(gpus)]
+    except Exception:
+        gn = []
+    return nodes, [g for g in gn if g >= 0]
 
 
 def host_plan(args, gpus: int, cores: int | None = None, nodes: dict | None = None,
@@ -205,13 +201,15 @@ def host_plan(args, gpus: int, cores: int | None = None, nodes: dict | None = No
     if cores is None:
         cores = usable_cores()[0] if not getattr(args, "plan_cores", 0) else int(args.plan_cores)
     if nodes is None:
-        nodes, probed = host_topology()
+        nodes, probed = host_topology(1 if os.environ.get("FDGPU_BENCH_ONE_DEVICE") == "1" else gpus)
         if getattr(args, "plan_cores", 0):
             nodes = {0: int(args.plan_cores)}
         gpu_nodes = probed if gpu_nodes is None else gpu_nodes
     nodes = {int(k): int(v) for k, v in nodes.items()}
     node_ids = sorted(nodes)
     gn = list(gpu_nodes or [])[:gpus]
+    if os.environ.get("FDGPU_BENCH_ONE_DEVICE") == "1" and len(gn) == 1:   # (rehearsal: every rank on device 0)
+        gn = gn * gpus
     if len(gn) < gpus or any(g not in nodes for g in gn):     # unknown placement: spread the GPUs over the nodes
         gn = [node_ids[i * len(node_ids) // gpus] for i in range(gpus)]
     P = args.stream_producers

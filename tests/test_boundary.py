@@ -83,3 +83,33 @@ def test_raw_record_layout_and_staging():
     sz = np.array([3, 3, 3, 0, 2], np.uint16)
     raw, lanes = engine.raw_records(payload, off, sz)
     assert raw["sig_lanes"].tolist() == [1, 3, 0, 0, 2] and raw["sig_base"].tolist() == [0, 1, 4, 4, 4] and lanes == 6
+
+
+REF_SRC = "/root/reference/src"
+
+
+def _compile_dropin(inc_dir):
+    return subprocess.run(["gcc", "-std=gnu17", "-Wall", "-Wextra", "-Werror", "-c", "-o", os.devnull,
+                           f"-I{REF_SRC}", f"-I{inc_dir}", os.path.join(ROOT, "tests", "boundary", "dropin_with_ref_header.c")],
+                          capture_output=True, text=True)
+
+
+def test_dropin_prototypes_compile_beside_the_reference_header(tmp_path):
+    """the reference's src/ballet/ed25519/fd_ed25519.h, included in place, and then
+    include/fd_ed25519_gpu.h in one translation unit under -Wall -Werror, calling both drop-ins -- and, as a
+    control, the same with a copy of our header whose fd_ed25519_verify takes a 32-bit msg_sz, which must not
+    compile (so the check bites).  Needs the reference tree (this container; absent on the GPU box)."""
+    import pytest
+    import shutil
+    if not os.path.exists(os.path.join(REF_SRC, "ballet", "ed25519", "fd_ed25519.h")):
+        pytest.skip("reference tree absent")
+    r = _compile_dropin(os.path.join(ROOT, "include"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    bad = tmp_path / "inc"
+    bad.mkdir()
+    src = open(os.path.join(ROOT, "include", "fd_ed25519_gpu.h")).read()
+    mut = src.replace("fd_ed25519_verify( unsigned char const   msg[], /* msg_sz */\n                   unsigned long  ",
+                      "fd_ed25519_verify( unsigned char const   msg[], /* msg_sz */\n                   unsigned int   ", 1)
+    assert mut != src
+    (bad / "fd_ed25519_gpu.h").write_text(mut)
+    assert _compile_dropin(str(bad)).returncode != 0
