@@ -57,6 +57,44 @@ GUIDE_MAD_PEAK = GUIDE_VALU_LANE_OPS / 2
 PCIE_GBS = 63.0        # MI355X_MICROARCH.md: host link PCIe Gen5 x16, 63 GB/s per direction (spec)
 PCIE_DMA_GBS = 55.2    # hipMemcpyAsync H2D, measured (tools/gatherprobe, profiles/r02/stream/gather_probe.log)
 PREP_MAC = PREP_MUL * MAC_PER_MUL + PREP_SQR * MAC_PER_SQR
+# SHA-512 of R || A || M: ceil((msg_sz + 81) / 128) blocks of ~2.75K 64-bit operations, each two
+# 32-bit VALU lane operations on CDNA4 -> priced against the full-rate VALU issue peak
+SHA_BLOCK_OPS64 = 2750
+# algorithmic bytes of a configs[1] signature over the whole path: R || S || A (96) + the 1167-byte message in, 1 out
+ALGO_BYTES_PER_SIG = 96 + 1167 + 1
+
+
+def roofline_per_kernel(nsig: int, ms_walk: float, ms_dec: float, ms_hash: float, pm: dict) -> dict:
+    """The throughput path's three big kernels against their rooflines (all VALU issue-bound), with HIP-event
+    times of this run and the work SURVEY §8(d) counts: the walk at its half-size work (HS_MAC) and at the
+    reference DSM's (DSM_MAC); the decode kernel at the two decompressions (PREP_MAC; the -A / -R table
+    additions on top are not priced); the hash kernel at SHA-512 (10 blocks for the 1167-byte message, two
+    32-bit lane operations per 64-bit operation) against the full-rate issue peak.  Plus the per-signature
+    tables' HBM traffic (PMC, profiles/dsm_pmc.json) against the path's algorithmic bytes."""
+    blocks = -(-(1167 + 81) // 128)
+    out = {}
+    for name, ms, work, peak, unit in (("walk", ms_walk, WALK_MAC, GUIDE_MAD_PEAK, "v_mad_u64_u32"),
+                                       ("walk_ref_equiv", ms_walk, DSM_MAC, GUIDE_MAD_PEAK, "v_mad_u64_u32"),
+                                       ("decode", ms_dec, PREP_MAC, GUIDE_MAD_PEAK, "v_mad_u64_u32"),
+                                       ("hash", ms_hash, blocks * SHA_BLOCK_OPS64 * 2, GUIDE_VALU_LANE_OPS, "32-bit lane op")):
+        if ms and ms > 0:
+            rate = work * nsig / (ms * 1e-3)
+            out[name] = {"ms": round(ms, 4), "work_per_sig": work, "work_unit": unit, "achieved_t_per_s": round(rate / 1e12, 3),
+                         "peak_t_per_s": round(peak / 1e12, 2), "frac": round(rate / peak, 4)}
+    k = {"walk": pm.get("fd_dsmh_kernel<1>") or {}, "decode": pm.get("fd_decode_kernel") or {},
+         "hash": pm.get("fd_hashh_kernel") or {}}
+    for name, e in k.items():
+        if name in out and e:
+            out[name]["valu_insts_per_wave"] = e.get("valu_insts_per_wave")
+            out[name]["valu_busy_flat4"] = round(e["valu_busy_flat4"], 4) if e.get("valu_busy_flat4") else None
+    wr, rd = (k["decode"].get("hbm_write_bytes") or 0), (k["walk"].get("hbm_read_bytes") or 0)
+    if wr and rd:
+        per_sig = (wr + rd) / (1 << 20)
+        out["table_traffic"] = {"decode_writes_gb_per_1m": round(wr / 1e9, 3), "walk_reads_gb_per_1m": round(rd / 1e9, 3),
+                                "bytes_per_sig": round(per_sig), "algorithmic_bytes_per_sig": ALGO_BYTES_PER_SIG,
+                                "vs_algorithmic": round(rd / (1 << 20) / ALGO_BYTES_PER_SIG, 2),
+                                "source": "profiles/dsm_pmc.json (PMC FETCH_SIZE x2 / WRITE_SIZE, KiB, per 1M-sig launch)"}
+    return out
 
 
 def cpu_model() -> str:
@@ -793,6 +831,10 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
         "mac_per_sig": rf.get("mac_per_sig"), "valu_busy": _r(rf.get("valu_busy")),
         "traffic": rf.get("traffic"), "traffic_unit": "HBM bytes per 1M-sig launch (PMC, profiles/dsm_pmc.json)",
         "hbm_frac": _r((rf.get("hbm") or {}).get("frac")),
+        # each big kernel's fraction of its roofline, same pricing, and the -A / -R tables' HBM
+        # traffic against the path's algorithmic bytes
+        "per_kernel_frac": {k: v.get("frac") for k, v in (rf.get("per_kernel") or {}).items() if "frac" in v},
+        "table_traffic_vs_algorithmic": ((rf.get("per_kernel") or {}).get("table_traffic") or {}).get("vs_algorithmic"),
     }
     if cpu:
         sw = (cpu.get("sweep_configs0") or {}).get("points") or []
@@ -1319,6 +1361,7 @@ def main():
         eng.verify_txns_device(pay_d.data_ptr(), desc_d.data_ptr(), n, nsig, out_d.data_ptr(), None, st)
     torch.cuda.synchronize()
     ms_prep, ms_dsm, ms_red = eng.kernel_ms(0), eng.kernel_ms(1), eng.kernel_ms(2)
+    ms_dec, ms_hash = eng.kernel_ms(3), eng.kernel_ms(4)    # the prep's two kernels (throughput path)
     eng.set_timing(False)
     ok = ok and bool(np.array_equal(out_d.cpu().numpy(), expect))
     # the same steps alternating over two contexts / streams (one batch's prep overlaps the other's walk
@@ -1506,13 +1549,14 @@ def main():
         ref_equiv = DSM_MAC * nsig / (dom_ms * 1e-3)     # the reference algorithm's work at this rate
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "dsm_pmc.json")
-        valu_busy = None
+        valu_busy, pm_k = None, {}
         if os.path.exists(pmc):
             try:
                 pm = json.load(open(pmc))
-                traffic, valu_busy = pm.get("hbm_bytes_per_launch"), pm.get("valu_busy")
+                traffic, valu_busy, pm_k = pm.get("hbm_bytes_per_launch"), pm.get("valu_busy"), pm.get("per_kernel") or {}
             except Exception:
                 traffic = None
+        per_kernel = roofline_per_kernel(nsig, ms_dsm, ms_dec, ms_hash, pm_k)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cores, core_src = usable_cores()
@@ -1538,7 +1582,7 @@ def main():
                        "parallelism": f"independent per-GPU shards x{world}", "semantics": "avx512",
                        "contexts_per_gpu": args.pipe},
             "results_ok": all_ok,
-            "kernel_ms": {"prep": ms_prep, "dsm": ms_dsm, "reduce": ms_red,
+            "kernel_ms": {"prep": ms_prep, "dsm": ms_dsm, "reduce": ms_red, "decode": ms_dec, "hash": ms_hash,
                           "source": f"roofline pass: {ROOF_STEPS} more steps of the same batch, HIP events"},
             "roofline": {"bound": "valu", "achieved": achieved / 1e9, "peak": peak / 1e9, "unit": "GMAC/s",
                          "frac": achieved / peak if peak > 0 else None, "traffic": traffic,
@@ -1573,9 +1617,15 @@ def main():
                          "hbm": ({"achieved": traffic * nsig / (1 << 20) / (dom_ms * 1e-3) / 1e9, "peak": 8000.0,
                                   "unit": "GB/s",
                                   "frac": traffic * nsig / (1 << 20) / (dom_ms * 1e-3) / 8e12,
-                                  "note": "PMC bytes (FETCH_SIZE x1024 x2 + WRITE_SIZE x1024) per 1M-sig launch, "
-                                          "scaled to this launch; L2/MALL-resident tables, not HBM-bound"}
-                                 if traffic else None)},
+                                  "note": "PMC bytes (FETCH_SIZE x1024 x2 + WRITE_SIZE x1024) per 1M-sig launch, scaled "
+                                          "to this launch: the walk reads each signature's -A / -R tables, which the "
+                                          "decode kernel wrote to HBM (per-signature tables: 2.3 GB per 1M does not fit "
+                                          "the 256 MB MALL; only the B tables stay L2/MALL-resident).  Not the bound "
+                                          "(frac ~0.2): the walk is VALU issue-bound"}
+                                 if traffic else None),
+                         # each big kernel of the step against its roofline, priced as SURVEY §8(d) prices it, and
+                         # the -A / -R tables' traffic against the algorithmic bytes
+                         "per_kernel": per_kernel},
             "cpu_baseline": cpu,
             "per_gpu": per_gpu,
             "latency": lat,

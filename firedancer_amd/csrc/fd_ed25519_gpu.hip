@@ -2382,9 +2382,10 @@ struct fdgpu_ed25519_ctx {
   uint4 * d_btab2;               /*                 [0..32768](2^120 B) */
   uint4 * d_khash;               /* NULL, or (drop-in, long messages) SHA-512(R||A||M) per signature, computed beforehand */
   uint4 * d_kdig;                /* FD_SHA_SPLIT: fd_sha_kernel's digests, [max_sig][4] */
-  hipEvent_t ev[4];
+  hipEvent_t ev[5];
   enum { NRING = 64 };
-  hipEvent_t ring[ NRING ][ 4 ];  /* per-batch kernel boundaries while timing is on */
+  hipEvent_t ring[ NRING ][ 5 ];  /* per-batch kernel boundaries while timing is on: prep start, walk start, walk end,
+                                     reduce end, and (throughput path) the decode kernel's end inside the prep */
   unsigned long ring_cnt;
   /* async pipeline: NSLOT pinned staging slots, all on ctx->stream */
   enum { NSLOT = 4 };
@@ -2628,6 +2629,7 @@ static int launch_batch( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payl
       hipLaunchKernelGGL( fd_decode_kernel, dim3(pg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, 1,
                           ctx->d_pstat, ctx->d_Rxy, ctx->d_Axy, (uint4 *)NULL, (uint4 *)NULL );
 #endif
+      if( ctx->timing ) hipEventRecord( ev[4], st );     /* (the decode kernel's own time, fdgpu_ed25519_kernel_ms 3) */
       uint4 const * kh = (uint4 const *)ctx->d_khash;
       if( FD_SHA_SPLIT && !kh ) {
         hipLaunchKernelGGL( fd_sha_kernel, dim3(sg), dim3(FD_WG), 0, st, d_payload, d_desc, ctx->d_map, nsig, ctx->d_kdig );
@@ -2818,8 +2820,8 @@ ctx_init( fdgpu_ed25519_ctx_t * ctx, int device, unsigned long max_txn, unsigned
   ctx->gather_rpb = dbg.gather_rpb == 1 ? 1 : 4;
   ctx->gather_cu_spread = dbg.gather_cu_spread;
   ctx->quad_sha = dbg.quad_sha;
-  for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
-  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
+  for( int i=0; i<5; i++ ) HIPCHK( hipEventCreate( &ctx->ev[i] ), -1 );
+  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<5; i++ ) HIPCHK( hipEventCreate( &ctx->ring[r][i] ), -1 );
   ctx->ring_cnt = 0;
   hipLaunchKernelGGL( fd_btab_kernel, dim3((FD_BTAB_ENTRIES + 255)/256), dim3(256), 0, ctx->stream, ctx->d_btab, 0 );
   if( ctx->half )
@@ -2878,8 +2880,8 @@ fdgpu_ed25519_ctx_delete( fdgpu_ed25519_ctx_t * ctx ) {
   (void)hipFree( ctx->d_tabR ); (void)hipFree( ctx->d_digR ); (void)hipFree( ctx->d_htop ); (void)hipFree( ctx->d_btab2 );
   (void)hipFree( ctx->d_kdig );
   (void)hipFree( ctx->d_P ); (void)hipFree( ctx->d_O ); (void)hipFree( ctx->d_blk ); (void)hipFree( ctx->d_slow );
-  for( int i=0; i<4; i++ ) if( ctx->ev[i] ) (void)hipEventDestroy( ctx->ev[i] );
-  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<4; i++ ) if( ctx->ring[r][i] ) (void)hipEventDestroy( ctx->ring[r][i] );
+  for( int i=0; i<5; i++ ) if( ctx->ev[i] ) (void)hipEventDestroy( ctx->ev[i] );
+  for( int r=0; r<fdgpu_ed25519_ctx_t::NRING; r++ ) for( int i=0; i<5; i++ ) if( ctx->ring[r][i] ) (void)hipEventDestroy( ctx->ring[r][i] );
   for( int i=0; i<fdgpu_ed25519_ctx_t::NSLOT; i++ ) {
     fd_slot & sl = ctx->slot[i];
     if( sl.h_payload ) (void)hipHostFree( sl.h_payload );
@@ -2914,12 +2916,14 @@ extern "C" void fdgpu_ed25519_set_timing( fdgpu_ed25519_ctx_t * ctx, int enable 
    stream the kernels ran on */
 extern "C" float
 fdgpu_ed25519_kernel_ms( fdgpu_ed25519_ctx_t * ctx, int idx ) {
-  if( idx<0 || idx>2 || !ctx->ring_cnt ) return -1.f;
+  if( idx<0 || idx>4 || !ctx->ring_cnt ) return -1.f;
   unsigned long n = ctx->ring_cnt < (unsigned long)fdgpu_ed25519_ctx_t::NRING ? ctx->ring_cnt : (unsigned long)fdgpu_ed25519_ctx_t::NRING;
+  /* 0 prep, 1 walk, 2 reduce; throughput path's prep split: 3 the decode kernel, 4 the hash (+ table) kernels */
+  static int const from[5] = { 0, 1, 2, 0, 4 }, to[5] = { 1, 2, 3, 4, 1 };
   double sum = 0.;
   for( unsigned long r=0; r<n; r++ ) {
     float ms = 0.f;
-    if( hipEventElapsedTime( &ms, ctx->ring[r][idx], ctx->ring[r][idx+1] ) != hipSuccess ) return -1.f;
+    if( hipEventElapsedTime( &ms, ctx->ring[r][ from[idx] ], ctx->ring[r][ to[idx] ] ) != hipSuccess ) return -1.f;
     sum += ms;
   }
   return (float)( sum / (double)n );

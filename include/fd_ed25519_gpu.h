@@ -674,8 +674,10 @@ fdgpu_ed25519_set_lat_share( fdgpu_ed25519_ctx_t * ctx, unsigned parts );
    since fdgpu_ed25519_set_timing(ctx,1) (at most the last 64) of HIP
    events recorded on the stream the kernels ran on.  idx: 0 = prep
    (SHA-512 + decode + checks + A-table), 1 = dsm (double-scalar
-   multiplication + compare), 2 = reduce.  Valid once those batches
-   completed; -1 when nothing was timed. */
+   multiplication + compare), 2 = reduce; on the throughput path the prep
+   split in two: 3 = the decode kernel (A and R, the -A / -R tables), 4 =
+   the hash kernel (SHA-512, k mod l, the half-size scalars).  Valid once
+   those batches completed; -1 when nothing was timed. */
 void
 fdgpu_ed25519_set_timing( fdgpu_ed25519_ctx_t * ctx, int enable );
 

@@ -98,7 +98,13 @@ if d and "hbm_read_bytes" in d:
                "valu_busy": busy,
                "valu_busy_source": os.path.relpath(os.path.abspath(im), os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
                                    + " (predicted issue time / this run's rocprof launch time)" if busy is not None else None,
-               "valu_busy_flat4": d.get("valu_busy_flat4"), "valu_insts_per_wave": d.get("valu_insts_per_wave")},
+               "valu_busy_flat4": d.get("valu_busy_flat4"), "valu_insts_per_wave": d.get("valu_insts_per_wave"),
+               # the throughput path's other big kernels, per 1M-sig launch: the decode kernel writes the -A / -R
+               # tables (per signature, HBM-resident) that the walk reads; the hash kernel reads the messages
+               "per_kernel": {k: {"hbm_read_bytes": out[k].get("hbm_read_bytes"), "hbm_write_bytes": out[k].get("hbm_write_bytes"),
+                                  "valu_busy_flat4": out[k].get("valu_busy_flat4"),
+                                  "valu_insts_per_wave": out[k].get("valu_insts_per_wave")}
+                              for k in (dk, "fd_decode_kernel", "fd_hashh_kernel") if k in out}},
               open(os.path.join(os.path.dirname(dst.rstrip("/")), "..", "dsm_pmc.json"), "w"), indent=1)
 for k, e in sorted(out.items()):
     print(k, {x: (round(y, 3) if isinstance(y, float) else y) for x, y in e.items() if x != "counters_mean_per_launch"})
