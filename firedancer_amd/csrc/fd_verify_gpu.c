@@ -627,7 +627,10 @@ vt_ctx_new( fdgpu_vtile_t const * vt, int k ) {
        the share is the context's own part): a walk wider than its share would wait on the other context's
        workgroups and hold the gathers queued behind it (profiles/r05/cb) */
     unsigned share = vt->opt.lat_share > 0 ? (unsigned)vt->opt.lat_share : vt->opt.lat_share < 0 ? 0u : (unsigned)vt->nctx;
-    if( excl > 0 && fdgpu_ed25519_set_lat_share( c, share ) ) {
+    /* by the context's actual mode: also when the engine's test hook chose it (excl 0 here) -- any mode with an
+       exclusive walk (1..3) gets its share */
+    int mode = fdgpu_ed25519_get_cu_exclusive( c );
+    if( mode >= 1 && mode <= 3 && fdgpu_ed25519_set_lat_share( c, share ) ) {
       fdgpu_ed25519_ctx_delete( c ); return NULL;
     }
     fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
@@ -1178,7 +1181,11 @@ vt_during_txnm( fdgpu_vtile_t * vt, int link, void const * frag, ulong sz, ulong
      was rewriting while the stem read its line (a lapped consumer) may claim more than sz, and the stem's
      seq re-check then drops it.  So on the chunk path a payload past sz is taken (its bytes lie in the
      link's region; the stem's check, or the GPU copy's, marks the frag overrun); by pointer, where only the
-     frag's sz bytes are known readable, it is corrupt. */
+     frag's sz bytes are known readable, it is corrupt.  Only that overrun case matches the reference: a frag
+     NOT lapped whose header claims a payload past sz is copied here as 80 + payload_sz bytes of the in link
+     (the bytes after the frag), where the reference copies sz bytes (fd_verify_tile.c:79) and parses the rest
+     from whatever its out dcache held there before -- stale memory, so the two verdicts may differ for such a
+     malformed producer (parity unpinned in that corner; no test covers it). */
   if( sz > FDGPU_TPU_RAW_MTU || sz < FDGPU_TXNM_HDR_SZ || in->payload_sz > 1232U ||
       FDGPU_TXNM_HDR_SZ + in->payload_sz > readable )
     return -4;

@@ -159,7 +159,8 @@ sv_ctx_new( fdgpu_vsvc_t * s, int k ) {
   int excl = s->cfg.cu_exclusive ? s->cfg.cu_exclusive : ( fdgpu_ed25519_get_cu_exclusive( c ) ? 0 : 1 );
   if( excl > 0 && fdgpu_ed25519_set_cu_exclusive( c, excl ) ) goto fail;
   unsigned share = s->cfg.lat_share > 0 ? (unsigned)s->cfg.lat_share : s->cfg.lat_share < 0 ? 0u : (unsigned)s->nctx;
-  if( fdgpu_ed25519_get_cu_exclusive( c ) > 0 && fdgpu_ed25519_set_lat_share( c, share ) ) goto fail;
+  int mode = fdgpu_ed25519_get_cu_exclusive( c );            /* any mode with an exclusive walk gets its share */
+  if( mode >= 1 && mode <= 3 && fdgpu_ed25519_set_lat_share( c, share ) ) goto fail;
   fdgpu_ed25519_set_record_fp_off( c, 10 );          /* offsetof( fd_txn_m_t, txn_t_sz ) */
   if( fdgpu_ed25519_prepare( c, 1 ) ) goto fail;
   if( s->launcher && fdgpu_ed25519_set_launcher( c, s->launcher ) ) goto fail;
