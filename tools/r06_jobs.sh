@@ -27,6 +27,17 @@ case "$job" in
       "bench:600:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-svc-tiles 1,2,3 --detail-out $d/detail.json > $d/line.json" \
       "tests:600:$T tests/test_gpu_stream_parity.py -k 'reliable and not launch and not host'"
     ;;
+  cmp)
+    # paced curves at equal device load: one tile process with its engine contexts (A), T = 1, 2, 3 served tile
+    # processes (A), and two tile processes each with a GPU context of its own (the N = 2 rehearsal on one
+    # device: per-rank rates half the device's), then A again
+    d=gpurun_out/r06_cmp; mkdir -p $d
+    A="python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-only-paced --stream-svc-tiles 1,2,3"
+    bash tools/gpu_job.sh \
+      "a1:400:$A --detail-out $d/a1.json > $d/a1.line" \
+      "own2:400:bash tools/rehearse_n2.sh --stream-only-paced --stream-rates 1e6,2.5e6,3.75e6,5e6,7.5e6 --no-cpu-baseline --detail-out $d/own2.json > $d/own2.line" \
+      "a2:400:$A --detail-out $d/a2.json > $d/a2.line"
+    ;;
   svcdbg)
     bash tools/gpu_job.sh \
       "tests:300:$T -x tests/test_gpu_vsvc.py -k 'in_process or launch_thread'"
