@@ -320,7 +320,21 @@ def _leg_cfg(args, leg, procs, cal_fps):
     # paced legs: a batch limit of about 4 ms of one tile's share of the offered load (8K..64K), so batches
     # stay small at low load (latency path) and can grow with it; adaptive launch sizes them below that
     pb = _pow2_clamp(rate / max(1, args.stream_lat_tiles) * 4e-3, args.stream_batch, args.stream_max_batch)
-    base = dict(batch_txn=args.stream_max_batch if not paced else pb,
+    # NUMA placement of each producer's mcache, in dcache part and thread: its GPU's node (the process it runs in,
+    # q % G), or (--stream-place opposite, the cross-socket arm) a node other than that GPU's
+    gn = plan["gpu_numa_nodes"]
+    nodes = sorted(int(k) for k in plan["cores_per_numa_node"])
+    Qn = args.stream_producers * procs
+
+    def pnode(q):
+        g = gn[q % procs] if q % procs < len(gn) else None
+        if args.stream_place == "none" or g is None:
+            return None
+        if args.stream_place == "opposite":
+            return next((n for n in nodes if n != g), g)
+        return g
+    base = dict(prod_node=[pnode(q) for q in range(Qn)],
+                batch_txn=args.stream_max_batch if not paced else pb,
                 max_inflight=args.stream_inflight if not paced else args.stream_lat_inflight,
                 zero_copy=not args.stream_copy, gpus=procs,
                 producers=args.stream_producers * procs,   # the reference's QUIC tiles: producer q in process q % G
@@ -696,6 +710,8 @@ def stream_child_main(args) -> None:
             cfg = _leg_cfg(args, leg, procs, cal_fps)
             link = vtile.Link(path, create=True, payload=payload, off=desc["payload_off"], sz=desc["payload_sz"], **cfg)
             huge_mb = _anon_huge_mb()
+            place = dict(link.placement(), gpu_node=vtile.gpu_numa_node(dev), place=args.stream_place,
+                         page_config=page_config())
             gpu_pause_log(reset=True)                 # (a fresh log for this leg)
             try:
                 with KfdSampler() as kq:
@@ -714,7 +730,7 @@ def stream_child_main(args) -> None:
                 cal_fps = st["frags_per_s"]
             else:
                 out[leg] = dict(_leg_summary(st, cfg), anon_huge_mb=huge_mb, kfd_queues_peak=kq.peak,
-                                gpu_pauses=gpu_pause_log(reset=True))
+                                gpu_pauses=gpu_pause_log(reset=True), placement=place)
                 if args.stream_svc:
                     sv = svc_stats[leg]
                     out[leg]["served"] = {"tile_processes": cfg["tiles"], "tiles_gpu_open": st["tiles_gpu_open"],
@@ -764,7 +780,8 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
          "--stream-tput-min-batch", str(args.stream_tput_min_batch),
          "--stream-tput-small-max", str(args.stream_tput_small_max), "--stream-lat-hk-us", str(args.stream_lat_hk_us),
          "--stream-lat-small-max", str(args.stream_lat_small_max), "--stream-quad-sha", str(args.stream_quad_sha),
-         "--stream-lat-share", str(args.stream_lat_share), "--stream-svc", str(getattr(args, "stream_svc", 0))]
+         "--stream-lat-share", str(args.stream_lat_share), "--stream-svc", str(getattr(args, "stream_svc", 0)),
+         "--stream-place", args.stream_place]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -893,6 +910,10 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 "paced_producer_tile_same_l3": [((c.get("host_cpu") or {}).get("producer_tile") or {}).get("same_l3")
                                                 for c in curve],
                 "all_published": st.get("all_published"),
+                # where the max-rate leg's link memory was: the GPU's node, each producer's dcache part node, and the
+                # link's bytes in 2 MiB pages / in all in the tile process (shared memory has no THP on shmem_thp never)
+                "link_placement": {k: (st.get("max_rate") or {}).get("placement", {}).get(k)
+                                   for k in ("place", "gpu_node", "dcache_nodes", "huge_mb", "map_mb")},
                 "host_cpu_share_min": _r(st.get("host_cpu_share_min")),
                 # verdicts neither published nor overrun (none expected in these all-valid streams), and the
                 # first one with the GPU batch that produced it (leg, tile, ctx, seq, payload, code, path)
@@ -1178,6 +1199,9 @@ def parse_args(argv=None) -> argparse.Namespace:
                          "program, no GPU context each) served by one verify service process per GPU (fdgpu_vsvc_*), at "
                          "the --stream-rates offered loads per GPU; stream.served[T] holds the curve and knee (empty: skip)")
     ap.add_argument("--stream-svc", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--stream-place", choices=("gpu", "opposite", "none"), default="gpu",
+                    help="NUMA node of each producer's mcache, in dcache part and thread: its GPU's (default), the node "
+                         "opposite its GPU (the cross-socket arm), or unplaced (first touch by the link's creator)")
     ap.add_argument("--stream-only-paced", action="store_true",
                     help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",

@@ -20,6 +20,7 @@
 #include <dirent.h>
 #include <dlfcn.h>
 #include <spawn.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 #include <stdatomic.h>
 #include <stdint.h>
@@ -1650,6 +1651,8 @@ typedef struct {
   ulong         prod_cpu_ns[ LINK_PROD_MAX ], prod_wall_ns[ LINK_PROD_MAX ], prod_nivcsw[ LINK_PROD_MAX ];
   long          prod_cpu[ LINK_PROD_MAX ];     /* the CPU each producer was pinned to (-1: none) */
   struct { _Atomic ulong v; uchar pad[56]; } fseq[ LINK_PROD_MAX ][ LINK_TILE_MAX ];   /* per link: next seq each tile may lose */
+  ulong         part_off[ LINK_PROD_MAX + 1 ];   /* the in dcache in per-producer parts (2 MiB aligned), from its start */
+  int           dc_node[ LINK_PROD_MAX ], mc_node[ LINK_PROD_MAX ];   /* NUMA node each part / mcache's first page got */
 } link_hdr_t;
 
 struct fdgpu_link {
@@ -1700,6 +1703,109 @@ static void link_view( fdgpu_link_t * l ) {
 /* frags producer q of Q publishes: n / Q, the first n % Q producers one more */
 static ulong prod_frags( ulong n, ulong Q, ulong q ) { return n / Q + ( q < n % Q ? 1UL : 0UL ); }
 
+/* NUMA placement of the link's memory without libnuma: the mbind / get_mempolicy system calls (MPOL_BIND of a
+   range before its first touch; the node a touched page got) */
+#define LINK_MPOL_BIND   2
+#define LINK_MPOL_F_NODE (1<<0)
+#define LINK_MPOL_F_ADDR (1<<1)
+static void link_bind( void * p, ulong sz, int node ) {
+  if( node < 0 || node >= 1024 ) return;
+  ulong mask[ 16 ] = { 0 };
+  mask[ node / 64 ] = 1UL << ( node % 64 );
+  ulong lo = (ulong)p & ~4095UL, hi = ( (ulong)p + sz + 4095UL ) & ~4095UL;
+  (void)syscall( SYS_mbind, lo, hi - lo, LINK_MPOL_BIND, mask, 1025UL, 0U );   /* (refused: first touch decides) */
+}
+static int link_node_of( void const * p ) {
+  int node = -1;
+  if( syscall( SYS_get_mempolicy, &node, NULL, 0UL, p, LINK_MPOL_F_NODE | LINK_MPOL_F_ADDR ) ) return -1;
+  return node;
+}
+/* a CPU of node `node` this thread may run on (-1: none) */
+static int node_cpu( int node ) {
+  if( node < 0 ) return -1;
+  char path[ 96 ]; snprintf( path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node );
+  static __thread uchar set[ 1024 ];
+  memset( set, 0, sizeof(set) );
+  FILE * f = fopen( path, "r" );
+  if( !f ) return -1;
+  char buf[ 4096 ]; size_t n = fread( buf, 1, sizeof(buf)-1, f ); fclose( f ); buf[n] = 0;
+  cpu_set_t aff; CPU_ZERO( &aff );
+  if( sched_getaffinity( 0, sizeof(aff), &aff ) ) return -1;
+  char * c = buf;
+  while( *c ) {
+    char * e; long a = strtol( c, &e, 10 ), b = a;
+    if( e == c ) break;
+    if( *e == '-' ) { c = e + 1; b = strtol( c, &e, 10 ); }
+    for( long i=a; i<=b && i<1024; i++ ) if( i >= 0 && CPU_ISSET( (int)i, &aff ) ) return (int)i;
+    c = e; if( *c == ',' ) c++; else break;
+  }
+  return -1;
+}
+
+typedef struct {
+  fdgpu_link_t * l; int q, Q, node; ulong depth;
+  uchar const * payload; unsigned const * off; unsigned short const * sz; ulong n_payload;
+} link_fill_arg_t;
+
+static void * link_fill( void * _a ) {
+  link_fill_arg_t * a = (link_fill_arg_t *)_a;
+  fdgpu_link_t * l = a->l;
+  link_hdr_t * h = l->h;
+  ulong q = (ulong)a->q, Q = (ulong)a->Q;
+  uchar * part = l->dcache + h->part_off[q];
+  ulong part_sz = h->part_off[q+1] - h->part_off[q];
+  if( a->node >= 0 ) {
+    int cpu = node_cpu( a->node );
+    if( cpu >= 0 ) { cpu_set_t s1; CPU_ZERO( &s1 ); CPU_SET( cpu, &s1 ); (void)pthread_setaffinity_np( pthread_self(), sizeof(s1), &s1 ); }
+    link_bind( part, part_sz, a->node );
+    link_bind( l->line[q], mc_bytes( a->depth ), a->node );
+  }
+  mc_init_lines( l->line[q], a->depth, 0UL );
+  ulong c = h->part_off[q] / FDGPU_CHUNK_SZ;
+  for( ulong p=q; p<a->n_payload; p+=Q ) {
+    fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( l->dcache + c * FDGPU_CHUNK_SZ );
+    memset( txnm, 0, FDGPU_TXNM_HDR_SZ );
+    txnm->payload_sz = a->sz[p];
+    memcpy( (uchar *)txnm + FDGPU_TXNM_HDR_SZ, a->payload + a->off[p], a->sz[p] );
+    l->chunk[p] = (unsigned)c; l->psz[p] = a->sz[p];
+    l->psig[p] = a->sz[p] ? a->payload[ a->off[p] ] : (uchar)0;
+    c = fdgpu_dcache_compact_next( c, FDGPU_TXNM_HDR_SZ + a->sz[p], 0UL, ~0UL );
+  }
+  for( uchar * t = part + ( ( c * FDGPU_CHUNK_SZ - h->part_off[q] + 4095UL ) & ~4095UL ); t < part + part_sz; t += 4096 ) *t = 0;
+  h->dc_node[q] = link_node_of( part );
+  h->mc_node[q] = link_node_of( l->line[q] );
+  return NULL;
+}
+
+/* where the link's memory is: each producer's dcache part and mcache NUMA node (q < producers), and of the link
+   region as this process maps it, the bytes in 2 MiB pages (AnonHugePages / ShmemPmdMapped / FilePmdMapped of its
+   mapping in /proc/self/smaps) and its size; returns the producer count */
+int
+fdgpu_link_placement( fdgpu_link_t const * l, int * dc_node, int * mc_node, unsigned long * huge_bytes,
+                      unsigned long * map_bytes ) {
+  link_hdr_t const * h = l->h;
+  for( int q=0; q<h->cfg.producers; q++ ) { dc_node[q] = h->dc_node[q]; mc_node[q] = h->mc_node[q]; }
+  *huge_bytes = 0UL; *map_bytes = 0UL;
+  FILE * f = fopen( "/proc/self/smaps", "r" );
+  if( f ) {
+    char line[ 512 ]; int in = 0;
+    while( fgets( line, sizeof(line), f ) ) {
+      ulong a, b;
+      char * sp = strchr( line, ' ' ), * da = strchr( line, '-' );
+      if( sp && da && da < sp && sscanf( line, "%lx-%lx ", &a, &b ) == 2 ) {   /* a mapping's header: "start-end perms ..." */
+        in = (ulong)l->dcache >= a && (ulong)l->dcache < b;
+        if( in ) *map_bytes += b - a;
+        continue;
+      }
+      ulong kb;
+      if( in && ( sscanf( line, "AnonHugePages: %lu kB", &kb ) == 1 || sscanf( line, "ShmemPmdMapped: %lu kB", &kb ) == 1 ||
+                  sscanf( line, "FilePmdMapped: %lu kB", &kb ) == 1 ) ) *huge_bytes += kb << 10;
+    }
+    fclose( f );
+  }
+  return h->cfg.producers;
+}
+
 fdgpu_link_t *
 fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const * payload, unsigned const * off,
                 unsigned short const * sz, ulong n_payload, ulong mcache_depth ) {
@@ -1708,11 +1814,18 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
     return NULL;
   ulong Q = cfg->producers ? (ulong)cfg->producers : 1UL;
   ulong depth = pow2_up( mcache_depth );
-  ulong in_bytes = 0UL;
-  for( ulong p=0; p<n_payload; p++ ) {
-    if( sz[p] > 1232U ) return NULL;
-    in_bytes += ( ( FDGPU_TXNM_HDR_SZ + sz[p] + 127UL ) >> 7 ) << 7;
+  /* the in dcache in Q parts: producer q's payloads (p % Q == q: producer q's frag s is payload (s Q + q) %
+     n_payload) in part q, each part 2 MiB aligned, so that each can live on its producer's NUMA node as the
+     reference places each QUIC tile's out link in a workspace on that tile's node (src/disco/topo/fd_topob.c:
+     505-540, fd_topo.c:82) */
+  ulong part_off[ LINK_PROD_MAX + 1 ] = { 0 };
+  for( ulong p=0; p<n_payload; p++ ) if( sz[p] > 1232U ) return NULL;
+  for( ulong q=0; q<Q; q++ ) {
+    ulong b = 0UL;
+    for( ulong p=q; p<n_payload; p+=Q ) b += ( ( FDGPU_TXNM_HDR_SZ + sz[p] + 127UL ) >> 7 ) << 7;
+    part_off[q+1] = ( ( part_off[q] + b ) + ( 2UL << 20 ) - 1UL ) & ~( ( 2UL << 20 ) - 1UL );
   }
+  ulong in_bytes = part_off[Q];
   ulong T = (ulong)cfg->tiles;
   ulong o = al64( sizeof(link_hdr_t) );
   ulong off_mcache[ LINK_PROD_MAX ] = { 0 };
@@ -1724,7 +1837,7 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   ulong off_res    = o;  o = al64( o + T * sizeof(link_res_t) );
   ulong off_hist   = o;  o = al64( o + T * LH_N * sizeof(ulong) );
   ulong off_trace  = o;  o = al64( o + T * cfg->trace_cap * sizeof(fdgpu_link_trace_t) );
-  o = ( o + 4095UL ) & ~4095UL;
+  o = ( o + ( 2UL << 20 ) - 1UL ) & ~( ( 2UL << 20 ) - 1UL );   /* (the parts' 2 MiB alignment holds in the region) */
   ulong off_dcache = o;  o += in_bytes + 4096UL;
   ulong total = ( o + 4095UL ) & ~4095UL;
   uchar * base;
@@ -1766,19 +1879,20 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   for( ulong q=0; q<Q; q++ ) h->off_mcache[q] = off_mcache[q];
   h->off_dcache = off_dcache; h->off_chunk = off_chunk; h->off_sz = off_sz; h->off_psig = off_psig;
   h->off_res = off_res; h->off_hist = off_hist; h->off_trace = off_trace;
+  for( ulong q=0; q<=Q; q++ ) h->part_off[q] = part_off[q];
   link_view( l );
-  for( ulong q=0; q<Q; q++ ) mc_init_lines( l->line[q], depth, 0UL );
   memset( (void *)l->res, 0, T * sizeof(link_res_t) );
   memset( (void *)l->hist, 0, T * LH_N * sizeof(ulong) );
-  for( ulong p=0, c=0; p<n_payload; p++ ) {
-    fdgpu_txnm_t * txnm = (fdgpu_txnm_t *)( l->dcache + c * FDGPU_CHUNK_SZ );
-    memset( txnm, 0, FDGPU_TXNM_HDR_SZ );
-    txnm->payload_sz = sz[p];
-    memcpy( (uchar *)txnm + FDGPU_TXNM_HDR_SZ, payload + off[p], sz[p] );
-    l->chunk[p] = (unsigned)c; l->psz[p] = sz[p];
-    l->psig[p] = sz[p] ? payload[ off[p] ] : (uchar)0;
-    c = fdgpu_dcache_compact_next( c, FDGPU_TXNM_HDR_SZ + sz[p], 0UL, ~0UL );
+  /* each producer's mcache and dcache part first touched by a thread on its node (cfg.prod_node; the memory
+     policy bound there too where the kernel allows it), its payloads prefilled (what QUIC reassembly leaves) */
+  link_fill_arg_t fa[ LINK_PROD_MAX ];
+  pthread_t fth[ LINK_PROD_MAX ];
+  for( ulong q=0; q<Q; q++ ) {
+    fa[q].l = l; fa[q].q = (int)q; fa[q].Q = (int)Q; fa[q].node = cfg->prod_node[q] - 1; fa[q].depth = depth;
+    fa[q].payload = payload; fa[q].off = off; fa[q].sz = sz; fa[q].n_payload = n_payload;
+    if( pthread_create( &fth[q], NULL, link_fill, &fa[q] ) ) link_fill( &fa[q] ), fth[q] = 0;
   }
+  for( ulong q=0; q<Q; q++ ) if( fth[q] ) pthread_join( fth[q], NULL );
   atomic_store_explicit( &h->joined, 1UL, memory_order_relaxed );
   atomic_store_explicit( &h->magic, LINK_MAGIC, memory_order_release );
   return l;
@@ -2172,6 +2286,26 @@ link_pick_cpus( int device, int proc, int n, int n_pair, int * out, int gpu_call
     }
   return got;
 }
+/* producers placed on a node other than the GPU's (cfg.prod_node: e.g. the cross-socket arm) run on that node:
+   cpus[i] of producer i becomes an allowed CPU of that node (one hardware thread per core) not otherwise taken */
+static void link_place_producers( fdgpu_stream_cfg_t const * c, int const * myq, int np, int * cpus, int ncpu, int gpu_node ) {
+  for( int i=0; i<np && i<ncpu; i++ ) {
+    int node = c->prod_node[ myq[i] ] - 1;
+    if( node < 0 || node == gpu_node ) continue;
+    char path[ 96 ]; snprintf( path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node );
+    uchar set[ LINK_CPU_MAX ]; memset( set, 0, sizeof(set) );
+    if( cpulist_read( path, set ) ) continue;
+    cpu_set_t aff; CPU_ZERO( &aff );
+    if( sched_getaffinity( 0, sizeof(aff), &aff ) ) continue;
+    for( int k=0; k<LINK_CPU_MAX && k<CPU_SETSIZE; k++ ) {
+      if( !set[k] || !CPU_ISSET( k, &aff ) ) continue;
+      if( cpu_first_of( "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", k ) != k ) continue;
+      int used = 0; for( int j=0; j<ncpu; j++ ) used |= cpus[j] == k;
+      if( !used ) { cpus[i] = k; break; }
+    }
+  }
+}
+
 static void link_pin( int cpu ) {
   if( cpu < 0 ) return;
   cpu_set_t s; CPU_ZERO( &s ); CPU_SET( cpu, &s );
@@ -2512,6 +2646,7 @@ fdgpu_link_run( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   int H = c->zero_copy && c->copy_threads > 0 ? ( c->copy_threads < FDGPU_VTILE_COPY_THREADS_MAX ? c->copy_threads
                                                                                                   : FDGPU_VTILE_COPY_THREADS_MAX ) : 0;
   int ncpu = link_pick_cpus( device, proc, nt + np + nl + nt*H, np + nt, cpus, 1 );   /* ... and their copy threads, after those */
+  link_place_producers( c, myq, np, cpus, ncpu, fdgpu_device_numa_node( device ) );
   if( getenv( "FDGPU_LINK_VERBOSE" ) ) {
     fprintf( stderr, "fdgpu_link: proc %d device %d numa %d producers %d tiles %d cpus:", proc, device,
              fdgpu_device_numa_node( device ), np, nt );
@@ -2583,6 +2718,7 @@ link_run_svc( fdgpu_link_t * l, int proc, int device, int run_producer ) {
   /* CPUs: producers, tiles, the service, its launch thread, the tiles' copy threads */
   int cpus[ ( 2 + FDGPU_VTILE_COPY_THREADS_MAX )*LINK_TILE_MAX + LINK_PROD_MAX + 2 ];
   int ncpu = link_pick_cpus( device, proc, np + nt + 1 + nl + nt*H, np + nt, cpus, 1 );
+  link_place_producers( c, myq, np, cpus, ncpu, fdgpu_device_numa_node( device ) );
   int svc_cpu = np + nt < ncpu ? cpus[ np + nt ] : -1, lcpu = nl && np + nt + 1 < ncpu ? cpus[ np + nt + 1 ] : -1;
   if( getenv( "FDGPU_LINK_VERBOSE" ) ) {
     fprintf( stderr, "fdgpu_link: served: proc %d device %d producers %d tiles %d service cpu %d cpus:", proc, device, np, nt, svc_cpu );

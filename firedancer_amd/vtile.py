@@ -39,7 +39,7 @@ EXPORTS = ("fdgpu_dedup_tag", "fdgpu_xxh64", "fdgpu_link_set_trace", "fdgpu_link
            "fdgpu_vsvc_start", "fdgpu_vsvc_ready", "fdgpu_vsvc_poll", "fdgpu_vsvc_run", "fdgpu_vsvc_stop",
            "fdgpu_vsvc_pending", "fdgpu_vsvc_stats", "fdgpu_vsvc_delete", "fdgpu_vtile_new_svc",
            "fdgpu_vtile_set_svc_region", "fdgpu_gpu_numa_node_sysfs", "fdgpu_link_svc_stats", "fdgpu_link_run_tile",
-           "fdgpu_vtile_debug_fail_launch", "fdgpu_vsvc_debug_serve")
+           "fdgpu_vtile_debug_fail_launch", "fdgpu_vsvc_debug_serve", "fdgpu_link_placement")
 
 TXNM_DTYPE = np.dtype([("reference_slot", "<u8"), ("payload_sz", "<u2"), ("txn_t_sz", "<u2"), ("source_ipv4", "<u4"),
                        ("source_tpu", "u1"), ("_pad0", "u1", (7,)), ("bundle_id", "<u8"), ("bundle_txn_cnt", "<u8"),
@@ -95,7 +95,7 @@ class StreamCfg(ctypes.Structure):
                 ("cu_exclusive", ctypes.c_int), ("no_huge_pages", ctypes.c_int), ("launcher", ctypes.c_int),
                 ("copy_threads", ctypes.c_int), ("min_batch", ctypes.c_ulong), ("small_max", ctypes.c_ulong),
                 ("hk_ns", ctypes.c_ulong), ("lat_share", ctypes.c_int), ("svc", ctypes.c_int),
-                ("trace_cap", ctypes.c_ulong)]
+                ("trace_cap", ctypes.c_ulong), ("prod_node", ctypes.c_int * 16)]
 
 
 class VsvcCfg(ctypes.Structure):
@@ -265,6 +265,8 @@ def load():
         L.fdgpu_vtile_debug_fail_launch.argtypes = [vp, ctypes.c_int]
         L.fdgpu_gpu_numa_node_sysfs.argtypes = [ctypes.c_char_p, ctypes.c_int]
         L.fdgpu_link_svc_stats.argtypes = [vp, ctypes.POINTER(VsvcStats), ctypes.POINTER(ctypes.c_int)]
+        L.fdgpu_link_placement.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                                           ctypes.POINTER(ctypes.c_ulong), ctypes.POINTER(ctypes.c_ulong)]
         _lib = L
     return _lib
 
@@ -539,8 +541,11 @@ def tiles_of(tiles: int, gpus: int, proc: int) -> list[int]:
 
 def _cfg(n_frags, tiles, gpus, batch_txn, max_inflight, rate_fps, zero_copy, reliable, producers=1, nctx=0, prof=0,
          out_mult=0, copy_wait_ns=0, copy_min=0, gather_cus=0, max_uncopied=0, pf_dist=0, no_huge_pages=0, cu_split=0, cu_exclusive=0,
-         launcher=0, copy_threads=0, min_batch=0, small_max=0, hk_ns=0, lat_share=0, svc=0, trace_cap=0) -> StreamCfg:
-    return StreamCfg(n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
+         launcher=0, copy_threads=0, min_batch=0, small_max=0, hk_ns=0, lat_share=0, svc=0, trace_cap=0,
+         prod_node=None) -> StreamCfg:
+    """prod_node: per producer q, the NUMA node of its mcache, dcache part and thread (None / -1: unplaced)."""
+    pn = (ctypes.c_int * 16)(*[(n + 1 if n is not None and n >= 0 else 0) for n in list(prod_node or [])[:16]])
+    return StreamCfg(prod_node=pn, n_frags=n_frags, batch_txn=batch_txn, max_inflight=max_inflight, rate_fps=rate_fps, tiles=tiles,
                      gpus=gpus, zero_copy=1 if zero_copy else 0, reliable=1 if reliable else 0, producers=producers,
                      nctx=nctx, prof=prof, out_mult=out_mult, copy_wait_ns=copy_wait_ns, copy_min=copy_min,
                      gather_cus=gather_cus, max_uncopied=max_uncopied, pf_dist=pf_dist, no_huge_pages=no_huge_pages, cu_split=cu_split,
@@ -590,7 +595,7 @@ class Link:
     def cfg(self) -> dict:
         c = StreamCfg()
         self.L.fdgpu_link_cfg(self.p, ctypes.byref(c))
-        return {k: getattr(c, k) for k, _ in c._fields_}
+        return {k: (list(getattr(c, k)) if k == "prod_node" else getattr(c, k)) for k, _ in c._fields_}
 
     def joined(self) -> int:
         return int(self.L.fdgpu_link_joined(self.p))
@@ -619,6 +624,15 @@ class Link:
         out = np.zeros(8, ANOM_DTYPE)
         n = int(self.L.fdgpu_link_anomalies(self.p, tile, out.ctypes.data, 8))
         return n, [{k: int(e[k]) for k in ANOM_DTYPE.names} for e in out[:min(n, 8)]]
+
+    def placement(self) -> dict:
+        """fdgpu_link_placement: per producer the NUMA node of its dcache part / mcache, and the link's bytes in
+        2 MiB pages in this process's mapping."""
+        dc, mc = (ctypes.c_int * 16)(), (ctypes.c_int * 16)()
+        hb, mb = ctypes.c_ulong(0), ctypes.c_ulong(0)
+        n = self.L.fdgpu_link_placement(self.p, dc, mc, ctypes.byref(hb), ctypes.byref(mb))
+        return {"dcache_nodes": list(dc[:n]), "mcache_nodes": list(mc[:n]), "huge_mb": round(hb.value / 2**20, 1),
+                "map_mb": round(mb.value / 2**20, 1)}
 
     def svc_stats(self) -> dict:
         """Served tiles (cfg svc): this process's verify service after run (fdgpu_link_svc_stats)."""

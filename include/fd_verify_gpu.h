@@ -534,6 +534,9 @@ typedef struct fdgpu_stream_cfg {
                                     engine contexts.  Needs a shared link (a path): the tile processes join it */
   unsigned long trace_cap;       /* > 0: every tile records up to this many verdicts in the link itself (fdgpu_link_trace,
                                     from any process; served tiles need it), instead of fdgpu_link_set_trace's arrays */
+  int           prod_node[ 16 ]; /* 1 + the NUMA node producer q's mcache and in dcache part live on, and its thread runs
+                                    on (0: the link's creator decides, and the producer runs by the tiles) -- the
+                                    reference gives every workspace a node (src/disco/topo/fd_topob.c:505-540) */
 } fdgpu_stream_cfg_t;
 
 typedef struct fdgpu_stream_stats {
@@ -633,6 +636,10 @@ unsigned long   fdgpu_link_anomalies( fdgpu_link_t const * link, int tile, fdgpu
 /* served tiles (cfg.svc): this process's verify service after fdgpu_link_run -- its metrics and the CPU its
    loop ran on */
 int             fdgpu_link_svc_stats( fdgpu_link_t const * link, fdgpu_vsvc_stats_t * out, int * svc_cpu );
+/* where the link's memory is: per producer q (returns the count) the NUMA node its in dcache part and its mcache
+   got (-1 unknown), and of the link region as this process maps it the bytes in 2 MiB pages and in all */
+int             fdgpu_link_placement( fdgpu_link_t const * link, int * dc_node, int * mc_node, unsigned long * huge_bytes,
+                                      unsigned long * map_bytes );
 /* served tiles: the tile program's body (fdgpu_tile <link> <service segment> <tile> <cpu> [copy cpus]): runs
    tile `tile` of the shared link in this process, served by the service segment at svc_path, with no GPU
    call; pinned to cpu (-1: not pinned).  0, or < 0 (the link's failure code, -10 - code). */
