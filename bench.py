@@ -554,9 +554,14 @@ def page_config() -> dict:
         except OSError:
             return None
     sel = lambda v: (v.split("[")[1].split("]")[0] if v and "[" in v else v)
+    mounts = []
+    try:
+        mounts = [l.split()[1] for l in open("/proc/mounts") if l.split()[2:3] == ["hugetlbfs"]]
+    except OSError:
+        pass
     return {"thp": sel(rd("/sys/kernel/mm/transparent_hugepage/enabled")),
             "shmem_thp": sel(rd("/sys/kernel/mm/transparent_hugepage/shmem_enabled")),
-            "hugetlb_pages": rd("/proc/sys/vm/nr_hugepages")}
+            "hugetlb_pages": rd("/proc/sys/vm/nr_hugepages"), "hugetlbfs_mounts": mounts}
 
 
 def _kfd_gpu_ids() -> set[str]:

@@ -1,20 +1,30 @@
 #!/bin/bash
-# The GPU verify tile under seccomp (tools/sandbox/vtile_sandbox.c): discover the syscalls a tile makes after
-# its privileged init, then enforce exactly the policy in firedancer_amd/fd_verify_gpu_tile.seccomppolicy.
-# usage: gpurun --timeout 300 -- 'bash tools/gpu_sandbox.sh'
+# The verify tile under seccomp (tools/sandbox/vtile_sandbox.c), round 6: the tile with its own GPU context at the
+# bench's paced defaults (two contexts, exclusive CUs within their shares, 16 copy CUs), without and with its launch
+# thread -- discover the syscalls it makes after privileged init, then enforce exactly
+# firedancer_amd/fd_verify_gpu_tile.seccomppolicy -- and the served form: a tile process without a GPU context
+# enforced under the reference verify tile's own policy (write, fsync: src/disco/verify/fd_verify_tile.seccomppolicy)
+# beside its verify service (discovered, then enforced under firedancer_amd/fd_verify_service.seccomppolicy).
+# usage: gpurun --timeout 400 -- 'bash tools/gpu_sandbox.sh [outdir]'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-d=gpurun_out/sandbox
+d=${1:-gpurun_out/sandbox}
 mkdir -p $d
-# the syscall names of the policy file: lines "name" or "name: (...)" outside comments
-allow=$(python3 -c "
-import re
+names() { python3 -c "
+import re,sys
 names=[]
-for l in open('firedancer_amd/fd_verify_gpu_tile.seccomppolicy'):
+for l in open(sys.argv[1]):
     m=re.match(r'^([a-z_0-9]+)\s*(:|$)', l)
     if m and not l.startswith('unsigned'): names.append(m.group(1))
-print(' '.join(names))")
-echo "policy: $allow" > $d/policy_names.txt
+print(' '.join(names))" "$1"; }
+tile=$(names firedancer_amd/fd_verify_gpu_tile.seccomppolicy)
+svc=$(names firedancer_amd/fd_verify_service.seccomppolicy)
+echo "tile policy: $tile / service policy: $svc" > $d/policy_names.txt
+S=tools/sandbox/vtile_sandbox
 bash "$(dirname "$0")/gpu_job.sh" \
-  "discover:120:tools/sandbox/vtile_sandbox discover > $d/discover.json" \
-  "enforce:120:tools/sandbox/vtile_sandbox enforce $allow > $d/enforce.json"
-cat $d/discover.json $d/enforce.json
+  "discover:120:$S discover > $d/discover.json" \
+  "enforce:120:$S enforce $tile > $d/enforce.json" \
+  "discover_launcher:120:$S discover --launcher > $d/discover_launcher.json" \
+  "enforce_launcher:120:$S enforce --launcher $tile > $d/enforce_launcher.json" \
+  "served_discover:120:$S served discover --launcher > $d/served_discover.json" \
+  "served_enforce:120:$S served enforce --launcher write fsync -- $svc > $d/served_enforce.json"
+cat $d/*.json

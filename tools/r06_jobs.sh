@@ -38,6 +38,21 @@ case "$job" in
       "own2:400:bash tools/rehearse_n2.sh --stream-only-paced --stream-rates 1e6,2.5e6,3.75e6,5e6,7.5e6 --no-cpu-baseline --detail-out $d/own2.json > $d/own2.line" \
       "a2:400:$A --detail-out $d/a2.json > $d/a2.line"
     ;;
+  m1)
+    # the sandbox measurements, then the paced comparison (job cmp)
+    bash tools/gpu_sandbox.sh gpurun_out/r06_sandbox && bash tools/r06_jobs.sh cmp
+    ;;
+  place)
+    # the link's NUMA placement: producer + its mcache and dcache part on the GPU's node vs on the other node
+    # (the cross-socket arm), interleaved: max rate, intake ns/frag, gather GB/s, paced p99 at 10M
+    d=gpurun_out/r06_place; mkdir -p $d
+    P="python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-rates 10e6 --stream-seconds 5 --stream-unrel-seconds 1"
+    bash tools/gpu_job.sh \
+      "g1:300:$P --stream-place gpu --detail-out $d/g1.json > $d/g1.line" \
+      "o1:300:$P --stream-place opposite --detail-out $d/o1.json > $d/o1.line" \
+      "g2:300:$P --stream-place gpu --detail-out $d/g2.json > $d/g2.line" \
+      "o2:300:$P --stream-place opposite --detail-out $d/o2.json > $d/o2.line"
+    ;;
   svcdbg)
     bash tools/gpu_job.sh \
       "tests:300:$T -x tests/test_gpu_vsvc.py -k 'in_process or launch_thread'"

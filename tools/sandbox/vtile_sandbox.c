@@ -28,8 +28,24 @@
              DRM render node, found before the filter goes on); anything
              else traps, and the handler names the syscall and exits 3.
 
-   usage: vtile_sandbox discover|enforce [syscall ...]   (enforce: the
-          allowed syscall names, e.g. from the policy file)
+   usage: vtile_sandbox discover|enforce [--launcher] [syscall ...]
+          (enforce: the allowed syscall names, e.g. from the policy file)
+   The tile runs with the bench's paced-tile defaults: two engine contexts,
+   latency-path workgroups alone on their CUs (cu_exclusive) within each
+   context's CU share (lat_share), 16 CUs reserved for the copies;
+   --launcher adds its launch thread (fdgpu_vtile_opts_t.launcher).  The
+   filter covers every thread (TSYNC): the HIP runtime's, the launch thread.
+
+   Served form (include/fd_verify_gpu.h, fdgpu_vsvc_*): the verify tile is a
+   process with no GPU context, its GPU's verify service another process.
+     vtile_sandbox served discover|enforce [--launcher] [tile syscall ...] -- [service syscall ...]
+   forks the tile process before the service touches the GPU (the two share
+   the in link and the service segment), runs the warm-up batch unfiltered,
+   then puts the tile under its filter (discover, or enforce of the names
+   before "--") and the service under its own (discover when no names follow
+   "--", else enforce of them) and runs the second batch.  Prints one JSON
+   line per process (role "tile" / "service").
+
    Prints one JSON line.  Needs libfdgpu_vtile.so, libfdgpu_ed25519.so
    and libfdsynth.so (LD_LIBRARY_PATH=firedancer_amd). */
 
@@ -45,6 +61,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdatomic.h>
+#include <sys/mman.h>
 #include <sys/prctl.h>
 #include <sys/syscall.h>
 #include <time.h>
@@ -198,7 +216,7 @@ driver_fds( int * fds, int max ) {
   if( !d ) return 0;
   struct dirent * e;
   while( ( e = readdir( d ) ) && n < max ) {
-    char p[ 64 ], t[ 256 ];
+    char p[ 320 ], t[ 256 ];
     snprintf( p, sizeof(p), "/proc/self/fd/%s", e->d_name );
     ssize_t k = readlink( p, t, sizeof(t) - 1 );
     if( k <= 0 ) continue;
@@ -246,13 +264,154 @@ run_batch( fdgpu_vtile_t * vt, fdgpu_mcache_t * mc, uchar * dcache, uchar const 
   return 0;
 }
 
+/* the JSON report of a run under the filter (stdout writes are syscalls too: counted after the snapshot) */
+static void
+report( char const * role, char const * mode, int rc, ulong frags, ulong published, ulong dt, int n_fds, char const * extra ) {
+  unsigned long snap[ MAX_NR ];
+  for( int i=0; i<MAX_NR; i++ ) snap[i] = g_count[i];
+  char buf[ 8192 ]; int n = 0;
+  n += snprintf( buf + n, sizeof(buf) - n, "{\"role\": \"%s\", \"mode\": \"%s\", \"rc\": %d, \"frags\": %lu, \"published\": %lu, "
+                 "\"batch_ms\": %.3f, \"driver_fds\": %d, \"filter_instructions\": %d, %s\"syscalls_after_init\": {",
+                 role, mode, rc, frags, published, (double)dt * 1e-6, n_fds, g_nins, extra );
+  int first = 1;
+  for( int i=0; i<MAX_NR; i++ ) if( snap[i] ) {
+    n += snprintf( buf + n, sizeof(buf) - n, "%s\"%s\": %lu", first ? "" : ", ", g_name[i][0] ? g_name[i] : "?", snap[i] );
+    first = 0;
+  }
+  n += snprintf( buf + n, sizeof(buf) - n, "}}\n" );
+  fdsb_tramp( SYS_write, 1, (long)buf, (long)n, 0, 0, 0 );   /* (the harness's own output: not counted, not filtered) */
+}
+
+static int
+names_to_nrs( char ** names, int n, int * allow, int * ioctl_ok ) {
+  int k = 0;
+  for( int i=0; i<n; i++ ) {
+    if( !strcmp( names[i], "ioctl" ) ) { *ioctl_ok = 1; continue; }
+    int nr = nr_of( names[i] );
+    if( nr < 0 ) { printf( "{\"error\": \"unknown syscall %s\"}\n", names[i] ); return -1; }
+    allow[ k++ ] = nr;
+  }
+  return k;
+}
+
+static int
+base_set( int * allow ) {               /* discover: what the handler itself and the process teardown need */
+  char const * base[] = { "rt_sigreturn", "exit", "exit_group" };
+  int k = 0;
+  for( unsigned i=0; i<sizeof(base)/sizeof(base[0]); i++ ) { int nr = nr_of( base[i] ); if( nr >= 0 ) allow[ k++ ] = nr; }
+  return k;
+}
+
+/* ---- the served form: a tile process without a GPU context, its verify service ---- */
+
+typedef struct { _Atomic int phase; _Atomic int tile_rc; } served_ctl_t;   /* phase: 1 warm-up done, 2 tile done */
+
+static int
+served_main( int argc, char ** argv, int launcher ) {
+  int i = 2;
+  int tile_discover = !strcmp( argv[i++], "discover" );
+  while( i < argc && !strncmp( argv[i], "--", 2 ) && argv[i][2] ) i++;       /* (options, parsed by main) */
+  char ** tnames = argv + i; int ntn = 0;
+  while( i < argc && strcmp( argv[i], "--" ) ) { i++; ntn++; }
+  char ** snames = NULL; int nsn = 0;
+  if( i < argc ) { snames = argv + i + 1; nsn = argc - i - 1; }
+  int svc_discover = nsn == 0;
+
+  /* privileged init, before anything touches the GPU: the payloads, the in link (mcache lines + in dcache in
+     shared memory: the tile process is the producer and the tile, the service's GPU reads the records) */
+  static fdsynth_key_t keys[ 64 ];
+  fdsynth_keys( keys, 64, 77 );
+  uchar * payload = (uchar *)malloc( 2*N_FRAG*1232UL + 1024UL );
+  fdgpu_txn_desc_t * desc = (fdgpu_txn_desc_t *)calloc( 2*N_FRAG, sizeof(fdgpu_txn_desc_t) );
+  int8_t * expect = (int8_t *)calloc( 2*N_FRAG, 1 );
+  fdsynth_txns( payload, 1232UL, desc, expect, 2*N_FRAG, 0, 1, 0.0, 4242UL, keys, 64, 4 );
+  ulong depth = 4UL*N_FRAG, dsz = 2UL*N_FRAG*REC_SZ, lsz = ( depth * 32UL + 4095UL ) & ~4095UL;
+  uchar * dc = (uchar *)mmap( NULL, dsz, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0 );
+  void * lines = mmap( NULL, lsz, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0 );
+  served_ctl_t * ctl = (served_ctl_t *)mmap( NULL, 4096, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0 );
+  if( dc == MAP_FAILED || lines == MAP_FAILED || ctl == MAP_FAILED ) { printf( "{\"error\": \"mmap\"}\n" ); return 1; }
+  fdgpu_mcache_t * tmp = fdgpu_mcache_new( depth, 0UL );           /* lines initialised "one lap behind" */
+  memcpy( lines, fdgpu_mcache_lines( tmp ), depth * 32UL );
+  fdgpu_mcache_delete( tmp );
+  fdgpu_vsvc_cfg_t cfg; memset( &cfg, 0, sizeof(cfg) );
+  cfg.clients = 1; cfg.out_dcache_bytes = 8UL*N_FRAG*REC_SZ; cfg.batch_txn = N_FRAG; cfg.max_inflight = 1; cfg.nctx = 2;
+  cfg.gather_cus = 16; cfg.launcher = launcher;
+  fdgpu_vsvc_t * svc = fdgpu_vsvc_new( NULL, &cfg );
+  if( !svc || fdgpu_vsvc_add_region( svc, 0, dc, dsz ) || fdgpu_vsvc_add_region( svc, 1, lines, lsz ) ) {
+    printf( "{\"error\": \"service segment\"}\n" ); return 1;
+  }
+  fflush( stdout ); fflush( stderr );
+  pid_t pid = fork();
+  if( pid < 0 ) { printf( "{\"error\": \"fork\"}\n" ); return 1; }
+  if( pid == 0 ) {                                        /* ---- the tile process: no GPU call ---- */
+    fdgpu_mcache_t * mc = fdgpu_mcache_wrap( lines, depth );
+    fdgpu_vtile_opts_t opt; memset( &opt, 0, sizeof(opt) );
+    fdgpu_vtile_t * vt = fdgpu_vtile_new_svc( svc, 0, 1UL << 16, 99UL, &opt );
+    if( !mc || !vt || fdgpu_vtile_set_svc_region( vt, 0, dc, dsz ) || fdgpu_vtile_set_svc_region( vt, 1, lines, lsz ) ||
+        fdgpu_vtile_set_in_link( vt, mc ) ) { printf( "{\"role\": \"tile\", \"error\": \"init\"}\n" ); _exit( 1 ); }
+    ulong pub0 = 0UL, pub1 = 0UL;
+    int rc = run_batch( vt, mc, dc, payload, desc, 0UL, &pub0 );       /* (waits for the service's verdicts) */
+    if( rc || pub0 != N_FRAG ) { printf( "{\"role\": \"tile\", \"error\": \"warm-up rc %d published %lu\"}\n", rc, pub0 ); _exit( 1 ); }
+    int fds[ 16 ]; int n_fds = driver_fds( fds, 16 );                  /* (none: no GPU context here) */
+    int allow[ MAX_NR ], n_allow = 0, ioctl_ok = 0;
+    n_allow = tile_discover ? base_set( allow ) : names_to_nrs( tnames, ntn, allow, &ioctl_ok );
+    if( n_allow < 0 ) _exit( 1 );
+    struct sigaction sa; memset( &sa, 0, sizeof(sa) );
+    sa.sa_sigaction = on_sigsys; sa.sa_flags = SA_SIGINFO;
+    sigaction( SIGSYS, &sa, NULL );
+    g_enforce = !tile_discover;
+    fflush( stdout );
+    atomic_store( &ctl->phase, 1 );                                      /* the service may go under its filter */
+    while( atomic_load( &ctl->phase ) < 2 ) ;                             /* ... and has */
+    if( ( rc = install( allow, n_allow, ioctl_ok, fds, n_fds ) ) ) { printf( "{\"role\": \"tile\", \"error\": \"seccomp %d\"}\n", rc ); _exit( 1 ); }
+    ulong t0 = now_ns();
+    rc = run_batch( vt, mc, dc, payload, desc + N_FRAG, N_FRAG, &pub1 );
+    ulong dt = now_ns() - t0;
+    report( "tile", tile_discover ? "discover" : "enforce", rc, N_FRAG, pub1, dt, n_fds, "\"gpu_open\": 0, " );
+    atomic_store( &ctl->tile_rc, rc || pub1 != N_FRAG ? 1 : 0 );
+    atomic_store( &ctl->phase, 3 );
+    fdsb_tramp( SYS_exit_group, 0, 0, 0, 0, 0, 0 );           /* (the harness's exit: the tile itself never exits) */
+  }
+  /* ---- the verify service: the GPU ---- */
+  if( fdgpu_vsvc_start( svc, 0 ) ) { printf( "{\"role\": \"service\", \"error\": \"start: %s\"}\n", fdgpu_last_error() ); return 1; }
+  while( atomic_load( &ctl->phase ) < 1 ) fdgpu_vsvc_poll( svc );        /* the warm-up batch */
+  int fds[ 16 ]; int n_fds = driver_fds( fds, 16 );
+  int allow[ MAX_NR ], n_allow = 0, ioctl_ok = 0;
+  n_allow = svc_discover ? base_set( allow ) : names_to_nrs( snames, nsn, allow, &ioctl_ok );
+  if( n_allow < 0 ) return 1;
+  struct sigaction sa; memset( &sa, 0, sizeof(sa) );
+  sa.sa_sigaction = on_sigsys; sa.sa_flags = SA_SIGINFO;
+  sigaction( SIGSYS, &sa, NULL );
+  g_enforce = !svc_discover;
+  fflush( stdout ); fflush( stderr );
+  int rc = install( allow, n_allow, ioctl_ok, fds, n_fds );
+  if( rc ) { printf( "{\"role\": \"service\", \"error\": \"seccomp %d\"}\n", rc ); return 1; }
+  atomic_store( &ctl->phase, 2 );
+  ulong t0 = now_ns();
+  while( atomic_load( &ctl->phase ) < 3 && now_ns() - t0 < 30000000000UL ) fdgpu_vsvc_poll( svc );
+  ulong dt = now_ns() - t0;
+  fdgpu_vsvc_stats_t st; fdgpu_vsvc_stats( svc, &st );
+  char extra[ 160 ];
+  snprintf( extra, sizeof(extra), "\"launcher\": %d, \"completed\": %lu, \"batches\": %lu, ", launcher, st.completed, st.gm.batches );
+  report( "service", svc_discover ? "discover" : "enforce", atomic_load( &ctl->phase ) < 3 ? -12 : atomic_load( &ctl->tile_rc ),
+          st.completed, st.completed, dt, n_fds, extra );
+  fdsb_tramp( SYS_exit_group, atomic_load( &ctl->phase ) < 3 || atomic_load( &ctl->tile_rc ) ? 1 : 0, 0, 0, 0, 0, 0 );
+  return 0;
+}
+
 int
 main( int argc, char ** argv ) {
+  int launcher = 0;
+  for( int i=1; i<argc; i++ ) if( !strcmp( argv[i], "--launcher" ) ) launcher = 1;
+  load_names();
+  if( argc >= 3 && !strcmp( argv[1], "served" ) && ( !strcmp( argv[2], "discover" ) || !strcmp( argv[2], "enforce" ) ) )
+    return served_main( argc, argv, launcher );
   if( argc < 2 || ( strcmp( argv[1], "discover" ) && strcmp( argv[1], "enforce" ) ) ) {
-    fprintf( stderr, "usage: %s discover|enforce [syscall ...]\n", argv[0] ); return 2;
+    fprintf( stderr, "usage: %s discover|enforce [--launcher] [syscall ...]\n"
+                     "       %s served discover|enforce [--launcher] [tile syscall ...] -- [service syscall ...]\n", argv[0], argv[0] );
+    return 2;
   }
   int discover = !strcmp( argv[1], "discover" );
-  load_names();
 
   /* ---- privileged init ---- */
   static fdsynth_key_t keys[ 64 ];
@@ -263,7 +422,9 @@ main( int argc, char ** argv ) {
   fdsynth_txns( payload, 1232UL, desc, expect, 2*N_FRAG, 0 /* LARGE_NOOP */, 1, 0.0, 4242UL, keys, 64, 4 );
   fdgpu_mcache_t * mc = fdgpu_mcache_new( 4UL*N_FRAG, 0UL );
   uchar * dcache = (uchar *)fdgpu_host_alloc( 2UL*N_FRAG*REC_SZ );
-  fdgpu_vtile_opts_t opt; memset( &opt, 0, sizeof(opt) ); opt.nctx = 1;
+  /* the bench's paced tile: two contexts, exclusive latency-path workgroups within each context's CU share (the
+     defaults), 16 CUs for the copies, and (--launcher) its launch thread */
+  fdgpu_vtile_opts_t opt; memset( &opt, 0, sizeof(opt) ); opt.nctx = 2; opt.gather_cus = 16; opt.launcher = launcher;
   fdgpu_vtile_t * vt = fdgpu_vtile_new_opts( 0, N_FRAG, 1UL << 16, 99UL, 8UL*N_FRAG*REC_SZ, 0, &opt );
   if( !mc || !dcache || !vt || fdgpu_vtile_set_in_link( vt, mc ) ) {
     printf( "{\"error\": \"init: %s\"}\n", fdgpu_last_error() ); return 1;
@@ -280,6 +441,7 @@ main( int argc, char ** argv ) {
     for( unsigned i=0; i<sizeof(base)/sizeof(base[0]); i++ ) { int nr = nr_of( base[i] ); if( nr >= 0 ) allow[ n_allow++ ] = nr; }
   } else {
     for( int i=2; i<argc; i++ ) {
+      if( !strcmp( argv[i], "--launcher" ) ) continue;
       if( !strcmp( argv[i], "ioctl" ) ) { ioctl_ok = 1; continue; }
       int nr = nr_of( argv[i] );
       if( nr < 0 ) { printf( "{\"error\": \"unknown syscall %s\"}\n", argv[i] ); return 1; }
@@ -301,21 +463,10 @@ main( int argc, char ** argv ) {
   rc = run_batch( vt, mc, dcache, payload, desc + N_FRAG, N_FRAG, &pub1 );
   ulong dt = now_ns() - t0;
 
-  /* report (stdout writes are syscalls too: in discover mode they are counted after the snapshot) */
-  unsigned long snap[ MAX_NR ];
-  for( int i=0; i<MAX_NR; i++ ) snap[i] = g_count[i];
-  char buf[ 8192 ]; int n = 0;
-  n += snprintf( buf + n, sizeof(buf) - n, "{\"mode\": \"%s\", \"rc\": %d, \"frags\": %lu, \"published\": %lu, "
-                 "\"batch_ms\": %.3f, \"driver_fds\": %d, \"filter_instructions\": %d, \"syscalls_after_init\": {",
-                 argv[1], rc, N_FRAG, pub1, (double)dt * 1e-6, n_fds, g_nins );
-  int first = 1;
-  for( int i=0; i<MAX_NR; i++ ) if( snap[i] ) {
-    n += snprintf( buf + n, sizeof(buf) - n, "%s\"%s\": %lu", first ? "" : ", ", g_name[i][0] ? g_name[i] : "?", snap[i] );
-    first = 0;
-  }
-  n += snprintf( buf + n, sizeof(buf) - n, "}}\n" );
-  ssize_t w = write( 1, buf, (size_t)n ); (void)w;
+  char extra[ 64 ];
+  snprintf( extra, sizeof(extra), "\"launcher\": %d, ", launcher );
+  report( "tile", argv[1], rc, N_FRAG, pub1, dt, n_fds, extra );
   /* exit without teardown: the HIP runtime's destructors would make syscalls the policy does not need */
-  syscall( SYS_exit_group, ( rc || pub1 != N_FRAG ) ? 1 : 0 );
+  fdsb_tramp( SYS_exit_group, ( rc || pub1 != N_FRAG ) ? 1 : 0, 0, 0, 0, 0, 0 );
   return 0;
 }
