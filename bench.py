@@ -262,21 +262,24 @@ def host_plan(args, gpus: int, cores: int | None = None, nodes: dict | None = No
     tiles = min(want_t, max(1, (b - P) // (1 + h)))
     lc = want_lc if b - P >= 1 + want_lc else 0               # a launch thread only where a paced tile fits beside it
     lat_tiles = min(want_l, max(1, (b - P) // (1 + lc)))
-    need = gpus * (max(want_t * (1 + want_h), want_l * (1 + want_lc)) + P)
-    used = gpus * (max(tiles * (1 + h), lat_tiles * (1 + lc)) + P)
-    capped = tiles < want_t or lat_tiles < want_l or lc < want_lc or h < want_h
+    # served paced legs (--stream-svc-tiles): T tile processes + the verify service (+ its launch thread) per GPU
+    want_s = max([int(x) for x in str(getattr(args, "stream_svc_tiles", "") or "").split(",") if x.strip()] or [0])
+    svc_tiles = min(want_s, max(0, b - P - 1 - lc)) if want_s else 0
+    need = gpus * (max(want_t * (1 + want_h), want_l * (1 + want_lc), want_s + 1 + want_lc if want_s else 0) + P)
+    used = gpus * (max(tiles * (1 + h), lat_tiles * (1 + lc), svc_tiles + 1 + lc if svc_tiles else 0) + P)
+    capped = tiles < want_t or lat_tiles < want_l or lc < want_lc or h < want_h or svc_tiles < want_s
     plan = {"gpus": gpus, "usable_cores": cores, "cores_per_numa_node": {str(k): v for k, v in nodes.items()},
             "gpu_numa_nodes": gn, "producers_per_gpu": P,
             "requested": {"tiles_per_gpu": want_t, "paced_tiles_per_gpu": want_l, "paced_launchers": want_lc,
-                          "copy_threads_per_tile": want_h, "cores": need},
+                          "copy_threads_per_tile": want_h, "served_tiles_per_gpu": want_s, "cores": need},
             "applied": {"tiles_per_gpu": tiles, "paced_tiles_per_gpu": lat_tiles, "paced_launchers": lc,
-                        "copy_threads_per_tile": h, "cores": used},
+                        "copy_threads_per_tile": h, "served_tiles_per_gpu": svc_tiles, "cores": used},
             "capped": capped, "oversubscribed": used > cores or b < 1 + P,
             "host_dram_gbs_est": round(gpus * 2 * HOST_GBS_PER_GPU_EACH_WAY, 1)}
     if capped:
         plan["cap"] = (f"{cores} usable cores ({min(budget, node_budget)} per GPU, {P} producer(s) each): tiles per GPU "
                        f"{want_t} -> {tiles}, paced {want_l} -> {lat_tiles}, paced launch threads {want_lc} -> {lc}, "
-                       f"copy threads per tile {want_h} -> {h}")
+                       f"copy threads per tile {want_h} -> {h}, served tiles {want_s} -> {svc_tiles}")
     return plan
 
 
@@ -1270,7 +1273,8 @@ def main():
         # served paced legs (--stream-svc-tiles): T tile processes + one verify service process per GPU, a fresh
         # stream child per T, every rank in step
         served_raw = {}
-        for T in [int(x) for x in str(args.stream_svc_tiles).split(",") if x.strip()]:
+        svc_max = host_plan(args, world)["applied"]["served_tiles_per_gpu"]
+        for T in [int(x) for x in str(args.stream_svc_tiles).split(",") if x.strip() and int(x) <= svc_max]:
             a2 = argparse.Namespace(**vars(args))
             a2.stream_svc = T
             try:

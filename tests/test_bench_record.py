@@ -282,3 +282,14 @@ def test_producer_tile_placement():
     q = bench._pair_place({"prod_cpu": [-1] * 4, "tile_cpu": [cpus[0]] + [0] * 7})
     assert q["producer"] is None and q["same_l3"] is None and q["same_node"] is None
     assert bench.cpu_place(-1) is None
+
+
+@pytest.mark.parametrize("cores,gpus,want,got", [(16, 1, "1,2,3", 3), (16, 8, "1,2,3", 0), (64, 8, "1,2,3", 3),
+                                                  (40, 8, "2,3", 2), (16, 1, "", 0)])
+def test_host_plan_served_tiles(cores, gpus, want, got):
+    """Served paced legs need T tile processes + the verify service + its launch thread + the producer per
+    GPU: the plan caps T to the cores (0: the served legs are skipped rather than oversubscribe)."""
+    args = bench.parse_args(["--stream-svc-tiles", want] if want else [])
+    plan = bench.host_plan(args, gpus, cores=cores, nodes={0: cores}, gpu_nodes=[0] * gpus)
+    assert plan["applied"]["served_tiles_per_gpu"] == got
+    assert plan["applied"]["cores"] <= max(cores, gpus * 2)
