@@ -53,6 +53,14 @@ case "$job" in
       "g2:300:$P --stream-place gpu --detail-out $d/g2.json > $d/g2.line" \
       "o2:300:$P --stream-place opposite --detail-out $d/o2.json > $d/o2.line"
     ;;
+  n2svc)
+    # the N = 2 flow with served legs, both ranks on one GPU (each rank's stream child is the verify service of
+    # its GPU and starts its own tile processes; the link is shared through /dev/shm): correctness of the G > 1
+    # served path (two services on one device contend, as two GPUs' would not)
+    d=gpurun_out/r06_n2svc; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "n2:500:bash tools/rehearse_n2.sh --stream-only-paced --stream-rates 1e6,2.5e6 --stream-svc-tiles 1,2 --no-cpu-baseline --detail-out $d/detail.json > $d/line.json"
+    ;;
   svcdbg)
     bash tools/gpu_job.sh \
       "tests:300:$T -x tests/test_gpu_vsvc.py -k 'in_process or launch_thread'"
