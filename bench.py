@@ -927,14 +927,15 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
                 # first one with the GPU batch that produced it (leg, tile, ctx, seq, payload, code, path)
                 "anomalies": n_anom, "anomaly_first": first_anom}
             rec["stream_ok"] = bool(st.get("all_published")) and n_anom == 0
-            sv = st.get("served")
-            if sv:   # T tile processes per GPU served by one verify service: knee and p99 per offered rate
-                rec["stream"]["served"] = {
-                    T: ({"error": v["error"][-200:]} if "error" in v else
-                        {"knee": v["knee"], "p99_us": [_r(x[2]) for x in v["paced_fps_p50_p99_us"]],
-                         "all_published": v["all_published"], "anomalies": v["anomalies"],
-                         "tiles_gpu_open": sum((x or {}).get("tiles_gpu_open", 0) for x in v["served"])})
-                    for T, v in sv["by_tiles"].items()}
+        sv = st.get("served") if "error" not in st else None
+        if sv:   # T tile processes per GPU served by one verify service: knee and p99 per offered rate
+            rec["stream"]["served"] = {
+                T: ({"error": v["error"][-200:]} if "error" in v else
+                    {"knee": v["knee"], "p99_us": [_r(x[2]) for x in v["paced_fps_p50_p99_us"]],
+                     "all_published": v["all_published"], "anomalies": v["anomalies"],
+                     "tiles_gpu_open": sum((x or {}).get("tiles_gpu_open", 0) for x in v["served"])})
+                for T, v in sv["by_tiles"].items()}
+            rec["stream"]["served_knee_one_process"] = sv.get("knee_one_process")
     hp = full.get("host_plan")
     if hp:      # the configs[4] stream's host budget at this N (cores for its spinning tiles and producers)
         rec["host_plan"] = {"usable_cores": hp["usable_cores"], "need_cores": hp["requested"]["cores"],
@@ -1341,7 +1342,11 @@ def main():
             else:
                 stream = {"error": err or "a stream child failed on another rank"}
             if served_raw:
-                stream["served"] = served_summary(args, served_raw, (stream.get("knee") or {}).get("frags_per_s_per_gpu"))
+                k1 = (stream.get("knee") or {}).get("frags_per_s_per_gpu")
+                if "only_paced" in stream:      # the one-process knee over the same offered rates
+                    k1 = knee_of([dict(stream["only_paced"][f"paced@{r}"], offered_frags_per_s_per_gpu=r)
+                                  for r in _rates(args)])
+                stream["served"] = served_summary(args, served_raw, k1)
 
         return stream
 
