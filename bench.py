@@ -421,7 +421,9 @@ def served_summary(args, raw: dict, knee_one_process) -> dict:
             "paced_fps_p50_p99_us": [[c["offered_frags_per_s_per_gpu"], c["p50_us"], c["p99_us"]] for c in curve],
             "lost": [c["lost"] for c in curve], "overruns": [c["overruns_at_verdict"] for c in curve],
             "all_published": all(c["metrics"][:4] == [0, 0, 0, 0] for c in curve),
-            "anomalies": sum(v["count"] for v in (r.get("anomalies") or {}).values()),
+            "lost_frac": [round((c["lost"] + c["overruns_at_verdict"]) / max(c["frags"], 1), 3) for c in curve],
+            "anomalies": anomaly_summary(r.get("anomalies"), legs)[0],
+            "dedup_after_loss": sum(v.get("dedup_after_loss", 0) for v in (r.get("anomalies") or {}).values()),
             "gpu_pauses_over_250us": [(c.get("gather_gpu") or {}).get("issue_to_start_over_250us") for c in curve],
             "mean_batch_txns": [round(c["mean_batch_txns"], 1) for c in curve],
             "served": [c.get("served") for c in curve],
@@ -686,13 +688,15 @@ def stream_child_main(args) -> None:
 
     def anomalies(link, leg):
         # verdicts neither published nor overrun: in these all-valid streams every one is an anomaly
-        n, first = 0, []
+        n, first, by = 0, [], [0] * 8
         for t in vtile.tiles_of(int(link.cfg()["tiles"]), procs, proc):
             c, f = link.anomalies(t)
             n += c
             first += [dict(e, tile=t) for e in f]
+            by = [a + b for a, b in zip(by, link.anomaly_results(t))]
         if n:
-            anom[leg] = {"count": n, "first": first[:8]}
+            anom[leg] = {"count": n, "first": first[:8],
+                         "by_result": {RESULT_NAMES[i]: c for i, c in enumerate(by) if c and i < len(RESULT_NAMES)}}
     wb = {"gather": 0, "none": 1, "finish": 2}[args.stream_writeback]
     if wb or args.stream_poll_prefetch or args.stream_gather_rpb or args.stream_gather_cu_spread or args.stream_quad_sha:
         from firedancer_amd import engine
@@ -819,11 +823,33 @@ PATH_NAMES = {8: "latency8", 4: "latency4", 2: "latency2", 1: "latency1", 0: "th
               -2: "none"}
 
 
-def anomaly_summary(anomalies: dict | None) -> tuple[int, dict | None]:
-    """(count, the first record) of a stream's anomalies (fdgpu_link_anomalies, merged per leg over ranks)."""
+RESULT_NAMES = ("publish", "parse", "verify", "dedup", "bundle_peer", "overrun", "gpu_fault")   # FDGPU_VTILE_*
+DEDUP_AFTER_LOSS = 0.5
+
+
+def dedup_after_loss(leg: dict | None) -> bool:
+    """A leg whose dedup failures are explained: the payloads recycle every 2 x the HA dedup depth frags per tile
+    (stream_child_main), so a tag can still be in the tcache at its next round only when the tile lost or saw
+    overrun more than half of the frags between the two (fd_verify_tile.c:125-135 drops it the same way)."""
+    if not leg or not leg.get("frags"):
+        return False
+    return (leg.get("lost", 0) + leg.get("overruns_at_verdict", 0)) / leg["frags"] > DEDUP_AFTER_LOSS
+
+
+def anomaly_summary(anomalies: dict | None, legs: dict | None = None) -> tuple[int, dict | None]:
+    """(count, the first record) of a stream's anomalies (fdgpu_link_anomalies, merged per leg over ranks).  With
+    `legs`, a leg's dedup failures are not counted where dedup_after_loss explains them (the merged record keeps
+    them as "dedup_after_loss")."""
     n, first = 0, None
     for leg, v in (anomalies or {}).items():
-        n += int(v.get("count", 0))
+        c = int(v.get("count", 0))
+        d = int((v.get("by_result") or {}).get("dedup", 0))
+        if d and dedup_after_loss((legs or {}).get(leg)):
+            v["dedup_after_loss"] = d
+            c -= d
+            if not c:
+                continue
+        n += c
         if first is None and v.get("first"):
             first = dict(v["first"][0], leg=leg)
             if "path" in first:
@@ -887,7 +913,13 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
         rec["extra_configs"] = {k.split("_")[0]: [_r(v["sigs_per_s"]), v["results_ok"]] for k, v in ex.items()}
     st = full.get("stream")
     if st:
-        n_anom, first_anom = anomaly_summary(st.get("anomalies"))
+        legs = dict(st.get("only_paced") or {})
+        for c in st.get("latency_curve") or []:
+            legs[f"paced@{c['offered_frags_per_s_per_gpu']}"] = c
+        for k in ("max_rate", "unreliable_max"):
+            if st.get(k):
+                legs[{"max_rate": "max", "unreliable_max": "unrel"}[k]] = st[k]
+        n_anom, first_anom = anomaly_summary(st.get("anomalies"), legs)
         if "error" in st:
             rec["stream"] = {"error": str(st["error"])[-300:]}
             rec["stream_ok"] = False
@@ -1295,6 +1327,8 @@ def main():
             for leg, v in (a or {}).items():
                 m = anomalies.setdefault(leg, {"count": 0, "first": []})
                 m["count"] += v["count"]
+                for k, c in (v.get("by_result") or {}).items():
+                    m.setdefault("by_result", {})[k] = m.get("by_result", {}).get(k, 0) + c
                 m["first"] = (m["first"] + [dict(e, rank=r) for e in v["first"]])[:8]
         if rank == 0:
             if res is not None and stream_ok and args.stream_only_paced:

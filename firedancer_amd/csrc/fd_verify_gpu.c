@@ -1632,6 +1632,7 @@ typedef struct {                 /* one tile's results, written once when it fin
      with how many there were -- in the link, so a tile in a process of its own (served tiles) reports them too */
   ulong trace_cnt;
   ulong anom_cnt;
+  ulong anom_by_result[ 8 ];     /* those verdicts by result (FDGPU_VTILE_*) */
   ulong gpu_open;                /* the tile's process had the GPU open (/dev/kfd, /dev/dri) when it finished */
   fdgpu_link_anomaly_t anom[ LINK_ANOM_MAX ];
 } link_res_t;
@@ -2359,6 +2360,14 @@ fdgpu_link_anomalies( fdgpu_link_t const * l, int tile, fdgpu_link_anomaly_t * o
   return r->anom_cnt;
 }
 
+ulong
+fdgpu_link_anomaly_results( fdgpu_link_t const * l, int tile, ulong * cnt ) {
+  if( tile < 0 || tile >= LINK_TILE_MAX || tile >= l->h->cfg.tiles ) return 0UL;
+  link_res_t const * r = &l->res[tile];
+  memcpy( cnt, r->anom_by_result, sizeof(r->anom_by_result) );
+  return r->anom_cnt;
+}
+
 static void
 link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs, ulong * lh, ulong * lmax,
               ulong * t_last, link_in_t * in ) {
@@ -2377,6 +2386,7 @@ link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, 
       *sigs += l->psig[ pmask ? ( ( s * Q + (ulong)q ) & pmask ) : ( s * Q + (ulong)q ) % np ];
     if( __builtin_expect( d[i].result != FDGPU_VTILE_PUBLISH && d[i].result != FDGPU_VTILE_OVERRUN, 0 ) ) {
       ulong k = l->res[idx].anom_cnt++;
+      l->res[idx].anom_by_result[ d[i].result & 7 ]++;
       if( k < LINK_ANOM_MAX ) {
         fdgpu_link_anomaly_t * e = &l->res[idx].anom[k];
         e->seq = s; e->in_idx = d[i].in_idx; e->tag = d[i].tag; e->result = d[i].result; e->code = d[i].code;

@@ -23,7 +23,7 @@ GOSSIP_MSG_SZ = 1297     # FD_GOSSIP_UPDATE_SZ_VOTE = 49 + sizeof(fd_gossip_vote
                          # (src/flamenco/gossip/fd_gossip_private.h:80, crds/fd_crds.c:938)
 LAT_BUCKETS = 40
 
-EXPORTS = ("fdgpu_dedup_tag", "fdgpu_xxh64", "fdgpu_link_set_trace", "fdgpu_link_trace", "fdgpu_link_anomalies", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
+EXPORTS = ("fdgpu_dedup_tag", "fdgpu_xxh64", "fdgpu_link_set_trace", "fdgpu_link_trace", "fdgpu_link_anomalies", "fdgpu_link_anomaly_results", "fdgpu_tcache_new", "fdgpu_tcache_delete", "fdgpu_tcache_query", "fdgpu_tcache_insert",
            "fdgpu_mcache_new", "fdgpu_mcache_delete", "fdgpu_mcache_publish", "fdgpu_mcache_poll",
            "fdgpu_mcache_query", "fdgpu_mcache_wrap", "fdgpu_mcache_depth", "fdgpu_mcache_lines",
            "fdgpu_dcache_compact_next", "fdgpu_vtile_new", "fdgpu_vtile_delete", "fdgpu_vtile_out_dcache",
@@ -239,6 +239,8 @@ def load():
         L.fdgpu_link_trace.argtypes = [vp, ctypes.c_int, vp, ul]
         L.fdgpu_link_anomalies.restype = ul
         L.fdgpu_link_anomalies.argtypes = [vp, ctypes.c_int, vp, ul]
+        L.fdgpu_link_anomaly_results.restype = ul
+        L.fdgpu_link_anomaly_results.argtypes = [vp, ctypes.c_int, vp]
         L.fdgpu_stream_run.argtypes = [ctypes.c_int, ctypes.POINTER(StreamCfg), vp, vp, vp, ul, ul,
                                        ctypes.POINTER(StreamStats)]
         L.fdgpu_stream_bench.argtypes = [ctypes.c_int, vp, vp, vp, ul, ul, ctypes.c_int, ul, ul, ul, ctypes.c_double,
@@ -624,6 +626,12 @@ class Link:
         out = np.zeros(8, ANOM_DTYPE)
         n = int(self.L.fdgpu_link_anomalies(self.p, tile, out.ctypes.data, 8))
         return n, [{k: int(e[k]) for k in ANOM_DTYPE.names} for e in out[:min(n, 8)]]
+
+    def anomaly_results(self, tile: int) -> list[int]:
+        """fdgpu_link_anomaly_results: `tile`'s anomalous verdicts by result code (index = PUBLISH .. GPU_FAULT)."""
+        cnt = np.zeros(8, np.uint64)
+        self.L.fdgpu_link_anomaly_results(self.p, tile, cnt.ctypes.data)
+        return [int(x) for x in cnt]
 
     def placement(self) -> dict:
         """fdgpu_link_placement: per producer the NUMA node of its dcache part / mcache, and the link's bytes in

@@ -293,3 +293,19 @@ def test_host_plan_served_tiles(cores, gpus, want, got):
     plan = bench.host_plan(args, gpus, cores=cores, nodes={0: cores}, gpu_nodes=[0] * gpus)
     assert plan["applied"]["served_tiles_per_gpu"] == got
     assert plan["applied"]["cores"] <= max(cores, gpus * 2)
+
+
+def test_dedup_after_loss_is_explained_only_under_heavy_loss():
+    """Dedup failures in the all-valid stream are anomalies, except in a leg that lost or saw overrun more than
+    half its frags (the payloads recycle every 2 x the tcache depth per tile: profiles/r06/n2svc)."""
+    import bench
+    anom = {"paced@2500000.0": {"count": 10, "first": [{"result": 3, "path": 0}], "by_result": {"dedup": 10}},
+            "paced@1000000.0": {"count": 3, "first": [{"result": 3, "path": 0}], "by_result": {"dedup": 2, "gpu_fault": 1}}}
+    legs = {"paced@2500000.0": {"frags": 100, "lost": 40, "overruns_at_verdict": 15},
+            "paced@1000000.0": {"frags": 100, "lost": 0, "overruns_at_verdict": 0}}
+    n, first = bench.anomaly_summary(anom, legs)
+    assert n == 3 and first["leg"] == "paced@1000000.0"
+    assert anom["paced@2500000.0"]["dedup_after_loss"] == 10
+    legs["paced@2500000.0"]["lost"] = 30                   # 45 % lost: the dedups are anomalies again
+    assert bench.anomaly_summary({k: dict(v) for k, v in anom.items()}, legs)[0] == 13
+    assert bench.anomaly_summary(anom)[0] == 13            # without the legs nothing is explained
