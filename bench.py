@@ -569,6 +569,34 @@ def page_config() -> dict:
             "hugetlb_pages": rd("/proc/sys/vm/nr_hugepages"), "hugetlbfs_mounts": mounts}
 
 
+LINK_BYTES_PER_PAYLOAD = 1.1 * 1312      # a link's bytes per distinct payload (record + mcache line, measured map_mb)
+
+
+def link_dir(choice: str, need_bytes: int, mounts_file: str = "/proc/mounts",
+             sys_hp: str = "/sys/kernel/mm/hugepages") -> str:
+    """Where a link of several processes lives.  "auto": a writable hugetlbfs mount whose huge pages have room for
+    the link (the reference's workspaces live on fd_shmem's hugetlbfs mounts, src/util/shmem/fd_shmem_admin.c),
+    else /dev/shm (4 KiB pages where shmem_enabled is never).  Every process of a run picks the same one (the
+    same host state).  Any other value: that directory."""
+    if choice != "auto":
+        return choice
+    try:
+        mounts = [l.split() for l in open(mounts_file) if l.split()[2:3] == ["hugetlbfs"]]
+    except OSError:
+        mounts = []
+    for m in mounts:
+        d, opts = m[1], m[3].split(",")
+        ps = next((o.split("=")[1] for o in opts if o.startswith("pagesize=")), "2M")
+        kb = {"2M": 2048, "1G": 1048576, "2048k": 2048, "1048576k": 1048576}.get(ps, 2048)
+        try:
+            free = int(open(f"{sys_hp}/hugepages-{kb}kB/free_hugepages").read())
+        except (OSError, ValueError):
+            continue
+        if free * kb * 1024 >= 1.25 * need_bytes and os.access(d, os.W_OK):
+            return d
+    return "/dev/shm"
+
+
 def _kfd_gpu_ids() -> set[str]:
     """KFD gpu_ids of the GPUs this process sees (topology nodes with SIMDs)."""
     ids, base = set(), "/sys/class/kfd/kfd/topology/nodes"
@@ -704,26 +732,27 @@ def stream_child_main(args) -> None:
                               gather_rpb=args.stream_gather_rpb, gather_cu_spread=args.stream_gather_cu_spread,
                               quad_sha=args.stream_quad_sha)
     payload = desc = None
+    # distinct payloads: every tile's share must exceed its HA dedup depth (1 << 16), or each
+    # payload's second round through the link would be dropped as a duplicate (correct dedup,
+    # but then the legs would verify-and-drop instead of verify-and-publish)
+    tiles = max(args.stream_tiles, args.stream_lat_tiles, args.stream_svc) * procs
+    n_pay = max(args.txns, 2 * tiles * (1 << 16))
+    ldir = link_dir(args.stream_link_dir, int(n_pay * LINK_BYTES_PER_PAYLOAD))
     if proc == 0:
         from firedancer_amd import synth
-        # distinct payloads: every tile's share must exceed its HA dedup depth (1 << 16), or each
-        # payload's second round through the link would be dropped as a duplicate (correct dedup,
-        # but then the legs would verify-and-drop instead of verify-and-publish)
-        tiles = max(args.stream_tiles, args.stream_lat_tiles) * procs
-        n_pay = max(args.txns, 2 * tiles * (1 << 16))
         payload, desc, _, _ = synth.make_batch(n_pay, synth.LARGE_NOOP, seed=args.stream_seed,
                                                threads=min(16, os.cpu_count() or 1))
     svc_stats = {}
     for leg in stream_legs(args):
         # (served tiles are processes of their own that join the link by its file)
-        path = (f"/dev/shm/fdgpu_link_{args.stream_token}_{leg.replace('@', '_')}"
+        path = (f"{ldir}/fdgpu_link_{args.stream_token}_{leg.replace('@', '_')}"
                 if procs > 1 or args.stream_svc else None)
         if proc == 0:
             cfg = _leg_cfg(args, leg, procs, cal_fps)
             link = vtile.Link(path, create=True, payload=payload, off=desc["payload_off"], sz=desc["payload_sz"], **cfg)
             huge_mb = _anon_huge_mb()
             place = dict(link.placement(), gpu_node=vtile.gpu_numa_node(dev), place=args.stream_place,
-                         page_config=page_config())
+                         page_config=page_config(), link_dir=ldir if path else None)
             gpu_pause_log(reset=True)                 # (a fresh log for this leg)
             try:
                 with KfdSampler() as kq:
@@ -793,7 +822,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
          "--stream-tput-small-max", str(args.stream_tput_small_max), "--stream-lat-hk-us", str(args.stream_lat_hk_us),
          "--stream-lat-small-max", str(args.stream_lat_small_max), "--stream-quad-sha", str(args.stream_quad_sha),
          "--stream-lat-share", str(args.stream_lat_share), "--stream-svc", str(getattr(args, "stream_svc", 0)),
-         "--stream-place", args.stream_place]
+         "--stream-place", args.stream_place, "--stream-link-dir", args.stream_link_dir]
     if args.stream_copy:
         cmd.append("--stream-copy")
     env = dict(os.environ)
@@ -1243,6 +1272,10 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-place", choices=("gpu", "opposite", "none"), default="gpu",
                     help="NUMA node of each producer's mcache, in dcache part and thread: its GPU's (default), the node "
                          "opposite its GPU (the cross-socket arm), or unplaced (first touch by the link's creator)")
+    ap.add_argument("--stream-link-dir", default="auto",
+                    help="directory of the link file of several processes (N > 1, served legs): auto = a writable "
+                         "hugetlbfs mount with free huge pages for it (2 MiB pages, as the reference's workspaces), "
+                         "else /dev/shm")
     ap.add_argument("--stream-only-paced", action="store_true",
                     help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",

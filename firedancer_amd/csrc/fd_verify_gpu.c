@@ -16,6 +16,7 @@
 #include <sys/mman.h>
 #include <sys/resource.h>
 #include <sys/stat.h>
+#include <sys/vfs.h>
 #include <sys/wait.h>
 #include <dirent.h>
 #include <dlfcn.h>
@@ -1779,8 +1780,9 @@ static void * link_fill( void * _a ) {
 }
 
 /* where the link's memory is: each producer's dcache part and mcache NUMA node (q < producers), and of the link
-   region as this process maps it, the bytes in 2 MiB pages (AnonHugePages / ShmemPmdMapped / FilePmdMapped of its
-   mapping in /proc/self/smaps) and its size; returns the producer count */
+   region as this process maps it, the bytes in 2 MiB pages (AnonHugePages / ShmemPmdMapped / FilePmdMapped, and
+   Shared_/Private_Hugetlb for a link file on hugetlbfs, of its mapping in /proc/self/smaps) and its size; returns
+   the producer count */
 int
 fdgpu_link_placement( fdgpu_link_t const * l, int * dc_node, int * mc_node, unsigned long * huge_bytes,
                       unsigned long * map_bytes ) {
@@ -1800,7 +1802,8 @@ fdgpu_link_placement( fdgpu_link_t const * l, int * dc_node, int * mc_node, unsi
       }
       ulong kb;
       if( in && ( sscanf( line, "AnonHugePages: %lu kB", &kb ) == 1 || sscanf( line, "ShmemPmdMapped: %lu kB", &kb ) == 1 ||
-                  sscanf( line, "FilePmdMapped: %lu kB", &kb ) == 1 ) ) *huge_bytes += kb << 10;
+                  sscanf( line, "FilePmdMapped: %lu kB", &kb ) == 1 || sscanf( line, "Shared_Hugetlb: %lu kB", &kb ) == 1 ||
+                  sscanf( line, "Private_Hugetlb: %lu kB", &kb ) == 1 ) ) *huge_bytes += kb << 10;
     }
     fclose( f );
   }
@@ -1846,6 +1849,11 @@ fdgpu_link_new( char const * path, fdgpu_stream_cfg_t const * cfg, uchar const *
   if( shared ) {
     int fd = open( path, O_RDWR | O_CREAT | O_EXCL, 0600 );
     if( fd < 0 ) return NULL;
+    /* a path on hugetlbfs (the reference's workspaces: fd_shmem's .huge / .gigantic mounts) gives the link huge
+       pages whatever shmem_enabled says: the file's size is then a whole number of its pages */
+    struct statfs sfs;
+    if( !fstatfs( fd, &sfs ) && (ulong)sfs.f_type == 0x958458f6UL && sfs.f_bsize > 0 )
+      total = ( total + (ulong)sfs.f_bsize - 1UL ) / (ulong)sfs.f_bsize * (ulong)sfs.f_bsize;
     if( ftruncate( fd, (off_t)total ) ) { close( fd ); unlink( path ); return NULL; }
     base = (uchar *)mmap( NULL, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0 );
     close( fd );
@@ -1908,11 +1916,14 @@ fdgpu_link_join( char const * path, double timeout_s ) {
     if( fd >= 0 ) {
       struct stat st;
       if( !fstat( fd, &st ) && (ulong)st.st_size >= sizeof(link_hdr_t) ) {
-        link_hdr_t * h = (link_hdr_t *)mmap( NULL, sizeof(link_hdr_t), PROT_READ, MAP_SHARED, fd, 0 );
+        /* (whole pages of the file's own size: a link on hugetlbfs is mapped and unmapped in huge pages) */
+        ulong pg = st.st_blksize > 4096 ? (ulong)st.st_blksize : 4096UL;
+        ulong hl = ( sizeof(link_hdr_t) + pg - 1UL ) / pg * pg;
+        link_hdr_t * h = (link_hdr_t *)mmap( NULL, hl, PROT_READ, MAP_SHARED, fd, 0 );
         if( h != MAP_FAILED ) {
           int ok = atomic_load_explicit( &h->magic, memory_order_acquire ) == LINK_MAGIC;
           ulong total = h->total_sz;
-          munmap( (void *)h, sizeof(link_hdr_t) );
+          munmap( (void *)h, hl );
           if( ok && (ulong)st.st_size >= total ) {
             /* every page mapped now (MAP_POPULATE): a tile that joins reads records all over the in dcache, and
                would otherwise take a page fault per page at the start of its stream (measured: multi-ms stalls

@@ -309,3 +309,20 @@ def test_dedup_after_loss_is_explained_only_under_heavy_loss():
     legs["paced@2500000.0"]["lost"] = 30                   # 45 % lost: the dedups are anomalies again
     assert bench.anomaly_summary({k: dict(v) for k, v in anom.items()}, legs)[0] == 13
     assert bench.anomaly_summary(anom)[0] == 13            # without the legs nothing is explained
+
+
+def test_link_dir_prefers_hugetlbfs_with_room(tmp_path):
+    """The link of several processes goes on a writable hugetlbfs mount with free pages for it (2 MiB pages, as the
+    reference's workspaces), else /dev/shm."""
+    import bench
+    mnt = tmp_path / "huge"; mnt.mkdir()
+    hp = tmp_path / "hp" / "hugepages-2048kB"; hp.mkdir(parents=True)
+    (hp / "free_hugepages").write_text("1024\n")                       # 2 GiB free
+    mounts = tmp_path / "mounts"
+    mounts.write_text(f"tmpfs /dev/shm tmpfs rw 0 0\nnone {mnt} hugetlbfs rw,relatime,pagesize=2M 0 0\n")
+    f = lambda need, choice="auto": bench.link_dir(choice, need, str(mounts), str(tmp_path / "hp"))
+    assert f(1 << 30) == str(mnt)
+    assert f(2 << 30) == "/dev/shm"                                    # not room for 1.25 x the link
+    assert f(1 << 30, "/tmp/x") == "/tmp/x"
+    mounts.write_text("tmpfs /dev/shm tmpfs rw 0 0\n")
+    assert f(1 << 20) == "/dev/shm"
