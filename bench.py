@@ -1264,7 +1264,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-copy-threads", type=int, default=0, choices=range(0, 9),
                     help="max-rate and unreliable legs: host threads per tile that copy each record into the out dcache "
                          "while the GPU copy only reads it (fdgpu_vtile_opts_t.copy_threads; a core each in the host plan)")
-    ap.add_argument("--stream-svc-tiles", default="",
+    ap.add_argument("--stream-svc-tiles", default="2",
                     help="served paced legs: for each T in this comma list, T verify-tile processes per GPU (the fdgpu_tile "
                          "program, no GPU context each) served by one verify service process per GPU (fdgpu_vsvc_*), at "
                          "the --stream-rates offered loads per GPU; stream.served[T] holds the curve and knee (empty: skip)")

@@ -176,7 +176,7 @@ def test_leg_copy_settings():
 def test_host_plan_caps_tiles_to_the_cores(cores, gpus, tiles, capped):
     """VERDICT r04 Missing 3: per GPU 2 max-rate tiles (or 1 paced tile) + 1 producer, each spinning on a core
     of its own (topology.c:167-170); tiles per GPU drop, never below 1, when the job's cores cannot hold them."""
-    args = bench.parse_args([])
+    args = bench.parse_args(["--stream-svc-tiles", ""])       # (the served legs' budget: below)
     plan = bench.host_plan(args, gpus, cores=cores, nodes={0: cores}, gpu_nodes=[0] * gpus)
     assert plan["requested"]["cores"] == gpus * 3
     assert plan["applied"]["tiles_per_gpu"] == tiles and plan["capped"] is capped
@@ -190,13 +190,13 @@ def test_host_plan_caps_tiles_to_the_cores(cores, gpus, tiles, capped):
 def test_host_plan_paced_launch_threads(cores, gpus, launchers):
     """--stream-lat-launcher: a paced tile's launch thread takes a core of its own; where a GPU's share
     cannot hold tile + launch thread + producer the plan drops the thread (and says so), never the tile."""
-    args = bench.parse_args(["--stream-lat-launcher", "1"])
+    args = bench.parse_args(["--stream-lat-launcher", "1", "--stream-svc-tiles", ""])
     plan = bench.host_plan(args, gpus, cores=cores, nodes={0: cores}, gpu_nodes=[0] * gpus)
     assert plan["requested"]["paced_launchers"] == 1 and plan["applied"]["paced_launchers"] == launchers
     assert plan["applied"]["paced_tiles_per_gpu"] == 1
     assert plan["applied"]["cores"] == gpus * (max(plan["applied"]["tiles_per_gpu"], 1 + launchers) + 1)
     assert plan["capped"] is (launchers == 0 or plan["applied"]["tiles_per_gpu"] < 2)
-    args = bench.parse_args(["--stream-lat-launcher", "1", "--plan-cores", str(cores)])
+    args = bench.parse_args(["--stream-lat-launcher", "1", "--plan-cores", str(cores), "--stream-svc-tiles", ""])
     assert bench._leg_cfg(args, "paced@5000000.0", gpus, 20e6)["launcher"] == launchers
     assert bench._leg_cfg(args, "max", gpus, 20e6)["launcher"] == 0
 
@@ -256,8 +256,9 @@ def test_dry_run_prints_the_plan(tmp_path):
                        capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     hp = json.loads(r.stdout.strip().splitlines()[-1])["host_plan"]
-    assert hp["need_cores"] == 24 and hp["used_cores"] == 16 and hp["tiles_per_gpu"] == 1 and hp["capped"]
-    assert "2 -> 1" in hp["cap"]
+    # per GPU the served legs ask the most: 2 tile processes + the verify service + its launch thread + a producer
+    assert hp["need_cores"] == 40 and hp["used_cores"] == 16 and hp["tiles_per_gpu"] == 1 and hp["capped"]
+    assert "2 -> 1" in hp["cap"] and "served tiles 2 -> 0" in hp["cap"]
 
 
 def test_kfd_queues_without_kfd():
@@ -285,11 +286,12 @@ def test_producer_tile_placement():
 
 
 @pytest.mark.parametrize("cores,gpus,want,got", [(16, 1, "1,2,3", 3), (16, 8, "1,2,3", 0), (64, 8, "1,2,3", 3),
-                                                  (40, 8, "2,3", 2), (16, 1, "", 0)])
+                                                  (40, 8, "2,3", 2), (16, 1, "", 0), (16, 1, None, 2)])
 def test_host_plan_served_tiles(cores, gpus, want, got):
     """Served paced legs need T tile processes + the verify service + its launch thread + the producer per
-    GPU: the plan caps T to the cores (0: the served legs are skipped rather than oversubscribe)."""
-    args = bench.parse_args(["--stream-svc-tiles", want] if want else [])
+    GPU: the plan caps T to the cores (0: the served legs are skipped rather than oversubscribe).  The default
+    (None) runs T = 2."""
+    args = bench.parse_args(["--stream-svc-tiles", want] if want is not None else [])
     plan = bench.host_plan(args, gpus, cores=cores, nodes={0: cores}, gpu_nodes=[0] * gpus)
     assert plan["applied"]["served_tiles_per_gpu"] == got
     assert plan["applied"]["cores"] <= max(cores, gpus * 2)
