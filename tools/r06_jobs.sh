@@ -61,6 +61,13 @@ case "$job" in
     bash tools/gpu_job.sh \
       "n2:500:bash tools/rehearse_n2.sh --stream-only-paced --stream-rates 1e6,2.5e6 --stream-svc-tiles 1,2 --no-cpu-baseline --detail-out $d/detail.json > $d/line.json"
     ;;
+  dflt)
+    # the default bench (served legs included) timed end to end, then the served tests
+    d=gpurun_out/r06_dflt; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "bench:600:python bench.py --detail-out $d/detail.json > $d/line.json" \
+      "tests:600:$T tests/test_gpu_vsvc.py"
+    ;;
   svcdbg)
     bash tools/gpu_job.sh \
       "tests:300:$T -x tests/test_gpu_vsvc.py -k 'in_process or launch_thread'"
