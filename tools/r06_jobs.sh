@@ -68,6 +68,14 @@ case "$job" in
       "bench:600:python bench.py --detail-out $d/detail.json > $d/line.json" \
       "tests:600:$T tests/test_gpu_vsvc.py"
     ;;
+  hi)
+    # served tiles above the knee: 10M, 12.5M, 15M per GPU, T = 2, 3 beside one process (twice, interleaved)
+    d=gpurun_out/r06_hi; mkdir -p $d
+    A="python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-only-paced --stream-rates 10e6,12.5e6,15e6 --stream-svc-tiles 2,3"
+    bash tools/gpu_job.sh \
+      "h1:400:$A --detail-out $d/h1.json > $d/h1.line" \
+      "h2:400:$A --detail-out $d/h2.json > $d/h2.line"
+    ;;
   svcdbg)
     bash tools/gpu_job.sh \
       "tests:300:$T -x tests/test_gpu_vsvc.py -k 'in_process or launch_thread'"
