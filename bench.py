@@ -1022,8 +1022,14 @@ def emit_record(full: dict, detail_path: str | None) -> str:
     line = json.dumps(compact_record(full, detail_path), separators=(",", ":"))
     if len(line) > HEADLINE_MAX_BYTES:       # never again an unparseable line: drop the side summaries first
         rec = compact_record(full, detail_path)
-        for k in ("stream", "extra_configs", "latency", "per_gpu"):
-            rec.pop(k, None)
+        st = rec.get("stream") if isinstance(rec.get("stream"), dict) else {}
+        # the stream's diagnostics first (all in the detail file), then whole side summaries
+        drops = [(st, k) for k in ("knee_def", "paced_producer_tile_same_l3", "paced_intake_ns_per_frag",
+                                   "paced_gpu_pause_max_us", "tile_host_ns_per_frag", "link_placement",
+                                   "host_cpu_share_min", "anomaly_first")] + \
+                [(rec, k) for k in ("extra_configs", "latency", "per_gpu", "stream")]
+        for d, k in drops:
+            d.pop(k, None)
             line = json.dumps(rec, separators=(",", ":"))
             if len(line) <= HEADLINE_MAX_BYTES:
                 break

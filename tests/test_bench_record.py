@@ -328,3 +328,18 @@ def test_link_dir_prefers_hugetlbfs_with_room(tmp_path):
     assert f(1 << 30, "/tmp/x") == "/tmp/x"
     mounts.write_text("tmpfs /dev/shm tmpfs rw 0 0\n")
     assert f(1 << 20) == "/dev/shm"
+
+
+def test_n8_line_keeps_the_stream_knee():
+    """At N = 8 the line grows (8 per_gpu rows, the host plan's cap text): the stream's diagnostics go first, so
+    the knee and the served curve stay in it (the default run of profiles/r06/dflt, widened to 8 ranks)."""
+    full = json.load(open(os.path.join(ROOT, "profiles", "r06", "dflt", "detail.json")))
+    full["n_gpus"] = 8
+    full["per_gpu"] = [dict(full["per_gpu"][0], rank=r) for r in range(8)]
+    full["host_plan"]["capped"] = True
+    full["host_plan"]["cap"] = "c" * 260
+    line = bench.emit_record(full, None)
+    rec = json.loads(line)
+    assert len(line) <= bench.HEADLINE_MAX_BYTES
+    assert rec["stream"]["knee"] == 10e6 and rec["stream"]["served"]["2"]["knee"] == 10e6
+    assert len(rec["per_gpu"]) == 8 and rec["host_plan"]["cap"]
