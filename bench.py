@@ -291,7 +291,9 @@ def host_plan(args, gpus: int, cores: int | None = None, nodes: dict | None = No
 def stream_legs(args) -> list[str]:
     """cal, max, one paced leg per --stream-rates entry (frags/s per GPU), unrel (--stream-only-paced: the paced
     legs alone, e.g. under a kernel trace)"""
-    if getattr(args, "stream_only_paced", False) or getattr(args, "stream_svc", 0):
+    if getattr(args, "stream_svc", 0):       # served: the paced legs (and, --stream-svc-max, the max rate first)
+        return (["max"] if getattr(args, "stream_svc_max", 0) else []) + [f"paced@{r}" for r in _rates(args)]
+    if getattr(args, "stream_only_paced", False):
         return [f"paced@{r}" for r in _rates(args)]
     return ["cal", "max"] + [f"paced@{r}" for r in _rates(args)] + ["unrel"]
 
@@ -374,6 +376,11 @@ def _leg_cfg(args, leg, procs, cal_fps):
     if leg == "cal":
         return dict(base, tiles=T, n_frags=args.stream_frags if args.stream_frags > 0 else 2_000_000 * procs,
                     rate_fps=0.0, reliable=True)
+    if leg == "max" and getattr(args, "stream_svc", 0):
+        # served max rate: T tile processes per GPU and the verify service on the reliable link (credit-based),
+        # with the max-rate legs' batching; sized for ~SVC_MAX_FPS_EST frags/s per GPU over --stream-seconds
+        n = args.stream_frags if args.stream_frags > 0 else int(SVC_MAX_FPS_EST * procs * args.stream_seconds)
+        return dict(base, tiles=args.stream_svc * procs, n_frags=n, rate_fps=0.0, reliable=True, svc=1)
     if leg == "max":            # credit-based: the sustained rate with no frag lost
         n = args.stream_frags if args.stream_frags > 0 else int(1.2 * cal_fps * args.stream_seconds)
         return dict(base, tiles=T, n_frags=n, rate_fps=0.0, reliable=True)
@@ -391,6 +398,7 @@ def _leg_cfg(args, leg, procs, cal_fps):
 
 
 KNEE_P99_US = 1000.0
+SVC_MAX_FPS_EST = 30e6          # the served max-rate leg's frag count per GPU-second (its length, not a bound)
 
 
 def knee_of(curve: list) -> float | None:
@@ -416,8 +424,13 @@ def served_summary(args, raw: dict, knee_one_process) -> dict:
             continue
         legs = r["legs"]
         curve = [dict(legs[f"paced@{x}"], offered_frags_per_s_per_gpu=x) for x in _rates(args)]
+        mx = legs.get("max")
         out["by_tiles"][str(T)] = {
             "knee": knee_of(curve),
+            # the reliable max-rate leg (--stream-svc-max): sigs/s of the GPU's T tile processes, every frag published
+            "max": ({"sigs_per_s": mx["sigs_per_s"], "lost": mx["lost"], "published_all": mx["published"] == mx["frags"],
+                     "tile_host_ns_per_frag": mx.get("tile_host_ns_per_frag"), "pcie": mx.get("pcie"),
+                     "served": mx.get("served")} if mx else None),
             "paced_fps_p50_p99_us": [[c["offered_frags_per_s_per_gpu"], c["p50_us"], c["p99_us"]] for c in curve],
             "lost": [c["lost"] for c in curve], "overruns": [c["overruns_at_verdict"] for c in curve],
             "all_published": all(c["metrics"][:4] == [0, 0, 0, 0] for c in curve),
@@ -822,6 +835,7 @@ def run_stream_child(args, dev, proc, procs, token) -> dict:
          "--stream-tput-small-max", str(args.stream_tput_small_max), "--stream-lat-hk-us", str(args.stream_lat_hk_us),
          "--stream-lat-small-max", str(args.stream_lat_small_max), "--stream-quad-sha", str(args.stream_quad_sha),
          "--stream-lat-share", str(args.stream_lat_share), "--stream-svc", str(getattr(args, "stream_svc", 0)),
+         "--stream-svc-max", str(getattr(args, "stream_svc_max", 0)),
          "--stream-place", args.stream_place, "--stream-link-dir", args.stream_link_dir]
     if args.stream_copy:
         cmd.append("--stream-copy")
@@ -993,6 +1007,7 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
             rec["stream"]["served"] = {
                 T: ({"error": v["error"][-200:]} if "error" in v else
                     {"knee": v["knee"], "p99_us": [_r(x[2]) for x in v["paced_fps_p50_p99_us"]],
+                     **({"max_sigs_per_s": _r(v["max"]["sigs_per_s"])} if v.get("max") else {}),
                      "all_published": v["all_published"], "anomalies": v["anomalies"],
                      "tiles_gpu_open": sum((x or {}).get("tiles_gpu_open", 0) for x in v["served"])})
                 for T, v in sv["by_tiles"].items()}
@@ -1186,7 +1201,7 @@ def parse_args(argv=None) -> argparse.Namespace:
                     help="mcache lines of the max-rate legs' link: a reliable producer runs depth/2 ahead of the "
                          "oldest frag a tile still holds, so the depth bounds the frags in flight (2^18: 13.8M, "
                          "2^20: 16-17.6M sigs/s on 2 tiles, profiles/r02/stream/sweep_depth.log)")
-    ap.add_argument("--stream-rates", default="2e6,5e6,7.5e6,10e6,15e6",
+    ap.add_argument("--stream-rates", default="2e6,5e6,7.5e6,10e6,12.5e6,15e6",
                     help="paced legs (the latency-under-load curve): offered frags/s per GPU, comma separated; "
                          "stream.knee = the highest whose p99 is <= 1 ms with no frag lost")
     ap.add_argument("--stream-paced-seconds", type=float, default=3.0, help="length of each paced leg")
@@ -1275,6 +1290,8 @@ def parse_args(argv=None) -> argparse.Namespace:
                          "program, no GPU context each) served by one verify service process per GPU (fdgpu_vsvc_*), at "
                          "the --stream-rates offered loads per GPU; stream.served[T] holds the curve and knee (empty: skip)")
     ap.add_argument("--stream-svc", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--stream-svc-max", type=int, default=0, choices=(0, 1),
+                    help="served legs: also a reliable max-rate leg with the T tile processes (stream.served[T].max)")
     ap.add_argument("--stream-place", choices=("gpu", "opposite", "none"), default="gpu",
                     help="NUMA node of each producer's mcache, in dcache part and thread: its GPU's (default), the node "
                          "opposite its GPU (the cross-socket arm), or unplaced (first touch by the link's creator)")
