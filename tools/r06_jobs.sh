@@ -76,6 +76,12 @@ case "$job" in
       "h1:400:$A --detail-out $d/h1.json > $d/h1.line" \
       "h2:400:$A --detail-out $d/h2.json > $d/h2.line"
     ;;
+  smax)
+    # served max rate (reliable link, credit-based) with T = 2, 3, 4 tile processes beside the one-process legs
+    d=gpurun_out/r06_smax; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "s1:500:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-rates 10e6,12.5e6 --stream-svc-tiles 2,3,4 --stream-svc-max 1 --detail-out $d/s1.json > $d/s1.line"
+    ;;
   svcdbg)
     bash tools/gpu_job.sh \
       "tests:300:$T -x tests/test_gpu_vsvc.py -k 'in_process or launch_thread'"
