@@ -380,7 +380,9 @@ def _leg_cfg(args, leg, procs, cal_fps):
         # served max rate: T tile processes per GPU and the verify service on the reliable link (credit-based),
         # with the max-rate legs' batching; sized for ~SVC_MAX_FPS_EST frags/s per GPU over --stream-seconds
         n = args.stream_frags if args.stream_frags > 0 else int(SVC_MAX_FPS_EST * procs * args.stream_seconds)
-        return dict(base, tiles=args.stream_svc * procs, n_frags=n, rate_fps=0.0, reliable=True, svc=1)
+        # the service holds the engine contexts the one-process max leg's tiles hold together (tiles x contexts)
+        return dict(base, tiles=args.stream_svc * procs, n_frags=n, rate_fps=0.0, reliable=True, svc=1,
+                    nctx=min(3, args.stream_ctx * args.stream_tiles))
     if leg == "max":            # credit-based: the sustained rate with no frag lost
         n = args.stream_frags if args.stream_frags > 0 else int(1.2 * cal_fps * args.stream_seconds)
         return dict(base, tiles=T, n_frags=n, rate_fps=0.0, reliable=True)

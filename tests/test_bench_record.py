@@ -343,3 +343,18 @@ def test_n8_line_keeps_the_stream_knee():
     assert len(line) <= bench.HEADLINE_MAX_BYTES
     assert rec["stream"]["knee"] == 10e6 and rec["stream"]["served"]["2"]["knee"] == 10e6
     assert len(rec["per_gpu"]) == 8 and rec["host_plan"]["cap"]
+
+
+def test_served_max_leg_cfg():
+    """--stream-svc-max: the served legs start with a reliable max-rate leg over the T tile processes, batched
+    as the max-rate legs are (throughput path), sized by SVC_MAX_FPS_EST."""
+    args = bench.parse_args(["--stream-svc-max", "1"])
+    args.stream_svc = 3
+    assert bench.stream_legs(args)[0] == "max" and bench.stream_legs(args)[1].startswith("paced@")
+    c = bench._leg_cfg(args, "max", 2, 0.0)
+    assert c["svc"] == 1 and c["tiles"] == 6 and c["reliable"] and c["rate_fps"] == 0.0
+    assert c["n_frags"] == int(bench.SVC_MAX_FPS_EST * 2 * args.stream_seconds)
+    assert c["batch_txn"] == bench._leg_cfg(args, "cal", 2, 0.0)["batch_txn"]
+    assert c["nctx"] == args.stream_ctx * args.stream_tiles     # the contexts of the one-process max leg's tiles
+    args.stream_svc_max = 0
+    assert "max" not in bench.stream_legs(args)

@@ -82,6 +82,12 @@ case "$job" in
     bash tools/gpu_job.sh \
       "s1:500:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-rates 10e6,12.5e6 --stream-svc-tiles 2,3,4 --stream-svc-max 1 --detail-out $d/s1.json > $d/s1.line"
     ;;
+  smax2)
+    # served max rate with the one-process max leg's engine contexts in the service (2), T = 2, 3, 4
+    d=gpurun_out/r06_smax2; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "s2:500:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-rates 10e6,12.5e6 --stream-svc-tiles 2,3,4 --stream-svc-max 1 --detail-out $d/s2.json > $d/s2.line"
+    ;;
   svcdbg)
     bash tools/gpu_job.sh \
       "tests:300:$T -x tests/test_gpu_vsvc.py -k 'in_process or launch_thread'"
