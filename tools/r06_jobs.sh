@@ -88,6 +88,25 @@ case "$job" in
     bash tools/gpu_job.sh \
       "s2:500:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-rates 10e6,12.5e6 --stream-svc-tiles 2,3,4 --stream-svc-max 1 --detail-out $d/s2.json > $d/s2.line"
     ;;
+  ftests)
+    # round-end evidence, part 1: the whole GPU suite and the smoke
+    d=gpurun_out/r06_final; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "tests:1100:$T tests -m gpu > $d/gpu_tests.log 2>&1" \
+      "smoke:300:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")' > $d/smoke.log 2>&1"
+    ;;
+  fbench)
+    # round-end evidence, part 2: the default bench, rocprof kernel stats of the headline bench, PMC passes
+    d=gpurun_out/r06_final; mkdir -p $d
+    B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
+    P="timeout -s KILL 120 rocprofv3 --kernel-include-regex fd_ -f csv"
+    bash tools/gpu_job.sh \
+      "bench:480:python bench.py --steps 20 --warmup 5 --detail-out $d/bench_detail.json > $d/bench_line.json" \
+      "stats:240:rocprofv3 --kernel-trace --stats -f csv -d $d/stats -o run -- $B > $d/bench_under_rocprof.json" \
+      "pmc_fetch:150:$P --pmc FETCH_SIZE -d $d/fetch -o run -- $B" \
+      "pmc_write:150:$P --pmc WRITE_SIZE -d $d/write -o run -- $B" \
+      "pmc_sq:150:$P --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE -d $d/sq -o run -- $B"
+    ;;
   svcdbg)
     bash tools/gpu_job.sh \
       "tests:300:$T -x tests/test_gpu_vsvc.py -k 'in_process or launch_thread'"
