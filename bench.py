@@ -437,8 +437,8 @@ def served_summary(args, raw: dict, knee_one_process) -> dict:
             "lost": [c["lost"] for c in curve], "overruns": [c["overruns_at_verdict"] for c in curve],
             "all_published": all(c["metrics"][:4] == [0, 0, 0, 0] for c in curve),
             "lost_frac": [round((c["lost"] + c["overruns_at_verdict"]) / max(c["frags"], 1), 3) for c in curve],
-            "anomalies": anomaly_summary(r.get("anomalies"), legs)[0],
-            "dedup_after_loss": sum(v.get("dedup_after_loss", 0) for v in (r.get("anomalies") or {}).values()),
+            "anomalies": anomaly_summary(r.get("anomalies"))[0],
+            "dedup_recycled": dedup_recycled(r.get("anomalies")),
             "gpu_pauses_over_250us": [(c.get("gather_gpu") or {}).get("issue_to_start_over_250us") for c in curve],
             "mean_batch_txns": [round(c["mean_batch_txns"], 1) for c in curve],
             "served": [c.get("served") for c in curve],
@@ -731,13 +731,15 @@ def stream_child_main(args) -> None:
 
     def anomalies(link, leg):
         # verdicts neither published nor overrun: in these all-valid streams every one is an anomaly
+        # (and, apart, the dedups of payloads a tile had published before: the payloads recycle, so after a tile
+        # lost most of its frags a tag can still be in its tcache -- correct drops, fdgpu_link_anomaly_results)
         n, first, by = 0, [], [0] * 8
         for t in vtile.tiles_of(int(link.cfg()["tiles"]), procs, proc):
             c, f = link.anomalies(t)
             n += c
             first += [dict(e, tile=t) for e in f]
             by = [a + b for a, b in zip(by, link.anomaly_results(t))]
-        if n:
+        if n or by[0]:
             anom[leg] = {"count": n, "first": first[:8],
                          "by_result": {RESULT_NAMES[i]: c for i, c in enumerate(by) if c and i < len(RESULT_NAMES)}}
     wb = {"gather": 0, "none": 1, "finish": 2}[args.stream_writeback]
@@ -868,33 +870,21 @@ PATH_NAMES = {8: "latency8", 4: "latency4", 2: "latency2", 1: "latency1", 0: "th
               -2: "none"}
 
 
-RESULT_NAMES = ("publish", "parse", "verify", "dedup", "bundle_peer", "overrun", "gpu_fault")   # FDGPU_VTILE_*
-DEDUP_AFTER_LOSS = 0.5
+# fdgpu_link_anomaly_results' slots (FDGPU_VTILE_*): slot 0 (PUBLISH, never an anomaly) counts the dedups of
+# payloads the tile had published before -- correct drops of the recycled synthetic payloads, not anomalies
+RESULT_NAMES = ("dedup_recycled", "parse", "verify", "dedup", "bundle_peer", "overrun", "gpu_fault")
 
 
-def dedup_after_loss(leg: dict | None) -> bool:
-    """A leg whose dedup failures are explained: the payloads recycle every 2 x the HA dedup depth frags per tile
-    (stream_child_main), so a tag can still be in the tcache at its next round only when the tile lost or saw
-    overrun more than half of the frags between the two (fd_verify_tile.c:125-135 drops it the same way)."""
-    if not leg or not leg.get("frags"):
-        return False
-    return (leg.get("lost", 0) + leg.get("overruns_at_verdict", 0)) / leg["frags"] > DEDUP_AFTER_LOSS
+def dedup_recycled(anomalies: dict | None) -> int:
+    """The correct dedups of recycled payloads over a stream's legs (not in the anomaly count)."""
+    return sum(int((v.get("by_result") or {}).get("dedup_recycled", 0)) for v in (anomalies or {}).values())
 
 
-def anomaly_summary(anomalies: dict | None, legs: dict | None = None) -> tuple[int, dict | None]:
-    """(count, the first record) of a stream's anomalies (fdgpu_link_anomalies, merged per leg over ranks).  With
-    `legs`, a leg's dedup failures are not counted where dedup_after_loss explains them (the merged record keeps
-    them as "dedup_after_loss")."""
+def anomaly_summary(anomalies: dict | None) -> tuple[int, dict | None]:
+    """(count, the first record) of a stream's anomalies (fdgpu_link_anomalies, merged per leg over ranks)."""
     n, first = 0, None
     for leg, v in (anomalies or {}).items():
-        c = int(v.get("count", 0))
-        d = int((v.get("by_result") or {}).get("dedup", 0))
-        if d and dedup_after_loss((legs or {}).get(leg)):
-            v["dedup_after_loss"] = d
-            c -= d
-            if not c:
-                continue
-        n += c
+        n += int(v.get("count", 0))
         if first is None and v.get("first"):
             first = dict(v["first"][0], leg=leg)
             if "path" in first:
@@ -958,13 +948,7 @@ def compact_record(full: dict, detail_path: str | None) -> dict:
         rec["extra_configs"] = {k.split("_")[0]: [_r(v["sigs_per_s"]), v["results_ok"]] for k, v in ex.items()}
     st = full.get("stream")
     if st:
-        legs = dict(st.get("only_paced") or {})
-        for c in st.get("latency_curve") or []:
-            legs[f"paced@{c['offered_frags_per_s_per_gpu']}"] = c
-        for k in ("max_rate", "unreliable_max"):
-            if st.get(k):
-                legs[{"max_rate": "max", "unreliable_max": "unrel"}[k]] = st[k]
-        n_anom, first_anom = anomaly_summary(st.get("anomalies"), legs)
+        n_anom, first_anom = anomaly_summary(st.get("anomalies"))
         if "error" in st:
             rec["stream"] = {"error": str(st["error"])[-300:]}
             rec["stream_ok"] = False

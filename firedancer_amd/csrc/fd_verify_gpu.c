@@ -1633,7 +1633,7 @@ typedef struct {                 /* one tile's results, written once when it fin
      with how many there were -- in the link, so a tile in a process of its own (served tiles) reports them too */
   ulong trace_cnt;
   ulong anom_cnt;
-  ulong anom_by_result[ 8 ];     /* those verdicts by result (FDGPU_VTILE_*) */
+  ulong anom_by_result[ 8 ];     /* those verdicts by result (FDGPU_VTILE_*); [0]: dedups of payloads the tile published before */
   ulong gpu_open;                /* the tile's process had the GPU open (/dev/kfd, /dev/dri) when it finished */
   fdgpu_link_anomaly_t anom[ LINK_ANOM_MAX ];
 } link_res_t;
@@ -2381,9 +2381,12 @@ fdgpu_link_anomaly_results( fdgpu_link_t const * l, int tile, ulong * cnt ) {
 
 static void
 link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, ulong * sigs, ulong * lh, ulong * lmax,
-              ulong * t_last, link_in_t * in ) {
+              ulong * t_last, link_in_t * in, uchar * pub ) {
   /* bench accounting only (not after_frag): the signature count comes from
-     the link's per-payload table, not from the (cold) record in the out dcache */
+     the link's per-payload table, not from the (cold) record in the out dcache.  pub: a bit per payload this
+     tile has published -- the link's payloads recycle, so a dedup failure of a payload the tile published
+     before is the tcache doing its job (its tag is still there: the tile lost or saw overrun most of the frags
+     since), not an anomaly */
   ulong t = now_ns(), np = l->h->n_payload, Q = (ulong)l->h->cfg.producers;
   ulong pmask = ( np & ( np - 1UL ) ) ? 0UL : np - 1UL;   /* a power-of-two payload count: a mask, not a division */
   for( ulong i=0; i<n; i++ ) {
@@ -2393,15 +2396,21 @@ link_account( fdgpu_link_t * l, int idx, fdgpu_vtile_done_t const * d, ulong n, 
     int q = (int)d[i].in_idx;                      /* < Q: the tile handed it over with its link */
     ulong s = d[i].seq;
     in[q].fin++;
+    ulong pi = pmask ? ( ( s * Q + (ulong)q ) & pmask ) : ( s * Q + (ulong)q ) % np;
     if( d[i].result == FDGPU_VTILE_PUBLISH || d[i].result == FDGPU_VTILE_VERIFY_FAIL || d[i].result == FDGPU_VTILE_DEDUP_FAIL )
-      *sigs += l->psig[ pmask ? ( ( s * Q + (ulong)q ) & pmask ) : ( s * Q + (ulong)q ) % np ];
-    if( __builtin_expect( d[i].result != FDGPU_VTILE_PUBLISH && d[i].result != FDGPU_VTILE_OVERRUN, 0 ) ) {
+      *sigs += l->psig[ pi ];
+    if( d[i].result == FDGPU_VTILE_PUBLISH ) { if( pub ) pub[ pi >> 3 ] |= (uchar)( 1u << ( pi & 7UL ) ); continue; }
+    if( d[i].result == FDGPU_VTILE_DEDUP_FAIL && pub && ( pub[ pi >> 3 ] >> ( pi & 7UL ) & 1 ) ) {
+      l->res[idx].anom_by_result[ 0 ]++;           /* (slot 0, PUBLISH, never an anomaly: the recycled dedups) */
+      continue;
+    }
+    if( __builtin_expect( d[i].result != FDGPU_VTILE_OVERRUN, 0 ) ) {
       ulong k = l->res[idx].anom_cnt++;
       l->res[idx].anom_by_result[ d[i].result & 7 ]++;
       if( k < LINK_ANOM_MAX ) {
         fdgpu_link_anomaly_t * e = &l->res[idx].anom[k];
         e->seq = s; e->in_idx = d[i].in_idx; e->tag = d[i].tag; e->result = d[i].result; e->code = d[i].code;
-        e->payload_idx = ( s * Q + (ulong)q ) % np;   /* the link's layout: producer q's frag s */
+        e->payload_idx = pi;                         /* the link's layout: producer q's frag s */
         e->ctx = d[i].ctx; e->batch_txns = d[i].batch_txns; e->batch_pos = d[i].batch_pos; e->path = d[i].path;
       }
     }
@@ -2489,6 +2498,7 @@ static void * link_tile( void * _a ) {
   ulong dcap = 4096UL;
   fdgpu_vtile_done_t * done = (fdgpu_vtile_done_t *)malloc( dcap * sizeof(fdgpu_vtile_done_t) );
   ulong * lh = (ulong *)calloc( LH_N, sizeof(ulong) ), lmax = 0UL, t_last = 0UL;
+  uchar * pub = (uchar *)calloc( ( h->n_payload + 7UL ) / 8UL, 1UL );   /* (link_account: payloads this tile published) */
   ulong sigs = 0UL, got = 0UL, lost = 0UL, mine = 0UL;
   link_in_t in[ LINK_PROD_MAX ];
   memset( in, 0, sizeof(in) );
@@ -2584,7 +2594,7 @@ static void * link_tile( void * _a ) {
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 1 );
       PROF_ADD( 3 );
       link_trace( l, idx, vt, done, n );
-      link_account( l, idx, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
+      link_account( l, idx, done, n, &sigs, lh, &lmax, &t_last, in, pub ); got += n;
       PROF_ADD( 5 );
       if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );
       PROF_ADD( 6 );
@@ -2603,7 +2613,7 @@ static void * link_tile( void * _a ) {
       ulong n = fdgpu_vtile_after_frags( vt, done, dcap, 0 );
       PROF_ADD( 4 );
       link_trace( l, idx, vt, done, n );
-      link_account( l, idx, done, n, &sigs, lh, &lmax, &t_last, in ); got += n;
+      link_account( l, idx, done, n, &sigs, lh, &lmax, &t_last, in, pub ); got += n;
       PROF_ADD( 5 );
       if( c->reliable && c->zero_copy ) for( ulong q=0; q<Q; q++ ) link_credit( h, (int)q, idx, &in[q], vt );
       PROF_ADD( 6 );
@@ -2629,7 +2639,7 @@ static void * link_tile( void * _a ) {
   memcpy( l->hist + (ulong)idx * LH_N, lh, LH_N * sizeof(ulong) );
   /* (a served tile is counted done by its service's process, once it has added the GPU side's metrics) */
   if( !a->svc ) atomic_fetch_add_explicit( &h->tiles_done, 1UL, memory_order_release );
-  free( done ); free( lh );
+  free( done ); free( lh ); free( pub );
   fdgpu_vtile_delete( vt );
   return NULL;
 }

@@ -632,10 +632,11 @@ typedef struct fdgpu_link_anomaly {
   int           path;                  /* FDGPU_PATH_* or latency lanes */
 } fdgpu_link_anomaly_t;
 unsigned long   fdgpu_link_anomalies( fdgpu_link_t const * link, int tile, fdgpu_link_anomaly_t * out, unsigned long max );
-/* All of them by result: cnt[ FDGPU_VTILE_* ] (8 entries).  A dedup failure in an all-valid stream is an anomaly
-   unless the leg lost most of its frags: the bench's payloads recycle every 2 x the tcache depth frags per tile,
-   and a tile that lost more than half of those between two rounds of a payload still holds its tag (the
-   reference tile's tcache drops it the same way).  Returns the total. */
+/* All of them by result: cnt[ FDGPU_VTILE_* ] (8 entries).  cnt[ FDGPU_VTILE_PUBLISH ] (never an anomaly) counts
+   instead the dedup failures that are not anomalies: the link's payloads recycle, and a tile that lost or saw
+   overrun most of its frags since it published a payload still holds that payload's tag at its next round (the
+   reference tile's tcache drops it the same way).  Those are the dedups of a payload this tile published
+   before, and they are not in the anomaly count.  Returns the anomaly count. */
 unsigned long   fdgpu_link_anomaly_results( fdgpu_link_t const * link, int tile, unsigned long * cnt );
 
 /* served tiles (cfg.svc): this process's verify service after fdgpu_link_run -- its metrics and the CPU its
