@@ -92,7 +92,7 @@ case "$job" in
     # where a served tile's time goes at the max rate: the rdtsc section profile, T = 2 and 4, one process beside
     d=gpurun_out/r06_sprof; mkdir -p $d
     bash tools/gpu_job.sh \
-      "p1:500:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-rates 10e6 --stream-svc-tiles 2,4 --stream-svc-max 1 --stream-prof 1 --detail-out $d/p1.json > $d/p1.line"
+      "p1:500:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-rates 10e6 --stream-svc-tiles 2,4 --stream-svc-max 1 --stream-prof --detail-out $d/p1.json > $d/p1.line"
     ;;
   ftests)
     # round-end evidence, part 1: the whole GPU suite and the smoke
