@@ -29,7 +29,7 @@ N_FRAGS = 200_000
 _seq = itertools.count()
 
 
-def run_served(pays, reliable, depth, n_frags=N_FRAGS, tiles=2, **kw):
+def run_served(pays, reliable, depth, n_frags=N_FRAGS, tiles=2, zero_copy=True, **kw):
     from firedancer_amd import vtile
     sz = np.array([len(p) for p in pays], np.uint16)
     off = np.zeros(len(pays), np.uint32)
@@ -39,7 +39,7 @@ def run_served(pays, reliable, depth, n_frags=N_FRAGS, tiles=2, **kw):
     cfg.update(kw)
     path = f"/dev/shm/fdgpu_tsvc_{os.getpid()}_{next(_seq)}"
     link = vtile.Link(path, create=True, payload=arena, off=off, sz=sz, n_frags=n_frags, tiles=tiles, gpus=1,
-                      zero_copy=True, reliable=reliable, mcache_depth=depth, producers=1, svc=1, trace_cap=n_frags,
+                      zero_copy=zero_copy, reliable=reliable, mcache_depth=depth, producers=1, svc=1, trace_cap=n_frags,
                       **cfg)
     try:
         assert link.run(0, 0, True) == 0
@@ -73,6 +73,17 @@ def test_served_parity_reliable(tiles):
     seen = list(check_tiles(pays, traces, tiles=tiles))
     assert sum(k for _, k, _ in seen) == N_FRAGS
     assert all(m[2] > 0 and m[1] > 0 for _, _, m in seen), "the stream should exercise dedup and verify failures"
+
+
+def test_served_parity_host_copy():
+    """The reference's own intake (during_frag copies the frag into the tile's out dcache, fd_verify_tile.c:79):
+    the service's GPU batch reads each record from its tile's out dcache in the service's segment."""
+    pays = payload_set()
+    st, traces, svc = run_served(pays, reliable=True, depth=1 << 16, tiles=2, zero_copy=False)
+    assert st["verdicts"] == N_FRAGS and st["lost"] == 0 and st["tiles_gpu_open"] == 0
+    assert svc["completed"] == N_FRAGS and svc["mixed_batches"] > 0
+    seen = list(check_tiles(pays, traces, tiles=2))
+    assert sum(k for _, k, _ in seen) == N_FRAGS
 
 
 def test_served_parity_unreliable_laps():
