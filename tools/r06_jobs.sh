@@ -94,6 +94,14 @@ case "$job" in
     bash tools/gpu_job.sh \
       "p1:500:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-rates 10e6 --stream-svc-tiles 2,4 --stream-svc-max 1 --stream-prof --detail-out $d/p1.json > $d/p1.line"
     ;;
+  db)
+    # default runs of the final build, back to back
+    d=gpurun_out/r06_db; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "d1:400:python bench.py --detail-out $d/d1.json > $d/d1.line" \
+      "d2:400:python bench.py --detail-out $d/d2.json > $d/d2.line" \
+      "d3:400:python bench.py --detail-out $d/d3.json > $d/d3.line"
+    ;;
   ftests)
     # round-end evidence, part 1: the whole GPU suite and the smoke
     d=gpurun_out/r06_final; mkdir -p $d
