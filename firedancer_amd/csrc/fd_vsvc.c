@@ -339,8 +339,12 @@ fdgpu_vsvc_poll( fdgpu_vsvc_t * s ) {
       if( !fdgpu_ed25519_faulted( s->ctx[f] ) ) {
         ulong rg = r->src >> 56, off = r->src & VSVC_OFF_MASK;
         uchar const * src; uchar const * src_dev;
-        if( rg == VSVC_RGN_OUT ) { src = s->base + k->off_out + off; src_dev = s->out_dev[c] + off; }
-        else if( rg < FDGPU_VSVC_RGN_MAX && s->rgn_dev[rg] && off + r->rec_sz <= s->rgn_sz[rg] ) {
+        /* every place a request names is checked against its region: a tile's request never makes the GPU
+           read or write outside what the service registered for it */
+        if( rg == VSVC_RGN_OUT && off + r->rec_sz + 16UL <= h->out_sz ) {
+          src = s->base + k->off_out + off; src_dev = s->out_dev[c] + off;
+        }
+        else if( rg < FDGPU_VSVC_RGN_MAX && s->rgn_dev[rg] && off + ( ( r->rec_sz + 15UL ) & ~15UL ) <= s->rgn_sz[rg] ) {
           src = s->rgn_host[rg] + off; src_dev = s->rgn_dev[rg] + off;
         } else src = src_dev = NULL;
         ulong const * seq_dev = NULL;
@@ -351,7 +355,8 @@ fdgpu_vsvc_poll( fdgpu_vsvc_t * s ) {
         }
         ulong dsto = (ulong)r->dst_chunk * FDGPU_CHUNK_SZ;
         int rc = -1;
-        if( src && r->rec_sz >= FDGPU_TXNM_HDR_SZ && dsto + SV_RESERVE_MAX <= h->out_sz ) {
+        if( src && r->rec_sz >= FDGPU_TXNM_HDR_SZ && r->rec_sz <= FDGPU_TXNM_HDR_SZ + 1232UL &&
+            dsto + SV_RESERVE_MAX <= h->out_sz ) {
           unsigned flags = FDGPU_GATHER_SEED( c ) | ( ( r->flags & VSVC_REQ_HOSTCOPY ) ? FDGPU_GATHER_NO_WRITEBACK : 0U );
           rc = fdgpu_ed25519_submit_raw_gather_to( s->ctx[f], src, src_dev, s->out_dev[c] + dsto, r->rec_sz,
                                                    (unsigned short)FDGPU_TXNM_HDR_SZ,
@@ -551,7 +556,9 @@ fdgpu_vsvc_debug_serve( fdgpu_vsvc_t * s, int const * codes, ulong ncodes, ulong
     for( ; s->next[c] < tail; s->next[c]++, done++ ) {
       vsvc_req_t const * r = &rq[ s->next[c] & mask ];
       ulong rg = r->src >> 56, off = r->src & VSVC_OFF_MASK;
-      uchar const * src = rg == VSVC_RGN_OUT ? out + off : rg < FDGPU_VSVC_RGN_MAX && s->rgn_host[rg] ? s->rgn_host[rg] + off : NULL;
+      uchar const * src = rg == VSVC_RGN_OUT ? ( off + r->rec_sz <= h->out_sz ? out + off : NULL )
+                        : rg < FDGPU_VSVC_RGN_MAX && s->rgn_host[rg] && off + r->rec_sz <= s->rgn_sz[rg] ? s->rgn_host[rg] + off : NULL;
+      if( (ulong)r->dst_chunk * FDGPU_CHUNK_SZ + r->rec_sz > h->out_sz ) src = NULL;
       uchar * dst = out + (ulong)r->dst_chunk * FDGPU_CHUNK_SZ;
       int code = codes[ s->next[c] % ncodes ];
       ulong dtag = 0UL;

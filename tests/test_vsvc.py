@@ -211,3 +211,18 @@ def test_gpu_numa_node_sysfs(tmp_path, monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "3")
     assert vtile.gpu_numa_node(0, root) == 1
     assert vtile.gpu_numa_node(0, str(tmp_path / "none")) == -1
+
+
+def test_served_request_outside_its_regions_is_refused():
+    """A frag whose record lies outside every region the service registered is refused by the tile (-3) and
+    never becomes a request; the service bounds every request it takes against its regions as well, so a
+    hostile tile process cannot make the GPU read or write outside them (fdgpu_vsvc_poll)."""
+    rig = Rig()
+    t = rig.tiles[0]
+    a, n = rig.put(0, _payload(0))
+    assert t.during_frag_at(a, n, 0) == 0
+    assert t.during_frag_at(rig.in_base + rig.in_dc.size - 4096 - 64, n, 1) == -3
+    assert t.pending() == 1
+    t.housekeep()
+    assert rig.svc.debug_serve(np.zeros(1, np.int32), FP) == 1
+    assert [d[1] for d in t.after_frags(16)] == [vtile.PUBLISH]
