@@ -211,3 +211,73 @@ def test_launch_thread_failure_does_not_hang_blocking_drain():
         assert t.faulted() == 1
     finally:
         t.close()
+
+
+@pytest.mark.parametrize("zero_copy", [False, True])
+def test_served_vtile_vs_reference_tile(oracle, zero_copy):
+    """A served tile over the mixed stream of tests/test_gpu_vtile.py -- valid / invalid signatures, parse
+    failures, HA duplicates (with tcache eviction) and bundles with failing members -- with the service driven
+    by hand in this process: per-frag outcomes, metrics, published records and dedup tags are the reference
+    tile's (fd_verify_tile.c:103-157), on the host-copy intake and on the zero-copy one."""
+    pytest.importorskip("xxhash")
+    from test_gpu_vtile import make_stream, expectation, in_dcache
+    from firedancer_amd import vtile
+    frags = make_stream(seed=13)
+    seed, depth = 0x77aa55, 1 << 12
+    want_res, want_m, want_recs, want_tags = expectation(oracle, frags, seed, depth)
+    L = vtile.load()
+    svc = vtile.Service(None, create=True, clients=1, batch_txn=256, nctx=2, max_inflight=1)
+    fbs = [vtile.frag_bytes(p, b) for p, b in frags]
+    buf, offs = in_dcache(fbs)
+    mdepth = 1 << 12
+    mc = L.fdgpu_mcache_new(mdepth, 0)
+    lines = L.fdgpu_mcache_lines(mc)
+    lo = buf.ctypes.data & ~4095
+    rsz = ((buf.ctypes.data + buf.size + 4095) & ~4095) - lo
+    t = None
+    try:
+        assert svc.add_region(0, lo, rsz) == 0 and svc.add_region(1, lines, mdepth * 32) == 0
+        t = vtile.VTile(service=svc, client=0, tcache_depth=depth, seed=seed)
+        assert t.set_svc_region(0, lo, rsz) == 0 and t.set_svc_region(1, lines, mdepth * 32) == 0
+        if zero_copy:
+            assert t.set_in_links([mc]) == 0
+        assert svc.start(0) == 0
+        got, bad = [], []
+
+        def drain(n_want):
+            for _ in range(200000):
+                svc.poll()
+                t.housekeep()
+                for seq, r, chunk, sz, tag, _ in t.after_frags(4096):
+                    got.append((seq, r))
+                    if r == vtile.PUBLISH:
+                        head, timg = want_recs.get(seq, (b"", b""))
+                        rec = t.record(chunk, sz)
+                        if rec[: len(head)] != head or rec[(len(head) + 1) & ~1:] != timg:
+                            bad.append(seq)
+                        if want_tags is not None and tag != want_tags.get(seq):
+                            bad.append(("tag", seq))
+                if len(got) >= n_want:
+                    return
+                t.flush()
+            raise AssertionError(f"{len(got)} of {n_want} verdicts")
+
+        for seq, fb in enumerate(fbs):
+            if zero_copy:
+                L.fdgpu_mcache_publish(mc, seq, 0, (buf.ctypes.data + offs[seq] - lo) // 64, len(fb), 0, 0)
+                rc = t.during_frag_at(buf.ctypes.data + offs[seq], len(fb), seq)
+            else:
+                rc = t.during_frag(fb, seq)
+            assert rc == 0, (seq, rc)
+            if seq % 97 == 96:
+                drain(seq + 1 - 32)
+        drain(len(frags))
+        assert [g[0] for g in got] == list(range(len(frags)))
+        assert [g[1] for g in got] == want_res
+        assert t.metrics() == want_m
+        assert bad == []
+        assert sum(want_m[:4]) > 100 and want_m[2] > 10 and want_m[3] > 0
+    finally:
+        if t is not None:
+            t.close()
+        svc.close()
