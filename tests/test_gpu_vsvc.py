@@ -281,3 +281,53 @@ def test_served_vtile_vs_reference_tile(oracle, zero_copy):
         if t is not None:
             t.close()
         svc.close()
+
+
+_CHILD = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from firedancer_amd import vtile
+link = vtile.Link(sys.argv[2], create=False, timeout_s=120.0)
+try:
+    rc = link.run(1, 0, True)          # process 1: its service (device 0 here) and its tiles 1, 3
+finally:
+    link.close()
+sys.exit(0 if rc == 0 else 3)
+"""
+
+
+def test_served_two_processes_parity(engine_path):
+    """The N = 2 wiring of the served stream with both processes on this one GPU: process 0 creates the link and
+    runs the producer, and each process runs the verify service of "its GPU" with its tile processes (tile i ->
+    process i % 2, fd_verify_tile.c:47-48).  Every tile's verdicts, tags and records against the reference tile."""
+    import subprocess
+    from firedancer_amd import engine, vtile
+    if engine_path != "throughput":
+        pytest.skip("the child process runs the product's defaults: runs once, on them")
+    engine.debug_reset_opts()
+    pays = payload_set()
+    sz = np.array([len(p) for p in pays], np.uint16)
+    off = np.zeros(len(pays), np.uint32)
+    off[1:] = np.cumsum(sz[:-1].astype(np.int64))
+    arena = np.frombuffer(b"".join(pays) + bytes(64), np.uint8)
+    n = 100_000
+    path = f"/dev/shm/fdgpu_tsvc2_{os.getpid()}"
+    link = vtile.Link(path, create=True, payload=arena, off=off, sz=sz, n_frags=n, tiles=4, gpus=2, zero_copy=True,
+                      reliable=True, mcache_depth=1 << 16, producers=1, svc=1, trace_cap=n, batch_txn=8192,
+                      max_inflight=2, rate_fps=0.0, nctx=1)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    child = subprocess.Popen([sys.executable, "-c", _CHILD, root, path])
+    try:
+        assert link.run(0, 0, True) == 0
+        assert child.wait(timeout=180) == 0
+        st = link.result(timeout_s=60.0)
+        traces = [link.trace(i, n) for i in range(4)]
+    finally:
+        if child.poll() is None:
+            child.kill()
+        link.close()
+        if os.path.exists(path):
+            os.unlink(path)
+    assert st["verdicts"] == n and st["lost"] == 0 and st["tiles_gpu_open"] == 0
+    seen = list(check_tiles(pays, traces, tiles=4))
+    assert sum(k for _, k, _ in seen) == n
