@@ -102,6 +102,12 @@ case "$job" in
       "d2:400:python bench.py --detail-out $d/d2.json > $d/d2.line" \
       "d3:400:python bench.py --detail-out $d/d3.json > $d/d3.line"
     ;;
+  soak)
+    # 30-s paced legs at 10M and 12.5M per GPU: one tile process, and 2 served tile processes
+    d=gpurun_out/r06_soak; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "k1:600:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-only-paced --stream-rates 10e6,12.5e6 --stream-paced-seconds 30 --stream-svc-tiles 2 --detail-out $d/k1.json > $d/k1.line"
+    ;;
   ftests)
     # round-end evidence, part 1: the whole GPU suite and the smoke
     d=gpurun_out/r06_final; mkdir -p $d
