@@ -108,6 +108,16 @@ case "$job" in
     bash tools/gpu_job.sh \
       "k1:600:python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-only-paced --stream-rates 10e6,12.5e6 --stream-paced-seconds 30 --stream-svc-tiles 2 --detail-out $d/k1.json > $d/k1.line"
     ;;
+  pages)
+    # 4 KiB vs 2 MiB pages under the one-process link (--stream-no-huge), 30-s paced legs at 10M, interleaved
+    d=gpurun_out/r06_pages; mkdir -p $d
+    P="python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-only-paced --stream-rates 10e6 --stream-paced-seconds 30 --stream-svc-tiles ''"
+    bash tools/gpu_job.sh \
+      "h1:300:$P --detail-out $d/h1.json > $d/h1.line" \
+      "s1:300:$P --stream-no-huge --detail-out $d/s1.json > $d/s1.line" \
+      "h2:300:$P --detail-out $d/h2.json > $d/h2.line" \
+      "s2:300:$P --stream-no-huge --detail-out $d/s2.json > $d/s2.line"
+    ;;
   ftests)
     # round-end evidence, part 1: the whole GPU suite and the smoke
     d=gpurun_out/r06_final; mkdir -p $d
