@@ -1281,10 +1281,11 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--stream-place", choices=("gpu", "opposite", "none"), default="gpu",
                     help="NUMA node of each producer's mcache, in dcache part and thread: its GPU's (default), the node "
                          "opposite its GPU (the cross-socket arm), or unplaced (first touch by the link's creator)")
-    ap.add_argument("--stream-link-dir", default="auto",
-                    help="directory of the link file of several processes (N > 1, served legs): auto = a writable "
+    ap.add_argument("--stream-link-dir", default="/dev/shm",
+                    help="directory of the link file of several processes (N > 1, served legs); auto = a writable "
                          "hugetlbfs mount with free huge pages for it (2 MiB pages, as the reference's workspaces), "
-                         "else /dev/shm")
+                         "else /dev/shm.  Not the default: no GPU box here has a hugetlbfs mount with pages, so the "
+                         "hugetlbfs path has not run on hardware")
     ap.add_argument("--stream-only-paced", action="store_true",
                     help="(diagnostic) run only the paced legs (no stream summary line: max_rate is absent)")
     ap.add_argument("--stream-hw-queues", type=int, default=0, choices=range(0, 17), metavar="0..16",
