@@ -118,6 +118,13 @@ case "$job" in
       "h2:300:$P --detail-out $d/h2.json > $d/h2.line" \
       "s2:300:$P --stream-no-huge --detail-out $d/s2.json > $d/s2.line"
     ;;
+  n4svc)
+    # the N = 4 flow with the default served legs (T = 2), all four ranks on one GPU: the wiring of 4 services and
+    # 8 tile processes over shared links (four services on one device contend, as four GPUs' would not)
+    d=gpurun_out/r06_n4svc; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "n4:600:bash tools/rehearse_n4.sh --stream-only-paced --stream-rates 5e5,1e6 --stream-paced-seconds 2 --detail-out $d/detail.json > $d/line.json"
+    ;;
   ftests)
     # round-end evidence, part 1: the whole GPU suite and the smoke
     d=gpurun_out/r06_final; mkdir -p $d
