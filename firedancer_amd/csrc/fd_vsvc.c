@@ -82,9 +82,11 @@ fdgpu_vsvc_new( char const * path, fdgpu_vsvc_cfg_t const * cfg ) {
   vsvc_hdr_t * h = s->h;
   memset( (void *)h, 0, sizeof(vsvc_hdr_t) );
   h->total_sz = total; h->clients = (int)C; h->ring_cap = ring; h->out_sz = out_sz;
+  s->nclients = (int)C; s->ring = ring; s->out_sz = out_sz;
   for( ulong c=0; c<C; c++ ) {
     vsvc_client_t * k = &h->client[c];
     k->off_req = off_req[c]; k->off_cpl = off_cpl[c]; k->off_out = off_out[c]; k->ring_cap = ring; k->out_sz = out_sz;
+    s->off_req[c] = off_req[c]; s->off_cpl[c] = off_cpl[c]; s->off_out[c] = off_out[c];
   }
   atomic_store_explicit( &h->joined, 1UL, memory_order_relaxed );
   atomic_store_explicit( &h->magic, VSVC_MAGIC, memory_order_release );
@@ -153,7 +155,7 @@ sv_ctx_new( fdgpu_vsvc_t * s, int k ) {
   if( !c ) return NULL;
   ulong sm = fdgpu_ed25519_set_small_batch_max( c, 0UL );
   fdgpu_ed25519_set_small_batch_max( c, s->cfg.small_max ? s->cfg.small_max : ( sm < b/2UL ? sm : b/2UL ) );
-  if( fdgpu_ed25519_set_dedup_seeds( c, s->seeds, s->h->clients ) ) goto fail;
+  if( fdgpu_ed25519_set_dedup_seeds( c, s->seeds, s->nclients ) ) goto fail;
   unsigned parts = s->cfg.cu_split ? (unsigned)s->nctx : 1u, part = s->cfg.cu_split ? (unsigned)k : 0u;
   if( s->cfg.gather_cus && fdgpu_ed25519_reserve_cus( c, s->cfg.gather_cus, part, parts ) ) goto fail;
   int excl = s->cfg.cu_exclusive ? s->cfg.cu_exclusive : ( fdgpu_ed25519_get_cu_exclusive( c ) ? 0 : 1 );
@@ -183,8 +185,7 @@ fdgpu_vsvc_start( fdgpu_vsvc_t * s, int device ) {
   if( !s->cfg.copy_min )     s->cfg.copy_min     = FDGPU_VTILE_COPY_MIN;
   if( !s->cfg.max_inflight ) s->cfg.max_inflight = 2UL;
   s->batch_ns = 500e3;
-  s->pcap = 0UL;
-  for( int c=0; c<h->clients; c++ ) s->pcap += h->client[c].ring_cap;
+  s->pcap = (ulong)s->nclients * s->ring;
   s->pend    = (vsvc_pend_t *)calloc( s->pcap, sizeof(vsvc_pend_t) );
   s->p_tags  = (ulong *)malloc( s->cfg.batch_txn * sizeof(ulong) );
   s->p_dtag  = (ulong *)malloc( s->cfg.batch_txn * sizeof(ulong) );
@@ -194,7 +195,7 @@ fdgpu_vsvc_start( fdgpu_vsvc_t * s, int device ) {
   if( !s->pend || !s->p_tags || !s->p_dtag || !s->p_codes || !s->p_fp ) goto fail;
   rc = -2;
   if( s->cfg.launcher && !( s->launcher = fdgpu_launcher_new( device, s->cfg.launcher_core - 1 ) ) ) goto fail;
-  for( int c=0; c<h->clients; c++ )                          /* tiles attached before the start */
+  for( int c=0; c<s->nclients; c++ )                         /* tiles attached before the start */
     if( atomic_load_explicit( &h->client[c].state, memory_order_acquire ) == 1 ) {
       s->seeds[c] = h->client[c].seed; s->attached[c] = 1;
     }
@@ -214,11 +215,11 @@ fdgpu_vsvc_start( fdgpu_vsvc_t * s, int device ) {
   }
   /* the tiles' out dcaches: one registration over all of them */
   {
-    ulong lo = h->client[0].off_out, hi = h->client[ h->clients - 1 ].off_out + h->out_sz;
+    ulong lo = s->off_out[0], hi = s->off_out[ s->nclients - 1 ] + s->out_sz;
     if( fdgpu_host_register( s->base + lo, hi - lo ) ) goto fail;
     s->out_reg = 1;
-    for( int c=0; c<h->clients; c++ ) {
-      s->out_dev[c] = (uchar *)fdgpu_host_dev_ptr( s->base + h->client[c].off_out, h->out_sz );
+    for( int c=0; c<s->nclients; c++ ) {
+      s->out_dev[c] = (uchar *)fdgpu_host_dev_ptr( s->base + s->off_out[c], s->out_sz );
       if( !s->out_dev[c] ) goto fail;
     }
   }
@@ -234,8 +235,8 @@ fail:
 
 /* ---- the loop ----------------------------------------------------------------- */
 
-static inline vsvc_req_t * sv_req( fdgpu_vsvc_t * s, int c ) { return (vsvc_req_t *)( s->base + s->h->client[c].off_req ); }
-static inline vsvc_cpl_t * sv_cpl( fdgpu_vsvc_t * s, int c ) { return (vsvc_cpl_t *)( s->base + s->h->client[c].off_cpl ); }
+static inline vsvc_req_t * sv_req( fdgpu_vsvc_t * s, int c ) { return (vsvc_req_t *)( s->base + s->off_req[c] ); }
+static inline vsvc_cpl_t * sv_cpl( fdgpu_vsvc_t * s, int c ) { return (vsvc_cpl_t *)( s->base + s->off_cpl[c] ); }
 
 /* launch decision (fdgpu_vtile_housekeep's, for the service's contexts): 1 if context f's filling batch
    should go now */
@@ -279,7 +280,7 @@ static inline void
 sv_complete( fdgpu_vsvc_t * s, vsvc_pend_t const * e, int code, unsigned fp, ulong dtag, ulong bt, ulong bp, int k, int path,
              uchar * touched ) {
   int c = (int)e->client;
-  vsvc_cpl_t * q = &sv_cpl( s, c )[ s->cpl_n[c] & ( s->h->client[c].ring_cap - 1UL ) ];
+  vsvc_cpl_t * q = &sv_cpl( s, c )[ s->cpl_n[c] & ( s->ring - 1UL ) ];
   q->dtag = dtag; q->req = (unsigned)e->req; q->code = (short)code; q->fp = (unsigned short)fp;
   q->batch_txns = (unsigned)bt; q->batch_pos = (unsigned)bp; q->ctx = (uchar)( k < 0 ? 255 : k ); q->path = (signed char)path;
   s->cpl_n[c]++;
@@ -293,7 +294,7 @@ int
 fdgpu_vsvc_poll( fdgpu_vsvc_t * s ) {
   if( !s->started ) return 0;
   vsvc_hdr_t * h = s->h;
-  int const C = h->clients;
+  int const C = s->nclients;
   ulong t0 = sv_now(), now = t0;
   int work = 0;
   uchar touched[ FDGPU_VSVC_CLIENT_MAX ] = { 0 }, copied_ch[ FDGPU_VSVC_CLIENT_MAX ] = { 0 };
@@ -324,11 +325,16 @@ fdgpu_vsvc_poll( fdgpu_vsvc_t * s ) {
     if( !s->attached[c] ) continue;
     vsvc_client_t * k = &h->client[c];
     ulong tail = atomic_load_explicit( &k->req_tail, memory_order_acquire );
-    ulong mask = k->ring_cap - 1UL, took = 0UL;
+    ulong mask = s->ring - 1UL, took = 0UL;
     vsvc_req_t const * rq = sv_req( s, c );
     while( s->next[c] < tail && took < 256UL ) {
       if( s->ptail - s->phead >= s->pcap ) { stalled = 1; break; }
-      vsvc_req_t const * r = &rq[ s->next[c] & mask ];
+      /* one read of the request: the tile can rewrite its ring at any time, so what is checked below is what is
+         submitted */
+      vsvc_req_t rq_local;
+      memcpy( &rq_local, &rq[ s->next[c] & mask ], sizeof(vsvc_req_t) );
+      __asm__ __volatile__( "" : : "r"( &rq_local ) : "memory" );
+      vsvc_req_t const * r = &rq_local;
       if( s->next[c] + 2UL < tail ) __builtin_prefetch( &rq[ ( s->next[c] + 2UL ) & mask ] );
       /* a faulted context takes nothing more: the next healthy one (none: the frag completes as a fault) */
       int f = s->fill;
@@ -341,8 +347,8 @@ fdgpu_vsvc_poll( fdgpu_vsvc_t * s ) {
         uchar const * src; uchar const * src_dev;
         /* every place a request names is checked against its region: a tile's request never makes the GPU
            read or write outside what the service registered for it */
-        if( rg == VSVC_RGN_OUT && off + r->rec_sz + 16UL <= h->out_sz ) {
-          src = s->base + k->off_out + off; src_dev = s->out_dev[c] + off;
+        if( rg == VSVC_RGN_OUT && off + r->rec_sz + 16UL <= s->out_sz ) {
+          src = s->base + s->off_out[c] + off; src_dev = s->out_dev[c] + off;
         }
         else if( rg < FDGPU_VSVC_RGN_MAX && s->rgn_dev[rg] && off + ( ( r->rec_sz + 15UL ) & ~15UL ) <= s->rgn_sz[rg] ) {
           src = s->rgn_host[rg] + off; src_dev = s->rgn_dev[rg] + off;
@@ -356,7 +362,7 @@ fdgpu_vsvc_poll( fdgpu_vsvc_t * s ) {
         ulong dsto = (ulong)r->dst_chunk * FDGPU_CHUNK_SZ;
         int rc = -1;
         if( src && r->rec_sz >= FDGPU_TXNM_HDR_SZ && r->rec_sz <= FDGPU_TXNM_HDR_SZ + 1232UL &&
-            dsto + SV_RESERVE_MAX <= h->out_sz ) {
+            dsto + SV_RESERVE_MAX <= s->out_sz ) {
           unsigned flags = FDGPU_GATHER_SEED( c ) | ( ( r->flags & VSVC_REQ_HOSTCOPY ) ? FDGPU_GATHER_NO_WRITEBACK : 0U );
           rc = fdgpu_ed25519_submit_raw_gather_to( s->ctx[f], src, src_dev, s->out_dev[c] + dsto, r->rec_sz,
                                                    (unsigned short)FDGPU_TXNM_HDR_SZ,
@@ -524,7 +530,7 @@ fdgpu_vsvc_delete( fdgpu_vsvc_t * s ) {
   for( int k=0; k<VSVC_NCTX_MAX; k++ ) if( s->ctx[k] ) fdgpu_ed25519_ctx_delete( s->ctx[k] );
   fdgpu_launcher_delete( s->launcher );
   for( int i=0; i<FDGPU_VSVC_RGN_MAX; i++ ) if( s->rgn_reg[i] ) fdgpu_host_unregister( s->rgn_host[i] );
-  if( s->out_reg ) fdgpu_host_unregister( s->base + s->h->client[0].off_out );
+  if( s->out_reg ) fdgpu_host_unregister( s->base + s->off_out[0] );
   free( s->pend ); free( s->p_tags ); free( s->p_dtag ); free( s->p_codes ); free( s->p_fp );
   if( s->creator && s->path[0] ) unlink( s->path );
   munmap( s->base, s->sz );
@@ -543,22 +549,25 @@ fdgpu_vsvc_debug_serve( fdgpu_vsvc_t * s, int const * codes, ulong ncodes, ulong
   if( !s || !s->creator || s->started || !codes || !ncodes ) return 0UL;
   vsvc_hdr_t * h = s->h;
   ulong done = 0UL;
-  for( int c=0; c<h->clients; c++ ) {
+  for( int c=0; c<s->nclients; c++ ) {
     vsvc_client_t * k = &h->client[c];
     if( !s->attached[c] ) {
       if( atomic_load_explicit( &k->state, memory_order_acquire ) != 1 ) continue;
       s->attached[c] = 1; s->seeds[c] = k->seed;
     }
-    ulong tail = atomic_load_explicit( &k->req_tail, memory_order_acquire ), mask = k->ring_cap - 1UL;
+    ulong tail = atomic_load_explicit( &k->req_tail, memory_order_acquire ), mask = s->ring - 1UL;
     vsvc_req_t const * rq = sv_req( s, c );
     vsvc_cpl_t * cq = sv_cpl( s, c );
-    uchar * out = s->base + k->off_out;
+    uchar * out = s->base + s->off_out[c];
     for( ; s->next[c] < tail; s->next[c]++, done++ ) {
-      vsvc_req_t const * r = &rq[ s->next[c] & mask ];
+      vsvc_req_t rq_local;
+      memcpy( &rq_local, &rq[ s->next[c] & mask ], sizeof(vsvc_req_t) );
+      __asm__ __volatile__( "" : : "r"( &rq_local ) : "memory" );
+      vsvc_req_t const * r = &rq_local;
       ulong rg = r->src >> 56, off = r->src & VSVC_OFF_MASK;
-      uchar const * src = rg == VSVC_RGN_OUT ? ( off + r->rec_sz <= h->out_sz ? out + off : NULL )
+      uchar const * src = rg == VSVC_RGN_OUT ? ( off + r->rec_sz <= s->out_sz ? out + off : NULL )
                         : rg < FDGPU_VSVC_RGN_MAX && s->rgn_host[rg] && off + r->rec_sz <= s->rgn_sz[rg] ? s->rgn_host[rg] + off : NULL;
-      if( (ulong)r->dst_chunk * FDGPU_CHUNK_SZ + r->rec_sz > h->out_sz ) src = NULL;
+      if( (ulong)r->dst_chunk * FDGPU_CHUNK_SZ + r->rec_sz > s->out_sz ) src = NULL;
       uchar * dst = out + (ulong)r->dst_chunk * FDGPU_CHUNK_SZ;
       int code = codes[ s->next[c] % ncodes ];
       ulong dtag = 0UL;
@@ -567,7 +576,8 @@ fdgpu_vsvc_debug_serve( fdgpu_vsvc_t * s, int const * codes, ulong ncodes, ulong
         if( !( r->flags & VSVC_REQ_HOSTCOPY ) && src != dst ) memmove( dst, src, r->rec_sz );
         if( r->line != VSVC_LINE_NONE ) {
           ulong lr = r->line >> 56, lo = r->line & VSVC_OFF_MASK;
-          ulong const * w = lr < FDGPU_VSVC_RGN_MAX && s->rgn_host[lr] ? (ulong const *)( s->rgn_host[lr] + lo ) : NULL;
+          ulong const * w = lr < FDGPU_VSVC_RGN_MAX && s->rgn_host[lr] && lo + 8UL <= s->rgn_sz[lr]
+                          ? (ulong const *)( s->rgn_host[lr] + lo ) : NULL;
           if( !w || atomic_load_explicit( (_Atomic ulong const *)w, memory_order_acquire ) != r->seq ) code = FDGPU_ERR_OVERRUN;
         }
         if( code != FDGPU_ERR_OVERRUN ) {

@@ -92,6 +92,11 @@ struct fdgpu_vsvc {
   unsigned long         sz;
   int                   creator;    /* made the segment (file: unlinks it at delete) */
   char                  path[ 256 ];
+  /* the creator's private copy of the layout: the service never takes a size or an offset from the
+     segment, which every tile can write */
+  int                   nclients;
+  unsigned long         ring, out_sz;
+  unsigned long         off_req[ FDGPU_VSVC_CLIENT_MAX ], off_cpl[ FDGPU_VSVC_CLIENT_MAX ], off_out[ FDGPU_VSVC_CLIENT_MAX ];
   /* service side (fdgpu_vsvc_start) */
   fdgpu_vsvc_cfg_t      cfg;
   int                   started, device, nctx;

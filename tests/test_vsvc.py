@@ -226,3 +226,33 @@ def test_served_request_outside_its_regions_is_refused():
     t.housekeep()
     assert rig.svc.debug_serve(np.zeros(1, np.int32), FP) == 1
     assert [d[1] for d in t.after_frags(16)] == [vtile.PUBLISH]
+
+
+def test_service_ignores_a_rewritten_layout():
+    """The segment is writable by every tile process, so the service takes no size or offset from it: it serves
+    from the layout it made (fdgpu_vsvc_t's private copy).  A tile rewriting the header's client count and
+    sizes, and its own ring and out-dcache offsets, changes nothing the service reads or writes."""
+    rig = Rig()
+    t = rig.tiles[0]
+    pays = [_payload(300 + i) for i in range(8)]
+    for s, p in enumerate(pays):
+        a, n = rig.put(s, p)
+        assert t.during_frag_at(a, n, s) == 0
+    t.housekeep()
+    h = ctypes.c_uint64.from_address(rig.svc.p).value          # fdgpu_vsvc_t.h: the shared header
+    u64 = lambda off: ctypes.c_uint64.from_address(h + off)
+    cl0 = 256                                                   # client[0] (64-aligned after rgn_sz[16])
+    assert u64(cl0 + 144).value != u64(cl0 + 128).value         # off_out, off_req as made
+    ctypes.c_int32.from_address(h + 16).value = 16              # clients
+    u64(24).value = 1 << 40                                     # ring_cap
+    u64(32).value = 1 << 50                                     # out_sz
+    u64(cl0 + 136).value = u64(cl0 + 144).value                 # off_cpl -> the out dcache
+    u64(cl0 + 144).value = u64(cl0 + 128).value                 # off_out -> the request ring
+    u64(cl0 + 152).value = 1 << 40                              # ring_cap
+    u64(cl0 + 160).value = 1 << 50                              # out_sz
+    assert rig.svc.debug_serve(np.zeros(8, np.int32), FP) == 8
+    out = t.after_frags(64)
+    assert [(d[0], d[1]) for d in out] == [(s, vtile.PUBLISH) for s in range(8)]
+    for s, (seq, r, chunk, sz, tag, _) in enumerate(out):
+        assert t.record(chunk, 80 + len(pays[s]))[80:] == pays[s]
+        assert tag == vtile.dedup_tag(0x5eed, pays[s][1:65])
