@@ -125,6 +125,14 @@ case "$job" in
     bash tools/gpu_job.sh \
       "n4:600:bash tools/rehearse_n4.sh --stream-only-paced --stream-rates 5e5,1e6 --stream-paced-seconds 2 --detail-out $d/detail.json > $d/line.json"
     ;;
+  hard)
+    # the service serving from its own copy of the layout: its GPU tests, then the driver's own N = 2 command
+    # (default flags) with both ranks on one GPU
+    d=gpurun_out/r06_hard; mkdir -p $d
+    bash tools/gpu_job.sh \
+      "tests:600:$T tests/test_gpu_vsvc.py > $d/tests_vsvc.log 2>&1" \
+      "n2:600:FDGPU_BENCH_ONE_DEVICE=1 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29535 bench.py --gpus 2 --steps 20 --warmup 5 --detail-out $d/n2_detail.json > $d/n2_line.json"
+    ;;
   ftests)
     # round-end evidence, part 1: the whole GPU suite and the smoke
     d=gpurun_out/r06_final; mkdir -p $d
