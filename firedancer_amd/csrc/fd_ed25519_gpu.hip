@@ -3270,7 +3270,11 @@ static int launch_raw( fdgpu_ed25519_ctx_t * ctx, unsigned char const * d_payloa
   fd_seeds ds;
   memset( &ds, 0, sizeof(ds) );
   ds.seed[0] = (u64)ctx->dedup_seed;
-  if( ctx->dedup_nseed ) { memcpy( ds.seed, ctx->dedup_seeds, sizeof(ds.seed) ); ds.nseed = (u32)ctx->dedup_nseed; }
+  int nseed = __atomic_load_n( &ctx->dedup_nseed, __ATOMIC_ACQUIRE );
+  if( nseed ) {
+    for( int i=0; i<16; i++ ) ds.seed[i] = (u64)__atomic_load_n( &ctx->dedup_seeds[i], __ATOMIC_RELAXED );
+    ds.nseed = (u32)nseed;
+  }
   hipLaunchKernelGGL( fd_parse_kernel, dim3(g), dim3(FD_WG), 0, st, d_payload, d_raw, (u32)txn_cnt,
                       ctx->d_rdesc, ctx->d_pflag, d_img, (u32)img_stride, d_fp, ds, d_dtag, d_ovr,
                       fused ? ctx->d_map : (u32 *)NULL, (u32)sig_cnt, fused ? ctx->d_slow + ctx->max_sig : (u32 *)NULL,
@@ -4377,9 +4381,12 @@ fdgpu_ed25519_set_dedup( fdgpu_ed25519_ctx_t * ctx, int enable, unsigned long se
 extern "C" int
 fdgpu_ed25519_set_dedup_seeds( fdgpu_ed25519_ctx_t * ctx, unsigned long const * seeds, int n ) {
   if( n < 0 || n > 16 || ( n && !seeds ) ) { fd_err = "fdgpu_ed25519_set_dedup_seeds: 0..16 seeds"; return -1; }
-  memset( ctx->dedup_seeds, 0, sizeof(ctx->dedup_seeds) );
-  if( n ) memcpy( ctx->dedup_seeds, seeds, (size_t)n * sizeof(unsigned long) );
-  ctx->dedup_nseed = n; ctx->dedup = 1;
+  /* element by element, with no transient zero: the verify service sets the seeds again when a tile attaches,
+     and a launch thread may be copying them into a batch's kernel arguments meanwhile (launch_raw) -- the
+     seeds of tiles already attached are rewritten with the same values */
+  for( int i=0; i<16; i++ ) __atomic_store_n( &ctx->dedup_seeds[i], i < n ? seeds[i] : 0UL, __ATOMIC_RELAXED );
+  __atomic_store_n( &ctx->dedup_nseed, n, __ATOMIC_RELEASE );
+  ctx->dedup = 1;
   return 0;
 }
 
