@@ -135,14 +135,14 @@ case "$job" in
     ;;
   ftests)
     # round-end evidence, part 1: the whole GPU suite and the smoke
-    d=gpurun_out/r06_final; mkdir -p $d
+    d=gpurun_out/${FDJOB_DIR:-r06_final}; mkdir -p $d
     bash tools/gpu_job.sh \
       "tests:1100:$T tests -m gpu > $d/gpu_tests.log 2>&1" \
       "smoke:300:python -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")' > $d/smoke.log 2>&1"
     ;;
   fbench)
     # round-end evidence, part 2: the default bench, rocprof kernel stats of the headline bench, PMC passes
-    d=gpurun_out/r06_final; mkdir -p $d
+    d=gpurun_out/${FDJOB_DIR:-r06_final}; mkdir -p $d
     B="python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --latency-batch 0 --stream-frags 0 --no-extra-configs"
     P="timeout -s KILL 120 rocprofv3 --kernel-include-regex fd_ -f csv"
     bash tools/gpu_job.sh \
