@@ -96,7 +96,7 @@ case "$job" in
     ;;
   db)
     # default runs of the final build, back to back
-    d=gpurun_out/r06_db; mkdir -p $d
+    d=gpurun_out/${FDJOB_DIR:-r06_db}; mkdir -p $d
     bash tools/gpu_job.sh \
       "d1:400:python bench.py --detail-out $d/d1.json > $d/d1.line" \
       "d2:400:python bench.py --detail-out $d/d2.json > $d/d2.line" \
