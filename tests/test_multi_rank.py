@@ -1,5 +1,5 @@
 """CPU: the N>1 bench path (independent shards, MAX-of-time / MIN-of-ok
-reductions, whole-job aggregation) over torch.distributed gloo, world_size 2."""
+reductions, whole-job aggregation) over torch.distributed gloo, world_size 2 and 4."""
 import os
 import socket
 
@@ -38,7 +38,7 @@ def _worker(rank, world, port, q):
     value = shard.aggregate_rate(world, nsig, 3, dt_max)
     # the configs[4] stream aggregate: SUM of per-rank sigs over the MAX per-rank stream time
     ssum, smax, sw = shard.reduce_sum_max(dist, units=1000 * (rank + 1), seconds=0.5 * (rank + 1), device="cpu")
-    assert (ssum, smax, sw) == (3000.0, 1.0, 2)
+    assert (ssum, smax, sw) == (1000.0 * world * (world + 1) / 2, 0.5 * world, world)
     # the per-GPU report: every rank's row, in rank order
     rows = shard.gather_rows(dist, [rank, 10.0 * rank + 0.5], device="cpu")
     assert rows == [[float(r), 10.0 * r + 0.5] for r in range(world)]
@@ -47,8 +47,9 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_shards_and_reductions():
-    world, port = 2, _free_port()
+@pytest.mark.parametrize("world", [2, 4])
+def test_rank_shards_and_reductions(world):
+    port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
@@ -58,12 +59,15 @@ def test_two_rank_shards_and_reductions():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, dt0, max0, ok0, nok0, v0, g0, n0), (r1, dt1, max1, ok1, nok1, v1, g1, n1) = res
-    assert max0 == max1 == pytest.approx(max(dt0, dt1))
-    assert max0 >= 3 * 0.02                      # rank 1 sleeps 20 ms x 3
-    assert ok0 and ok1 and not nok0 and not nok1
-    assert v0 == v1 == pytest.approx(2 * n0 * 3 / max0)
-    assert g0 == g1 and g0[0] != g0[1]            # shards are distinct transactions
+    assert [r[0] for r in res] == list(range(world))
+    dts, maxs = [r[1] for r in res], [r[2] for r in res]
+    assert all(m == pytest.approx(max(dts)) for m in maxs)
+    assert maxs[0] >= 3 * 0.01 * world           # the last rank sleeps 10 ms x world, 3 steps
+    assert all(r[3] for r in res) and not any(r[4] for r in res)
+    n0 = res[0][7]
+    assert all(r[5] == pytest.approx(world * n0 * 3 / maxs[0]) for r in res)
+    g0 = res[0][6]
+    assert all(r[6] == g0 for r in res) and len(set(g0)) == world   # shards are distinct transactions
 
 
 def test_shard_range_partitions():
