@@ -125,6 +125,17 @@ case "$job" in
     bash tools/gpu_job.sh \
       "n4:600:bash tools/rehearse_n4.sh --stream-only-paced --stream-rates 5e5,1e6 --stream-paced-seconds 2 --detail-out $d/detail.json > $d/line.json"
     ;;
+  ctx3)
+    # served legs above the knee with three engine contexts in the service (and the one-process tile) against the
+    # default two, interleaved: does a third staggered context move the served knee past 12.5M?
+    d=gpurun_out/r06_ctx3; mkdir -p $d
+    A="python bench.py --steps 2 --warmup 1 --txns 262144 --no-cpu-baseline --no-extra-configs --latency-batch 0 --stream-only-paced --stream-rates 10e6,12.5e6,15e6 --stream-svc-tiles 2,3"
+    bash tools/gpu_job.sh \
+      "c2a:400:$A --stream-lat-ctx 2 --detail-out $d/c2a.json > $d/c2a.line" \
+      "c3a:400:$A --stream-lat-ctx 3 --detail-out $d/c3a.json > $d/c3a.line" \
+      "c2b:400:$A --stream-lat-ctx 2 --detail-out $d/c2b.json > $d/c2b.line" \
+      "c3b:400:$A --stream-lat-ctx 3 --detail-out $d/c3b.json > $d/c3b.line"
+    ;;
   hard)
     # the service serving from its own copy of the layout: its GPU tests, then the driver's own N = 2 command
     # (default flags) with both ranks on one GPU
