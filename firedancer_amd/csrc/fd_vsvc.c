@@ -310,8 +310,10 @@ fdgpu_vsvc_poll( fdgpu_vsvc_t * s ) {
       for( int j=0; j<s->nctx; j++ ) if( s->ctx[j] ) fdgpu_ed25519_set_dedup_seeds( s->ctx[j], s->seeds, C );
     }
     if( !s->attached[c] ) continue;
-    int f = atomic_exchange_explicit( &k->dbg_fault, 0, memory_order_acq_rel );   /* bit k: fault context k */
-    for( int j=0; j<s->nctx; j++ ) if( ( f >> j ) & 1 ) fdgpu_ed25519_debug_fault( s->ctx[j] );
+    if( s->cfg.debug_hooks ) {                          /* (tests only: otherwise no tile can fault the contexts) */
+      int f = atomic_exchange_explicit( &k->dbg_fault, 0, memory_order_acq_rel );   /* bit k: fault context k */
+      for( int j=0; j<s->nctx; j++ ) if( ( f >> j ) & 1 ) fdgpu_ed25519_debug_fault( s->ctx[j] );
+    }
     ulong fl = atomic_load_explicit( &k->flush, memory_order_acquire );
     if( fl != s->flush_seen[c] ) { s->flush_seen[c] = fl; want_flush = 1; }
     ulong ga = atomic_load_explicit( &k->gather, memory_order_acquire );

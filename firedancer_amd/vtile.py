@@ -105,7 +105,8 @@ class VsvcCfg(ctypes.Structure):
                 ("small_max", ctypes.c_ulong), ("min_batch", ctypes.c_ulong), ("max_wait_ns", ctypes.c_ulong),
                 ("copy_wait_ns", ctypes.c_ulong), ("copy_min", ctypes.c_ulong), ("gather_cus", ctypes.c_uint),
                 ("cu_split", ctypes.c_int), ("cu_exclusive", ctypes.c_int), ("lat_share", ctypes.c_int),
-                ("launcher", ctypes.c_int), ("launcher_core", ctypes.c_int)]
+                ("launcher", ctypes.c_int), ("launcher_core", ctypes.c_int),
+                ("debug_hooks", ctypes.c_int)]
 
 
 class VsvcStats(ctypes.Structure):

@@ -379,7 +379,8 @@ unsigned long   fdgpu_vtile_pending( fdgpu_vtile_t const * vt );
    nonzero fdgpu_vtile_faulted as the reference's FD_LOG_ERR or recovers. */
 int             fdgpu_vtile_faulted( fdgpu_vtile_t const * vt );
 int             fdgpu_vtile_recover( fdgpu_vtile_t * vt );
-/* host-side test hook: engine context k of the tile fails (fdgpu_ed25519_debug_fault) */
+/* host-side test hook: engine context k of the tile fails (fdgpu_ed25519_debug_fault); a served tile asks its
+   service, which honours it only when made with fdgpu_vsvc_cfg_t.debug_hooks */
 void            fdgpu_vtile_debug_fault( fdgpu_vtile_t * vt, int k );
 /* host-side test hook: the launch thread (fdgpu_vtile_opts_t.launcher) fails every batch launch of engine
    context k from now on (fdgpu_ed25519_debug_fail_launch): the context faults asynchronously, on that thread */
@@ -430,6 +431,8 @@ typedef struct fdgpu_vsvc_cfg {
   int           cu_split, cu_exclusive, lat_share;
   int           launcher;         /* 1: the batch launches and copies on a launch thread of the service's own */
   int           launcher_core;    /* with launcher: 1 + its CPU (0: not pinned) */
+  int           debug_hooks;      /* 1: honour a tile's fdgpu_vtile_debug_fault (tests only; 0: a tile cannot fault the
+                                     service's engine contexts) */
 } fdgpu_vsvc_cfg_t;
 
 /* metrics of a service, as a tile's GPU metrics: batches, transactions batched, in-flight

@@ -116,12 +116,13 @@ class _InProc:
     """A service and one served tile in this process (the service's loop driven by hand), over an in link
     of host memory the service maps as its regions 0 (records) and 1 (mcache lines)."""
 
-    def __init__(self, n_rec=1024, depth=4096):
+    def __init__(self, n_rec=1024, depth=4096, debug_hooks=1):
         from firedancer_amd import vtile
         self.vt = vtile
         L = vtile.load()
         self.L = L
-        self.svc = vtile.Service(None, create=True, clients=1, batch_txn=1024, nctx=2, max_inflight=1)
+        self.svc = vtile.Service(None, create=True, clients=1, batch_txn=1024, nctx=2, max_inflight=1,
+                                  debug_hooks=debug_hooks)
         self.mc = L.fdgpu_mcache_new(depth, 0)
         self.lines = L.fdgpu_mcache_lines(self.mc)
         self.buf = np.zeros(n_rec * 24 * 64 + 8192, np.uint8)
@@ -173,6 +174,24 @@ def test_served_in_process_codes_and_fault_recovery():
     try:
         _in_process_phases(r, pays, want)
     finally:                                             # (before the interpreter's exit tears HIP down)
+        r.tile.close(); r.svc.close()
+
+
+def test_served_tile_cannot_fault_the_service_without_debug_hooks():
+    """fdgpu_vtile_debug_fault is a test hook: a service made without cfg.debug_hooks ignores a tile's request
+    to fault its engine contexts, and every frag verifies."""
+    from firedancer_amd import synth
+    payload, desc, expect, _ = synth.make_batch(200, synth.LARGE_NOOP, invalid_frac=0.25, seed=8)
+    pays = [payload[d["payload_off"]: d["payload_off"] + d["payload_sz"]].tobytes() for d in desc]
+    want = [0 if e == 0 else 2 for e in expect]
+    r = _InProc(debug_hooks=0)
+    try:
+        r.feed(pays)
+        out = r.drain(200, faults_at=0)
+        assert [d[0] for d in out] == list(range(200)) and [d[1] for d in out] == want
+        st = r.svc.stats()
+        assert st["faults"] == 0 and st["fault_completions"] == 0
+    finally:
         r.tile.close(); r.svc.close()
 
 
